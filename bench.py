@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""Benchmark of the eray ray-tracing hot path on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[1]): objects/cube.obj with src/main.rs's scene
+and material graph, 1920x1080 per GPU.  One step = one frame: every rank renders its 1080-row
+tile of a 1920 x (1080*N) frame (camera rays, first-hit triangle scan, shading with shadow rays)
+with the f32 image and the PPM bytes written by the fused kernel, and for N > 1 the PPM rows are
+gathered to rank 0 over RCCL (xGMI).  Inputs (mesh, material textures) are resident in HBM before
+timing; the material graph is evaluated once, as Material::update is (reported separately).
+Per-GPU work is fixed as N grows (weak scaling).
+
+Prints ONE JSON line on rank 0 (metric "Mrays/s": primary rays of all ranks / wall time).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (imported before the HIP library: one HIP runtime per process)
+import torch.distributed as dist  # noqa: E402
+
+from eray_amd import capi  # noqa: E402
+from eray_amd.frame import MainScene  # noqa: E402
+from eray_amd.objfile import load_obj_file  # noqa: E402
+
+WIDTH, HEIGHT_PER_GPU, TEXTURE = 1920, 1080, 1024
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def frame_camera_fov(n: int) -> tuple[float, float]:
+    """Fov giving Camera::size() == (1920, 1080*n) exactly (16:9 for one GPU)."""
+    for fov in ((16.0, 9.0 * n), (float(WIDTH), float(HEIGHT_PER_GPU * n))):
+        cam = capi.make_camera((0.0, 0.0, 5.0), fov, WIDTH, 1.0)
+        if capi.camera_size(cam) == (WIDTH, HEIGHT_PER_GPU * n):
+            return fov
+    raise RuntimeError(f"no Fov gives a 1920x{HEIGHT_PER_GPU * n} camera")
+
+
+def algorithmic_bytes(hit_pixels: int, pixels: int, triangles: int) -> int:
+    """Bytes the render kernel must move per launch:
+    15 B/pixel written (12 B f32 RGB + 3 B PPM), 16 B of texels read per hit (IColor 12 + IValue 4),
+    and the triangle records once (48 B hot + 64 B culling + 64 B shading)."""
+    return 15 * pixels + 16 * hit_pixels + (48 + 64 + 64) * triangles
+
+
+def cpu_baseline(mesh, seconds: float = 10.0) -> dict:
+    """The single-threaded C++ restatement (oracle/, 'port') on this host: full C2 frames
+    (render + PPM byte pack) repeated for >= `seconds`."""
+    from oracle import pyoracle as O
+
+    scene = O.main_rs_scene(*mesh, texture=TEXTURE)
+    cam = O.camera((0.0, 0.0, 5.0), (16.0, 9.0), WIDTH, 1.0)
+    frames, t0 = 0, time.perf_counter()
+    while True:
+        rgb, _ = O.render(scene, cam)
+        O.ppm_bytes(rgb)
+        frames += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    rays = frames * WIDTH * HEIGHT_PER_GPU
+    return {"value": rays / el / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
+            "sample": f"{frames} full 1920x1080 cube frames (main.rs scene, render + PPM pack) "
+                      f"in {el:.1f} s, single thread, oracle/eray_oracle.cpp (g++ -O2 -ffp-contract=off)"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--mesh", default=os.path.join(ROOT, "objects", "cube.obj"))
+    ap.add_argument("--brute-force", action="store_true", help="disable the exact wave culling")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    mesh = load_obj_file(args.mesh)
+    ctx = capi.Context(local_rank)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    H_total = HEIGHT_PER_GPU * world
+    t_mat0 = time.perf_counter()
+    scene = MainScene(ctx, *mesh, WIDTH, H_total, texture=TEXTURE, fov=frame_camera_fov(world))
+    torch.cuda.synchronize()
+    t_mat = time.perf_counter() - t_mat0
+
+    # rank r renders the r-th block of PPM file rows: camera rows [H - (r+1)*h, H - r*h)
+    rows = HEIGHT_PER_GPU
+    row0 = H_total - (rank + 1) * rows
+    rgb = torch.empty((rows, WIDTH, 3), dtype=torch.float32, device="cuda")
+    ppm = torch.empty((rows, WIDTH, 3), dtype=torch.uint8, device="cuda")
+    face = torch.empty((rows, WIDTH), dtype=torch.int32, device="cuda")
+    frame = torch.empty((H_total, WIDTH, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
+    flags = capi.RENDER_BRUTE_FORCE if args.brute_force else capi.RENDER_DEFAULT
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record()
+        scene.render(out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr(), row0=row0, rows=rows, flags=flags)
+        if ev is not None:
+            ev[1].record()
+        if world > 1:
+            dist.gather(ppm, list(frame.chunk(world, 0)) if rank == 0 else None, dst=0)
+
+    # one untimed instrumented frame: hit count for the algorithmic-bytes model
+    scene.render(out_rgb=rgb.data_ptr(), out_face=face.data_ptr(), row0=row0, rows=rows, flags=flags)
+    torch.cuda.synchronize()
+    hits = int((face >= 0).sum().item())
+
+    for _ in range(args.warmup):
+        step()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        h = torch.tensor([hits], dtype=torch.int64, device="cuda")
+        dist.all_reduce(h)
+        hits_all = int(h.item())
+    else:
+        hits_all = hits
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+
+    if rank == 0:
+        pixels = WIDTH * rows
+        ms_per_step = elapsed / args.steps * 1e3
+        rays = WIDTH * H_total * args.steps
+        value = rays / elapsed / 1e6
+        alg = algorithmic_bytes(hits, pixels, len(mesh[0]))
+        achieved = alg / (kernel_ms * 1e-3) / 1e9
+        result = {
+            "metric": "Mrays/s",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 6),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic scene of src/main.rs: objects/cube.obj (the reference's own file), "
+                    "procedural material graph",
+            "config": {
+                "workload": "C2: cube.obj, 1920x1080 per GPU, main.rs scene + material graph; step = "
+                            "one frame (camera rays, first-hit scan, shading + shadow rays, f32 image "
+                            "and PPM bytes) + RCCL gather of PPM rows to rank 0 when N > 1",
+                "mesh": os.path.relpath(args.mesh, ROOT),
+                "triangles": int(len(mesh[0])),
+                "frame": [WIDTH, H_total],
+                "rows_per_gpu": rows,
+                "texture": TEXTURE,
+                "parallelism": f"row tiles x{world}" if world > 1 else "single GPU",
+                "culling": not args.brute_force,
+            },
+            "frame_ms": round(ms_per_step, 6),
+            "render_kernel_ms": round(kernel_ms, 6),
+            "material_graph_s": round(t_mat, 4),
+            "hit_pixels": hits_all,
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": PEAK_HBM_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / PEAK_HBM_GBS, 4),
+                "traffic": None,
+                "kernel": "render_kernel<true> (eray_amd/csrc/render.hip)",
+                "algorithmic_bytes_per_launch": alg,
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(mesh, args.cpu_seconds)
+        print(json.dumps(result), flush=True)
+
+    scene.close()
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

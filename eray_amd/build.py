@@ -1,0 +1,94 @@
+"""Build recipe of the product library eray_amd/lib/liberay_hip.so (gfx950 only).
+
+    python -m eray_amd.build [--jobs N] [--verbose]
+
+Compiles the HIP kernels and the C-ABI layer with hipcc for gfx950 and links them into one
+shared library next to this package, so it travels to the GPU box with the repository.
+Floating-point flags are part of the contract: -ffp-contract=off keeps a*b+c unfused so the
+kernels reproduce the reference's f32 results bit-for-bit; hipcc's defaults already give
+correctly rounded f32 division/sqrt and keep f32 denormals.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+OBJ = os.path.join(PKG, "_obj")
+LIB_DIR = os.path.join(PKG, "lib")
+LIB = os.path.join(LIB_DIR, "liberay_hip.so")
+
+SOURCES = ["render.hip", "shaderlib.hip", "capi.cpp"]
+ARCH = "gfx950"
+CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
+            f"--offload-arch={ARCH}", "-I" + os.path.join(ROOT, "include")]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the eray_amd HIP library cannot be built")
+
+
+def _newer(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return False
+    t = os.path.getmtime(target)
+    return all(os.path.getmtime(d) <= t for d in deps)
+
+
+def _headers() -> list[str]:
+    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
+    hs.append(os.path.join(ROOT, "include", "eray_hip.h"))
+    return hs
+
+
+def build(jobs: int = 4, verbose: bool = False, force: bool = False) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    os.makedirs(LIB_DIR, exist_ok=True)
+    cc = hipcc()
+    headers = _headers()
+    objs, cmds = [], []
+    for src in SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(OBJ, src + ".o")
+        objs.append(o)
+        if force or not _newer(o, [s] + headers):
+            lang = [] if src.endswith(".hip") else ["-x", "hip"]
+            cmds.append([cc, *CXXFLAGS, *lang, "-c", s, "-o", o])
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        return r.stderr
+
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        for warn in ex.map(run, cmds):
+            if warn.strip() and verbose:
+                print(warn, file=sys.stderr)
+    if force or cmds or not _newer(LIB, objs):
+        run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs])
+    return LIB
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--force", action="store_true")
+    a = ap.parse_args()
+    print(build(a.jobs, a.verbose, a.force))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,322 @@
+"""ctypes binding of include/eray_hip.h (the product C-ABI, eray_amd/lib/liberay_hip.so).
+
+This is the Python host's view of the drop-in boundary: thin wrappers with the C names,
+status codes turned into exceptions.  There is no CPU fallback anywhere: if the HIP library
+is missing or no GPU is present, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "lib", "liberay_hip.so")
+
+# eray_status (include/eray_hip.h)
+OK = 0
+E_INVALID_ARGUMENT = -1
+E_HIP = -2
+E_OUT_OF_MEMORY = -3
+E_MISSING = -4
+E_MISSING_MANY = -5
+E_INVALID_TYPE = -6
+E_OUT_OF_BOUNDS = -7
+E_IO = -8
+E_PARSE = -9
+E_BUILD = -10
+E_UNSUPPORTED = -11
+E_CYCLE = -12
+
+RENDER_DEFAULT = 0
+RENDER_BRUTE_FORCE = 1
+
+LIGHT_POINT = 0
+LIGHT_AMBIENT = 1
+
+
+class ErayError(RuntimeError):
+    def __init__(self, status: int, message: str):
+        super().__init__(f"eray status {status}: {message}")
+        self.status = status
+        self.message = message
+
+
+class Image(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("width", C.c_uint32), ("height", C.c_uint32)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("center", C.c_float * 3), ("fov", C.c_float * 2), ("width", C.c_uint32),
+                ("z_dist", C.c_float)]
+
+
+class Light(C.Structure):
+    _fields_ = [("position", C.c_float * 3), ("variant", C.c_int32), ("color", C.c_float * 3),
+                ("brightness", C.c_float)]
+
+
+class Material(C.Structure):
+    _fields_ = [("color", Image), ("diffuse", Image), ("specular", Image),
+                ("specular_power", Image), ("reflection", Image)]
+
+
+class Object(C.Structure):
+    _fields_ = [("positions", C.c_void_p), ("normals", C.c_void_p), ("uvs", C.c_void_p),
+                ("triangle_count", C.c_uint32), ("bbox_min", C.c_float * 3),
+                ("bbox_max", C.c_float * 3), ("material", Material)]
+
+
+class RenderParams(C.Structure):
+    _fields_ = [("image_width", C.c_uint32), ("image_height", C.c_uint32), ("row0", C.c_uint32),
+                ("rows", C.c_uint32), ("bounces", C.c_uint32), ("anti_aliasing", C.c_uint32),
+                ("out_rgb", C.c_void_p), ("out_ppm", C.c_void_p), ("out_face", C.c_void_p),
+                ("flags", C.c_uint32)]
+
+
+# Every exported symbol of include/eray_hip.h with its (restype, argtypes).
+_P = C.c_void_p
+_U = C.c_uint32
+_F = C.c_float
+SIGNATURES = {
+    "eray_abi_version": (C.c_int, []),
+    "eray_ctx_create": (C.c_int, [C.c_int, C.POINTER(_P)]),
+    "eray_ctx_destroy": (C.c_int, [_P]),
+    "eray_last_error": (C.c_char_p, [_P]),
+    "eray_set_stream": (C.c_int, [_P, _P]),
+    "eray_get_stream": (_P, [_P]),
+    "eray_synchronize": (C.c_int, [_P]),
+    "eray_device_alloc": (C.c_int, [_P, C.c_size_t, C.POINTER(_P)]),
+    "eray_device_free": (C.c_int, [_P, _P]),
+    "eray_memset": (C.c_int, [_P, _P, C.c_int, C.c_size_t]),
+    "eray_copy_to_device": (C.c_int, [_P, _P, _P, C.c_size_t]),
+    "eray_copy_to_host": (C.c_int, [_P, _P, _P, C.c_size_t]),
+    "eray_node_wave": (C.c_int, [_P, _U, _U, _F, _F, _P]),
+    "eray_node_rgb": (C.c_int, [_P, _U, _U, Image, Image, Image, _P]),
+    "eray_node_flat_color": (C.c_int, [_P, _U, _U, _F, _F, _F, _P]),
+    "eray_node_mix_color": (C.c_int, [_P, _U, _U, Image, Image, _F, _P]),
+    "eray_material_example": (C.c_int, [_P, _U, _U, _F, _F, _F, _F, _F, _F, _P, _P]),
+    "eray_scene_reset": (C.c_int, [_P]),
+    "eray_scene_set_camera": (C.c_int, [_P, C.POINTER(Camera)]),
+    "eray_scene_add_light": (C.c_int, [_P, C.POINTER(Light)]),
+    "eray_scene_add_object": (C.c_int, [_P, C.POINTER(Object), C.POINTER(_U)]),
+    "eray_camera_size": (C.c_int, [C.POINTER(Camera), C.POINTER(_U), C.POINTER(_U)]),
+    "eray_render": (C.c_int, [_P, C.POINTER(RenderParams)]),
+    "eray_pack_ppm": (C.c_int, [_P, _P, _U, _U, _P]),
+    "eray_ppm_header": (C.c_int, [_U, _U, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+}
+
+_lib = None
+
+
+def _preload_hip_runtime() -> None:
+    """Make sure exactly one HIP runtime serves this process.
+
+    PyTorch ships its own libamdhip64.so.7; our library links the same SONAME.  Importing torch
+    first makes the loader reuse torch's copy for us too, so device pointers and streams are
+    shared.  ERAY_HIP_RUNTIME=rocm instead preloads /opt/rocm's runtime (then torch reuses it).
+    """
+    policy = os.environ.get("ERAY_HIP_RUNTIME", "torch")
+    if policy == "rocm":
+        for cand in ("/opt/rocm/lib/libamdhip64.so.7", "/opt/rocm/lib/libamdhip64.so"):
+            if os.path.exists(cand):
+                C.CDLL(cand, mode=C.RTLD_GLOBAL)
+                break
+    try:  # noqa: SIM105 - torch is optional for the C-ABI itself
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
+def lib():
+    """Load eray_amd/lib/liberay_hip.so (build it with `python -m eray_amd.build`)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: run `python -m eray_amd.build` (no CPU fallback)")
+        _preload_hip_runtime()
+        L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error(ctx=None) -> str:
+    msg = lib().eray_last_error(ctx)
+    return msg.decode() if msg else ""
+
+
+def check(status: int, ctx=None) -> None:
+    if status != OK:
+        raise ErayError(status, last_error(ctx))
+
+
+def camera_size(cam: Camera) -> tuple[int, int]:
+    w, h = _U(), _U()
+    check(lib().eray_camera_size(C.byref(cam), C.byref(w), C.byref(h)))
+    return w.value, h.value
+
+
+def make_camera(center=(0.0, 0.0, 5.0), fov=(60.0, 60.0), width=1024, z_dist=1.0) -> Camera:
+    return Camera((C.c_float * 3)(*center), (C.c_float * 2)(*fov), width, z_dist)
+
+
+def make_light(position, variant, color=(1.0, 1.0, 1.0), brightness=1.0) -> Light:
+    v = LIGHT_AMBIENT if variant in (LIGHT_AMBIENT, "ambient") else LIGHT_POINT
+    return Light((C.c_float * 3)(*position), v, (C.c_float * 3)(*color), brightness)
+
+
+def ppm_header(width: int, height: int) -> bytes:
+    buf = C.create_string_buffer(64)
+    n = C.c_size_t()
+    check(lib().eray_ppm_header(width, height, buf, 64, C.byref(n)))
+    return buf.raw[: n.value]
+
+
+class DeviceArray:
+    """A device allocation owned by a Context (numpy-like shape/dtype bookkeeping only)."""
+
+    def __init__(self, ctx: "Context", shape, dtype):
+        self.ctx = ctx
+        self.shape = tuple(int(s) for s in shape)
+        self.dtype = np.dtype(dtype)
+        self.nbytes = int(np.prod(self.shape, dtype=np.int64)) * self.dtype.itemsize
+        self.ptr = ctx.alloc(self.nbytes)
+
+    def numpy(self) -> np.ndarray:
+        out = np.empty(self.shape, self.dtype)
+        self.ctx.copy_to_host(out, self.ptr)
+        return out
+
+    def upload(self, a: np.ndarray) -> "DeviceArray":
+        a = np.ascontiguousarray(a, self.dtype)
+        assert a.nbytes == self.nbytes, (a.shape, self.shape)
+        self.ctx.copy_to_device(self.ptr, a)
+        return self
+
+    def image(self) -> Image:
+        h, w = self.shape[0], self.shape[1]
+        return Image(self.ptr, w, h)
+
+    def free(self) -> None:
+        if self.ptr:
+            self.ctx.free(self.ptr)
+            self.ptr = None
+
+
+class Context:
+    """One eray_ctx (one GPU)."""
+
+    def __init__(self, device: int = 0):
+        self._h = _P()
+        check(lib().eray_ctx_create(device, C.byref(self._h)))
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self) -> None:
+        if self._h:
+            lib().eray_ctx_destroy(self._h)
+            self._h = _P()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, st: int) -> None:
+        check(st, self._h)
+
+    # memory ------------------------------------------------------------------------------
+    def alloc(self, nbytes: int) -> int:
+        p = _P()
+        self._check(lib().eray_device_alloc(self._h, nbytes, C.byref(p)))
+        return p.value
+
+    def free(self, ptr: int) -> None:
+        self._check(lib().eray_device_free(self._h, ptr))
+
+    def empty(self, shape, dtype=np.float32) -> DeviceArray:
+        return DeviceArray(self, shape, dtype)
+
+    def to_device(self, a: np.ndarray) -> DeviceArray:
+        a = np.ascontiguousarray(a)
+        return DeviceArray(self, a.shape, a.dtype).upload(a)
+
+    def memset(self, ptr: int, value: int, nbytes: int) -> None:
+        self._check(lib().eray_memset(self._h, ptr, value, nbytes))
+
+    def copy_to_device(self, dst: int, a: np.ndarray) -> None:
+        self._check(lib().eray_copy_to_device(self._h, dst, a.ctypes.data, a.nbytes))
+
+    def copy_to_host(self, a: np.ndarray, src: int) -> None:
+        self._check(lib().eray_copy_to_host(self._h, a.ctypes.data, src, a.nbytes))
+
+    def set_stream(self, stream_ptr) -> None:
+        self._check(lib().eray_set_stream(self._h, stream_ptr))
+
+    def synchronize(self) -> None:
+        self._check(lib().eray_synchronize(self._h))
+
+    # shaderlib ---------------------------------------------------------------------------
+    def node_wave(self, w, h, x_fac, y_fac, out_ptr) -> None:
+        self._check(lib().eray_node_wave(self._h, w, h, x_fac, y_fac, out_ptr))
+
+    def node_rgb(self, w, h, r: Image, g: Image, b: Image, out_ptr) -> None:
+        self._check(lib().eray_node_rgb(self._h, w, h, r, g, b, out_ptr))
+
+    def node_flat_color(self, w, h, r, g, b, out_ptr) -> None:
+        self._check(lib().eray_node_flat_color(self._h, w, h, r, g, b, out_ptr))
+
+    def node_mix_color(self, w, h, left: Image, right: Image, factor, out_ptr) -> None:
+        self._check(lib().eray_node_mix_color(self._h, w, h, left, right, factor, out_ptr))
+
+    def material_example(self, w, h, x_fac, y_fac, r, g, b, factor, color_ptr, diffuse_ptr) -> None:
+        self._check(lib().eray_material_example(self._h, w, h, x_fac, y_fac, r, g, b, factor,
+                                                color_ptr, diffuse_ptr))
+
+    # scene -------------------------------------------------------------------------------
+    def scene_reset(self) -> None:
+        self._check(lib().eray_scene_reset(self._h))
+
+    def set_camera(self, cam: Camera) -> None:
+        self._check(lib().eray_scene_set_camera(self._h, C.byref(cam)))
+
+    def add_light(self, light: Light) -> None:
+        self._check(lib().eray_scene_add_light(self._h, C.byref(light)))
+
+    def add_object(self, positions, normals, uvs, bbox_min=(0.0, 0.0, 0.0), bbox_max=(0.0, 0.0, 0.0),
+                   color: Image | None = None, diffuse: Image | None = None,
+                   specular: Image | None = None, specular_power: Image | None = None,
+                   reflection: Image | None = None) -> int:
+        P = np.ascontiguousarray(positions, np.float32).reshape(-1, 9)
+        N = np.ascontiguousarray(normals, np.float32).reshape(-1, 9)
+        U = np.ascontiguousarray(uvs, np.float32).reshape(-1, 6)
+        if not (P.shape[0] == N.shape[0] == U.shape[0]):
+            raise ValueError("positions/normals/uvs disagree on the triangle count")
+        none = Image(None, 0, 0)
+        mat = Material(color or none, diffuse or none, specular or none, specular_power or none,
+                       reflection or none)
+        obj = Object(P.ctypes.data, N.ctypes.data, U.ctypes.data, P.shape[0],
+                     (C.c_float * 3)(*bbox_min), (C.c_float * 3)(*bbox_max), mat)
+        idx = _U()
+        self._check(lib().eray_scene_add_object(self._h, C.byref(obj), C.byref(idx)))
+        return idx.value
+
+    def render(self, image_width, image_height, row0=0, rows=None, out_rgb=None, out_ppm=None,
+               out_face=None, bounces=0, anti_aliasing=0, flags=RENDER_DEFAULT) -> None:
+        if rows is None:
+            rows = image_height - row0
+        p = RenderParams(image_width, image_height, row0, rows, bounces, anti_aliasing,
+                         out_rgb or None, out_ppm or None, out_face or None, flags)
+        self._check(lib().eray_render(self._h, C.byref(p)))
+
+    def pack_ppm(self, rgb_ptr, w, h, out_ptr) -> None:
+        self._check(lib().eray_pack_ppm(self._h, rgb_ptr, w, h, out_ptr))

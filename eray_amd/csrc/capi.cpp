@@ -1,0 +1,505 @@
+// capi.cpp — implementation of include/eray_hip.h: context, device memory, scene upload and
+// kernel launches.  Host code only; the kernels live in render.hip and shaderlib.hip.
+//
+// Error policy: every HIP call is checked; failures and every case where the reference would
+// panic become a status code plus a message (eray_last_error).  Nothing here falls back to a
+// CPU path: without a usable GPU the calls fail loudly.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/eray_hip.h"
+#include "internal.hpp"
+
+using namespace eray::gpu;
+
+namespace {
+thread_local std::string g_thread_error;
+
+struct HostObject {
+    std::vector<float> raw;  // T*9 positions | T*9 normals | T*6 uvs
+    uint32_t T = 0;
+    float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+    eray_material mat{};
+};
+}  // namespace
+
+struct eray_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    eray_camera camera{{0.0f, 0.0f, 0.0f}, {60.0f, 60.0f}, 1024u, 1.0f};  // Camera::default()
+    std::vector<eray_light> lights;
+    std::vector<HostObject> objects;
+
+    bool geom_dirty = true, desc_dirty = true, cull_dirty = true;
+    TriHot* d_hot = nullptr;
+    TriShade* d_shade = nullptr;
+    TriCull* d_cull = nullptr;
+    size_t tri_cap = 0;
+    float* d_raw = nullptr;
+    size_t raw_cap = 0;
+    ObjectDesc* d_objs = nullptr;
+    size_t objs_cap = 0;
+    LightDesc* d_lights = nullptr;
+    size_t lights_cap = 0;
+    std::vector<ObjectDesc> h_objs;  // kept alive for the async uploads
+    std::vector<LightDesc> h_lights;
+    std::vector<float> h_raw;
+    uint32_t total_tris = 0;
+};
+
+namespace {
+
+int set_error(eray_ctx* ctx, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (ctx)
+        ctx->err = buf;
+    else
+        g_thread_error = buf;
+    return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                   \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return set_error((ctx), e_ == hipErrorOutOfMemory ? ERAY_E_OUT_OF_MEMORY : ERAY_E_HIP, \
+                             "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+    } while (0)
+
+int use_device(eray_ctx* ctx) {
+    if (!ctx) return set_error(nullptr, ERAY_E_INVALID_ARGUMENT, "null context");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    return ERAY_OK;
+}
+
+template <typename T>
+int ensure(eray_ctx* ctx, T** ptr, size_t* cap, size_t need) {
+    if (need <= *cap && *ptr) return ERAY_OK;
+    if (*ptr) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipFree(*ptr));
+        *ptr = nullptr;
+        *cap = 0;
+    }
+    size_t n = need ? need : 1;
+    HIP_TRY(ctx, hipMalloc((void**)ptr, n * sizeof(T)));
+    *cap = n;
+    return ERAY_OK;
+}
+
+uint32_t sat_u32_host(float f) {
+    if (!(f > 0.0f)) return 0u;
+    if (f >= 4294967296.0f) return 0xffffffffu;
+    return (uint32_t)f;
+}
+
+bool image_ok(const eray_image& im) { return !im.data || (im.width > 0 && im.height > 0); }
+TexView tex(const eray_image& im) { return TexView{im.data, im.width, im.height}; }
+
+int sync_scene(eray_ctx* ctx, bool need_cull) {
+    int st;
+    // The host staging vectors below feed async copies: drain earlier ones before reuse.
+    if (ctx->geom_dirty || ctx->desc_dirty) HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->geom_dirty) {
+        uint32_t T = 0;
+        for (auto& o : ctx->objects) T += o.T;
+        ctx->total_tris = T;
+        if ((st = ensure(ctx, &ctx->d_hot, &ctx->tri_cap, T))) return st;
+        size_t shade_cap = ctx->tri_cap;
+        // shade shares the capacity bookkeeping of hot: (re)allocate alongside
+        if (ctx->d_shade) {
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            HIP_TRY(ctx, hipFree(ctx->d_shade));
+            ctx->d_shade = nullptr;
+        }
+        HIP_TRY(ctx, hipMalloc((void**)&ctx->d_shade, shade_cap * sizeof(TriShade)));
+        if (ctx->d_cull) {
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            HIP_TRY(ctx, hipFree(ctx->d_cull));
+            ctx->d_cull = nullptr;
+        }
+        HIP_TRY(ctx, hipMalloc((void**)&ctx->d_cull, shade_cap * sizeof(TriCull)));
+        ctx->h_raw.assign((size_t)T * 24, 0.0f);
+        size_t off = 0;
+        for (auto& o : ctx->objects) {
+            std::memcpy(&ctx->h_raw[off * 9], o.raw.data(), sizeof(float) * 9 * o.T);
+            std::memcpy(&ctx->h_raw[(size_t)T * 9 + off * 9], o.raw.data() + 9 * (size_t)o.T,
+                        sizeof(float) * 9 * o.T);
+            std::memcpy(&ctx->h_raw[(size_t)T * 18 + off * 6], o.raw.data() + 18 * (size_t)o.T,
+                        sizeof(float) * 6 * o.T);
+            off += o.T;
+        }
+        if ((st = ensure(ctx, &ctx->d_raw, &ctx->raw_cap, (size_t)T * 24))) return st;
+        if (T) {
+            HIP_TRY(ctx, hipMemcpyAsync(ctx->d_raw, ctx->h_raw.data(), sizeof(float) * 24 * (size_t)T,
+                                        hipMemcpyHostToDevice, ctx->stream));
+            HIP_TRY(ctx, launch_tri_precompute(ctx->d_raw, ctx->d_raw + 9 * (size_t)T,
+                                               ctx->d_raw + 18 * (size_t)T, T, ctx->d_hot,
+                                               ctx->d_shade, ctx->stream));
+        }
+        ctx->geom_dirty = false;
+        ctx->cull_dirty = true;
+        ctx->desc_dirty = true;
+    }
+    if (ctx->desc_dirty) {
+        ctx->h_objs.clear();
+        uint32_t begin = 0;
+        for (auto& o : ctx->objects) {
+            ObjectDesc d{};
+            d.tri_begin = begin;
+            d.tri_count = o.T;
+            for (int k = 0; k < 3; ++k) {
+                d.bb_lo[k] = o.lo[k];
+                d.bb_hi[k] = o.hi[k];
+            }
+            d.mat = MaterialDesc{tex(o.mat.color), tex(o.mat.diffuse), tex(o.mat.specular),
+                                 tex(o.mat.specular_power), tex(o.mat.reflection)};
+            ctx->h_objs.push_back(d);
+            begin += o.T;
+        }
+        ctx->h_lights.clear();
+        for (auto& l : ctx->lights) {
+            LightDesc d{};
+            for (int k = 0; k < 3; ++k) {
+                d.pos[k] = l.position[k];
+                d.color[k] = l.color[k];
+            }
+            d.variant = l.variant;
+            d.brightness = l.brightness;
+            ctx->h_lights.push_back(d);
+        }
+        if ((st = ensure(ctx, &ctx->d_objs, &ctx->objs_cap, ctx->h_objs.size()))) return st;
+        if ((st = ensure(ctx, &ctx->d_lights, &ctx->lights_cap, ctx->h_lights.size()))) return st;
+        if (!ctx->h_objs.empty())
+            HIP_TRY(ctx, hipMemcpyAsync(ctx->d_objs, ctx->h_objs.data(), sizeof(ObjectDesc) * ctx->h_objs.size(),
+                                        hipMemcpyHostToDevice, ctx->stream));
+        if (!ctx->h_lights.empty())
+            HIP_TRY(ctx, hipMemcpyAsync(ctx->d_lights, ctx->h_lights.data(),
+                                        sizeof(LightDesc) * ctx->h_lights.size(), hipMemcpyHostToDevice,
+                                        ctx->stream));
+        ctx->desc_dirty = false;
+    }
+    if (need_cull && ctx->cull_dirty) {
+        const eray_camera& c = ctx->camera;
+        HIP_TRY(ctx, launch_tri_cull(ctx->d_hot, ctx->total_tris, c.center[0], c.center[1], c.center[2],
+                                     c.fov[0] / c.fov[1], c.z_dist, ctx->d_cull, ctx->stream));
+        ctx->cull_dirty = false;
+    }
+    return ERAY_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int eray_abi_version(void) { return ERAY_ABI_VERSION; }
+
+int eray_ctx_create(int device, eray_ctx** out) {
+    if (!out) return set_error(nullptr, ERAY_E_INVALID_ARGUMENT, "out is null");
+    *out = nullptr;
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count == 0)
+        return set_error(nullptr, ERAY_E_HIP, "no HIP device available (%s)",
+                         e == hipSuccess ? "0 devices" : hipGetErrorString(e));
+    if (device < 0 || device >= count)
+        return set_error(nullptr, ERAY_E_INVALID_ARGUMENT, "device %d out of range (%d devices)", device, count);
+    eray_ctx* ctx = new (std::nothrow) eray_ctx();
+    if (!ctx) return set_error(nullptr, ERAY_E_OUT_OF_MEMORY, "context allocation failed");
+    ctx->device = device;
+    e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete ctx;
+        return set_error(nullptr, ERAY_E_HIP, "context init: %s", hipGetErrorString(e));
+    }
+    ctx->stream = ctx->own_stream;
+    *out = ctx;
+    return ERAY_OK;
+}
+
+int eray_ctx_destroy(eray_ctx* ctx) {
+    if (!ctx) return ERAY_OK;
+    hipSetDevice(ctx->device);
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    void* bufs[] = {ctx->d_hot, ctx->d_shade, ctx->d_cull, ctx->d_raw, ctx->d_objs, ctx->d_lights};
+    for (void* b : bufs)
+        if (b) hipFree(b);
+    if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+    return ERAY_OK;
+}
+
+const char* eray_last_error(const eray_ctx* ctx) {
+    return ctx ? ctx->err.c_str() : g_thread_error.c_str();
+}
+
+int eray_set_stream(eray_ctx* ctx, void* stream) {
+    if (int st = use_device(ctx)) return st;
+    ctx->stream = stream ? (hipStream_t)stream : ctx->own_stream;
+    return ERAY_OK;
+}
+
+void* eray_get_stream(eray_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int eray_synchronize(eray_ctx* ctx) {
+    if (int st = use_device(ctx)) return st;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return ERAY_OK;
+}
+
+int eray_device_alloc(eray_ctx* ctx, size_t bytes, void** dev_ptr) {
+    if (int st = use_device(ctx)) return st;
+    if (!dev_ptr) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "dev_ptr is null");
+    HIP_TRY(ctx, hipMalloc(dev_ptr, bytes ? bytes : 1));
+    return ERAY_OK;
+}
+
+int eray_device_free(eray_ctx* ctx, void* dev_ptr) {
+    if (int st = use_device(ctx)) return st;
+    if (!dev_ptr) return ERAY_OK;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipFree(dev_ptr));
+    return ERAY_OK;
+}
+
+int eray_memset(eray_ctx* ctx, void* dev_ptr, int value, size_t bytes) {
+    if (int st = use_device(ctx)) return st;
+    if (!bytes) return ERAY_OK;
+    if (!dev_ptr) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "dev_ptr is null");
+    HIP_TRY(ctx, hipMemsetAsync(dev_ptr, value, bytes, ctx->stream));
+    return ERAY_OK;
+}
+
+int eray_copy_to_device(eray_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (int st = use_device(ctx)) return st;
+    if (!bytes) return ERAY_OK;
+    if (!dst || !src) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "null pointer");
+    HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return ERAY_OK;
+}
+
+int eray_copy_to_host(eray_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (int st = use_device(ctx)) return st;
+    if (!bytes) return ERAY_OK;
+    if (!dst || !src) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "null pointer");
+    HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return ERAY_OK;
+}
+
+// ------------------------------------------------------------------------ shaderlib ---------
+int eray_node_wave(eray_ctx* ctx, uint32_t w, uint32_t h, float x_fac, float y_fac, float* out) {
+    if (int st = use_device(ctx)) return st;
+    if ((size_t)w * h && !out) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "wave: out is null");
+    HIP_TRY(ctx, launch_wave(w, h, x_fac, y_fac, out, ctx->stream));
+    return ERAY_OK;
+}
+
+int eray_node_rgb(eray_ctx* ctx, uint32_t w, uint32_t h, eray_image r, eray_image g, eray_image b,
+                  float* out) {
+    if (int st = use_device(ctx)) return st;
+    const size_t n = (size_t)w * h;
+    const eray_image* in[3] = {&r, &g, &b};
+    const char* names[3] = {"red", "green", "blue"};
+    for (int k = 0; k < 3; ++k) {
+        if (!in[k]->data)
+            return set_error(ctx, ERAY_E_MISSING, "rgb: missing input `%s`", names[k]);
+        if ((size_t)in[k]->width * in[k]->height < n)
+            return set_error(ctx, ERAY_E_OUT_OF_BOUNDS,
+                             "rgb: input `%s` has %zu pixels, the %ux%u output indexes %zu",
+                             names[k], (size_t)in[k]->width * in[k]->height, w, h, n);
+    }
+    if (n && !out) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "rgb: out is null");
+    HIP_TRY(ctx, launch_rgb(w, h, r.data, g.data, b.data, out, ctx->stream));
+    return ERAY_OK;
+}
+
+int eray_node_flat_color(eray_ctx* ctx, uint32_t w, uint32_t h, float r, float g, float b,
+                         float* out) {
+    if (int st = use_device(ctx)) return st;
+    if ((size_t)w * h && !out) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "flat_color: out is null");
+    HIP_TRY(ctx, launch_flat(w, h, r, g, b, out, ctx->stream));
+    return ERAY_OK;
+}
+
+int eray_node_mix_color(eray_ctx* ctx, uint32_t w, uint32_t h, eray_image left, eray_image right,
+                        float factor, float* out) {
+    if (int st = use_device(ctx)) return st;
+    if (!left.data) return set_error(ctx, ERAY_E_MISSING, "mix_color: missing input `left`");
+    if (!right.data) return set_error(ctx, ERAY_E_MISSING, "mix_color: missing input `right`");
+    const size_t n = (size_t)w * h;
+    if (n && (!left.width || !left.height || !right.width || !right.height))
+        return set_error(ctx, ERAY_E_OUT_OF_BOUNDS, "mix_color: empty input image (mod_get by 0)");
+    if (n && !out) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "mix_color: out is null");
+    HIP_TRY(ctx, launch_mix(w, h, tex(left), tex(right), factor, out, ctx->stream));
+    return ERAY_OK;
+}
+
+int eray_material_example(eray_ctx* ctx, uint32_t w, uint32_t h, float x_fac, float y_fac, float r,
+                          float g, float b, float factor, float* out_color, float* out_diffuse) {
+    if (int st = use_device(ctx)) return st;
+    HIP_TRY(ctx, launch_material_example(w, h, x_fac, y_fac, r, g, b, factor, out_color, out_diffuse,
+                                         ctx->stream));
+    return ERAY_OK;
+}
+
+// ------------------------------------------------------------------------ scene -------------
+int eray_scene_reset(eray_ctx* ctx) {
+    if (!ctx) return set_error(nullptr, ERAY_E_INVALID_ARGUMENT, "null context");
+    ctx->objects.clear();
+    ctx->lights.clear();
+    ctx->camera = eray_camera{{0.0f, 0.0f, 0.0f}, {60.0f, 60.0f}, 1024u, 1.0f};
+    ctx->geom_dirty = ctx->desc_dirty = ctx->cull_dirty = true;
+    return ERAY_OK;
+}
+
+int eray_scene_set_camera(eray_ctx* ctx, const eray_camera* camera) {
+    if (!ctx || !camera) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "null argument");
+    if (std::memcmp(&ctx->camera, camera, sizeof(eray_camera)) != 0) {
+        ctx->camera = *camera;
+        ctx->cull_dirty = true;
+    }
+    return ERAY_OK;
+}
+
+int eray_scene_add_light(eray_ctx* ctx, const eray_light* light) {
+    if (!ctx || !light) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "null argument");
+    if (light->variant != ERAY_LIGHT_POINT && light->variant != ERAY_LIGHT_AMBIENT)
+        return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "unknown light variant %d", light->variant);
+    ctx->lights.push_back(*light);
+    ctx->desc_dirty = true;
+    return ERAY_OK;
+}
+
+int eray_scene_add_object(eray_ctx* ctx, const eray_object* obj, uint32_t* index) {
+    if (!ctx || !obj) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "null argument");
+    const uint32_t T = obj->triangle_count;
+    if (T && (!obj->positions || !obj->normals || !obj->uvs))
+        return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "object arrays are null");
+    const eray_material& m = obj->material;
+    if (!image_ok(m.color) || !image_ok(m.diffuse) || !image_ok(m.specular) ||
+        !image_ok(m.specular_power) || !image_ok(m.reflection))
+        return set_error(ctx, ERAY_E_OUT_OF_BOUNDS, "material image with zero width or height (mod_get by 0)");
+    uint64_t total = T;
+    for (auto& o : ctx->objects) total += o.T;
+    if (total > (1ull << 31)) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "too many triangles");
+    HostObject h;
+    h.T = T;
+    h.raw.resize((size_t)T * 24);
+    if (T) {
+        std::memcpy(h.raw.data(), obj->positions, sizeof(float) * 9 * (size_t)T);
+        std::memcpy(h.raw.data() + 9 * (size_t)T, obj->normals, sizeof(float) * 9 * (size_t)T);
+        std::memcpy(h.raw.data() + 18 * (size_t)T, obj->uvs, sizeof(float) * 6 * (size_t)T);
+    }
+    for (int k = 0; k < 3; ++k) {
+        h.lo[k] = obj->bbox_min[k];
+        h.hi[k] = obj->bbox_max[k];
+    }
+    h.mat = m;
+    ctx->objects.push_back(std::move(h));
+    if (index) *index = (uint32_t)(ctx->objects.size() - 1);
+    ctx->geom_dirty = ctx->desc_dirty = ctx->cull_dirty = true;
+    return ERAY_OK;
+}
+
+int eray_camera_size(const eray_camera* c, uint32_t* w, uint32_t* h) {
+    if (!c || !w || !h) return set_error(nullptr, ERAY_E_INVALID_ARGUMENT, "null argument");
+    *w = c->width;
+    *h = sat_u32_host((float)c->width / (c->fov[0] / c->fov[1]));
+    return ERAY_OK;
+}
+
+// ------------------------------------------------------------------------ render ------------
+int eray_render(eray_ctx* ctx, const eray_render_params* rp) {
+    if (int st = use_device(ctx)) return st;
+    if (!rp) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "params is null");
+    if (rp->anti_aliasing != 0)
+        return set_error(ctx, ERAY_E_UNSUPPORTED,
+                         "anti_aliasing > 0 uses rand::thread_rng (engine.rs:49,62-69); not supported");
+    if (rp->bounces > 0)
+        for (auto& o : ctx->objects)
+            if (o.mat.reflection.data)
+                return set_error(ctx, ERAY_E_UNSUPPORTED,
+                                 "reflection bounces (engine.rs:181-191) are not supported yet");
+    uint32_t W, H;
+    eray_camera_size(&ctx->camera, &W, &H);
+    if ((uint64_t)rp->row0 + rp->rows > H)
+        return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "rows [%u, %u) exceed the camera height %u", rp->row0,
+                         rp->row0 + rp->rows, H);
+    // Image::set indexes y * image.width + x and panics past the end (image.rs:41-43)
+    if (W && H &&
+        (uint64_t)(H - 1) * rp->image_width + (W - 1) >= (uint64_t)rp->image_width * rp->image_height)
+        return set_error(ctx, ERAY_E_OUT_OF_BOUNDS,
+                         "camera size %ux%u does not fit the %ux%u engine image (Image::set panics)", W, H,
+                         rp->image_width, rp->image_height);
+    if (rp->out_ppm && (W != rp->image_width || H != rp->image_height))
+        return set_error(ctx, ERAY_E_INVALID_ARGUMENT,
+                         "fused PPM output needs camera size == image size; use eray_pack_ppm");
+    const bool cull = !(rp->flags & ERAY_RENDER_BRUTE_FORCE);
+    if (int st = sync_scene(ctx, cull)) return st;
+    if (!rp->rows || !W) return ERAY_OK;
+
+    FrameParams p{};
+    const eray_camera& c = ctx->camera;
+    p.cx = c.center[0];
+    p.cy = c.center[1];
+    p.cz = c.center[2];
+    p.ratio = c.fov[0] / c.fov[1];
+    p.z_dist = c.z_dist;
+    p.cam_w = W;
+    p.cam_h = H;
+    p.img_w = rp->image_width;
+    p.img_h = rp->image_height;
+    p.row0 = rp->row0;
+    p.rows = rp->rows;
+    p.out_rgb = rp->out_rgb;
+    p.out_ppm = rp->out_ppm;
+    p.out_face = rp->out_face;
+    p.tris = ctx->d_hot;
+    p.shade = ctx->d_shade;
+    p.cull = cull ? ctx->d_cull : nullptr;
+    p.objects = ctx->d_objs;
+    p.lights = ctx->d_lights;
+    p.nobj = (uint32_t)ctx->objects.size();
+    p.nlights = (uint32_t)ctx->lights.size();
+    p.tiles_x = (W + 15) / 16;
+    HIP_TRY(ctx, launch_render(p, ctx->stream));
+    return ERAY_OK;
+}
+
+int eray_pack_ppm(eray_ctx* ctx, const float* rgb, uint32_t w, uint32_t h, uint8_t* out) {
+    if (int st = use_device(ctx)) return st;
+    if ((size_t)w * h && (!rgb || !out)) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "null pointer");
+    HIP_TRY(ctx, launch_pack_ppm(rgb, w, h, out, ctx->stream));
+    return ERAY_OK;
+}
+
+int eray_ppm_header(uint32_t w, uint32_t h, char* buf, size_t cap, size_t* len) {
+    char tmp[64];
+    int n = std::snprintf(tmp, sizeof tmp, "P6 %u %u %u\n", w, h, 255u);
+    if (n < 0) return set_error(nullptr, ERAY_E_INVALID_ARGUMENT, "format failed");
+    if (len) *len = (size_t)n;
+    if (buf) {
+        if (cap < (size_t)n + 1) return set_error(nullptr, ERAY_E_INVALID_ARGUMENT, "buffer too small");
+        std::memcpy(buf, tmp, (size_t)n + 1);
+    }
+    return ERAY_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,158 @@
+// glibc_cosf.hpp — f32 cosine bit-identical to the reference's `f32::cos` on x86-64 Linux.
+//
+// The reference's wave node (src/shaderlib/wave.rs:127) calls Rust's f32::cos, which lowers
+// to the platform libm's `cosf`.  On the reference's platform (x86-64 glibc, here 2.35) that is
+// the ARM optimized-routines single-precision sin/cos (glibc sysdeps/ieee754/flt-32/s_cosf.c,
+// sincosf.h, sincosf_data.c; in glibc since 2.28).  Its published algorithm:
+//   |x| < pi/4         : cos polynomial in double (1 for |x| < 2^-12)
+//   |x| < 120          : n = round(x * 2/pi) via a 2^24-scaled multiply, r = x - n*pi/2
+//   |x| < inf          : Payne-Hanek style reduction with a 4/pi bit table (reduce_large)
+//   then sin or cos polynomial of r (selected and signed by the quadrant), rounded to float.
+// All intermediate arithmetic is double.  GCC contracts the polynomial steps and the reduction
+// into FMAs on FMA-capable hosts (the __cosf_fma ifunc variant); the float result was checked
+// to be identical with and without contraction, and this restatement was checked bit-for-bit
+// against the host glibc over every finite float (tests/test_libm_restatement.py).
+//
+// The 4/pi table is the binary expansion of 4/pi in sliding 32-bit windows (8 new bits per
+// entry); it is derived from first principles in tests/test_libm_restatement.py.
+#pragma once
+
+#include <stdint.h>
+#include <string.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define ERAY_HD __host__ __device__
+#else
+#include <math.h>
+#define ERAY_HD
+#endif
+
+namespace eray {
+namespace libm {
+
+struct SinCosCoeffs {
+    double sign[4];
+    double hpi_inv;  // 2/pi * 2^24
+    double hpi;      // pi/2
+    double c0, c1, c2, c3, c4;
+    double s1, s2, s3;
+};
+
+ERAY_HD inline const SinCosCoeffs& sincos_coeffs(int which) {
+    static const SinCosCoeffs kTab[2] = {
+        {{1.0, -1.0, -1.0, 1.0},
+         0x1.45F306DC9C883p+23,
+         0x1.921FB54442D18p0,
+         0x1p0,
+         -0x1.ffffffd0c621cp-2,
+         0x1.55553e1068f19p-5,
+         -0x1.6c087e89a359dp-10,
+         0x1.99343027bf8c3p-16,
+         -0x1.555545995a603p-3,
+         0x1.1107605230bc4p-7,
+         -0x1.994eb3774cf24p-13},
+        {{1.0, -1.0, -1.0, 1.0},
+         0x1.45F306DC9C883p+23,
+         0x1.921FB54442D18p0,
+         -0x1p0,
+         0x1.ffffffd0c621cp-2,
+         -0x1.55553e1068f19p-5,
+         0x1.6c087e89a359dp-10,
+         -0x1.99343027bf8c3p-16,
+         -0x1.555545995a603p-3,
+         0x1.1107605230bc4p-7,
+         -0x1.994eb3774cf24p-13},
+    };
+    return kTab[which];
+}
+
+ERAY_HD inline uint32_t inv_pio4(int i) {
+    static const uint32_t kInvPio4[24] = {
+        0xa2u,       0xa2f9u,     0xa2f983u,   0xa2f9836eu, 0xf9836e4eu, 0x836e4e44u,
+        0x6e4e4415u, 0x4e441529u, 0x441529fcu, 0x1529fc27u, 0x29fc2757u, 0xfc2757d1u,
+        0x2757d1f5u, 0x57d1f534u, 0xd1f534ddu, 0xf534ddc0u, 0x34ddc0dbu, 0xddc0db62u,
+        0xc0db6295u, 0xdb629599u, 0x6295993cu, 0x95993c43u, 0x993c4390u, 0x3c439041u};
+    return kInvPio4[i];
+}
+
+ERAY_HD inline uint32_t f32_bits(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return u;
+}
+ERAY_HD inline uint32_t abstop12(float f) { return (f32_bits(f) >> 20) & 0x7ff; }
+
+ERAY_HD inline double fma_d(double a, double b, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_fma(a, b, c);
+#else
+    return fma(a, b, c);
+#endif
+}
+
+// sin (n even) or cos (n odd) polynomial of the reduced argument, rounded to float.
+ERAY_HD inline float sincos_poly(double x, double x2, const SinCosCoeffs& p, int n) {
+    if ((n & 1) == 0) {
+        double x3 = x * x2;
+        double s1 = fma_d(x2, p.s3, p.s2);
+        double x7 = x3 * x2;
+        double s = fma_d(x3, p.s1, x);
+        return (float)fma_d(x7, s1, s);
+    }
+    double x4 = x2 * x2;
+    double c2 = fma_d(x2, p.c4, p.c3);
+    double c1 = fma_d(x2, p.c1, p.c0);
+    double x6 = x4 * x2;
+    double c = fma_d(x4, p.c2, c1);
+    return (float)fma_d(x6, c2, c);
+}
+
+// Reduction of |x| >= 120 with 4/pi to 96 significant bits: returns r in [-pi/4, pi/4]
+// (before the final scaling) and the quadrant.
+ERAY_HD inline double reduce_large(uint32_t xi, int* np) {
+    int base = (int)((xi >> 26) & 15);
+    int shift = (int)((xi >> 23) & 7);
+    xi = (xi & 0xffffffu) | 0x800000u;
+    xi <<= shift;
+    uint64_t res0 = (uint64_t)(uint32_t)(xi * inv_pio4(base));
+    uint64_t res1 = (uint64_t)xi * inv_pio4(base + 4);
+    uint64_t res2 = (uint64_t)xi * inv_pio4(base + 8);
+    res0 = (res2 >> 32) | (res0 << 32);
+    res0 += res1;
+    uint64_t n = (res0 + (1ULL << 61)) >> 62;
+    res0 -= n << 62;
+    double x = (double)(int64_t)res0;
+    *np = (int)n;
+    return x * 0x1.921FB54442D18p-62;
+}
+
+// cosf(y) as computed by the reference platform's libm.
+ERAY_HD inline float cosf_glibc(float y) {
+    double x = y;
+    const SinCosCoeffs* p = &sincos_coeffs(0);
+    int n;
+    if (abstop12(y) < abstop12(0x1.921FB6p-1f)) {  // |y| < pi/4
+        double x2 = x * x;
+        if (abstop12(y) < abstop12(0x1p-12f)) return 1.0f;
+        return sincos_poly(x, x2, *p, 1);
+    } else if (abstop12(y) < abstop12(120.0f)) {
+        double r = x * p->hpi_inv;
+        n = ((int32_t)r + 0x800000) >> 24;
+        x = fma_d(-(double)n, p->hpi, x);
+        double s = p->sign[n & 3];
+        if (n & 2) p = &sincos_coeffs(1);
+        return sincos_poly(x * s, x * x, *p, n ^ 1);
+    } else if (abstop12(y) < abstop12(__builtin_inff())) {
+        uint32_t xi = f32_bits(y);
+        int sign = (int)(xi >> 31);
+        x = reduce_large(xi, &n);
+        double s = p->sign[(n + sign) & 3];
+        if ((n + sign) & 2) p = &sincos_coeffs(1);
+        return sincos_poly(x * s, x * x, *p, n ^ 1);
+    }
+    return (y - y) / (y - y);  // inf or NaN -> NaN
+}
+
+}  // namespace libm
+}  // namespace eray

@@ -1,0 +1,104 @@
+// internal.hpp — descriptors shared by the C-ABI layer (capi.cpp) and the gfx950 kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace eray {
+namespace gpu {
+
+// Hot per-triangle record of the exact test, 48 B (three 16-B loads), computed on the device
+// from the face vertices with the reference's own operations (primitives.rs:44-46):
+//   q0 = (e1.x, e1.y, e1.z, e2.x)   q1 = (e2.y, e2.z, n.x, n.y)   q2 = (n.z, a.x, a.y, a.z)
+struct __align__(16) TriHot {
+    float4 q0, q1, q2;
+};
+
+// Cold per-triangle shading record, 64 B, read only for the hit face:
+//   s0 = (na.x, na.y, na.z, nb.x)  s1 = (nb.y, nb.z, nc.x, nc.y)
+//   s2 = (nc.z, uva.u, uva.v, uvb.u)  s3 = (uvb.v, uvc.u, uvc.v, 0)
+struct __align__(16) TriShade {
+    float4 s0, s1, s2, s3;
+};
+
+// Camera-dependent culling record of a triangle for primary rays (see render.hip,
+// "exact wave culling").  For each of the four conditions k in {u, v, w, n}:
+//   f_k(x', y') = K_k + A_k x' + B_k y'   (a real-valued bound of the reference's test value
+//   along the camera ray through viewport coordinate (x', y')), rejected for a whole pixel
+//   rectangle when max f_k < -T_k.
+struct __align__(16) TriCull {
+    float4 A;  // A_u, A_v, A_w, A_n
+    float4 B;
+    float4 K;
+    float4 T;  // thresholds (>= 0; +inf disables the condition)
+};
+
+struct TexView {
+    const float* data;  // nullptr: the output is absent (Option::None)
+    uint32_t w, h;
+};
+
+struct MaterialDesc {
+    TexView color;  // IColor, 3 floats per texel
+    TexView diffuse, specular, specular_power, reflection;  // IValue
+};
+
+struct ObjectDesc {
+    uint32_t tri_begin, tri_count;
+    float bb_lo[3], bb_hi[3];
+    MaterialDesc mat;
+};
+
+struct LightDesc {
+    float pos[3];
+    int32_t variant;  // 0 point, 1 ambient
+    float color[3];
+    float brightness;
+};
+
+constexpr int kMaxObjects = 64;
+constexpr int kMaxLights = 64;
+
+struct FrameParams {
+    // camera (camera.rs:57-76)
+    float cx, cy, cz;
+    float ratio;  // fov0 / fov1
+    float z_dist;
+    uint32_t cam_w, cam_h;
+    // output
+    uint32_t img_w, img_h;
+    uint32_t row0, rows;
+    float* out_rgb;
+    uint8_t* out_ppm;
+    int32_t* out_face;
+    // scene
+    const TriHot* tris;
+    const TriShade* shade;
+    const TriCull* cull;  // nullptr: brute force
+    const ObjectDesc* objects;
+    const LightDesc* lights;
+    uint32_t nobj, nlights;
+    uint32_t tiles_x;  // pixel tiles per row
+};
+
+// ------------------------------------------------------------- launchers (.hip files) ------
+hipError_t launch_tri_precompute(const float* pos, const float* nrm, const float* uv, uint32_t T,
+                                 TriHot* hot, TriShade* shade, hipStream_t s);
+hipError_t launch_tri_cull(const TriHot* hot, uint32_t T, float cx, float cy, float cz, float ratio,
+                           float z_dist, TriCull* cull, hipStream_t s);
+hipError_t launch_render(const FrameParams& p, hipStream_t s);
+hipError_t launch_pack_ppm(const float* rgb, uint32_t w, uint32_t h, uint8_t* out, hipStream_t s);
+
+hipError_t launch_wave(uint32_t w, uint32_t h, float xf, float yf, float* out, hipStream_t s);
+hipError_t launch_rgb(uint32_t w, uint32_t h, const float* r, const float* g, const float* b,
+                      float* out, hipStream_t s);
+hipError_t launch_flat(uint32_t w, uint32_t h, float r, float g, float b, float* out,
+                       hipStream_t s);
+hipError_t launch_mix(uint32_t w, uint32_t h, TexView left, TexView right, float factor,
+                      float* out, hipStream_t s);
+hipError_t launch_material_example(uint32_t w, uint32_t h, float xf, float yf, float r, float g,
+                                   float b, float factor, float* color, float* diffuse,
+                                   hipStream_t s);
+
+}  // namespace gpu
+}  // namespace eray

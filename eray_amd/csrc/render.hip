@@ -1,0 +1,517 @@
+// render.hip — the per-pixel ray-tracing hot path on gfx950 (CDNA4).
+//
+// Replaces Engine::render (src/lib/engine.rs:46-81) with the PPM byte pack of
+// Image::save_as_ppm (src/lib/image.rs:48-74) fused in.  One thread per pixel; a 256-thread
+// workgroup owns a 16x16 pixel tile and each 64-lane wave an 8x8 sub-tile.
+//
+// First-hit search (Object::intersects, object.rs:58-81): the workgroup streams the object's
+// triangles in index order through LDS in tiles of kTriTile records; each ray keeps the FIRST
+// face (by index) whose Triangle::intersects (primitives.rs:41-72) passes — the reference's
+// semantics, not the nearest hit.  The loop ends as soon as no ray of the workgroup is still
+// searching (__syncthreads_or).
+//
+// Exact wave culling (primary rays only; disabled by ERAY_RENDER_BRUTE_FORCE).  For a camera
+// ray the reference's test quantities are linear in the (unnormalised) ray direction, and the
+// camera directions of an 8x8 pixel block span a small convex cone.  Per camera, each triangle
+// gets four affine bounds f_k(x', y') of those quantities with float-error margins T_k
+// (tri_cull_kernel, see the derivation there).  A wave evaluates them triangle-parallel —
+// lane j takes triangle j of a 64-triangle chunk — and __ballot()s the survivors; only the
+// survivors are tested ray-parallel, in index order, with the reference's exact arithmetic.
+// The margins make the cull conservative: a triangle the exact test could accept for any ray
+// of the block is never dropped, so results are identical to the brute-force scan
+// (tests/test_render_gpu.py checks this bit-for-bit).
+//
+// Shadow rays (engine.rs:136-142, 218-228) go through the same LDS tiles without culling; the
+// reference's degenerate bounding box rejects almost all of them before the scan.
+#include "device_math.hpp"
+#include "internal.hpp"
+
+namespace eray {
+namespace gpu {
+namespace {
+
+using namespace eray::dev;
+
+constexpr int kWG = 256;
+constexpr int kTileW = 16, kTileH = 16;
+constexpr int kTriTile = 256;
+
+// --------------------------------------------------------------------- triangle setup ------
+// Triangle::intersects recomputes e1 = b - a, e2 = c - a, n = e1 x e2 for every test
+// (primitives.rs:44-46); they do not depend on the ray, so they are computed once here with
+// the same f32 operations (bit-identical values).
+__global__ void __launch_bounds__(256) tri_precompute_kernel(const float* __restrict__ pos,
+                                                             const float* __restrict__ nrm,
+                                                             const float* __restrict__ uv,
+                                                             uint32_t T, TriHot* __restrict__ hot,
+                                                             TriShade* __restrict__ shade) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= T) return;
+    const float* P = pos + 9 * (size_t)i;
+    f3 a = mk3(P[0], P[1], P[2]), b = mk3(P[3], P[4], P[5]), c = mk3(P[6], P[7], P[8]);
+    f3 e1 = sub(b, a), e2 = sub(c, a);
+    f3 n = cross(e1, e2);
+    hot[i].q0 = make_float4(e1.x, e1.y, e1.z, e2.x);
+    hot[i].q1 = make_float4(e2.y, e2.z, n.x, n.y);
+    hot[i].q2 = make_float4(n.z, a.x, a.y, a.z);
+    const float* N = nrm + 9 * (size_t)i;
+    const float* U = uv + 6 * (size_t)i;
+    shade[i].s0 = make_float4(N[0], N[1], N[2], N[3]);
+    shade[i].s1 = make_float4(N[4], N[5], N[6], N[7]);
+    shade[i].s2 = make_float4(N[8], U[0], U[1], U[2]);
+    shade[i].s3 = make_float4(U[3], U[4], U[5], 0.0f);
+}
+
+// --------------------------------------------------------------------- culling record ------
+// Derivation (u = 2^-24, all norms are 1-norms of the float inputs; d = normalised direction).
+// The reference computes, in f32 from ao = C - a (C the camera centre),
+//   det = -(d.n),  a_u = e2.(ao x d),  a_v = -(e1.(ao x d)),  u = a_u/det, v = a_v/det,
+//   t = (ao.n)/det,  hit iff det >= 1e-6, t >= 0, u >= 0, v >= 0, u + v <= 1.
+// In real arithmetic on the same float inputs these are linear in d:
+//   det = d.(-n), a_u = d.w_u (w_u = e2 x ao), a_v = d.w_v (w_v = ao x e1), and
+//   det - a_u - a_v = d.w_w (w_w = -(n + w_u + w_v)).
+// Float evaluation errors (|d_i| <= 1 + 4u): |det_f - det| <= E_n = 4u|n|,
+// |a_u_f - a_u| <= 8u|e2||ao|, |a_v_f - a_v| <= 8u|e1||ao|; an a_u within 2^-149|n| of 0 can
+// still round u to -0 (accepted), hence the 2^-149|n| floors.  A hit needs u+v <= 1 after
+// rounding, which implies d.w_w >= -(E_u + E_v + 1.01 E_n + 3.2u|n|).  So condition k certainly
+// fails for direction d when d.w_k < -E_k.
+// The camera's unnormalised direction is D(x', y') = (bl - C) + (vw x', 2y', 0) with bl, vw the
+// reference's float viewport corner and width (camera.rs:57-76), so D.w_k = K + A x' + B y' is
+// affine and its maximum over a pixel rectangle sits at a corner.  The reference's float
+// direction differs from D/|D| by at most 4u S (S = |bl| + vw + 2 + |C|) before and 4u after
+// normalisation, so condition k fails for every pixel of the rectangle when
+//   max_rect (K + A x' + B y') < -T_k,
+//   T_k = 2 * [ (E_k + 4u|w_k|) Dmax + 4u S |w_k| + 6u (|K| + |A| + |B|) ]
+// (Dmax = largest |D| over the frame; factor 2 = safety).  t >= 0 does not depend on d: when
+// ao.n < -2^-149 |n| (or |n|(1+8u) < 1e-6) no camera ray can hit the face and the whole
+// record rejects.  Any non-finite input disables culling for the face (T = +inf).
+__global__ void __launch_bounds__(256) tri_cull_kernel(const TriHot* __restrict__ hot, uint32_t T,
+                                                       float cx, float cy, float cz, float ratio,
+                                                       float z_dist, TriCull* __restrict__ cull) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= T) return;
+    const double u = 0x1p-24;
+    const TriHot h = hot[i];
+    const f3 e1f = mk3(h.q0.x, h.q0.y, h.q0.z), e2f = mk3(h.q0.w, h.q1.x, h.q1.y);
+    const f3 nf = mk3(h.q1.z, h.q1.w, h.q2.x), af = mk3(h.q2.y, h.q2.z, h.q2.w);
+    const f3 Cf = mk3(cx, cy, cz);
+    const f3 aof = sub(Cf, af);        // exactly the reference's `*ray.start() - a`
+    const float atf = dot0(aof, nf);   // exactly the reference's `ao.dot_product(&n)`
+    // camera.rs:57-76 in f32, as the reference computes it
+    const float vw = ratio * 2.0f;
+    const f3 bl = sub(sub(sub(Cf, divs(mk3(vw, 0.0f, 0.0f), 2.0f)), divs(mk3(0.0f, 2.0f, 0.0f), 2.0f)),
+                      mk3(0.0f, 0.0f, z_dist));
+    // doubles from here on
+    const double e1[3] = {e1f.x, e1f.y, e1f.z}, e2[3] = {e2f.x, e2f.y, e2f.z};
+    const double n[3] = {nf.x, nf.y, nf.z}, ao[3] = {aof.x, aof.y, aof.z};
+    const double blc[3] = {(double)bl.x - cx, (double)bl.y - cy, (double)bl.z - cz};
+    auto n1 = [](const double* v) { return fabs(v[0]) + fabs(v[1]) + fabs(v[2]); };
+    auto crs = [](const double* s, const double* o, double* r) {
+        r[0] = s[1] * o[2] - s[2] * o[1];
+        r[1] = s[2] * o[0] - s[0] * o[2];
+        r[2] = s[0] * o[1] - s[1] * o[0];
+    };
+    double wu[3], wv[3], ww[3], wn[3];
+    crs(e2, ao, wu);
+    crs(ao, e1, wv);
+    for (int k = 0; k < 3; ++k) {
+        ww[k] = -(n[k] + wu[k] + wv[k]);
+        wn[k] = -n[k];
+    }
+    const double nn = n1(n), ne1 = n1(e1), ne2 = n1(e2), nao = n1(ao);
+    const double floor_n = nn * 0x1p-149;
+    const double Eu = 8.0 * u * ne2 * nao + floor_n;
+    const double Ev = 8.0 * u * ne1 * nao + floor_n;
+    const double En = 4.0 * u * nn;
+    const double Ew = (8.0 * u * ne2 * nao) + (8.0 * u * ne1 * nao) + 1.01 * En + 3.2 * u * nn + floor_n;
+    // largest |D| over the frame (corners of x', y' in [0, 1]) and the magnitude scale S
+    double dmax = 0.0;
+    for (int cxr = 0; cxr < 2; ++cxr)
+        for (int cyr = 0; cyr < 2; ++cyr) {
+            double D0 = blc[0] + (double)vw * cxr, D1 = blc[1] + 2.0 * cyr, D2 = blc[2];
+            double l = sqrt(D0 * D0 + D1 * D1 + D2 * D2);
+            dmax = l > dmax ? l : dmax;
+        }
+    const double S = fabs((double)bl.x) + fabs((double)bl.y) + fabs((double)bl.z) + fabs((double)vw) + 2.0 +
+                     fabs((double)cx) + fabs((double)cy) + fabs((double)cz);
+    dmax = dmax * (1.0 + 1e-6) + 8.0 * u * S;
+    const double* W[4] = {wu, wv, ww, wn};
+    const double E[4] = {Eu, Ev, Ew, En};
+    float A[4], B[4], K[4], Tt[4];
+    bool finite = true;
+    for (int k = 0; k < 4; ++k) {
+        const double* w = W[k];
+        double Kd = blc[0] * w[0] + blc[1] * w[1] + blc[2] * w[2];
+        double Ad = (double)vw * w[0];
+        double Bd = 2.0 * w[1];
+        double thr = 2.0 * ((E[k] + 4.0 * u * n1(w)) * dmax + 4.0 * u * S * n1(w) +
+                            6.0 * u * (fabs(Kd) + fabs(Ad) + fabs(Bd)));
+        thr = thr * (1.0 + 0x1p-20) + 0x1p-126;  // round the float threshold up
+        A[k] = (float)Ad;
+        B[k] = (float)Bd;
+        K[k] = (float)Kd;
+        Tt[k] = (float)thr;
+        finite = finite && isfinite(A[k]) && isfinite(B[k]) && isfinite(K[k]) && isfinite(Tt[k]);
+    }
+    bool all_finite = finite && isfinite(atf) && isfinite(nn) && isfinite(nao) && isfinite(ne1) &&
+                      isfinite(ne2) && isfinite(dmax);
+    // t >= 0 fails for every camera ray / det >= 1e-6 is unreachable: reject the whole face
+    bool reject_all = all_finite && (((double)atf < -floor_n * 2.0) || (nn * (1.0 + 8.0 * u) < 1e-6));
+    if (!all_finite) {
+        for (int k = 0; k < 4; ++k) {
+            A[k] = B[k] = K[k] = 0.0f;
+            Tt[k] = __builtin_inff();
+        }
+    } else if (reject_all) {
+        A[3] = B[3] = K[3] = 0.0f;
+        Tt[3] = -__builtin_inff();
+    }
+    cull[i].A = make_float4(A[0], A[1], A[2], A[3]);
+    cull[i].B = make_float4(B[0], B[1], B[2], B[3]);
+    cull[i].K = make_float4(K[0], K[1], K[2], K[3]);
+    cull[i].T = make_float4(Tt[0], Tt[1], Tt[2], Tt[3]);
+}
+
+// true when condition k fails for every pixel of [xlo,xhi] x [ylo,yhi]
+__device__ __forceinline__ bool cull_one(float A, float B, float K, float T, float xlo, float xhi,
+                                         float ylo, float yhi) {
+    float ax = __builtin_fmaxf(A * xlo, A * xhi);
+    float by = __builtin_fmaxf(B * ylo, B * yhi);
+    float fmax = (K + ax) + by;
+    return fmax < -T;
+}
+__device__ __forceinline__ bool cull_rejects(const TriCull& c, float xlo, float xhi, float ylo,
+                                             float yhi) {
+    return cull_one(c.A.x, c.B.x, c.K.x, c.T.x, xlo, xhi, ylo, yhi) ||
+           cull_one(c.A.y, c.B.y, c.K.y, c.T.y, xlo, xhi, ylo, yhi) ||
+           cull_one(c.A.z, c.B.z, c.K.z, c.T.z, xlo, xhi, ylo, yhi) ||
+           cull_one(c.A.w, c.B.w, c.K.w, c.T.w, xlo, xhi, ylo, yhi);
+}
+
+// --------------------------------------------------------------------- exact test ----------
+// Triangle::intersects (primitives.rs:41-72) with e1/e2/n precomputed.  The conjunction is
+// evaluated det-first so culled lanes skip the division; the outcome is the same conjunction.
+__device__ __forceinline__ bool exact_test(const TriHot& r, f3 o, f3 d, float& u, float& v,
+                                           float& t) {
+    const f3 e1 = mk3(r.q0.x, r.q0.y, r.q0.z), e2 = mk3(r.q0.w, r.q1.x, r.q1.y);
+    const f3 n = mk3(r.q1.z, r.q1.w, r.q2.x), a = mk3(r.q2.y, r.q2.z, r.q2.w);
+    if (dot0(n, d) > 0.0f) return false;  // backface culling
+    const float det = -dot0(d, n);
+    if (!(det >= 1e-6f)) return false;
+    const float invdet = 1.0f / det;
+    const f3 ao = sub(o, a);
+    const f3 dao = cross(ao, d);
+    u = dot0(e2, dao) * invdet;
+    v = -dot0(e1, dao) * invdet;
+    t = dot0(ao, n) * invdet;
+    return t >= 0.0f && u >= 0.0f && v >= 0.0f && (u + v) <= 1.0f;
+}
+
+// BoundingBox::intersects (object.rs:327-379), general box.
+__device__ __forceinline__ bool bbox_hit(const ObjectDesc& ob, f3 s, f3 d) {
+    const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+    const bool sx = ix < 0.0f, sy = iy < 0.0f, sz = iz < 0.0f;
+    float txmin = ((sx ? ob.bb_hi[0] : ob.bb_lo[0]) - s.x) * ix;
+    float txmax = ((sx ? ob.bb_lo[0] : ob.bb_hi[0]) - s.x) * ix;
+    const float tymin = ((sy ? ob.bb_hi[1] : ob.bb_lo[1]) - s.y) * iy;
+    const float tymax = ((sy ? ob.bb_lo[1] : ob.bb_hi[1]) - s.y) * iy;
+    if ((txmin > tymax) || (tymin > txmax)) return false;
+    if (tymin > txmin) txmin = tymin;
+    if (tymax < txmax) txmax = tymax;
+    const float tzmin = ((sz ? ob.bb_hi[2] : ob.bb_lo[2]) - s.z) * iz;
+    const float tzmax = ((sz ? ob.bb_lo[2] : ob.bb_hi[2]) - s.z) * iz;
+    if (tzmin > txmin) txmin = tzmin;
+    if (tzmax < txmax) txmax = tzmax;
+    if (txmin < 0.0f) {
+        if (txmax < 0.0f) return false;
+    }
+    return true;
+}
+
+struct Bundle {  // the wave's pixel rectangle in viewport coordinates
+    float xlo, xhi, ylo, yhi;
+};
+
+// Workgroup-cooperative first-hit search over triangles [begin, begin + count).  Every thread
+// of the workgroup must call it (it contains barriers); `active` lanes search.
+template <bool kCull>
+__device__ int wg_first_hit(const FrameParams& p, uint32_t begin, uint32_t count, bool active,
+                            f3 o, f3 d, const Bundle& bd, TriHot* s_hot, TriCull* s_cull,
+                            float& hu, float& hv, float& ht) {
+    int found = -1;
+    const int lane = threadIdx.x & 63;
+    for (uint32_t base = 0; base < count; base += kTriTile) {
+        if (!__syncthreads_or(active)) break;  // also orders the LDS reuse below
+        const uint32_t n = min((uint32_t)kTriTile, count - base);
+        if (threadIdx.x < n) {
+            s_hot[threadIdx.x] = p.tris[begin + base + threadIdx.x];
+            if (kCull) s_cull[threadIdx.x] = p.cull[begin + base + threadIdx.x];
+        }
+        __syncthreads();
+        if (kCull) {
+            if (__any(active)) {
+                for (uint32_t c = 0; c < n; c += 64) {
+                    const uint32_t j = c + lane;
+                    const bool keep = j < n && !cull_rejects(s_cull[j], bd.xlo, bd.xhi, bd.ylo, bd.yhi);
+                    unsigned long long mask = __ballot(keep);
+                    while (mask) {
+                        const int bit = __ffsll(mask) - 1;
+                        mask &= mask - 1;
+                        if (active) {
+                            float u, v, t;
+                            if (exact_test(s_hot[c + bit], o, d, u, v, t)) {
+                                found = (int)(base + c + bit);
+                                hu = u;
+                                hv = v;
+                                ht = t;
+                                active = false;
+                            }
+                        }
+                        if (!__any(active)) break;
+                    }
+                    if (!__any(active)) break;
+                }
+            }
+        } else if (active) {
+            for (uint32_t j = 0; j < n; ++j) {
+                float u, v, t;
+                if (exact_test(s_hot[j], o, d, u, v, t)) {
+                    found = (int)(base + j);
+                    hu = u;
+                    hv = v;
+                    ht = t;
+                    active = false;
+                    break;
+                }
+            }
+        }
+    }
+    return found;
+}
+
+__device__ __forceinline__ bool tex_value(const TexView& tv, float x, float y, float& out) {
+    if (!tv.data) return false;
+    const uint32_t ix = sat_u32(x * (float)tv.w) % tv.w;
+    const uint32_t iy = sat_u32(y * (float)tv.h) % tv.h;
+    out = tv.data[(size_t)iy * tv.w + ix];
+    return true;
+}
+
+template <bool kCull>
+__global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
+    __shared__ TriHot s_hot[kTriTile];
+    __shared__ TriCull s_cull[kCull ? kTriTile : 1];
+
+    const uint32_t tile = blockIdx.x;
+    const uint32_t tx = tile % p.tiles_x, ty = tile / p.tiles_x;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t wx0 = tx * kTileW + (wave & 1) * 8, wy0 = ty * kTileH + (wave >> 1) * 8;
+    const uint32_t px = wx0 + (lane & 7);
+    const uint32_t py = wy0 + (lane >> 3);  // local row (0 .. rows-1)
+    const bool valid = px < p.cam_w && py < p.rows;
+    const uint32_t y = p.row0 + py;
+
+    // Camera::pixel_to_ray(x / W, y / H) (engine.rs:100-109, camera.rs:57-76)
+    const f3 C = mk3(p.cx, p.cy, p.cz);
+    const float xf = (float)px / (float)p.cam_w;
+    const float yf = (float)y / (float)p.cam_h;
+    const float vw = p.ratio * 2.0f;
+    const f3 horizontal = mk3(vw, 0.0f, 0.0f), vertical = mk3(0.0f, 2.0f, 0.0f);
+    const f3 botleft = sub(sub(sub(C, divs(horizontal, 2.0f)), divs(vertical, 2.0f)),
+                           mk3(0.0f, 0.0f, p.z_dist));
+    const f3 d = normalize(sub(add(add(botleft, mul(horizontal, xf)), mul(vertical, yf)), C));
+
+    Bundle bd;
+    {
+        const uint32_t xe = min(wx0 + 7, p.cam_w ? p.cam_w - 1 : 0);
+        const uint32_t ye = p.row0 + min(wy0 + 7, p.rows ? p.rows - 1 : 0);
+        bd.xlo = (float)wx0 / (float)p.cam_w;
+        bd.xhi = (float)xe / (float)p.cam_w;
+        bd.ylo = (float)(p.row0 + wy0) / (float)p.cam_h;
+        bd.yhi = (float)ye / (float)p.cam_h;
+    }
+
+    // ---- cast_ray (engine.rs:112-216): closest object among first hits -------------------
+    bool have = false;
+    float closest = 0.0f;
+    uint32_t best_obj = 0;
+    int best_face = -1;
+    float bu = 0.0f, bv = 0.0f, bt = 0.0f;
+    for (uint32_t oi = 0; oi < p.nobj; ++oi) {
+        const ObjectDesc& ob = p.objects[oi];
+        const bool act = valid && bbox_hit(ob, C, d);
+        float u = 0.0f, v = 0.0f, t = 0.0f;
+        const int f = wg_first_hit<kCull>(p, ob.tri_begin, ob.tri_count, act, C, d, bd, s_hot,
+                                          s_cull, u, v, t);
+        if (f >= 0) {
+            const f3 P = add(C, mul(d, t));
+            const float dsq = len_sq(sub(P, C));
+            if (!have || dsq < closest) {
+                have = true;
+                closest = dsq;
+                best_obj = oi;
+                best_face = f;
+                bu = u;
+                bv = v;
+                bt = t;
+            }
+        }
+    }
+
+    // ---- hit data and Material::get (material.rs:56-94) ----------------------------------
+    f3 P = mk3(0.0f, 0.0f, 0.0f), N = mk3(0.0f, 0.0f, 0.0f);
+    rgb color{0.0f, 0.0f, 0.0f};
+    float kd = 0.5f, ks = 0.5f, sp = 1.0f;
+    if (have) {
+        const ObjectDesc& ob = p.objects[best_obj];
+        const TriShade sh = p.shade[ob.tri_begin + (uint32_t)best_face];
+        P = add(C, mul(d, bt));
+        const f3 na = mk3(sh.s0.x, sh.s0.y, sh.s0.z), nb = mk3(sh.s0.w, sh.s1.x, sh.s1.y);
+        const f3 nc = mk3(sh.s1.z, sh.s1.w, sh.s2.x);
+        N = normalize(add(add(mul(na, bu), mul(nb, bv)), mul(nc, bt)));
+        const float w = 1.0f - bu - bv;
+        const float uv0 = ((sh.s2.y * w) + (sh.s2.w * bu)) + (sh.s3.y * bv);
+        const float uv1 = ((sh.s2.z * w) + (sh.s3.x * bu)) + (sh.s3.z * bv);
+        if (ob.mat.color.data) {
+            const TexView& tv = ob.mat.color;
+            const uint32_t ix = sat_u32(uv0 * (float)tv.w) % tv.w;
+            const uint32_t iy = sat_u32(uv1 * (float)tv.h) % tv.h;
+            const float* c = tv.data + 3 * ((size_t)iy * tv.w + ix);
+            color = rgb{c[0], c[1], c[2]};
+        }
+        tex_value(ob.mat.diffuse, uv0, uv1, kd);
+        tex_value(ob.mat.specular, uv0, uv1, ks);
+        tex_value(ob.mat.specular_power, uv0, uv1, sp);
+    }
+
+    // lighting list as a running left fold (impl Sum for Color, color.rs:82-87)
+    bool any = false;
+    rgb acc{0.0f, 0.0f, 0.0f};
+    auto push = [&](rgb c) {
+        if (any) {
+            acc = cadd(acc, c);
+        } else {
+            acc = c;
+            any = true;
+        }
+    };
+
+    for (uint32_t li = 0; li < p.nlights; ++li) {
+        const LightDesc L = p.lights[li];
+        if (L.variant == 1) continue;  // point lights first (engine.rs:274-279)
+        const f3 Lp = mk3(L.pos[0], L.pos[1], L.pos[2]);
+        // reaches_light(Ray::new(P + N * 0.1, Lp - P)) (engine.rs:280-286, 218-228)
+        const f3 S = add(P, mul(N, 0.1f));
+        const f3 sd = normalize(sub(Lp, P));
+        const float dist = len(sub(Lp, S));
+        bool reached = true, decided = false;
+        for (uint32_t oi = 0; oi < p.nobj; ++oi) {
+            const ObjectDesc& ob = p.objects[oi];
+            const bool act = have && !decided && bbox_hit(ob, S, sd);
+            float u = 0.0f, v = 0.0f, t = 0.0f;
+            const int f = wg_first_hit<false>(p, ob.tri_begin, ob.tri_count, act, S, sd, bd, s_hot,
+                                              s_cull, u, v, t);
+            if (f >= 0) {
+                const f3 hp = add(S, mul(sd, t));
+                reached = len(sub(hp, S)) > dist;
+                decided = true;
+            }
+        }
+        if (have && reached) {  // engine.rs:287-322
+            const f3 LmP = sub(Lp, P);
+            float prod = rust_clamp(dot0(N, LmP), 0.0f, 1.0f);
+            if (prod != prod) prod = 0.0f;
+            const float falloff = 1.0f / len(LmP);
+            const rgb lc{L.color[0], L.color[1], L.color[2]};
+            const rgb diffusion = cmul(cmul(cmul(cmul(cmulc(color, lc), kd), prod), L.brightness), falloff);
+            const f3 reflected = sub(d, mul(mul(N, 2.0f), dot0(d, N)));
+            const float res = rust_clamp(
+                ks * L.brightness * powf_ref(dot0(normalize(reflected), normalize(LmP)), sp), 0.0f, 1.0f);
+            const float sf = rust_clamp(powf_ref(falloff, sp), 0.0f, 1.0f);
+            const rgb specular{res * sf, res * sf, res * sf};
+            push(cadd(diffusion, specular));
+        }
+    }
+    if (have) {
+        for (uint32_t li = 0; li < p.nlights; ++li) {  // ambient lights (engine.rs:341-352)
+            const LightDesc L = p.lights[li];
+            if (L.variant != 1) continue;
+            const rgb m{rust_min(L.color[0], color.r), rust_min(L.color[1], color.g),
+                        rust_min(L.color[2], color.b)};
+            push(cmul(cmul(m, kd), L.brightness));
+        }
+    } else {
+        push(rgb{0.1f, 0.1f, 0.2f});  // engine.rs:355-357
+    }
+
+    if (valid) {
+        const size_t idx = (size_t)py * p.img_w + px;
+        if (p.out_rgb) {
+            float* o = p.out_rgb + 3 * idx;
+            o[0] = acc.r;
+            o[1] = acc.g;
+            o[2] = acc.b;
+        }
+        if (p.out_ppm) {  // Color::as_bytes, rows bottom-up (color.rs:31-37, image.rs:61-66)
+            uint8_t* o = p.out_ppm + 3 * ((size_t)(p.rows - 1 - py) * p.img_w + px);
+            o[0] = (uint8_t)sat_u8(acc.r * 255.0f);
+            o[1] = (uint8_t)sat_u8(acc.g * 255.0f);
+            o[2] = (uint8_t)sat_u8(acc.b * 255.0f);
+        }
+        if (p.out_face) p.out_face[idx] = have ? best_face : -1;
+    }
+}
+
+// Image<Color>::save_as_ppm body: byte row k = image row h-1-k.
+__global__ void __launch_bounds__(256) pack_ppm_kernel(const float* __restrict__ rgb, uint32_t w,
+                                                       uint32_t h, uint8_t* __restrict__ out) {
+    const size_t n = (size_t)w * h;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t y = (uint32_t)(i / w), x = (uint32_t)(i - (size_t)y * w);
+        const float* c = rgb + 3 * i;
+        uint8_t* o = out + 3 * ((size_t)(h - 1 - y) * w + x);
+        o[0] = (uint8_t)sat_u8(c[0] * 255.0f);
+        o[1] = (uint8_t)sat_u8(c[1] * 255.0f);
+        o[2] = (uint8_t)sat_u8(c[2] * 255.0f);
+    }
+}
+
+}  // namespace
+
+hipError_t launch_tri_precompute(const float* pos, const float* nrm, const float* uv, uint32_t T,
+                                 TriHot* hot, TriShade* shade, hipStream_t s) {
+    if (!T) return hipSuccess;
+    tri_precompute_kernel<<<(T + 255) / 256, 256, 0, s>>>(pos, nrm, uv, T, hot, shade);
+    return hipGetLastError();
+}
+
+hipError_t launch_tri_cull(const TriHot* hot, uint32_t T, float cx, float cy, float cz, float ratio,
+                           float z_dist, TriCull* cull, hipStream_t s) {
+    if (!T) return hipSuccess;
+    tri_cull_kernel<<<(T + 255) / 256, 256, 0, s>>>(hot, T, cx, cy, cz, ratio, z_dist, cull);
+    return hipGetLastError();
+}
+
+hipError_t launch_render(const FrameParams& p, hipStream_t s) {
+    const uint32_t tiles_y = (p.rows + kTileH - 1) / kTileH;
+    const uint32_t blocks = p.tiles_x * tiles_y;
+    if (!blocks) return hipSuccess;
+    if (p.cull)
+        render_kernel<true><<<blocks, kWG, 0, s>>>(p);
+    else
+        render_kernel<false><<<blocks, kWG, 0, s>>>(p);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_ppm(const float* rgb, uint32_t w, uint32_t h, uint8_t* out, hipStream_t s) {
+    const size_t n = (size_t)w * h;
+    if (!n) return hipSuccess;
+    size_t blocks = (n + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    pack_ppm_kernel<<<(unsigned)blocks, 256, 0, s>>>(rgb, w, h, out);
+    return hipGetLastError();
+}
+
+}  // namespace gpu
+}  // namespace eray

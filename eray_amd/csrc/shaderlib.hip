@@ -1,0 +1,199 @@
+// shaderlib.hip — gfx950 kernels for the four shaderlib node operators (src/shaderlib/*.rs)
+// and the fused evaluation of main.rs's material graph.
+//
+// All of them are streaming, HBM-write-bound kernels (0 reads for wave/flat, 12 B/texel of
+// reads for rgb, 24 for mix): each thread produces kVec consecutive texels so that every
+// store is a 16-B-per-lane (dwordx4) store when the row is aligned, with a scalar tail.
+// The grid is capped at 256 CUs x 8 blocks and strides over the image.
+#include "device_math.hpp"
+#include "glibc_cosf.hpp"
+#include "internal.hpp"
+
+namespace eray {
+namespace gpu {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kVec = 4;
+
+inline unsigned grid_for(size_t items) {
+    size_t blocks = (items + (size_t)kBlock * kVec - 1) / ((size_t)kBlock * kVec);
+    if (blocks > 2048) blocks = 2048;
+    return blocks ? (unsigned)blocks : 1u;
+}
+
+// wave.rs:127 — |cos((x as f32 * x_fac + y as f32 * y_fac) / 10.)|
+__device__ __forceinline__ float wave_value(uint32_t x, uint32_t y, float xf, float yf) {
+    float arg = ((float)x * xf + (float)y * yf) / 10.0f;
+    return __builtin_fabsf(libm::cosf_glibc(arg));
+}
+
+__global__ void __launch_bounds__(kBlock) wave_kernel(uint32_t w, uint32_t h, float xf, float yf,
+                                                      float* __restrict__ out) {
+    const size_t n = (size_t)w * h;
+    const size_t stride = (size_t)gridDim.x * kBlock * kVec;
+    for (size_t i0 = ((size_t)blockIdx.x * kBlock + threadIdx.x) * kVec; i0 < n; i0 += stride) {
+        float v[kVec];
+        uint32_t y = (uint32_t)(i0 / w), x = (uint32_t)(i0 - (size_t)y * w);
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            v[k] = wave_value(x, y, xf, yf);
+            if (++x == w) { x = 0; ++y; }
+        }
+        if (i0 + kVec <= n && ((reinterpret_cast<uintptr_t>(out + i0) & 15) == 0)) {
+            *reinterpret_cast<float4*>(out + i0) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+            for (int k = 0; k < kVec && i0 + k < n; ++k) out[i0 + k] = v[k];
+        }
+    }
+}
+
+__device__ __forceinline__ void store_rgb4(float* __restrict__ out, size_t i0, size_t n,
+                                           const float (&c)[kVec][3]) {
+    float* p = out + 3 * i0;
+    if (i0 + kVec <= n && ((reinterpret_cast<uintptr_t>(p) & 15) == 0)) {
+        float4* q = reinterpret_cast<float4*>(p);
+        q[0] = make_float4(c[0][0], c[0][1], c[0][2], c[1][0]);
+        q[1] = make_float4(c[1][1], c[1][2], c[2][0], c[2][1]);
+        q[2] = make_float4(c[2][2], c[3][0], c[3][1], c[3][2]);
+    } else {
+        for (int k = 0; k < kVec && i0 + k < n; ++k) {
+            p[3 * k + 0] = c[k][0];
+            p[3 * k + 1] = c[k][1];
+            p[3 * k + 2] = c[k][2];
+        }
+    }
+}
+
+// rgb.rs:89-95 — Color::new(red.pixels[i], green.pixels[i], blue.pixels[i])
+__global__ void __launch_bounds__(kBlock) rgb_kernel(size_t n, const float* __restrict__ r,
+                                                     const float* __restrict__ g,
+                                                     const float* __restrict__ b,
+                                                     float* __restrict__ out) {
+    const size_t stride = (size_t)gridDim.x * kBlock * kVec;
+    for (size_t i0 = ((size_t)blockIdx.x * kBlock + threadIdx.x) * kVec; i0 < n; i0 += stride) {
+        float c[kVec][3];
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            size_t i = i0 + k < n ? i0 + k : n - 1;
+            c[k][0] = r[i];
+            c[k][1] = g[i];
+            c[k][2] = b[i];
+        }
+        store_rgb4(out, i0, n, c);
+    }
+}
+
+// flat_color.rs:88 — Image::new(w, h, Color::new(r, g, b))
+__global__ void __launch_bounds__(kBlock) flat_kernel(size_t n, float r, float g, float b,
+                                                      float* __restrict__ out) {
+    const size_t stride = (size_t)gridDim.x * kBlock * kVec;
+    for (size_t i0 = ((size_t)blockIdx.x * kBlock + threadIdx.x) * kVec; i0 < n; i0 += stride) {
+        float c[kVec][3];
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            c[k][0] = r;
+            c[k][1] = g;
+            c[k][2] = b;
+        }
+        store_rgb4(out, i0, n, c);
+    }
+}
+
+// mix_color.rs:84-91 — interp(l, r) = l * (1. - factor) + r * factor on mod_get'd texels
+__global__ void __launch_bounds__(kBlock) mix_kernel(uint32_t w, uint32_t h, TexView left,
+                                                     TexView right, float factor,
+                                                     float* __restrict__ out) {
+    const size_t n = (size_t)w * h;
+    const float omf = 1.0f - factor;
+    const size_t stride = (size_t)gridDim.x * kBlock * kVec;
+    for (size_t i0 = ((size_t)blockIdx.x * kBlock + threadIdx.x) * kVec; i0 < n; i0 += stride) {
+        float c[kVec][3];
+        uint32_t y = (uint32_t)(i0 / w), x = (uint32_t)(i0 - (size_t)y * w);
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            uint32_t yy = y < h ? y : h - 1;
+            const float* l = left.data + 3 * (size_t)((yy % left.h) * left.w + x % left.w);
+            const float* rr = right.data + 3 * (size_t)((yy % right.h) * right.w + x % right.w);
+            c[k][0] = l[0] * omf + rr[0] * factor;
+            c[k][1] = l[1] * omf + rr[1] * factor;
+            c[k][2] = l[2] * omf + rr[2] * factor;
+            if (++x == w) { x = 0; ++y; }
+        }
+        store_rgb4(out, i0, n, c);
+    }
+}
+
+// main.rs:80-144 fused: wave -> rgb(wave, wave, wave) -> mix(.., flat(r, g, b), factor);
+// diffuse = wave.  Every node's image has the graph's width x height, so mix's mod_get is the
+// identity and the chain reduces to per-texel arithmetic in the nodes' own operation order.
+__global__ void __launch_bounds__(kBlock) material_example_kernel(
+    uint32_t w, uint32_t h, float xf, float yf, float r, float g, float b, float factor,
+    float* __restrict__ color, float* __restrict__ diffuse) {
+    const size_t n = (size_t)w * h;
+    const float omf = 1.0f - factor;
+    const size_t stride = (size_t)gridDim.x * kBlock * kVec;
+    for (size_t i0 = ((size_t)blockIdx.x * kBlock + threadIdx.x) * kVec; i0 < n; i0 += stride) {
+        float v[kVec];
+        float c[kVec][3];
+        uint32_t y = (uint32_t)(i0 / w), x = (uint32_t)(i0 - (size_t)y * w);
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            v[k] = wave_value(x, y, xf, yf);
+            c[k][0] = v[k] * omf + r * factor;
+            c[k][1] = v[k] * omf + g * factor;
+            c[k][2] = v[k] * omf + b * factor;
+            if (++x == w) { x = 0; ++y; }
+        }
+        if (color) store_rgb4(color, i0, n, c);
+        if (diffuse) {
+            if (i0 + kVec <= n && ((reinterpret_cast<uintptr_t>(diffuse + i0) & 15) == 0)) {
+                *reinterpret_cast<float4*>(diffuse + i0) = make_float4(v[0], v[1], v[2], v[3]);
+            } else {
+                for (int k = 0; k < kVec && i0 + k < n; ++k) diffuse[i0 + k] = v[k];
+            }
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_wave(uint32_t w, uint32_t h, float xf, float yf, float* out, hipStream_t s) {
+    size_t n = (size_t)w * h;
+    if (!n) return hipSuccess;
+    wave_kernel<<<grid_for(n), kBlock, 0, s>>>(w, h, xf, yf, out);
+    return hipGetLastError();
+}
+hipError_t launch_rgb(uint32_t w, uint32_t h, const float* r, const float* g, const float* b,
+                      float* out, hipStream_t s) {
+    size_t n = (size_t)w * h;
+    if (!n) return hipSuccess;
+    rgb_kernel<<<grid_for(n), kBlock, 0, s>>>(n, r, g, b, out);
+    return hipGetLastError();
+}
+hipError_t launch_flat(uint32_t w, uint32_t h, float r, float g, float b, float* out,
+                       hipStream_t s) {
+    size_t n = (size_t)w * h;
+    if (!n) return hipSuccess;
+    flat_kernel<<<grid_for(n), kBlock, 0, s>>>(n, r, g, b, out);
+    return hipGetLastError();
+}
+hipError_t launch_mix(uint32_t w, uint32_t h, TexView left, TexView right, float factor,
+                      float* out, hipStream_t s) {
+    size_t n = (size_t)w * h;
+    if (!n) return hipSuccess;
+    mix_kernel<<<grid_for(n), kBlock, 0, s>>>(w, h, left, right, factor, out);
+    return hipGetLastError();
+}
+hipError_t launch_material_example(uint32_t w, uint32_t h, float xf, float yf, float r, float g,
+                                   float b, float factor, float* color, float* diffuse,
+                                   hipStream_t s) {
+    size_t n = (size_t)w * h;
+    if (!n) return hipSuccess;
+    material_example_kernel<<<grid_for(n), kBlock, 0, s>>>(w, h, xf, yf, r, g, b, factor, color,
+                                                           diffuse);
+    return hipGetLastError();
+}
+
+}  // namespace gpu
+}  // namespace eray

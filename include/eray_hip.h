@@ -1,0 +1,202 @@
+/*
+ * eray_hip.h — the C-ABI drop-in boundary of the MI355X (gfx950) implementation of
+ * HoloTheDrunk/eray's per-pixel ray-tracing hot path.
+ *
+ * Everything here is plain C: opaque context pointer, plain pointers, sizes and status codes.
+ * It is what the reference's Rust host (Engine / Scene / Material / shader Graph) would bind
+ * with one `extern "C"` block, and what this repository's own C++ host
+ * (include/eray/*.hpp) and Python tooling (eray_amd/) call.
+ *
+ * Entry points and the reference interface each one replaces (paths relative to the
+ * reference checkout, src/...):
+ *
+ *   eray_node_wave          lib shaderlib/wave.rs:100-137        (wave::node closure)
+ *   eray_node_rgb           shaderlib/rgb.rs:64-103              (rgb::node closure)
+ *   eray_node_flat_color    shaderlib/flat_color.rs:65-95        (flat_color::node closure)
+ *   eray_node_mix_color     shaderlib/mix_color.rs:57-102        (mix_color::node closure)
+ *   eray_material_example   main.rs:80-144 + lib/material.rs:35-53 (Graph::run of main's graph,
+ *                           all four nodes fused into one pass)
+ *   eray_scene_*            lib/scene.rs:39-54 (add_object / add_light / set_camera) and
+ *                           lib/object.rs:213-230 (Object::build -> device triangle arrays)
+ *   eray_render             lib/engine.rs:46-81 (Engine::render: camera rays, first-hit
+ *                           Object::intersects object.rs:58-81, Triangle::intersects
+ *                           primitives.rs:41-72, cast_ray shading engine.rs:112-216,
+ *                           reaches_light engine.rs:218-228) fused with the PPM byte pack
+ *   eray_pack_ppm           lib/image.rs:48-74 + lib/color.rs:31-37 (save_as_ppm body bytes)
+ *   eray_ppm_header         lib/image.rs:56
+ *   eray_camera_size        lib/camera.rs:36-38
+ *
+ * Conventions
+ *   - Every function returns an eray_status (0 = OK, < 0 = error) unless stated otherwise.
+ *     The reference's Result errors and panics map onto these codes; a message is available
+ *     from eray_last_error(ctx).  No C++ exception ever crosses this boundary.
+ *   - "device" pointers are HIP device allocations (eray_device_alloc or any other allocator
+ *     on the context's device).  Work is enqueued on the context's stream and is asynchronous;
+ *     call eray_synchronize (or synchronise the stream) before reading results on the host.
+ *   - Images are row-major f32: an IValue image holds 1 float per pixel, an IColor image 3
+ *     (r, g, b), exactly like Image<f32> / Image<Color> (#[repr(C)] Color, color.rs:12-22).
+ *   - One context per GPU; a context is used from one host thread at a time.
+ */
+#ifndef ERAY_HIP_H
+#define ERAY_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ERAY_ABI_VERSION 1
+
+typedef enum eray_status {
+    ERAY_OK = 0,
+    ERAY_E_INVALID_ARGUMENT = -1,
+    ERAY_E_HIP = -2,            /* a HIP runtime call failed (message has the HIP error) */
+    ERAY_E_OUT_OF_MEMORY = -3,
+    ERAY_E_MISSING = -4,        /* shader::Error::Missing / graph::Error::Missing          */
+    ERAY_E_MISSING_MANY = -5,   /* shader::Error::MissingMany (utils.rs:15-34)             */
+    ERAY_E_INVALID_TYPE = -6,   /* shader::Error::InvalidType (shader.rs:140-178)          */
+    ERAY_E_OUT_OF_BOUNDS = -7,  /* an index the reference would panic on (image.rs:36-43,
+                                   rgb.rs:89-95, `% 0` in mod_get)                         */
+    ERAY_E_IO = -8,
+    ERAY_E_PARSE = -9,          /* Object::load_obj panics (object.rs:101-186,396-421)     */
+    ERAY_E_BUILD = -10,         /* Object::build Err (object.rs:213-218)                   */
+    ERAY_E_UNSUPPORTED = -11,   /* a reference feature this build does not offer (yet)     */
+    ERAY_E_CYCLE = -12          /* graph::Error::Cycle (graph.rs:326-338)                  */
+} eray_status;
+
+typedef struct eray_ctx eray_ctx;
+
+/* ------------------------------------------------------------------ context & memory --- */
+int eray_abi_version(void);                      /* returns ERAY_ABI_VERSION */
+int eray_ctx_create(int device, eray_ctx** out);
+int eray_ctx_destroy(eray_ctx* ctx);
+/* Last error message of ctx (or of the calling thread when ctx is NULL); never NULL. */
+const char* eray_last_error(const eray_ctx* ctx);
+/* Use an external hipStream_t (e.g. PyTorch's current stream); NULL restores the context's
+ * own stream. */
+int eray_set_stream(eray_ctx* ctx, void* hip_stream);
+void* eray_get_stream(eray_ctx* ctx);
+int eray_synchronize(eray_ctx* ctx);
+int eray_device_alloc(eray_ctx* ctx, size_t bytes, void** dev_ptr);
+int eray_device_free(eray_ctx* ctx, void* dev_ptr);
+int eray_memset(eray_ctx* ctx, void* dev_ptr, int value, size_t bytes);
+int eray_copy_to_device(eray_ctx* ctx, void* dev_dst, const void* host_src, size_t bytes);
+int eray_copy_to_host(eray_ctx* ctx, void* host_dst, const void* dev_src, size_t bytes);
+
+/* ------------------------------------------------------------------ images -------------- */
+/* A read-only view of a device image socket value.  data == NULL means "no value" (the
+ * Option is None).  For IValue images channels are implied 1, for IColor 3. */
+typedef struct eray_image {
+    const float* data;
+    uint32_t width;
+    uint32_t height;
+} eray_image;
+
+/* ------------------------------------------------------------------ shaderlib nodes ----- *
+ * Each node writes its output image into a caller-allocated device buffer of
+ * width*height pixels (the reference's node allocates `Image::new(width, height, ..)` and
+ * `out.replace`s it; ownership stays with the caller here).  `width`/`height` are the node's
+ * Value inputs already converted with Rust's saturating `as u32`.                           */
+
+/* wave.rs:123-130: out[y*w+x] = |cosf((x*x_fac + y*y_fac)/10)| (glibc cosf, bit-exact). */
+int eray_node_wave(eray_ctx* ctx, uint32_t width, uint32_t height, float x_fac, float y_fac,
+                   float* out_value);
+/* rgb.rs:89-95: out[i] = (red[i], green[i], blue[i]); each input must hold >= width*height
+ * pixels (the reference indexes the input's pixel vector with the output's index). */
+int eray_node_rgb(eray_ctx* ctx, uint32_t width, uint32_t height, eray_image red,
+                  eray_image green, eray_image blue, float* out_color);
+/* flat_color.rs:88: a width x height image filled with (r, g, b). */
+int eray_node_flat_color(eray_ctx* ctx, uint32_t width, uint32_t height, float r, float g,
+                         float b, float* out_color);
+/* mix_color.rs:85-95: out = left.mod_get(x,y)*(1-factor) + right.mod_get(x,y)*factor. */
+int eray_node_mix_color(eray_ctx* ctx, uint32_t width, uint32_t height, eray_image left,
+                        eray_image right, float factor, float* out_color);
+/* main.rs:80-144 evaluated in one pass: color = mix(rgb(w,w,w), flat(r,g,b), factor),
+ * diffuse = w with w = wave(x_fac, y_fac).  Either output may be NULL. */
+int eray_material_example(eray_ctx* ctx, uint32_t width, uint32_t height, float x_fac,
+                          float y_fac, float r, float g, float b, float factor,
+                          float* out_color, float* out_diffuse);
+
+/* ------------------------------------------------------------------ scene --------------- */
+typedef struct eray_camera {        /* camera.rs:15-31 (target/up are unused by the path) */
+    float center[3];
+    float fov[2];                   /* Fov(f32, f32); only fov[0]/fov[1] is used */
+    uint32_t width;
+    float z_dist;
+} eray_camera;
+
+typedef enum eray_light_variant {   /* light.rs:20-25 */
+    ERAY_LIGHT_POINT = 0,
+    ERAY_LIGHT_AMBIENT = 1
+} eray_light_variant;
+
+typedef struct eray_light {         /* light.rs:7-16 */
+    float position[3];              /* transform.translation() */
+    int32_t variant;                /* eray_light_variant */
+    float color[3];
+    float brightness;
+} eray_light;
+
+typedef struct eray_material {      /* Material::get's selected outputs (material.rs:56-94) */
+    eray_image color;               /* IColor output or data == NULL */
+    eray_image diffuse;             /* IValue outputs or data == NULL */
+    eray_image specular;
+    eray_image specular_power;
+    eray_image reflection;
+} eray_material;
+
+typedef struct eray_object {        /* Object<Built> (object.rs:30-52) */
+    const float* positions;         /* host, T x 9: face vertices a.xyz b.xyz c.xyz */
+    const float* normals;           /* host, T x 9: per-vertex normals of a, b, c   */
+    const float* uvs;               /* host, T x 6: per-vertex uv of a, b, c        */
+    uint32_t triangle_count;        /* T (faces in file order: first hit is by index) */
+    float bbox_min[3];              /* bounding_box x/y/z range starts (0 for load_obj meshes) */
+    float bbox_max[3];              /* ... range ends */
+    eray_material material;         /* device textures; must outlive the scene */
+} eray_object;
+
+int eray_scene_reset(eray_ctx* ctx);
+int eray_scene_set_camera(eray_ctx* ctx, const eray_camera* camera);
+int eray_scene_add_light(eray_ctx* ctx, const eray_light* light);
+/* Copies the host arrays; *object_index (optional) receives the object's position. */
+int eray_scene_add_object(eray_ctx* ctx, const eray_object* object, uint32_t* object_index);
+/* Camera::size(): (width, (width as f32 / (fov0/fov1)) as u32) */
+int eray_camera_size(const eray_camera* camera, uint32_t* width, uint32_t* height);
+
+/* ------------------------------------------------------------------ render -------------- */
+typedef struct eray_render_params {
+    uint32_t image_width;           /* the Engine's image size (Engine::new((w, h), ..))    */
+    uint32_t image_height;
+    uint32_t row0;                  /* render camera rows [row0, row0 + rows)               */
+    uint32_t rows;
+    uint32_t bounces;               /* Engine::bounces (reflection recursion depth)         */
+    uint32_t anti_aliasing;         /* Engine::anti_aliasing; only 0 is supported           */
+    float* out_rgb;                 /* device or NULL: rows x image_width x 3 f32, pixel
+                                       (x, row0 + j) at ((j * image_width) + x) * 3         */
+    uint8_t* out_ppm;               /* device or NULL: the PPM body bytes of these rows, in
+                                       file (bottom-up) order: rows x image_width x 3 bytes,
+                                       byte row k holds camera row row0 + rows - 1 - k      */
+    int32_t* out_face;              /* device or NULL: rows x image_width, the face index of
+                                       the closest object's first hit, -1 for a miss        */
+    uint32_t flags;                 /* ERAY_RENDER_* */
+} eray_render_params;
+
+#define ERAY_RENDER_DEFAULT 0u
+#define ERAY_RENDER_BRUTE_FORCE 1u  /* disable the exact per-wave triangle culling (A/B) */
+
+int eray_render(eray_ctx* ctx, const eray_render_params* params);
+
+/* ------------------------------------------------------------------ PPM ----------------- */
+/* Body bytes of Image<Color>::save_as_ppm for a width x height device image: rows bottom-up,
+ * each channel (c * 255.) as u8 (saturating, NaN -> 0). out: device, width*height*3 bytes. */
+int eray_pack_ppm(eray_ctx* ctx, const float* rgb, uint32_t width, uint32_t height,
+                  uint8_t* out);
+/* Writes "P6 {width} {height} 255\n" into buf; *len receives its length (buf may be NULL). */
+int eray_ppm_header(uint32_t width, uint32_t height, char* buf, size_t cap, size_t* len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ERAY_HIP_H */

@@ -1,0 +1,211 @@
+"""GPU parity of the render path (eray_render through the C-ABI) against the CPU oracle.
+
+Bar: bit-identical f32 RGB, identical first-hit face index per pixel, identical PPM bytes
+(the kernels use the reference's exact f32 operation order).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from eray_amd import capi, meshgen
+from eray_amd.frame import MainScene, fov_for
+from tests.helpers import assert_bit_equal, mismatch_report, random_mesh
+
+pytestmark = pytest.mark.gpu
+
+
+def gpu_render(ctx, img_w, img_h, row0=0, rows=None, flags=0, ppm=True):
+    rows = img_h - row0 if rows is None else rows
+    rgb = ctx.empty((rows, img_w, 3), np.float32)
+    face = ctx.empty((rows, img_w), np.int32)
+    ctx.memset(rgb.ptr, 0, rgb.nbytes)
+    ctx.memset(face.ptr, 0xFF, face.nbytes)
+    out_ppm = ctx.empty((rows, img_w, 3), np.uint8) if ppm else None
+    ctx.render(img_w, img_h, row0=row0, rows=rows, out_rgb=rgb.ptr, out_face=face.ptr,
+               out_ppm=out_ppm.ptr if ppm else None, flags=flags)
+    res = rgb.numpy(), face.numpy(), (out_ppm.numpy() if ppm else None)
+    for a in (rgb, face, out_ppm):
+        if a is not None:
+            a.free()
+    return res
+
+
+def oracle_main_scene(oracle, mesh, W, H, texture=1024, rows=None, row0=0):
+    s = oracle.main_rs_scene(*mesh, texture=texture)
+    cam = oracle.camera((0.0, 0.0, 5.0), fov_for(W, H), W, 1.0)
+    rgb, faces, stats = oracle.render(s, cam, row0=row0, rows=rows, want_faces=True)
+    return rgb, faces, stats
+
+
+@pytest.mark.parametrize("W,H", [(256, 256), (1920, 1080)])
+def test_cube_frame_matches_oracle(gpu, oracle, cube, W, H):
+    """C1 and C2: main.rs's scene, bit-exact frame, faces and PPM."""
+    sc = MainScene(gpu, *cube, W, H)
+    rgb, face, ppm = gpu_render(gpu, W, H)
+    sc.close()
+    ref, ref_face, stats = oracle_main_scene(oracle, cube, W, H)
+    assert_bit_equal(rgb, ref, f"cube {W}x{H} rgb")
+    assert np.array_equal(face, ref_face)
+    body = oracle.ppm_bytes(ref)
+    header = capi.ppm_header(W, H)
+    assert body[: len(header)] == header
+    assert ppm.tobytes() == body[len(header):]
+    assert int((face >= 0).sum()) == stats["hit_pixels"]
+
+
+def test_cube_centre_pixel_known_answer(gpu, cube):
+    """pixel (W/2, H/2) hits face 1 and shades to ~(0.548175, 0.311178, 0.311178),
+    bytes (139, 79, 79)."""
+    sc = MainScene(gpu, *cube, 256, 256)
+    rgb, face, ppm = gpu_render(gpu, 256, 256)
+    sc.close()
+    assert face[128, 128] == 1
+    np.testing.assert_allclose(rgb[128, 128], [0.548175, 0.311178, 0.311178], atol=2e-6)
+    assert tuple(ppm[255 - 128, 128]) == (139, 79, 79)
+
+
+def test_brute_force_and_culled_agree_on_cube(gpu, cube):
+    sc = MainScene(gpu, *cube, 1920, 1080)
+    a = gpu_render(gpu, 1920, 1080)
+    b = gpu_render(gpu, 1920, 1080, flags=capi.RENDER_BRUTE_FORCE)
+    sc.close()
+    assert_bit_equal(a[0], b[0], "culled vs brute force")
+    assert np.array_equal(a[1], b[1])
+
+
+@pytest.fixture(scope="module")
+def sphere8k():
+    v, n, t, fv, ft, fn = meshgen.displaced_sphere(8000, 7)
+    return (np.ascontiguousarray(v[fv].reshape(-1, 9)), np.ascontiguousarray(n[fn].reshape(-1, 9)),
+            np.ascontiguousarray(t[ft].reshape(-1, 6)))
+
+
+def test_displaced_sphere_matches_oracle(gpu, oracle, sphere8k):
+    """A permuted non-convex mesh: first hits spread over the whole index range."""
+    W, H = 256, 144
+    sc = MainScene(gpu, *sphere8k, W, H, texture=256)
+    rgb, face, ppm = gpu_render(gpu, W, H)
+    rgb_b, face_b, _ = gpu_render(gpu, W, H, flags=capi.RENDER_BRUTE_FORCE)
+    sc.close()
+    ref, ref_face, stats = oracle_main_scene(oracle, sphere8k, W, H, texture=256)
+    assert stats["hit_pixels"] > 1000
+    assert np.array_equal(face, ref_face)
+    assert_bit_equal(rgb, ref, "sphere8k culled")
+    assert_bit_equal(rgb_b, ref, "sphere8k brute force")
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_multi_object_scene(gpu, oracle, seed):
+    """Several objects (general bounding boxes), coloured point/ambient lights, off-axis camera,
+    random textures of different sizes: exercises closest-object selection, bbox gating and
+    shadow rays that reach the triangle scan."""
+    rng = np.random.default_rng(seed)
+    W, H = 96, 64
+    cam_center = tuple(rng.uniform(-0.7, 0.7, 3).astype(np.float32) + np.float32([0, 0, 4]))
+    s = oracle.Scene()
+    gpu.scene_reset()
+    cam = capi.make_camera(cam_center, (3.0, 2.0), W, 1.0)
+    gpu.set_camera(cam)
+    keep = []
+    for k in range(3):
+        T = int(rng.integers(5, 300))
+        pos, nrm, uv = random_mesh(rng, T, scale=float(rng.uniform(0.3, 1.2)),
+                                   center=rng.uniform(-0.8, 0.8, 3))
+        lo = pos.reshape(-1, 3).min(0) if k != 1 else np.zeros(3, np.float32)
+        hi = pos.reshape(-1, 3).max(0) if k != 1 else np.zeros(3, np.float32)
+        tw, th = int(rng.integers(1, 40)), int(rng.integers(1, 40))
+        color = rng.uniform(0, 1.2, (th, tw, 3)).astype(np.float32)
+        diffuse = rng.uniform(0, 1, (th + 1, tw + 2)).astype(np.float32) if k != 2 else None
+        spec = rng.uniform(0, 1, (5, 7)).astype(np.float32) if k == 0 else None
+        dc, dd = gpu.to_device(color), (gpu.to_device(diffuse) if diffuse is not None else None)
+        ds = gpu.to_device(spec) if spec is not None else None
+        keep += [x for x in (dc, dd, ds) if x is not None]
+        gpu.add_object(pos, nrm, uv, tuple(lo), tuple(hi), color=dc.image(),
+                       diffuse=dd.image() if dd else None, specular=ds.image() if ds else None)
+        s.add_object(pos, nrm, uv, tuple(lo), tuple(hi), color=color, diffuse=diffuse, specular=spec)
+    lights = [((0.0, 2.0, 0.0), "ambient", (0.9, 0.5, 1.0), 0.3),
+              ((1.0, 1.0, 2.0), "point", (1.0, 1.0, 1.0), 1.0),
+              ((-2.0, 0.5, 1.0), "point", (0.2, 0.9, 0.4), 0.7),
+              ((0.0, -1.0, 0.5), "ambient", (1.0, 1.0, 1.0), 0.1)]
+    for pos, var, col, b in lights:
+        gpu.add_light(capi.make_light(pos, var, col, b))
+        s.add_light(pos, var, col, b)
+    rgb, face, _ = gpu_render(gpu, W, H)
+    rgb_b, face_b, _ = gpu_render(gpu, W, H, flags=capi.RENDER_BRUTE_FORCE)
+    ocam = oracle.camera(cam_center, (3.0, 2.0), W, 1.0)
+    ref, ref_face, stats = oracle.render(s, ocam, want_faces=True)
+    for a in keep:
+        a.free()
+    assert stats["shadow_tests"] > 0
+    assert np.array_equal(face, ref_face)
+    assert_bit_equal(rgb, ref, f"random scene {seed}")
+    assert_bit_equal(rgb_b, ref, f"random scene {seed} brute")
+
+
+def test_row_tiles_equal_full_frame(gpu, cube):
+    W, H = 640, 360
+    sc = MainScene(gpu, *cube, W, H)
+    full_rgb, full_face, full_ppm = gpu_render(gpu, W, H)
+    cuts = [0, 100, 101, 250, H]
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        rgb, face, ppm = gpu_render(gpu, W, H, row0=a, rows=b - a)
+        assert_bit_equal(rgb, full_rgb[a:b], f"rows {a}:{b}")
+        assert np.array_equal(face, full_face[a:b])
+        # PPM byte rows of a tile are the file rows H-b .. H-a-1
+        assert np.array_equal(ppm, full_ppm[H - b:H - a])
+    sc.close()
+
+
+def test_engine_image_wider_than_camera(gpu, oracle, cube):
+    """Image::set indexes with the engine image's width (image.rs:41-43)."""
+    sc = MainScene(gpu, *cube, 128, 128)
+    rgb, face, _ = gpu_render(gpu, 200, 150, rows=128, ppm=False)
+    sc.close()
+    s = oracle.main_rs_scene(*cube)
+    ref, stats = oracle.render(s, oracle.camera(width=128), image_width=200, image_height=150)
+    assert_bit_equal(rgb, ref, "stride")
+
+
+def test_render_errors(gpu, cube):
+    sc = MainScene(gpu, *cube, 64, 64)
+    buf = gpu.empty((64, 64, 3), np.float32)
+    with pytest.raises(capi.ErayError) as e:
+        gpu.render(64, 64, out_rgb=buf.ptr, anti_aliasing=2)
+    assert e.value.status == capi.E_UNSUPPORTED
+    with pytest.raises(capi.ErayError) as e:
+        gpu.render(64, 64, row0=60, rows=10, out_rgb=buf.ptr)
+    assert e.value.status == capi.E_INVALID_ARGUMENT
+    with pytest.raises(capi.ErayError) as e:  # camera 64x64 does not fit a 64x32 engine image
+        gpu.render(64, 32, rows=64, out_rgb=buf.ptr)
+    assert e.value.status == capi.E_OUT_OF_BOUNDS
+    buf.free()
+    sc.close()
+
+
+def test_empty_scene_and_empty_object(gpu, oracle):
+    gpu.scene_reset()
+    gpu.set_camera(capi.make_camera((0, 0, 5), (60, 60), 32, 1.0))
+    gpu.add_light(capi.make_light((1, 1, 2), "point"))
+    rgb, face, _ = gpu_render(gpu, 32, 32)
+    assert np.all(face == -1)
+    assert np.all(rgb == np.float32([0.1, 0.1, 0.2]))
+    z = np.zeros((0, 9), np.float32)
+    gpu.add_object(z, z, np.zeros((0, 6), np.float32))
+    rgb2, face2, _ = gpu_render(gpu, 32, 32)
+    assert_bit_equal(rgb2, rgb, "empty object")
+
+
+def test_pack_ppm_matches_oracle(gpu, oracle):
+    rng = np.random.default_rng(5)
+    img = rng.uniform(-0.5, 1.5, (37, 53, 3)).astype(np.float32)
+    img[0, 0] = [np.nan, np.inf, -np.inf]
+    img[1, 1] = [1.0, 254.5 / 255.0, 0.0039215689]
+    d = gpu.to_device(img)
+    out = gpu.empty((37, 53, 3), np.uint8)
+    gpu.pack_ppm(d.ptr, 53, 37, out.ptr)
+    got = out.numpy().tobytes()
+    d.free()
+    out.free()
+    ref = oracle.ppm_bytes(img)
+    assert got == ref[len(capi.ppm_header(53, 37)):]
