@@ -250,7 +250,7 @@ const char* eray_last_error(const eray_ctx* ctx) {
 
 int eray_set_stream(eray_ctx* ctx, void* stream) {
     if (int st = use_device(ctx)) return st;
-    ctx->stream = stream ? (hipStream_t)stream : ctx->own_stream;
+    ctx->stream = (hipStream_t)stream;
     return ERAY_OK;
 }
 
@@ -426,7 +426,8 @@ int eray_camera_size(const eray_camera* c, uint32_t* w, uint32_t* h) {
 }
 
 // ------------------------------------------------------------------------ render ------------
-int eray_render(eray_ctx* ctx, const eray_render_params* rp) {
+namespace {
+int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out, bool* empty) {
     if (int st = use_device(ctx)) return st;
     if (!rp) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "params is null");
     if (rp->anti_aliasing != 0)
@@ -453,9 +454,11 @@ int eray_render(eray_ctx* ctx, const eray_render_params* rp) {
                          "fused PPM output needs camera size == image size; use eray_pack_ppm");
     const bool cull = !(rp->flags & ERAY_RENDER_BRUTE_FORCE);
     if (int st = sync_scene(ctx, cull)) return st;
-    if (!rp->rows || !W) return ERAY_OK;
+    *empty = !rp->rows || !W;
+    if (*empty) return ERAY_OK;
 
-    FrameParams p{};
+    FrameParams& p = *out;
+    p = FrameParams{};
     const eray_camera& c = ctx->camera;
     p.cx = c.center[0];
     p.cy = c.center[1];
@@ -478,9 +481,59 @@ int eray_render(eray_ctx* ctx, const eray_render_params* rp) {
     p.lights = ctx->d_lights;
     p.nobj = (uint32_t)ctx->objects.size();
     p.nlights = (uint32_t)ctx->lights.size();
-    p.tiles_x = (W + 15) / 16;
-    HIP_TRY(ctx, launch_render(p, ctx->stream));
+    p.tiles_x = (W + 63) / 64;
     return ERAY_OK;
+}
+}  // namespace
+
+int eray_render(eray_ctx* ctx, const eray_render_params* rp) {
+    FrameParams p;
+    bool empty = false;
+    if (int st = prepare_render(ctx, rp, &p, &empty)) return st;
+    if (!empty) HIP_TRY(ctx, launch_render(p, ctx->stream));
+    return ERAY_OK;
+}
+
+int eray_render_frames(eray_ctx* ctx, const eray_render_params* rp, uint32_t frames,
+                       float* mean_kernel_ms) {
+    FrameParams p;
+    bool empty = false;
+    if (int st = prepare_render(ctx, rp, &p, &empty)) return st;
+    if (mean_kernel_ms) *mean_kernel_ms = 0.0f;
+    if (empty || !frames) return ERAY_OK;
+    if (!mean_kernel_ms) {
+        for (uint32_t f = 0; f < frames; ++f) HIP_TRY(ctx, launch_render(p, ctx->stream));
+        return ERAY_OK;
+    }
+    std::vector<hipEvent_t> ev(2 * (size_t)frames, nullptr);
+    int st = ERAY_OK;
+    for (auto& e : ev) {
+        hipError_t he = hipEventCreate(&e);
+        if (he != hipSuccess) {
+            st = set_error(ctx, ERAY_E_HIP, "hipEventCreate: %s", hipGetErrorString(he));
+            break;
+        }
+    }
+    for (uint32_t f = 0; f < frames && st == ERAY_OK; ++f) {
+        hipError_t he = hipEventRecord(ev[2 * f], ctx->stream);
+        if (he == hipSuccess) he = launch_render(p, ctx->stream);
+        if (he == hipSuccess) he = hipEventRecord(ev[2 * f + 1], ctx->stream);
+        if (he != hipSuccess) st = set_error(ctx, ERAY_E_HIP, "render loop: %s", hipGetErrorString(he));
+    }
+    double total = 0.0;
+    if (st == ERAY_OK) {
+        hipError_t he = hipStreamSynchronize(ctx->stream);
+        for (uint32_t f = 0; f < frames && he == hipSuccess; ++f) {
+            float ms = 0.0f;
+            he = hipEventElapsedTime(&ms, ev[2 * f], ev[2 * f + 1]);
+            total += ms;
+        }
+        if (he != hipSuccess) st = set_error(ctx, ERAY_E_HIP, "render timing: %s", hipGetErrorString(he));
+    }
+    for (auto e : ev)
+        if (e) hipEventDestroy(e);
+    if (st == ERAY_OK) *mean_kernel_ms = (float)(total / frames);
+    return st;
 }
 
 int eray_pack_ppm(eray_ctx* ctx, const float* rgb, uint32_t w, uint32_t h, uint8_t* out) {

@@ -2,7 +2,8 @@
 //
 // Replaces Engine::render (src/lib/engine.rs:46-81) with the PPM byte pack of
 // Image::save_as_ppm (src/lib/image.rs:48-74) fused in.  One thread per pixel; a 256-thread
-// workgroup owns a 16x16 pixel tile and each 64-lane wave an 8x8 sub-tile.
+// workgroup owns a 64x4 pixel tile and each 64-lane wave a 16x4 sub-tile; the tile's f32 RGB
+// and PPM rows leave through LDS as 16-byte coalesced stores.
 //
 // First-hit search (Object::intersects, object.rs:58-81): the workgroup streams the object's
 // triangles in index order through LDS in tiles of kTriTile records; each ray keeps the FIRST
@@ -12,7 +13,7 @@
 //
 // Exact wave culling (primary rays only; disabled by ERAY_RENDER_BRUTE_FORCE).  For a camera
 // ray the reference's test quantities are linear in the (unnormalised) ray direction, and the
-// camera directions of an 8x8 pixel block span a small convex cone.  Per camera, each triangle
+// camera directions of a 16x4 pixel block span a small convex cone.  Per camera, each triangle
 // gets four affine bounds f_k(x', y') of those quantities with float-error margins T_k
 // (tri_cull_kernel, see the derivation there).  A wave evaluates them triangle-parallel —
 // lane j takes triangle j of a 64-triangle chunk — and __ballot()s the survivors; only the
@@ -33,7 +34,8 @@ namespace {
 using namespace eray::dev;
 
 constexpr int kWG = 256;
-constexpr int kTileW = 16, kTileH = 16;
+constexpr int kTileW = 64, kTileH = 4;  // workgroup pixel tile (4 waves side by side)
+constexpr int kWaveW = 16;               // each wave: a 16 x 4 pixel bundle
 constexpr int kTriTile = 256;
 
 // --------------------------------------------------------------------- triangle setup ------
@@ -301,13 +303,17 @@ template <bool kCull>
 __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
     __shared__ TriHot s_hot[kTriTile];
     __shared__ TriCull s_cull[kCull ? kTriTile : 1];
+    __shared__ float4 s_rgb[kTileH * kTileW * 3 / 4];  // the tile's f32 RGB rows, staged
+    __shared__ uint32_t s_ppm[kTileH * kTileW * 3 / 4];  // ... and its PPM byte rows
 
     const uint32_t tile = blockIdx.x;
     const uint32_t tx = tile % p.tiles_x, ty = tile / p.tiles_x;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t wx0 = tx * kTileW + (wave & 1) * 8, wy0 = ty * kTileH + (wave >> 1) * 8;
-    const uint32_t px = wx0 + (lane & 7);
-    const uint32_t py = wy0 + (lane >> 3);  // local row (0 .. rows-1)
+    const uint32_t tx0 = tx * kTileW, ty0 = ty * kTileH;
+    const uint32_t wx0 = tx0 + wave * kWaveW, wy0 = ty0;
+    const uint32_t lx = wave * kWaveW + (lane % kWaveW), ly = lane / kWaveW;  // in the tile
+    const uint32_t px = tx0 + lx;
+    const uint32_t py = ty0 + ly;  // local row (0 .. rows-1)
     const bool valid = px < p.cam_w && py < p.rows;
     const uint32_t y = p.row0 + py;
 
@@ -321,10 +327,10 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
                            mk3(0.0f, 0.0f, p.z_dist));
     const f3 d = normalize(sub(add(add(botleft, mul(horizontal, xf)), mul(vertical, yf)), C));
 
-    Bundle bd;
+    Bundle bd;  // the wave's kWaveW x kTileH pixel rectangle
     {
-        const uint32_t xe = min(wx0 + 7, p.cam_w ? p.cam_w - 1 : 0);
-        const uint32_t ye = p.row0 + min(wy0 + 7, p.rows ? p.rows - 1 : 0);
+        const uint32_t xe = min(wx0 + kWaveW - 1, p.cam_w ? p.cam_w - 1 : 0);
+        const uint32_t ye = p.row0 + min(wy0 + kTileH - 1, p.rows ? p.rows - 1 : 0);
         bd.xlo = (float)wx0 / (float)p.cam_w;
         bd.xhi = (float)xe / (float)p.cam_w;
         bd.ylo = (float)(p.row0 + wy0) / (float)p.cam_h;
@@ -397,13 +403,17 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
     };
 
     for (uint32_t li = 0; li < p.nlights; ++li) {
-        const LightDesc L = p.lights[li];
+        const LightDesc& L = p.lights[li];
         if (L.variant == 1) continue;  // point lights first (engine.rs:274-279)
         const f3 Lp = mk3(L.pos[0], L.pos[1], L.pos[2]);
         // reaches_light(Ray::new(P + N * 0.1, Lp - P)) (engine.rs:280-286, 218-228)
-        const f3 S = add(P, mul(N, 0.1f));
-        const f3 sd = normalize(sub(Lp, P));
-        const float dist = len(sub(Lp, S));
+        f3 S = mk3(0.0f, 0.0f, 0.0f), sd = mk3(0.0f, 0.0f, 1.0f);
+        float dist = 0.0f;
+        if (have) {
+            S = add(P, mul(N, 0.1f));
+            sd = normalize(sub(Lp, P));
+            dist = len(sub(Lp, S));
+        }
         bool reached = true, decided = false;
         for (uint32_t oi = 0; oi < p.nobj; ++oi) {
             const ObjectDesc& ob = p.objects[oi];
@@ -434,7 +444,7 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
     }
     if (have) {
         for (uint32_t li = 0; li < p.nlights; ++li) {  // ambient lights (engine.rs:341-352)
-            const LightDesc L = p.lights[li];
+            const LightDesc& L = p.lights[li];
             if (L.variant != 1) continue;
             const rgb m{rust_min(L.color[0], color.r), rust_min(L.color[1], color.g),
                         rust_min(L.color[2], color.b)};
@@ -444,7 +454,42 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
         push(rgb{0.1f, 0.1f, 0.2f});  // engine.rs:355-357
     }
 
-    if (valid) {
+    // ---- outputs: Image::set + Color::as_bytes rows bottom-up (image.rs:41-74) ------------
+    const uint32_t b0 = (uint32_t)sat_u8(acc.r * 255.0f), b1 = (uint32_t)sat_u8(acc.g * 255.0f),
+                   b2 = (uint32_t)sat_u8(acc.b * 255.0f);
+    if (valid && p.out_face) p.out_face[(size_t)py * p.img_w + px] = have ? best_face : -1;
+    // Full, aligned tiles leave through LDS as 16-byte row stores; edge tiles store per pixel.
+    const bool full = tx0 + kTileW <= p.cam_w && ty0 + kTileH <= p.rows && (p.img_w % 16) == 0 &&
+                      ((reinterpret_cast<uintptr_t>(p.out_rgb) | reinterpret_cast<uintptr_t>(p.out_ppm)) & 15) == 0;
+    if (full) {
+        float* srgb = reinterpret_cast<float*>(s_rgb) + 3 * (ly * kTileW + lx);
+        srgb[0] = acc.r;
+        srgb[1] = acc.g;
+        srgb[2] = acc.b;
+        uint8_t* sppm = reinterpret_cast<uint8_t*>(s_ppm) + 3 * ((kTileH - 1 - ly) * kTileW + lx);
+        sppm[0] = (uint8_t)b0;
+        sppm[1] = (uint8_t)b1;
+        sppm[2] = (uint8_t)b2;
+        __syncthreads();
+        constexpr uint32_t kRgbRow4 = kTileW * 3 / 4;  // float4 per tile row
+        const uint32_t t = threadIdx.x;
+        if (p.out_rgb) {
+            for (uint32_t i = t; i < kTileH * kRgbRow4; i += kWG) {
+                const uint32_t r = i / kRgbRow4, c = i % kRgbRow4;
+                float4* dst = reinterpret_cast<float4*>(p.out_rgb + 3 * ((size_t)(ty0 + r) * p.img_w + tx0)) + c;
+                *dst = s_rgb[i];
+            }
+        }
+        if (p.out_ppm) {
+            constexpr uint32_t kPpmRow16 = kTileW * 3 / 16;  // 16-byte words per tile row
+            for (uint32_t i = t; i < kTileH * kPpmRow16; i += kWG) {
+                const uint32_t r = i / kPpmRow16, c = i % kPpmRow16;  // r-th byte row of the tile block
+                const size_t row = (size_t)(p.rows - ty0 - kTileH + r);
+                uint4* dst = reinterpret_cast<uint4*>(p.out_ppm + 3 * (row * p.img_w + tx0)) + c;
+                *dst = reinterpret_cast<const uint4*>(s_ppm)[i];
+            }
+        }
+    } else if (valid) {
         const size_t idx = (size_t)py * p.img_w + px;
         if (p.out_rgb) {
             float* o = p.out_rgb + 3 * idx;
@@ -452,13 +497,12 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
             o[1] = acc.g;
             o[2] = acc.b;
         }
-        if (p.out_ppm) {  // Color::as_bytes, rows bottom-up (color.rs:31-37, image.rs:61-66)
+        if (p.out_ppm) {
             uint8_t* o = p.out_ppm + 3 * ((size_t)(p.rows - 1 - py) * p.img_w + px);
-            o[0] = (uint8_t)sat_u8(acc.r * 255.0f);
-            o[1] = (uint8_t)sat_u8(acc.g * 255.0f);
-            o[2] = (uint8_t)sat_u8(acc.b * 255.0f);
+            o[0] = (uint8_t)b0;
+            o[1] = (uint8_t)b1;
+            o[2] = (uint8_t)b2;
         }
-        if (p.out_face) p.out_face[idx] = have ? best_face : -1;
     }
 }
 

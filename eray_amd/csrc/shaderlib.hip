@@ -16,6 +16,12 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kVec = 4;
 
+inline unsigned grid_for1(size_t items) {
+    size_t blocks = (items + kBlock - 1) / kBlock;
+    if (blocks > 8192) blocks = 8192;
+    return blocks ? (unsigned)blocks : 1u;
+}
+
 inline unsigned grid_for(size_t items) {
     size_t blocks = (items + (size_t)kBlock * kVec - 1) / ((size_t)kBlock * kVec);
     if (blocks > 2048) blocks = 2048;
@@ -28,23 +34,15 @@ __device__ __forceinline__ float wave_value(uint32_t x, uint32_t y, float xf, fl
     return __builtin_fabsf(libm::cosf_glibc(arg));
 }
 
+// One texel per thread: the restated cosf is a chain of dependent double-precision steps, so
+// latency is hidden by occupancy rather than by per-thread ILP; stores stay 256 B per wave.
 __global__ void __launch_bounds__(kBlock) wave_kernel(uint32_t w, uint32_t h, float xf, float yf,
                                                       float* __restrict__ out) {
     const size_t n = (size_t)w * h;
-    const size_t stride = (size_t)gridDim.x * kBlock * kVec;
-    for (size_t i0 = ((size_t)blockIdx.x * kBlock + threadIdx.x) * kVec; i0 < n; i0 += stride) {
-        float v[kVec];
-        uint32_t y = (uint32_t)(i0 / w), x = (uint32_t)(i0 - (size_t)y * w);
-#pragma unroll
-        for (int k = 0; k < kVec; ++k) {
-            v[k] = wave_value(x, y, xf, yf);
-            if (++x == w) { x = 0; ++y; }
-        }
-        if (i0 + kVec <= n && ((reinterpret_cast<uintptr_t>(out + i0) & 15) == 0)) {
-            *reinterpret_cast<float4*>(out + i0) = make_float4(v[0], v[1], v[2], v[3]);
-        } else {
-            for (int k = 0; k < kVec && i0 + k < n; ++k) out[i0 + k] = v[k];
-        }
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        const uint32_t y = (uint32_t)(i / w), x = (uint32_t)(i - (size_t)y * w);
+        out[i] = wave_value(x, y, xf, yf);
     }
 }
 
@@ -132,27 +130,17 @@ __global__ void __launch_bounds__(kBlock) material_example_kernel(
     float* __restrict__ color, float* __restrict__ diffuse) {
     const size_t n = (size_t)w * h;
     const float omf = 1.0f - factor;
-    const size_t stride = (size_t)gridDim.x * kBlock * kVec;
-    for (size_t i0 = ((size_t)blockIdx.x * kBlock + threadIdx.x) * kVec; i0 < n; i0 += stride) {
-        float v[kVec];
-        float c[kVec][3];
-        uint32_t y = (uint32_t)(i0 / w), x = (uint32_t)(i0 - (size_t)y * w);
-#pragma unroll
-        for (int k = 0; k < kVec; ++k) {
-            v[k] = wave_value(x, y, xf, yf);
-            c[k][0] = v[k] * omf + r * factor;
-            c[k][1] = v[k] * omf + g * factor;
-            c[k][2] = v[k] * omf + b * factor;
-            if (++x == w) { x = 0; ++y; }
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        const uint32_t y = (uint32_t)(i / w), x = (uint32_t)(i - (size_t)y * w);
+        const float v = wave_value(x, y, xf, yf);
+        if (color) {
+            float* c = color + 3 * i;
+            c[0] = v * omf + r * factor;
+            c[1] = v * omf + g * factor;
+            c[2] = v * omf + b * factor;
         }
-        if (color) store_rgb4(color, i0, n, c);
-        if (diffuse) {
-            if (i0 + kVec <= n && ((reinterpret_cast<uintptr_t>(diffuse + i0) & 15) == 0)) {
-                *reinterpret_cast<float4*>(diffuse + i0) = make_float4(v[0], v[1], v[2], v[3]);
-            } else {
-                for (int k = 0; k < kVec && i0 + k < n; ++k) diffuse[i0 + k] = v[k];
-            }
-        }
+        if (diffuse) diffuse[i] = v;
     }
 }
 
@@ -161,7 +149,7 @@ __global__ void __launch_bounds__(kBlock) material_example_kernel(
 hipError_t launch_wave(uint32_t w, uint32_t h, float xf, float yf, float* out, hipStream_t s) {
     size_t n = (size_t)w * h;
     if (!n) return hipSuccess;
-    wave_kernel<<<grid_for(n), kBlock, 0, s>>>(w, h, xf, yf, out);
+    wave_kernel<<<grid_for1(n), kBlock, 0, s>>>(w, h, xf, yf, out);
     return hipGetLastError();
 }
 hipError_t launch_rgb(uint32_t w, uint32_t h, const float* r, const float* g, const float* b,
@@ -190,7 +178,7 @@ hipError_t launch_material_example(uint32_t w, uint32_t h, float xf, float yf, f
                                    hipStream_t s) {
     size_t n = (size_t)w * h;
     if (!n) return hipSuccess;
-    material_example_kernel<<<grid_for(n), kBlock, 0, s>>>(w, h, xf, yf, r, g, b, factor, color,
+    material_example_kernel<<<grid_for1(n), kBlock, 0, s>>>(w, h, xf, yf, r, g, b, factor, color,
                                                            diffuse);
     return hipGetLastError();
 }

@@ -74,8 +74,8 @@ int eray_ctx_create(int device, eray_ctx** out);
 int eray_ctx_destroy(eray_ctx* ctx);
 /* Last error message of ctx (or of the calling thread when ctx is NULL); never NULL. */
 const char* eray_last_error(const eray_ctx* ctx);
-/* Use an external hipStream_t (e.g. PyTorch's current stream); NULL restores the context's
- * own stream. */
+/* Enqueue all further work on `hip_stream` (e.g. PyTorch's current stream).  NULL selects
+ * HIP's null (default) stream; a new context starts on a stream of its own. */
 int eray_set_stream(eray_ctx* ctx, void* hip_stream);
 void* eray_get_stream(eray_ctx* ctx);
 int eray_synchronize(eray_ctx* ctx);
@@ -187,6 +187,12 @@ typedef struct eray_render_params {
 #define ERAY_RENDER_BRUTE_FORCE 1u  /* disable the exact per-wave triangle culling (A/B) */
 
 int eray_render(eray_ctx* ctx, const eray_render_params* params);
+/* Renders `frames` frames back to back with the same parameters (a serving / animation loop
+ * without a host round trip per frame).  When mean_kernel_ms is not NULL, HIP events are
+ * recorded around every launch and the mean render-kernel duration is returned (this call then
+ * synchronises the stream). */
+int eray_render_frames(eray_ctx* ctx, const eray_render_params* params, uint32_t frames,
+                       float* mean_kernel_ms);
 
 /* ------------------------------------------------------------------ PPM ----------------- */
 /* Body bytes of Image<Color>::save_as_ppm for a width x height device image: rows bottom-up,
