@@ -234,58 +234,95 @@ struct Bundle {  // the wave's pixel rectangle in viewport coordinates
     float xlo, xhi, ylo, yhi;
 };
 
-// Workgroup-cooperative first-hit search over triangles [begin, begin + count).  Every thread
-// of the workgroup must call it (it contains barriers); `active` lanes search.
-template <bool kCull>
-__device__ int wg_first_hit(const FrameParams& p, uint32_t begin, uint32_t count, bool active,
-                            f3 o, f3 d, const Bundle& bd, TriHot* s_hot, TriCull* s_cull,
-                            float& hu, float& hv, float& ht) {
+// Per-lane search state: kUndecided (ray and bounding-box test not evaluated yet), kSearching,
+// kDone (hit found, bbox rejected, or not a pixel of the image).
+constexpr int kUndecided = 0, kSearching = 1, kDone = 2;
+
+// Objects with at most this many triangles are searched by each wave on its own (records read
+// straight from global memory / the scalar cache, no LDS, no barrier); larger ones go through
+// workgroup-shared LDS tiles.
+constexpr uint32_t kDirectMax = 256;
+
+// First-hit search over triangles [begin, begin + count) (Object::intersects' face loop,
+// object.rs:63-78).  `st` is the lane's search state; lanes still kUndecided when the wave
+// meets its first candidate triangle call activate(), which must generate the ray (writing
+// `d`) and return the bounding-box verdict (object.rs:59-61).  Returns the face index relative
+// to `begin`, or -1.  kLds: every thread of the workgroup must call it (barriers).
+template <bool kCull, bool kLds, typename Activate>
+__device__ int first_hit(const FrameParams& p, uint32_t begin, uint32_t count, int st, f3 o,
+                         const f3& d, const Bundle& bd, TriHot* s_hot, TriCull* s_cull,
+                         Activate&& activate, float& hu, float& hv, float& ht) {
     int found = -1;
-    const int lane = threadIdx.x & 63;
+    const uint32_t lane = threadIdx.x & 63;
+    auto test = [&](const TriHot& h, uint32_t idx) {
+        if (st == kSearching) {
+            float u, v, t;
+            if (exact_test(h, o, d, u, v, t)) {
+                found = (int)idx;
+                hu = u;
+                hv = v;
+                ht = t;
+                st = kDone;
+            }
+        }
+    };
+    // returns false when no lane of the wave can hit anything in this object any more
+    auto resolve = [&]() -> bool {
+        if (__any(st == kUndecided)) {
+            const bool a = activate();
+            if (st == kUndecided) st = a ? kSearching : kDone;
+        }
+        return __any(st == kSearching);
+    };
+    if (!kLds) {
+        for (uint32_t base = 0; base < count; base += 64) {
+            if (!__any(st != kDone)) break;
+            unsigned long long mask;
+            if (kCull) {
+                const uint32_t j = base + lane;
+                mask = __ballot(j < count && !cull_rejects(p.cull[begin + j], bd.xlo, bd.xhi, bd.ylo, bd.yhi));
+            } else {
+                const uint32_t n = min(64u, count - base);
+                mask = n == 64 ? ~0ull : ((1ull << n) - 1ull);
+            }
+            if (!mask) continue;
+            if (!resolve()) break;
+            while (mask) {
+                const uint32_t bit = (uint32_t)(__ffsll(mask) - 1);
+                mask &= mask - 1;
+                test(p.tris[begin + base + bit], base + bit);
+                if (!__any(st == kSearching)) return found;
+            }
+        }
+        return found;
+    }
     for (uint32_t base = 0; base < count; base += kTriTile) {
-        if (!__syncthreads_or(active)) break;  // also orders the LDS reuse below
+        if (!__syncthreads_or(st != kDone)) break;  // also orders the LDS reuse below
         const uint32_t n = min((uint32_t)kTriTile, count - base);
         if (threadIdx.x < n) {
             s_hot[threadIdx.x] = p.tris[begin + base + threadIdx.x];
             if (kCull) s_cull[threadIdx.x] = p.cull[begin + base + threadIdx.x];
         }
         __syncthreads();
-        if (kCull) {
-            if (__any(active)) {
-                for (uint32_t c = 0; c < n; c += 64) {
-                    const uint32_t j = c + lane;
-                    const bool keep = j < n && !cull_rejects(s_cull[j], bd.xlo, bd.xhi, bd.ylo, bd.yhi);
-                    unsigned long long mask = __ballot(keep);
-                    while (mask) {
-                        const int bit = __ffsll(mask) - 1;
-                        mask &= mask - 1;
-                        if (active) {
-                            float u, v, t;
-                            if (exact_test(s_hot[c + bit], o, d, u, v, t)) {
-                                found = (int)(base + c + bit);
-                                hu = u;
-                                hv = v;
-                                ht = t;
-                                active = false;
-                            }
-                        }
-                        if (!__any(active)) break;
-                    }
-                    if (!__any(active)) break;
-                }
+        if (!__any(st != kDone)) continue;
+        for (uint32_t c = 0; c < n; c += 64) {
+            unsigned long long mask;
+            if (kCull) {
+                const uint32_t j = c + lane;
+                mask = __ballot(j < n && !cull_rejects(s_cull[j], bd.xlo, bd.xhi, bd.ylo, bd.yhi));
+            } else {
+                const uint32_t m = min(64u, n - c);
+                mask = m == 64 ? ~0ull : ((1ull << m) - 1ull);
             }
-        } else if (active) {
-            for (uint32_t j = 0; j < n; ++j) {
-                float u, v, t;
-                if (exact_test(s_hot[j], o, d, u, v, t)) {
-                    found = (int)(base + j);
-                    hu = u;
-                    hv = v;
-                    ht = t;
-                    active = false;
-                    break;
-                }
+            if (!mask) continue;
+            if (!resolve()) break;
+            while (mask) {
+                const uint32_t bit = (uint32_t)(__ffsll(mask) - 1);
+                mask &= mask - 1;
+                test(s_hot[c + bit], base + c + bit);
+                if (!__any(st == kSearching)) break;
             }
+            if (!__any(st == kSearching)) break;
         }
     }
     return found;
@@ -297,6 +334,18 @@ __device__ __forceinline__ bool tex_value(const TexView& tv, float x, float y, f
     const uint32_t iy = sat_u32(y * (float)tv.h) % tv.h;
     out = tv.data[(size_t)iy * tv.w + ix];
     return true;
+}
+
+// Camera::pixel_to_ray(x / W, y / H).dir (engine.rs:100-109, camera.rs:57-76, Ray::new)
+__device__ __forceinline__ f3 camera_dir(const FrameParams& p, uint32_t px, uint32_t y) {
+    const f3 C = mk3(p.cx, p.cy, p.cz);
+    const float xf = (float)px / (float)p.cam_w;
+    const float yf = (float)y / (float)p.cam_h;
+    const float vw = p.ratio * 2.0f;
+    const f3 horizontal = mk3(vw, 0.0f, 0.0f), vertical = mk3(0.0f, 2.0f, 0.0f);
+    const f3 botleft = sub(sub(sub(C, divs(horizontal, 2.0f)), divs(vertical, 2.0f)),
+                           mk3(0.0f, 0.0f, p.z_dist));
+    return normalize(sub(add(add(botleft, mul(horizontal, xf)), mul(vertical, yf)), C));
 }
 
 template <bool kCull>
@@ -316,16 +365,7 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
     const uint32_t py = ty0 + ly;  // local row (0 .. rows-1)
     const bool valid = px < p.cam_w && py < p.rows;
     const uint32_t y = p.row0 + py;
-
-    // Camera::pixel_to_ray(x / W, y / H) (engine.rs:100-109, camera.rs:57-76)
     const f3 C = mk3(p.cx, p.cy, p.cz);
-    const float xf = (float)px / (float)p.cam_w;
-    const float yf = (float)y / (float)p.cam_h;
-    const float vw = p.ratio * 2.0f;
-    const f3 horizontal = mk3(vw, 0.0f, 0.0f), vertical = mk3(0.0f, 2.0f, 0.0f);
-    const f3 botleft = sub(sub(sub(C, divs(horizontal, 2.0f)), divs(vertical, 2.0f)),
-                           mk3(0.0f, 0.0f, p.z_dist));
-    const f3 d = normalize(sub(add(add(botleft, mul(horizontal, xf)), mul(vertical, yf)), C));
 
     Bundle bd;  // the wave's kWaveW x kTileH pixel rectangle
     {
@@ -337,6 +377,11 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
         bd.yhi = (float)ye / (float)p.cam_h;
     }
 
+    // The camera ray is generated lazily: a wave whose pixel block meets no candidate triangle
+    // of any object (most of the frame) never needs it — its pixels are background.
+    f3 d = mk3(0.0f, 0.0f, 0.0f);
+    bool ray_ready = false;
+
     // ---- cast_ray (engine.rs:112-216): closest object among first hits -------------------
     bool have = false;
     float closest = 0.0f;
@@ -345,10 +390,20 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
     float bu = 0.0f, bv = 0.0f, bt = 0.0f;
     for (uint32_t oi = 0; oi < p.nobj; ++oi) {
         const ObjectDesc& ob = p.objects[oi];
-        const bool act = valid && bbox_hit(ob, C, d);
+        auto activate = [&]() -> bool {
+            if (!ray_ready) {
+                d = camera_dir(p, px, y);
+                ray_ready = true;
+            }
+            return bbox_hit(ob, C, d);
+        };
+        const int st0 = valid ? kUndecided : kDone;
         float u = 0.0f, v = 0.0f, t = 0.0f;
-        const int f = wg_first_hit<kCull>(p, ob.tri_begin, ob.tri_count, act, C, d, bd, s_hot,
-                                          s_cull, u, v, t);
+        const int f = ob.tri_count <= kDirectMax
+                          ? first_hit<kCull, false>(p, ob.tri_begin, ob.tri_count, st0, C, d, bd, s_hot,
+                                                    s_cull, activate, u, v, t)
+                          : first_hit<kCull, true>(p, ob.tri_begin, ob.tri_count, st0, C, d, bd, s_hot,
+                                                   s_cull, activate, u, v, t);
         if (f >= 0) {
             const f3 P = add(C, mul(d, t));
             const float dsq = len_sq(sub(P, C));
@@ -417,10 +472,14 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
         bool reached = true, decided = false;
         for (uint32_t oi = 0; oi < p.nobj; ++oi) {
             const ObjectDesc& ob = p.objects[oi];
-            const bool act = have && !decided && bbox_hit(ob, S, sd);
+            const int st0 = (have && !decided && bbox_hit(ob, S, sd)) ? kSearching : kDone;
+            auto never = []() -> bool { return false; };
             float u = 0.0f, v = 0.0f, t = 0.0f;
-            const int f = wg_first_hit<false>(p, ob.tri_begin, ob.tri_count, act, S, sd, bd, s_hot,
-                                              s_cull, u, v, t);
+            const int f = ob.tri_count <= kDirectMax
+                              ? first_hit<false, false>(p, ob.tri_begin, ob.tri_count, st0, S, sd, bd, s_hot,
+                                                        s_cull, never, u, v, t)
+                              : first_hit<false, true>(p, ob.tri_begin, ob.tri_count, st0, S, sd, bd, s_hot,
+                                                       s_cull, never, u, v, t);
             if (f >= 0) {
                 const f3 hp = add(S, mul(sd, t));
                 reached = len(sub(hp, S)) > dist;
