@@ -481,6 +481,8 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     p.lights = ctx->d_lights;
     p.nobj = (uint32_t)ctx->objects.size();
     p.nlights = (uint32_t)ctx->lights.size();
+    p.max_object_tris = 0;
+    for (auto& o : ctx->objects) p.max_object_tris = o.T > p.max_object_tris ? o.T : p.max_object_tris;
     p.tiles_x = (W + 63) / 64;
     return ERAY_OK;
 }

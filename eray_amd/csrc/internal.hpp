@@ -78,6 +78,7 @@ struct FrameParams {
     const ObjectDesc* objects;
     const LightDesc* lights;
     uint32_t nobj, nlights;
+    uint32_t max_object_tris;  // selects the kernel variant with LDS triangle tiles
     uint32_t tiles_x;  // pixel tiles per row
 };
 

@@ -348,11 +348,13 @@ __device__ __forceinline__ f3 camera_dir(const FrameParams& p, uint32_t px, uint
     return normalize(sub(add(add(botleft, mul(horizontal, xf)), mul(vertical, yf)), C));
 }
 
-template <bool kCull>
+// kLdsTiles: some object has more than kDirectMax triangles (workgroup LDS tiles needed);
+// without it the kernel has no barrier at all and waves retire independently.
+template <bool kCull, bool kLdsTiles>
 __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
-    __shared__ TriHot s_hot[kTriTile];
-    __shared__ TriCull s_cull[kCull ? kTriTile : 1];
-    __shared__ float4 s_rgb[kTileH * kTileW * 3 / 4];  // the tile's f32 RGB rows, staged
+    __shared__ TriHot s_hot[kLdsTiles ? kTriTile : 1];
+    __shared__ TriCull s_cull[(kCull && kLdsTiles) ? kTriTile : 1];
+    __shared__ float4 s_rgb[kTileH * kTileW * 3 / 4];  // each wave's f32 RGB rows, staged
     __shared__ uint32_t s_ppm[kTileH * kTileW * 3 / 4];  // ... and its PPM byte rows
 
     const uint32_t tile = blockIdx.x;
@@ -389,7 +391,7 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
     int best_face = -1;
     float bu = 0.0f, bv = 0.0f, bt = 0.0f;
     for (uint32_t oi = 0; oi < p.nobj; ++oi) {
-        const ObjectDesc& ob = p.objects[oi];
+        const ObjectDesc ob = p.objects[oi];  // uniform: scalar loads
         auto activate = [&]() -> bool {
             if (!ray_ready) {
                 d = camera_dir(p, px, y);
@@ -399,11 +401,11 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
         };
         const int st0 = valid ? kUndecided : kDone;
         float u = 0.0f, v = 0.0f, t = 0.0f;
-        const int f = ob.tri_count <= kDirectMax
+        const int f = (!kLdsTiles || ob.tri_count <= kDirectMax)
                           ? first_hit<kCull, false>(p, ob.tri_begin, ob.tri_count, st0, C, d, bd, s_hot,
                                                     s_cull, activate, u, v, t)
-                          : first_hit<kCull, true>(p, ob.tri_begin, ob.tri_count, st0, C, d, bd, s_hot,
-                                                   s_cull, activate, u, v, t);
+                          : first_hit<kCull, kLdsTiles>(p, ob.tri_begin, ob.tri_count, st0, C, d, bd, s_hot,
+                                                        s_cull, activate, u, v, t);
         if (f >= 0) {
             const f3 P = add(C, mul(d, t));
             const float dsq = len_sq(sub(P, C));
@@ -458,7 +460,7 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
     };
 
     for (uint32_t li = 0; li < p.nlights; ++li) {
-        const LightDesc& L = p.lights[li];
+        const LightDesc L = p.lights[li];  // uniform: scalar loads
         if (L.variant == 1) continue;  // point lights first (engine.rs:274-279)
         const f3 Lp = mk3(L.pos[0], L.pos[1], L.pos[2]);
         // reaches_light(Ray::new(P + N * 0.1, Lp - P)) (engine.rs:280-286, 218-228)
@@ -471,15 +473,15 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
         }
         bool reached = true, decided = false;
         for (uint32_t oi = 0; oi < p.nobj; ++oi) {
-            const ObjectDesc& ob = p.objects[oi];
+            const ObjectDesc ob = p.objects[oi];
             const int st0 = (have && !decided && bbox_hit(ob, S, sd)) ? kSearching : kDone;
             auto never = []() -> bool { return false; };
             float u = 0.0f, v = 0.0f, t = 0.0f;
-            const int f = ob.tri_count <= kDirectMax
+            const int f = (!kLdsTiles || ob.tri_count <= kDirectMax)
                               ? first_hit<false, false>(p, ob.tri_begin, ob.tri_count, st0, S, sd, bd, s_hot,
                                                         s_cull, never, u, v, t)
-                              : first_hit<false, true>(p, ob.tri_begin, ob.tri_count, st0, S, sd, bd, s_hot,
-                                                       s_cull, never, u, v, t);
+                              : first_hit<false, kLdsTiles>(p, ob.tri_begin, ob.tri_count, st0, S, sd, bd,
+                                                            s_hot, s_cull, never, u, v, t);
             if (f >= 0) {
                 const f3 hp = add(S, mul(sd, t));
                 reached = len(sub(hp, S)) > dist;
@@ -503,7 +505,7 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
     }
     if (have) {
         for (uint32_t li = 0; li < p.nlights; ++li) {  // ambient lights (engine.rs:341-352)
-            const LightDesc& L = p.lights[li];
+            const LightDesc L = p.lights[li];
             if (L.variant != 1) continue;
             const rgb m{rust_min(L.color[0], color.r), rust_min(L.color[1], color.g),
                         rust_min(L.color[2], color.b)};
@@ -517,36 +519,38 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
     const uint32_t b0 = (uint32_t)sat_u8(acc.r * 255.0f), b1 = (uint32_t)sat_u8(acc.g * 255.0f),
                    b2 = (uint32_t)sat_u8(acc.b * 255.0f);
     if (valid && p.out_face) p.out_face[(size_t)py * p.img_w + px] = have ? best_face : -1;
-    // Full, aligned tiles leave through LDS as 16-byte row stores; edge tiles store per pixel.
-    const bool full = tx0 + kTileW <= p.cam_w && ty0 + kTileH <= p.rows && (p.img_w % 16) == 0 &&
+    // Full, aligned wave blocks leave through the wave's own LDS slice as 16-byte row stores
+    // (no workgroup barrier); edge blocks store per pixel.
+    const bool full = wx0 + kWaveW <= p.cam_w && ty0 + kTileH <= p.rows && (p.img_w % 16) == 0 &&
                       ((reinterpret_cast<uintptr_t>(p.out_rgb) | reinterpret_cast<uintptr_t>(p.out_ppm)) & 15) == 0;
     if (full) {
-        float* srgb = reinterpret_cast<float*>(s_rgb) + 3 * (ly * kTileW + lx);
+        constexpr uint32_t kWavePix = kWaveW * kTileH;
+        float* wrgb = reinterpret_cast<float*>(s_rgb) + 3 * kWavePix * wave;
+        uint8_t* wppm = reinterpret_cast<uint8_t*>(s_ppm) + 3 * kWavePix * wave;
+        const uint32_t wl = lane % kWaveW;
+        float* srgb = wrgb + 3 * (ly * kWaveW + wl);
         srgb[0] = acc.r;
         srgb[1] = acc.g;
         srgb[2] = acc.b;
-        uint8_t* sppm = reinterpret_cast<uint8_t*>(s_ppm) + 3 * ((kTileH - 1 - ly) * kTileW + lx);
+        uint8_t* sppm = wppm + 3 * ((kTileH - 1 - ly) * kWaveW + wl);
         sppm[0] = (uint8_t)b0;
         sppm[1] = (uint8_t)b1;
         sppm[2] = (uint8_t)b2;
-        __syncthreads();
-        constexpr uint32_t kRgbRow4 = kTileW * 3 / 4;  // float4 per tile row
-        const uint32_t t = threadIdx.x;
-        if (p.out_rgb) {
-            for (uint32_t i = t; i < kTileH * kRgbRow4; i += kWG) {
-                const uint32_t r = i / kRgbRow4, c = i % kRgbRow4;
-                float4* dst = reinterpret_cast<float4*>(p.out_rgb + 3 * ((size_t)(ty0 + r) * p.img_w + tx0)) + c;
-                *dst = s_rgb[i];
-            }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        constexpr uint32_t kRgbRow4 = kWaveW * 3 / 4;   // float4 per wave row (12)
+        constexpr uint32_t kPpmRow16 = kWaveW * 3 / 16; // 16-byte words per wave row (3)
+        if (p.out_rgb && lane < kTileH * kRgbRow4) {
+            const uint32_t r = lane / kRgbRow4, c = lane % kRgbRow4;
+            float4* dst = reinterpret_cast<float4*>(p.out_rgb + 3 * ((size_t)(ty0 + r) * p.img_w + wx0)) + c;
+            *dst = reinterpret_cast<const float4*>(wrgb)[lane];
         }
-        if (p.out_ppm) {
-            constexpr uint32_t kPpmRow16 = kTileW * 3 / 16;  // 16-byte words per tile row
-            for (uint32_t i = t; i < kTileH * kPpmRow16; i += kWG) {
-                const uint32_t r = i / kPpmRow16, c = i % kPpmRow16;  // r-th byte row of the tile block
-                const size_t row = (size_t)(p.rows - ty0 - kTileH + r);
-                uint4* dst = reinterpret_cast<uint4*>(p.out_ppm + 3 * (row * p.img_w + tx0)) + c;
-                *dst = reinterpret_cast<const uint4*>(s_ppm)[i];
-            }
+        if (p.out_ppm && lane < kTileH * kPpmRow16) {
+            const uint32_t r = lane / kPpmRow16, c = lane % kPpmRow16;  // r-th byte row of the block
+            const size_t row = (size_t)(p.rows - ty0 - kTileH + r);
+            uint4* dst = reinterpret_cast<uint4*>(p.out_ppm + 3 * (row * p.img_w + wx0)) + c;
+            *dst = reinterpret_cast<const uint4*>(wppm)[lane];
         }
     } else if (valid) {
         const size_t idx = (size_t)py * p.img_w + px;
@@ -600,10 +604,18 @@ hipError_t launch_render(const FrameParams& p, hipStream_t s) {
     const uint32_t tiles_y = (p.rows + kTileH - 1) / kTileH;
     const uint32_t blocks = p.tiles_x * tiles_y;
     if (!blocks) return hipSuccess;
-    if (p.cull)
-        render_kernel<true><<<blocks, kWG, 0, s>>>(p);
-    else
-        render_kernel<false><<<blocks, kWG, 0, s>>>(p);
+    const bool lds = p.max_object_tris > kDirectMax;
+    if (p.cull) {
+        if (lds)
+            render_kernel<true, true><<<blocks, kWG, 0, s>>>(p);
+        else
+            render_kernel<true, false><<<blocks, kWG, 0, s>>>(p);
+    } else {
+        if (lds)
+            render_kernel<false, true><<<blocks, kWG, 0, s>>>(p);
+        else
+            render_kernel<false, false><<<blocks, kWG, 0, s>>>(p);
+    }
     return hipGetLastError();
 }
 
