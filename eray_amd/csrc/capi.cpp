@@ -481,6 +481,8 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     p.lights = ctx->d_lights;
     p.nobj = (uint32_t)ctx->objects.size();
     p.nlights = (uint32_t)ctx->lights.size();
+    for (size_t i = 0; i < ctx->h_objs.size() && i < (size_t)kInlineObjects; ++i) p.obj_inline[i] = ctx->h_objs[i];
+    for (size_t i = 0; i < ctx->h_lights.size() && i < (size_t)kInlineLights; ++i) p.light_inline[i] = ctx->h_lights[i];
     p.max_object_tris = 0;
     for (auto& o : ctx->objects) p.max_object_tris = o.T > p.max_object_tris ? o.T : p.max_object_tris;
     p.tiles_x = (W + 63) / 64;

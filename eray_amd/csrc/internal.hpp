@@ -56,8 +56,10 @@ struct LightDesc {
     float brightness;
 };
 
-constexpr int kMaxObjects = 64;
-constexpr int kMaxLights = 64;
+// The first objects / lights also travel inline in the kernel arguments (scalar constant
+// loads, no dependent global round trip); larger scenes read the rest from device arrays.
+constexpr int kInlineObjects = 4;
+constexpr int kInlineLights = 8;
 
 struct FrameParams {
     // camera (camera.rs:57-76)
@@ -80,6 +82,8 @@ struct FrameParams {
     uint32_t nobj, nlights;
     uint32_t max_object_tris;  // selects the kernel variant with LDS triangle tiles
     uint32_t tiles_x;  // pixel tiles per row
+    ObjectDesc obj_inline[kInlineObjects];
+    LightDesc light_inline[kInlineLights];
 };
 
 // ------------------------------------------------------------- launchers (.hip files) ------

@@ -182,11 +182,12 @@ __device__ __forceinline__ bool cull_one(float A, float B, float K, float T, flo
     float fmax = (K + ax) + by;
     return fmax < -T;
 }
-__device__ __forceinline__ bool cull_rejects(const TriCull& c, float xlo, float xhi, float ylo,
+__device__ __forceinline__ bool cull_rejects(const TriCull c, float xlo, float xhi, float ylo,
                                              float yhi) {
-    return cull_one(c.A.x, c.B.x, c.K.x, c.T.x, xlo, xhi, ylo, yhi) ||
-           cull_one(c.A.y, c.B.y, c.K.y, c.T.y, xlo, xhi, ylo, yhi) ||
-           cull_one(c.A.z, c.B.z, c.K.z, c.T.z, xlo, xhi, ylo, yhi) ||
+    // all four conditions, no short-circuit: the record is one 64-byte load
+    return cull_one(c.A.x, c.B.x, c.K.x, c.T.x, xlo, xhi, ylo, yhi) |
+           cull_one(c.A.y, c.B.y, c.K.y, c.T.y, xlo, xhi, ylo, yhi) |
+           cull_one(c.A.z, c.B.z, c.K.z, c.T.z, xlo, xhi, ylo, yhi) |
            cull_one(c.A.w, c.B.w, c.K.w, c.T.w, xlo, xhi, ylo, yhi);
 }
 
@@ -369,14 +370,16 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
     const uint32_t y = p.row0 + py;
     const f3 C = mk3(p.cx, p.cy, p.cz);
 
-    Bundle bd;  // the wave's kWaveW x kTileH pixel rectangle
-    {
+    Bundle bd;  // the wave's kWaveW x kTileH pixel rectangle, widened to contain every
+    {           // pixel's x' = x/W and y' = y/H (approximate reciprocal, then 2^-20 outward)
         const uint32_t xe = min(wx0 + kWaveW - 1, p.cam_w ? p.cam_w - 1 : 0);
         const uint32_t ye = p.row0 + min(wy0 + kTileH - 1, p.rows ? p.rows - 1 : 0);
-        bd.xlo = (float)wx0 / (float)p.cam_w;
-        bd.xhi = (float)xe / (float)p.cam_w;
-        bd.ylo = (float)(p.row0 + wy0) / (float)p.cam_h;
-        bd.yhi = (float)ye / (float)p.cam_h;
+        const float rw = __builtin_amdgcn_rcpf((float)p.cam_w), rh = __builtin_amdgcn_rcpf((float)p.cam_h);
+        const float lo = 1.0f - 0x1p-20f, hi = 1.0f + 0x1p-20f;
+        bd.xlo = ((float)wx0 * rw) * lo;
+        bd.xhi = ((float)xe * rw) * hi;
+        bd.ylo = ((float)(p.row0 + wy0) * rh) * lo;
+        bd.yhi = ((float)ye * rh) * hi;
     }
 
     // The camera ray is generated lazily: a wave whose pixel block meets no candidate triangle
@@ -391,10 +394,14 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
     int best_face = -1;
     float bu = 0.0f, bv = 0.0f, bt = 0.0f;
     for (uint32_t oi = 0; oi < p.nobj; ++oi) {
-        const ObjectDesc ob = p.objects[oi];  // uniform: scalar loads
+        const ObjectDesc ob = oi < kInlineObjects ? p.obj_inline[oi] : p.objects[oi];  // uniform
         auto activate = [&]() -> bool {
             if (!ray_ready) {
-                d = camera_dir(p, px, y);
+                // opaque to the optimiser: keeps the ray generation on this (rare) path
+                // instead of being speculated into every wave
+                uint32_t pxo = px, yo = y;
+                asm volatile("" : "+v"(pxo), "+v"(yo));
+                d = camera_dir(p, pxo, yo);
                 ray_ready = true;
             }
             return bbox_hit(ob, C, d);
@@ -460,7 +467,7 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
     };
 
     for (uint32_t li = 0; li < p.nlights; ++li) {
-        const LightDesc L = p.lights[li];  // uniform: scalar loads
+        const LightDesc L = li < kInlineLights ? p.light_inline[li] : p.lights[li];  // uniform
         if (L.variant == 1) continue;  // point lights first (engine.rs:274-279)
         const f3 Lp = mk3(L.pos[0], L.pos[1], L.pos[2]);
         // reaches_light(Ray::new(P + N * 0.1, Lp - P)) (engine.rs:280-286, 218-228)
@@ -473,7 +480,7 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
         }
         bool reached = true, decided = false;
         for (uint32_t oi = 0; oi < p.nobj; ++oi) {
-            const ObjectDesc ob = p.objects[oi];
+            const ObjectDesc ob = oi < kInlineObjects ? p.obj_inline[oi] : p.objects[oi];
             const int st0 = (have && !decided && bbox_hit(ob, S, sd)) ? kSearching : kDone;
             auto never = []() -> bool { return false; };
             float u = 0.0f, v = 0.0f, t = 0.0f;
@@ -505,7 +512,7 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
     }
     if (have) {
         for (uint32_t li = 0; li < p.nlights; ++li) {  // ambient lights (engine.rs:341-352)
-            const LightDesc L = p.lights[li];
+            const LightDesc L = li < kInlineLights ? p.light_inline[li] : p.lights[li];
             if (L.variant != 1) continue;
             const rgb m{rust_min(L.color[0], color.r), rust_min(L.color[1], color.g),
                         rust_min(L.color[2], color.b)};

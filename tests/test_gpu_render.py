@@ -209,3 +209,34 @@ def test_pack_ppm_matches_oracle(gpu, oracle):
     out.free()
     ref = oracle.ppm_bytes(img)
     assert got == ref[len(capi.ppm_header(53, 37)):]
+
+
+def test_many_objects_and_lights(gpu, oracle):
+    """More objects and lights than travel inline in the kernel arguments."""
+    rng = np.random.default_rng(11)
+    W, H = 64, 48
+    s = oracle.Scene()
+    gpu.scene_reset()
+    cam = capi.make_camera((0.1, -0.2, 4.5), (4.0, 3.0), W, 1.0)
+    gpu.set_camera(cam)
+    keep = []
+    for k in range(6):
+        pos, nrm, uv = random_mesh(rng, int(rng.integers(3, 40)), scale=0.6, center=rng.uniform(-1, 1, 3))
+        color = rng.uniform(0, 1, (4, 4, 3)).astype(np.float32)
+        dc = gpu.to_device(color)
+        keep.append(dc)
+        lo, hi = pos.reshape(-1, 3).min(0), pos.reshape(-1, 3).max(0)
+        gpu.add_object(pos, nrm, uv, tuple(lo), tuple(hi), color=dc.image())
+        s.add_object(pos, nrm, uv, tuple(lo), tuple(hi), color=color)
+    for k in range(10):
+        var = "ambient" if k % 3 == 0 else "point"
+        p, c, b = tuple(rng.uniform(-2, 2, 3)), tuple(rng.uniform(0, 1, 3)), float(rng.uniform(0.1, 1))
+        gpu.add_light(capi.make_light(p, var, c, b))
+        s.add_light(p, var, c, b)
+    rgb, face, _ = gpu_render(gpu, W, H)
+    ref, ref_face, stats = oracle.render(s, oracle.camera((0.1, -0.2, 4.5), (4.0, 3.0), W, 1.0), want_faces=True)
+    for a in keep:
+        a.free()
+    assert stats["hit_pixels"] > 0
+    assert np.array_equal(face, ref_face)
+    assert_bit_equal(rgb, ref, "many objects/lights")
