@@ -55,6 +55,10 @@ struct eray_ctx {
     std::vector<LightDesc> h_lights;
     std::vector<float> h_raw;
     uint32_t total_tris = 0;
+    uint4* d_queue = nullptr;  // hit queue (2 x uint4 per pixel)
+    size_t queue_cap = 0;
+    uint32_t* d_queue_count = nullptr;  // two parity counters
+    uint32_t parity = 0;
 };
 
 namespace {
@@ -236,7 +240,8 @@ int eray_ctx_destroy(eray_ctx* ctx) {
     if (!ctx) return ERAY_OK;
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
-    void* bufs[] = {ctx->d_hot, ctx->d_shade, ctx->d_cull, ctx->d_raw, ctx->d_objs, ctx->d_lights};
+    void* bufs[] = {ctx->d_hot, ctx->d_shade, ctx->d_cull, ctx->d_raw, ctx->d_objs, ctx->d_lights,
+                    ctx->d_queue, ctx->d_queue_count};
     for (void* b : bufs)
         if (b) hipFree(b);
     if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
@@ -486,7 +491,22 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     p.max_object_tris = 0;
     for (auto& o : ctx->objects) p.max_object_tris = o.T > p.max_object_tris ? o.T : p.max_object_tris;
     p.tiles_x = (W + 63) / 64;
+    const size_t need = 2 * (size_t)rp->rows * W;
+    if (int st = ensure(ctx, &ctx->d_queue, &ctx->queue_cap, need)) return st;
+    if (!ctx->d_queue_count) {
+        HIP_TRY(ctx, hipMalloc((void**)&ctx->d_queue_count, 2 * sizeof(uint32_t)));
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_queue_count, 0, 2 * sizeof(uint32_t), ctx->stream));
+    }
+    p.queue = ctx->d_queue;
+    p.queue_count = ctx->d_queue_count;
     return ERAY_OK;
+}
+
+// one frame = visibility + shading; the queue parity alternates per frame
+hipError_t launch_frame(eray_ctx* ctx, FrameParams& p) {
+    p.queue_parity = ctx->parity;
+    ctx->parity ^= 1u;
+    return launch_render(p, ctx->stream);
 }
 }  // namespace
 
@@ -494,7 +514,7 @@ int eray_render(eray_ctx* ctx, const eray_render_params* rp) {
     FrameParams p;
     bool empty = false;
     if (int st = prepare_render(ctx, rp, &p, &empty)) return st;
-    if (!empty) HIP_TRY(ctx, launch_render(p, ctx->stream));
+    if (!empty) HIP_TRY(ctx, launch_frame(ctx, p));
     return ERAY_OK;
 }
 
@@ -506,7 +526,7 @@ int eray_render_frames(eray_ctx* ctx, const eray_render_params* rp, uint32_t fra
     if (mean_kernel_ms) *mean_kernel_ms = 0.0f;
     if (empty || !frames) return ERAY_OK;
     if (!mean_kernel_ms) {
-        for (uint32_t f = 0; f < frames; ++f) HIP_TRY(ctx, launch_render(p, ctx->stream));
+        for (uint32_t f = 0; f < frames; ++f) HIP_TRY(ctx, launch_frame(ctx, p));
         return ERAY_OK;
     }
     std::vector<hipEvent_t> ev(2 * (size_t)frames, nullptr);
@@ -520,7 +540,7 @@ int eray_render_frames(eray_ctx* ctx, const eray_render_params* rp, uint32_t fra
     }
     for (uint32_t f = 0; f < frames && st == ERAY_OK; ++f) {
         hipError_t he = hipEventRecord(ev[2 * f], ctx->stream);
-        if (he == hipSuccess) he = launch_render(p, ctx->stream);
+        if (he == hipSuccess) he = launch_frame(ctx, p);
         if (he == hipSuccess) he = hipEventRecord(ev[2 * f + 1], ctx->stream);
         if (he != hipSuccess) st = set_error(ctx, ERAY_E_HIP, "render loop: %s", hipGetErrorString(he));
     }

@@ -82,6 +82,10 @@ struct FrameParams {
     uint32_t nobj, nlights;
     uint32_t max_object_tris;  // selects the kernel variant with LDS triangle tiles
     uint32_t tiles_x;  // pixel tiles per row
+    // hit queue between the visibility and shading passes: 2 x uint4 per hit
+    uint4* queue;
+    uint32_t* queue_count;  // two counters; the frame uses [queue_parity]
+    uint32_t queue_parity;
     ObjectDesc obj_inline[kInlineObjects];
     LightDesc light_inline[kInlineLights];
 };

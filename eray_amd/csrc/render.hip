@@ -34,8 +34,6 @@ namespace {
 using namespace eray::dev;
 
 constexpr int kWG = 256;
-constexpr int kTileW = 64, kTileH = 4;  // workgroup pixel tile (4 waves side by side)
-constexpr int kWaveW = 16;               // each wave: a 16 x 4 pixel bundle
 constexpr int kTriTile = 256;
 
 // --------------------------------------------------------------------- triangle setup ------
@@ -231,11 +229,11 @@ __device__ __forceinline__ bool bbox_hit(const ObjectDesc& ob, f3 s, f3 d) {
     return true;
 }
 
-struct Bundle {  // the wave's pixel rectangle in viewport coordinates
+struct Bundle {  // a wave's pixel rectangle in viewport coordinates
     float xlo, xhi, ylo, yhi;
 };
 
-// Per-lane search state: kUndecided (ray and bounding-box test not evaluated yet), kSearching,
+// Per-ray search state: kUndecided (ray and bounding-box test not evaluated yet), kSearching,
 // kDone (hit found, bbox rejected, or not a pixel of the image).
 constexpr int kUndecided = 0, kSearching = 1, kDone = 2;
 
@@ -244,40 +242,58 @@ constexpr int kUndecided = 0, kSearching = 1, kDone = 2;
 // workgroup-shared LDS tiles.
 constexpr uint32_t kDirectMax = 256;
 
-// First-hit search over triangles [begin, begin + count) (Object::intersects' face loop,
-// object.rs:63-78).  `st` is the lane's search state; lanes still kUndecided when the wave
-// meets its first candidate triangle call activate(), which must generate the ray (writing
-// `d`) and return the bounding-box verdict (object.rs:59-61).  Returns the face index relative
-// to `begin`, or -1.  kLds: every thread of the workgroup must call it (barriers).
-template <bool kCull, bool kLds, typename Activate>
-__device__ int first_hit(const FrameParams& p, uint32_t begin, uint32_t count, int st, f3 o,
-                         const f3& d, const Bundle& bd, TriHot* s_hot, TriCull* s_cull,
-                         Activate&& activate, float& hu, float& hv, float& ht) {
-    int found = -1;
+// First-hit search over triangles [begin, begin + count) for R rays per lane (Object::intersects'
+// face loop, object.rs:63-78).  Rays still kUndecided when the wave meets its first candidate
+// triangle are resolved by activate(a), which must generate their directions (into `d`) and
+// return the bounding-box verdicts (object.rs:59-61) in a[].  found[k] receives the face index
+// relative to `begin`, or stays -1.  kLds: every thread of the workgroup must call it.
+template <bool kCull, bool kLds, int R, typename Activate>
+__device__ void first_hit(const FrameParams& p, uint32_t begin, uint32_t count, int (&st)[R],
+                          const f3& o, const f3 (&d)[R], const Bundle& bd, TriHot* s_hot,
+                          TriCull* s_cull, Activate&& activate, int (&found)[R], float (&hu)[R],
+                          float (&hv)[R], float (&ht)[R]) {
     const uint32_t lane = threadIdx.x & 63;
+    auto any_state = [&](int s) {
+        bool a = false;
+#pragma unroll
+        for (int k = 0; k < R; ++k) a = a || st[k] == s;
+        return __any(a);
+    };
+    auto not_done = [&]() {
+        bool a = false;
+#pragma unroll
+        for (int k = 0; k < R; ++k) a = a || st[k] != kDone;
+        return a;
+    };
     auto test = [&](const TriHot& h, uint32_t idx) {
-        if (st == kSearching) {
-            float u, v, t;
-            if (exact_test(h, o, d, u, v, t)) {
-                found = (int)idx;
-                hu = u;
-                hv = v;
-                ht = t;
-                st = kDone;
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            if (st[k] == kSearching) {
+                float u, v, t;
+                if (exact_test(h, o, d[k], u, v, t)) {
+                    found[k] = (int)idx;
+                    hu[k] = u;
+                    hv[k] = v;
+                    ht[k] = t;
+                    st[k] = kDone;
+                }
             }
         }
     };
-    // returns false when no lane of the wave can hit anything in this object any more
+    // false when no ray of the wave can hit anything in this object any more
     auto resolve = [&]() -> bool {
-        if (__any(st == kUndecided)) {
-            const bool a = activate();
-            if (st == kUndecided) st = a ? kSearching : kDone;
+        if (any_state(kUndecided)) {
+            bool a[R];
+            activate(a);
+#pragma unroll
+            for (int k = 0; k < R; ++k)
+                if (st[k] == kUndecided) st[k] = a[k] ? kSearching : kDone;
         }
-        return __any(st == kSearching);
+        return any_state(kSearching);
     };
     if (!kLds) {
         for (uint32_t base = 0; base < count; base += 64) {
-            if (!__any(st != kDone)) break;
+            if (!__any(not_done())) break;
             unsigned long long mask;
             if (kCull) {
                 const uint32_t j = base + lane;
@@ -292,20 +308,20 @@ __device__ int first_hit(const FrameParams& p, uint32_t begin, uint32_t count, i
                 const uint32_t bit = (uint32_t)(__ffsll(mask) - 1);
                 mask &= mask - 1;
                 test(p.tris[begin + base + bit], base + bit);
-                if (!__any(st == kSearching)) return found;
+                if (!any_state(kSearching)) return;
             }
         }
-        return found;
+        return;
     }
     for (uint32_t base = 0; base < count; base += kTriTile) {
-        if (!__syncthreads_or(st != kDone)) break;  // also orders the LDS reuse below
+        if (!__syncthreads_or(not_done())) break;  // also orders the LDS reuse below
         const uint32_t n = min((uint32_t)kTriTile, count - base);
         if (threadIdx.x < n) {
             s_hot[threadIdx.x] = p.tris[begin + base + threadIdx.x];
             if (kCull) s_cull[threadIdx.x] = p.cull[begin + base + threadIdx.x];
         }
         __syncthreads();
-        if (!__any(st != kDone)) continue;
+        if (!__any(not_done())) continue;
         for (uint32_t c = 0; c < n; c += 64) {
             unsigned long long mask;
             if (kCull) {
@@ -321,12 +337,11 @@ __device__ int first_hit(const FrameParams& p, uint32_t begin, uint32_t count, i
                 const uint32_t bit = (uint32_t)(__ffsll(mask) - 1);
                 mask &= mask - 1;
                 test(s_hot[c + bit], base + c + bit);
-                if (!__any(st == kSearching)) break;
+                if (!any_state(kSearching)) break;
             }
-            if (!__any(st == kSearching)) break;
+            if (!any_state(kSearching)) break;
         }
     }
-    return found;
 }
 
 __device__ __forceinline__ bool tex_value(const TexView& tv, float x, float y, float& out) {
@@ -349,31 +364,43 @@ __device__ __forceinline__ f3 camera_dir(const FrameParams& p, uint32_t px, uint
     return normalize(sub(add(add(botleft, mul(horizontal, xf)), mul(vertical, yf)), C));
 }
 
-// kLdsTiles: some object has more than kDirectMax triangles (workgroup LDS tiles needed);
-// without it the kernel has no barrier at all and waves retire independently.
+__device__ __forceinline__ ObjectDesc object_desc(const FrameParams& p, uint32_t oi) {
+    return oi < kInlineObjects ? p.obj_inline[oi] : p.objects[oi];
+}
+__device__ __forceinline__ LightDesc light_desc(const FrameParams& p, uint32_t li) {
+    return li < kInlineLights ? p.light_inline[li] : p.lights[li];
+}
+
+// ---------------------------------------------------------------------- visibility ----------
+// Pass 1 of a frame, over every pixel: the closest object's first hit of each camera ray
+// (cast_ray's object loop, engine.rs:119-126).  Each lane owns kVisR horizontally adjacent
+// pixels; a wave owns a 64 x 4 pixel block (its culling bundle), a workgroup 64 x 16.  Every
+// pixel gets the background colour (engine.rs:355-357) written with 16-byte stores; hit pixels
+// are appended to the hit queue and overwritten by the shading pass.
+constexpr int kVisR = 4;
+constexpr uint32_t kVisWaveW = 64, kVisWaveH = 4, kVisTileW = 64, kVisTileH = 16;
+
 template <bool kCull, bool kLdsTiles>
-__global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
+__global__ void __launch_bounds__(kWG) visibility_kernel(FrameParams p) {
     __shared__ TriHot s_hot[kLdsTiles ? kTriTile : 1];
     __shared__ TriCull s_cull[(kCull && kLdsTiles) ? kTriTile : 1];
-    __shared__ float4 s_rgb[kTileH * kTileW * 3 / 4];  // each wave's f32 RGB rows, staged
-    __shared__ uint32_t s_ppm[kTileH * kTileW * 3 / 4];  // ... and its PPM byte rows
 
     const uint32_t tile = blockIdx.x;
     const uint32_t tx = tile % p.tiles_x, ty = tile / p.tiles_x;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t tx0 = tx * kTileW, ty0 = ty * kTileH;
-    const uint32_t wx0 = tx0 + wave * kWaveW, wy0 = ty0;
-    const uint32_t lx = wave * kWaveW + (lane % kWaveW), ly = lane / kWaveW;  // in the tile
-    const uint32_t px = tx0 + lx;
-    const uint32_t py = ty0 + ly;  // local row (0 .. rows-1)
-    const bool valid = px < p.cam_w && py < p.rows;
+    const uint32_t wx0 = tx * kVisTileW, wy0 = ty * kVisTileH + wave * kVisWaveH;
+    const uint32_t px0 = wx0 + (lane & 15) * kVisR;
+    const uint32_t py = wy0 + (lane >> 4);  // local row (0 .. rows-1)
     const uint32_t y = p.row0 + py;
     const f3 C = mk3(p.cx, p.cy, p.cz);
+    bool valid[kVisR];
+#pragma unroll
+    for (int k = 0; k < kVisR; ++k) valid[k] = px0 + k < p.cam_w && py < p.rows;
 
-    Bundle bd;  // the wave's kWaveW x kTileH pixel rectangle, widened to contain every
-    {           // pixel's x' = x/W and y' = y/H (approximate reciprocal, then 2^-20 outward)
-        const uint32_t xe = min(wx0 + kWaveW - 1, p.cam_w ? p.cam_w - 1 : 0);
-        const uint32_t ye = p.row0 + min(wy0 + kTileH - 1, p.rows ? p.rows - 1 : 0);
+    Bundle bd;  // the wave's pixel block, widened to contain every pixel's x' = x/W, y' = y/H
+    {           // (approximate reciprocal, then 2^-20 outward; x', y' >= 0)
+        const uint32_t xe = min(wx0 + kVisWaveW - 1, p.cam_w ? p.cam_w - 1 : 0);
+        const uint32_t ye = p.row0 + min(wy0 + kVisWaveH - 1, p.rows ? p.rows - 1 : 0);
         const float rw = __builtin_amdgcn_rcpf((float)p.cam_w), rh = __builtin_amdgcn_rcpf((float)p.cam_h);
         const float lo = 1.0f - 0x1p-20f, hi = 1.0f + 0x1p-20f;
         bd.xlo = ((float)wx0 * rw) * lo;
@@ -382,196 +409,271 @@ __global__ void __launch_bounds__(kWG) render_kernel(FrameParams p) {
         bd.yhi = ((float)ye * rh) * hi;
     }
 
-    // The camera ray is generated lazily: a wave whose pixel block meets no candidate triangle
-    // of any object (most of the frame) never needs it — its pixels are background.
-    f3 d = mk3(0.0f, 0.0f, 0.0f);
+    // Camera rays are generated lazily: a wave whose block meets no candidate triangle of any
+    // object (most of the frame) never needs them.
+    f3 d[kVisR];
+#pragma unroll
+    for (int k = 0; k < kVisR; ++k) d[k] = mk3(0.0f, 0.0f, 0.0f);
     bool ray_ready = false;
 
-    // ---- cast_ray (engine.rs:112-216): closest object among first hits -------------------
-    bool have = false;
-    float closest = 0.0f;
-    uint32_t best_obj = 0;
-    int best_face = -1;
-    float bu = 0.0f, bv = 0.0f, bt = 0.0f;
+    bool have[kVisR];
+    float closest[kVisR], bu[kVisR], bv[kVisR], bt[kVisR];
+    uint32_t best_obj[kVisR];
+    int best_face[kVisR];
+#pragma unroll
+    for (int k = 0; k < kVisR; ++k) {
+        have[k] = false;
+        closest[k] = bu[k] = bv[k] = bt[k] = 0.0f;
+        best_obj[k] = 0;
+        best_face[k] = -1;
+    }
     for (uint32_t oi = 0; oi < p.nobj; ++oi) {
-        const ObjectDesc ob = oi < kInlineObjects ? p.obj_inline[oi] : p.objects[oi];  // uniform
-        auto activate = [&]() -> bool {
+        const ObjectDesc ob = object_desc(p, oi);  // uniform: scalar loads
+        auto activate = [&](bool (&a)[kVisR]) {
             if (!ray_ready) {
-                // opaque to the optimiser: keeps the ray generation on this (rare) path
-                // instead of being speculated into every wave
-                uint32_t pxo = px, yo = y;
+                // opaque to the optimiser: keeps ray generation on this (rare) path instead of
+                // being speculated into every wave
+                uint32_t pxo = px0, yo = y;
                 asm volatile("" : "+v"(pxo), "+v"(yo));
-                d = camera_dir(p, pxo, yo);
+#pragma unroll
+                for (int k = 0; k < kVisR; ++k) d[k] = camera_dir(p, pxo + k, yo);
                 ray_ready = true;
             }
-            return bbox_hit(ob, C, d);
+#pragma unroll
+            for (int k = 0; k < kVisR; ++k) a[k] = bbox_hit(ob, C, d[k]);
         };
-        const int st0 = valid ? kUndecided : kDone;
-        float u = 0.0f, v = 0.0f, t = 0.0f;
-        const int f = (!kLdsTiles || ob.tri_count <= kDirectMax)
-                          ? first_hit<kCull, false>(p, ob.tri_begin, ob.tri_count, st0, C, d, bd, s_hot,
-                                                    s_cull, activate, u, v, t)
-                          : first_hit<kCull, kLdsTiles>(p, ob.tri_begin, ob.tri_count, st0, C, d, bd, s_hot,
-                                                        s_cull, activate, u, v, t);
-        if (f >= 0) {
-            const f3 P = add(C, mul(d, t));
-            const float dsq = len_sq(sub(P, C));
-            if (!have || dsq < closest) {
-                have = true;
-                closest = dsq;
-                best_obj = oi;
-                best_face = f;
-                bu = u;
-                bv = v;
-                bt = t;
+        int st[kVisR], f[kVisR];
+        float u[kVisR], v[kVisR], t[kVisR];
+#pragma unroll
+        for (int k = 0; k < kVisR; ++k) {
+            st[k] = valid[k] ? kUndecided : kDone;
+            f[k] = -1;
+        }
+        if (!kLdsTiles || ob.tri_count <= kDirectMax)
+            first_hit<kCull, false, kVisR>(p, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull,
+                                           activate, f, u, v, t);
+        else
+            first_hit<kCull, kLdsTiles, kVisR>(p, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot,
+                                               s_cull, activate, f, u, v, t);
+#pragma unroll
+        for (int k = 0; k < kVisR; ++k) {
+            if (f[k] >= 0) {
+                const f3 P = add(C, mul(d[k], t[k]));
+                const float dsq = len_sq(sub(P, C));
+                if (!have[k] || dsq < closest[k]) {  // strict `<`: first object wins ties
+                    have[k] = true;
+                    closest[k] = dsq;
+                    best_obj[k] = oi;
+                    best_face[k] = f[k];
+                    bu[k] = u[k];
+                    bv[k] = v[k];
+                    bt[k] = t[k];
+                }
             }
         }
     }
 
-    // ---- hit data and Material::get (material.rs:56-94) ----------------------------------
-    f3 P = mk3(0.0f, 0.0f, 0.0f), N = mk3(0.0f, 0.0f, 0.0f);
-    rgb color{0.0f, 0.0f, 0.0f};
-    float kd = 0.5f, ks = 0.5f, sp = 1.0f;
-    if (have) {
-        const ObjectDesc& ob = p.objects[best_obj];
-        const TriShade sh = p.shade[ob.tri_begin + (uint32_t)best_face];
-        P = add(C, mul(d, bt));
-        const f3 na = mk3(sh.s0.x, sh.s0.y, sh.s0.z), nb = mk3(sh.s0.w, sh.s1.x, sh.s1.y);
-        const f3 nc = mk3(sh.s1.z, sh.s1.w, sh.s2.x);
-        N = normalize(add(add(mul(na, bu), mul(nb, bv)), mul(nc, bt)));
-        const float w = 1.0f - bu - bv;
-        const float uv0 = ((sh.s2.y * w) + (sh.s2.w * bu)) + (sh.s3.y * bv);
-        const float uv1 = ((sh.s2.z * w) + (sh.s3.x * bu)) + (sh.s3.z * bv);
-        if (ob.mat.color.data) {
-            const TexView& tv = ob.mat.color;
-            const uint32_t ix = sat_u32(uv0 * (float)tv.w) % tv.w;
-            const uint32_t iy = sat_u32(uv1 * (float)tv.h) % tv.h;
-            const float* c = tv.data + 3 * ((size_t)iy * tv.w + ix);
-            color = rgb{c[0], c[1], c[2]};
+    // ---- background for every pixel (sat_u8(0.1*255), sat_u8(0.2*255) = 25, 51) ----------
+    const float b01 = 0.1f, b02 = 0.2f;
+    const uint32_t c01 = sat_u8(b01 * 255.0f), c02 = sat_u8(b02 * 255.0f);
+    const bool all_valid = valid[0] && valid[kVisR - 1];
+    const size_t idx0 = (size_t)py * p.img_w + px0;
+    const size_t prow = (size_t)(p.rows - 1 - py);  // PPM byte row of this camera row
+    if (all_valid && (p.img_w % 4) == 0 &&
+        ((reinterpret_cast<uintptr_t>(p.out_rgb) | reinterpret_cast<uintptr_t>(p.out_face)) & 15) == 0 &&
+        (reinterpret_cast<uintptr_t>(p.out_ppm) & 3) == 0) {
+        if (p.out_rgb) {  // 4 pixels = 12 floats = 3 x 16 B
+            float4* o = reinterpret_cast<float4*>(p.out_rgb + 3 * idx0);
+            o[0] = make_float4(b01, b01, b02, b01);
+            o[1] = make_float4(b01, b02, b01, b01);
+            o[2] = make_float4(b02, b01, b01, b02);
         }
-        tex_value(ob.mat.diffuse, uv0, uv1, kd);
-        tex_value(ob.mat.specular, uv0, uv1, ks);
-        tex_value(ob.mat.specular_power, uv0, uv1, sp);
-    }
-
-    // lighting list as a running left fold (impl Sum for Color, color.rs:82-87)
-    bool any = false;
-    rgb acc{0.0f, 0.0f, 0.0f};
-    auto push = [&](rgb c) {
-        if (any) {
-            acc = cadd(acc, c);
-        } else {
-            acc = c;
-            any = true;
+        if (p.out_ppm) {  // 4 pixels = 12 bytes
+            const uint32_t w0 = c01 | (c01 << 8) | (c02 << 16) | (c01 << 24);
+            const uint32_t w1 = c01 | (c02 << 8) | (c01 << 16) | (c01 << 24);
+            const uint32_t w2 = c02 | (c01 << 8) | (c01 << 16) | (c02 << 24);
+            uint32_t* o = reinterpret_cast<uint32_t*>(p.out_ppm + 3 * (prow * p.img_w + px0));
+            o[0] = w0;
+            o[1] = w1;
+            o[2] = w2;
         }
-    };
-
-    for (uint32_t li = 0; li < p.nlights; ++li) {
-        const LightDesc L = li < kInlineLights ? p.light_inline[li] : p.lights[li];  // uniform
-        if (L.variant == 1) continue;  // point lights first (engine.rs:274-279)
-        const f3 Lp = mk3(L.pos[0], L.pos[1], L.pos[2]);
-        // reaches_light(Ray::new(P + N * 0.1, Lp - P)) (engine.rs:280-286, 218-228)
-        f3 S = mk3(0.0f, 0.0f, 0.0f), sd = mk3(0.0f, 0.0f, 1.0f);
-        float dist = 0.0f;
-        if (have) {
-            S = add(P, mul(N, 0.1f));
-            sd = normalize(sub(Lp, P));
-            dist = len(sub(Lp, S));
-        }
-        bool reached = true, decided = false;
-        for (uint32_t oi = 0; oi < p.nobj; ++oi) {
-            const ObjectDesc ob = oi < kInlineObjects ? p.obj_inline[oi] : p.objects[oi];
-            const int st0 = (have && !decided && bbox_hit(ob, S, sd)) ? kSearching : kDone;
-            auto never = []() -> bool { return false; };
-            float u = 0.0f, v = 0.0f, t = 0.0f;
-            const int f = (!kLdsTiles || ob.tri_count <= kDirectMax)
-                              ? first_hit<false, false>(p, ob.tri_begin, ob.tri_count, st0, S, sd, bd, s_hot,
-                                                        s_cull, never, u, v, t)
-                              : first_hit<false, kLdsTiles>(p, ob.tri_begin, ob.tri_count, st0, S, sd, bd,
-                                                            s_hot, s_cull, never, u, v, t);
-            if (f >= 0) {
-                const f3 hp = add(S, mul(sd, t));
-                reached = len(sub(hp, S)) > dist;
-                decided = true;
-            }
-        }
-        if (have && reached) {  // engine.rs:287-322
-            const f3 LmP = sub(Lp, P);
-            float prod = rust_clamp(dot0(N, LmP), 0.0f, 1.0f);
-            if (prod != prod) prod = 0.0f;
-            const float falloff = 1.0f / len(LmP);
-            const rgb lc{L.color[0], L.color[1], L.color[2]};
-            const rgb diffusion = cmul(cmul(cmul(cmul(cmulc(color, lc), kd), prod), L.brightness), falloff);
-            const f3 reflected = sub(d, mul(mul(N, 2.0f), dot0(d, N)));
-            const float res = rust_clamp(
-                ks * L.brightness * powf_ref(dot0(normalize(reflected), normalize(LmP)), sp), 0.0f, 1.0f);
-            const float sf = rust_clamp(powf_ref(falloff, sp), 0.0f, 1.0f);
-            const rgb specular{res * sf, res * sf, res * sf};
-            push(cadd(diffusion, specular));
-        }
-    }
-    if (have) {
-        for (uint32_t li = 0; li < p.nlights; ++li) {  // ambient lights (engine.rs:341-352)
-            const LightDesc L = li < kInlineLights ? p.light_inline[li] : p.lights[li];
-            if (L.variant != 1) continue;
-            const rgb m{rust_min(L.color[0], color.r), rust_min(L.color[1], color.g),
-                        rust_min(L.color[2], color.b)};
-            push(cmul(cmul(m, kd), L.brightness));
-        }
+        if (p.out_face)
+            *reinterpret_cast<int4*>(p.out_face + idx0) = make_int4(best_face[0], best_face[1], best_face[2], best_face[3]);
     } else {
-        push(rgb{0.1f, 0.1f, 0.2f});  // engine.rs:355-357
+#pragma unroll
+        for (int k = 0; k < kVisR; ++k) {
+            if (!valid[k]) continue;
+            if (p.out_rgb) {
+                float* o = p.out_rgb + 3 * (idx0 + k);
+                o[0] = b01;
+                o[1] = b01;
+                o[2] = b02;
+            }
+            if (p.out_ppm) {
+                uint8_t* o = p.out_ppm + 3 * (prow * p.img_w + px0 + k);
+                o[0] = (uint8_t)c01;
+                o[1] = (uint8_t)c01;
+                o[2] = (uint8_t)c02;
+            }
+            if (p.out_face) p.out_face[idx0 + k] = best_face[k];
+        }
     }
 
-    // ---- outputs: Image::set + Color::as_bytes rows bottom-up (image.rs:41-74) ------------
-    const uint32_t b0 = (uint32_t)sat_u8(acc.r * 255.0f), b1 = (uint32_t)sat_u8(acc.g * 255.0f),
-                   b2 = (uint32_t)sat_u8(acc.b * 255.0f);
-    if (valid && p.out_face) p.out_face[(size_t)py * p.img_w + px] = have ? best_face : -1;
-    // Full, aligned wave blocks leave through the wave's own LDS slice as 16-byte row stores
-    // (no workgroup barrier); edge blocks store per pixel.
-    const bool full = wx0 + kWaveW <= p.cam_w && ty0 + kTileH <= p.rows && (p.img_w % 16) == 0 &&
-                      ((reinterpret_cast<uintptr_t>(p.out_rgb) | reinterpret_cast<uintptr_t>(p.out_ppm)) & 15) == 0;
-    if (full) {
-        constexpr uint32_t kWavePix = kWaveW * kTileH;
-        float* wrgb = reinterpret_cast<float*>(s_rgb) + 3 * kWavePix * wave;
-        uint8_t* wppm = reinterpret_cast<uint8_t*>(s_ppm) + 3 * kWavePix * wave;
-        const uint32_t wl = lane % kWaveW;
-        float* srgb = wrgb + 3 * (ly * kWaveW + wl);
-        srgb[0] = acc.r;
-        srgb[1] = acc.g;
-        srgb[2] = acc.b;
-        uint8_t* sppm = wppm + 3 * ((kTileH - 1 - ly) * kWaveW + wl);
-        sppm[0] = (uint8_t)b0;
-        sppm[1] = (uint8_t)b1;
-        sppm[2] = (uint8_t)b2;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        constexpr uint32_t kRgbRow4 = kWaveW * 3 / 4;   // float4 per wave row (12)
-        constexpr uint32_t kPpmRow16 = kWaveW * 3 / 16; // 16-byte words per wave row (3)
-        if (p.out_rgb && lane < kTileH * kRgbRow4) {
-            const uint32_t r = lane / kRgbRow4, c = lane % kRgbRow4;
-            float4* dst = reinterpret_cast<float4*>(p.out_rgb + 3 * ((size_t)(ty0 + r) * p.img_w + wx0)) + c;
-            *dst = reinterpret_cast<const float4*>(wrgb)[lane];
+    // ---- append the hits to the queue (one atomic per wave) --------------------------------
+    unsigned long long m[kVisR];
+    uint32_t total = 0;
+#pragma unroll
+    for (int k = 0; k < kVisR; ++k) {
+        m[k] = __ballot(have[k]);
+        total += (uint32_t)__popcll(m[k]);
+    }
+    if (total) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(p.queue_count + p.queue_parity, total);
+        base = __shfl(base, 0);
+        const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+        for (int k = 0; k < kVisR; ++k) {
+            if (have[k]) {
+                const uint32_t slot = base + (uint32_t)__popcll(m[k] & below);
+                p.queue[2 * (size_t)slot] = make_uint4(px0 + k, py, best_obj[k], (uint32_t)best_face[k]);
+                p.queue[2 * (size_t)slot + 1] =
+                    make_uint4(__float_as_uint(bu[k]), __float_as_uint(bv[k]), __float_as_uint(bt[k]), 0u);
+            }
+            base += (uint32_t)__popcll(m[k]);
         }
-        if (p.out_ppm && lane < kTileH * kPpmRow16) {
-            const uint32_t r = lane / kPpmRow16, c = lane % kPpmRow16;  // r-th byte row of the block
-            const size_t row = (size_t)(p.rows - ty0 - kTileH + r);
-            uint4* dst = reinterpret_cast<uint4*>(p.out_ppm + 3 * (row * p.img_w + wx0)) + c;
-            *dst = reinterpret_cast<const uint4*>(wppm)[lane];
+    }
+}
+
+// ---------------------------------------------------------------------- shading -------------
+// Pass 2: one thread per queued hit — hit data, Material::get (material.rs:56-94), shadow rays
+// (reaches_light, engine.rs:218-228), diffuse + specular + ambient (engine.rs:128-208), the
+// left-fold sum (color.rs:82-87) — then the pixel's f32 RGB and PPM bytes.  The grid strides
+// over the queue; block 0 clears the other parity's counter for the next frame.
+template <bool kLdsTiles>
+__global__ void __launch_bounds__(kWG) shade_kernel(FrameParams p) {
+    __shared__ TriHot s_hot[kLdsTiles ? kTriTile : 1];
+    __shared__ TriCull s_cull[1];
+    const uint32_t n = __hip_atomic_load(p.queue_count + p.queue_parity, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x == 0 && threadIdx.x == 0) p.queue_count[p.queue_parity ^ 1u] = 0u;
+    const f3 C = mk3(p.cx, p.cy, p.cz);
+    const Bundle bd{0.0f, 0.0f, 0.0f, 0.0f};
+    for (uint32_t base = blockIdx.x * kWG; base < n; base += gridDim.x * kWG) {
+        const uint32_t i = base + threadIdx.x;
+        const bool have = i < n;
+        uint4 e0 = make_uint4(0u, 0u, 0u, 0u), e1 = e0;
+        if (have) {
+            e0 = p.queue[2 * (size_t)i];
+            e1 = p.queue[2 * (size_t)i + 1];
         }
-    } else if (valid) {
-        const size_t idx = (size_t)py * p.img_w + px;
-        if (p.out_rgb) {
-            float* o = p.out_rgb + 3 * idx;
-            o[0] = acc.r;
-            o[1] = acc.g;
-            o[2] = acc.b;
+        const uint32_t px = e0.x, py = e0.y, oi = e0.z, face = e0.w;
+        const float bu = __uint_as_float(e1.x), bv = __uint_as_float(e1.y), bt = __uint_as_float(e1.z);
+        const f3 d = camera_dir(p, px, p.row0 + py);  // the same f32 ray as the visibility pass
+
+        f3 P = mk3(0.0f, 0.0f, 0.0f), N = mk3(0.0f, 0.0f, 0.0f);
+        rgb color{0.0f, 0.0f, 0.0f};
+        float kd = 0.5f, ks = 0.5f, sp = 1.0f;
+        if (have) {
+            const ObjectDesc ob = p.objects[oi];
+            const TriShade sh = p.shade[ob.tri_begin + face];
+            P = add(C, mul(d, bt));
+            const f3 na = mk3(sh.s0.x, sh.s0.y, sh.s0.z), nb = mk3(sh.s0.w, sh.s1.x, sh.s1.y);
+            const f3 nc = mk3(sh.s1.z, sh.s1.w, sh.s2.x);
+            N = normalize(add(add(mul(na, bu), mul(nb, bv)), mul(nc, bt)));
+            const float w = 1.0f - bu - bv;
+            const float uv0 = ((sh.s2.y * w) + (sh.s2.w * bu)) + (sh.s3.y * bv);
+            const float uv1 = ((sh.s2.z * w) + (sh.s3.x * bu)) + (sh.s3.z * bv);
+            if (ob.mat.color.data) {
+                const TexView& tv = ob.mat.color;
+                const uint32_t ix = sat_u32(uv0 * (float)tv.w) % tv.w;
+                const uint32_t iy = sat_u32(uv1 * (float)tv.h) % tv.h;
+                const float* c = tv.data + 3 * ((size_t)iy * tv.w + ix);
+                color = rgb{c[0], c[1], c[2]};
+            }
+            tex_value(ob.mat.diffuse, uv0, uv1, kd);
+            tex_value(ob.mat.specular, uv0, uv1, ks);
+            tex_value(ob.mat.specular_power, uv0, uv1, sp);
         }
-        if (p.out_ppm) {
-            uint8_t* o = p.out_ppm + 3 * ((size_t)(p.rows - 1 - py) * p.img_w + px);
-            o[0] = (uint8_t)b0;
-            o[1] = (uint8_t)b1;
-            o[2] = (uint8_t)b2;
+
+        bool any = false;  // the lighting list as a running left fold
+        rgb acc{0.0f, 0.0f, 0.0f};
+        auto push = [&](rgb c) {
+            if (any) {
+                acc = cadd(acc, c);
+            } else {
+                acc = c;
+                any = true;
+            }
+        };
+        for (uint32_t li = 0; li < p.nlights; ++li) {
+            const LightDesc L = light_desc(p, li);
+            if (L.variant == 1) continue;  // point lights first (engine.rs:274-279)
+            const f3 Lp = mk3(L.pos[0], L.pos[1], L.pos[2]);
+            // reaches_light(Ray::new(P + N * 0.1, Lp - P)) (engine.rs:280-286, 218-228)
+            f3 S = mk3(0.0f, 0.0f, 0.0f);
+            f3 sd[1] = {mk3(0.0f, 0.0f, 1.0f)};
+            float dist = 0.0f;
+            if (have) {
+                S = add(P, mul(N, 0.1f));
+                sd[0] = normalize(sub(Lp, P));
+                dist = len(sub(Lp, S));
+            }
+            bool reached = true, decided = false;
+            for (uint32_t oj = 0; oj < p.nobj; ++oj) {
+                const ObjectDesc ob = object_desc(p, oj);
+                int st[1] = {(have && !decided && bbox_hit(ob, S, sd[0])) ? kSearching : kDone};
+                int f[1] = {-1};
+                float u[1], v[1], t[1];
+                auto never = [](bool (&a)[1]) { a[0] = false; };
+                if (!kLdsTiles || ob.tri_count <= kDirectMax)
+                    first_hit<false, false, 1>(p, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot, s_cull,
+                                               never, f, u, v, t);
+                else
+                    first_hit<false, kLdsTiles, 1>(p, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot,
+                                                   s_cull, never, f, u, v, t);
+                if (f[0] >= 0) {
+                    const f3 hp = add(S, mul(sd[0], t[0]));
+                    reached = len(sub(hp, S)) > dist;
+                    decided = true;
+                }
+            }
+            if (have && reached) {  // engine.rs:287-322
+                const f3 LmP = sub(Lp, P);
+                float prod = rust_clamp(dot0(N, LmP), 0.0f, 1.0f);
+                if (prod != prod) prod = 0.0f;
+                const float falloff = 1.0f / len(LmP);
+                const rgb lc{L.color[0], L.color[1], L.color[2]};
+                const rgb diffusion = cmul(cmul(cmul(cmul(cmulc(color, lc), kd), prod), L.brightness), falloff);
+                const f3 reflected = sub(d, mul(mul(N, 2.0f), dot0(d, N)));
+                const float res = rust_clamp(
+                    ks * L.brightness * powf_ref(dot0(normalize(reflected), normalize(LmP)), sp), 0.0f, 1.0f);
+                const float sf = rust_clamp(powf_ref(falloff, sp), 0.0f, 1.0f);
+                const rgb specular{res * sf, res * sf, res * sf};
+                push(cadd(diffusion, specular));
+            }
+        }
+        if (have) {
+            for (uint32_t li = 0; li < p.nlights; ++li) {  // ambient lights (engine.rs:341-352)
+                const LightDesc L = light_desc(p, li);
+                if (L.variant != 1) continue;
+                const rgb m{rust_min(L.color[0], color.r), rust_min(L.color[1], color.g),
+                            rust_min(L.color[2], color.b)};
+                push(cmul(cmul(m, kd), L.brightness));
+            }
+            const size_t idx = (size_t)py * p.img_w + px;
+            if (p.out_rgb) {
+                float* o = p.out_rgb + 3 * idx;
+                o[0] = acc.r;
+                o[1] = acc.g;
+                o[2] = acc.b;
+            }
+            if (p.out_ppm) {  // Color::as_bytes, rows bottom-up (color.rs:31-37, image.rs:61-66)
+                uint8_t* o = p.out_ppm + 3 * ((size_t)(p.rows - 1 - py) * p.img_w + px);
+                o[0] = (uint8_t)sat_u8(acc.r * 255.0f);
+                o[1] = (uint8_t)sat_u8(acc.g * 255.0f);
+                o[2] = (uint8_t)sat_u8(acc.b * 255.0f);
+            }
         }
     }
 }
@@ -608,21 +710,31 @@ hipError_t launch_tri_cull(const TriHot* hot, uint32_t T, float cx, float cy, fl
 }
 
 hipError_t launch_render(const FrameParams& p, hipStream_t s) {
-    const uint32_t tiles_y = (p.rows + kTileH - 1) / kTileH;
+    const uint32_t tiles_y = (p.rows + kVisTileH - 1) / kVisTileH;
     const uint32_t blocks = p.tiles_x * tiles_y;
     if (!blocks) return hipSuccess;
     const bool lds = p.max_object_tris > kDirectMax;
     if (p.cull) {
         if (lds)
-            render_kernel<true, true><<<blocks, kWG, 0, s>>>(p);
+            visibility_kernel<true, true><<<blocks, kWG, 0, s>>>(p);
         else
-            render_kernel<true, false><<<blocks, kWG, 0, s>>>(p);
+            visibility_kernel<true, false><<<blocks, kWG, 0, s>>>(p);
     } else {
         if (lds)
-            render_kernel<false, true><<<blocks, kWG, 0, s>>>(p);
+            visibility_kernel<false, true><<<blocks, kWG, 0, s>>>(p);
         else
-            render_kernel<false, false><<<blocks, kWG, 0, s>>>(p);
+            visibility_kernel<false, false><<<blocks, kWG, 0, s>>>(p);
     }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // the shading grid strides over the queue; its length is only known on the device
+    const size_t max_hits = (size_t)p.rows * p.cam_w;
+    size_t sblocks = (max_hits + kWG - 1) / kWG;
+    if (sblocks > 1024) sblocks = 1024;
+    if (lds)
+        shade_kernel<true><<<(unsigned)sblocks, kWG, 0, s>>>(p);
+    else
+        shade_kernel<false><<<(unsigned)sblocks, kWG, 0, s>>>(p);
     return hipGetLastError();
 }
 
