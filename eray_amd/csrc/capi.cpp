@@ -55,7 +55,7 @@ struct eray_ctx {
     std::vector<LightDesc> h_lights;
     std::vector<float> h_raw;
     uint32_t total_tris = 0;
-    uint4* d_queue = nullptr;  // hit queue (2 x uint4 per pixel)
+    uint32_t* d_queue = nullptr;  // block queue (one entry per 64x4 pixel block)
     size_t queue_cap = 0;
     uint32_t* d_queue_count = nullptr;  // two parity counters
     uint32_t parity = 0;
@@ -491,13 +491,13 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     p.max_object_tris = 0;
     for (auto& o : ctx->objects) p.max_object_tris = o.T > p.max_object_tris ? o.T : p.max_object_tris;
     p.tiles_x = (W + 63) / 64;
-    const size_t need = 2 * (size_t)rp->rows * W;
+    const size_t need = (size_t)((W + 63) / 64) * ((rp->rows + 3) / 4);
     if (int st = ensure(ctx, &ctx->d_queue, &ctx->queue_cap, need)) return st;
     if (!ctx->d_queue_count) {
         HIP_TRY(ctx, hipMalloc((void**)&ctx->d_queue_count, 2 * sizeof(uint32_t)));
         HIP_TRY(ctx, hipMemsetAsync(ctx->d_queue_count, 0, 2 * sizeof(uint32_t), ctx->stream));
     }
-    p.queue = ctx->d_queue;
+    p.block_queue = ctx->d_queue;
     p.queue_count = ctx->d_queue_count;
     return ERAY_OK;
 }

@@ -82,8 +82,8 @@ struct FrameParams {
     uint32_t nobj, nlights;
     uint32_t max_object_tris;  // selects the kernel variant with LDS triangle tiles
     uint32_t tiles_x;  // pixel tiles per row
-    // hit queue between the visibility and shading passes: 2 x uint4 per hit
-    uint4* queue;
+    // queue of 64x4 pixel blocks that need pass 2 (block index = block_row * tiles_x + bx)
+    uint32_t* block_queue;
     uint32_t* queue_count;  // two counters; the frame uses [queue_parity]
     uint32_t queue_parity;
     ObjectDesc obj_inline[kInlineObjects];

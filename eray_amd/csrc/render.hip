@@ -371,213 +371,198 @@ __device__ __forceinline__ LightDesc light_desc(const FrameParams& p, uint32_t l
     return li < kInlineLights ? p.light_inline[li] : p.lights[li];
 }
 
-// ---------------------------------------------------------------------- visibility ----------
-// Pass 1 of a frame, over every pixel: the closest object's first hit of each camera ray
-// (cast_ray's object loop, engine.rs:119-126).  Each lane owns kVisR horizontally adjacent
-// pixels; a wave owns a 64 x 4 pixel block (its culling bundle), a workgroup 64 x 16.  Every
-// pixel gets the background colour (engine.rs:355-357) written with 16-byte stores; hit pixels
-// are appended to the hit queue and overwritten by the shading pass.
-constexpr int kVisR = 4;
-constexpr uint32_t kVisWaveW = 64, kVisWaveH = 4, kVisTileW = 64, kVisTileH = 16;
+// A frame runs in two passes over 64 x 4 pixel blocks.
+//
+// Pass 1, cull_fill_kernel (every pixel, 4 horizontally adjacent pixels per lane, one block per
+// wave): the wave culls every triangle of every object against its block's camera-ray bundle
+// (exact wave culling above).  Every pixel gets the background colour (engine.rs:355-357) and
+// face -1, written with 16-byte stores; blocks where some triangle survives are appended to a
+// block queue.  No exact test and no shading code lives here, so the kernel is light on
+// registers and runs at full occupancy: it is the HBM-write-bound part of the frame.
+//
+// Pass 2, detail_kernel (queued blocks only, one pixel per thread, one block per workgroup):
+// Engine::cast_ray for those pixels — lazy camera rays, exact first-hit search per object,
+// closest object, Material::get, shadow rays, lighting — overwriting the block's pixels.
+constexpr uint32_t kBlkW = 64, kBlkH = 4;  // pixel block: pass-1 wave bundle, pass-2 workgroup
+constexpr int kFillR = 4;                  // pass 1: pixels per lane
+constexpr uint32_t kSubW = 16;             // pass 2: each wave culls a 16 x 4 sub-block
+
+__device__ __forceinline__ Bundle make_bundle(const FrameParams& p, uint32_t x0, uint32_t xe,
+                                              uint32_t py0, uint32_t pye) {
+    // the pixel rectangle in viewport coordinates, widened to contain every pixel's x' = x/W and
+    // y' = y/H (approximate reciprocal, then 2^-20 outward; x', y' >= 0)
+    const float rw = __builtin_amdgcn_rcpf((float)p.cam_w), rh = __builtin_amdgcn_rcpf((float)p.cam_h);
+    const float lo = 1.0f - 0x1p-20f, hi = 1.0f + 0x1p-20f;
+    return Bundle{((float)x0 * rw) * lo, ((float)xe * rw) * hi, ((float)(p.row0 + py0) * rh) * lo,
+                  ((float)(p.row0 + pye) * rh) * hi};
+}
 
 template <bool kCull, bool kLdsTiles>
-__global__ void __launch_bounds__(kWG) visibility_kernel(FrameParams p) {
-    __shared__ TriHot s_hot[kLdsTiles ? kTriTile : 1];
+__global__ void __launch_bounds__(kWG) cull_fill_kernel(FrameParams p) {
     __shared__ TriCull s_cull[(kCull && kLdsTiles) ? kTriTile : 1];
-
-    const uint32_t tile = blockIdx.x;
-    const uint32_t tx = tile % p.tiles_x, ty = tile / p.tiles_x;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t wx0 = tx * kVisTileW, wy0 = ty * kVisTileH + wave * kVisWaveH;
-    const uint32_t px0 = wx0 + (lane & 15) * kVisR;
-    const uint32_t py = wy0 + (lane >> 4);  // local row (0 .. rows-1)
-    const uint32_t y = p.row0 + py;
-    const f3 C = mk3(p.cx, p.cy, p.cz);
-    bool valid[kVisR];
-#pragma unroll
-    for (int k = 0; k < kVisR; ++k) valid[k] = px0 + k < p.cam_w && py < p.rows;
-
-    Bundle bd;  // the wave's pixel block, widened to contain every pixel's x' = x/W, y' = y/H
-    {           // (approximate reciprocal, then 2^-20 outward; x', y' >= 0)
-        const uint32_t xe = min(wx0 + kVisWaveW - 1, p.cam_w ? p.cam_w - 1 : 0);
-        const uint32_t ye = p.row0 + min(wy0 + kVisWaveH - 1, p.rows ? p.rows - 1 : 0);
-        const float rw = __builtin_amdgcn_rcpf((float)p.cam_w), rh = __builtin_amdgcn_rcpf((float)p.cam_h);
-        const float lo = 1.0f - 0x1p-20f, hi = 1.0f + 0x1p-20f;
-        bd.xlo = ((float)wx0 * rw) * lo;
-        bd.xhi = ((float)xe * rw) * hi;
-        bd.ylo = ((float)(p.row0 + wy0) * rh) * lo;
-        bd.yhi = ((float)ye * rh) * hi;
-    }
-
-    // Camera rays are generated lazily: a wave whose block meets no candidate triangle of any
-    // object (most of the frame) never needs them.
-    f3 d[kVisR];
-#pragma unroll
-    for (int k = 0; k < kVisR; ++k) d[k] = mk3(0.0f, 0.0f, 0.0f);
-    bool ray_ready = false;
-
-    bool have[kVisR];
-    float closest[kVisR], bu[kVisR], bv[kVisR], bt[kVisR];
-    uint32_t best_obj[kVisR];
-    int best_face[kVisR];
-#pragma unroll
-    for (int k = 0; k < kVisR; ++k) {
-        have[k] = false;
-        closest[k] = bu[k] = bv[k] = bt[k] = 0.0f;
-        best_obj[k] = 0;
-        best_face[k] = -1;
-    }
-    for (uint32_t oi = 0; oi < p.nobj; ++oi) {
-        const ObjectDesc ob = object_desc(p, oi);  // uniform: scalar loads
-        auto activate = [&](bool (&a)[kVisR]) {
-            if (!ray_ready) {
-                // opaque to the optimiser: keeps ray generation on this (rare) path instead of
-                // being speculated into every wave
-                uint32_t pxo = px0, yo = y;
-                asm volatile("" : "+v"(pxo), "+v"(yo));
-#pragma unroll
-                for (int k = 0; k < kVisR; ++k) d[k] = camera_dir(p, pxo + k, yo);
-                ray_ready = true;
-            }
-#pragma unroll
-            for (int k = 0; k < kVisR; ++k) a[k] = bbox_hit(ob, C, d[k]);
-        };
-        int st[kVisR], f[kVisR];
-        float u[kVisR], v[kVisR], t[kVisR];
-#pragma unroll
-        for (int k = 0; k < kVisR; ++k) {
-            st[k] = valid[k] ? kUndecided : kDone;
-            f[k] = -1;
-        }
-        if (!kLdsTiles || ob.tri_count <= kDirectMax)
-            first_hit<kCull, false, kVisR>(p, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull,
-                                           activate, f, u, v, t);
-        else
-            first_hit<kCull, kLdsTiles, kVisR>(p, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot,
-                                               s_cull, activate, f, u, v, t);
-#pragma unroll
-        for (int k = 0; k < kVisR; ++k) {
-            if (f[k] >= 0) {
-                const f3 P = add(C, mul(d[k], t[k]));
-                const float dsq = len_sq(sub(P, C));
-                if (!have[k] || dsq < closest[k]) {  // strict `<`: first object wins ties
-                    have[k] = true;
-                    closest[k] = dsq;
-                    best_obj[k] = oi;
-                    best_face[k] = f[k];
-                    bu[k] = u[k];
-                    bv[k] = v[k];
-                    bt[k] = t[k];
+    const uint32_t bx = blockIdx.x % p.tiles_x;
+    const uint32_t by = (blockIdx.x / p.tiles_x) * (kWG / 64) + wave;  // block row of this wave
+    const uint32_t x0 = bx * kBlkW, py0 = by * kBlkH;
+    const bool blk_valid = py0 < p.rows;
+    const Bundle bd = make_bundle(p, x0, min(x0 + kBlkW - 1, p.cam_w - 1), py0,
+                                  min(py0 + kBlkH - 1, p.rows ? p.rows - 1 : 0));
+    bool need = !kCull && blk_valid;  // brute force: every block goes to pass 2
+    if (kCull) {
+        for (uint32_t oi = 0; oi < p.nobj; ++oi) {
+            const ObjectDesc ob = object_desc(p, oi);
+            if (!kLdsTiles || ob.tri_count <= kDirectMax) {
+                if (!blk_valid || need) continue;
+                for (uint32_t base = 0; base < ob.tri_count; base += 64) {
+                    const uint32_t j = base + lane;
+                    const bool keep = j < ob.tri_count &&
+                                      !cull_rejects(p.cull[ob.tri_begin + j], bd.xlo, bd.xhi, bd.ylo, bd.yhi);
+                    if (__ballot(keep)) {
+                        need = true;
+                        break;
+                    }
+                }
+            } else {
+                for (uint32_t base = 0; base < ob.tri_count; base += kTriTile) {
+                    if (!__syncthreads_or(blk_valid && !need)) break;
+                    const uint32_t n = min((uint32_t)kTriTile, ob.tri_count - base);
+                    if (threadIdx.x < n) s_cull[threadIdx.x] = p.cull[ob.tri_begin + base + threadIdx.x];
+                    __syncthreads();
+                    if (blk_valid && !need) {
+                        for (uint32_t c = 0; c < n; c += 64) {
+                            const uint32_t j = c + lane;
+                            const bool keep = j < n && !cull_rejects(s_cull[j], bd.xlo, bd.xhi, bd.ylo, bd.yhi);
+                            if (__ballot(keep)) {
+                                need = true;
+                                break;
+                            }
+                        }
+                    }
                 }
             }
         }
     }
 
-    // ---- background for every pixel (sat_u8(0.1*255), sat_u8(0.2*255) = 25, 51) ----------
+    // ---- background and face -1 for every pixel (sat_u8(0.1*255) = 25, sat_u8(0.2*255) = 51)
+    const uint32_t px0 = x0 + (lane & 15) * kFillR;
+    const uint32_t py = py0 + (lane >> 4);
     const float b01 = 0.1f, b02 = 0.2f;
     const uint32_t c01 = sat_u8(b01 * 255.0f), c02 = sat_u8(b02 * 255.0f);
-    const bool all_valid = valid[0] && valid[kVisR - 1];
     const size_t idx0 = (size_t)py * p.img_w + px0;
     const size_t prow = (size_t)(p.rows - 1 - py);  // PPM byte row of this camera row
-    if (all_valid && (p.img_w % 4) == 0 &&
-        ((reinterpret_cast<uintptr_t>(p.out_rgb) | reinterpret_cast<uintptr_t>(p.out_face)) & 15) == 0 &&
-        (reinterpret_cast<uintptr_t>(p.out_ppm) & 3) == 0) {
-        if (p.out_rgb) {  // 4 pixels = 12 floats = 3 x 16 B
-            float4* o = reinterpret_cast<float4*>(p.out_rgb + 3 * idx0);
-            o[0] = make_float4(b01, b01, b02, b01);
-            o[1] = make_float4(b01, b02, b01, b01);
-            o[2] = make_float4(b02, b01, b01, b02);
-        }
-        if (p.out_ppm) {  // 4 pixels = 12 bytes
-            const uint32_t w0 = c01 | (c01 << 8) | (c02 << 16) | (c01 << 24);
-            const uint32_t w1 = c01 | (c02 << 8) | (c01 << 16) | (c01 << 24);
-            const uint32_t w2 = c02 | (c01 << 8) | (c01 << 16) | (c02 << 24);
-            uint32_t* o = reinterpret_cast<uint32_t*>(p.out_ppm + 3 * (prow * p.img_w + px0));
-            o[0] = w0;
-            o[1] = w1;
-            o[2] = w2;
-        }
-        if (p.out_face)
-            *reinterpret_cast<int4*>(p.out_face + idx0) = make_int4(best_face[0], best_face[1], best_face[2], best_face[3]);
-    } else {
-#pragma unroll
-        for (int k = 0; k < kVisR; ++k) {
-            if (!valid[k]) continue;
-            if (p.out_rgb) {
-                float* o = p.out_rgb + 3 * (idx0 + k);
-                o[0] = b01;
-                o[1] = b01;
-                o[2] = b02;
+    if (py < p.rows) {
+        if (px0 + kFillR <= p.cam_w && (p.img_w % 4) == 0 &&
+            ((reinterpret_cast<uintptr_t>(p.out_rgb) | reinterpret_cast<uintptr_t>(p.out_face)) & 15) == 0 &&
+            (reinterpret_cast<uintptr_t>(p.out_ppm) & 3) == 0) {
+            if (p.out_rgb) {  // 4 pixels = 12 floats = 3 x 16 B
+                float4* o = reinterpret_cast<float4*>(p.out_rgb + 3 * idx0);
+                o[0] = make_float4(b01, b01, b02, b01);
+                o[1] = make_float4(b01, b02, b01, b01);
+                o[2] = make_float4(b02, b01, b01, b02);
             }
-            if (p.out_ppm) {
-                uint8_t* o = p.out_ppm + 3 * (prow * p.img_w + px0 + k);
-                o[0] = (uint8_t)c01;
-                o[1] = (uint8_t)c01;
-                o[2] = (uint8_t)c02;
+            if (p.out_ppm) {  // 4 pixels = 12 bytes
+                uint32_t* o = reinterpret_cast<uint32_t*>(p.out_ppm + 3 * (prow * p.img_w + px0));
+                o[0] = c01 | (c01 << 8) | (c02 << 16) | (c01 << 24);
+                o[1] = c01 | (c02 << 8) | (c01 << 16) | (c01 << 24);
+                o[2] = c02 | (c01 << 8) | (c01 << 16) | (c02 << 24);
             }
-            if (p.out_face) p.out_face[idx0 + k] = best_face[k];
+            if (p.out_face) *reinterpret_cast<int4*>(p.out_face + idx0) = make_int4(-1, -1, -1, -1);
+        } else {
+            for (int k = 0; k < kFillR; ++k) {
+                if (px0 + k >= p.cam_w) break;
+                if (p.out_rgb) {
+                    float* o = p.out_rgb + 3 * (idx0 + k);
+                    o[0] = b01;
+                    o[1] = b01;
+                    o[2] = b02;
+                }
+                if (p.out_ppm) {
+                    uint8_t* o = p.out_ppm + 3 * (prow * p.img_w + px0 + k);
+                    o[0] = (uint8_t)c01;
+                    o[1] = (uint8_t)c01;
+                    o[2] = (uint8_t)c02;
+                }
+                if (p.out_face) p.out_face[idx0 + k] = -1;
+            }
         }
     }
-
-    // ---- append the hits to the queue (one atomic per wave) --------------------------------
-    unsigned long long m[kVisR];
-    uint32_t total = 0;
-#pragma unroll
-    for (int k = 0; k < kVisR; ++k) {
-        m[k] = __ballot(have[k]);
-        total += (uint32_t)__popcll(m[k]);
-    }
-    if (total) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(p.queue_count + p.queue_parity, total);
-        base = __shfl(base, 0);
-        const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-#pragma unroll
-        for (int k = 0; k < kVisR; ++k) {
-            if (have[k]) {
-                const uint32_t slot = base + (uint32_t)__popcll(m[k] & below);
-                p.queue[2 * (size_t)slot] = make_uint4(px0 + k, py, best_obj[k], (uint32_t)best_face[k]);
-                p.queue[2 * (size_t)slot + 1] =
-                    make_uint4(__float_as_uint(bu[k]), __float_as_uint(bv[k]), __float_as_uint(bt[k]), 0u);
-            }
-            base += (uint32_t)__popcll(m[k]);
-        }
+    if (need && lane == 0) {
+        const uint32_t slot = atomicAdd(p.queue_count + p.queue_parity, 1u);
+        p.block_queue[slot] = by * p.tiles_x + bx;
     }
 }
 
-// ---------------------------------------------------------------------- shading -------------
-// Pass 2: one thread per queued hit — hit data, Material::get (material.rs:56-94), shadow rays
-// (reaches_light, engine.rs:218-228), diffuse + specular + ambient (engine.rs:128-208), the
-// left-fold sum (color.rs:82-87) — then the pixel's f32 RGB and PPM bytes.  The grid strides
-// over the queue; block 0 clears the other parity's counter for the next frame.
-template <bool kLdsTiles>
-__global__ void __launch_bounds__(kWG) shade_kernel(FrameParams p) {
+template <bool kCull, bool kLdsTiles>
+__global__ void __launch_bounds__(kWG) detail_kernel(FrameParams p) {
     __shared__ TriHot s_hot[kLdsTiles ? kTriTile : 1];
-    __shared__ TriCull s_cull[1];
-    const uint32_t n = __hip_atomic_load(p.queue_count + p.queue_parity, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-    if (blockIdx.x == 0 && threadIdx.x == 0) p.queue_count[p.queue_parity ^ 1u] = 0u;
+    __shared__ TriCull s_cull[(kCull && kLdsTiles) ? kTriTile : 1];
+    __shared__ float4 s_rgb[kBlkW * kBlkH * 3 / 4];      // each wave's f32 RGB rows, staged
+    __shared__ uint32_t s_ppm[kBlkW * kBlkH * 3 / 4];    // ... and its PPM byte rows
+    const uint32_t nq = __hip_atomic_load(p.queue_count + p.queue_parity, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x == 0 && threadIdx.x == 0) p.queue_count[p.queue_parity ^ 1u] = 0u;  // next frame's
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const f3 C = mk3(p.cx, p.cy, p.cz);
-    const Bundle bd{0.0f, 0.0f, 0.0f, 0.0f};
-    for (uint32_t base = blockIdx.x * kWG; base < n; base += gridDim.x * kWG) {
-        const uint32_t i = base + threadIdx.x;
-        const bool have = i < n;
-        uint4 e0 = make_uint4(0u, 0u, 0u, 0u), e1 = e0;
-        if (have) {
-            e0 = p.queue[2 * (size_t)i];
-            e1 = p.queue[2 * (size_t)i + 1];
-        }
-        const uint32_t px = e0.x, py = e0.y, oi = e0.z, face = e0.w;
-        const float bu = __uint_as_float(e1.x), bv = __uint_as_float(e1.y), bt = __uint_as_float(e1.z);
-        const f3 d = camera_dir(p, px, p.row0 + py);  // the same f32 ray as the visibility pass
+    for (uint32_t q = blockIdx.x; q < nq; q += gridDim.x) {
+        const uint32_t blk = p.block_queue[q];
+        const uint32_t bx = blk % p.tiles_x, by = blk / p.tiles_x;
+        const uint32_t wx0 = bx * kBlkW + wave * kSubW, py0 = by * kBlkH;
+        const uint32_t px = wx0 + (lane % kSubW), ly = lane / kSubW;
+        const uint32_t py = py0 + ly;
+        const bool valid = px < p.cam_w && py < p.rows;
+        const uint32_t y = p.row0 + py;
+        const Bundle bd = make_bundle(p, wx0, min(wx0 + kSubW - 1, p.cam_w - 1), py0,
+                                      min(py0 + kBlkH - 1, p.rows - 1));
 
+        // ---- cast_ray (engine.rs:112-216): closest object among first hits ---------------
+        f3 d[1] = {mk3(0.0f, 0.0f, 0.0f)};
+        bool ray_ready = false;
+        bool have = false;
+        float closest = 0.0f, bu = 0.0f, bv = 0.0f, bt = 0.0f;
+        uint32_t best_obj = 0;
+        int best_face = -1;
+        for (uint32_t oi = 0; oi < p.nobj; ++oi) {
+            const ObjectDesc ob = object_desc(p, oi);  // uniform: scalar loads
+            auto activate = [&](bool (&a)[1]) {
+                if (!ray_ready) {
+                    uint32_t pxo = px, yo = y;  // opaque: keep ray generation on this path
+                    asm volatile("" : "+v"(pxo), "+v"(yo));
+                    d[0] = camera_dir(p, pxo, yo);
+                    ray_ready = true;
+                }
+                a[0] = bbox_hit(ob, C, d[0]);
+            };
+            int st[1] = {valid ? kUndecided : kDone}, f[1] = {-1};
+            float u[1], v[1], t[1];
+            if (!kLdsTiles || ob.tri_count <= kDirectMax)
+                first_hit<kCull, false, 1>(p, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull,
+                                           activate, f, u, v, t);
+            else
+                first_hit<kCull, kLdsTiles, 1>(p, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot,
+                                               s_cull, activate, f, u, v, t);
+            if (f[0] >= 0) {
+                const f3 P = add(C, mul(d[0], t[0]));
+                const float dsq = len_sq(sub(P, C));
+                if (!have || dsq < closest) {  // strict `<`: the first object wins ties
+                    have = true;
+                    closest = dsq;
+                    best_obj = oi;
+                    best_face = f[0];
+                    bu = u[0];
+                    bv = v[0];
+                    bt = t[0];
+                }
+            }
+        }
+
+        // ---- hit data and Material::get (material.rs:56-94) ------------------------------
         f3 P = mk3(0.0f, 0.0f, 0.0f), N = mk3(0.0f, 0.0f, 0.0f);
         rgb color{0.0f, 0.0f, 0.0f};
         float kd = 0.5f, ks = 0.5f, sp = 1.0f;
         if (have) {
-            const ObjectDesc ob = p.objects[oi];
-            const TriShade sh = p.shade[ob.tri_begin + face];
-            P = add(C, mul(d, bt));
+            const ObjectDesc ob = p.objects[best_obj];
+            const TriShade sh = p.shade[ob.tri_begin + (uint32_t)best_face];
+            P = add(C, mul(d[0], bt));
             const f3 na = mk3(sh.s0.x, sh.s0.y, sh.s0.z), nb = mk3(sh.s0.w, sh.s1.x, sh.s1.y);
             const f3 nc = mk3(sh.s1.z, sh.s1.w, sh.s2.x);
             N = normalize(add(add(mul(na, bu), mul(nb, bv)), mul(nc, bt)));
@@ -596,7 +581,7 @@ __global__ void __launch_bounds__(kWG) shade_kernel(FrameParams p) {
             tex_value(ob.mat.specular_power, uv0, uv1, sp);
         }
 
-        bool any = false;  // the lighting list as a running left fold
+        bool any = false;  // the lighting list as a running left fold (color.rs:82-87)
         rgb acc{0.0f, 0.0f, 0.0f};
         auto push = [&](rgb c) {
             if (any) {
@@ -645,7 +630,7 @@ __global__ void __launch_bounds__(kWG) shade_kernel(FrameParams p) {
                 const float falloff = 1.0f / len(LmP);
                 const rgb lc{L.color[0], L.color[1], L.color[2]};
                 const rgb diffusion = cmul(cmul(cmul(cmul(cmulc(color, lc), kd), prod), L.brightness), falloff);
-                const f3 reflected = sub(d, mul(mul(N, 2.0f), dot0(d, N)));
+                const f3 reflected = sub(d[0], mul(mul(N, 2.0f), dot0(d[0], N)));
                 const float res = rust_clamp(
                     ks * L.brightness * powf_ref(dot0(normalize(reflected), normalize(LmP)), sp), 0.0f, 1.0f);
                 const float sf = rust_clamp(powf_ref(falloff, sp), 0.0f, 1.0f);
@@ -661,6 +646,46 @@ __global__ void __launch_bounds__(kWG) shade_kernel(FrameParams p) {
                             rust_min(L.color[2], color.b)};
                 push(cmul(cmul(m, kd), L.brightness));
             }
+        } else {
+            push(rgb{0.1f, 0.1f, 0.2f});  // engine.rs:355-357
+        }
+
+        // ---- outputs: Image::set + Color::as_bytes, rows bottom-up (image.rs:41-74) -------
+        const uint32_t b0 = sat_u8(acc.r * 255.0f), b1 = sat_u8(acc.g * 255.0f), b2 = sat_u8(acc.b * 255.0f);
+        if (valid && p.out_face) p.out_face[(size_t)py * p.img_w + px] = have ? best_face : -1;
+        const bool full = wx0 + kSubW <= p.cam_w && py0 + kBlkH <= p.rows && (p.img_w % 16) == 0 &&
+                          ((reinterpret_cast<uintptr_t>(p.out_rgb) | reinterpret_cast<uintptr_t>(p.out_ppm)) & 15) == 0;
+        if (full) {  // the wave's 16 x 4 pixels leave through its own LDS slice as 16-B row stores
+            constexpr uint32_t kWavePix = kSubW * kBlkH;
+            float* wrgb = reinterpret_cast<float*>(s_rgb) + 3 * kWavePix * wave;
+            uint8_t* wppm = reinterpret_cast<uint8_t*>(s_ppm) + 3 * kWavePix * wave;
+            const uint32_t wl = lane % kSubW;
+            float* srgb = wrgb + 3 * (ly * kSubW + wl);
+            srgb[0] = acc.r;
+            srgb[1] = acc.g;
+            srgb[2] = acc.b;
+            uint8_t* sppm = wppm + 3 * ((kBlkH - 1 - ly) * kSubW + wl);
+            sppm[0] = (uint8_t)b0;
+            sppm[1] = (uint8_t)b1;
+            sppm[2] = (uint8_t)b2;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            constexpr uint32_t kRgbRow4 = kSubW * 3 / 4;    // float4 per wave row (12)
+            constexpr uint32_t kPpmRow16 = kSubW * 3 / 16;  // 16-byte words per wave row (3)
+            if (p.out_rgb && lane < kBlkH * kRgbRow4) {
+                const uint32_t r = lane / kRgbRow4, c = lane % kRgbRow4;
+                float4* dst = reinterpret_cast<float4*>(p.out_rgb + 3 * ((size_t)(py0 + r) * p.img_w + wx0)) + c;
+                *dst = reinterpret_cast<const float4*>(wrgb)[lane];
+            }
+            if (p.out_ppm && lane < kBlkH * kPpmRow16) {
+                const uint32_t r = lane / kPpmRow16, c = lane % kPpmRow16;  // r-th byte row of the block
+                const size_t row = (size_t)(p.rows - py0 - kBlkH + r);
+                uint4* dst = reinterpret_cast<uint4*>(p.out_ppm + 3 * (row * p.img_w + wx0)) + c;
+                *dst = reinterpret_cast<const uint4*>(wppm)[lane];
+            }
+            __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next queued block
+        } else if (valid) {
             const size_t idx = (size_t)py * p.img_w + px;
             if (p.out_rgb) {
                 float* o = p.out_rgb + 3 * idx;
@@ -668,11 +693,11 @@ __global__ void __launch_bounds__(kWG) shade_kernel(FrameParams p) {
                 o[1] = acc.g;
                 o[2] = acc.b;
             }
-            if (p.out_ppm) {  // Color::as_bytes, rows bottom-up (color.rs:31-37, image.rs:61-66)
+            if (p.out_ppm) {
                 uint8_t* o = p.out_ppm + 3 * ((size_t)(p.rows - 1 - py) * p.img_w + px);
-                o[0] = (uint8_t)sat_u8(acc.r * 255.0f);
-                o[1] = (uint8_t)sat_u8(acc.g * 255.0f);
-                o[2] = (uint8_t)sat_u8(acc.b * 255.0f);
+                o[0] = (uint8_t)b0;
+                o[1] = (uint8_t)b1;
+                o[2] = (uint8_t)b2;
             }
         }
     }
@@ -710,31 +735,37 @@ hipError_t launch_tri_cull(const TriHot* hot, uint32_t T, float cx, float cy, fl
 }
 
 hipError_t launch_render(const FrameParams& p, hipStream_t s) {
-    const uint32_t tiles_y = (p.rows + kVisTileH - 1) / kVisTileH;
-    const uint32_t blocks = p.tiles_x * tiles_y;
-    if (!blocks) return hipSuccess;
+    const uint32_t block_rows = (p.rows + kBlkH - 1) / kBlkH;
+    const uint32_t wgs = p.tiles_x * ((block_rows + (kWG / 64) - 1) / (kWG / 64));
+    if (!wgs) return hipSuccess;
     const bool lds = p.max_object_tris > kDirectMax;
     if (p.cull) {
         if (lds)
-            visibility_kernel<true, true><<<blocks, kWG, 0, s>>>(p);
+            cull_fill_kernel<true, true><<<wgs, kWG, 0, s>>>(p);
         else
-            visibility_kernel<true, false><<<blocks, kWG, 0, s>>>(p);
+            cull_fill_kernel<true, false><<<wgs, kWG, 0, s>>>(p);
     } else {
         if (lds)
-            visibility_kernel<false, true><<<blocks, kWG, 0, s>>>(p);
+            cull_fill_kernel<false, true><<<wgs, kWG, 0, s>>>(p);
         else
-            visibility_kernel<false, false><<<blocks, kWG, 0, s>>>(p);
+            cull_fill_kernel<false, false><<<wgs, kWG, 0, s>>>(p);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    // the shading grid strides over the queue; its length is only known on the device
-    const size_t max_hits = (size_t)p.rows * p.cam_w;
-    size_t sblocks = (max_hits + kWG - 1) / kWG;
-    if (sblocks > 1024) sblocks = 1024;
-    if (lds)
-        shade_kernel<true><<<(unsigned)sblocks, kWG, 0, s>>>(p);
-    else
-        shade_kernel<false><<<(unsigned)sblocks, kWG, 0, s>>>(p);
+    // pass 2 strides over the block queue, whose length is only known on the device
+    uint32_t dgrid = p.tiles_x * block_rows;
+    if (dgrid > 2048) dgrid = 2048;
+    if (p.cull) {
+        if (lds)
+            detail_kernel<true, true><<<dgrid, kWG, 0, s>>>(p);
+        else
+            detail_kernel<true, false><<<dgrid, kWG, 0, s>>>(p);
+    } else {
+        if (lds)
+            detail_kernel<false, true><<<dgrid, kWG, 0, s>>>(p);
+        else
+            detail_kernel<false, false><<<dgrid, kWG, 0, s>>>(p);
+    }
     return hipGetLastError();
 }
 
