@@ -55,10 +55,6 @@ struct eray_ctx {
     std::vector<LightDesc> h_lights;
     std::vector<float> h_raw;
     uint32_t total_tris = 0;
-    uint32_t* d_queue = nullptr;  // block queue (one entry per 64x4 pixel block)
-    size_t queue_cap = 0;
-    uint32_t* d_queue_count = nullptr;  // two parity counters
-    uint32_t parity = 0;
 };
 
 namespace {
@@ -162,10 +158,17 @@ int sync_scene(eray_ctx* ctx, bool need_cull) {
     if (ctx->desc_dirty) {
         ctx->h_objs.clear();
         uint32_t begin = 0;
+        uint32_t cache_used = 0;
         for (auto& o : ctx->objects) {
             ObjectDesc d{};
             d.tri_begin = begin;
             d.tri_count = o.T;
+            // small objects' culling records are cached in LDS by the frame kernel (512 max)
+            d.cache_off = kNotCached;
+            if (o.T && o.T <= 256 && cache_used + o.T <= 512) {
+                d.cache_off = cache_used;
+                cache_used += o.T;
+            }
             for (int k = 0; k < 3; ++k) {
                 d.bb_lo[k] = o.lo[k];
                 d.bb_hi[k] = o.hi[k];
@@ -240,8 +243,7 @@ int eray_ctx_destroy(eray_ctx* ctx) {
     if (!ctx) return ERAY_OK;
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
-    void* bufs[] = {ctx->d_hot, ctx->d_shade, ctx->d_cull, ctx->d_raw, ctx->d_objs, ctx->d_lights,
-                    ctx->d_queue, ctx->d_queue_count};
+    void* bufs[] = {ctx->d_hot, ctx->d_shade, ctx->d_cull, ctx->d_raw, ctx->d_objs, ctx->d_lights};
     for (void* b : bufs)
         if (b) hipFree(b);
     if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
@@ -491,23 +493,10 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     p.max_object_tris = 0;
     for (auto& o : ctx->objects) p.max_object_tris = o.T > p.max_object_tris ? o.T : p.max_object_tris;
     p.tiles_x = (W + 63) / 64;
-    const size_t need = (size_t)((W + 63) / 64) * ((rp->rows + 3) / 4);
-    if (int st = ensure(ctx, &ctx->d_queue, &ctx->queue_cap, need)) return st;
-    if (!ctx->d_queue_count) {
-        HIP_TRY(ctx, hipMalloc((void**)&ctx->d_queue_count, 2 * sizeof(uint32_t)));
-        HIP_TRY(ctx, hipMemsetAsync(ctx->d_queue_count, 0, 2 * sizeof(uint32_t), ctx->stream));
-    }
-    p.block_queue = ctx->d_queue;
-    p.queue_count = ctx->d_queue_count;
     return ERAY_OK;
 }
 
-// one frame = visibility + shading; the queue parity alternates per frame
-hipError_t launch_frame(eray_ctx* ctx, FrameParams& p) {
-    p.queue_parity = ctx->parity;
-    ctx->parity ^= 1u;
-    return launch_render(p, ctx->stream);
-}
+hipError_t launch_frame(eray_ctx* ctx, FrameParams& p) { return launch_render(p, ctx->stream); }
 }  // namespace
 
 int eray_render(eray_ctx* ctx, const eray_render_params* rp) {

@@ -43,8 +43,11 @@ struct MaterialDesc {
     TexView diffuse, specular, specular_power, reflection;  // IValue
 };
 
+constexpr uint32_t kNotCached = 0xffffffffu;
+
 struct ObjectDesc {
     uint32_t tri_begin, tri_count;
+    uint32_t cache_off;  // offset of its culling records in the LDS cache, or kNotCached
     float bb_lo[3], bb_hi[3];
     MaterialDesc mat;
 };
@@ -82,10 +85,6 @@ struct FrameParams {
     uint32_t nobj, nlights;
     uint32_t max_object_tris;  // selects the kernel variant with LDS triangle tiles
     uint32_t tiles_x;  // pixel tiles per row
-    // queue of 64x4 pixel blocks that need pass 2 (block index = block_row * tiles_x + bx)
-    uint32_t* block_queue;
-    uint32_t* queue_count;  // two counters; the frame uses [queue_parity]
-    uint32_t queue_parity;
     ObjectDesc obj_inline[kInlineObjects];
     LightDesc light_inline[kInlineLights];
 };

@@ -241,6 +241,8 @@ constexpr int kUndecided = 0, kSearching = 1, kDone = 2;
 // straight from global memory / the scalar cache, no LDS, no barrier); larger ones go through
 // workgroup-shared LDS tiles.
 constexpr uint32_t kDirectMax = 256;
+// Culling records of small objects are cached in LDS once per workgroup, up to this many.
+constexpr uint32_t kCullCache = 512;
 
 // First-hit search over triangles [begin, begin + count) for R rays per lane (Object::intersects'
 // face loop, object.rs:63-78).  Rays still kUndecided when the wave meets its first candidate
@@ -251,7 +253,8 @@ template <bool kCull, bool kLds, int R, typename Activate>
 __device__ void first_hit(const FrameParams& p, uint32_t begin, uint32_t count, int (&st)[R],
                           const f3& o, const f3 (&d)[R], const Bundle& bd, TriHot* s_hot,
                           TriCull* s_cull, Activate&& activate, int (&found)[R], float (&hu)[R],
-                          float (&hv)[R], float (&ht)[R]) {
+                          float (&hv)[R], float (&ht)[R], const TriCull* s_cache = nullptr,
+                          uint32_t cache_off = kNotCached) {
     const uint32_t lane = threadIdx.x & 63;
     auto any_state = [&](int s) {
         bool a = false;
@@ -297,7 +300,12 @@ __device__ void first_hit(const FrameParams& p, uint32_t begin, uint32_t count, 
             unsigned long long mask;
             if (kCull) {
                 const uint32_t j = base + lane;
-                mask = __ballot(j < count && !cull_rejects(p.cull[begin + j], bd.xlo, bd.xhi, bd.ylo, bd.yhi));
+                bool keep = false;
+                if (j < count) {
+                    const TriCull c = cache_off != kNotCached ? s_cache[cache_off + j] : p.cull[begin + j];
+                    keep = !cull_rejects(c, bd.xlo, bd.xhi, bd.ylo, bd.yhi);
+                }
+                mask = __ballot(keep);
             } else {
                 const uint32_t n = min(64u, count - base);
                 mask = n == 64 ? ~0ull : ((1ull << n) - 1ull);
@@ -371,21 +379,16 @@ __device__ __forceinline__ LightDesc light_desc(const FrameParams& p, uint32_t l
     return li < kInlineLights ? p.light_inline[li] : p.lights[li];
 }
 
-// A frame runs in two passes over 64 x 4 pixel blocks.
-//
-// Pass 1, cull_fill_kernel (every pixel, 4 horizontally adjacent pixels per lane, one block per
-// wave): the wave culls every triangle of every object against its block's camera-ray bundle
-// (exact wave culling above).  Every pixel gets the background colour (engine.rs:355-357) and
-// face -1, written with 16-byte stores; blocks where some triangle survives are appended to a
-// block queue.  No exact test and no shading code lives here, so the kernel is light on
-// registers and runs at full occupancy: it is the HBM-write-bound part of the frame.
-//
-// Pass 2, detail_kernel (queued blocks only, one pixel per thread, one block per workgroup):
-// Engine::cast_ray for those pixels — lazy camera rays, exact first-hit search per object,
-// closest object, Material::get, shadow rays, lighting — overwriting the block's pixels.
-constexpr uint32_t kBlkW = 64, kBlkH = 4;  // pixel block: pass-1 wave bundle, pass-2 workgroup
-constexpr int kFillR = 4;                  // pass 1: pixels per lane
-constexpr uint32_t kSubW = 16;             // pass 2: each wave culls a 16 x 4 sub-block
+// The frame kernel.  The image is cut into 64 x 4 pixel blocks; a persistent grid of
+// workgroups strides over them and each wave of a workgroup takes a 16 x 4 sub-block (one pixel
+// per lane, the wave's culling bundle).  Small objects' culling records are cached in LDS once
+// per workgroup.  A sub-block where no triangle survives the cull (most of a frame) costs a few
+// LDS reads and one wave-contiguous 16-byte store per output row — the frame is bound by its
+// HBM writes — while sub-blocks with candidates run Engine::cast_ray in full (lazy camera
+// rays, exact first hits, closest object, Material::get, shadow rays, lighting) in the same
+// launch, overlapping the stores of the others.
+constexpr uint32_t kBlkW = 64, kBlkH = 4;  // pixel block: one workgroup iteration
+constexpr uint32_t kSubW = 16;             // each wave: a 16 x 4 sub-block
 
 __device__ __forceinline__ Bundle make_bundle(const FrameParams& p, uint32_t x0, uint32_t xe,
                                               uint32_t py0, uint32_t pye) {
@@ -398,119 +401,38 @@ __device__ __forceinline__ Bundle make_bundle(const FrameParams& p, uint32_t x0,
 }
 
 template <bool kCull, bool kLdsTiles>
-__global__ void __launch_bounds__(kWG) cull_fill_kernel(FrameParams p) {
-    __shared__ TriCull s_cull[(kCull && kLdsTiles) ? kTriTile : 1];
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t bx = blockIdx.x % p.tiles_x;
-    const uint32_t by = (blockIdx.x / p.tiles_x) * (kWG / 64) + wave;  // block row of this wave
-    const uint32_t x0 = bx * kBlkW, py0 = by * kBlkH;
-    const bool blk_valid = py0 < p.rows;
-    const Bundle bd = make_bundle(p, x0, min(x0 + kBlkW - 1, p.cam_w - 1), py0,
-                                  min(py0 + kBlkH - 1, p.rows ? p.rows - 1 : 0));
-    bool need = !kCull && blk_valid;  // brute force: every block goes to pass 2
-    if (kCull) {
-        for (uint32_t oi = 0; oi < p.nobj; ++oi) {
-            const ObjectDesc ob = object_desc(p, oi);
-            if (!kLdsTiles || ob.tri_count <= kDirectMax) {
-                if (!blk_valid || need) continue;
-                for (uint32_t base = 0; base < ob.tri_count; base += 64) {
-                    const uint32_t j = base + lane;
-                    const bool keep = j < ob.tri_count &&
-                                      !cull_rejects(p.cull[ob.tri_begin + j], bd.xlo, bd.xhi, bd.ylo, bd.yhi);
-                    if (__ballot(keep)) {
-                        need = true;
-                        break;
-                    }
-                }
-            } else {
-                for (uint32_t base = 0; base < ob.tri_count; base += kTriTile) {
-                    if (!__syncthreads_or(blk_valid && !need)) break;
-                    const uint32_t n = min((uint32_t)kTriTile, ob.tri_count - base);
-                    if (threadIdx.x < n) s_cull[threadIdx.x] = p.cull[ob.tri_begin + base + threadIdx.x];
-                    __syncthreads();
-                    if (blk_valid && !need) {
-                        for (uint32_t c = 0; c < n; c += 64) {
-                            const uint32_t j = c + lane;
-                            const bool keep = j < n && !cull_rejects(s_cull[j], bd.xlo, bd.xhi, bd.ylo, bd.yhi);
-                            if (__ballot(keep)) {
-                                need = true;
-                                break;
-                            }
-                        }
-                    }
-                }
-            }
-        }
-    }
-
-    // ---- background and face -1 for every pixel (sat_u8(0.1*255) = 25, sat_u8(0.2*255) = 51)
-    const uint32_t px0 = x0 + (lane & 15) * kFillR;
-    const uint32_t py = py0 + (lane >> 4);
-    const float b01 = 0.1f, b02 = 0.2f;
-    const uint32_t c01 = sat_u8(b01 * 255.0f), c02 = sat_u8(b02 * 255.0f);
-    const size_t idx0 = (size_t)py * p.img_w + px0;
-    const size_t prow = (size_t)(p.rows - 1 - py);  // PPM byte row of this camera row
-    if (py < p.rows) {
-        if (px0 + kFillR <= p.cam_w && (p.img_w % 4) == 0 &&
-            ((reinterpret_cast<uintptr_t>(p.out_rgb) | reinterpret_cast<uintptr_t>(p.out_face)) & 15) == 0 &&
-            (reinterpret_cast<uintptr_t>(p.out_ppm) & 3) == 0) {
-            if (p.out_rgb) {  // 4 pixels = 12 floats = 3 x 16 B
-                float4* o = reinterpret_cast<float4*>(p.out_rgb + 3 * idx0);
-                o[0] = make_float4(b01, b01, b02, b01);
-                o[1] = make_float4(b01, b02, b01, b01);
-                o[2] = make_float4(b02, b01, b01, b02);
-            }
-            if (p.out_ppm) {  // 4 pixels = 12 bytes
-                uint32_t* o = reinterpret_cast<uint32_t*>(p.out_ppm + 3 * (prow * p.img_w + px0));
-                o[0] = c01 | (c01 << 8) | (c02 << 16) | (c01 << 24);
-                o[1] = c01 | (c02 << 8) | (c01 << 16) | (c01 << 24);
-                o[2] = c02 | (c01 << 8) | (c01 << 16) | (c02 << 24);
-            }
-            if (p.out_face) *reinterpret_cast<int4*>(p.out_face + idx0) = make_int4(-1, -1, -1, -1);
-        } else {
-            for (int k = 0; k < kFillR; ++k) {
-                if (px0 + k >= p.cam_w) break;
-                if (p.out_rgb) {
-                    float* o = p.out_rgb + 3 * (idx0 + k);
-                    o[0] = b01;
-                    o[1] = b01;
-                    o[2] = b02;
-                }
-                if (p.out_ppm) {
-                    uint8_t* o = p.out_ppm + 3 * (prow * p.img_w + px0 + k);
-                    o[0] = (uint8_t)c01;
-                    o[1] = (uint8_t)c01;
-                    o[2] = (uint8_t)c02;
-                }
-                if (p.out_face) p.out_face[idx0 + k] = -1;
-            }
-        }
-    }
-    if (need && lane == 0) {
-        const uint32_t slot = atomicAdd(p.queue_count + p.queue_parity, 1u);
-        p.block_queue[slot] = by * p.tiles_x + bx;
-    }
-}
-
-template <bool kCull, bool kLdsTiles>
-__global__ void __launch_bounds__(kWG) detail_kernel(FrameParams p) {
+__global__ void __launch_bounds__(kWG) frame_kernel(FrameParams p) {
     __shared__ TriHot s_hot[kLdsTiles ? kTriTile : 1];
     __shared__ TriCull s_cull[(kCull && kLdsTiles) ? kTriTile : 1];
-    __shared__ float4 s_rgb[kBlkW * kBlkH * 3 / 4];      // each wave's f32 RGB rows, staged
-    __shared__ uint32_t s_ppm[kBlkW * kBlkH * 3 / 4];    // ... and its PPM byte rows
-    const uint32_t nq = __hip_atomic_load(p.queue_count + p.queue_parity, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-    if (blockIdx.x == 0 && threadIdx.x == 0) p.queue_count[p.queue_parity ^ 1u] = 0u;  // next frame's
+    __shared__ TriCull s_cache[kCull ? kCullCache : 1];
+    __shared__ float4 s_rgb[kBlkW * kBlkH * 3 / 4];    // each wave's f32 RGB rows, staged
+    __shared__ uint32_t s_ppm[kBlkW * kBlkH * 3 / 4];  // ... and its PPM byte rows
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const f3 C = mk3(p.cx, p.cy, p.cz);
-    for (uint32_t q = blockIdx.x; q < nq; q += gridDim.x) {
-        const uint32_t blk = p.block_queue[q];
+
+    if (kCull) {  // cache the small objects' culling records
+        for (uint32_t oi = 0; oi < p.nobj; ++oi) {
+            const ObjectDesc ob = object_desc(p, oi);
+            if (ob.cache_off == kNotCached) continue;
+            for (uint32_t i = threadIdx.x; i < ob.tri_count; i += kWG) s_cache[ob.cache_off + i] = p.cull[ob.tri_begin + i];
+        }
+        __syncthreads();
+    }
+
+    // background (engine.rs:355-357) and its bytes: sat_u8(0.1*255) = 25, sat_u8(0.2*255) = 51
+    const float b01 = 0.1f, b02 = 0.2f;
+    const uint32_t c01 = sat_u8(b01 * 255.0f), c02 = sat_u8(b02 * 255.0f);
+
+    const uint32_t block_rows = (p.rows + kBlkH - 1) / kBlkH;
+    const uint32_t nblk = p.tiles_x * block_rows;
+    for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
         const uint32_t bx = blk % p.tiles_x, by = blk / p.tiles_x;
         const uint32_t wx0 = bx * kBlkW + wave * kSubW, py0 = by * kBlkH;
         const uint32_t px = wx0 + (lane % kSubW), ly = lane / kSubW;
         const uint32_t py = py0 + ly;
         const bool valid = px < p.cam_w && py < p.rows;
         const uint32_t y = p.row0 + py;
+        const bool wave_live = wx0 < p.cam_w;
         const Bundle bd = make_bundle(p, wx0, min(wx0 + kSubW - 1, p.cam_w - 1), py0,
                                       min(py0 + kBlkH - 1, p.rows - 1));
 
@@ -536,7 +458,7 @@ __global__ void __launch_bounds__(kWG) detail_kernel(FrameParams p) {
             float u[1], v[1], t[1];
             if (!kLdsTiles || ob.tri_count <= kDirectMax)
                 first_hit<kCull, false, 1>(p, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull,
-                                           activate, f, u, v, t);
+                                           activate, f, u, v, t, s_cache, kCull ? ob.cache_off : kNotCached);
             else
                 first_hit<kCull, kLdsTiles, 1>(p, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot,
                                                s_cull, activate, f, u, v, t);
@@ -553,6 +475,53 @@ __global__ void __launch_bounds__(kWG) detail_kernel(FrameParams p) {
                     bt = t[0];
                 }
             }
+        }
+
+        const bool full = wave_live && wx0 + kSubW <= p.cam_w && py0 + kBlkH <= p.rows && (p.img_w % 16) == 0 &&
+                          ((reinterpret_cast<uintptr_t>(p.out_rgb) | reinterpret_cast<uintptr_t>(p.out_ppm) |
+                            reinterpret_cast<uintptr_t>(p.out_face)) & 15) == 0;
+        if (!__any(have)) {
+            // ---- no hit in the sub-block: background, 16-byte stores along each row ---------
+            if (full) {
+                constexpr uint32_t kRgbRow4 = kSubW * 3 / 4;    // 12 float4 per row
+                constexpr uint32_t kPpmRow16 = kSubW * 3 / 16;  // 3 x 16 B per row
+                if (p.out_rgb && lane < kBlkH * kRgbRow4) {
+                    const uint32_t r = lane / kRgbRow4, c = lane % kRgbRow4, ph = c % 3;
+                    const float4 v = ph == 0 ? make_float4(b01, b01, b02, b01)
+                                             : ph == 1 ? make_float4(b01, b02, b01, b01) : make_float4(b02, b01, b01, b02);
+                    reinterpret_cast<float4*>(p.out_rgb + 3 * ((size_t)(py0 + r) * p.img_w + wx0))[c] = v;
+                }
+                if (p.out_ppm && lane < kBlkH * kPpmRow16) {
+                    const uint32_t r = lane / kPpmRow16, c = lane % kPpmRow16, ph = c % 3;
+                    const uint32_t w0 = c01 | (c01 << 8) | (c02 << 16) | (c01 << 24);  // bytes 25 25 51 25
+                    const uint32_t w1 = c01 | (c02 << 8) | (c01 << 16) | (c01 << 24);  // 25 51 25 25
+                    const uint32_t w2 = c02 | (c01 << 8) | (c01 << 16) | (c02 << 24);  // 51 25 25 51
+                    const uint4 v = ph == 0 ? make_uint4(w0, w1, w2, w0)
+                                            : ph == 1 ? make_uint4(w1, w2, w0, w1) : make_uint4(w2, w0, w1, w2);
+                    const size_t row = (size_t)(p.rows - py0 - kBlkH + r);
+                    reinterpret_cast<uint4*>(p.out_ppm + 3 * (row * p.img_w + wx0))[c] = v;
+                }
+                if (p.out_face && lane < kBlkH * (kSubW / 4)) {
+                    const uint32_t r = lane / (kSubW / 4), c = lane % (kSubW / 4);
+                    reinterpret_cast<int4*>(p.out_face + (size_t)(py0 + r) * p.img_w + wx0)[c] = make_int4(-1, -1, -1, -1);
+                }
+            } else if (valid) {
+                const size_t idx = (size_t)py * p.img_w + px;
+                if (p.out_rgb) {
+                    float* o = p.out_rgb + 3 * idx;
+                    o[0] = b01;
+                    o[1] = b01;
+                    o[2] = b02;
+                }
+                if (p.out_ppm) {
+                    uint8_t* o = p.out_ppm + 3 * ((size_t)(p.rows - 1 - py) * p.img_w + px);
+                    o[0] = (uint8_t)c01;
+                    o[1] = (uint8_t)c01;
+                    o[2] = (uint8_t)c02;
+                }
+                if (p.out_face) p.out_face[idx] = -1;
+            }
+            continue;
         }
 
         // ---- hit data and Material::get (material.rs:56-94) ------------------------------
@@ -647,14 +616,12 @@ __global__ void __launch_bounds__(kWG) detail_kernel(FrameParams p) {
                 push(cmul(cmul(m, kd), L.brightness));
             }
         } else {
-            push(rgb{0.1f, 0.1f, 0.2f});  // engine.rs:355-357
+            push(rgb{b01, b01, b02});  // engine.rs:355-357
         }
 
         // ---- outputs: Image::set + Color::as_bytes, rows bottom-up (image.rs:41-74) -------
         const uint32_t b0 = sat_u8(acc.r * 255.0f), b1 = sat_u8(acc.g * 255.0f), b2 = sat_u8(acc.b * 255.0f);
         if (valid && p.out_face) p.out_face[(size_t)py * p.img_w + px] = have ? best_face : -1;
-        const bool full = wx0 + kSubW <= p.cam_w && py0 + kBlkH <= p.rows && (p.img_w % 16) == 0 &&
-                          ((reinterpret_cast<uintptr_t>(p.out_rgb) | reinterpret_cast<uintptr_t>(p.out_ppm)) & 15) == 0;
         if (full) {  // the wave's 16 x 4 pixels leave through its own LDS slice as 16-B row stores
             constexpr uint32_t kWavePix = kSubW * kBlkH;
             float* wrgb = reinterpret_cast<float*>(s_rgb) + 3 * kWavePix * wave;
@@ -684,7 +651,9 @@ __global__ void __launch_bounds__(kWG) detail_kernel(FrameParams p) {
                 uint4* dst = reinterpret_cast<uint4*>(p.out_ppm + 3 * (row * p.img_w + wx0)) + c;
                 *dst = reinterpret_cast<const uint4*>(wppm)[lane];
             }
-            __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next queued block
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next sub-block
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         } else if (valid) {
             const size_t idx = (size_t)py * p.img_w + px;
             if (p.out_rgb) {
@@ -734,39 +703,32 @@ hipError_t launch_tri_cull(const TriHot* hot, uint32_t T, float cx, float cy, fl
     return hipGetLastError();
 }
 
-hipError_t launch_render(const FrameParams& p, hipStream_t s) {
-    const uint32_t block_rows = (p.rows + kBlkH - 1) / kBlkH;
-    const uint32_t wgs = p.tiles_x * ((block_rows + (kWG / 64) - 1) / (kWG / 64));
-    if (!wgs) return hipSuccess;
-    const bool lds = p.max_object_tris > kDirectMax;
-    if (p.cull) {
-        if (lds)
-            cull_fill_kernel<true, true><<<wgs, kWG, 0, s>>>(p);
-        else
-            cull_fill_kernel<true, false><<<wgs, kWG, 0, s>>>(p);
-    } else {
-        if (lds)
-            cull_fill_kernel<false, true><<<wgs, kWG, 0, s>>>(p);
-        else
-            cull_fill_kernel<false, false><<<wgs, kWG, 0, s>>>(p);
+// Persistent grid: as many workgroups as can be resident (occupancy query x CUs), never more
+// than there are pixel blocks.  No inter-workgroup synchronisation, so residency only affects
+// speed.
+template <bool kCull, bool kLdsTiles>
+static hipError_t launch_frame_kernel(const FrameParams& p, uint32_t nblk, hipStream_t s) {
+    static int resident = 0;
+    if (!resident) {
+        int dev = 0, cus = 0, per_cu = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e == hipSuccess)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, frame_kernel<kCull, kLdsTiles>, kWG, 0);
+        if (e != hipSuccess) return e;
+        resident = (per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 1);
     }
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    // pass 2 strides over the block queue, whose length is only known on the device
-    uint32_t dgrid = p.tiles_x * block_rows;
-    if (dgrid > 2048) dgrid = 2048;
-    if (p.cull) {
-        if (lds)
-            detail_kernel<true, true><<<dgrid, kWG, 0, s>>>(p);
-        else
-            detail_kernel<true, false><<<dgrid, kWG, 0, s>>>(p);
-    } else {
-        if (lds)
-            detail_kernel<false, true><<<dgrid, kWG, 0, s>>>(p);
-        else
-            detail_kernel<false, false><<<dgrid, kWG, 0, s>>>(p);
-    }
+    const uint32_t grid = nblk < (uint32_t)resident ? nblk : (uint32_t)resident;
+    frame_kernel<kCull, kLdsTiles><<<grid, kWG, 0, s>>>(p);
     return hipGetLastError();
+}
+
+hipError_t launch_render(const FrameParams& p, hipStream_t s) {
+    const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
+    if (!nblk) return hipSuccess;
+    const bool lds = p.max_object_tris > kDirectMax;
+    if (p.cull) return lds ? launch_frame_kernel<true, true>(p, nblk, s) : launch_frame_kernel<true, false>(p, nblk, s);
+    return lds ? launch_frame_kernel<false, true>(p, nblk, s) : launch_frame_kernel<false, false>(p, nblk, s);
 }
 
 hipError_t launch_pack_ppm(const float* rgb, uint32_t w, uint32_t h, uint8_t* out, hipStream_t s) {
