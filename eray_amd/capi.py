@@ -104,6 +104,7 @@ SIGNATURES = {
     "eray_camera_size": (C.c_int, [C.POINTER(Camera), C.POINTER(_U), C.POINTER(_U)]),
     "eray_render": (C.c_int, [_P, C.POINTER(RenderParams)]),
     "eray_render_frames": (C.c_int, [_P, C.POINTER(RenderParams), _U, C.POINTER(C.c_float)]),
+    "eray_render_prepare": (C.c_int, [_P, C.POINTER(RenderParams), _U]),
     "eray_pack_ppm": (C.c_int, [_P, _P, _U, _U, _P]),
     "eray_ppm_header": (C.c_int, [_U, _U, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
 }
@@ -320,12 +321,16 @@ class Context:
         self._check(lib().eray_render(self._h, C.byref(p)))
 
     def render_frames(self, frames, image_width, image_height, row0=0, rows=None, out_rgb=None,
-                      out_ppm=None, out_face=None, flags=RENDER_DEFAULT, timed=False):
-        """`frames` back-to-back renders; returns the mean kernel ms when `timed`."""
+                      out_ppm=None, out_face=None, flags=RENDER_DEFAULT, timed=False, prepare_only=False):
+        """`frames` back-to-back renders (replayed from a cached HIP graph); returns the mean
+        device ms per frame when `timed`.  `prepare_only` builds the launch plan and returns."""
         if rows is None:
             rows = image_height - row0
         p = RenderParams(image_width, image_height, row0, rows, 0, 0, out_rgb or None, out_ppm or None,
                          out_face or None, flags)
+        if prepare_only:
+            self._check(lib().eray_render_prepare(self._h, C.byref(p), frames))
+            return None
         ms = C.c_float()
         self._check(lib().eray_render_frames(self._h, C.byref(p), frames, C.byref(ms) if timed else None))
         return ms.value if timed else None

@@ -51,10 +51,20 @@ struct eray_ctx {
     size_t objs_cap = 0;
     LightDesc* d_lights = nullptr;
     size_t lights_cap = 0;
+    // launch plan of eray_render_frames: a HIP graph of kGraphFrames frame launches, cached
+    // for the frame parameters + stream it was captured with
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t graph_exec = nullptr;
+    std::vector<unsigned char> graph_key;
+    uint32_t* d_rect = nullptr;  // per-object pixel-rectangle accumulators (4 x uint32)
+    size_t rect_cap = 0;
+    std::vector<uint32_t> h_rect;
     std::vector<ObjectDesc> h_objs;  // kept alive for the async uploads
     std::vector<LightDesc> h_lights;
     std::vector<float> h_raw;
     uint32_t total_tris = 0;
+    uint32_t cached_tris = 0;  // triangles of small objects whose records live in LDS per frame
+    bool spec_pow = false;     // some material has a specular-power output
 };
 
 namespace {
@@ -159,13 +169,16 @@ int sync_scene(eray_ctx* ctx, bool need_cull) {
         ctx->h_objs.clear();
         uint32_t begin = 0;
         uint32_t cache_used = 0;
+        ctx->spec_pow = false;
         for (auto& o : ctx->objects) {
             ObjectDesc d{};
             d.tri_begin = begin;
             d.tri_count = o.T;
-            // small objects' culling records are cached in LDS by the frame kernel (512 max)
+            d.rect[0] = d.rect[2] = 0;  // every pixel until the culling pass computes it
+            d.rect[1] = d.rect[3] = INT32_MAX;
+            // small objects' records are cached in LDS by the frame kernels (kCacheTris max)
             d.cache_off = kNotCached;
-            if (o.T && o.T <= 256 && cache_used + o.T <= 512) {
+            if (o.T && cache_used + o.T <= kCacheTris) {
                 d.cache_off = cache_used;
                 cache_used += o.T;
             }
@@ -176,8 +189,10 @@ int sync_scene(eray_ctx* ctx, bool need_cull) {
             d.mat = MaterialDesc{tex(o.mat.color), tex(o.mat.diffuse), tex(o.mat.specular),
                                  tex(o.mat.specular_power), tex(o.mat.reflection)};
             ctx->h_objs.push_back(d);
+            ctx->spec_pow |= o.mat.specular_power.data != nullptr;
             begin += o.T;
         }
+        ctx->cached_tris = cache_used;
         ctx->h_lights.clear();
         for (auto& l : ctx->lights) {
             LightDesc d{};
@@ -199,11 +214,45 @@ int sync_scene(eray_ctx* ctx, bool need_cull) {
                                         sizeof(LightDesc) * ctx->h_lights.size(), hipMemcpyHostToDevice,
                                         ctx->stream));
         ctx->desc_dirty = false;
+        ctx->cull_dirty = true;  // the rectangles live in the descriptors just rebuilt
     }
     if (need_cull && ctx->cull_dirty) {
         const eray_camera& c = ctx->camera;
         HIP_TRY(ctx, launch_tri_cull(ctx->d_hot, ctx->total_tris, c.center[0], c.center[1], c.center[2],
                                      c.fov[0] / c.fov[1], c.z_dist, ctx->d_cull, ctx->stream));
+        // each object's pixel rectangle (where its faces can be hit by a primary ray), read back
+        // once per camera / geometry change and carried in the object descriptors
+        const size_t nobj = ctx->objects.size();
+        uint32_t W, H;
+        eray_camera_size(&c, &W, &H);
+        if (nobj) {
+            if ((st = ensure(ctx, &ctx->d_rect, &ctx->rect_cap, 4 * nobj))) return st;
+            HIP_TRY(ctx, hipMemsetAsync(ctx->d_rect, 0, sizeof(uint32_t) * 4 * nobj, ctx->stream));
+            for (size_t i = 0; i < nobj; ++i)
+                HIP_TRY(ctx, launch_tri_rect(ctx->d_cull + ctx->h_objs[i].tri_begin, ctx->h_objs[i].tri_count, W, H,
+                                             ctx->d_rect + 4 * i, ctx->stream));
+            ctx->h_rect.assign(4 * nobj, 0u);
+            HIP_TRY(ctx, hipMemcpyAsync(ctx->h_rect.data(), ctx->d_rect, sizeof(uint32_t) * 4 * nobj,
+                                        hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            for (size_t i = 0; i < nobj; ++i) {
+                const uint32_t* a = &ctx->h_rect[4 * i];
+                int32_t* r = ctx->h_objs[i].rect;
+                if (a[1] == 0) {  // no face can be hit
+                    r[0] = 1;
+                    r[1] = 0;
+                    r[2] = 1;
+                    r[3] = 0;
+                } else {
+                    r[0] = (int32_t)~a[0];
+                    r[1] = (int32_t)a[1] - 1;
+                    r[2] = (int32_t)~a[2];
+                    r[3] = (int32_t)a[3] - 1;
+                }
+            }
+            HIP_TRY(ctx, hipMemcpyAsync(ctx->d_objs, ctx->h_objs.data(), sizeof(ObjectDesc) * nobj,
+                                        hipMemcpyHostToDevice, ctx->stream));
+        }
         ctx->cull_dirty = false;
     }
     return ERAY_OK;
@@ -243,9 +292,11 @@ int eray_ctx_destroy(eray_ctx* ctx) {
     if (!ctx) return ERAY_OK;
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
-    void* bufs[] = {ctx->d_hot, ctx->d_shade, ctx->d_cull, ctx->d_raw, ctx->d_objs, ctx->d_lights};
+    void* bufs[] = {ctx->d_hot, ctx->d_shade, ctx->d_cull, ctx->d_raw, ctx->d_objs, ctx->d_lights, ctx->d_rect};
     for (void* b : bufs)
         if (b) hipFree(b);
+    if (ctx->graph_exec) hipGraphExecDestroy(ctx->graph_exec);
+    if (ctx->graph) hipGraphDestroy(ctx->graph);
     if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
     delete ctx;
     return ERAY_OK;
@@ -465,7 +516,7 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     if (*empty) return ERAY_OK;
 
     FrameParams& p = *out;
-    p = FrameParams{};
+    std::memset(&p, 0, sizeof p);  // padding too: the launch-plan cache compares the bytes
     const eray_camera& c = ctx->camera;
     p.cx = c.center[0];
     p.cy = c.center[1];
@@ -492,6 +543,8 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     for (size_t i = 0; i < ctx->h_lights.size() && i < (size_t)kInlineLights; ++i) p.light_inline[i] = ctx->h_lights[i];
     p.max_object_tris = 0;
     for (auto& o : ctx->objects) p.max_object_tris = o.T > p.max_object_tris ? o.T : p.max_object_tris;
+    p.cached_tris = ctx->cached_tris;
+    p.spec_pow = ctx->spec_pow ? 1u : 0u;
     p.tiles_x = (W + 63) / 64;
     return ERAY_OK;
 }
@@ -507,46 +560,90 @@ int eray_render(eray_ctx* ctx, const eray_render_params* rp) {
     return ERAY_OK;
 }
 
-int eray_render_frames(eray_ctx* ctx, const eray_render_params* rp, uint32_t frames,
-                       float* mean_kernel_ms) {
+namespace {
+constexpr uint32_t kGraphFrames = 64;
+
+// (Re)builds the cached graph of min(frames, kGraphFrames) back-to-back frame launches.
+// Returns the graph's frame count, 0 when the plain launch path must be used.
+int ensure_plan(eray_ctx* ctx, const FrameParams& p, uint32_t frames, uint32_t* chunk) {
+    *chunk = 0;
+    if (!ctx->stream || frames < 2) return ERAY_OK;  // the null stream cannot be captured
+    const uint32_t n = frames < kGraphFrames ? frames : kGraphFrames;
+    std::vector<unsigned char> key(sizeof p + sizeof n + sizeof ctx->stream);
+    std::memcpy(key.data(), &p, sizeof p);
+    std::memcpy(key.data() + sizeof p, &n, sizeof n);
+    std::memcpy(key.data() + sizeof p + sizeof n, &ctx->stream, sizeof ctx->stream);
+    if (ctx->graph_exec && key == ctx->graph_key) {
+        *chunk = n;
+        return ERAY_OK;
+    }
+    if (ctx->graph_exec) hipGraphExecDestroy(ctx->graph_exec);
+    if (ctx->graph) hipGraphDestroy(ctx->graph);
+    ctx->graph_exec = nullptr;
+    ctx->graph = nullptr;
+    ctx->graph_key.clear();
+    HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+    hipError_t e = hipSuccess;
+    for (uint32_t f = 0; f < n && e == hipSuccess; ++f) e = launch_render(p, ctx->stream);
+    hipGraph_t g = nullptr;
+    const hipError_t e2 = hipStreamEndCapture(ctx->stream, &g);
+    if (e == hipSuccess) e = e2;
+    if (e == hipSuccess) e = hipGraphInstantiate(&ctx->graph_exec, g, nullptr, nullptr, 0);
+    if (e != hipSuccess) {
+        if (g) hipGraphDestroy(g);
+        ctx->graph_exec = nullptr;
+        return set_error(ctx, ERAY_E_HIP, "frame graph capture: %s", hipGetErrorString(e));
+    }
+    ctx->graph = g;
+    ctx->graph_key = std::move(key);
+    *chunk = n;
+    return ERAY_OK;
+}
+}  // namespace
+
+int eray_render_prepare(eray_ctx* ctx, const eray_render_params* rp, uint32_t frames) {
     FrameParams p;
     bool empty = false;
     if (int st = prepare_render(ctx, rp, &p, &empty)) return st;
-    if (mean_kernel_ms) *mean_kernel_ms = 0.0f;
+    uint32_t chunk;
+    return empty ? ERAY_OK : ensure_plan(ctx, p, frames, &chunk);
+}
+
+int eray_render_frames(eray_ctx* ctx, const eray_render_params* rp, uint32_t frames,
+                       float* mean_frame_ms) {
+    FrameParams p;
+    bool empty = false;
+    if (int st = prepare_render(ctx, rp, &p, &empty)) return st;
+    if (mean_frame_ms) *mean_frame_ms = 0.0f;
     if (empty || !frames) return ERAY_OK;
-    if (!mean_kernel_ms) {
-        for (uint32_t f = 0; f < frames; ++f) HIP_TRY(ctx, launch_frame(ctx, p));
-        return ERAY_OK;
-    }
-    std::vector<hipEvent_t> ev(2 * (size_t)frames, nullptr);
-    int st = ERAY_OK;
-    for (auto& e : ev) {
-        hipError_t he = hipEventCreate(&e);
-        if (he != hipSuccess) {
-            st = set_error(ctx, ERAY_E_HIP, "hipEventCreate: %s", hipGetErrorString(he));
-            break;
+    uint32_t chunk = 0;
+    if (int st = ensure_plan(ctx, p, frames, &chunk)) return st;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    if (mean_frame_ms) {
+        for (auto& e : ev) {
+            hipError_t he = hipEventCreate(&e);
+            if (he != hipSuccess) {
+                if (ev[0]) hipEventDestroy(ev[0]);
+                return set_error(ctx, ERAY_E_HIP, "hipEventCreate: %s", hipGetErrorString(he));
+            }
         }
     }
-    for (uint32_t f = 0; f < frames && st == ERAY_OK; ++f) {
-        hipError_t he = hipEventRecord(ev[2 * f], ctx->stream);
-        if (he == hipSuccess) he = launch_frame(ctx, p);
-        if (he == hipSuccess) he = hipEventRecord(ev[2 * f + 1], ctx->stream);
-        if (he != hipSuccess) st = set_error(ctx, ERAY_E_HIP, "render loop: %s", hipGetErrorString(he));
-    }
-    double total = 0.0;
-    if (st == ERAY_OK) {
-        hipError_t he = hipStreamSynchronize(ctx->stream);
-        for (uint32_t f = 0; f < frames && he == hipSuccess; ++f) {
-            float ms = 0.0f;
-            he = hipEventElapsedTime(&ms, ev[2 * f], ev[2 * f + 1]);
-            total += ms;
-        }
-        if (he != hipSuccess) st = set_error(ctx, ERAY_E_HIP, "render timing: %s", hipGetErrorString(he));
+    hipError_t he = mean_frame_ms ? hipEventRecord(ev[0], ctx->stream) : hipSuccess;
+    uint32_t done = 0;
+    for (; chunk && done + chunk <= frames && he == hipSuccess; done += chunk)
+        he = hipGraphLaunch(ctx->graph_exec, ctx->stream);
+    for (; done < frames && he == hipSuccess; ++done) he = launch_frame(ctx, p);
+    if (mean_frame_ms && he == hipSuccess) {
+        he = hipEventRecord(ev[1], ctx->stream);
+        if (he == hipSuccess) he = hipEventSynchronize(ev[1]);
+        float ms = 0.0f;
+        if (he == hipSuccess) he = hipEventElapsedTime(&ms, ev[0], ev[1]);
+        if (he == hipSuccess) *mean_frame_ms = ms / (float)frames;
     }
     for (auto e : ev)
         if (e) hipEventDestroy(e);
-    if (st == ERAY_OK) *mean_kernel_ms = (float)(total / frames);
-    return st;
+    if (he != hipSuccess) return set_error(ctx, ERAY_E_HIP, "render loop: %s", hipGetErrorString(he));
+    return ERAY_OK;
 }
 
 int eray_pack_ppm(eray_ctx* ctx, const float* rgb, uint32_t w, uint32_t h, uint8_t* out) {

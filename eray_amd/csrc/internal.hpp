@@ -44,10 +44,14 @@ struct MaterialDesc {
 };
 
 constexpr uint32_t kNotCached = 0xffffffffu;
+constexpr uint32_t kCacheTris = 256;  // LDS record cache capacity of the frame kernels (triangles)
 
 struct ObjectDesc {
     uint32_t tri_begin, tri_count;
-    uint32_t cache_off;  // offset of its culling records in the LDS cache, or kNotCached
+    uint32_t cache_off;  // offset of its records in the frame kernels' LDS cache, or kNotCached
+    // Camera pixels whose primary ray can hit the object: x0..x1 x y0..y1 (inclusive, camera
+    // rows), from the culling records (tri_rect_kernel); empty when x0 > x1.
+    int32_t rect[4];
     float bb_lo[3], bb_hi[3];
     MaterialDesc mat;
 };
@@ -84,6 +88,8 @@ struct FrameParams {
     const LightDesc* lights;
     uint32_t nobj, nlights;
     uint32_t max_object_tris;  // selects the kernel variant with LDS triangle tiles
+    uint32_t cached_tris;      // triangles whose records the frame kernels cache in LDS
+    uint32_t spec_pow;         // some material has a specular-power output (powf != identity)
     uint32_t tiles_x;  // pixel tiles per row
     ObjectDesc obj_inline[kInlineObjects];
     LightDesc light_inline[kInlineLights];
@@ -94,6 +100,10 @@ hipError_t launch_tri_precompute(const float* pos, const float* nrm, const float
                                  TriHot* hot, TriShade* shade, hipStream_t s);
 hipError_t launch_tri_cull(const TriHot* hot, uint32_t T, float cx, float cy, float cz, float ratio,
                            float z_dist, TriCull* cull, hipStream_t s);
+// Per-object pixel rectangle accumulator: 4 uint32 per object, zeroed before the launch, all
+// updated by atomicMax: (~x0, x1 + 1, ~y0, y1 + 1); a1 == 0 means empty.
+hipError_t launch_tri_rect(const TriCull* cull, uint32_t T, uint32_t cam_w, uint32_t cam_h,
+                           uint32_t* acc, hipStream_t s);
 hipError_t launch_render(const FrameParams& p, hipStream_t s);
 hipError_t launch_pack_ppm(const float* rgb, uint32_t w, uint32_t h, uint8_t* out, hipStream_t s);
 

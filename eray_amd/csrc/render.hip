@@ -172,6 +172,81 @@ __global__ void __launch_bounds__(256) tri_cull_kernel(const TriHot* __restrict_
     cull[i].T = make_float4(Tt[0], Tt[1], Tt[2], Tt[3]);
 }
 
+// ------------------------------------------------------------- object pixel rectangle ------
+// The culling records also bound where a face can be hit at all: condition k can only pass at
+// viewport points with K_k + A_k x' + B_k y' >= -T_k (x' = x / W, y' = y / H, camera_dir).
+// Clipping the viewport square by the four half-planes (double precision; each relaxed by 1e-9
+// of its magnitude, far above the clip's rounding, so the computed polygon contains the exact
+// one) and widening its bounding box by 2 pixels (covers the f32 rounding of x/W, y/H) gives a
+// conservative pixel rectangle per face.  The object's rectangle is the union: no primary ray
+// outside it can hit the object, so those pixels need no test for it.
+__device__ bool face_rect(const TriCull& c, uint32_t W, uint32_t H, int32_t (&r)[4]) {
+    const float A[4] = {c.A.x, c.A.y, c.A.z, c.A.w}, B[4] = {c.B.x, c.B.y, c.B.z, c.B.w};
+    const float K[4] = {c.K.x, c.K.y, c.K.z, c.K.w}, T[4] = {c.T.x, c.T.y, c.T.z, c.T.w};
+    double px[12] = {0.0, 1.0, 1.0, 0.0}, py[12] = {0.0, 0.0, 1.0, 1.0}, qx[12], qy[12];
+    int n = 4;
+    for (int k = 0; k < 4; ++k) {
+        if (T[k] == __builtin_inff()) continue;  // condition disabled (non-finite record)
+        if (!(T[k] > -__builtin_inff())) return false;  // the face rejects every camera ray
+        const double a = A[k], b = B[k];
+        const double mag = fabs((double)K[k]) + fabs(a) + fabs(b) + fabs((double)T[k]);
+        const double cc = (double)K[k] + (double)T[k] + 1e-9 * mag + 1e-300;
+        int m = 0;
+        for (int i = 0; i < n; ++i) {
+            const int j = i + 1 == n ? 0 : i + 1;
+            const double fi = a * px[i] + b * py[i] + cc, fj = a * px[j] + b * py[j] + cc;
+            if (fi >= 0.0) {
+                qx[m] = px[i];
+                qy[m] = py[i];
+                ++m;
+            }
+            if ((fi >= 0.0) != (fj >= 0.0)) {
+                double t = fi / (fi - fj);
+                t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
+                qx[m] = px[i] + t * (px[j] - px[i]);
+                qy[m] = py[i] + t * (py[j] - py[i]);
+                ++m;
+            }
+        }
+        n = m;
+        if (!n) return false;
+        for (int i = 0; i < n; ++i) {
+            px[i] = qx[i];
+            py[i] = qy[i];
+        }
+    }
+    double xmin = px[0], xmax = px[0], ymin = py[0], ymax = py[0];
+    for (int i = 1; i < n; ++i) {
+        xmin = fmin(xmin, px[i]);
+        xmax = fmax(xmax, px[i]);
+        ymin = fmin(ymin, py[i]);
+        ymax = fmax(ymax, py[i]);
+    }
+    r[0] = max((int32_t)floor(xmin * W) - 2, 0);
+    r[1] = min((int32_t)ceil(xmax * W) + 2, (int32_t)W - 1);
+    r[2] = max((int32_t)floor(ymin * H) - 2, 0);
+    r[3] = min((int32_t)ceil(ymax * H) + 2, (int32_t)H - 1);
+    return r[0] <= r[1] && r[2] <= r[3];
+}
+
+__global__ void __launch_bounds__(256) tri_rect_kernel(const TriCull* __restrict__ cull, uint32_t T,
+                                                       uint32_t W, uint32_t H, uint32_t* __restrict__ acc) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t a[4] = {0u, 0u, 0u, 0u};
+    int32_t r[4];
+    if (i < T && face_rect(cull[i], W, H, r)) {
+        a[0] = ~(uint32_t)r[0];
+        a[1] = (uint32_t)r[1] + 1u;
+        a[2] = ~(uint32_t)r[2];
+        a[3] = (uint32_t)r[3] + 1u;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        for (int off = 32; off > 0; off >>= 1) a[k] = max(a[k], (uint32_t)__shfl_xor((int)a[k], off));
+    if ((threadIdx.x & 63) == 0 && a[1])
+        for (int k = 0; k < 4; ++k) atomicMax(acc + k, a[k]);
+}
+
 // true when condition k fails for every pixel of [xlo,xhi] x [ylo,yhi]
 __device__ __forceinline__ bool cull_one(float A, float B, float K, float T, float xlo, float xhi,
                                          float ylo, float yhi) {
@@ -241,8 +316,7 @@ constexpr int kUndecided = 0, kSearching = 1, kDone = 2;
 // straight from global memory / the scalar cache, no LDS, no barrier); larger ones go through
 // workgroup-shared LDS tiles.
 constexpr uint32_t kDirectMax = 256;
-// Culling records of small objects are cached in LDS once per workgroup, up to this many.
-constexpr uint32_t kCullCache = 512;
+// Records of small objects are cached in LDS once per workgroup, up to this many triangles.
 
 // First-hit search over triangles [begin, begin + count) for R rays per lane (Object::intersects'
 // face loop, object.rs:63-78).  Rays still kUndecided when the wave meets its first candidate
@@ -254,7 +328,7 @@ __device__ void first_hit(const FrameParams& p, uint32_t begin, uint32_t count, 
                           const f3& o, const f3 (&d)[R], const Bundle& bd, TriHot* s_hot,
                           TriCull* s_cull, Activate&& activate, int (&found)[R], float (&hu)[R],
                           float (&hv)[R], float (&ht)[R], const TriCull* s_cache = nullptr,
-                          uint32_t cache_off = kNotCached) {
+                          uint32_t cache_off = kNotCached, const TriHot* s_hot_cache = nullptr) {
     const uint32_t lane = threadIdx.x & 63;
     auto any_state = [&](int s) {
         bool a = false;
@@ -315,7 +389,8 @@ __device__ void first_hit(const FrameParams& p, uint32_t begin, uint32_t count, 
             while (mask) {
                 const uint32_t bit = (uint32_t)(__ffsll(mask) - 1);
                 mask &= mask - 1;
-                test(p.tris[begin + base + bit], base + bit);
+                test(cache_off != kNotCached ? s_hot_cache[cache_off + base + bit] : p.tris[begin + base + bit],
+                     base + bit);
                 if (!any_state(kSearching)) return;
             }
         }
@@ -379,16 +454,45 @@ __device__ __forceinline__ LightDesc light_desc(const FrameParams& p, uint32_t l
     return li < kInlineLights ? p.light_inline[li] : p.lights[li];
 }
 
-// The frame kernel.  The image is cut into 64 x 4 pixel blocks; a persistent grid of
-// workgroups strides over them and each wave of a workgroup takes a 16 x 4 sub-block (one pixel
-// per lane, the wave's culling bundle).  Small objects' culling records are cached in LDS once
-// per workgroup.  A sub-block where no triangle survives the cull (most of a frame) costs a few
-// LDS reads and one wave-contiguous 16-byte store per output row — the frame is bound by its
-// HBM writes — while sub-blocks with candidates run Engine::cast_ray in full (lazy camera
-// rays, exact first hits, closest object, Material::get, shadow rays, lighting) in the same
-// launch, overlapping the stores of the others.
-constexpr uint32_t kBlkW = 64, kBlkH = 4;  // pixel block: one workgroup iteration
-constexpr uint32_t kSubW = 16;             // each wave: a 16 x 4 sub-block
+// ---------------------------------------------------------------------- frame kernel -------
+// The image (rank-local rows) is cut into 64 x 4 pixel blocks of four 16 x 4 sub-blocks.  A
+// sub-block inside some object's pixel rectangle (ObjectDesc::rect) is "detail": one wave runs
+// Engine::cast_ray for its 64 pixels, one pixel per lane.  Every other sub-block is background
+// (engine.rs:355-357) with no test at all.  One persistent launch does both, in this order:
+//  1. fill: waves stride over the 64 x 4 blocks and write the background of the non-detail
+//     sub-blocks — a whole block as 3 + 1 + 1 wave-contiguous 16-byte stores.  This is the
+//     frame's HBM-write floor, and the stores drain while the detail work runs;
+//  2. detail: the detail sub-blocks are enumerated rectangle by rectangle (a sub-block in
+//     several rectangles belongs to the first) and dealt out round-robin over the workgroups,
+//     four consecutive ones per workgroup, so the latency-bound shading is spread over all CUs
+//     instead of clustering on the CUs that own the screen region of the object.
+// Small objects' culling, intersection and shading records are cached in LDS per workgroup.
+constexpr uint32_t kBlkW = 64, kBlkH = 4;  // pixel block
+constexpr uint32_t kSubW = 16;             // sub-block width (x kBlkH rows): one wave's pixels
+
+// LDS caches of small objects' records (dynamic shared memory, sized by p.cached_tris):
+// [TriCull x n | TriHot x n | TriShade x n], all 16-byte aligned.
+__device__ __forceinline__ TriCull* cache_cull(char* dyn) { return reinterpret_cast<TriCull*>(dyn); }
+__device__ __forceinline__ TriHot* cache_hot(char* dyn, uint32_t n) {
+    return reinterpret_cast<TriHot*>(dyn + sizeof(TriCull) * n);
+}
+__device__ __forceinline__ TriShade* cache_shade(char* dyn, uint32_t n) {
+    return reinterpret_cast<TriShade*>(dyn + (sizeof(TriCull) + sizeof(TriHot)) * n);
+}
+
+template <bool kCull>
+__device__ void load_caches(const FrameParams& p, char* dyn) {
+    const uint32_t n = p.cached_tris;
+    for (uint32_t oi = 0; oi < p.nobj; ++oi) {
+        const ObjectDesc ob = object_desc(p, oi);
+        if (ob.cache_off == kNotCached) continue;
+        for (uint32_t i = threadIdx.x; i < ob.tri_count; i += kWG) {
+            if (kCull) cache_cull(dyn)[ob.cache_off + i] = p.cull[ob.tri_begin + i];
+            cache_hot(dyn, n)[ob.cache_off + i] = p.tris[ob.tri_begin + i];
+            cache_shade(dyn, n)[ob.cache_off + i] = p.shade[ob.tri_begin + i];
+        }
+    }
+}
 
 __device__ __forceinline__ Bundle make_bundle(const FrameParams& p, uint32_t x0, uint32_t xe,
                                               uint32_t py0, uint32_t pye) {
@@ -400,275 +504,378 @@ __device__ __forceinline__ Bundle make_bundle(const FrameParams& p, uint32_t x0,
                   ((float)(p.row0 + pye) * rh) * hi};
 }
 
-template <bool kCull, bool kLdsTiles>
-__global__ void __launch_bounds__(kWG) frame_kernel(FrameParams p) {
-    __shared__ TriHot s_hot[kLdsTiles ? kTriTile : 1];
-    __shared__ TriCull s_cull[(kCull && kLdsTiles) ? kTriTile : 1];
-    __shared__ TriCull s_cache[kCull ? kCullCache : 1];
-    __shared__ float4 s_rgb[kBlkW * kBlkH * 3 / 4];    // each wave's f32 RGB rows, staged
-    __shared__ uint32_t s_ppm[kBlkW * kBlkH * 3 / 4];  // ... and its PPM byte rows
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const f3 C = mk3(p.cx, p.cy, p.cz);
+struct SubRect {  // sub-block coordinates (x in kSubW columns, y in kBlkH local rows), inclusive
+    int32_t sx0, sx1, sy0, sy1;
+};
+__device__ __forceinline__ SubRect sub_rect(const FrameParams& p, const ObjectDesc& ob) {
+    const int32_t x0 = ob.rect[0], x1 = min(ob.rect[1], (int32_t)p.cam_w - 1);
+    const int32_t y0 = max(ob.rect[2] - (int32_t)p.row0, 0);
+    const int32_t y1 = min(ob.rect[3] - (int32_t)p.row0, (int32_t)p.rows - 1);
+    if (x0 > x1 || y0 > y1 || !ob.tri_count) return SubRect{1, 0, 1, 0};
+    return SubRect{x0 / (int32_t)kSubW, x1 / (int32_t)kSubW, y0 / (int32_t)kBlkH, y1 / (int32_t)kBlkH};
+}
+__device__ __forceinline__ uint32_t area(const SubRect& r) {
+    return r.sx0 > r.sx1 ? 0u : (uint32_t)(r.sx1 - r.sx0 + 1) * (uint32_t)(r.sy1 - r.sy0 + 1);
+}
+__device__ __forceinline__ bool inside(const SubRect& r, int32_t sx, int32_t sy) {
+    return sx >= r.sx0 && sx <= r.sx1 && sy >= r.sy0 && sy <= r.sy1;
+}
 
-    if (kCull) {  // cache the small objects' culling records
-        for (uint32_t oi = 0; oi < p.nobj; ++oi) {
-            const ObjectDesc ob = object_desc(p, oi);
-            if (ob.cache_off == kNotCached) continue;
-            for (uint32_t i = threadIdx.x; i < ob.tri_count; i += kWG) s_cache[ob.cache_off + i] = p.cull[ob.tri_begin + i];
-        }
-        __syncthreads();
-    }
+// background (engine.rs:355-357) and its bytes: sat_u8(0.1*255) = 25, sat_u8(0.2*255) = 51
+__device__ __forceinline__ float4 bg_rgb4(uint32_t phase) {  // 16-byte word at float offset 4c
+    const float a = 0.1f, b = 0.2f;
+    return phase == 0 ? make_float4(a, a, b, a) : phase == 1 ? make_float4(a, b, a, a) : make_float4(b, a, a, b);
+}
+__device__ __forceinline__ uint4 bg_ppm16(uint32_t phase) {  // 16-byte word at byte offset 16c
+    const uint32_t c01 = sat_u8(0.1f * 255.0f), c02 = sat_u8(0.2f * 255.0f);
+    const uint32_t w0 = c01 | (c01 << 8) | (c02 << 16) | (c01 << 24);  // 25 25 51 25
+    const uint32_t w1 = c01 | (c02 << 8) | (c01 << 16) | (c01 << 24);  // 25 51 25 25
+    const uint32_t w2 = c02 | (c01 << 8) | (c01 << 16) | (c02 << 24);  // 51 25 25 51
+    return phase == 0 ? make_uint4(w0, w1, w2, w0) : phase == 1 ? make_uint4(w1, w2, w0, w1) : make_uint4(w2, w0, w1, w2);
+}
 
-    // background (engine.rs:355-357) and its bytes: sat_u8(0.1*255) = 25, sat_u8(0.2*255) = 51
-    const float b01 = 0.1f, b02 = 0.2f;
-    const uint32_t c01 = sat_u8(b01 * 255.0f), c02 = sat_u8(b02 * 255.0f);
-
-    const uint32_t block_rows = (p.rows + kBlkH - 1) / kBlkH;
-    const uint32_t nblk = p.tiles_x * block_rows;
-    for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-        const uint32_t bx = blk % p.tiles_x, by = blk / p.tiles_x;
-        const uint32_t wx0 = bx * kBlkW + wave * kSubW, py0 = by * kBlkH;
-        const uint32_t px = wx0 + (lane % kSubW), ly = lane / kSubW;
-        const uint32_t py = py0 + ly;
-        const bool valid = px < p.cam_w && py < p.rows;
-        const uint32_t y = p.row0 + py;
-        const bool wave_live = wx0 < p.cam_w;
-        const Bundle bd = make_bundle(p, wx0, min(wx0 + kSubW - 1, p.cam_w - 1), py0,
-                                      min(py0 + kBlkH - 1, p.rows - 1));
-
-        // ---- cast_ray (engine.rs:112-216): closest object among first hits ---------------
-        f3 d[1] = {mk3(0.0f, 0.0f, 0.0f)};
-        bool ray_ready = false;
-        bool have = false;
-        float closest = 0.0f, bu = 0.0f, bv = 0.0f, bt = 0.0f;
-        uint32_t best_obj = 0;
-        int best_face = -1;
-        for (uint32_t oi = 0; oi < p.nobj; ++oi) {
-            const ObjectDesc ob = object_desc(p, oi);  // uniform: scalar loads
-            auto activate = [&](bool (&a)[1]) {
-                if (!ray_ready) {
-                    uint32_t pxo = px, yo = y;  // opaque: keep ray generation on this path
-                    asm volatile("" : "+v"(pxo), "+v"(yo));
-                    d[0] = camera_dir(p, pxo, yo);
-                    ray_ready = true;
-                }
-                a[0] = bbox_hit(ob, C, d[0]);
-            };
-            int st[1] = {valid ? kUndecided : kDone}, f[1] = {-1};
-            float u[1], v[1], t[1];
-            if (!kLdsTiles || ob.tri_count <= kDirectMax)
-                first_hit<kCull, false, 1>(p, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull,
-                                           activate, f, u, v, t, s_cache, kCull ? ob.cache_off : kNotCached);
-            else
-                first_hit<kCull, kLdsTiles, 1>(p, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot,
-                                               s_cull, activate, f, u, v, t);
-            if (f[0] >= 0) {
-                const f3 P = add(C, mul(d[0], t[0]));
-                const float dsq = len_sq(sub(P, C));
-                if (!have || dsq < closest) {  // strict `<`: the first object wins ties
-                    have = true;
-                    closest = dsq;
-                    best_obj = oi;
-                    best_face = f[0];
-                    bu = u[0];
-                    bv = v[0];
-                    bt = t[0];
-                }
+// Background for the pixels [x0, x0 + w) x rows [py0, py0 + kBlkH) (w = 64 or 16), wave-wide.
+template <uint32_t kW>
+__device__ __forceinline__ void fill_background(const FrameParams& p, uint32_t x0, uint32_t py0, bool aligned,
+                                                uint32_t lane) {
+    if (aligned && x0 + kW <= p.cam_w && py0 + kBlkH <= p.rows) {
+        constexpr uint32_t kRow4 = kW * 3 / 4;    // float4 per RGB row
+        constexpr uint32_t kRow16 = kW * 3 / 16;  // 16-byte words per PPM row
+        constexpr uint32_t kFace4 = kW / 4;       // int4 per face row
+        if (p.out_rgb) {
+#pragma unroll
+            for (uint32_t i = lane; i < kBlkH * kRow4; i += 64) {
+                const uint32_t r = i / kRow4, c = i % kRow4;
+                reinterpret_cast<float4*>(p.out_rgb + 3 * ((size_t)(py0 + r) * p.img_w + x0))[c] = bg_rgb4(c % 3);
             }
         }
-
-        const bool full = wave_live && wx0 + kSubW <= p.cam_w && py0 + kBlkH <= p.rows && (p.img_w % 16) == 0 &&
-                          ((reinterpret_cast<uintptr_t>(p.out_rgb) | reinterpret_cast<uintptr_t>(p.out_ppm) |
-                            reinterpret_cast<uintptr_t>(p.out_face)) & 15) == 0;
-        if (!__any(have)) {
-            // ---- no hit in the sub-block: background, 16-byte stores along each row ---------
-            if (full) {
-                constexpr uint32_t kRgbRow4 = kSubW * 3 / 4;    // 12 float4 per row
-                constexpr uint32_t kPpmRow16 = kSubW * 3 / 16;  // 3 x 16 B per row
-                if (p.out_rgb && lane < kBlkH * kRgbRow4) {
-                    const uint32_t r = lane / kRgbRow4, c = lane % kRgbRow4, ph = c % 3;
-                    const float4 v = ph == 0 ? make_float4(b01, b01, b02, b01)
-                                             : ph == 1 ? make_float4(b01, b02, b01, b01) : make_float4(b02, b01, b01, b02);
-                    reinterpret_cast<float4*>(p.out_rgb + 3 * ((size_t)(py0 + r) * p.img_w + wx0))[c] = v;
-                }
-                if (p.out_ppm && lane < kBlkH * kPpmRow16) {
-                    const uint32_t r = lane / kPpmRow16, c = lane % kPpmRow16, ph = c % 3;
-                    const uint32_t w0 = c01 | (c01 << 8) | (c02 << 16) | (c01 << 24);  // bytes 25 25 51 25
-                    const uint32_t w1 = c01 | (c02 << 8) | (c01 << 16) | (c01 << 24);  // 25 51 25 25
-                    const uint32_t w2 = c02 | (c01 << 8) | (c01 << 16) | (c02 << 24);  // 51 25 25 51
-                    const uint4 v = ph == 0 ? make_uint4(w0, w1, w2, w0)
-                                            : ph == 1 ? make_uint4(w1, w2, w0, w1) : make_uint4(w2, w0, w1, w2);
-                    const size_t row = (size_t)(p.rows - py0 - kBlkH + r);
-                    reinterpret_cast<uint4*>(p.out_ppm + 3 * (row * p.img_w + wx0))[c] = v;
-                }
-                if (p.out_face && lane < kBlkH * (kSubW / 4)) {
-                    const uint32_t r = lane / (kSubW / 4), c = lane % (kSubW / 4);
-                    reinterpret_cast<int4*>(p.out_face + (size_t)(py0 + r) * p.img_w + wx0)[c] = make_int4(-1, -1, -1, -1);
-                }
-            } else if (valid) {
-                const size_t idx = (size_t)py * p.img_w + px;
-                if (p.out_rgb) {
-                    float* o = p.out_rgb + 3 * idx;
-                    o[0] = b01;
-                    o[1] = b01;
-                    o[2] = b02;
-                }
-                if (p.out_ppm) {
-                    uint8_t* o = p.out_ppm + 3 * ((size_t)(p.rows - 1 - py) * p.img_w + px);
-                    o[0] = (uint8_t)c01;
-                    o[1] = (uint8_t)c01;
-                    o[2] = (uint8_t)c02;
-                }
-                if (p.out_face) p.out_face[idx] = -1;
-            }
-            continue;
+        if (p.out_ppm && lane < kBlkH * kRow16) {
+            const uint32_t r = lane / kRow16, c = lane % kRow16;
+            const size_t row = (size_t)(p.rows - py0 - kBlkH + r);  // file rows, bottom-up
+            reinterpret_cast<uint4*>(p.out_ppm + 3 * (row * p.img_w + x0))[c] = bg_ppm16(c % 3);
         }
-
-        // ---- hit data and Material::get (material.rs:56-94) ------------------------------
-        f3 P = mk3(0.0f, 0.0f, 0.0f), N = mk3(0.0f, 0.0f, 0.0f);
-        rgb color{0.0f, 0.0f, 0.0f};
-        float kd = 0.5f, ks = 0.5f, sp = 1.0f;
-        if (have) {
-            const ObjectDesc ob = p.objects[best_obj];
-            const TriShade sh = p.shade[ob.tri_begin + (uint32_t)best_face];
-            P = add(C, mul(d[0], bt));
-            const f3 na = mk3(sh.s0.x, sh.s0.y, sh.s0.z), nb = mk3(sh.s0.w, sh.s1.x, sh.s1.y);
-            const f3 nc = mk3(sh.s1.z, sh.s1.w, sh.s2.x);
-            N = normalize(add(add(mul(na, bu), mul(nb, bv)), mul(nc, bt)));
-            const float w = 1.0f - bu - bv;
-            const float uv0 = ((sh.s2.y * w) + (sh.s2.w * bu)) + (sh.s3.y * bv);
-            const float uv1 = ((sh.s2.z * w) + (sh.s3.x * bu)) + (sh.s3.z * bv);
-            if (ob.mat.color.data) {
-                const TexView& tv = ob.mat.color;
-                const uint32_t ix = sat_u32(uv0 * (float)tv.w) % tv.w;
-                const uint32_t iy = sat_u32(uv1 * (float)tv.h) % tv.h;
-                const float* c = tv.data + 3 * ((size_t)iy * tv.w + ix);
-                color = rgb{c[0], c[1], c[2]};
-            }
-            tex_value(ob.mat.diffuse, uv0, uv1, kd);
-            tex_value(ob.mat.specular, uv0, uv1, ks);
-            tex_value(ob.mat.specular_power, uv0, uv1, sp);
+        if (p.out_face && lane < kBlkH * kFace4) {
+            const uint32_t r = lane / kFace4, c = lane % kFace4;
+            reinterpret_cast<int4*>(p.out_face + (size_t)(py0 + r) * p.img_w + x0)[c] = make_int4(-1, -1, -1, -1);
         }
-
-        bool any = false;  // the lighting list as a running left fold (color.rs:82-87)
-        rgb acc{0.0f, 0.0f, 0.0f};
-        auto push = [&](rgb c) {
-            if (any) {
-                acc = cadd(acc, c);
-            } else {
-                acc = c;
-                any = true;
-            }
-        };
-        for (uint32_t li = 0; li < p.nlights; ++li) {
-            const LightDesc L = light_desc(p, li);
-            if (L.variant == 1) continue;  // point lights first (engine.rs:274-279)
-            const f3 Lp = mk3(L.pos[0], L.pos[1], L.pos[2]);
-            // reaches_light(Ray::new(P + N * 0.1, Lp - P)) (engine.rs:280-286, 218-228)
-            f3 S = mk3(0.0f, 0.0f, 0.0f);
-            f3 sd[1] = {mk3(0.0f, 0.0f, 1.0f)};
-            float dist = 0.0f;
-            if (have) {
-                S = add(P, mul(N, 0.1f));
-                sd[0] = normalize(sub(Lp, P));
-                dist = len(sub(Lp, S));
-            }
-            bool reached = true, decided = false;
-            for (uint32_t oj = 0; oj < p.nobj; ++oj) {
-                const ObjectDesc ob = object_desc(p, oj);
-                int st[1] = {(have && !decided && bbox_hit(ob, S, sd[0])) ? kSearching : kDone};
-                int f[1] = {-1};
-                float u[1], v[1], t[1];
-                auto never = [](bool (&a)[1]) { a[0] = false; };
-                if (!kLdsTiles || ob.tri_count <= kDirectMax)
-                    first_hit<false, false, 1>(p, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot, s_cull,
-                                               never, f, u, v, t);
-                else
-                    first_hit<false, kLdsTiles, 1>(p, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot,
-                                                   s_cull, never, f, u, v, t);
-                if (f[0] >= 0) {
-                    const f3 hp = add(S, mul(sd[0], t[0]));
-                    reached = len(sub(hp, S)) > dist;
-                    decided = true;
-                }
-            }
-            if (have && reached) {  // engine.rs:287-322
-                const f3 LmP = sub(Lp, P);
-                float prod = rust_clamp(dot0(N, LmP), 0.0f, 1.0f);
-                if (prod != prod) prod = 0.0f;
-                const float falloff = 1.0f / len(LmP);
-                const rgb lc{L.color[0], L.color[1], L.color[2]};
-                const rgb diffusion = cmul(cmul(cmul(cmul(cmulc(color, lc), kd), prod), L.brightness), falloff);
-                const f3 reflected = sub(d[0], mul(mul(N, 2.0f), dot0(d[0], N)));
-                const float res = rust_clamp(
-                    ks * L.brightness * powf_ref(dot0(normalize(reflected), normalize(LmP)), sp), 0.0f, 1.0f);
-                const float sf = rust_clamp(powf_ref(falloff, sp), 0.0f, 1.0f);
-                const rgb specular{res * sf, res * sf, res * sf};
-                push(cadd(diffusion, specular));
-            }
-        }
-        if (have) {
-            for (uint32_t li = 0; li < p.nlights; ++li) {  // ambient lights (engine.rs:341-352)
-                const LightDesc L = light_desc(p, li);
-                if (L.variant != 1) continue;
-                const rgb m{rust_min(L.color[0], color.r), rust_min(L.color[1], color.g),
-                            rust_min(L.color[2], color.b)};
-                push(cmul(cmul(m, kd), L.brightness));
-            }
-        } else {
-            push(rgb{b01, b01, b02});  // engine.rs:355-357
-        }
-
-        // ---- outputs: Image::set + Color::as_bytes, rows bottom-up (image.rs:41-74) -------
-        const uint32_t b0 = sat_u8(acc.r * 255.0f), b1 = sat_u8(acc.g * 255.0f), b2 = sat_u8(acc.b * 255.0f);
-        if (valid && p.out_face) p.out_face[(size_t)py * p.img_w + px] = have ? best_face : -1;
-        if (full) {  // the wave's 16 x 4 pixels leave through its own LDS slice as 16-B row stores
-            constexpr uint32_t kWavePix = kSubW * kBlkH;
-            float* wrgb = reinterpret_cast<float*>(s_rgb) + 3 * kWavePix * wave;
-            uint8_t* wppm = reinterpret_cast<uint8_t*>(s_ppm) + 3 * kWavePix * wave;
-            const uint32_t wl = lane % kSubW;
-            float* srgb = wrgb + 3 * (ly * kSubW + wl);
-            srgb[0] = acc.r;
-            srgb[1] = acc.g;
-            srgb[2] = acc.b;
-            uint8_t* sppm = wppm + 3 * ((kBlkH - 1 - ly) * kSubW + wl);
-            sppm[0] = (uint8_t)b0;
-            sppm[1] = (uint8_t)b1;
-            sppm[2] = (uint8_t)b2;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            constexpr uint32_t kRgbRow4 = kSubW * 3 / 4;    // float4 per wave row (12)
-            constexpr uint32_t kPpmRow16 = kSubW * 3 / 16;  // 16-byte words per wave row (3)
-            if (p.out_rgb && lane < kBlkH * kRgbRow4) {
-                const uint32_t r = lane / kRgbRow4, c = lane % kRgbRow4;
-                float4* dst = reinterpret_cast<float4*>(p.out_rgb + 3 * ((size_t)(py0 + r) * p.img_w + wx0)) + c;
-                *dst = reinterpret_cast<const float4*>(wrgb)[lane];
-            }
-            if (p.out_ppm && lane < kBlkH * kPpmRow16) {
-                const uint32_t r = lane / kPpmRow16, c = lane % kPpmRow16;  // r-th byte row of the block
-                const size_t row = (size_t)(p.rows - py0 - kBlkH + r);
-                uint4* dst = reinterpret_cast<uint4*>(p.out_ppm + 3 * (row * p.img_w + wx0)) + c;
-                *dst = reinterpret_cast<const uint4*>(wppm)[lane];
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next sub-block
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        } else if (valid) {
+    } else {  // image edge or unaligned output: per pixel
+        const float4 b = bg_rgb4(0);
+        const uint32_t c01 = sat_u8(0.1f * 255.0f), c02 = sat_u8(0.2f * 255.0f);
+        for (uint32_t k = lane; k < kW * kBlkH; k += 64) {
+            const uint32_t px = x0 + k % kW, py = py0 + k / kW;
+            if (px >= p.cam_w || py >= p.rows) continue;
             const size_t idx = (size_t)py * p.img_w + px;
             if (p.out_rgb) {
                 float* o = p.out_rgb + 3 * idx;
-                o[0] = acc.r;
-                o[1] = acc.g;
-                o[2] = acc.b;
+                o[0] = b.x;
+                o[1] = b.y;
+                o[2] = b.z;
             }
             if (p.out_ppm) {
                 uint8_t* o = p.out_ppm + 3 * ((size_t)(p.rows - 1 - py) * p.img_w + px);
-                o[0] = (uint8_t)b0;
-                o[1] = (uint8_t)b1;
-                o[2] = (uint8_t)b2;
+                o[0] = (uint8_t)c01;
+                o[1] = (uint8_t)c01;
+                o[2] = (uint8_t)c02;
+            }
+            if (p.out_face) p.out_face[idx] = -1;
+        }
+    }
+}
+
+// Engine::cast_ray for the 16 x 4 pixels at (wx0, py0) (rank-local rows), one pixel per lane;
+// `active` false: the wave only takes part in the workgroup's LDS-tile barriers.
+template <bool kCull, bool kLdsTiles, bool kSpecPow>
+__device__ __forceinline__ void render_sub(const FrameParams& p, uint32_t wx0, uint32_t py0, bool active,
+                                           TriHot* s_hot, TriCull* s_cull, float4* s_rgb, uint32_t* s_ppm,
+                                           const TriCull* c_cull, const TriHot* c_hot, const TriShade* c_shade,
+                                           bool aligned) {
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const f3 C = mk3(p.cx, p.cy, p.cz);
+    const uint32_t px = wx0 + (lane % kSubW), ly = lane / kSubW;
+    const uint32_t py = py0 + ly;
+    const bool valid = active && px < p.cam_w && py < p.rows;
+    const uint32_t y = p.row0 + py;
+    const int32_t sx = (int32_t)(wx0 / kSubW), sy = (int32_t)(py0 / kBlkH);
+    const Bundle bd = make_bundle(p, wx0, min(wx0 + kSubW - 1, p.cam_w - 1), py0, min(py0 + kBlkH - 1, p.rows - 1));
+
+    // ---- cast_ray (engine.rs:112-216): closest object among first hits -----------
+    f3 d[1] = {mk3(0.0f, 0.0f, 0.0f)};
+    bool ray_ready = false;
+    bool have = false;
+    float closest = 0.0f, bu = 0.0f, bv = 0.0f, bt = 0.0f;
+    uint32_t best_obj = 0;
+    int best_face = -1;
+    for (uint32_t oi = 0; oi < p.nobj; ++oi) {
+        const ObjectDesc ob = object_desc(p, oi);  // uniform: scalar loads
+        const bool direct = !kLdsTiles || ob.tri_count <= kDirectMax;
+        // outside the object's pixel rectangle no primary ray can hit it
+        if (kCull && direct && !inside(sub_rect(p, ob), sx, sy)) continue;
+        auto activate = [&](bool (&a)[1]) {
+            if (!ray_ready) {
+                uint32_t pxo = px, yo = y;  // opaque: keep ray generation on this path
+                asm volatile("" : "+v"(pxo), "+v"(yo));
+                d[0] = camera_dir(p, pxo, yo);
+                ray_ready = true;
+            }
+            a[0] = bbox_hit(ob, C, d[0]);
+        };
+        int st[1] = {valid ? kUndecided : kDone}, f[1] = {-1};
+        float u[1], v[1], t[1];
+        if (direct)
+            first_hit<kCull, false, 1>(p, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull,
+                                       activate, f, u, v, t, c_cull, ob.cache_off, c_hot);
+        else
+            first_hit<kCull, kLdsTiles, 1>(p, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot,
+                                           s_cull, activate, f, u, v, t);
+        if (f[0] >= 0) {
+            const f3 P = add(C, mul(d[0], t[0]));
+            const float dsq = len_sq(sub(P, C));
+            if (!have || dsq < closest) {  // strict `<`: the first object wins ties
+                have = true;
+                closest = dsq;
+                best_obj = oi;
+                best_face = f[0];
+                bu = u[0];
+                bv = v[0];
+                bt = t[0];
             }
         }
+    }
+
+    // ---- hit data and Material::get (material.rs:56-94) --------------------------
+    f3 P = mk3(0.0f, 0.0f, 0.0f), N = mk3(0.0f, 0.0f, 0.0f);
+    rgb color{0.0f, 0.0f, 0.0f};
+    float kd = 0.5f, ks = 0.5f, sp = 1.0f;
+    for (uint32_t oi = 0; oi < p.nobj; ++oi) {  // per-lane object, read from scalar copies
+        if (!__any(have && best_obj == oi)) continue;
+        const ObjectDesc ob = object_desc(p, oi);
+        if (!(have && best_obj == oi)) continue;
+        const TriShade sh = ob.cache_off != kNotCached ? c_shade[ob.cache_off + (uint32_t)best_face]
+                                                       : p.shade[ob.tri_begin + (uint32_t)best_face];
+        P = add(C, mul(d[0], bt));
+        const f3 na = mk3(sh.s0.x, sh.s0.y, sh.s0.z), nb = mk3(sh.s0.w, sh.s1.x, sh.s1.y);
+        const f3 nc = mk3(sh.s1.z, sh.s1.w, sh.s2.x);
+        N = normalize(add(add(mul(na, bu), mul(nb, bv)), mul(nc, bt)));
+        const float w = 1.0f - bu - bv;
+        const float uv0 = ((sh.s2.y * w) + (sh.s2.w * bu)) + (sh.s3.y * bv);
+        const float uv1 = ((sh.s2.z * w) + (sh.s3.x * bu)) + (sh.s3.z * bv);
+        if (ob.mat.color.data) {
+            const TexView& tv = ob.mat.color;
+            const uint32_t ix = sat_u32(uv0 * (float)tv.w) % tv.w;
+            const uint32_t iy = sat_u32(uv1 * (float)tv.h) % tv.h;
+            const float* c = tv.data + 3 * ((size_t)iy * tv.w + ix);
+            color = rgb{c[0], c[1], c[2]};
+        }
+        tex_value(ob.mat.diffuse, uv0, uv1, kd);
+        tex_value(ob.mat.specular, uv0, uv1, ks);
+        if (kSpecPow) tex_value(ob.mat.specular_power, uv0, uv1, sp);
+    }
+
+    bool any = false;  // the lighting list as a running left fold (color.rs:82-87)
+    rgb acc{0.0f, 0.0f, 0.0f};
+    auto push = [&](rgb c) {
+        if (any) {
+            acc = cadd(acc, c);
+        } else {
+            acc = c;
+            any = true;
+        }
+    };
+    for (uint32_t li = 0; li < p.nlights; ++li) {
+        const LightDesc L = light_desc(p, li);
+        if (L.variant == 1) continue;  // point lights first (engine.rs:274-279)
+        const f3 Lp = mk3(L.pos[0], L.pos[1], L.pos[2]);
+        // reaches_light(Ray::new(P + N * 0.1, Lp - P)) (engine.rs:280-286, 218-228)
+        f3 S = mk3(0.0f, 0.0f, 0.0f);
+        f3 sd[1] = {mk3(0.0f, 0.0f, 1.0f)};
+        float dist = 0.0f;
+        if (have) {
+            S = add(P, mul(N, 0.1f));
+            sd[0] = normalize(sub(Lp, P));
+            dist = len(sub(Lp, S));
+        }
+        bool reached = true, decided = false;
+        for (uint32_t oj = 0; oj < p.nobj; ++oj) {
+            const ObjectDesc ob = object_desc(p, oj);
+            int st[1] = {(have && !decided && bbox_hit(ob, S, sd[0])) ? kSearching : kDone};
+            int f[1] = {-1};
+            float u[1], v[1], t[1];
+            auto never = [](bool (&a)[1]) { a[0] = false; };
+            if (!kLdsTiles || ob.tri_count <= kDirectMax)
+                first_hit<false, false, 1>(p, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot, s_cull,
+                                           never, f, u, v, t, c_cull, ob.cache_off, c_hot);
+            else
+                first_hit<false, kLdsTiles, 1>(p, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot,
+                                               s_cull, never, f, u, v, t);
+            if (f[0] >= 0) {
+                const f3 hp = add(S, mul(sd[0], t[0]));
+                reached = len(sub(hp, S)) > dist;
+                decided = true;
+            }
+        }
+        if (have && reached) {  // engine.rs:287-322
+            const f3 LmP = sub(Lp, P);
+            float prod = rust_clamp(dot0(N, LmP), 0.0f, 1.0f);
+            if (prod != prod) prod = 0.0f;
+            const float falloff = 1.0f / len(LmP);
+            const rgb lc{L.color[0], L.color[1], L.color[2]};
+            const rgb diffusion =
+                cmul(cmul(cmul(cmul(cmulc(color, lc), kd), prod), L.brightness), falloff);
+            const f3 reflected = sub(d[0], mul(mul(N, 2.0f), dot0(d[0], N)));
+            const float dotr = dot0(normalize(reflected), normalize(LmP));
+            // specular_power defaults to 1 and powf(x, 1) == x; pow only when a
+            // material has a specular-power output (kSpecPow)
+            const float res =
+                rust_clamp(ks * L.brightness * (kSpecPow ? powf_ref(dotr, sp) : dotr), 0.0f, 1.0f);
+            const float sf = rust_clamp(kSpecPow ? powf_ref(falloff, sp) : falloff, 0.0f, 1.0f);
+            const rgb specular{res * sf, res * sf, res * sf};
+            push(cadd(diffusion, specular));
+        }
+    }
+    if (have) {
+        for (uint32_t li = 0; li < p.nlights; ++li) {  // ambient lights (engine.rs:341-352)
+            const LightDesc L = light_desc(p, li);
+            if (L.variant != 1) continue;
+            const rgb m{rust_min(L.color[0], color.r), rust_min(L.color[1], color.g),
+                        rust_min(L.color[2], color.b)};
+            push(cmul(cmul(m, kd), L.brightness));
+        }
+    } else {
+        push(rgb{0.1f, 0.1f, 0.2f});  // engine.rs:355-357
+    }
+
+    // ---- outputs: Image::set + Color::as_bytes, rows bottom-up (image.rs:41-74) ---
+    const uint32_t b0 = sat_u8(acc.r * 255.0f), b1 = sat_u8(acc.g * 255.0f), b2 = sat_u8(acc.b * 255.0f);
+    if (valid && p.out_face) p.out_face[(size_t)py * p.img_w + px] = have ? best_face : -1;
+    if (active && aligned && wx0 + kSubW <= p.cam_w && py0 + kBlkH <= p.rows) {
+        // the wave's 16 x 4 pixels leave through its own LDS slice as 16-B row stores
+        constexpr uint32_t kWavePix = kSubW * kBlkH;
+        float* wrgb = reinterpret_cast<float*>(s_rgb) + 3 * kWavePix * wave;
+        uint8_t* wppm = reinterpret_cast<uint8_t*>(s_ppm) + 3 * kWavePix * wave;
+        const uint32_t wl = lane % kSubW;
+        float* srgb = wrgb + 3 * (ly * kSubW + wl);
+        srgb[0] = acc.r;
+        srgb[1] = acc.g;
+        srgb[2] = acc.b;
+        uint8_t* sppm = wppm + 3 * ((kBlkH - 1 - ly) * kSubW + wl);
+        sppm[0] = (uint8_t)b0;
+        sppm[1] = (uint8_t)b1;
+        sppm[2] = (uint8_t)b2;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        constexpr uint32_t kRgbRow4 = kSubW * 3 / 4;    // float4 per wave row (12)
+        constexpr uint32_t kPpmRow16 = kSubW * 3 / 16;  // 16-byte words per wave row (3)
+        if (p.out_rgb && lane < kBlkH * kRgbRow4) {
+            const uint32_t r = lane / kRgbRow4, c = lane % kRgbRow4;
+            float4* dst = reinterpret_cast<float4*>(p.out_rgb + 3 * ((size_t)(py0 + r) * p.img_w + wx0)) + c;
+            *dst = reinterpret_cast<const float4*>(wrgb)[lane];
+        }
+        if (p.out_ppm && lane < kBlkH * kPpmRow16) {
+            const uint32_t r = lane / kPpmRow16, c = lane % kPpmRow16;  // r-th byte row of the block
+            const size_t row = (size_t)(p.rows - py0 - kBlkH + r);
+            uint4* dst = reinterpret_cast<uint4*>(p.out_ppm + 3 * (row * p.img_w + wx0)) + c;
+            *dst = reinterpret_cast<const uint4*>(wppm)[lane];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next block
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else if (valid) {
+        const size_t idx = (size_t)py * p.img_w + px;
+        if (p.out_rgb) {
+            float* o = p.out_rgb + 3 * idx;
+            o[0] = acc.r;
+            o[1] = acc.g;
+            o[2] = acc.b;
+        }
+        if (p.out_ppm) {
+            uint8_t* o = p.out_ppm + 3 * ((size_t)(p.rows - 1 - py) * p.img_w + px);
+            o[0] = (uint8_t)b0;
+            o[1] = (uint8_t)b1;
+            o[2] = (uint8_t)b2;
+        }
+    }
+}
+
+template <bool kCull, bool kLdsTiles, bool kSpecPow>
+__global__ void __launch_bounds__(kWG) frame_kernel(FrameParams p) {
+    __shared__ TriHot s_hot[kLdsTiles ? kTriTile : 1];
+    __shared__ TriCull s_cull[(kCull && kLdsTiles) ? kTriTile : 1];
+    __shared__ float4 s_rgb[kBlkW * kBlkH * 3 / 4];    // each wave's f32 RGB rows, staged
+    __shared__ uint32_t s_ppm[kBlkW * kBlkH * 3 / 4];  // ... and its PPM byte rows
+    extern __shared__ __attribute__((aligned(16))) char dyn[];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t nwaves = kWG / 64;
+    const bool aligned = (p.img_w % 16) == 0 &&
+                         ((reinterpret_cast<uintptr_t>(p.out_rgb) | reinterpret_cast<uintptr_t>(p.out_ppm) |
+                           reinterpret_cast<uintptr_t>(p.out_face)) & 15) == 0;
+    const uint32_t by_n = (p.rows + kBlkH - 1) / kBlkH;
+
+    // ---- 1. background of the non-detail sub-blocks ------------------------------------
+    if (kCull) {
+        const uint32_t nblk = p.tiles_x * by_n;
+        for (uint32_t blk = wave * gridDim.x + blockIdx.x; blk < nblk; blk += gridDim.x * nwaves) {
+            const uint32_t bx = blk % p.tiles_x, by = blk / p.tiles_x;
+            uint32_t mask = 0;  // detail sub-blocks of this block
+            for (uint32_t oi = 0; oi < p.nobj; ++oi) {
+                const SubRect r = sub_rect(p, object_desc(p, oi));
+                if ((int32_t)by < r.sy0 || (int32_t)by > r.sy1) continue;
+#pragma unroll
+                for (int32_t i = 0; i < 4; ++i) {
+                    const int32_t sx = (int32_t)(4 * bx) + i;
+                    mask |= (sx >= r.sx0 && sx <= r.sx1) ? (1u << i) : 0u;
+                }
+            }
+            if (!mask) {
+                fill_background<kBlkW>(p, bx * kBlkW, by * kBlkH, aligned, lane);
+            } else if (mask != 0xfu) {
+                for (uint32_t i = 0; i < 4; ++i)
+                    if (!((mask >> i) & 1u)) fill_background<kSubW>(p, bx * kBlkW + i * kSubW, by * kBlkH, aligned, lane);
+            }
+        }
+    }
+
+    // ---- 2. detail sub-blocks --------------------------------------------------------------
+    const uint32_t n_cached = p.cached_tris;
+    if (n_cached) load_caches<kCull>(p, dyn);
+    __syncthreads();
+    const TriCull* c_cull = cache_cull(dyn);
+    const TriHot* c_hot = cache_hot(dyn, n_cached);
+    const TriShade* c_shade = cache_shade(dyn, n_cached);
+    uint32_t total = 0;
+    if (kCull) {
+        for (uint32_t oi = 0; oi < p.nobj; ++oi) total += area(sub_rect(p, object_desc(p, oi)));
+    } else {
+        total = ((p.cam_w + kSubW - 1) / kSubW) * by_n;  // brute force: every sub-block
+    }
+    for (uint32_t c = blockIdx.x * nwaves; c < total; c += gridDim.x * nwaves) {  // workgroup-uniform
+        uint32_t j = c + wave;
+        bool active = j < total;
+        int32_t sx = 0, sy = 0;
+        if (active) {
+            if (kCull) {
+                for (uint32_t oi = 0; oi < p.nobj; ++oi) {
+                    const SubRect r = sub_rect(p, object_desc(p, oi));
+                    const uint32_t a = area(r);
+                    if (j >= a) {
+                        j -= a;
+                        continue;
+                    }
+                    const uint32_t w = (uint32_t)(r.sx1 - r.sx0 + 1);
+                    sx = r.sx0 + (int32_t)(j % w);
+                    sy = r.sy0 + (int32_t)(j / w);
+                    for (uint32_t ok = 0; ok < oi; ++ok)  // owned by an earlier rectangle
+                        if (inside(sub_rect(p, object_desc(p, ok)), sx, sy)) active = false;
+                    break;
+                }
+            } else {
+                const uint32_t w = (p.cam_w + kSubW - 1) / kSubW;
+                sx = (int32_t)(j % w);
+                sy = (int32_t)(j / w);
+            }
+        }
+        render_sub<kCull, kLdsTiles, kSpecPow>(p, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH, active, s_hot, s_cull,
+                                               s_rgb, s_ppm, c_cull, c_hot, c_shade, aligned);
     }
 }
 
@@ -703,32 +910,54 @@ hipError_t launch_tri_cull(const TriHot* hot, uint32_t T, float cx, float cy, fl
     return hipGetLastError();
 }
 
-// Persistent grid: as many workgroups as can be resident (occupancy query x CUs), never more
-// than there are pixel blocks.  No inter-workgroup synchronisation, so residency only affects
-// speed.
-template <bool kCull, bool kLdsTiles>
-static hipError_t launch_frame_kernel(const FrameParams& p, uint32_t nblk, hipStream_t s) {
-    static int resident = 0;
-    if (!resident) {
-        int dev = 0, cus = 0, per_cu = 0;
-        hipError_t e = hipGetDevice(&dev);
-        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e == hipSuccess)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, frame_kernel<kCull, kLdsTiles>, kWG, 0);
-        if (e != hipSuccess) return e;
-        resident = (per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 1);
-    }
-    const uint32_t grid = nblk < (uint32_t)resident ? nblk : (uint32_t)resident;
-    frame_kernel<kCull, kLdsTiles><<<grid, kWG, 0, s>>>(p);
+hipError_t launch_tri_rect(const TriCull* cull, uint32_t T, uint32_t cam_w, uint32_t cam_h, uint32_t* acc,
+                           hipStream_t s) {
+    if (!T) return hipSuccess;
+    tri_rect_kernel<<<(T + 255) / 256, 256, 0, s>>>(cull, T, cam_w, cam_h, acc);
     return hipGetLastError();
 }
 
+namespace {
+// Persistent grid: as many workgroups as are resident at once (occupancy API), capped by the
+// work (fill blocks or detail sub-blocks, whichever needs more workgroups).
+template <bool C, bool L, bool S>
+hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, hipStream_t s) {
+    static int per_cu = -1, cus = 0;
+    static size_t per_cu_dyn = 0;
+    if (per_cu < 0 || per_cu_dyn != dyn) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, frame_kernel<C, L, S>, kWG, dyn) != hipSuccess ||
+            per_cu <= 0)
+            per_cu = 1;
+        per_cu_dyn = dyn;
+    }
+    const uint32_t grid = min(want, (uint32_t)(per_cu * cus));
+    frame_kernel<C, L, S><<<grid, kWG, dyn, s>>>(p);
+    return hipGetLastError();
+}
+}  // namespace
+
 hipError_t launch_render(const FrameParams& p, hipStream_t s) {
-    const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
+    const uint32_t by_n = (p.rows + kBlkH - 1) / kBlkH;
+    const uint32_t nblk = p.tiles_x * by_n;
     if (!nblk) return hipSuccess;
-    const bool lds = p.max_object_tris > kDirectMax;
-    if (p.cull) return lds ? launch_frame_kernel<true, true>(p, nblk, s) : launch_frame_kernel<true, false>(p, nblk, s);
-    return lds ? launch_frame_kernel<false, true>(p, nblk, s) : launch_frame_kernel<false, false>(p, nblk, s);
+    const uint32_t nsub = ((p.cam_w + kSubW - 1) / kSubW) * by_n;
+    const uint32_t want = p.cull ? (nblk + 3) / 4 : (nsub + 3) / 4;
+    const size_t dyn = (size_t)p.cached_tris * (sizeof(TriCull) + sizeof(TriHot) + sizeof(TriShade));
+    const bool lds = p.max_object_tris > kDirectMax, sp = p.spec_pow != 0;
+    if (p.cull) {
+        if (lds) return sp ? launch_frame_kernel<true, true, true>(p, want, dyn, s)
+                           : launch_frame_kernel<true, true, false>(p, want, dyn, s);
+        return sp ? launch_frame_kernel<true, false, true>(p, want, dyn, s)
+                  : launch_frame_kernel<true, false, false>(p, want, dyn, s);
+    }
+    if (lds) return sp ? launch_frame_kernel<false, true, true>(p, want, dyn, s)
+                       : launch_frame_kernel<false, true, false>(p, want, dyn, s);
+    return sp ? launch_frame_kernel<false, false, true>(p, want, dyn, s)
+              : launch_frame_kernel<false, false, false>(p, want, dyn, s);
 }
 
 hipError_t launch_pack_ppm(const float* rgb, uint32_t w, uint32_t h, uint8_t* out, hipStream_t s) {

@@ -240,3 +240,72 @@ def test_many_objects_and_lights(gpu, oracle):
     assert stats["hit_pixels"] > 0
     assert np.array_equal(face, ref_face)
     assert_bit_equal(rgb, ref, "many objects/lights")
+
+
+def test_render_frames_graph_replay_matches_render(gpu, cube):
+    """eray_render_frames replays a cached HIP graph (64 frames + plain launches for the rest);
+    every replayed frame must be the frame eray_render writes, and a camera change must
+    rebuild the plan (new culling records, new pixel rectangles)."""
+    W, H = 320, 180
+    sc = MainScene(gpu, *cube, W, H, texture=256, fov=(16.0, 9.0))
+    ref = gpu_render(gpu, W, H)
+    rgb = gpu.empty((H, W, 3), np.float32)
+    ppm = gpu.empty((H, W, 3), np.uint8)
+    face = gpu.empty((H, W), np.int32)
+    try:
+        for frames in (1, 70):
+            gpu.memset(rgb.ptr, 0, rgb.nbytes)
+            gpu.memset(face.ptr, 0x7F, face.nbytes)
+            gpu.render_frames(frames, W, H, out_rgb=rgb.ptr, out_ppm=ppm.ptr, out_face=face.ptr,
+                              prepare_only=True)
+            ms = gpu.render_frames(frames, W, H, out_rgb=rgb.ptr, out_ppm=ppm.ptr, out_face=face.ptr,
+                                   timed=True)
+            assert ms > 0.0
+            assert_bit_equal(rgb.numpy(), ref[0], f"render_frames({frames})")
+            assert np.array_equal(face.numpy(), ref[1])
+            assert np.array_equal(ppm.numpy(), ref[2])
+        gpu.set_camera(capi.make_camera((0.4, -0.3, 4.0), (16.0, 9.0), W, 1.0))
+        moved = gpu_render(gpu, W, H)
+        assert not np.array_equal(moved[1], ref[1])
+        gpu.memset(rgb.ptr, 0, rgb.nbytes)
+        gpu.render_frames(70, W, H, out_rgb=rgb.ptr, out_ppm=ppm.ptr, out_face=face.ptr)
+        gpu.synchronize()
+        assert_bit_equal(rgb.numpy(), moved[0], "render_frames after a camera move")
+        assert np.array_equal(face.numpy(), moved[1])
+    finally:
+        for a in (rgb, ppm, face):
+            a.free()
+        sc.close()
+
+
+def test_every_pixel_written_and_rectangles_conservative(gpu, oracle):
+    """Off-centre objects partly outside the frame, edge-sized images (not multiples of 16 / 4):
+    the background fill and the detail sub-blocks must cover every pixel exactly as the oracle
+    renders it, with culling on and off."""
+    rng = np.random.default_rng(11)
+    for W, H in ((101, 37), (64, 4), (17, 130)):
+        s = oracle.Scene()
+        gpu.scene_reset()
+        cam = capi.make_camera((0.2, 0.1, 3.0), (float(W), float(H)), W, 1.0)
+        gpu.set_camera(cam)
+        keep = []
+        for k in range(2):
+            pos, nrm, uv = random_mesh(rng, 40, scale=0.8, center=rng.uniform(-1.5, 1.5, 3) * [1, 1, 0])
+            color = rng.uniform(0, 1, (8, 8, 3)).astype(np.float32)
+            dc = gpu.to_device(color)
+            keep.append(dc)
+            z = (0.0, 0.0, 0.0)
+            gpu.add_object(pos, nrm, uv, z, z, color=dc.image())
+            s.add_object(pos, nrm, uv, z, z, color=color)
+        s.add_light((1.0, 1.0, 2.0), "point", (1.0, 1.0, 1.0), 1.0)
+        gpu.add_light(capi.make_light((1.0, 1.0, 2.0), "point", (1.0, 1.0, 1.0), 1.0))
+        if capi.camera_size(cam) != (W, H):
+            continue
+        ref, ref_face, _ = oracle.render(s, oracle.camera((0.2, 0.1, 3.0), (float(W), float(H)), W, 1.0),
+                                         want_faces=True)
+        for flags in (capi.RENDER_DEFAULT, capi.RENDER_BRUTE_FORCE):
+            rgb, face, _ = gpu_render(gpu, W, H, flags=flags)
+            assert np.array_equal(face, ref_face), (W, H, flags)
+            assert_bit_equal(rgb, ref, f"{W}x{H} flags={flags}")
+        for a in keep:
+            a.free()
