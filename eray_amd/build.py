@@ -50,19 +50,26 @@ def _headers() -> list[str]:
     return hs
 
 
-def build(jobs: int = 4, verbose: bool = False, force: bool = False) -> str:
-    os.makedirs(OBJ, exist_ok=True)
+def build(jobs: int = 4, verbose: bool = False, force: bool = False, trace: bool = False) -> str:
+    """Build the product library; `trace` builds the diagnostic variant
+    lib/liberay_hip_trace.so instead (frame-kernel phase timestamps, ERAY_PHASE_TRACE)."""
+    obj_dir = os.path.join(OBJ, "trace") if trace else OBJ
+    lib_path = LIB.replace(".so", "_trace.so") if trace else LIB
+    extra = ["-DERAY_PHASE_TRACE"] if trace else []
+    if trace and os.environ.get("ERAY_TRACE_REPEAT"):
+        extra.append("-DERAY_PHASE_TRACE_REPEAT")
+    os.makedirs(obj_dir, exist_ok=True)
     os.makedirs(LIB_DIR, exist_ok=True)
     cc = hipcc()
     headers = _headers()
     objs, cmds = [], []
     for src in SOURCES:
         s = os.path.join(CSRC, src)
-        o = os.path.join(OBJ, src + ".o")
+        o = os.path.join(obj_dir, src + ".o")
         objs.append(o)
         if force or not _newer(o, [s] + headers):
             lang = [] if src.endswith(".hip") else ["-x", "hip"]
-            cmds.append([cc, *CXXFLAGS, *lang, "-c", s, "-o", o])
+            cmds.append([cc, *CXXFLAGS, *extra, *lang, "-c", s, "-o", o])
 
     def run(cmd):
         if verbose:
@@ -76,9 +83,9 @@ def build(jobs: int = 4, verbose: bool = False, force: bool = False) -> str:
         for warn in ex.map(run, cmds):
             if warn.strip() and verbose:
                 print(warn, file=sys.stderr)
-    if force or cmds or not _newer(LIB, objs):
-        run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs])
-    return LIB
+    if force or cmds or not _newer(lib_path, objs):
+        run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib_path, *objs])
+    return lib_path
 
 
 def main() -> None:
@@ -86,8 +93,9 @@ def main() -> None:
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--trace", action="store_true", help="build the diagnostic phase-trace variant")
     a = ap.parse_args()
-    print(build(a.jobs, a.verbose, a.force))
+    print(build(a.jobs, a.verbose, a.force, a.trace))
 
 
 if __name__ == "__main__":

@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "lib", "liberay_hip.so")
+# ERAY_LIB selects another build of the same ABI (diagnostics: lib/liberay_hip_trace.so)
+LIB_PATH = os.environ.get("ERAY_LIB") or os.path.join(_PKG, "lib", "liberay_hip.so")
 
 # eray_status (include/eray_hip.h)
 OK = 0

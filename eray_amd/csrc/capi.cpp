@@ -63,7 +63,6 @@ struct eray_ctx {
     std::vector<LightDesc> h_lights;
     std::vector<float> h_raw;
     uint32_t total_tris = 0;
-    uint32_t cached_tris = 0;  // triangles of small objects whose records live in LDS per frame
     bool spec_pow = false;     // some material has a specular-power output
 };
 
@@ -168,23 +167,16 @@ int sync_scene(eray_ctx* ctx, bool need_cull) {
     if (ctx->desc_dirty) {
         ctx->h_objs.clear();
         uint32_t begin = 0;
-        uint32_t cache_used = 0;
         ctx->spec_pow = false;
         for (auto& o : ctx->objects) {
             ObjectDesc d{};
-            d.tri_begin = begin;
-            d.tri_count = o.T;
-            d.rect[0] = d.rect[2] = 0;  // every pixel until the culling pass computes it
-            d.rect[1] = d.rect[3] = INT32_MAX;
-            // small objects' records are cached in LDS by the frame kernels (kCacheTris max)
-            d.cache_off = kNotCached;
-            if (o.T && cache_used + o.T <= kCacheTris) {
-                d.cache_off = cache_used;
-                cache_used += o.T;
-            }
+            d.g.tri_begin = begin;
+            d.g.tri_count = o.T;
+            d.g.rect[0] = d.g.rect[2] = 0;  // every pixel until the culling pass computes it
+            d.g.rect[1] = d.g.rect[3] = INT32_MAX;
             for (int k = 0; k < 3; ++k) {
-                d.bb_lo[k] = o.lo[k];
-                d.bb_hi[k] = o.hi[k];
+                d.g.bb_lo[k] = o.lo[k];
+                d.g.bb_hi[k] = o.hi[k];
             }
             d.mat = MaterialDesc{tex(o.mat.color), tex(o.mat.diffuse), tex(o.mat.specular),
                                  tex(o.mat.specular_power), tex(o.mat.reflection)};
@@ -192,7 +184,6 @@ int sync_scene(eray_ctx* ctx, bool need_cull) {
             ctx->spec_pow |= o.mat.specular_power.data != nullptr;
             begin += o.T;
         }
-        ctx->cached_tris = cache_used;
         ctx->h_lights.clear();
         for (auto& l : ctx->lights) {
             LightDesc d{};
@@ -229,7 +220,7 @@ int sync_scene(eray_ctx* ctx, bool need_cull) {
             if ((st = ensure(ctx, &ctx->d_rect, &ctx->rect_cap, 4 * nobj))) return st;
             HIP_TRY(ctx, hipMemsetAsync(ctx->d_rect, 0, sizeof(uint32_t) * 4 * nobj, ctx->stream));
             for (size_t i = 0; i < nobj; ++i)
-                HIP_TRY(ctx, launch_tri_rect(ctx->d_cull + ctx->h_objs[i].tri_begin, ctx->h_objs[i].tri_count, W, H,
+                HIP_TRY(ctx, launch_tri_rect(ctx->d_cull + ctx->h_objs[i].g.tri_begin, ctx->h_objs[i].g.tri_count, W, H,
                                              ctx->d_rect + 4 * i, ctx->stream));
             ctx->h_rect.assign(4 * nobj, 0u);
             HIP_TRY(ctx, hipMemcpyAsync(ctx->h_rect.data(), ctx->d_rect, sizeof(uint32_t) * 4 * nobj,
@@ -237,7 +228,7 @@ int sync_scene(eray_ctx* ctx, bool need_cull) {
             HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
             for (size_t i = 0; i < nobj; ++i) {
                 const uint32_t* a = &ctx->h_rect[4 * i];
-                int32_t* r = ctx->h_objs[i].rect;
+                int32_t* r = ctx->h_objs[i].g.rect;
                 if (a[1] == 0) {  // no face can be hit
                     r[0] = 1;
                     r[1] = 0;
@@ -539,11 +530,60 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     p.lights = ctx->d_lights;
     p.nobj = (uint32_t)ctx->objects.size();
     p.nlights = (uint32_t)ctx->lights.size();
-    for (size_t i = 0; i < ctx->h_objs.size() && i < (size_t)kInlineObjects; ++i) p.obj_inline[i] = ctx->h_objs[i];
-    for (size_t i = 0; i < ctx->h_lights.size() && i < (size_t)kInlineLights; ++i) p.light_inline[i] = ctx->h_lights[i];
     p.max_object_tris = 0;
     for (auto& o : ctx->objects) p.max_object_tris = o.T > p.max_object_tris ? o.T : p.max_object_tris;
-    p.cached_tris = ctx->cached_tris;
+    p.total_tris = ctx->total_tris;
+    p.lds_scene = (ctx->total_tris <= kCacheTris && p.nobj <= kCacheObjects && p.nlights <= kCacheLights) ? 1u : 0u;
+    // detail rectangles in sub-block units (16 px x 4 rank-local rows); brute force: the frame
+    const int32_t rows_i = (int32_t)rp->rows, w_i = (int32_t)W;
+    p.nrect = 0;
+    p.total_sub = 0;
+    auto add_rect = [&](int32_t x0, int32_t x1, int32_t y0, int32_t y1) {  // pixels, local rows
+        x1 = x1 < w_i - 1 ? x1 : w_i - 1;
+        y0 = y0 > 0 ? y0 : 0;
+        y1 = y1 < rows_i - 1 ? y1 : rows_i - 1;
+        if (x0 > x1 || y0 > y1) return;
+        int32_t r[4] = {x0 / 16, x1 / 16, y0 / 4, y1 / 4};
+        if (p.nrect == (uint32_t)kMaxRects) {  // out of slots: widen the last one
+            int32_t* l = p.rects[kMaxRects - 1];
+            l[0] = l[0] < r[0] ? l[0] : r[0];
+            l[1] = l[1] > r[1] ? l[1] : r[1];
+            l[2] = l[2] < r[2] ? l[2] : r[2];
+            l[3] = l[3] > r[3] ? l[3] : r[3];
+            return;
+        }
+        std::memcpy(p.rects[p.nrect++], r, sizeof r);
+    };
+    if (cull) {
+        for (size_t i = 0; i < ctx->h_objs.size(); ++i) {
+            const ObjectDesc& d = ctx->h_objs[i];
+            if (!d.g.tri_count) continue;
+            add_rect(d.g.rect[0], d.g.rect[1], d.g.rect[2] - (int32_t)rp->row0, d.g.rect[3] - (int32_t)rp->row0);
+        }
+    } else if (p.nobj) {
+        add_rect(0, w_i - 1, 0, rows_i - 1);
+    }
+    // the frame kernel wants disjoint rectangles: merge overlapping ones into their bounding box
+    for (bool merged = true; merged;) {
+        merged = false;
+        for (uint32_t a = 0; a < p.nrect && !merged; ++a)
+            for (uint32_t b = a + 1; b < p.nrect && !merged; ++b) {
+                int32_t* ra = p.rects[a];
+                const int32_t* rb = p.rects[b];
+                if (ra[0] > rb[1] || rb[0] > ra[1] || ra[2] > rb[3] || rb[2] > ra[3]) continue;
+                ra[0] = ra[0] < rb[0] ? ra[0] : rb[0];
+                ra[1] = ra[1] > rb[1] ? ra[1] : rb[1];
+                ra[2] = ra[2] < rb[2] ? ra[2] : rb[2];
+                ra[3] = ra[3] > rb[3] ? ra[3] : rb[3];
+                std::memmove(p.rects[b], p.rects[b + 1], sizeof(p.rects[0]) * (p.nrect - b - 1));
+                --p.nrect;
+                merged = true;
+            }
+    }
+    for (uint32_t k = 0; k < p.nrect; ++k) {  // sub-blocks the frame kernel renders in detail
+        const int32_t* r = p.rects[k];
+        p.total_sub += (uint32_t)(r[1] - r[0] + 1) * (uint32_t)(r[3] - r[2] + 1);
+    }
     p.spec_pow = ctx->spec_pow ? 1u : 0u;
     p.tiles_x = (W + 63) / 64;
     return ERAY_OK;

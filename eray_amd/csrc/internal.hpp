@@ -43,16 +43,21 @@ struct MaterialDesc {
     TexView diffuse, specular, specular_power, reflection;  // IValue
 };
 
-constexpr uint32_t kNotCached = 0xffffffffu;
-constexpr uint32_t kCacheTris = 256;  // LDS record cache capacity of the frame kernels (triangles)
+// Scenes up to these sizes are preloaded whole into each frame workgroup's LDS.
+constexpr uint32_t kCacheTris = 256, kCacheObjects = 16, kCacheLights = 16;
+// Detail rectangles carried in the kernel arguments (more objects: merged into the last one).
+constexpr int kMaxRects = 8;
 
-struct ObjectDesc {
+struct ObjGeom {  // what the triangle scans need of an object, 48 B
     uint32_t tri_begin, tri_count;
-    uint32_t cache_off;  // offset of its records in the frame kernels' LDS cache, or kNotCached
     // Camera pixels whose primary ray can hit the object: x0..x1 x y0..y1 (inclusive, camera
     // rows), from the culling records (tri_rect_kernel); empty when x0 > x1.
     int32_t rect[4];
     float bb_lo[3], bb_hi[3];
+};
+
+struct alignas(16) ObjectDesc {  // 128 B: the LDS scene copy moves whole 16-B words
+    ObjGeom g;
     MaterialDesc mat;
 };
 
@@ -62,11 +67,6 @@ struct LightDesc {
     float color[3];
     float brightness;
 };
-
-// The first objects / lights also travel inline in the kernel arguments (scalar constant
-// loads, no dependent global round trip); larger scenes read the rest from device arrays.
-constexpr int kInlineObjects = 4;
-constexpr int kInlineLights = 8;
 
 struct FrameParams {
     // camera (camera.rs:57-76)
@@ -88,12 +88,31 @@ struct FrameParams {
     const LightDesc* lights;
     uint32_t nobj, nlights;
     uint32_t max_object_tris;  // selects the kernel variant with LDS triangle tiles
-    uint32_t cached_tris;      // triangles whose records the frame kernels cache in LDS
+    uint32_t total_tris;
+    uint32_t lds_scene;        // the scene is small enough to preload into LDS (kCache*)
+    uint32_t nrect;            // detail rectangles (sub-block units: 16 px x 4 rank-local rows,
+    uint32_t total_sub;        // inclusive) and the number of sub-blocks they cover, counting
+    int32_t rects[kMaxRects][4];  // overlaps once: x0, x1, y0, y1
     uint32_t spec_pow;         // some material has a specular-power output (powf != identity)
     uint32_t tiles_x;  // pixel tiles per row
-    ObjectDesc obj_inline[kInlineObjects];
-    LightDesc light_inline[kInlineLights];
 };
+
+// Byte offsets of the LDS scene copy: [ObjectDesc x nobj | LightDesc x nl | TriCull x n (if
+// culling) | TriHot x n | TriShade x n]; every section is a whole number of 16-B words.
+struct SceneLdsLayout {
+    uint32_t objs, lights, cull, hot, shade, bytes;
+};
+__host__ __device__ inline SceneLdsLayout scene_lds_layout(uint32_t nobj, uint32_t nl, uint32_t n, bool cull) {
+    SceneLdsLayout L;
+    L.objs = 0;
+    L.lights = L.objs + nobj * (uint32_t)sizeof(ObjectDesc);
+    L.cull = L.lights + nl * (uint32_t)sizeof(LightDesc);
+    L.hot = L.cull + (cull ? n * (uint32_t)sizeof(TriCull) : 0u);
+    L.shade = L.hot + n * (uint32_t)sizeof(TriHot);
+    L.bytes = L.shade + n * (uint32_t)sizeof(TriShade);
+    return L;
+}
+static_assert(sizeof(ObjectDesc) % 16 == 0 && sizeof(LightDesc) % 16 == 0, "16-B words");
 
 // ------------------------------------------------------------- launchers (.hip files) ------
 hipError_t launch_tri_precompute(const float* pos, const float* nrm, const float* uv, uint32_t T,

@@ -36,6 +36,43 @@ using namespace eray::dev;
 constexpr int kWG = 256;
 constexpr int kTriTile = 256;
 
+// Scene descriptors and triangle records are read-only for the whole frame: reading them
+// through the constant address space lets wave-uniform reads become scalar (s_load) loads.
+// Texture pointers come out of the descriptors: say they are global (no flat loads).
+__device__ __forceinline__ const __attribute__((address_space(1))) float* as_global(const float* ptr) {
+    return (const __attribute__((address_space(1))) float*)ptr;
+}
+template <typename T>
+__device__ __forceinline__ T load_const(const T* base, size_t i) {
+    static_assert(sizeof(T) % 4 == 0, "dword-sized records only");
+    using cu32 = const __attribute__((address_space(4))) uint32_t;
+    cu32* src = (cu32*)(base + i);
+    T out;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&out);
+#pragma unroll
+    for (size_t k = 0; k < sizeof(T) / 4; ++k) dst[k] = src[k];
+    return out;
+}
+
+// Diagnostic builds only (python -m eray_amd.build --trace): workgroups 0, 16, ..., 1008 (waves)
+// record s_memrealtime (100 MHz) at the frame kernel's phase boundaries.
+#ifdef ERAY_PHASE_TRACE
+constexpr int kTraceSlots = 16;
+__device__ uint64_t g_trace[2 * 64 * 4 * kTraceSlots];  // [realtime | shader clock]
+#define ERAY_TRACE(slot)                                                                          \
+    do {                                                                                          \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x % 16 == 0 && blockIdx.x < 1024) {               \
+            const uint32_t i_ = (blockIdx.x / 16 * 4 + (threadIdx.x >> 6)) * kTraceSlots + (slot); \
+            g_trace[i_] = __builtin_amdgcn_s_memrealtime();                                       \
+            g_trace[64 * 4 * kTraceSlots + i_] = __builtin_amdgcn_s_memtime();                   \
+        }                                                                                         \
+    } while (0)
+#else
+#define ERAY_TRACE(slot) \
+    do {                 \
+    } while (0)
+#endif
+
 // --------------------------------------------------------------------- triangle setup ------
 // Triangle::intersects recomputes e1 = b - a, e2 = c - a, n = e1 x e2 for every test
 // (primitives.rs:44-46); they do not depend on the ray, so they are computed once here with
@@ -283,8 +320,26 @@ __device__ __forceinline__ bool exact_test(const TriHot& r, f3 o, f3 d, float& u
     return t >= 0.0f && u >= 0.0f && v >= 0.0f && (u + v) <= 1.0f;
 }
 
+// The same test without branches: every quantity is computed (a failed det check may divide
+// by zero; its u, v, t are then discarded) and the outcome is the same conjunction, so several
+// tests can be interleaved by the compiler.
+__device__ __forceinline__ bool exact_test_flat(const TriHot& r, f3 o, f3 d, float& u, float& v,
+                                                float& t) {
+    const f3 e1 = mk3(r.q0.x, r.q0.y, r.q0.z), e2 = mk3(r.q0.w, r.q1.x, r.q1.y);
+    const f3 n = mk3(r.q1.z, r.q1.w, r.q2.x), a = mk3(r.q2.y, r.q2.z, r.q2.w);
+    const float nd = dot0(n, d);
+    const float det = -dot0(d, n);
+    const float invdet = 1.0f / det;
+    const f3 ao = sub(o, a);
+    const f3 dao = cross(ao, d);
+    u = dot0(e2, dao) * invdet;
+    v = -dot0(e1, dao) * invdet;
+    t = dot0(ao, n) * invdet;
+    return !(nd > 0.0f) & (det >= 1e-6f) & (t >= 0.0f) & (u >= 0.0f) & (v >= 0.0f) & ((u + v) <= 1.0f);
+}
+
 // BoundingBox::intersects (object.rs:327-379), general box.
-__device__ __forceinline__ bool bbox_hit(const ObjectDesc& ob, f3 s, f3 d) {
+__device__ __forceinline__ bool bbox_hit(const ObjGeom& ob, f3 s, f3 d) {
     const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
     const bool sx = ix < 0.0f, sy = iy < 0.0f, sz = iz < 0.0f;
     float txmin = ((sx ? ob.bb_hi[0] : ob.bb_lo[0]) - s.x) * ix;
@@ -308,77 +363,169 @@ struct Bundle {  // a wave's pixel rectangle in viewport coordinates
     float xlo, xhi, ylo, yhi;
 };
 
+// --------------------------------------------------------------------- scene views ---------
+// Read paths of the frame's scene data (descriptors, lights, triangle records).
+//  * SceneGlobal reads the device arrays; uniform reads go through the constant address
+//    space and become scalar loads.
+//  * SceneLds reads a copy of the whole scene that each workgroup preloads into LDS in one
+//    round trip (small scenes: kCacheTris triangles, kCacheObjects objects, kCacheLights
+//    lights).  Uniform reads are LDS broadcasts moved to SGPRs with readfirstlane.
+// Either way one instantiation touches one address space (no generic "flat" loads).
+template <typename T>
+__device__ __forceinline__ T lds_uniform(const T* ptr) {
+    static_assert(sizeof(T) % 4 == 0, "dword-sized records only");
+    T out;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(ptr);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&out);
+#pragma unroll
+    for (size_t k = 0; k < sizeof(T) / 4; ++k) dst[k] = __builtin_amdgcn_readfirstlane(src[k]);
+    return out;
+}
+
+struct SceneGlobal {
+    const FrameParams& p;
+    __device__ ObjGeom geom(uint32_t i) const { return load_const(&p.objects[i].g, 0); }
+    __device__ MaterialDesc mat(uint32_t i) const { return load_const(&p.objects[i].mat, 0); }
+    __device__ LightDesc light(uint32_t i) const { return load_const(p.lights, i); }
+    __device__ TriCull cull(uint32_t g) const { return p.cull[g]; }        // per lane
+    __device__ TriHot hot(uint32_t g) const { return load_const(p.tris, g); }  // uniform
+    __device__ TriShade shade(uint32_t g) const { return p.shade[g]; }     // per lane
+};
+
+struct SceneLds {
+    const ObjectDesc* objs;
+    const LightDesc* lights;
+    const TriCull* culls;
+    const TriHot* hots;
+    const TriShade* shades;
+    __device__ ObjGeom geom(uint32_t i) const { return lds_uniform(&objs[i].g); }
+    __device__ MaterialDesc mat(uint32_t i) const { return lds_uniform(&objs[i].mat); }
+    __device__ LightDesc light(uint32_t i) const { return lds_uniform(lights + i); }
+    __device__ TriCull cull(uint32_t g) const { return culls[g]; }
+    __device__ TriHot hot(uint32_t g) const { return hots[g]; }  // broadcast read (VGPRs)
+    __device__ TriShade shade(uint32_t g) const { return shades[g]; }
+};
+
+// Copies the scene into LDS (layout: scene_lds_layout, internal.hpp): every 16-byte word is
+// loaded before any is stored, four per thread per pass, so a small scene costs one round trip.
+__device__ SceneLds preload_scene(const FrameParams& p, char* dyn) {
+    const SceneLdsLayout L = scene_lds_layout(p.nobj, p.nlights, p.total_tris, p.cull != nullptr);
+    const uint32_t n_obj = L.lights / 16, n_light = (L.cull - L.lights) / 16;
+    const uint32_t n_cull = (L.hot - L.cull) / 16, n_hot = (L.shade - L.hot) / 16;
+    const uint32_t total = L.bytes / 16;
+    using v4 = unsigned int __attribute__((ext_vector_type(4)));
+    using gv4 = const __attribute__((address_space(1))) v4;
+    gv4* src_obj = (gv4*)p.objects;
+    gv4* src_light = (gv4*)p.lights;
+    gv4* src_cull = (gv4*)p.cull;
+    gv4* src_hot = (gv4*)p.tris;
+    gv4* src_shade = (gv4*)p.shade;
+    v4* dst = reinterpret_cast<v4*>(dyn);
+    for (uint32_t base = 0; base < total; base += 4 * kWG) {
+        v4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t i = base + k * kWG + threadIdx.x;
+            if (i >= total) continue;
+            gv4* src;
+            if (i < n_obj) {
+                src = src_obj + i;
+            } else if ((i -= n_obj) < n_light) {
+                src = src_light + i;
+            } else if ((i -= n_light) < n_cull) {
+                src = src_cull + i;
+            } else if ((i -= n_cull) < n_hot) {
+                src = src_hot + i;
+            } else {
+                src = src_shade + (i - n_hot);
+            }
+            v[k] = *src;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t i = base + k * kWG + threadIdx.x;
+            if (i < total) dst[i] = v[k];
+        }
+    }
+    return SceneLds{reinterpret_cast<const ObjectDesc*>(dyn + L.objs), reinterpret_cast<const LightDesc*>(dyn + L.lights),
+                    reinterpret_cast<const TriCull*>(dyn + L.cull), reinterpret_cast<const TriHot*>(dyn + L.hot),
+                    reinterpret_cast<const TriShade*>(dyn + L.shade)};
+}
+
+// --------------------------------------------------------------------- first hit -----------
 // Per-ray search state: kUndecided (ray and bounding-box test not evaluated yet), kSearching,
 // kDone (hit found, bbox rejected, or not a pixel of the image).
 constexpr int kUndecided = 0, kSearching = 1, kDone = 2;
 
-// Objects with at most this many triangles are searched by each wave on its own (records read
-// straight from global memory / the scalar cache, no LDS, no barrier); larger ones go through
-// workgroup-shared LDS tiles.
+// Objects with at most this many triangles are searched by each wave on its own (no LDS tiles,
+// no barrier); larger ones go through workgroup-shared LDS tiles.
 constexpr uint32_t kDirectMax = 256;
-// Records of small objects are cached in LDS once per workgroup, up to this many triangles.
+// Candidate triangles tested together per step (independent, branch-free tests: their long
+// dependent chains, division included, overlap).
+constexpr int kBatch = 4;
 
-// First-hit search over triangles [begin, begin + count) for R rays per lane (Object::intersects'
-// face loop, object.rs:63-78).  Rays still kUndecided when the wave meets its first candidate
-// triangle are resolved by activate(a), which must generate their directions (into `d`) and
-// return the bounding-box verdicts (object.rs:59-61) in a[].  found[k] receives the face index
-// relative to `begin`, or stays -1.  kLds: every thread of the workgroup must call it.
-template <bool kCull, bool kLds, int R, typename Activate>
-__device__ void first_hit(const FrameParams& p, uint32_t begin, uint32_t count, int (&st)[R],
-                          const f3& o, const f3 (&d)[R], const Bundle& bd, TriHot* s_hot,
-                          TriCull* s_cull, Activate&& activate, int (&found)[R], float (&hu)[R],
-                          float (&hv)[R], float (&ht)[R], const TriCull* s_cache = nullptr,
-                          uint32_t cache_off = kNotCached, const TriHot* s_hot_cache = nullptr) {
-    const uint32_t lane = threadIdx.x & 63;
-    auto any_state = [&](int s) {
-        bool a = false;
+// Tests the candidates of `mask` (bit i = triangle idx0 + i) in index order, kBatch at a time;
+// hot(i) returns triangle idx0 + i's record.  Returns false once no lane is searching.
+template <typename Hot>
+__device__ __forceinline__ bool test_candidates(unsigned long long mask, uint32_t idx0, Hot&& hot, int& st,
+                                                const f3& o, const f3& d, int& found, float& hu, float& hv,
+                                                float& ht) {
+    while (mask) {
+        uint32_t ids[kBatch];
+        bool has[kBatch];
+        TriHot h[kBatch];
 #pragma unroll
-        for (int k = 0; k < R; ++k) a = a || st[k] == s;
-        return __any(a);
-    };
-    auto not_done = [&]() {
-        bool a = false;
+        for (int k = 0; k < kBatch; ++k) {
+            has[k] = mask != 0;
+            ids[k] = has[k] ? (uint32_t)(__ffsll(mask) - 1) : 0u;
+            mask &= mask - 1;
+            h[k] = hot(ids[k]);
+        }
+        bool hit[kBatch];
+        float u[kBatch], v[kBatch], t[kBatch];
 #pragma unroll
-        for (int k = 0; k < R; ++k) a = a || st[k] != kDone;
-        return a;
-    };
-    auto test = [&](const TriHot& h, uint32_t idx) {
+        for (int k = 0; k < kBatch; ++k) hit[k] = has[k] && exact_test_flat(h[k], o, d, u[k], v[k], t[k]);
 #pragma unroll
-        for (int k = 0; k < R; ++k) {
-            if (st[k] == kSearching) {
-                float u, v, t;
-                if (exact_test(h, o, d[k], u, v, t)) {
-                    found[k] = (int)idx;
-                    hu[k] = u;
-                    hv[k] = v;
-                    ht[k] = t;
-                    st[k] = kDone;
-                }
+        for (int k = 0; k < kBatch; ++k) {
+            if (st == kSearching && hit[k]) {
+                found = (int)(idx0 + ids[k]);
+                hu = u[k];
+                hv = v[k];
+                ht = t[k];
+                st = kDone;
             }
         }
-    };
+        if (!__any(st == kSearching)) return false;
+    }
+    return true;
+}
+
+// First-hit search over triangles [begin, begin + count) (Object::intersects' face loop,
+// object.rs:63-78).  A ray still kUndecided when the wave meets its first candidate triangle is
+// resolved by activate(), which must generate its direction (into `d`) and return the
+// bounding-box verdict (object.rs:59-61).  `found` receives the face index relative to
+// `begin`, or stays -1.  kLds: every thread of the workgroup must call it.
+template <bool kCull, bool kLds, typename Scene, typename Activate>
+__device__ void first_hit(const FrameParams& p, const Scene& sc, uint32_t begin, uint32_t count, int& st,
+                          const f3& o, const f3& d, const Bundle& bd, TriHot* s_hot, TriCull* s_cull,
+                          Activate&& activate, int& found, float& hu, float& hv, float& ht) {
+    const uint32_t lane = threadIdx.x & 63;
     // false when no ray of the wave can hit anything in this object any more
     auto resolve = [&]() -> bool {
-        if (any_state(kUndecided)) {
-            bool a[R];
-            activate(a);
-#pragma unroll
-            for (int k = 0; k < R; ++k)
-                if (st[k] == kUndecided) st[k] = a[k] ? kSearching : kDone;
+        if (__any(st == kUndecided)) {
+            const bool a = activate();
+            if (st == kUndecided) st = a ? kSearching : kDone;
         }
-        return any_state(kSearching);
+        return __any(st == kSearching);
     };
     if (!kLds) {
         for (uint32_t base = 0; base < count; base += 64) {
-            if (!__any(not_done())) break;
+            if (!__any(st != kDone)) break;
             unsigned long long mask;
             if (kCull) {
                 const uint32_t j = base + lane;
                 bool keep = false;
-                if (j < count) {
-                    const TriCull c = cache_off != kNotCached ? s_cache[cache_off + j] : p.cull[begin + j];
-                    keep = !cull_rejects(c, bd.xlo, bd.xhi, bd.ylo, bd.yhi);
-                }
+                if (j < count) keep = !cull_rejects(sc.cull(begin + j), bd.xlo, bd.xhi, bd.ylo, bd.yhi);
                 mask = __ballot(keep);
             } else {
                 const uint32_t n = min(64u, count - base);
@@ -386,25 +533,20 @@ __device__ void first_hit(const FrameParams& p, uint32_t begin, uint32_t count, 
             }
             if (!mask) continue;
             if (!resolve()) break;
-            while (mask) {
-                const uint32_t bit = (uint32_t)(__ffsll(mask) - 1);
-                mask &= mask - 1;
-                test(cache_off != kNotCached ? s_hot_cache[cache_off + base + bit] : p.tris[begin + base + bit],
-                     base + bit);
-                if (!any_state(kSearching)) return;
-            }
+            auto hot = [&](uint32_t i) { return sc.hot(begin + base + i); };
+            if (!test_candidates(mask, base, hot, st, o, d, found, hu, hv, ht)) return;
         }
         return;
     }
     for (uint32_t base = 0; base < count; base += kTriTile) {
-        if (!__syncthreads_or(not_done())) break;  // also orders the LDS reuse below
+        if (!__syncthreads_or(st != kDone)) break;  // also orders the LDS reuse below
         const uint32_t n = min((uint32_t)kTriTile, count - base);
         if (threadIdx.x < n) {
             s_hot[threadIdx.x] = p.tris[begin + base + threadIdx.x];
             if (kCull) s_cull[threadIdx.x] = p.cull[begin + base + threadIdx.x];
         }
         __syncthreads();
-        if (!__any(not_done())) continue;
+        if (!__any(st != kDone)) continue;
         for (uint32_t c = 0; c < n; c += 64) {
             unsigned long long mask;
             if (kCull) {
@@ -416,13 +558,8 @@ __device__ void first_hit(const FrameParams& p, uint32_t begin, uint32_t count, 
             }
             if (!mask) continue;
             if (!resolve()) break;
-            while (mask) {
-                const uint32_t bit = (uint32_t)(__ffsll(mask) - 1);
-                mask &= mask - 1;
-                test(s_hot[c + bit], base + c + bit);
-                if (!any_state(kSearching)) break;
-            }
-            if (!any_state(kSearching)) break;
+            auto hot = [&](uint32_t i) { return s_hot[c + i]; };
+            if (!test_candidates(mask, base + c, hot, st, o, d, found, hu, hv, ht)) break;
         }
     }
 }
@@ -431,7 +568,7 @@ __device__ __forceinline__ bool tex_value(const TexView& tv, float x, float y, f
     if (!tv.data) return false;
     const uint32_t ix = sat_u32(x * (float)tv.w) % tv.w;
     const uint32_t iy = sat_u32(y * (float)tv.h) % tv.h;
-    out = tv.data[(size_t)iy * tv.w + ix];
+    out = as_global(tv.data)[(size_t)iy * tv.w + ix];
     return true;
 }
 
@@ -447,52 +584,22 @@ __device__ __forceinline__ f3 camera_dir(const FrameParams& p, uint32_t px, uint
     return normalize(sub(add(add(botleft, mul(horizontal, xf)), mul(vertical, yf)), C));
 }
 
-__device__ __forceinline__ ObjectDesc object_desc(const FrameParams& p, uint32_t oi) {
-    return oi < kInlineObjects ? p.obj_inline[oi] : p.objects[oi];
-}
-__device__ __forceinline__ LightDesc light_desc(const FrameParams& p, uint32_t li) {
-    return li < kInlineLights ? p.light_inline[li] : p.lights[li];
-}
-
 // ---------------------------------------------------------------------- frame kernel -------
 // The image (rank-local rows) is cut into 64 x 4 pixel blocks of four 16 x 4 sub-blocks.  A
-// sub-block inside some object's pixel rectangle (ObjectDesc::rect) is "detail": one wave runs
-// Engine::cast_ray for its 64 pixels, one pixel per lane.  Every other sub-block is background
-// (engine.rs:355-357) with no test at all.  One persistent launch does both, in this order:
-//  1. fill: waves stride over the 64 x 4 blocks and write the background of the non-detail
-//     sub-blocks — a whole block as 3 + 1 + 1 wave-contiguous 16-byte stores.  This is the
-//     frame's HBM-write floor, and the stores drain while the detail work runs;
-//  2. detail: the detail sub-blocks are enumerated rectangle by rectangle (a sub-block in
-//     several rectangles belongs to the first) and dealt out round-robin over the workgroups,
-//     four consecutive ones per workgroup, so the latency-bound shading is spread over all CUs
-//     instead of clustering on the CUs that own the screen region of the object.
-// Small objects' culling, intersection and shading records are cached in LDS per workgroup.
+// sub-block inside one of the frame's detail rectangles (FrameParams::rects: the objects' pixel
+// rectangles, ObjectDesc::rect, in sub-block units) is "detail": one wave runs Engine::cast_ray
+// for its 64 pixels, one pixel per lane.  Every other sub-block is background
+// (engine.rs:355-357) with no test at all.  One persistent launch does both:
+//  * detail: the detail sub-blocks are enumerated rectangle by rectangle (the host makes the
+//    rectangles disjoint) and dealt out round-robin over the first
+//    workgroups, four consecutive ones per workgroup, so the latency-bound shading is spread
+//    over all CUs instead of clustering on the CUs that own the object's screen region;
+//  * fill: the remaining workgroups stride over the 64 x 4 blocks and write the background of
+//    the non-detail sub-blocks — a whole block as 3 + 1 + 1 wave-contiguous 16-byte stores.
+//    This is the frame's HBM-write floor.  Keeping it off the detail workgroups matters: their
+//    loads must not wait behind their own stores (a CDNA wave's vmcnt counts both).
 constexpr uint32_t kBlkW = 64, kBlkH = 4;  // pixel block
 constexpr uint32_t kSubW = 16;             // sub-block width (x kBlkH rows): one wave's pixels
-
-// LDS caches of small objects' records (dynamic shared memory, sized by p.cached_tris):
-// [TriCull x n | TriHot x n | TriShade x n], all 16-byte aligned.
-__device__ __forceinline__ TriCull* cache_cull(char* dyn) { return reinterpret_cast<TriCull*>(dyn); }
-__device__ __forceinline__ TriHot* cache_hot(char* dyn, uint32_t n) {
-    return reinterpret_cast<TriHot*>(dyn + sizeof(TriCull) * n);
-}
-__device__ __forceinline__ TriShade* cache_shade(char* dyn, uint32_t n) {
-    return reinterpret_cast<TriShade*>(dyn + (sizeof(TriCull) + sizeof(TriHot)) * n);
-}
-
-template <bool kCull>
-__device__ void load_caches(const FrameParams& p, char* dyn) {
-    const uint32_t n = p.cached_tris;
-    for (uint32_t oi = 0; oi < p.nobj; ++oi) {
-        const ObjectDesc ob = object_desc(p, oi);
-        if (ob.cache_off == kNotCached) continue;
-        for (uint32_t i = threadIdx.x; i < ob.tri_count; i += kWG) {
-            if (kCull) cache_cull(dyn)[ob.cache_off + i] = p.cull[ob.tri_begin + i];
-            cache_hot(dyn, n)[ob.cache_off + i] = p.tris[ob.tri_begin + i];
-            cache_shade(dyn, n)[ob.cache_off + i] = p.shade[ob.tri_begin + i];
-        }
-    }
-}
 
 __device__ __forceinline__ Bundle make_bundle(const FrameParams& p, uint32_t x0, uint32_t xe,
                                               uint32_t py0, uint32_t pye) {
@@ -504,21 +611,14 @@ __device__ __forceinline__ Bundle make_bundle(const FrameParams& p, uint32_t x0,
                   ((float)(p.row0 + pye) * rh) * hi};
 }
 
-struct SubRect {  // sub-block coordinates (x in kSubW columns, y in kBlkH local rows), inclusive
-    int32_t sx0, sx1, sy0, sy1;
-};
-__device__ __forceinline__ SubRect sub_rect(const FrameParams& p, const ObjectDesc& ob) {
-    const int32_t x0 = ob.rect[0], x1 = min(ob.rect[1], (int32_t)p.cam_w - 1);
-    const int32_t y0 = max(ob.rect[2] - (int32_t)p.row0, 0);
-    const int32_t y1 = min(ob.rect[3] - (int32_t)p.row0, (int32_t)p.rows - 1);
-    if (x0 > x1 || y0 > y1 || !ob.tri_count) return SubRect{1, 0, 1, 0};
-    return SubRect{x0 / (int32_t)kSubW, x1 / (int32_t)kSubW, y0 / (int32_t)kBlkH, y1 / (int32_t)kBlkH};
+// Frame outputs are written once and not read back by the kernel: non-temporal 16-byte stores
+// keep them from evicting the scene and the textures from L2 (the next frame reads those).
+using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void stream16(void* dst, uint4 v) {
+    __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(dst));
 }
-__device__ __forceinline__ uint32_t area(const SubRect& r) {
-    return r.sx0 > r.sx1 ? 0u : (uint32_t)(r.sx1 - r.sx0 + 1) * (uint32_t)(r.sy1 - r.sy0 + 1);
-}
-__device__ __forceinline__ bool inside(const SubRect& r, int32_t sx, int32_t sy) {
-    return sx >= r.sx0 && sx <= r.sx1 && sy >= r.sy0 && sy <= r.sy1;
+__device__ __forceinline__ void stream16(void* dst, float4 v) {
+    stream16(dst, make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)));
 }
 
 // background (engine.rs:355-357) and its bytes: sat_u8(0.1*255) = 25, sat_u8(0.2*255) = 51
@@ -546,17 +646,18 @@ __device__ __forceinline__ void fill_background(const FrameParams& p, uint32_t x
 #pragma unroll
             for (uint32_t i = lane; i < kBlkH * kRow4; i += 64) {
                 const uint32_t r = i / kRow4, c = i % kRow4;
-                reinterpret_cast<float4*>(p.out_rgb + 3 * ((size_t)(py0 + r) * p.img_w + x0))[c] = bg_rgb4(c % 3);
+                stream16(reinterpret_cast<float4*>(p.out_rgb + 3 * ((size_t)(py0 + r) * p.img_w + x0)) + c, bg_rgb4(c % 3));
             }
         }
         if (p.out_ppm && lane < kBlkH * kRow16) {
             const uint32_t r = lane / kRow16, c = lane % kRow16;
             const size_t row = (size_t)(p.rows - py0 - kBlkH + r);  // file rows, bottom-up
-            reinterpret_cast<uint4*>(p.out_ppm + 3 * (row * p.img_w + x0))[c] = bg_ppm16(c % 3);
+            stream16(reinterpret_cast<uint4*>(p.out_ppm + 3 * (row * p.img_w + x0)) + c, bg_ppm16(c % 3));
         }
         if (p.out_face && lane < kBlkH * kFace4) {
             const uint32_t r = lane / kFace4, c = lane % kFace4;
-            reinterpret_cast<int4*>(p.out_face + (size_t)(py0 + r) * p.img_w + x0)[c] = make_int4(-1, -1, -1, -1);
+            stream16(reinterpret_cast<int4*>(p.out_face + (size_t)(py0 + r) * p.img_w + x0) + c,
+                     make_uint4(~0u, ~0u, ~0u, ~0u));
         }
     } else {  // image edge or unaligned output: per pixel
         const float4 b = bg_rgb4(0);
@@ -582,95 +683,102 @@ __device__ __forceinline__ void fill_background(const FrameParams& p, uint32_t x
     }
 }
 
+// the pixel rectangle of `ob` (camera rows) meets the sub-block's pixels
+__device__ __forceinline__ bool rect_meets(const ObjGeom& ob, const FrameParams& p, uint32_t wx0, uint32_t py0) {
+    const int32_t x0 = (int32_t)wx0, y0 = (int32_t)(p.row0 + py0);
+    return ob.rect[0] <= x0 + (int32_t)kSubW - 1 && ob.rect[1] >= x0 && ob.rect[2] <= y0 + (int32_t)kBlkH - 1 &&
+           ob.rect[3] >= y0;
+}
+
 // Engine::cast_ray for the 16 x 4 pixels at (wx0, py0) (rank-local rows), one pixel per lane;
 // `active` false: the wave only takes part in the workgroup's LDS-tile barriers.
-template <bool kCull, bool kLdsTiles, bool kSpecPow>
-__device__ __forceinline__ void render_sub(const FrameParams& p, uint32_t wx0, uint32_t py0, bool active,
-                                           TriHot* s_hot, TriCull* s_cull, float4* s_rgb, uint32_t* s_ppm,
-                                           const TriCull* c_cull, const TriHot* c_hot, const TriShade* c_shade,
-                                           bool aligned) {
+template <bool kCull, bool kLdsTiles, bool kSpecPow, typename Scene>
+__device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc, uint32_t wx0, uint32_t py0,
+                                           bool active, TriHot* s_hot, TriCull* s_cull, float4* s_rgb,
+                                           uint32_t* s_ppm, bool aligned) {
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const f3 C = mk3(p.cx, p.cy, p.cz);
     const uint32_t px = wx0 + (lane % kSubW), ly = lane / kSubW;
     const uint32_t py = py0 + ly;
     const bool valid = active && px < p.cam_w && py < p.rows;
     const uint32_t y = p.row0 + py;
-    const int32_t sx = (int32_t)(wx0 / kSubW), sy = (int32_t)(py0 / kBlkH);
     const Bundle bd = make_bundle(p, wx0, min(wx0 + kSubW - 1, p.cam_w - 1), py0, min(py0 + kBlkH - 1, p.rows - 1));
 
     // ---- cast_ray (engine.rs:112-216): closest object among first hits -----------
-    f3 d[1] = {mk3(0.0f, 0.0f, 0.0f)};
+    f3 d = mk3(0.0f, 0.0f, 0.0f);
     bool ray_ready = false;
     bool have = false;
     float closest = 0.0f, bu = 0.0f, bv = 0.0f, bt = 0.0f;
     uint32_t best_obj = 0;
     int best_face = -1;
     for (uint32_t oi = 0; oi < p.nobj; ++oi) {
-        const ObjectDesc ob = object_desc(p, oi);  // uniform: scalar loads
+        const ObjGeom ob = sc.geom(oi);  // uniform
         const bool direct = !kLdsTiles || ob.tri_count <= kDirectMax;
         // outside the object's pixel rectangle no primary ray can hit it
-        if (kCull && direct && !inside(sub_rect(p, ob), sx, sy)) continue;
-        auto activate = [&](bool (&a)[1]) {
+        if (kCull && direct && !rect_meets(ob, p, wx0, py0)) continue;
+        auto activate = [&]() {
             if (!ray_ready) {
                 uint32_t pxo = px, yo = y;  // opaque: keep ray generation on this path
                 asm volatile("" : "+v"(pxo), "+v"(yo));
-                d[0] = camera_dir(p, pxo, yo);
+                d = camera_dir(p, pxo, yo);
                 ray_ready = true;
             }
-            a[0] = bbox_hit(ob, C, d[0]);
+            return bbox_hit(ob, C, d);
         };
-        int st[1] = {valid ? kUndecided : kDone}, f[1] = {-1};
-        float u[1], v[1], t[1];
+        int st = valid ? kUndecided : kDone, f = -1;
+        float u, v, t;
         if (direct)
-            first_hit<kCull, false, 1>(p, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull,
-                                       activate, f, u, v, t, c_cull, ob.cache_off, c_hot);
+            first_hit<kCull, false>(p, sc, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull, activate, f, u,
+                                    v, t);
         else
-            first_hit<kCull, kLdsTiles, 1>(p, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot,
-                                           s_cull, activate, f, u, v, t);
-        if (f[0] >= 0) {
-            const f3 P = add(C, mul(d[0], t[0]));
+            first_hit<kCull, kLdsTiles>(p, sc, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull, activate,
+                                        f, u, v, t);
+        if (f >= 0) {
+            const f3 P = add(C, mul(d, t));
             const float dsq = len_sq(sub(P, C));
             if (!have || dsq < closest) {  // strict `<`: the first object wins ties
                 have = true;
                 closest = dsq;
                 best_obj = oi;
-                best_face = f[0];
-                bu = u[0];
-                bv = v[0];
-                bt = t[0];
+                best_face = f;
+                bu = u;
+                bv = v;
+                bt = t;
             }
         }
     }
 
+    ERAY_TRACE(2);
     // ---- hit data and Material::get (material.rs:56-94) --------------------------
     f3 P = mk3(0.0f, 0.0f, 0.0f), N = mk3(0.0f, 0.0f, 0.0f);
     rgb color{0.0f, 0.0f, 0.0f};
     float kd = 0.5f, ks = 0.5f, sp = 1.0f;
-    for (uint32_t oi = 0; oi < p.nobj; ++oi) {  // per-lane object, read from scalar copies
+    for (uint32_t oi = 0; oi < p.nobj; ++oi) {  // per-lane object, read from uniform copies
         if (!__any(have && best_obj == oi)) continue;
-        const ObjectDesc ob = object_desc(p, oi);
+        const ObjGeom ob = sc.geom(oi);
+        const MaterialDesc mat = sc.mat(oi);
         if (!(have && best_obj == oi)) continue;
-        const TriShade sh = ob.cache_off != kNotCached ? c_shade[ob.cache_off + (uint32_t)best_face]
-                                                       : p.shade[ob.tri_begin + (uint32_t)best_face];
-        P = add(C, mul(d[0], bt));
+        const TriShade sh = sc.shade(ob.tri_begin + (uint32_t)best_face);
+        P = add(C, mul(d, bt));
         const f3 na = mk3(sh.s0.x, sh.s0.y, sh.s0.z), nb = mk3(sh.s0.w, sh.s1.x, sh.s1.y);
         const f3 nc = mk3(sh.s1.z, sh.s1.w, sh.s2.x);
         N = normalize(add(add(mul(na, bu), mul(nb, bv)), mul(nc, bt)));
         const float w = 1.0f - bu - bv;
         const float uv0 = ((sh.s2.y * w) + (sh.s2.w * bu)) + (sh.s3.y * bv);
         const float uv1 = ((sh.s2.z * w) + (sh.s3.x * bu)) + (sh.s3.z * bv);
-        if (ob.mat.color.data) {
-            const TexView& tv = ob.mat.color;
+        if (mat.color.data) {
+            const TexView& tv = mat.color;
             const uint32_t ix = sat_u32(uv0 * (float)tv.w) % tv.w;
             const uint32_t iy = sat_u32(uv1 * (float)tv.h) % tv.h;
-            const float* c = tv.data + 3 * ((size_t)iy * tv.w + ix);
+            const auto* c = as_global(tv.data) + 3 * ((size_t)iy * tv.w + ix);
             color = rgb{c[0], c[1], c[2]};
         }
-        tex_value(ob.mat.diffuse, uv0, uv1, kd);
-        tex_value(ob.mat.specular, uv0, uv1, ks);
-        if (kSpecPow) tex_value(ob.mat.specular_power, uv0, uv1, sp);
+        tex_value(mat.diffuse, uv0, uv1, kd);
+        tex_value(mat.specular, uv0, uv1, ks);
+        if (kSpecPow) tex_value(mat.specular_power, uv0, uv1, sp);
     }
 
+    ERAY_TRACE(3);
     bool any = false;  // the lighting list as a running left fold (color.rs:82-87)
     rgb acc{0.0f, 0.0f, 0.0f};
     auto push = [&](rgb c) {
@@ -682,33 +790,33 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, uint32_t wx0, u
         }
     };
     for (uint32_t li = 0; li < p.nlights; ++li) {
-        const LightDesc L = light_desc(p, li);
+        const LightDesc L = sc.light(li);
         if (L.variant == 1) continue;  // point lights first (engine.rs:274-279)
         const f3 Lp = mk3(L.pos[0], L.pos[1], L.pos[2]);
         // reaches_light(Ray::new(P + N * 0.1, Lp - P)) (engine.rs:280-286, 218-228)
         f3 S = mk3(0.0f, 0.0f, 0.0f);
-        f3 sd[1] = {mk3(0.0f, 0.0f, 1.0f)};
+        f3 sd = mk3(0.0f, 0.0f, 1.0f);
         float dist = 0.0f;
         if (have) {
             S = add(P, mul(N, 0.1f));
-            sd[0] = normalize(sub(Lp, P));
+            sd = normalize(sub(Lp, P));
             dist = len(sub(Lp, S));
         }
         bool reached = true, decided = false;
         for (uint32_t oj = 0; oj < p.nobj; ++oj) {
-            const ObjectDesc ob = object_desc(p, oj);
-            int st[1] = {(have && !decided && bbox_hit(ob, S, sd[0])) ? kSearching : kDone};
-            int f[1] = {-1};
-            float u[1], v[1], t[1];
-            auto never = [](bool (&a)[1]) { a[0] = false; };
+            const ObjGeom ob = sc.geom(oj);
+            int st = (have && !decided && bbox_hit(ob, S, sd)) ? kSearching : kDone;
+            int f = -1;
+            float u, v, t;
+            auto never = []() { return false; };
             if (!kLdsTiles || ob.tri_count <= kDirectMax)
-                first_hit<false, false, 1>(p, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot, s_cull,
-                                           never, f, u, v, t, c_cull, ob.cache_off, c_hot);
+                first_hit<false, false>(p, sc, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot, s_cull, never, f, u,
+                                        v, t);
             else
-                first_hit<false, kLdsTiles, 1>(p, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot,
-                                               s_cull, never, f, u, v, t);
-            if (f[0] >= 0) {
-                const f3 hp = add(S, mul(sd[0], t[0]));
+                first_hit<false, kLdsTiles>(p, sc, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot, s_cull, never,
+                                            f, u, v, t);
+            if (f >= 0) {
+                const f3 hp = add(S, mul(sd, t));
                 reached = len(sub(hp, S)) > dist;
                 decided = true;
             }
@@ -721,7 +829,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, uint32_t wx0, u
             const rgb lc{L.color[0], L.color[1], L.color[2]};
             const rgb diffusion =
                 cmul(cmul(cmul(cmul(cmulc(color, lc), kd), prod), L.brightness), falloff);
-            const f3 reflected = sub(d[0], mul(mul(N, 2.0f), dot0(d[0], N)));
+            const f3 reflected = sub(d, mul(mul(N, 2.0f), dot0(d, N)));
             const float dotr = dot0(normalize(reflected), normalize(LmP));
             // specular_power defaults to 1 and powf(x, 1) == x; pow only when a
             // material has a specular-power output (kSpecPow)
@@ -734,7 +842,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, uint32_t wx0, u
     }
     if (have) {
         for (uint32_t li = 0; li < p.nlights; ++li) {  // ambient lights (engine.rs:341-352)
-            const LightDesc L = light_desc(p, li);
+            const LightDesc L = sc.light(li);
             if (L.variant != 1) continue;
             const rgb m{rust_min(L.color[0], color.r), rust_min(L.color[1], color.g),
                         rust_min(L.color[2], color.b)};
@@ -744,6 +852,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, uint32_t wx0, u
         push(rgb{0.1f, 0.1f, 0.2f});  // engine.rs:355-357
     }
 
+    ERAY_TRACE(4);
     // ---- outputs: Image::set + Color::as_bytes, rows bottom-up (image.rs:41-74) ---
     const uint32_t b0 = sat_u8(acc.r * 255.0f), b1 = sat_u8(acc.g * 255.0f), b2 = sat_u8(acc.b * 255.0f);
     if (valid && p.out_face) p.out_face[(size_t)py * p.img_w + px] = have ? best_face : -1;
@@ -769,13 +878,13 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, uint32_t wx0, u
         if (p.out_rgb && lane < kBlkH * kRgbRow4) {
             const uint32_t r = lane / kRgbRow4, c = lane % kRgbRow4;
             float4* dst = reinterpret_cast<float4*>(p.out_rgb + 3 * ((size_t)(py0 + r) * p.img_w + wx0)) + c;
-            *dst = reinterpret_cast<const float4*>(wrgb)[lane];
+            stream16(dst, reinterpret_cast<const float4*>(wrgb)[lane]);
         }
         if (p.out_ppm && lane < kBlkH * kPpmRow16) {
             const uint32_t r = lane / kPpmRow16, c = lane % kPpmRow16;  // r-th byte row of the block
             const size_t row = (size_t)(p.rows - py0 - kBlkH + r);
             uint4* dst = reinterpret_cast<uint4*>(p.out_ppm + 3 * (row * p.img_w + wx0)) + c;
-            *dst = reinterpret_cast<const uint4*>(wppm)[lane];
+            stream16(dst, reinterpret_cast<const uint4*>(wppm)[lane]);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next block
@@ -795,9 +904,21 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, uint32_t wx0, u
             o[2] = (uint8_t)b2;
         }
     }
+    ERAY_TRACE(5);
 }
 
-template <bool kCull, bool kLdsTiles, bool kSpecPow>
+// detail rectangle k of the frame (kernel arguments, uniform index: scalar loads)
+struct SubRect {  // sub-block coordinates (x in kSubW columns, y in kBlkH local rows), inclusive
+    int32_t sx0, sx1, sy0, sy1;
+};
+__device__ __forceinline__ SubRect frame_rect(const FrameParams& p, uint32_t k) {
+    return SubRect{p.rects[k][0], p.rects[k][1], p.rects[k][2], p.rects[k][3]};
+}
+__device__ __forceinline__ bool inside(const SubRect& r, int32_t sx, int32_t sy) {
+    return sx >= r.sx0 && sx <= r.sx1 && sy >= r.sy0 && sy <= r.sy1;
+}
+
+template <bool kCull, bool kLdsTiles, bool kSpecPow, bool kLdsScene>
 __global__ void __launch_bounds__(kWG) frame_kernel(FrameParams p) {
     __shared__ TriHot s_hot[kLdsTiles ? kTriTile : 1];
     __shared__ TriCull s_cull[(kCull && kLdsTiles) ? kTriTile : 1];
@@ -809,74 +930,80 @@ __global__ void __launch_bounds__(kWG) frame_kernel(FrameParams p) {
     const bool aligned = (p.img_w % 16) == 0 &&
                          ((reinterpret_cast<uintptr_t>(p.out_rgb) | reinterpret_cast<uintptr_t>(p.out_ppm) |
                            reinterpret_cast<uintptr_t>(p.out_face)) & 15) == 0;
-    const uint32_t by_n = (p.rows + kBlkH - 1) / kBlkH;
+    const uint32_t total = p.total_sub;  // detail sub-blocks
+    // workgroups [0, nd) render the detail sub-blocks, the others write the background; when
+    // every workgroup has detail work, all of them fill afterwards
+    const uint32_t nd = min(gridDim.x, (total + nwaves - 1) / nwaves);
+    ERAY_TRACE(0);
 
-    // ---- 1. background of the non-detail sub-blocks ------------------------------------
-    if (kCull) {
-        const uint32_t nblk = p.tiles_x * by_n;
-        for (uint32_t blk = wave * gridDim.x + blockIdx.x; blk < nblk; blk += gridDim.x * nwaves) {
-            const uint32_t bx = blk % p.tiles_x, by = blk / p.tiles_x;
-            uint32_t mask = 0;  // detail sub-blocks of this block
-            for (uint32_t oi = 0; oi < p.nobj; ++oi) {
-                const SubRect r = sub_rect(p, object_desc(p, oi));
-                if ((int32_t)by < r.sy0 || (int32_t)by > r.sy1) continue;
-#pragma unroll
-                for (int32_t i = 0; i < 4; ++i) {
-                    const int32_t sx = (int32_t)(4 * bx) + i;
-                    mask |= (sx >= r.sx0 && sx <= r.sx1) ? (1u << i) : 0u;
-                }
-            }
-            if (!mask) {
-                fill_background<kBlkW>(p, bx * kBlkW, by * kBlkH, aligned, lane);
-            } else if (mask != 0xfu) {
-                for (uint32_t i = 0; i < 4; ++i)
-                    if (!((mask >> i) & 1u)) fill_background<kSubW>(p, bx * kBlkW + i * kSubW, by * kBlkH, aligned, lane);
-            }
-        }
-    }
-
-    // ---- 2. detail sub-blocks --------------------------------------------------------------
-    const uint32_t n_cached = p.cached_tris;
-    if (n_cached) load_caches<kCull>(p, dyn);
-    __syncthreads();
-    const TriCull* c_cull = cache_cull(dyn);
-    const TriHot* c_hot = cache_hot(dyn, n_cached);
-    const TriShade* c_shade = cache_shade(dyn, n_cached);
-    uint32_t total = 0;
-    if (kCull) {
-        for (uint32_t oi = 0; oi < p.nobj; ++oi) total += area(sub_rect(p, object_desc(p, oi)));
-    } else {
-        total = ((p.cam_w + kSubW - 1) / kSubW) * by_n;  // brute force: every sub-block
-    }
-    for (uint32_t c = blockIdx.x * nwaves; c < total; c += gridDim.x * nwaves) {  // workgroup-uniform
-        uint32_t j = c + wave;
-        bool active = j < total;
-        int32_t sx = 0, sy = 0;
-        if (active) {
-            if (kCull) {
-                for (uint32_t oi = 0; oi < p.nobj; ++oi) {
-                    const SubRect r = sub_rect(p, object_desc(p, oi));
-                    const uint32_t a = area(r);
-                    if (j >= a) {
+    // ---- detail sub-blocks -------------------------------------------------------------------
+    if (blockIdx.x < nd) {
+        auto detail = [&](const auto& sc) {
+            for (uint32_t c = blockIdx.x * nwaves; c < total; c += gridDim.x * nwaves) {  // workgroup-uniform
+                uint32_t j = c + wave;
+                bool active = j < total;
+                int32_t sx = 0, sy = 0;
+                if (active) {
+                    // the rectangles are disjoint (host): find j's by area
+                    for (uint32_t k = 0; k < p.nrect; ++k) {
+                        const SubRect r = frame_rect(p, k);
+                        const uint32_t w = (uint32_t)(r.sx1 - r.sx0 + 1);
+                        const uint32_t a = w * (uint32_t)(r.sy1 - r.sy0 + 1);
+                        if (j < a) {
+                            sx = r.sx0 + (int32_t)(j % w);
+                            sy = r.sy0 + (int32_t)(j / w);
+                            break;
+                        }
                         j -= a;
-                        continue;
                     }
-                    const uint32_t w = (uint32_t)(r.sx1 - r.sx0 + 1);
-                    sx = r.sx0 + (int32_t)(j % w);
-                    sy = r.sy0 + (int32_t)(j / w);
-                    for (uint32_t ok = 0; ok < oi; ++ok)  // owned by an earlier rectangle
-                        if (inside(sub_rect(p, object_desc(p, ok)), sx, sy)) active = false;
-                    break;
                 }
-            } else {
-                const uint32_t w = (p.cam_w + kSubW - 1) / kSubW;
-                sx = (int32_t)(j % w);
-                sy = (int32_t)(j / w);
+                render_sub<kCull, kLdsTiles, kSpecPow>(p, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH, active,
+                                                       s_hot, s_cull, s_rgb, s_ppm, aligned);
+#ifdef ERAY_PHASE_TRACE_REPEAT  // diagnostics: the same sub-block again, instruction cache warm
+                ERAY_TRACE(6);
+                render_sub<kCull, kLdsTiles, kSpecPow>(p, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH, active,
+                                                       s_hot, s_cull, s_rgb, s_ppm, aligned);
+#endif
+            }
+        };
+        if constexpr (kLdsScene) {
+            const SceneLds sc = preload_scene(p, dyn);
+            __syncthreads();
+            ERAY_TRACE(1);
+            detail(sc);
+        } else {
+            const SceneGlobal sc{p};
+            ERAY_TRACE(1);
+            detail(sc);
+        }
+        ERAY_TRACE(7);
+        if (nd < gridDim.x) return;
+    }
+
+    // ---- background of the non-detail sub-blocks ---------------------------------------------
+    const uint32_t nf = nd < gridDim.x ? gridDim.x - nd : gridDim.x;  // filling workgroups
+    const uint32_t f = nd < gridDim.x ? blockIdx.x - nd : blockIdx.x;
+    const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
+    for (uint32_t blk = wave * nf + f; blk < nblk; blk += nf * nwaves) {
+        const uint32_t bx = blk % p.tiles_x, by = blk / p.tiles_x;
+        uint32_t mask = 0;  // detail sub-blocks of this block
+        for (uint32_t k = 0; k < p.nrect; ++k) {
+            const SubRect r = frame_rect(p, k);
+            if ((int32_t)by < r.sy0 || (int32_t)by > r.sy1) continue;
+#pragma unroll
+            for (int32_t i = 0; i < 4; ++i) {
+                const int32_t sx = (int32_t)(4 * bx) + i;
+                mask |= (sx >= r.sx0 && sx <= r.sx1) ? (1u << i) : 0u;
             }
         }
-        render_sub<kCull, kLdsTiles, kSpecPow>(p, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH, active, s_hot, s_cull,
-                                               s_rgb, s_ppm, c_cull, c_hot, c_shade, aligned);
+        if (!mask) {
+            fill_background<kBlkW>(p, bx * kBlkW, by * kBlkH, aligned, lane);
+        } else if (mask != 0xfu) {
+            for (uint32_t i = 0; i < 4; ++i)
+                if (!((mask >> i) & 1u)) fill_background<kSubW>(p, bx * kBlkW + i * kSubW, by * kBlkH, aligned, lane);
+        }
     }
+    ERAY_TRACE(8);
 }
 
 // Image<Color>::save_as_ppm body: byte row k = image row h-1-k.
@@ -910,6 +1037,13 @@ hipError_t launch_tri_cull(const TriHot* hot, uint32_t T, float cx, float cy, fl
     return hipGetLastError();
 }
 
+#ifdef ERAY_PHASE_TRACE
+extern "C" int eray_debug_trace(uint64_t* out, size_t n) {
+    if (n > sizeof(g_trace) / sizeof(uint64_t)) n = sizeof(g_trace) / sizeof(uint64_t);
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace), n * sizeof(uint64_t)) == hipSuccess ? 0 : -2;
+}
+#endif
+
 hipError_t launch_tri_rect(const TriCull* cull, uint32_t T, uint32_t cam_w, uint32_t cam_h, uint32_t* acc,
                            hipStream_t s) {
     if (!T) return hipSuccess;
@@ -920,7 +1054,7 @@ hipError_t launch_tri_rect(const TriCull* cull, uint32_t T, uint32_t cam_w, uint
 namespace {
 // Persistent grid: as many workgroups as are resident at once (occupancy API), capped by the
 // work (fill blocks or detail sub-blocks, whichever needs more workgroups).
-template <bool C, bool L, bool S>
+template <bool C, bool L, bool S, bool K>
 hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, hipStream_t s) {
     static int per_cu = -1, cus = 0;
     static size_t per_cu_dyn = 0;
@@ -929,14 +1063,27 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, frame_kernel<C, L, S>, kWG, dyn) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, frame_kernel<C, L, S, K>, kWG, dyn) !=
+                hipSuccess ||
             per_cu <= 0)
             per_cu = 1;
         per_cu_dyn = dyn;
     }
     const uint32_t grid = min(want, (uint32_t)(per_cu * cus));
-    frame_kernel<C, L, S><<<grid, kWG, dyn, s>>>(p);
+    frame_kernel<C, L, S, K><<<grid, kWG, dyn, s>>>(p);
     return hipGetLastError();
+}
+
+template <bool C, bool S>
+hipError_t launch_frame_cs(const FrameParams& p, uint32_t want, hipStream_t s) {
+    // small scenes are preloaded into LDS whole (no object then needs the LDS tiles); otherwise
+    // everything is read from the device arrays
+    if (p.lds_scene) {
+        const size_t dyn = scene_lds_layout(p.nobj, p.nlights, p.total_tris, C).bytes;
+        return launch_frame_kernel<C, false, S, true>(p, want, dyn, s);
+    }
+    if (p.max_object_tris > kDirectMax) return launch_frame_kernel<C, true, S, false>(p, want, 0, s);
+    return launch_frame_kernel<C, false, S, false>(p, want, 0, s);
 }
 }  // namespace
 
@@ -944,20 +1091,10 @@ hipError_t launch_render(const FrameParams& p, hipStream_t s) {
     const uint32_t by_n = (p.rows + kBlkH - 1) / kBlkH;
     const uint32_t nblk = p.tiles_x * by_n;
     if (!nblk) return hipSuccess;
-    const uint32_t nsub = ((p.cam_w + kSubW - 1) / kSubW) * by_n;
-    const uint32_t want = p.cull ? (nblk + 3) / 4 : (nsub + 3) / 4;
-    const size_t dyn = (size_t)p.cached_tris * (sizeof(TriCull) + sizeof(TriHot) + sizeof(TriShade));
-    const bool lds = p.max_object_tris > kDirectMax, sp = p.spec_pow != 0;
-    if (p.cull) {
-        if (lds) return sp ? launch_frame_kernel<true, true, true>(p, want, dyn, s)
-                           : launch_frame_kernel<true, true, false>(p, want, dyn, s);
-        return sp ? launch_frame_kernel<true, false, true>(p, want, dyn, s)
-                  : launch_frame_kernel<true, false, false>(p, want, dyn, s);
-    }
-    if (lds) return sp ? launch_frame_kernel<false, true, true>(p, want, dyn, s)
-                       : launch_frame_kernel<false, true, false>(p, want, dyn, s);
-    return sp ? launch_frame_kernel<false, false, true>(p, want, dyn, s)
-              : launch_frame_kernel<false, false, false>(p, want, dyn, s);
+    // enough workgroups for one fill block or one round of detail sub-blocks per wave
+    const uint32_t want = max((nblk + 3) / 4, (p.total_sub + 3) / 4);
+    if (p.cull) return p.spec_pow ? launch_frame_cs<true, true>(p, want, s) : launch_frame_cs<true, false>(p, want, s);
+    return p.spec_pow ? launch_frame_cs<false, true>(p, want, s) : launch_frame_cs<false, false>(p, want, s);
 }
 
 hipError_t launch_pack_ppm(const float* rgb, uint32_t w, uint32_t h, uint8_t* out, hipStream_t s) {
