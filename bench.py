@@ -31,6 +31,7 @@ import torch  # noqa: E402  (imported before the HIP library: one HIP runtime pe
 import torch.distributed as dist  # noqa: E402
 
 from eray_amd import capi  # noqa: E402
+from eray_amd.dist import gather_ppm_rows, row_block  # noqa: E402
 from eray_amd.frame import MainScene  # noqa: E402
 from eray_amd.objfile import load_obj_file  # noqa: E402
 
@@ -52,6 +53,18 @@ def algorithmic_bytes(hit_pixels: int, pixels: int, triangles: int) -> int:
     15 B/pixel written (12 B f32 RGB + 3 B PPM), 16 B of texels read per hit (IColor 12 + IValue 4),
     and the triangle records once (48 B hot + 64 B culling + 64 B shading)."""
     return 15 * pixels + 16 * hit_pixels + (48 + 64 + 64) * triangles
+
+
+def pmc_traffic():
+    """HBM bytes per frame-kernel launch from the committed rocprofv3 counter summary of this
+    workload (scripts/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
+    MI355X_MICROARCH.md), or None when no summary is committed."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return int(json.load(f)["frame_kernel"]["hbm_bytes_per_launch"])
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def cpu_baseline(mesh, seconds: float = 10.0) -> dict:
@@ -107,8 +120,7 @@ def main() -> None:
     t_mat = time.perf_counter() - t_mat0
 
     # rank r renders the r-th block of PPM file rows: camera rows [H - (r+1)*h, H - r*h)
-    rows = HEIGHT_PER_GPU
-    row0 = H_total - (rank + 1) * rows
+    row0, rows = row_block(rank, world, HEIGHT_PER_GPU)
     rgb = torch.empty((rows, WIDTH, 3), dtype=torch.float32, device="cuda")
     ppm = torch.empty((rows, WIDTH, 3), dtype=torch.uint8, device="cuda")
     face = torch.empty((rows, WIDTH), dtype=torch.int32, device="cuda")
@@ -122,7 +134,7 @@ def main() -> None:
         if ev is not None:
             ev[1].record()
         if world > 1:
-            dist.gather(ppm, list(frame.chunk(world, 0)) if rank == 0 else None, dst=0)
+            gather_ppm_rows(ppm, frame, world, rank)
 
     # one untimed instrumented frame: hit count for the algorithmic-bytes model
     scene.render(out_rgb=rgb.data_ptr(), out_face=face.data_ptr(), row0=row0, rows=rows, flags=flags)
@@ -141,10 +153,9 @@ def main() -> None:
     t0 = time.perf_counter()
     if world == 1:
         # the frame loop runs inside the library, replayed from a HIP graph (no per-frame host
-        # round trip); HIP events bracketing the frames give the mean device time per frame
-        kernel_ms = scene.ctx.render_frames(args.steps, WIDTH, H_total, row0=row0, rows=rows,
-                                            out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr(),
-                                            flags=flags, timed=True)
+        # round trip)
+        scene.ctx.render_frames(args.steps, WIDTH, H_total, row0=row0, rows=rows, out_rgb=rgb.data_ptr(),
+                                out_ppm=ppm.data_ptr(), flags=flags)
     else:
         events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                   for _ in range(args.steps)]
@@ -163,6 +174,11 @@ def main() -> None:
         dist.all_reduce(h)
         hits_all = int(h.item())
     else:
+        # the frame kernel's own duration: the same frames once more, each launch bracketed by
+        # HIP events on the library's stream (the graph replay above leaves no room for them)
+        kernel_ms = scene.ctx.render_frames(args.steps, WIDTH, H_total, row0=row0, rows=rows,
+                                            out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr(), flags=flags,
+                                            timed=True)
         hits_all = hits
 
     if rank == 0:
@@ -208,9 +224,10 @@ def main() -> None:
                 "peak": PEAK_HBM_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4),
-                "traffic": None,
-                "kernel": "render_kernel<true> (eray_amd/csrc/render.hip)",
+                "traffic": pmc_traffic(),
+                "kernel": "frame_kernel (eray_amd/csrc/render.hip)",
                 "algorithmic_bytes_per_launch": alg,
+                "kernel_ms": round(kernel_ms, 6),
             },
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -1,6 +1,7 @@
 """Diagnostic timings of the frame kernel on controlled scenes (not part of the product)."""
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -22,8 +23,13 @@ def timed(label, flags=0, frames=200, row0=0, rows=H, ppm_out=True):
     kw = dict(row0=row0, rows=rows, out_rgb=rgb.ptr, out_ppm=ppm.ptr if ppm_out else None, flags=flags)
     ctx.render_frames(frames, W, H, prepare_only=True, **kw)
     ctx.render_frames(20, W, H, **kw)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    ctx.render_frames(frames, W, H, **kw)
+    ctx.synchronize()
+    wall = (time.perf_counter() - t0) / frames
     ms = ctx.render_frames(frames, W, H, timed=True, **kw)
-    print(f"{label:48s} {ms * 1e3:8.2f} us", flush=True)
+    print(f"{label:48s} frame {wall * 1e6:8.2f} us   kernel {ms * 1e3:8.2f} us", flush=True)
 
 
 sc = MainScene(ctx, *mesh, W, H)

@@ -8,7 +8,7 @@ ARGS=${BENCH_ARGS:---steps 50 --warmup 5 --no-cpu-baseline}
 pass() {  # name counters...
   local name=$1; shift
   echo "=== pmc $name: $*"
-  timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex 'fill_kernel|detail_kernel' \
+  timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex 'frame_kernel' \
       --output-format csv -d gpurun_out/pmc/$name -o $name -- python bench.py $ARGS \
       > gpurun_out/pmc/$name.log 2>&1
   local rc=$?

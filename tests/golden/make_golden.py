@@ -1,0 +1,74 @@
+"""Generates the committed golden fixtures of tests/golden/ from the CPU oracle (oracle/, the
+literal restatement of the reference's arithmetic, itself pinned by the reference's own known
+answers in tests/test_oracle_known_answers.py).  The reference (Rust) cannot be built here
+(SURVEY.md §8c), so these fixtures freeze the oracle's outputs: the GPU path and any later
+oracle change are checked against the same bytes.
+
+    python tests/golden/make_golden.py
+
+Fixtures
+  cube_c1_256.npz   C1 (cube.obj, 256x256, main.rs scene): the PPM body bytes (file order),
+                    the hit face per pixel, and the f32 RGB of the hit pixels (indices + values)
+  digests.json      SHA-256 of the PPM body and of the f32 image for C1 and for C2
+                    (1920x1080), the per-frame hit/test counters, and the P6 headers
+  texture_8x4.npz   the example material graph (wave -> rgb -> mix with flat) at 8x4 texels:
+                    color and diffuse images
+"""
+import hashlib
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+from eray_amd.objfile import load_obj_file  # noqa: E402
+from oracle import pyoracle as O  # noqa: E402
+
+
+def frame(mesh, w, h, fov):
+    scene = O.main_rs_scene(*mesh, texture=1024)
+    cam = O.camera((0.0, 0.0, 5.0), fov, w, 1.0)
+    assert O.camera_size(cam) == (w, h)
+    rgb, face, stats = O.render(scene, cam, want_faces=True)
+    return rgb, face, stats
+
+
+def main() -> None:
+    mesh = load_obj_file(os.path.join(ROOT, "objects", "cube.obj"))
+    digests = {}
+    for tag, (w, h, fov) in {"c1": (256, 256, (60.0, 60.0)), "c2": (1920, 1080, (16.0, 9.0))}.items():
+        rgb, face, stats = frame(mesh, w, h, fov)
+        full = O.ppm_bytes(rgb)  # the whole P6 file: header + body
+        header = f"P6 {w} {h} 255\n".encode()
+        assert full.startswith(header)
+        body = full[len(header):]
+        digests[tag] = {
+            "width": w, "height": h, "fov": list(fov),
+            "ppm_header": f"P6 {w} {h} 255\n",
+            "ppm_body_sha256": hashlib.sha256(body).hexdigest(),
+            "ppm_file_sha256": hashlib.sha256(full).hexdigest(),
+            "rgb_f32_sha256": hashlib.sha256(np.ascontiguousarray(rgb, np.float32).tobytes()).hexdigest(),
+            "face_sha256": hashlib.sha256(np.ascontiguousarray(face, np.int32).tobytes()).hexdigest(),
+            "hit_pixels": int((face >= 0).sum()),
+            "stats": {k: int(v) for k, v in stats.items()},
+        }
+        if tag == "c1":
+            hit = np.flatnonzero(face.reshape(-1) >= 0).astype(np.int32)
+            np.savez_compressed(os.path.join(HERE, "cube_c1_256.npz"),
+                                ppm=np.frombuffer(body, np.uint8).reshape(h, w, 3),
+                                face=face.astype(np.int16),
+                                hit_index=hit,
+                                hit_rgb=rgb.reshape(-1, 3)[hit].astype(np.float32))
+    with open(os.path.join(HERE, "digests.json"), "w") as f:
+        json.dump(digests, f, indent=2, sort_keys=True)
+    color, diffuse = O.example_material(8, 4)
+    np.savez_compressed(os.path.join(HERE, "texture_8x4.npz"), color=color, diffuse=diffuse)
+    print("wrote", sorted(os.listdir(HERE)))
+
+
+if __name__ == "__main__":
+    main()
