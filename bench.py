@@ -8,10 +8,11 @@
 Workload (BASELINE.json configs[1]): objects/cube.obj with src/main.rs's scene
 and material graph, 1920x1080 per GPU.  One step = one frame: every rank renders its 1080-row
 tile of a 1920 x (1080*N) frame (camera rays, first-hit triangle scan, shading with shadow rays)
-with the f32 image and the PPM bytes written by the fused kernel, and for N > 1 the PPM rows are
-gathered to rank 0 over RCCL (xGMI).  Inputs (mesh, material textures) are resident in HBM before
-timing; the material graph is evaluated once, as Material::update is (reported separately).
-Per-GPU work is fixed as N grows (weak scaling).
+with the f32 image and the PPM bytes written by the fused kernel.  For N > 1 the job ends with the
+final RCCL gather (xGMI) of the PPM rows to rank 0 inside the timed region (north_star: "a final
+RCCL gather"); --gather-every-frame gathers after every frame instead.  Inputs (mesh, material
+textures) are resident in HBM before timing; the material graph is evaluated once, as
+Material::update is (reported separately).  Per-GPU work is fixed as N grows (weak scaling).
 
 Prints ONE JSON line on rank 0 (metric "Mrays/s": primary rays of all ranks / wall time).
 """
@@ -97,6 +98,8 @@ def main() -> None:
     ap.add_argument("--brute-force", action="store_true", help="disable the exact wave culling")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gather-every-frame", action="store_true",
+                    help="N > 1: gather the PPM rows to rank 0 after every frame (default: one final gather)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -127,14 +130,8 @@ def main() -> None:
     frame = torch.empty((H_total, WIDTH, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
     flags = capi.RENDER_BRUTE_FORCE if args.brute_force else capi.RENDER_DEFAULT
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record()
-        scene.render(out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr(), row0=row0, rows=rows, flags=flags)
-        if ev is not None:
-            ev[1].record()
-        if world > 1:
-            gather_ppm_rows(ppm, frame, world, rank)
+    def render_args():
+        return dict(row0=row0, rows=rows, out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr(), flags=flags)
 
     # one untimed instrumented frame: hit count for the algorithmic-bytes model
     scene.render(out_rgb=rgb.data_ptr(), out_face=face.data_ptr(), row0=row0, rows=rows, flags=flags)
@@ -142,31 +139,31 @@ def main() -> None:
     hits = int((face >= 0).sum().item())
 
     for _ in range(args.warmup):
-        step()
-    if world == 1:  # capture the frame-loop graph outside the timed region
-        scene.ctx.render_frames(args.steps, WIDTH, H_total, row0=row0, rows=rows, out_rgb=rgb.data_ptr(),
-                                out_ppm=ppm.data_ptr(), flags=flags, prepare_only=True)
+        scene.render(**render_args())
+    # capture the frame-loop graph and warm the gather outside the timed region
+    scene.ctx.render_frames(args.steps, WIDTH, H_total, prepare_only=True, **render_args())
+    if world > 1:
+        gather_ppm_rows(ppm, frame, world, rank)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if world == 1:
-        # the frame loop runs inside the library, replayed from a HIP graph (no per-frame host
-        # round trip)
-        scene.ctx.render_frames(args.steps, WIDTH, H_total, row0=row0, rows=rows, out_rgb=rgb.data_ptr(),
-                                out_ppm=ppm.data_ptr(), flags=flags)
+    # every rank renders its row tile of each frame; the frame loop runs inside the library,
+    # replayed from a HIP graph (no per-frame host round trip)
+    if args.gather_every_frame and world > 1:
+        for _ in range(args.steps):
+            scene.render(**render_args())
+            gather_ppm_rows(ppm, frame, world, rank)
     else:
-        events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                  for _ in range(args.steps)]
-        for k in range(args.steps):
-            step(events[k])
+        scene.ctx.render_frames(args.steps, WIDTH, H_total, **render_args())
+        if world > 1:  # the final RCCL gather of the PPM rows to rank 0 (file order)
+            gather_ppm_rows(ppm, frame, world, rank)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -174,12 +171,18 @@ def main() -> None:
         dist.all_reduce(h)
         hits_all = int(h.item())
     else:
-        # the frame kernel's own duration: the same frames once more, each launch bracketed by
-        # HIP events on the library's stream (the graph replay above leaves no room for them)
-        kernel_ms = scene.ctx.render_frames(args.steps, WIDTH, H_total, row0=row0, rows=rows,
-                                            out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr(), flags=flags,
-                                            timed=True)
         hits_all = hits
+    # the frame kernel's own duration: the same frames once more, each launch bracketed by HIP
+    # events on the library's stream (the graph replay above leaves no room for them)
+    kernel_ms = scene.ctx.render_frames(args.steps, WIDTH, H_total, timed=True, **render_args())
+    gather_ms = None
+    if world > 1:  # one frame's gather, for the record
+        torch.cuda.synchronize()
+        dist.barrier()
+        g0 = time.perf_counter()
+        gather_ppm_rows(ppm, frame, world, rank)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - g0) * 1e3
 
     if rank == 0:
         pixels = WIDTH * rows
@@ -205,7 +208,7 @@ def main() -> None:
             "config": {
                 "workload": "C2: cube.obj, 1920x1080 per GPU, main.rs scene + material graph; step = "
                             "one frame (camera rays, first-hit scan, shading + shadow rays, f32 image "
-                            "and PPM bytes) + RCCL gather of PPM rows to rank 0 when N > 1",
+                            "and PPM bytes); N > 1: row tiles, final RCCL gather of the PPM rows to rank 0",
                 "mesh": os.path.relpath(args.mesh, ROOT),
                 "triangles": int(len(mesh[0])),
                 "frame": [WIDTH, H_total],
@@ -217,6 +220,8 @@ def main() -> None:
             "frame_ms": round(ms_per_step, 6),
             "render_kernel_ms": round(kernel_ms, 6),
             "material_graph_s": round(t_mat, 4),
+            "gather_ms": None if gather_ms is None else round(gather_ms, 4),
+            "gather": ("every frame" if args.gather_every_frame else "final frame") if world > 1 else None,
             "hit_pixels": hits_all,
             "roofline": {
                 "bound": "hbm",
