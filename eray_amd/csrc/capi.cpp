@@ -59,6 +59,10 @@ struct eray_ctx {
     uint32_t* d_rect = nullptr;  // per-object pixel-rectangle accumulators (4 x uint32)
     size_t rect_cap = 0;
     std::vector<uint32_t> h_rect;
+    // screen bins of the large objects' faces (bins.hip), per object; valid for bins_phase
+    std::vector<ObjBins> bins;
+    bool bins_dirty = true;
+    uint32_t bins_phase = 0;
     std::vector<ObjectDesc> h_objs;  // kept alive for the async uploads
     std::vector<LightDesc> h_lights;
     std::vector<float> h_raw;
@@ -245,7 +249,41 @@ int sync_scene(eray_ctx* ctx, bool need_cull) {
                                         hipMemcpyHostToDevice, ctx->stream));
         }
         ctx->cull_dirty = false;
+        ctx->bins_dirty = true;
     }
+    return ERAY_OK;
+}
+
+// Screen bins for the objects the frame kernel does not scan per wave (> kDirectMax faces),
+// for the camera and the row phase of this render.
+int sync_bins(eray_ctx* ctx, uint32_t phase) {
+    bool need = false;
+    for (auto& o : ctx->objects) need |= o.T > kDirectMax;
+    if (!need || (!ctx->bins_dirty && ctx->bins_phase == phase)) return ERAY_OK;
+    uint32_t W, H;
+    eray_camera_size(&ctx->camera, &W, &H);
+    const uint32_t bins_x = (W + kBinW - 1) / kBinW;
+    const uint32_t bins_y = H ? (H - 1 + kBinH - phase) / kBinH + 1 : 1;
+    if (ctx->bins.size() < ctx->objects.size()) ctx->bins.resize(ctx->objects.size());
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // h_objs is about to change
+    for (size_t i = 0; i < ctx->objects.size(); ++i) {
+        ObjGeom& g = ctx->h_objs[i].g;
+        g.bin_start = nullptr;
+        g.bin_tri = nullptr;
+        g.bin_mask = nullptr;
+        g.bin_hot = nullptr;
+        if (ctx->objects[i].T <= kDirectMax) continue;
+        HIP_TRY(ctx, build_bins(ctx->d_cull + g.tri_begin, ctx->d_hot + g.tri_begin, g.tri_count, W, H, phase, bins_x, bins_y, &ctx->bins[i],
+                                ctx->stream));
+        g.bin_start = ctx->bins[i].start;
+        g.bin_tri = ctx->bins[i].tri;
+        g.bin_mask = ctx->bins[i].mask;
+        g.bin_hot = ctx->bins[i].hot;
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_objs, ctx->h_objs.data(), sizeof(ObjectDesc) * ctx->h_objs.size(),
+                                hipMemcpyHostToDevice, ctx->stream));
+    ctx->bins_dirty = false;
+    ctx->bins_phase = phase;
     return ERAY_OK;
 }
 
@@ -283,6 +321,12 @@ int eray_ctx_destroy(eray_ctx* ctx) {
     if (!ctx) return ERAY_OK;
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    for (auto& b : ctx->bins) {
+        if (b.start) hipFree(b.start);
+        if (b.tri) hipFree(b.tri);
+        if (b.mask) hipFree(b.mask);
+        if (b.hot) hipFree(b.hot);
+    }
     void* bufs[] = {ctx->d_hot, ctx->d_shade, ctx->d_cull, ctx->d_raw, ctx->d_objs, ctx->d_lights, ctx->d_rect};
     for (void* b : bufs)
         if (b) hipFree(b);
@@ -503,6 +547,8 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
                          "fused PPM output needs camera size == image size; use eray_pack_ppm");
     const bool cull = !(rp->flags & ERAY_RENDER_BRUTE_FORCE);
     if (int st = sync_scene(ctx, cull)) return st;
+    if (cull)
+        if (int st = sync_bins(ctx, rp->row0 % kBinH)) return st;
     *empty = !rp->rows || !W;
     if (*empty) return ERAY_OK;
 
@@ -586,6 +632,8 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     }
     p.spec_pow = ctx->spec_pow ? 1u : 0u;
     p.tiles_x = (W + 63) / 64;
+    p.bins_x = (W + kBinW - 1) / kBinW;
+    p.bin_phase = rp->row0 % kBinH;
     return ERAY_OK;
 }
 

@@ -1,0 +1,140 @@
+// face_rect.hpp — conservative pixel rectangle of a face from its culling record (device).
+#pragma once
+
+#include "internal.hpp"
+
+namespace eray {
+namespace gpu {
+
+// The culling records also bound where a face can be hit at all: condition k can only pass at
+// viewport points with K_k + A_k x' + B_k y' >= -T_k (x' = x / W, y' = y / H, camera_dir).
+// Clipping the viewport square by the four half-planes (double precision; each relaxed by 1e-9
+// of its magnitude, far above the clip's rounding, so the computed polygon contains the exact
+// one) and widening its bounding box by 1 pixel (x' is the reference's f32 x/W, within a relative
+// 2^-24 of x/W: far less than a pixel) gives a conservative pixel rectangle per face.  The object's rectangle is the union: no primary ray
+// outside it can hit the object, so those pixels need no test for it.
+__device__ inline bool face_rect(const TriCull& c, uint32_t W, uint32_t H, int32_t (&r)[4]) {
+    const float A[4] = {c.A.x, c.A.y, c.A.z, c.A.w}, B[4] = {c.B.x, c.B.y, c.B.z, c.B.w};
+    const float K[4] = {c.K.x, c.K.y, c.K.z, c.K.w}, T[4] = {c.T.x, c.T.y, c.T.z, c.T.w};
+    double px[12] = {0.0, 1.0, 1.0, 0.0}, py[12] = {0.0, 0.0, 1.0, 1.0}, qx[12], qy[12];
+    int n = 4;
+    for (int k = 0; k < 4; ++k) {
+        if (T[k] == __builtin_inff()) continue;  // condition disabled (non-finite record)
+        if (!(T[k] > -__builtin_inff())) return false;  // the face rejects every camera ray
+        const double a = A[k], b = B[k];
+        const double mag = fabs((double)K[k]) + fabs(a) + fabs(b) + fabs((double)T[k]);
+        const double cc = (double)K[k] + (double)T[k] + 1e-9 * mag + 1e-300;
+        int m = 0;
+        for (int i = 0; i < n; ++i) {
+            const int j = i + 1 == n ? 0 : i + 1;
+            const double fi = a * px[i] + b * py[i] + cc, fj = a * px[j] + b * py[j] + cc;
+            if (fi >= 0.0) {
+                qx[m] = px[i];
+                qy[m] = py[i];
+                ++m;
+            }
+            if ((fi >= 0.0) != (fj >= 0.0)) {
+                double t = fi / (fi - fj);
+                t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
+                qx[m] = px[i] + t * (px[j] - px[i]);
+                qy[m] = py[i] + t * (py[j] - py[i]);
+                ++m;
+            }
+        }
+        n = m;
+        if (!n) return false;
+        for (int i = 0; i < n; ++i) {
+            px[i] = qx[i];
+            py[i] = qy[i];
+        }
+    }
+    double xmin = px[0], xmax = px[0], ymin = py[0], ymax = py[0];
+    for (int i = 1; i < n; ++i) {
+        xmin = fmin(xmin, px[i]);
+        xmax = fmax(xmax, px[i]);
+        ymin = fmin(ymin, py[i]);
+        ymax = fmax(ymax, py[i]);
+    }
+    r[0] = max((int32_t)floor(xmin * W) - 1, 0);
+    r[1] = min((int32_t)ceil(xmax * W) + 1, (int32_t)W - 1);
+    r[2] = max((int32_t)floor(ymin * H) - 1, 0);
+    r[3] = min((int32_t)ceil(ymax * H) + 1, (int32_t)H - 1);
+    return r[0] <= r[1] && r[2] <= r[3];
+}
+
+
+// Where condition k of a culling record can pass along a camera row, in pixels: from
+// K + A xf + B yf >= -T (the culling bound at the pixel's own f32 viewport coordinates), solved
+// for xf in double: x >= c0 - c1 yf (A > 0) or x <= c0 - c1 yf (A < 0), widened by a pixel (the
+// f32 xf = x/W is within 2^-24 of x/W; the double solve within ~1e-15 of a pixel).  A condition
+// nearly independent of x is decided per row from its x-free part (kind 3); a disabled one
+// (T = +inf) does not narrow the interval (kind 0).
+struct CondLine {
+    double c0, c1, tol;
+    int kind;  // 0 none, 1 lower bound x >= c0 - c1 yf, 2 upper bound, 3 flat: fails if c0 - c1 yf > tol
+};
+__device__ inline CondLine cond_line(float A, float B, float K, float T, uint32_t W) {
+    CondLine l{0.0, 0.0, 0.0, 0};
+    if (!(T < __builtin_inff())) return l;
+    const double mag = fabs((double)K) + fabs((double)T) + fabs((double)B) + 1e-300;
+    if (fabs((double)A) <= 1e-9 * mag) {
+        // A xf >= R(yf) with |A xf| <= 1e-9 mag: the row fails only when R exceeds that
+        l.c0 = -((double)K + (double)T);
+        l.c1 = (double)B;
+        l.tol = 2e-9 * mag;
+        l.kind = 3;
+        return l;
+    }
+    const double inv = (double)W / (double)A;
+    l.c0 = -((double)K + (double)T) * inv;
+    l.c1 = (double)B * inv;
+    l.kind = A > 0.0f ? 1 : 2;
+    return l;
+}
+__device__ inline void apply_line(const CondLine& l, double yf, int32_t& xl, int32_t& xr) {
+    if (l.kind == 0) return;
+    const double q = l.c0 - l.c1 * yf;
+    if (l.kind == 3) {
+        if (q > l.tol) {
+            xl = 1;
+            xr = 0;
+        }
+    } else if (l.kind == 1) {
+        const double lo = floor(q) - 1.0;
+        if (lo > (double)xl) xl = lo > 2e9 ? 2000000000 : (int32_t)lo;
+    } else {
+        const double hi = ceil(q) + 1.0;
+        if (hi < (double)xr) xr = hi < -2e9 ? -2000000000 : (int32_t)hi;
+    }
+}
+
+// Pixels of the kBinW x kBinH bin at (bx, by) (camera columns bx*kBinW.., rows y0..y0+3 with
+// y0 = by*kBinH + phase - kBinH) where all four conditions of record c can pass: bit
+// r * kBinW + col.  The rows' yf are the reference's f32 y/H (camera_dir).
+__device__ inline unsigned long long bin_pixels(const TriCull& c, uint32_t W, uint32_t H, uint32_t phase,
+                                                uint32_t bx, uint32_t by) {
+    const CondLine l0 = cond_line(c.A.x, c.B.x, c.K.x, c.T.x, W);
+    const CondLine l1 = cond_line(c.A.y, c.B.y, c.K.y, c.T.y, W);
+    const CondLine l2 = cond_line(c.A.z, c.B.z, c.K.z, c.T.z, W);
+    const CondLine l3 = cond_line(c.A.w, c.B.w, c.K.w, c.T.w, W);
+    const int32_t x_lo = (int32_t)(bx * kBinW), x_hi = min((int32_t)((bx + 1) * kBinW), (int32_t)W) - 1;
+    unsigned long long pix = 0;
+    for (uint32_t r = 0; r < kBinH; ++r) {
+        const int32_t y = (int32_t)(by * kBinH + phase + r) - (int32_t)kBinH;
+        if (y < 0 || y >= (int32_t)H) continue;
+        const double yf = (double)((float)(uint32_t)y / (float)H);
+        int32_t xl = x_lo, xr = x_hi;
+        apply_line(l0, yf, xl, xr);
+        apply_line(l1, yf, xl, xr);
+        apply_line(l2, yf, xl, xr);
+        apply_line(l3, yf, xl, xr);
+        if (xl <= xr) {
+            const uint32_t n = (uint32_t)(xr - xl + 1), s = (uint32_t)(xl - x_lo);
+            pix |= (unsigned long long)((((n >= 32 ? 0xffffffffu : ((1u << n) - 1u)) << s) & 0xffffu)) << (kBinW * r);
+        }
+    }
+    return pix;
+}
+
+}  // namespace gpu
+}  // namespace eray

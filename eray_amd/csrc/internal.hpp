@@ -45,18 +45,30 @@ struct MaterialDesc {
 
 // Scenes up to these sizes are preloaded whole into each frame workgroup's LDS.
 constexpr uint32_t kCacheTris = 256, kCacheObjects = 16, kCacheLights = 16;
+// Objects with more faces than this are not scanned per wave: screen bins / LDS tiles.
+constexpr uint32_t kDirectMax = 256;
+// Screen bins of large objects' faces: kBinW x kBinH pixels (one wave's 16 x 4 sub-block).
+constexpr uint32_t kBinW = 16, kBinH = 4;
 // Detail rectangles carried in the kernel arguments (more objects: merged into the last one).
 constexpr int kMaxRects = 8;
 
-struct ObjGeom {  // what the triangle scans need of an object, 48 B
+struct ObjGeom {  // what the triangle scans need of an object, 80 B
     uint32_t tri_begin, tri_count;
     // Camera pixels whose primary ray can hit the object: x0..x1 x y0..y1 (inclusive, camera
     // rows), from the culling records (tri_rect_kernel); empty when x0 > x1.
     int32_t rect[4];
     float bb_lo[3], bb_hi[3];
+    // Screen bins of a large object's faces (bins.hip), or null: bin b's faces, in increasing
+    // index, are bin_tri[bin_start[b] .. bin_start[b + 1]) (indices relative to tri_begin);
+    // bin_mask[] holds the bin's pixels each may cover (bit row * kBinW + column) and bin_hot[]
+    // its intersection record, at the same positions.
+    const uint32_t* bin_start;
+    const uint32_t* bin_tri;
+    const unsigned long long* bin_mask;
+    const TriHot* bin_hot;
 };
 
-struct alignas(16) ObjectDesc {  // 128 B: the LDS scene copy moves whole 16-B words
+struct alignas(16) ObjectDesc {  // 160 B: the LDS scene copy moves whole 16-B words
     ObjGeom g;
     MaterialDesc mat;
 };
@@ -94,7 +106,9 @@ struct FrameParams {
     uint32_t total_sub;        // inclusive) and the number of sub-blocks they cover, counting
     int32_t rects[kMaxRects][4];  // overlaps once: x0, x1, y0, y1
     uint32_t spec_pow;         // some material has a specular-power output (powf != identity)
-    uint32_t tiles_x;  // pixel tiles per row
+    uint32_t tiles_x;    // 64 x 4 pixel blocks per row
+    uint32_t bins_x;     // screen bins per row
+    uint32_t bin_phase;  // bins start at camera rows bin_phase + k * kBinH (row0 % kBinH)
 };
 
 // Byte offsets of the LDS scene copy: [ObjectDesc x nobj | LightDesc x nl | TriCull x n (if
@@ -124,6 +138,18 @@ hipError_t launch_tri_cull(const TriHot* hot, uint32_t T, float cx, float cy, fl
 hipError_t launch_tri_rect(const TriCull* cull, uint32_t T, uint32_t cam_w, uint32_t cam_h,
                            uint32_t* acc, hipStream_t s);
 hipError_t launch_render(const FrameParams& p, hipStream_t s);
+
+struct ObjBins {  // device arrays of one object's bins (owned by the context)
+    uint32_t* start = nullptr;
+    uint32_t* tri = nullptr;
+    unsigned long long* mask = nullptr;
+    TriHot* hot = nullptr;
+    size_t start_cap = 0, tri_cap = 0, mask_cap = 0, hot_cap = 0, n = 0;
+};
+// Builds `out` for the object's records `cull[0, T)`, `hot[0, T)` and a W x H camera; bins_x x bins_y
+// bins of kBinW x kBinH pixels starting at camera row phase - kBinH.  Synchronises `s`.
+hipError_t build_bins(const TriCull* cull, const TriHot* hot, uint32_t T, uint32_t W, uint32_t H, uint32_t phase, uint32_t bins_x,
+                      uint32_t bins_y, ObjBins* out, hipStream_t s);
 hipError_t launch_pack_ppm(const float* rgb, uint32_t w, uint32_t h, uint8_t* out, hipStream_t s);
 
 hipError_t launch_wave(uint32_t w, uint32_t h, float xf, float yf, float* out, hipStream_t s);

@@ -25,6 +25,7 @@
 // Shadow rays (engine.rs:136-142, 218-228) go through the same LDS tiles without culling; the
 // reference's degenerate bounding box rejects almost all of them before the scan.
 #include "device_math.hpp"
+#include "face_rect.hpp"
 #include "internal.hpp"
 
 namespace eray {
@@ -67,7 +68,18 @@ __device__ uint64_t g_trace[2 * 64 * 4 * kTraceSlots];  // [realtime | shader cl
             g_trace[64 * 4 * kTraceSlots + i_] = __builtin_amdgcn_s_memtime();                   \
         }                                                                                         \
     } while (0)
+#define ERAY_TRACE_VAL(slot, v)                                                                   \
+    do {                                                                                          \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x % 16 == 0 && blockIdx.x < 1024) {               \
+            const uint32_t i_ = (blockIdx.x / 16 * 4 + (threadIdx.x >> 6)) * kTraceSlots + (slot); \
+            g_trace[i_] = (v);                                                                    \
+            g_trace[64 * 4 * kTraceSlots + i_] = 0;                                               \
+        }                                                                                         \
+    } while (0)
 #else
+#define ERAY_TRACE_VAL(slot, v) \
+    do {                        \
+    } while (0)
 #define ERAY_TRACE(slot) \
     do {                 \
     } while (0)
@@ -210,62 +222,7 @@ __global__ void __launch_bounds__(256) tri_cull_kernel(const TriHot* __restrict_
 }
 
 // ------------------------------------------------------------- object pixel rectangle ------
-// The culling records also bound where a face can be hit at all: condition k can only pass at
-// viewport points with K_k + A_k x' + B_k y' >= -T_k (x' = x / W, y' = y / H, camera_dir).
-// Clipping the viewport square by the four half-planes (double precision; each relaxed by 1e-9
-// of its magnitude, far above the clip's rounding, so the computed polygon contains the exact
-// one) and widening its bounding box by 2 pixels (covers the f32 rounding of x/W, y/H) gives a
-// conservative pixel rectangle per face.  The object's rectangle is the union: no primary ray
-// outside it can hit the object, so those pixels need no test for it.
-__device__ bool face_rect(const TriCull& c, uint32_t W, uint32_t H, int32_t (&r)[4]) {
-    const float A[4] = {c.A.x, c.A.y, c.A.z, c.A.w}, B[4] = {c.B.x, c.B.y, c.B.z, c.B.w};
-    const float K[4] = {c.K.x, c.K.y, c.K.z, c.K.w}, T[4] = {c.T.x, c.T.y, c.T.z, c.T.w};
-    double px[12] = {0.0, 1.0, 1.0, 0.0}, py[12] = {0.0, 0.0, 1.0, 1.0}, qx[12], qy[12];
-    int n = 4;
-    for (int k = 0; k < 4; ++k) {
-        if (T[k] == __builtin_inff()) continue;  // condition disabled (non-finite record)
-        if (!(T[k] > -__builtin_inff())) return false;  // the face rejects every camera ray
-        const double a = A[k], b = B[k];
-        const double mag = fabs((double)K[k]) + fabs(a) + fabs(b) + fabs((double)T[k]);
-        const double cc = (double)K[k] + (double)T[k] + 1e-9 * mag + 1e-300;
-        int m = 0;
-        for (int i = 0; i < n; ++i) {
-            const int j = i + 1 == n ? 0 : i + 1;
-            const double fi = a * px[i] + b * py[i] + cc, fj = a * px[j] + b * py[j] + cc;
-            if (fi >= 0.0) {
-                qx[m] = px[i];
-                qy[m] = py[i];
-                ++m;
-            }
-            if ((fi >= 0.0) != (fj >= 0.0)) {
-                double t = fi / (fi - fj);
-                t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
-                qx[m] = px[i] + t * (px[j] - px[i]);
-                qy[m] = py[i] + t * (py[j] - py[i]);
-                ++m;
-            }
-        }
-        n = m;
-        if (!n) return false;
-        for (int i = 0; i < n; ++i) {
-            px[i] = qx[i];
-            py[i] = qy[i];
-        }
-    }
-    double xmin = px[0], xmax = px[0], ymin = py[0], ymax = py[0];
-    for (int i = 1; i < n; ++i) {
-        xmin = fmin(xmin, px[i]);
-        xmax = fmax(xmax, px[i]);
-        ymin = fmin(ymin, py[i]);
-        ymax = fmax(ymax, py[i]);
-    }
-    r[0] = max((int32_t)floor(xmin * W) - 2, 0);
-    r[1] = min((int32_t)ceil(xmax * W) + 2, (int32_t)W - 1);
-    r[2] = max((int32_t)floor(ymin * H) - 2, 0);
-    r[3] = min((int32_t)ceil(ymax * H) + 2, (int32_t)H - 1);
-    return r[0] <= r[1] && r[2] <= r[3];
-}
-
+// Union of the faces' conservative pixel rectangles (face_rect.hpp).
 __global__ void __launch_bounds__(256) tri_rect_kernel(const TriCull* __restrict__ cull, uint32_t T,
                                                        uint32_t W, uint32_t H, uint32_t* __restrict__ acc) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -457,17 +414,18 @@ __device__ SceneLds preload_scene(const FrameParams& p, char* dyn) {
 // kDone (hit found, bbox rejected, or not a pixel of the image).
 constexpr int kUndecided = 0, kSearching = 1, kDone = 2;
 
-// Objects with at most this many triangles are searched by each wave on its own (no LDS tiles,
-// no barrier); larger ones go through workgroup-shared LDS tiles.
-constexpr uint32_t kDirectMax = 256;
+// Objects with at most kDirectMax (internal.hpp) triangles are searched by each wave on its
+// own (no LDS tiles, no barrier); larger ones through their screen bins (primary rays, culled)
+// or workgroup-shared LDS tiles (shadow rays, brute force).
 // Candidate triangles tested together per step (independent, branch-free tests: their long
 // dependent chains, division included, overlap).
 constexpr int kBatch = 4;
 
-// Tests the candidates of `mask` (bit i = triangle idx0 + i) in index order, kBatch at a time;
-// hot(i) returns triangle idx0 + i's record.  Returns false once no lane is searching.
-template <typename Hot>
-__device__ __forceinline__ bool test_candidates(unsigned long long mask, uint32_t idx0, Hot&& hot, int& st,
+// Tests the candidates of `mask` in index order, kBatch at a time: bit i stands for face
+// face(i) (relative to the object) whose record is hot(i).  Returns false once no lane is
+// searching.
+template <typename Face, typename Hot>
+__device__ __forceinline__ bool test_candidates(unsigned long long mask, Face&& face, Hot&& hot, int& st,
                                                 const f3& o, const f3& d, int& found, float& hu, float& hv,
                                                 float& ht) {
     while (mask) {
@@ -488,7 +446,7 @@ __device__ __forceinline__ bool test_candidates(unsigned long long mask, uint32_
 #pragma unroll
         for (int k = 0; k < kBatch; ++k) {
             if (st == kSearching && hit[k]) {
-                found = (int)(idx0 + ids[k]);
+                found = (int)face(ids[k]);
                 hu = u[k];
                 hv = v[k];
                 ht = t[k];
@@ -533,8 +491,9 @@ __device__ void first_hit(const FrameParams& p, const Scene& sc, uint32_t begin,
             }
             if (!mask) continue;
             if (!resolve()) break;
+            auto face = [&](uint32_t i) { return base + i; };
             auto hot = [&](uint32_t i) { return sc.hot(begin + base + i); };
-            if (!test_candidates(mask, base, hot, st, o, d, found, hu, hv, ht)) return;
+            if (!test_candidates(mask, face, hot, st, o, d, found, hu, hv, ht)) return;
         }
         return;
     }
@@ -558,10 +517,145 @@ __device__ void first_hit(const FrameParams& p, const Scene& sc, uint32_t begin,
             }
             if (!mask) continue;
             if (!resolve()) break;
+            auto face = [&](uint32_t i) { return base + c + i; };
             auto hot = [&](uint32_t i) { return s_hot[c + i]; };
-            if (!test_candidates(mask, base + c, hot, st, o, d, found, hu, hv, ht)) break;
+            if (!test_candidates(mask, face, hot, st, o, d, found, hu, hv, ht)) break;
         }
     }
+    __syncthreads();  // the tiles' LDS is reused (aliased by the binned search)
+}
+
+constexpr uint32_t kBlkW = 64, kBlkH = 4;  // pixel block
+constexpr uint32_t kSubW = 16;             // sub-block width (x kBlkH rows): one wave's pixels
+static_assert(kSubW == kBinW && kBlkH == kBinH, "a screen bin is one wave's sub-block");
+
+// Per-wave LDS of the binned primary search.
+struct BinLds {
+    float dir[3][64];         // each pixel's camera ray (lane = pixel)
+    uint32_t best[64];        // each pixel's earliest hit so far: bin position, 0xffffffff = none
+    TriHot cand[64];          // the chunk's candidate records (slot = lane that loaded it)
+    uint16_t pairs[64 * 64];  // (candidate slot << 6) | pixel, for every pixel a candidate may hit
+};
+constexpr uint32_t kBinLdsBytes = (sizeof(BinLds) + 15) / 16 * 16;
+constexpr uint32_t kWide = 16;  // candidates that may cover more pixels are tested by the whole wave
+
+// Primary-ray first hit of a binned object (bins.hip).  The reference's first hit by index is
+// the smallest index among the faces whose Triangle::intersects passes, so the candidates of the
+// sub-block's bin are processed 64 at a time as (candidate, pixel) pairs: each entry carries the
+// pixels where its four culling bounds can pass (bin_pixels), restricted to pixels still without
+// a hit; narrow candidates' pairs are compacted in LDS and tested one per lane, wide ones by the
+// whole wave; every hit lowers the pixel's best bin position (positions increase with the face
+// index).  Work follows the pixels a face can cover, not 64 lanes per face.  The winner is
+// re-tested for u, v, t.
+template <typename Activate>
+__device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32_t bin, uint32_t wx0, uint32_t py0,
+                                 int& st, const f3& o, const f3& d, Activate&& activate, int& found, float& hu,
+                                 float& hv, float& ht, BinLds& L) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lo = load_const(ob.bin_start, bin), hi = load_const(ob.bin_start, bin + 1);
+    if (lo == hi) return;
+    if (__any(st == kUndecided)) {  // every pixel's ray and bbox verdict, up front
+        const bool a = activate();
+        if (st == kUndecided) st = a ? kSearching : kDone;
+    }
+    if (!__any(st == kSearching)) return;
+    L.dir[0][lane] = d.x;
+    L.dir[1][lane] = d.y;
+    L.dir[2][lane] = d.z;
+    L.best[lane] = st == kSearching ? 0xffffffffu : 0u;  // 0: never improved
+    uint32_t n_pairs = 0, n_chunks = 0;
+    if (hi - lo > 200) ERAY_TRACE(12);
+    // the next chunk's entries are loaded while the current chunk is processed
+    unsigned long long m_n = 0;
+    TriHot h_n{};
+    auto fetch = [&](uint32_t base) {
+        if (base + lane < hi) {
+            m_n = ob.bin_mask[base + lane];
+            h_n = ob.bin_hot[base + lane];
+        }
+    };
+    fetch(lo);
+    for (uint32_t base = lo; base < hi; base += 64) {
+        ++n_chunks;
+        const uint32_t j = base + lane;
+        // pixels still without a hit (later chunks hold later faces: a hit is final)
+        const unsigned long long live = __ballot(st == kSearching && L.best[lane] == 0xffffffffu);
+        const unsigned long long pix = j < hi ? (m_n & live) : 0ull;  // the live pixels this face may hit
+        L.cand[lane] = h_n;
+        if (base + 64 < hi) fetch(base + 64);
+        const uint32_t cnt = (uint32_t)__popcll(pix);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // L.cand of this chunk visible to the wave
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // wide candidates (many pixels): the whole wave tests them, each lane its own pixel
+        unsigned long long wide = __ballot(cnt > kWide);
+        while (wide) {
+            const uint32_t s = (uint32_t)(__ffsll(wide) - 1);
+            wide &= wide - 1;
+            const unsigned long long ps = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pix >> 32), (int)s) << 32) |
+                                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pix, (int)s);
+            const uint32_t pos = base + s;
+            if (((ps >> lane) & 1ull) && pos < L.best[lane]) {
+                float u, v, t;
+                if (exact_test(L.cand[s], o, d, u, v, t)) L.best[lane] = pos;
+            }
+        }
+        // narrow candidates: (candidate, pixel) pairs compacted in LDS, one test per lane
+        const uint32_t ncnt = cnt > kWide ? 0u : cnt;
+        uint32_t incl = ncnt;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off);
+            if ((int)lane >= off) incl += y;
+        }
+        const uint32_t total = __shfl(incl, 63);
+        n_pairs += total;
+        uint32_t at = incl - ncnt;
+        unsigned long long np = ncnt ? pix : 0ull;
+        while (np) {
+            const uint32_t bpos = (uint32_t)(__ffsll(np) - 1);
+            np &= np - 1;
+            L.pairs[at++] = (uint16_t)((lane << 6) | bpos);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t q = 0; q < total; q += 64) {
+            if (q + lane < total) {
+                const uint32_t pr = L.pairs[q + lane];
+                const uint32_t slot = pr >> 6, px = pr & 63;
+                const uint32_t pos = base + slot;
+                if (pos < L.best[px]) {  // a pixel already hit by an earlier face needs no test
+                    float u, v, t;
+                    const f3 dd = mk3(L.dir[0][px], L.dir[1][px], L.dir[2][px]);
+                    if (exact_test(L.cand[slot], o, dd, u, v, t)) atomicMin(&L.best[px], pos);
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (!__any(st == kSearching && L.best[lane] == 0xffffffffu)) break;
+    }
+    if (hi - lo > 200) {
+        ERAY_TRACE(13);
+        ERAY_TRACE_VAL(9, hi - lo);
+        ERAY_TRACE_VAL(10, n_pairs);
+        ERAY_TRACE_VAL(11, n_chunks);
+    }
+    const uint32_t mine = L.best[lane];
+    if (st == kSearching && mine != 0xffffffffu) {
+        float u, v, t;
+        exact_test(ob.bin_hot[mine], o, d, u, v, t);  // the winner again, for its u, v, t
+        found = (int)ob.bin_tri[mine];
+        hu = u;
+        hv = v;
+        ht = t;
+        st = kDone;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // L is reused by the next object / sub-block
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 __device__ __forceinline__ bool tex_value(const TexView& tv, float x, float y, float& out) {
@@ -598,8 +692,6 @@ __device__ __forceinline__ f3 camera_dir(const FrameParams& p, uint32_t px, uint
 //    the non-detail sub-blocks — a whole block as 3 + 1 + 1 wave-contiguous 16-byte stores.
 //    This is the frame's HBM-write floor.  Keeping it off the detail workgroups matters: their
 //    loads must not wait behind their own stores (a CDNA wave's vmcnt counts both).
-constexpr uint32_t kBlkW = 64, kBlkH = 4;  // pixel block
-constexpr uint32_t kSubW = 16;             // sub-block width (x kBlkH rows): one wave's pixels
 
 __device__ __forceinline__ Bundle make_bundle(const FrameParams& p, uint32_t x0, uint32_t xe,
                                               uint32_t py0, uint32_t pye) {
@@ -694,7 +786,7 @@ __device__ __forceinline__ bool rect_meets(const ObjGeom& ob, const FrameParams&
 // `active` false: the wave only takes part in the workgroup's LDS-tile barriers.
 template <bool kCull, bool kLdsTiles, bool kSpecPow, typename Scene>
 __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc, uint32_t wx0, uint32_t py0,
-                                           bool active, TriHot* s_hot, TriCull* s_cull, float4* s_rgb,
+                                           bool active, TriHot* s_hot, TriCull* s_cull, char* s_bins, float4* s_rgb,
                                            uint32_t* s_ppm, bool aligned) {
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const f3 C = mk3(p.cx, p.cy, p.cz);
@@ -714,8 +806,9 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
     for (uint32_t oi = 0; oi < p.nobj; ++oi) {
         const ObjGeom ob = sc.geom(oi);  // uniform
         const bool direct = !kLdsTiles || ob.tri_count <= kDirectMax;
-        // outside the object's pixel rectangle no primary ray can hit it
-        if (kCull && direct && !rect_meets(ob, p, wx0, py0)) continue;
+        // outside the object's pixel rectangle no primary ray can hit it (only where skipping
+        // keeps the workgroup's barriers uniform)
+        if (kCull && (direct || ob.bin_start) && !rect_meets(ob, p, wx0, py0)) continue;
         auto activate = [&]() {
             if (!ray_ready) {
                 uint32_t pxo = px, yo = y;  // opaque: keep ray generation on this path
@@ -727,12 +820,17 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
         };
         int st = valid ? kUndecided : kDone, f = -1;
         float u, v, t;
-        if (direct)
+        if (direct) {
             first_hit<kCull, false>(p, sc, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull, activate, f, u,
                                     v, t);
-        else
+        } else if (kCull && ob.bin_start) {  // per wave: no LDS tiles, no barrier
+            const uint32_t bin = ((p.row0 + py0 + kBinH - p.bin_phase) / kBinH) * p.bins_x + wx0 / kBinW;
+            first_hit_binned(p, ob, bin, wx0, py0, st, C, d, activate, f, u, v, t,
+                             *reinterpret_cast<BinLds*>(s_bins + wave * kBinLdsBytes));
+        } else {
             first_hit<kCull, kLdsTiles>(p, sc, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull, activate,
                                         f, u, v, t);
+        }
         if (f >= 0) {
             const f3 P = add(C, mul(d, t));
             const float dsq = len_sq(sub(P, C));
@@ -920,8 +1018,14 @@ __device__ __forceinline__ bool inside(const SubRect& r, int32_t sx, int32_t sy)
 
 template <bool kCull, bool kLdsTiles, bool kSpecPow, bool kLdsScene>
 __global__ void __launch_bounds__(kWG) frame_kernel(FrameParams p) {
-    __shared__ TriHot s_hot[kLdsTiles ? kTriTile : 1];
-    __shared__ TriCull s_cull[(kCull && kLdsTiles) ? kTriTile : 1];
+    // large objects: LDS tiles (shadow rays, brute force) and, aliased, the per-wave binned
+    // primary search (first_hit ends its tile loop on a barrier, so the two never overlap)
+    constexpr size_t kTileBytes = kTriTile * (sizeof(TriHot) + ((kCull && kLdsTiles) ? sizeof(TriCull) : 0));
+    constexpr size_t kBinBytes = (kCull && kLdsTiles) ? (kWG / 64) * kBinLdsBytes : 0;
+    __shared__ __attribute__((aligned(16))) char s_large[kLdsTiles ? (kTileBytes > kBinBytes ? kTileBytes : kBinBytes) : 16];
+    TriHot* s_hot = reinterpret_cast<TriHot*>(s_large);
+    TriCull* s_cull = reinterpret_cast<TriCull*>(s_large + kTriTile * sizeof(TriHot));
+    char* s_bins = s_large;
     __shared__ float4 s_rgb[kBlkW * kBlkH * 3 / 4];    // each wave's f32 RGB rows, staged
     __shared__ uint32_t s_ppm[kBlkW * kBlkH * 3 / 4];  // ... and its PPM byte rows
     extern __shared__ __attribute__((aligned(16))) char dyn[];
@@ -958,11 +1062,11 @@ __global__ void __launch_bounds__(kWG) frame_kernel(FrameParams p) {
                     }
                 }
                 render_sub<kCull, kLdsTiles, kSpecPow>(p, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH, active,
-                                                       s_hot, s_cull, s_rgb, s_ppm, aligned);
+                                                       s_hot, s_cull, s_bins, s_rgb, s_ppm, aligned);
 #ifdef ERAY_PHASE_TRACE_REPEAT  // diagnostics: the same sub-block again, instruction cache warm
                 ERAY_TRACE(6);
                 render_sub<kCull, kLdsTiles, kSpecPow>(p, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH, active,
-                                                       s_hot, s_cull, s_rgb, s_ppm, aligned);
+                                                       s_hot, s_cull, s_bins, s_rgb, s_ppm, aligned);
 #endif
             }
         };

@@ -22,7 +22,7 @@ from eray_amd.objfile import load_obj_file  # noqa: E402
 W, H = 1920, 1080
 rows = int(sys.argv[1]) if len(sys.argv) > 1 else H
 row0 = (H - rows) // 2
-mesh = load_obj_file(os.path.join(ROOT, "objects", "cube.obj"))
+mesh = load_obj_file(sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "objects", "cube.obj"))
 ctx = capi.Context(0)
 rgb = ctx.empty((H, W, 3), np.float32)
 ppm = ctx.empty((H, W, 3), np.uint8)
@@ -53,4 +53,6 @@ for g in range(64):
         row = t[g, w]
         if row[0] == 0:
             continue
-        print(f"{16 * g:4d}.{w} " + " ".join(f"{(row[k] - t0) if row[k] else -1:8d}" for k in sorted(names)))
+        print(f"{16 * g:4d}.{w} " + " ".join(f"{(row[k] - t0) if row[k] else -1:8d}" for k in sorted(names))
+              + f"   heavy bin: list {row[9]:6d} pairs {row[10]:6d} chunks {row[11]:4d} "
+              f"scan {(row[13] - row[12]) if row[12] else -1:6d}")
