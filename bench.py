@@ -36,17 +36,17 @@ from eray_amd.dist import gather_ppm_rows, row_block  # noqa: E402
 from eray_amd.frame import MainScene  # noqa: E402
 from eray_amd.objfile import load_obj_file  # noqa: E402
 
-WIDTH, HEIGHT_PER_GPU, TEXTURE = 1920, 1080, 1024
+WIDTH, HEIGHT_PER_GPU, TEXTURE = 1920, 1080, 1024  # C2 (defaults; --width / --rows-per-gpu)
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def frame_camera_fov(n: int) -> tuple[float, float]:
-    """Fov giving Camera::size() == (1920, 1080*n) exactly (16:9 for one GPU)."""
-    for fov in ((16.0, 9.0 * n), (float(WIDTH), float(HEIGHT_PER_GPU * n))):
-        cam = capi.make_camera((0.0, 0.0, 5.0), fov, WIDTH, 1.0)
-        if capi.camera_size(cam) == (WIDTH, HEIGHT_PER_GPU * n):
+def frame_camera_fov(width: int, height: int) -> tuple[float, float]:
+    """Fov giving Camera::size() == (width, height) exactly (Fov(16, 9) for 16:9 frames)."""
+    for fov in ((16.0, 9.0 * height * 16 / (9.0 * width)), (16.0, 9.0), (float(width), float(height))):
+        cam = capi.make_camera((0.0, 0.0, 5.0), fov, width, 1.0)
+        if capi.camera_size(cam) == (width, height):
             return fov
-    raise RuntimeError(f"no Fov gives a 1920x{HEIGHT_PER_GPU * n} camera")
+    raise RuntimeError(f"no Fov gives a {width}x{height} camera")
 
 
 def algorithmic_bytes(hit_pixels: int, pixels: int, triangles: int) -> int:
@@ -68,25 +68,43 @@ def pmc_traffic():
         return None
 
 
-def cpu_baseline(mesh, seconds: float = 10.0) -> dict:
-    """The single-threaded C++ restatement (oracle/, 'port') on this host: full C2 frames
-    (render + PPM byte pack) repeated for >= `seconds`."""
+def cpu_baseline(mesh, width: int, height: int, fov, seconds: float = 10.0) -> dict:
+    """The single-threaded C++ restatement (oracle/, 'port') on this host, on the bench's own
+    frame (width x height, same scene): whole frames (render + PPM byte pack) repeated for
+    >= `seconds` when a frame takes under a second (the cube), otherwise a deterministic row
+    sample — every 64th row, then the rows between — until `seconds` have passed."""
     from oracle import pyoracle as O
 
     scene = O.main_rs_scene(*mesh, texture=TEXTURE)
-    cam = O.camera((0.0, 0.0, 5.0), (16.0, 9.0), WIDTH, 1.0)
-    frames, t0 = 0, time.perf_counter()
-    while True:
-        rgb, _ = O.render(scene, cam)
-        O.ppm_bytes(rgb)
-        frames += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    rays = frames * WIDTH * HEIGHT_PER_GPU
+    cam = O.camera((0.0, 0.0, 5.0), fov, width, 1.0)
+    t0 = time.perf_counter()
+    rgb, _ = O.render(scene, cam, rows=1, row0=height // 2)  # one row: decide frames vs rows
+    one_row = time.perf_counter() - t0
+    if one_row * height < 1.0:
+        frames, t0 = 0, time.perf_counter()
+        while True:
+            rgb, _ = O.render(scene, cam)
+            O.ppm_bytes(rgb)
+            frames += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+        rays = frames * width * height
+        sample = f"{frames} full {width}x{height} frames (main.rs scene, render + PPM pack) in {el:.1f} s"
+    else:
+        order = [r for s in range(64) for r in range(s, height, 64)]
+        done, t0 = 0, time.perf_counter()
+        for r in order:
+            O.render(scene, cam, row0=height - 1 - r, rows=1)
+            done += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+        rays = done * width
+        sample = (f"{done} of the {height} rows of the {width}x{height} frame (every 64th row first), "
+                  f"render only, in {el:.1f} s")
     return {"value": rays / el / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
-            "sample": f"{frames} full 1920x1080 cube frames (main.rs scene, render + PPM pack) "
-                      f"in {el:.1f} s, single thread, oracle/eray_oracle.cpp (g++ -O2 -ffp-contract=off)"}
+            "sample": sample + ", single thread, oracle/eray_oracle.cpp (g++ -O2 -ffp-contract=off)"}
 
 
 def main() -> None:
@@ -95,6 +113,8 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--mesh", default=os.path.join(ROOT, "objects", "cube.obj"))
+    ap.add_argument("--width", type=int, default=WIDTH, help="frame width (C2: 1920)")
+    ap.add_argument("--rows-per-gpu", type=int, default=HEIGHT_PER_GPU, help="frame rows per GPU (C2: 1080)")
     ap.add_argument("--brute-force", action="store_true", help="disable the exact wave culling")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -116,32 +136,38 @@ def main() -> None:
     stream = torch.cuda.Stream()  # one stream shared by the library, torch and RCCL
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
-    H_total = HEIGHT_PER_GPU * world
+    width, per_gpu = args.width, args.rows_per_gpu
+    H_total = per_gpu * world
     t_mat0 = time.perf_counter()
-    scene = MainScene(ctx, *mesh, WIDTH, H_total, texture=TEXTURE, fov=frame_camera_fov(world))
+    scene = MainScene(ctx, *mesh, width, H_total, texture=TEXTURE, fov=frame_camera_fov(width, H_total))
     torch.cuda.synchronize()
     t_mat = time.perf_counter() - t_mat0
 
     # rank r renders the r-th block of PPM file rows: camera rows [H - (r+1)*h, H - r*h)
-    row0, rows = row_block(rank, world, HEIGHT_PER_GPU)
-    rgb = torch.empty((rows, WIDTH, 3), dtype=torch.float32, device="cuda")
-    ppm = torch.empty((rows, WIDTH, 3), dtype=torch.uint8, device="cuda")
-    face = torch.empty((rows, WIDTH), dtype=torch.int32, device="cuda")
-    frame = torch.empty((H_total, WIDTH, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
+    row0, rows = row_block(rank, world, per_gpu)
+    rgb = torch.empty((rows, width, 3), dtype=torch.float32, device="cuda")
+    ppm = torch.empty((rows, width, 3), dtype=torch.uint8, device="cuda")
+    face = torch.empty((rows, width), dtype=torch.int32, device="cuda")
+    frame = torch.empty((H_total, width, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
     flags = capi.RENDER_BRUTE_FORCE if args.brute_force else capi.RENDER_DEFAULT
 
     def render_args():
         return dict(row0=row0, rows=rows, out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr(), flags=flags)
 
-    # one untimed instrumented frame: hit count for the algorithmic-bytes model
+    # one untimed instrumented frame: hit count for the algorithmic-bytes model; being the first
+    # render of the camera it also builds the per-camera data (culling records, pixel
+    # rectangles, screen bins of large meshes): reported as scene_setup_ms
+    torch.cuda.synchronize()
+    t_setup0 = time.perf_counter()
     scene.render(out_rgb=rgb.data_ptr(), out_face=face.data_ptr(), row0=row0, rows=rows, flags=flags)
     torch.cuda.synchronize()
+    t_setup = time.perf_counter() - t_setup0
     hits = int((face >= 0).sum().item())
 
     for _ in range(args.warmup):
         scene.render(**render_args())
     # capture the frame-loop graph and warm the gather outside the timed region
-    scene.ctx.render_frames(args.steps, WIDTH, H_total, prepare_only=True, **render_args())
+    scene.ctx.render_frames(args.steps, width, H_total, prepare_only=True, **render_args())
     if world > 1:
         gather_ppm_rows(ppm, frame, world, rank)
     torch.cuda.synchronize()
@@ -156,7 +182,7 @@ def main() -> None:
             scene.render(**render_args())
             gather_ppm_rows(ppm, frame, world, rank)
     else:
-        scene.ctx.render_frames(args.steps, WIDTH, H_total, **render_args())
+        scene.ctx.render_frames(args.steps, width, H_total, **render_args())
         if world > 1:  # the final RCCL gather of the PPM rows to rank 0 (file order)
             gather_ppm_rows(ppm, frame, world, rank)
     if world > 1:
@@ -174,7 +200,7 @@ def main() -> None:
         hits_all = hits
     # the frame kernel's own duration: the same frames once more, each launch bracketed by HIP
     # events on the library's stream (the graph replay above leaves no room for them)
-    kernel_ms = scene.ctx.render_frames(args.steps, WIDTH, H_total, timed=True, **render_args())
+    kernel_ms = scene.ctx.render_frames(args.steps, width, H_total, timed=True, **render_args())
     gather_ms = None
     if world > 1:  # one frame's gather, for the record
         torch.cuda.synchronize()
@@ -185,9 +211,9 @@ def main() -> None:
         gather_ms = (time.perf_counter() - g0) * 1e3
 
     if rank == 0:
-        pixels = WIDTH * rows
+        pixels = width * rows
         ms_per_step = elapsed / args.steps * 1e3
-        rays = WIDTH * H_total * args.steps
+        rays = width * H_total * args.steps
         value = rays / elapsed / 1e6
         alg = algorithmic_bytes(hits, pixels, len(mesh[0]))
         achieved = alg / (kernel_ms * 1e-3) / 1e9
@@ -203,15 +229,17 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic scene of src/main.rs: objects/cube.obj (the reference's own file), "
-                    "procedural material graph",
+            "data": (f"synthetic scene of src/main.rs around {os.path.relpath(args.mesh, ROOT)}"
+                     + (" (the reference's own file)" if args.mesh.endswith("objects/cube.obj") else "")
+                     + ", procedural material graph"),
             "config": {
-                "workload": "C2: cube.obj, 1920x1080 per GPU, main.rs scene + material graph; step = "
+                "workload": f"{'C2: ' if (width, per_gpu) == (1920, 1080) and args.mesh.endswith('objects/cube.obj') else ''}"
+                            f"{os.path.basename(args.mesh)}, {width}x{per_gpu} per GPU, main.rs scene + material graph; step = "
                             "one frame (camera rays, first-hit scan, shading + shadow rays, f32 image "
                             "and PPM bytes); N > 1: row tiles, final RCCL gather of the PPM rows to rank 0",
                 "mesh": os.path.relpath(args.mesh, ROOT),
                 "triangles": int(len(mesh[0])),
-                "frame": [WIDTH, H_total],
+                "frame": [width, H_total],
                 "rows_per_gpu": rows,
                 "texture": TEXTURE,
                 "parallelism": f"row tiles x{world}" if world > 1 else "single GPU",
@@ -220,6 +248,7 @@ def main() -> None:
             "frame_ms": round(ms_per_step, 6),
             "render_kernel_ms": round(kernel_ms, 6),
             "material_graph_s": round(t_mat, 4),
+            "scene_setup_ms": round(t_setup * 1e3, 3),
             "gather_ms": None if gather_ms is None else round(gather_ms, 4),
             "gather": ("every frame" if args.gather_every_frame else "final frame") if world > 1 else None,
             "hit_pixels": hits_all,
@@ -236,7 +265,7 @@ def main() -> None:
             },
         }
         if world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline(mesh, args.cpu_seconds)
+            result["cpu_baseline"] = cpu_baseline(mesh, width, H_total, frame_camera_fov(width, H_total), args.cpu_seconds)
         print(json.dumps(result), flush=True)
 
     scene.close()
