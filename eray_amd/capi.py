@@ -69,6 +69,11 @@ class Object(C.Structure):
                 ("bbox_max", C.c_float * 3), ("material", Material)]
 
 
+class ExampleMaterial(C.Structure):  # eray_material_example_params
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("x_fac", C.c_float), ("y_fac", C.c_float),
+                ("r", C.c_float), ("g", C.c_float), ("b", C.c_float), ("factor", C.c_float)]
+
+
 class RenderParams(C.Structure):
     _fields_ = [("image_width", C.c_uint32), ("image_height", C.c_uint32), ("row0", C.c_uint32),
                 ("rows", C.c_uint32), ("bounces", C.c_uint32), ("anti_aliasing", C.c_uint32),
@@ -101,6 +106,7 @@ SIGNATURES = {
     "eray_scene_reset": (C.c_int, [_P]),
     "eray_scene_set_camera": (C.c_int, [_P, C.POINTER(Camera)]),
     "eray_scene_add_light": (C.c_int, [_P, C.POINTER(Light)]),
+    "eray_scene_set_object_example_material": (C.c_int, [_P, _U, C.POINTER(ExampleMaterial)]),
     "eray_scene_add_object": (C.c_int, [_P, C.POINTER(Object), C.POINTER(_U)]),
     "eray_camera_size": (C.c_int, [C.POINTER(Camera), C.POINTER(_U), C.POINTER(_U)]),
     "eray_render": (C.c_int, [_P, C.POINTER(RenderParams)]),
@@ -294,6 +300,10 @@ class Context:
 
     def add_light(self, light: Light) -> None:
         self._check(lib().eray_scene_add_light(self._h, C.byref(light)))
+
+    def set_object_example_material(self, index, width, height, x_fac, y_fac, r, g, b, factor) -> None:
+        m = ExampleMaterial(width, height, x_fac, y_fac, r, g, b, factor)
+        self._check(lib().eray_scene_set_object_example_material(self._h, index, C.byref(m)))
 
     def add_object(self, positions, normals, uvs, bbox_min=(0.0, 0.0, 0.0), bbox_max=(0.0, 0.0, 0.0),
                    color: Image | None = None, diffuse: Image | None = None,

@@ -27,6 +27,8 @@ struct HostObject {
     uint32_t T = 0;
     float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
     eray_material mat{};
+    bool example = false;  // color + diffuse from main.rs's graph at the hit texel
+    eray_material_example_params ex{};
 };
 }  // namespace
 
@@ -184,6 +186,19 @@ int sync_scene(eray_ctx* ctx, bool need_cull) {
             }
             d.mat = MaterialDesc{tex(o.mat.color), tex(o.mat.diffuse), tex(o.mat.specular),
                                  tex(o.mat.specular_power), tex(o.mat.reflection)};
+            if (o.example) {
+                d.mat.color = TexView{nullptr, 0, 0};
+                d.mat.diffuse = TexView{nullptr, 0, 0};
+                d.mat.example = 1;
+                d.mat.ex_w = o.ex.width;
+                d.mat.ex_h = o.ex.height;
+                d.mat.ex_xf = o.ex.x_fac;
+                d.mat.ex_yf = o.ex.y_fac;
+                d.mat.ex_r = o.ex.r;
+                d.mat.ex_g = o.ex.g;
+                d.mat.ex_b = o.ex.b;
+                d.mat.ex_factor = o.ex.factor;
+            }
             ctx->h_objs.push_back(d);
             ctx->spec_pow |= o.mat.specular_power.data != nullptr;
             begin += o.T;
@@ -476,6 +491,19 @@ int eray_scene_add_light(eray_ctx* ctx, const eray_light* light) {
     if (light->variant != ERAY_LIGHT_POINT && light->variant != ERAY_LIGHT_AMBIENT)
         return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "unknown light variant %d", light->variant);
     ctx->lights.push_back(*light);
+    ctx->desc_dirty = true;
+    return ERAY_OK;
+}
+
+int eray_scene_set_object_example_material(eray_ctx* ctx, uint32_t index, const eray_material_example_params* m) {
+    if (!ctx || !m) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "null argument");
+    if (index >= ctx->objects.size())
+        return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "object %u out of range (%zu objects)", index,
+                         ctx->objects.size());
+    if (!m->width || !m->height)  // Image::mod_get by 0 panics (image.rs:36-38)
+        return set_error(ctx, ERAY_E_OUT_OF_BOUNDS, "example material of zero width or height");
+    ctx->objects[index].example = true;
+    ctx->objects[index].ex = *m;
     ctx->desc_dirty = true;
     return ERAY_OK;
 }

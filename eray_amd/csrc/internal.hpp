@@ -41,6 +41,9 @@ struct TexView {
 struct MaterialDesc {
     TexView color;  // IColor, 3 floats per texel
     TexView diffuse, specular, specular_power, reflection;  // IValue
+    // example: 1 = color and diffuse are main.rs's graph evaluated at the hit texel
+    uint32_t example, ex_w, ex_h;
+    float ex_xf, ex_yf, ex_r, ex_g, ex_b, ex_factor;
 };
 
 // Scenes up to these sizes are preloaded whole into each frame workgroup's LDS.
@@ -68,7 +71,7 @@ struct ObjGeom {  // what the triangle scans need of an object, 80 B
     const TriHot* bin_hot;
 };
 
-struct alignas(16) ObjectDesc {  // 160 B: the LDS scene copy moves whole 16-B words
+struct alignas(16) ObjectDesc {  // 208 B: the LDS scene copy moves whole 16-B words
     ObjGeom g;
     MaterialDesc mat;
 };

@@ -24,7 +24,10 @@
 //
 // Shadow rays (engine.rs:136-142, 218-228) go through the same LDS tiles without culling; the
 // reference's degenerate bounding box rejects almost all of them before the scan.
+#include <cstdlib>
+
 #include "device_math.hpp"
+#include "glibc_cosf.hpp"
 #include "face_rect.hpp"
 #include "internal.hpp"
 
@@ -864,6 +867,15 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
         const float w = 1.0f - bu - bv;
         const float uv0 = ((sh.s2.y * w) + (sh.s2.w * bu)) + (sh.s3.y * bv);
         const float uv1 = ((sh.s2.z * w) + (sh.s3.x * bu)) + (sh.s3.z * bv);
+        if (mat.example) {  // main.rs's graph at the texel Material::get would read
+            const uint32_t ix = sat_u32(uv0 * (float)mat.ex_w) % mat.ex_w;
+            const uint32_t iy = sat_u32(uv1 * (float)mat.ex_h) % mat.ex_h;
+            const float wv = __builtin_fabsf(libm::cosf_glibc(((float)ix * mat.ex_xf + (float)iy * mat.ex_yf) / 10.0f));
+            const float omf = 1.0f - mat.ex_factor;  // mix_color.rs:89 (material_example_kernel)
+            color = rgb{wv * omf + mat.ex_r * mat.ex_factor, wv * omf + mat.ex_g * mat.ex_factor,
+                        wv * omf + mat.ex_b * mat.ex_factor};
+            kd = wv;
+        }
         if (mat.color.data) {
             const TexView& tv = mat.color;
             const uint32_t ix = sat_u32(uv0 * (float)tv.w) % tv.w;
@@ -1173,7 +1185,12 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
             per_cu = 1;
         per_cu_dyn = dyn;
     }
-    const uint32_t grid = min(want, (uint32_t)(per_cu * cus));
+    static const int cap = [] {  // tuning knob (diagnostics): workgroups per CU at most
+        const char* e = getenv("ERAY_FRAME_WG_PER_CU");
+        return e ? atoi(e) : 0;
+    }();
+    const int wg_cu = cap > 0 && cap < per_cu ? cap : per_cu;
+    const uint32_t grid = min(want, (uint32_t)(wg_cu * cus));
     frame_kernel<C, L, S, K><<<grid, kWG, dyn, s>>>(p);
     return hipGetLastError();
 }

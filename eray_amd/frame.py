@@ -26,10 +26,16 @@ def fov_for(width: int, height: int) -> tuple[float, float]:
 
 
 class MainScene:
-    """Uploads the mesh, evaluates the material on the GPU and configures camera + lights."""
+    """Uploads the mesh, evaluates the material on the GPU and configures camera + lights.
+
+    material="textures": Material::update's textures (eray_material_example), sampled per hit
+    as the reference does.  material="example": the same graph evaluated at the hit texel
+    (eray_scene_set_object_example_material) — bit-identical, no textures."""
 
     def __init__(self, ctx: capi.Context, positions, normals, uvs, width: int, height: int,
-                 texture: int = 1024, fov=None):
+                 texture: int = 1024, fov=None, material: str = "textures"):
+        if material not in ("textures", "example"):
+            raise ValueError(f"material {material!r}")
         self.ctx = ctx
         self.width, self.height = width, height
         self.texture = texture
@@ -44,7 +50,11 @@ class MainScene:
         ctx.set_camera(cam)
         ctx.add_light(capi.make_light((0.0, 2.0, 0.0), "ambient", (1.0, 1.0, 1.0), 0.2))
         ctx.add_light(capi.make_light((1.0, 1.0, 2.0), "point", (1.0, 1.0, 1.0), 1.0))
-        ctx.add_object(positions, normals, uvs, color=self.color.image(), diffuse=self.diffuse.image())
+        idx = ctx.add_object(positions, normals, uvs, color=self.color.image(), diffuse=self.diffuse.image())
+        if material == "example":
+            i = MAIN_RS_INPUTS
+            ctx.set_object_example_material(idx, texture, texture, i["x_fac"], i["y_fac"], i["r"], i["g"], i["b"],
+                                            i["factor"])
 
     def evaluate_material(self) -> None:
         """Material::update of main.rs's graph (one fused pass)."""

@@ -17,7 +17,9 @@
  *   eray_material_example   main.rs:80-144 + lib/material.rs:35-53 (Graph::run of main's graph,
  *                           all four nodes fused into one pass)
  *   eray_scene_*            lib/scene.rs:39-54 (add_object / add_light / set_camera) and
- *                           lib/object.rs:213-230 (Object::build -> device triangle arrays)
+ *                           lib/object.rs:213-230 (Object::build -> device triangle arrays);
+ *                           eray_scene_set_object_example_material: lib/material.rs:56-94
+ *                           (Material::get) over main.rs:80-144's graph, per hit texel
  *   eray_render             lib/engine.rs:46-81 (Engine::render: camera rays, first-hit
  *                           Object::intersects object.rs:58-81, Triangle::intersects
  *                           primitives.rs:41-72, cast_ray shading engine.rs:112-216,
@@ -157,11 +159,28 @@ typedef struct eray_object {        /* Object<Built> (object.rs:30-52) */
     eray_material material;         /* device textures; must outlive the scene */
 } eray_object;
 
+/* main.rs:80-144's material graph (wave -> rgb -> mix with flat_color) evaluated at the hit
+ * texel instead of sampled from its textures: Material::get reads texel
+ * ((u*width) as u32 % width, (v*height) as u32 % height) of width x height images, so computing
+ * that one texel (wave.rs:127, mix_color.rs:89) is bit-identical to eray_material_example's
+ * textures and needs neither the 16 B/texel images nor a memory round trip per hit. */
+typedef struct eray_material_example_params {
+    uint32_t width;                 /* the graph's "width" / "height" inputs (as u32) */
+    uint32_t height;
+    float x_fac, y_fac;             /* wave inputs */
+    float r, g, b;                  /* flat_color inputs */
+    float factor;                   /* mix_color input */
+} eray_material_example_params;
+
 int eray_scene_reset(eray_ctx* ctx);
 int eray_scene_set_camera(eray_ctx* ctx, const eray_camera* camera);
 int eray_scene_add_light(eray_ctx* ctx, const eray_light* light);
 /* Copies the host arrays; *object_index (optional) receives the object's position. */
 int eray_scene_add_object(eray_ctx* ctx, const eray_object* object, uint32_t* object_index);
+/* The object's color and diffuse outputs become main.rs's graph evaluated per hit (see
+ * eray_material_example_params); its other outputs stay as given. */
+int eray_scene_set_object_example_material(eray_ctx* ctx, uint32_t object_index,
+                                           const eray_material_example_params* params);
 /* Camera::size(): (width, (width as f32 / (fov0/fov1)) as u32) */
 int eray_camera_size(const eray_camera* camera, uint32_t* width, uint32_t* height);
 

@@ -32,6 +32,9 @@ def timed(label, flags=0, frames=200, row0=0, rows=H, ppm_out=True):
     print(f"{label:48s} frame {wall * 1e6:8.2f} us   kernel {ms * 1e3:8.2f} us", flush=True)
 
 
+sc = MainScene(ctx, *mesh, W, H, material="example")
+timed("cube, material evaluated per hit")
+sc.close()
 sc = MainScene(ctx, *mesh, W, H)
 timed("cube (main.rs scene)")
 timed("cube, f32 image only (no PPM)", ppm_out=False)

@@ -54,8 +54,8 @@ def test_oracle_reproduces_texture_fixture(oracle):
     assert np.array_equal(color, fx["color"]) and np.array_equal(diffuse, fx["diffuse"])
 
 
-def _gpu_frame(gpu, cube, w, h, fov):
-    sc = MainScene(gpu, *cube, w, h, texture=1024, fov=fov)
+def _gpu_frame(gpu, cube, w, h, fov, material="textures"):
+    sc = MainScene(gpu, *cube, w, h, texture=1024, fov=fov, material=material)
     rgb = gpu.empty((h, w, 3), np.float32)
     ppm = gpu.empty((h, w, 3), np.uint8)
     face = gpu.empty((h, w), np.int32)
@@ -69,9 +69,10 @@ def _gpu_frame(gpu, cube, w, h, fov):
 
 
 @pytest.mark.gpu
-def test_gpu_c1_matches_fixture(gpu, cube):
+@pytest.mark.parametrize("material", ["textures", "example"])
+def test_gpu_c1_matches_fixture(gpu, cube, material):
     fx = np.load(os.path.join(GOLDEN, "cube_c1_256.npz"))
-    rgb, ppm, face = _gpu_frame(gpu, cube, 256, 256, (60.0, 60.0))
+    rgb, ppm, face = _gpu_frame(gpu, cube, 256, 256, (60.0, 60.0), material)
     assert np.array_equal(face, fx["face"].astype(np.int32))
     assert np.array_equal(ppm, fx["ppm"])
     got = rgb.reshape(-1, 3)[fx["hit_index"]]
@@ -80,10 +81,12 @@ def test_gpu_c1_matches_fixture(gpu, cube):
 
 
 @pytest.mark.gpu
-def test_gpu_c2_matches_digests(gpu, cube):
-    """The bench workload at full size, bit for bit, against the oracle's committed digests."""
+@pytest.mark.parametrize("material", ["textures", "example"])
+def test_gpu_c2_matches_digests(gpu, cube, material):
+    """The bench workload at full size, bit for bit, against the oracle's committed digests —
+    with the material sampled from its textures and evaluated per hit texel."""
     g = _digests()["c2"]
-    rgb, ppm, face = _gpu_frame(gpu, cube, 1920, 1080, (16.0, 9.0))
+    rgb, ppm, face = _gpu_frame(gpu, cube, 1920, 1080, (16.0, 9.0), material)
     assert _sha(face.astype(np.int32)) == g["face_sha256"]
     assert _sha(rgb.astype(np.float32)) == g["rgb_f32_sha256"]
     assert _sha(ppm) == g["ppm_body_sha256"]

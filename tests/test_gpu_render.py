@@ -319,10 +319,11 @@ def standin70k():
             np.ascontiguousarray(t[ft].reshape(-1, 6)))
 
 
-def test_c3_binned_equals_brute_force(gpu, standin70k):
+@pytest.mark.parametrize("material", ["textures", "example"])
+def test_c3_binned_equals_brute_force(gpu, standin70k, material):
     """Screen bins (bins.hip) for a 70k-face object: bit-identical to the brute-force scan."""
     W, H = 480, 270
-    sc = MainScene(gpu, *standin70k, W, H, texture=256, fov=(16.0, 9.0))
+    sc = MainScene(gpu, *standin70k, W, H, texture=256, fov=(16.0, 9.0), material=material)
     a = gpu_render(gpu, W, H)
     b = gpu_render(gpu, W, H, flags=capi.RENDER_BRUTE_FORCE)
     sc.close()
@@ -347,4 +348,15 @@ def test_c3_full_size_rows_match_oracle(gpu, oracle, standin70k):
         part, part_face, _ = gpu_render(gpu, W, H, row0=row0, rows=rows)
         assert np.array_equal(part_face, ref_face)
         assert_bit_equal(part, ref, f"c3 row block {row0}+{rows}")
+    sc.close()
+
+
+def test_example_material_errors(gpu, cube):
+    sc = MainScene(gpu, *cube, 64, 64, texture=16)
+    with pytest.raises(capi.ErayError) as e:
+        gpu.set_object_example_material(5, 16, 16, 1.0, 1.0, 1.0, 0.0, 0.0, 0.5)
+    assert e.value.status == capi.E_INVALID_ARGUMENT
+    with pytest.raises(capi.ErayError) as e:
+        gpu.set_object_example_material(0, 0, 16, 1.0, 1.0, 1.0, 0.0, 0.0, 0.5)
+    assert e.value.status == capi.E_OUT_OF_BOUNDS
     sc.close()
