@@ -661,10 +661,16 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// i % n for the texture sizes of Image::mod_get (image.rs:36-38); n is wave-uniform and a power
+// of two in practice, where the modulo is a mask
+__device__ __forceinline__ uint32_t mod_size(uint32_t i, uint32_t n) {
+    return (n & (n - 1)) == 0 ? (i & (n - 1)) : i % n;
+}
+
 __device__ __forceinline__ bool tex_value(const TexView& tv, float x, float y, float& out) {
     if (!tv.data) return false;
-    const uint32_t ix = sat_u32(x * (float)tv.w) % tv.w;
-    const uint32_t iy = sat_u32(y * (float)tv.h) % tv.h;
+    const uint32_t ix = mod_size(sat_u32(x * (float)tv.w), tv.w);
+    const uint32_t iy = mod_size(sat_u32(y * (float)tv.h), tv.h);
     out = as_global(tv.data)[(size_t)iy * tv.w + ix];
     return true;
 }
@@ -868,8 +874,8 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
         const float uv0 = ((sh.s2.y * w) + (sh.s2.w * bu)) + (sh.s3.y * bv);
         const float uv1 = ((sh.s2.z * w) + (sh.s3.x * bu)) + (sh.s3.z * bv);
         if (mat.example) {  // main.rs's graph at the texel Material::get would read
-            const uint32_t ix = sat_u32(uv0 * (float)mat.ex_w) % mat.ex_w;
-            const uint32_t iy = sat_u32(uv1 * (float)mat.ex_h) % mat.ex_h;
+            const uint32_t ix = mod_size(sat_u32(uv0 * (float)mat.ex_w), mat.ex_w);
+            const uint32_t iy = mod_size(sat_u32(uv1 * (float)mat.ex_h), mat.ex_h);
             const float wv = __builtin_fabsf(libm::cosf_glibc(((float)ix * mat.ex_xf + (float)iy * mat.ex_yf) / 10.0f));
             const float omf = 1.0f - mat.ex_factor;  // mix_color.rs:89 (material_example_kernel)
             color = rgb{wv * omf + mat.ex_r * mat.ex_factor, wv * omf + mat.ex_g * mat.ex_factor,
@@ -878,8 +884,8 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
         }
         if (mat.color.data) {
             const TexView& tv = mat.color;
-            const uint32_t ix = sat_u32(uv0 * (float)tv.w) % tv.w;
-            const uint32_t iy = sat_u32(uv1 * (float)tv.h) % tv.h;
+            const uint32_t ix = mod_size(sat_u32(uv0 * (float)tv.w), tv.w);
+            const uint32_t iy = mod_size(sat_u32(uv1 * (float)tv.h), tv.h);
             const auto* c = as_global(tv.data) + 3 * ((size_t)iy * tv.w + ix);
             color = rgb{c[0], c[1], c[2]};
         }
