@@ -88,14 +88,66 @@ def build(jobs: int = 4, verbose: bool = False, force: bool = False, trace: bool
     return lib_path
 
 
+HOST_SOURCES = ["image.cpp", "graph.cpp", "shaderlib.cpp", "engine.cpp"]
+HOST_LIB = os.path.join(LIB_DIR, "liberay_host.so")
+BIN_DIR = os.path.join(PKG, "bin")
+ROCM_LIB = "/opt/rocm/lib"
+
+
+def build_host(jobs: int = 4, verbose: bool = False, force: bool = False) -> list[str]:
+    """The C++ host (include/eray/, eray_amd/host/): liberay_host.so over the C-ABI library,
+    the eray_main CLI (main.rs) and the tests/cpp/test_host unit-test binary.  Plain g++: the
+    host code never includes HIP headers."""
+    hip_lib = build(jobs, verbose, force)
+    host = os.path.join(PKG, "host")
+    cxx = shutil.which("g++") or "g++"
+    flags = ["-std=c++17", "-O2", "-fPIC", "-Wall", "-I" + os.path.join(ROOT, "include")]
+    headers = [os.path.join(ROOT, "include", "eray", f) for f in os.listdir(os.path.join(ROOT, "include", "eray"))]
+    headers.append(os.path.join(ROOT, "include", "eray_hip.h"))
+    obj_dir = os.path.join(OBJ, "host")
+    os.makedirs(obj_dir, exist_ok=True)
+    os.makedirs(BIN_DIR, exist_ok=True)
+    link = ["-L" + LIB_DIR, "-leray_hip", "-Wl,-rpath,$ORIGIN", "-Wl,-rpath,$ORIGIN/../lib",
+            "-Wl,-rpath-link," + ROCM_LIB, "-Wl,-rpath," + ROCM_LIB]
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"host build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+
+    objs, cmds = [], []
+    for src in HOST_SOURCES:
+        s, o = os.path.join(host, src), os.path.join(obj_dir, src + ".o")
+        objs.append(o)
+        if force or not _newer(o, [s] + headers):
+            cmds.append([cxx, *flags, "-c", s, "-o", o])
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        list(ex.map(run, cmds))
+    if force or cmds or not _newer(HOST_LIB, objs + [hip_lib]):
+        run([cxx, "-shared", "-o", HOST_LIB, *objs, *link])
+    outs = [HOST_LIB]
+    for name, src in (("eray_main", os.path.join(host, "main.cpp")),
+                      ("test_host", os.path.join(ROOT, "tests", "cpp", "test_host.cpp"))):
+        exe = os.path.join(BIN_DIR, name)
+        if force or not _newer(exe, [src, HOST_LIB] + headers):
+            run([cxx, *flags, src, "-o", exe, "-L" + LIB_DIR, "-leray_host", *link])
+        outs.append(exe)
+    return outs
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--trace", action="store_true", help="build the diagnostic phase-trace variant")
+    ap.add_argument("--host", action="store_true", help="also build the C++ host (liberay_host.so, bin/)")
     a = ap.parse_args()
     print(build(a.jobs, a.verbose, a.force, a.trace))
+    if a.host:
+        print("\n".join(build_host(a.jobs, a.verbose, a.force)))
 
 
 if __name__ == "__main__":

@@ -5,7 +5,7 @@
  * Everything here is plain C: opaque context pointer, plain pointers, sizes and status codes.
  * It is what the reference's Rust host (Engine / Scene / Material / shader Graph) would bind
  * with one `extern "C"` block, and what this repository's own C++ host
- * (include/eray/*.hpp) and Python tooling (eray_amd/) call.
+ * (include/eray/ headers) and Python tooling (eray_amd/) call.
  *
  * Entry points and the reference interface each one replaces (paths relative to the
  * reference checkout, src/...):

@@ -9,8 +9,9 @@ oracle change are checked against the same bytes.
 Fixtures
   cube_c1_256.npz   C1 (cube.obj, 256x256, main.rs scene): the PPM body bytes (file order),
                     the hit face per pixel, and the f32 RGB of the hit pixels (indices + values)
-  digests.json      SHA-256 of the PPM body and of the f32 image for C1 and for C2
-                    (1920x1080), the per-frame hit/test counters, and the P6 headers
+  digests.json      SHA-256 of the PPM body and of the f32 image for C1, C2 (1920x1080) and
+                    main.rs's 1024x1024 output.ppm, the per-frame hit/test counters, and the P6
+                    headers
   texture_8x4.npz   the example material graph (wave -> rgb -> mix with flat) at 8x4 texels:
                     color and diffuse images
 """
@@ -40,7 +41,9 @@ def frame(mesh, w, h, fov):
 def main() -> None:
     mesh = load_obj_file(os.path.join(ROOT, "objects", "cube.obj"))
     digests = {}
-    for tag, (w, h, fov) in {"c1": (256, 256, (60.0, 60.0)), "c2": (1920, 1080, (16.0, 9.0))}.items():
+    configs = {"c1": (256, 256, (60.0, 60.0)), "c2": (1920, 1080, (16.0, 9.0)),
+               "main_rs": (1024, 1024, (60.0, 60.0))}  # main.rs's own 1024x1024 render
+    for tag, (w, h, fov) in configs.items():
         rgb, face, stats = frame(mesh, w, h, fov)
         full = O.ppm_bytes(rgb)  # the whole P6 file: header + body
         header = f"P6 {w} {h} 255\n".encode()
