@@ -542,50 +542,61 @@ struct BinLds {
 constexpr uint32_t kBinLdsBytes = (sizeof(BinLds) + 15) / 16 * 16;
 constexpr uint32_t kWide = 16;  // candidates that may cover more pixels are tested by the whole wave
 
-// Primary-ray first hit of a binned object (bins.hip).  The reference's first hit by index is
-// the smallest index among the faces whose Triangle::intersects passes, so the candidates of the
-// sub-block's bin are processed 64 at a time as (candidate, pixel) pairs: each entry carries the
-// pixels where its four culling bounds can pass (bin_pixels), restricted to pixels still without
-// a hit; narrow candidates' pairs are compacted in LDS and tested one per lane, wide ones by the
-// whole wave; every hit lowers the pixel's best bin position (positions increase with the face
-// index).  Work follows the pixels a face can cover, not 64 lanes per face.  The winner is
-// re-tested for u, v, t.
+// Primary-ray first hit of a binned object (bins.hip), all four waves of the workgroup together
+// (every wave calls it; workgroup-uniform).  The reference's first hit by index is the smallest
+// index among the faces whose Triangle::intersects passes, so each wave's sub-block bin is cut
+// into chunks of 64 entries and the workgroup's chunks are dealt round-robin over its waves — a
+// bin at a dense spot (thousands of faces) is shared four ways.  A chunk is tested as (face,
+// pixel) pairs: each entry carries the pixels where its four culling bounds can pass
+// (bin_pixels), restricted to the sub-block's pixels still without a hit; narrow faces' pairs
+// are compacted in LDS and tested one per lane, wide ones by the whole wave; a hit lowers the
+// pixel's best bin position with an LDS atomicMin (positions grow with the face index).  Work
+// follows the pixels a face can cover, not 64 lanes per face.  Each wave then re-tests its
+// pixels' winners for u, v, t.
 template <typename Activate>
-__device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32_t bin, uint32_t wx0, uint32_t py0,
-                                 int& st, const f3& o, const f3& d, Activate&& activate, int& found, float& hu,
-                                 float& hv, float& ht, BinLds& L) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t lo = load_const(ob.bin_start, bin), hi = load_const(ob.bin_start, bin + 1);
-    if (lo == hi) return;
-    if (__any(st == kUndecided)) {  // every pixel's ray and bbox verdict, up front
+__device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32_t bin, int& st, const f3& o,
+                                 const f3& d, Activate&& activate, int& found, float& hu, float& hv, float& ht,
+                                 char* s_bins) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr uint32_t kWaves = kWG / 64;
+    BinLds& L = *reinterpret_cast<BinLds*>(s_bins + wave * kBinLdsBytes);
+    uint32_t* s_range = reinterpret_cast<uint32_t*>(s_bins + kWaves * kBinLdsBytes);  // [lo, hi] per wave
+    uint32_t lo = load_const(ob.bin_start, bin), hi = load_const(ob.bin_start, bin + 1);
+    if (lo != hi && __any(st == kUndecided)) {  // every pixel's ray and bbox verdict, up front
         const bool a = activate();
         if (st == kUndecided) st = a ? kSearching : kDone;
     }
-    if (!__any(st == kSearching)) return;
+    if (!__any(st == kSearching)) hi = lo;  // nothing to search in this sub-block
     L.dir[0][lane] = d.x;
     L.dir[1][lane] = d.y;
     L.dir[2][lane] = d.z;
     L.best[lane] = st == kSearching ? 0xffffffffu : 0u;  // 0: never improved
-    uint32_t n_pairs = 0, n_chunks = 0;
-    if (hi - lo > 200) ERAY_TRACE(12);
-    // the next chunk's entries are loaded while the current chunk is processed
-    unsigned long long m_n = 0;
-    TriHot h_n{};
-    auto fetch = [&](uint32_t base) {
-        if (base + lane < hi) {
-            m_n = ob.bin_mask[base + lane];
-            h_n = ob.bin_hot[base + lane];
-        }
-    };
-    fetch(lo);
-    for (uint32_t base = lo; base < hi; base += 64) {
-        ++n_chunks;
+    if (lane == 0) {
+        s_range[2 * wave] = lo;
+        s_range[2 * wave + 1] = hi;
+    }
+    __syncthreads();
+    uint32_t chunks[kWaves], total = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kWaves; ++w) {
+        chunks[w] = (s_range[2 * w + 1] - s_range[2 * w] + 63) / 64;
+        total += chunks[w];
+    }
+    for (uint32_t item = wave; item < total; item += kWaves) {  // this wave's chunks
+        uint32_t w = 0, c = item;
+        while (c >= chunks[w]) c -= chunks[w++];
+        BinLds& T = *reinterpret_cast<BinLds*>(s_bins + w * kBinLdsBytes);  // the chunk's sub-block
+        const uint32_t base = s_range[2 * w] + 64 * c, end = s_range[2 * w + 1];
+        // pixels of that sub-block this chunk can still improve: chunks run out of order, so a
+        // pixel stays live while its best position lies beyond the chunk's first entry
+        const unsigned long long live = __ballot(T.best[lane] > base);
+        if (!live) continue;
         const uint32_t j = base + lane;
-        // pixels still without a hit (later chunks hold later faces: a hit is final)
-        const unsigned long long live = __ballot(st == kSearching && L.best[lane] == 0xffffffffu);
-        const unsigned long long pix = j < hi ? (m_n & live) : 0ull;  // the live pixels this face may hit
-        L.cand[lane] = h_n;
-        if (base + 64 < hi) fetch(base + 64);
+        unsigned long long pix = 0;  // live pixels this face may hit
+        if (j < end) {
+            pix = ob.bin_mask[j] & live;
+            L.cand[lane] = ob.bin_hot[j];
+        }
         const uint32_t cnt = (uint32_t)__popcll(pix);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();  // L.cand of this chunk visible to the wave
@@ -595,12 +606,14 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
         while (wide) {
             const uint32_t s = (uint32_t)(__ffsll(wide) - 1);
             wide &= wide - 1;
-            const unsigned long long ps = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pix >> 32), (int)s) << 32) |
-                                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pix, (int)s);
+            const unsigned long long ps =
+                ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pix >> 32), (int)s) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pix, (int)s);
             const uint32_t pos = base + s;
-            if (((ps >> lane) & 1ull) && pos < L.best[lane]) {
+            if (((ps >> lane) & 1ull) && pos < T.best[lane]) {
                 float u, v, t;
-                if (exact_test(L.cand[s], o, d, u, v, t)) L.best[lane] = pos;
+                const f3 dd = mk3(T.dir[0][lane], T.dir[1][lane], T.dir[2][lane]);
+                if (exact_test(L.cand[s], o, dd, u, v, t)) atomicMin(&T.best[lane], pos);
             }
         }
         // narrow candidates: (candidate, pixel) pairs compacted in LDS, one test per lane
@@ -611,8 +624,7 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
             const uint32_t y = __shfl_up(incl, off);
             if ((int)lane >= off) incl += y;
         }
-        const uint32_t total = __shfl(incl, 63);
-        n_pairs += total;
+        const uint32_t npairs = __shfl(incl, 63);
         uint32_t at = incl - ncnt;
         unsigned long long np = ncnt ? pix : 0ull;
         while (np) {
@@ -623,29 +635,23 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (uint32_t q = 0; q < total; q += 64) {
-            if (q + lane < total) {
+        for (uint32_t q = 0; q < npairs; q += 64) {
+            if (q + lane < npairs) {
                 const uint32_t pr = L.pairs[q + lane];
                 const uint32_t slot = pr >> 6, px = pr & 63;
                 const uint32_t pos = base + slot;
-                if (pos < L.best[px]) {  // a pixel already hit by an earlier face needs no test
+                if (pos < T.best[px]) {  // a pixel already hit by an earlier face needs no test
                     float u, v, t;
-                    const f3 dd = mk3(L.dir[0][px], L.dir[1][px], L.dir[2][px]);
-                    if (exact_test(L.cand[slot], o, dd, u, v, t)) atomicMin(&L.best[px], pos);
+                    const f3 dd = mk3(T.dir[0][px], T.dir[1][px], T.dir[2][px]);
+                    if (exact_test(L.cand[slot], o, dd, u, v, t)) atomicMin(&T.best[px], pos);
                 }
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_wave_barrier();  // L.cand / L.pairs are rewritten by the next chunk
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (!__any(st == kSearching && L.best[lane] == 0xffffffffu)) break;
     }
-    if (hi - lo > 200) {
-        ERAY_TRACE(13);
-        ERAY_TRACE_VAL(9, hi - lo);
-        ERAY_TRACE_VAL(10, n_pairs);
-        ERAY_TRACE_VAL(11, n_chunks);
-    }
+    __syncthreads();  // every chunk of every sub-block is done
     const uint32_t mine = L.best[lane];
     if (st == kSearching && mine != 0xffffffffu) {
         float u, v, t;
@@ -656,9 +662,7 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
         ht = t;
         st = kDone;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();  // L is reused by the next object / sub-block
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __syncthreads();  // the LDS is reused by the next object / sub-block
 }
 
 // i % n for the texture sizes of Image::mod_get (image.rs:36-38); n is wave-uniform and a power
@@ -817,7 +821,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
         const bool direct = !kLdsTiles || ob.tri_count <= kDirectMax;
         // outside the object's pixel rectangle no primary ray can hit it (only where skipping
         // keeps the workgroup's barriers uniform)
-        if (kCull && (direct || ob.bin_start) && !rect_meets(ob, p, wx0, py0)) continue;
+        if (kCull && direct && !rect_meets(ob, p, wx0, py0)) continue;
         auto activate = [&]() {
             if (!ray_ready) {
                 uint32_t pxo = px, yo = y;  // opaque: keep ray generation on this path
@@ -832,10 +836,9 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
         if (direct) {
             first_hit<kCull, false>(p, sc, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull, activate, f, u,
                                     v, t);
-        } else if (kCull && ob.bin_start) {  // per wave: no LDS tiles, no barrier
+        } else if (kCull && ob.bin_start) {  // the workgroup's four sub-blocks together
             const uint32_t bin = ((p.row0 + py0 + kBinH - p.bin_phase) / kBinH) * p.bins_x + wx0 / kBinW;
-            first_hit_binned(p, ob, bin, wx0, py0, st, C, d, activate, f, u, v, t,
-                             *reinterpret_cast<BinLds*>(s_bins + wave * kBinLdsBytes));
+            first_hit_binned(p, ob, bin, st, C, d, activate, f, u, v, t, s_bins);
         } else {
             first_hit<kCull, kLdsTiles>(p, sc, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull, activate,
                                         f, u, v, t);
@@ -1039,7 +1042,7 @@ __global__ void __launch_bounds__(kWG) frame_kernel(FrameParams p) {
     // large objects: LDS tiles (shadow rays, brute force) and, aliased, the per-wave binned
     // primary search (first_hit ends its tile loop on a barrier, so the two never overlap)
     constexpr size_t kTileBytes = kTriTile * (sizeof(TriHot) + ((kCull && kLdsTiles) ? sizeof(TriCull) : 0));
-    constexpr size_t kBinBytes = (kCull && kLdsTiles) ? (kWG / 64) * kBinLdsBytes : 0;
+    constexpr size_t kBinBytes = (kCull && kLdsTiles) ? (kWG / 64) * kBinLdsBytes + 2 * (kWG / 64) * 4 : 0;
     __shared__ __attribute__((aligned(16))) char s_large[kLdsTiles ? (kTileBytes > kBinBytes ? kTileBytes : kBinBytes) : 16];
     TriHot* s_hot = reinterpret_cast<TriHot*>(s_large);
     TriCull* s_cull = reinterpret_cast<TriCull*>(s_large + kTriTile * sizeof(TriHot));
