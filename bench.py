@@ -127,12 +127,25 @@ def main() -> None:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
+    # ERAY_BENCH_REHEARSAL=1 rehearses the N > 1 path on ONE GPU: every rank on device 0, gloo
+    # collectives through host memory (RCCL will not put two ranks on one device).  Never used
+    # for a reported number.
+    rehearsal = os.environ.get("ERAY_BENCH_REHEARSAL") == "1"
+    device = 0 if rehearsal else local_rank
+    torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+
+    def allreduce(value, dtype, op):
+        t = torch.tensor([value], dtype=dtype, device="cpu" if rehearsal else "cuda")
+        dist.all_reduce(t, op=op)
+        return t.item()
 
     mesh = load_obj_file(args.mesh)
-    ctx = capi.Context(local_rank)
+    ctx = capi.Context(device)
     stream = torch.cuda.Stream()  # one stream shared by the library, torch and RCCL
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
@@ -190,16 +203,12 @@ def main() -> None:
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        h = torch.tensor([hits], dtype=torch.int64, device="cuda")
-        dist.all_reduce(h)
-        hits_all = int(h.item())
+        elapsed = float(allreduce(elapsed, torch.float64, dist.ReduceOp.MAX))
+        hits_all = int(allreduce(hits, torch.int64, dist.ReduceOp.SUM))
     else:
         hits_all = hits
-    # the frame kernel's own duration: the same frames once more, each launch bracketed by HIP
-    # events on the library's stream (the graph replay above leaves no room for them)
+    # the frame kernel's duration: the same frames replayed once more, bracketed by HIP events on
+    # the library's stream (back-to-back kernels: device time per frame)
     kernel_ms = scene.ctx.render_frames(args.steps, width, H_total, timed=True, **render_args())
     gather_ms = None
     if world > 1:  # one frame's gather, for the record
@@ -251,6 +260,7 @@ def main() -> None:
             "scene_setup_ms": round(t_setup * 1e3, 3),
             "gather_ms": None if gather_ms is None else round(gather_ms, 4),
             "gather": ("every frame" if args.gather_every_frame else "final frame") if world > 1 else None,
+            **({"rehearsal": "all ranks on GPU 0, gloo collectives: not a measurement"} if rehearsal else {}),
             "hit_pixels": hits_all,
             "roofline": {
                 "bound": "hbm",

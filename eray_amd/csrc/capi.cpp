@@ -726,53 +726,41 @@ int eray_render_prepare(eray_ctx* ctx, const eray_render_params* rp, uint32_t fr
 }
 
 int eray_render_frames(eray_ctx* ctx, const eray_render_params* rp, uint32_t frames,
-                       float* mean_kernel_ms) {
+                       float* mean_frame_ms) {
     FrameParams p;
     bool empty = false;
     if (int st = prepare_render(ctx, rp, &p, &empty)) return st;
-    if (mean_kernel_ms) *mean_kernel_ms = 0.0f;
+    if (mean_frame_ms) *mean_frame_ms = 0.0f;
     if (empty || !frames) return ERAY_OK;
-    if (!mean_kernel_ms) {  // replay the cached graph; plain launches for the remainder
-        uint32_t chunk = 0;
-        if (int st = ensure_plan(ctx, p, frames, &chunk)) return st;
-        hipError_t he = hipSuccess;
-        uint32_t done = 0;
-        for (; chunk && done + chunk <= frames && he == hipSuccess; done += chunk)
-            he = hipGraphLaunch(ctx->graph_exec, ctx->stream);
-        for (; done < frames && he == hipSuccess; ++done) he = launch_frame(ctx, p);
-        if (he != hipSuccess) return set_error(ctx, ERAY_E_HIP, "render loop: %s", hipGetErrorString(he));
-        return ERAY_OK;
-    }
-    // instrumented: plain launches, each bracketed by HIP events on the context's stream
-    std::vector<hipEvent_t> ev(2 * (size_t)frames, nullptr);
-    int st = ERAY_OK;
-    for (auto& e : ev) {
-        hipError_t he = hipEventCreate(&e);
-        if (he != hipSuccess) {
-            st = set_error(ctx, ERAY_E_HIP, "hipEventCreate: %s", hipGetErrorString(he));
-            break;
+    uint32_t chunk = 0;
+    if (int st = ensure_plan(ctx, p, frames, &chunk)) return st;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    if (mean_frame_ms) {
+        for (auto& e : ev) {
+            hipError_t he = hipEventCreate(&e);
+            if (he != hipSuccess) {
+                if (ev[0]) hipEventDestroy(ev[0]);
+                return set_error(ctx, ERAY_E_HIP, "hipEventCreate: %s", hipGetErrorString(he));
+            }
         }
     }
-    for (uint32_t f = 0; f < frames && st == ERAY_OK; ++f) {
-        hipError_t he = hipEventRecord(ev[2 * f], ctx->stream);
-        if (he == hipSuccess) he = launch_frame(ctx, p);
-        if (he == hipSuccess) he = hipEventRecord(ev[2 * f + 1], ctx->stream);
-        if (he != hipSuccess) st = set_error(ctx, ERAY_E_HIP, "render loop: %s", hipGetErrorString(he));
-    }
-    double total = 0.0;
-    if (st == ERAY_OK) {
-        hipError_t he = hipStreamSynchronize(ctx->stream);
-        for (uint32_t f = 0; f < frames && he == hipSuccess; ++f) {
-            float ms = 0.0f;
-            he = hipEventElapsedTime(&ms, ev[2 * f], ev[2 * f + 1]);
-            total += ms;
-        }
-        if (he != hipSuccess) st = set_error(ctx, ERAY_E_HIP, "render timing: %s", hipGetErrorString(he));
+    // replay the cached graph (back-to-back frame kernels); plain launches for the remainder
+    hipError_t he = mean_frame_ms ? hipEventRecord(ev[0], ctx->stream) : hipSuccess;
+    uint32_t done = 0;
+    for (; chunk && done + chunk <= frames && he == hipSuccess; done += chunk)
+        he = hipGraphLaunch(ctx->graph_exec, ctx->stream);
+    for (; done < frames && he == hipSuccess; ++done) he = launch_frame(ctx, p);
+    if (mean_frame_ms && he == hipSuccess) {
+        he = hipEventRecord(ev[1], ctx->stream);
+        if (he == hipSuccess) he = hipEventSynchronize(ev[1]);
+        float ms = 0.0f;
+        if (he == hipSuccess) he = hipEventElapsedTime(&ms, ev[0], ev[1]);
+        if (he == hipSuccess) *mean_frame_ms = ms / (float)frames;
     }
     for (auto e : ev)
         if (e) hipEventDestroy(e);
-    if (st == ERAY_OK) *mean_kernel_ms = (float)(total / frames);
-    return st;
+    if (he != hipSuccess) return set_error(ctx, ERAY_E_HIP, "render loop: %s", hipGetErrorString(he));
+    return ERAY_OK;
 }
 
 int eray_pack_ppm(eray_ctx* ctx, const float* rgb, uint32_t w, uint32_t h, uint8_t* out) {

@@ -28,4 +28,11 @@ def gather_ppm_rows(local: torch.Tensor, frame: torch.Tensor | None, world: int,
         if frame is not None and frame.data_ptr() != local.data_ptr():
             frame.copy_(local)
         return
+    if local.is_cuda and dist.get_backend() == "gloo":  # gloo gathers host tensors
+        host = local.cpu()
+        parts = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
+        dist.gather(host, parts, dst=0)
+        if rank == 0:
+            frame.copy_(torch.cat(parts, 0))
+        return
     dist.gather(local, list(frame.chunk(world, 0)) if rank == 0 else None, dst=0)

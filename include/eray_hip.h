@@ -207,12 +207,13 @@ typedef struct eray_render_params {
 
 int eray_render(eray_ctx* ctx, const eray_render_params* params);
 /* Renders `frames` frames back to back with the same parameters (a serving / animation loop
- * without a host round trip per frame).  By default the frame launches are replayed from a HIP
- * graph of up to 64 frames, captured on the context's stream and cached for these parameters.
- * When mean_kernel_ms is not NULL the frames are instead launched one by one, each bracketed by
- * HIP events, and the mean frame-kernel duration is returned (this call then waits). */
+ * without a host round trip per frame): the frame launches are replayed from a HIP graph of up
+ * to 64 frames, captured on the context's stream and cached for these parameters.  When
+ * mean_frame_ms is not NULL, two HIP events on the stream bracket the frames and the mean
+ * device time per frame is returned — the frame kernel back to back, within the graph's
+ * inter-kernel gap of its own duration (this call then waits). */
 int eray_render_frames(eray_ctx* ctx, const eray_render_params* params, uint32_t frames,
-                       float* mean_kernel_ms);
+                       float* mean_frame_ms);
 /* Builds (and caches) the launch plan eray_render_frames uses for these parameters and frame
  * count, without rendering: the one-time capture cost stays out of a timed or serving loop. */
 int eray_render_prepare(eray_ctx* ctx, const eray_render_params* params, uint32_t frames);
