@@ -27,7 +27,9 @@ LIB = os.path.join(LIB_DIR, "liberay_hip.so")
 SOURCES = ["render.hip", "bins.hip", "shaderlib.hip", "capi.cpp"]
 ARCH = "gfx950"
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
-            f"--offload-arch={ARCH}", "-I" + os.path.join(ROOT, "include")]
+            f"--offload-arch={ARCH}", "-I" + os.path.join(ROOT, "include"),
+            # the first 14 kernel-argument dwords arrive in SGPRs (frame_kernel's FrameHot)
+            "-mllvm", "-amdgpu-kernarg-preload-count=14"]
 
 
 def hipcc() -> str:
@@ -50,12 +52,17 @@ def _headers() -> list[str]:
     return hs
 
 
-def build(jobs: int = 4, verbose: bool = False, force: bool = False, trace: bool = False) -> str:
+def build(jobs: int = 4, verbose: bool = False, force: bool = False, trace: bool = False,
+          variant: str = "", defines: tuple = ()) -> str:
     """Build the product library; `trace` builds the diagnostic variant
-    lib/liberay_hip_trace.so instead (frame-kernel phase timestamps, ERAY_PHASE_TRACE)."""
-    obj_dir = os.path.join(OBJ, "trace") if trace else OBJ
-    lib_path = LIB.replace(".so", "_trace.so") if trace else LIB
+    lib/liberay_hip_trace.so instead (frame-kernel phase timestamps, ERAY_PHASE_TRACE).
+    `variant` + `defines`: a diagnostic A/B build lib/liberay_hip_<variant>.so with extra -D macros
+    (scripts/ab_variants.py); never the product library."""
+    tag = "trace" if trace else variant
+    obj_dir = os.path.join(OBJ, tag) if tag else OBJ
+    lib_path = LIB.replace(".so", f"_{tag}.so") if tag else LIB
     extra = ["-DERAY_PHASE_TRACE"] if trace else []
+    extra += [f"-D{d}" for d in defines]
     if trace and os.environ.get("ERAY_TRACE_REPEAT"):
         extra.append("-DERAY_PHASE_TRACE_REPEAT")
     os.makedirs(obj_dir, exist_ok=True)

@@ -597,6 +597,9 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     p.out_rgb = rp->out_rgb;
     p.out_ppm = rp->out_ppm;
     p.out_face = rp->out_face;
+    p.aligned = (p.img_w % 16) == 0 &&
+                ((reinterpret_cast<uintptr_t>(p.out_rgb) | reinterpret_cast<uintptr_t>(p.out_ppm) |
+                  reinterpret_cast<uintptr_t>(p.out_face)) & 15) == 0;
     p.tris = ctx->d_hot;
     p.shade = ctx->d_shade;
     p.cull = cull ? ctx->d_cull : nullptr;

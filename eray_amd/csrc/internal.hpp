@@ -95,6 +95,7 @@ struct FrameParams {
     float* out_rgb;
     uint8_t* out_ppm;
     int32_t* out_face;
+    uint32_t aligned;  // img_w % 16 == 0 and 16-byte aligned outputs: 16-byte row stores
     // scene
     const TriHot* tris;
     const TriShade* shade;

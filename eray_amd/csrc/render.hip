@@ -47,6 +47,18 @@ __device__ __forceinline__ const __attribute__((address_space(1))) float* as_glo
     return (const __attribute__((address_space(1))) float*)ptr;
 }
 template <typename T>
+__device__ __forceinline__ T as_global_rec(const T* ptr) {  // per-lane record read, global
+    static_assert(sizeof(T) % 16 == 0, "16-byte records only");
+    using v4 = unsigned int __attribute__((ext_vector_type(4)));
+    using gv4 = const __attribute__((address_space(1))) v4;
+    gv4* src = (gv4*)ptr;
+    T out;
+    v4* dst = reinterpret_cast<v4*>(&out);
+#pragma unroll
+    for (size_t k = 0; k < sizeof(T) / 16; ++k) dst[k] = src[k];
+    return out;
+}
+template <typename T>
 __device__ __forceinline__ T load_const(const T* base, size_t i) {
     static_assert(sizeof(T) % 4 == 0, "dword-sized records only");
     using cu32 = const __attribute__((address_space(4))) uint32_t;
@@ -59,27 +71,50 @@ __device__ __forceinline__ T load_const(const T* base, size_t i) {
 }
 
 // Diagnostic builds only (python -m eray_amd.build --trace): workgroups 0, 16, ..., 1008 (waves)
-// record s_memrealtime (100 MHz) at the frame kernel's phase boundaries.
+// record s_memrealtime (100 MHz) and s_memtime (shader clock) at the frame kernel's phase
+// boundaries.  Stamps go to LDS (no vector-memory counter the kernel's own waits would include)
+// and are copied out when the wave ends (ERAY_TRACE_FLUSH).
 #ifdef ERAY_PHASE_TRACE
 constexpr int kTraceSlots = 16;
 __device__ uint64_t g_trace[2 * 64 * 4 * kTraceSlots];  // [realtime | shader clock]
-#define ERAY_TRACE(slot)                                                                          \
-    do {                                                                                          \
-        if ((threadIdx.x & 63) == 0 && blockIdx.x % 16 == 0 && blockIdx.x < 1024) {               \
-            const uint32_t i_ = (blockIdx.x / 16 * 4 + (threadIdx.x >> 6)) * kTraceSlots + (slot); \
-            g_trace[i_] = __builtin_amdgcn_s_memrealtime();                                       \
-            g_trace[64 * 4 * kTraceSlots + i_] = __builtin_amdgcn_s_memtime();                   \
-        }                                                                                         \
+__shared__ uint64_t s_trace[4][kTraceSlots][2];
+#define ERAY_TRACE_ON() ((threadIdx.x & 63) == 0 && blockIdx.x % 16 == 0 && blockIdx.x < 1024)
+#define ERAY_TRACE(slot)                                                  \
+    do {                                                                  \
+        if (ERAY_TRACE_ON()) {                                            \
+            s_trace[threadIdx.x >> 6][slot][0] = __builtin_amdgcn_s_memrealtime(); \
+            s_trace[threadIdx.x >> 6][slot][1] = __builtin_amdgcn_s_memtime();     \
+        }                                                                 \
     } while (0)
-#define ERAY_TRACE_VAL(slot, v)                                                                   \
-    do {                                                                                          \
-        if ((threadIdx.x & 63) == 0 && blockIdx.x % 16 == 0 && blockIdx.x < 1024) {               \
-            const uint32_t i_ = (blockIdx.x / 16 * 4 + (threadIdx.x >> 6)) * kTraceSlots + (slot); \
-            g_trace[i_] = (v);                                                                    \
-            g_trace[64 * 4 * kTraceSlots + i_] = 0;                                               \
-        }                                                                                         \
+#define ERAY_TRACE_VAL(slot, v)                                           \
+    do {                                                                  \
+        if (ERAY_TRACE_ON()) {                                            \
+            s_trace[threadIdx.x >> 6][slot][0] = (v);                     \
+            s_trace[threadIdx.x >> 6][slot][1] = 0;                       \
+        }                                                                 \
+    } while (0)
+#define ERAY_TRACE_CLEAR()                                                \
+    do {                                                                  \
+        if (ERAY_TRACE_ON())                                              \
+            for (int k_ = 0; k_ < kTraceSlots; ++k_) s_trace[threadIdx.x >> 6][k_][0] = s_trace[threadIdx.x >> 6][k_][1] = 0; \
+    } while (0)
+#define ERAY_TRACE_FLUSH()                                                \
+    do {                                                                  \
+        if (ERAY_TRACE_ON()) {                                            \
+            const uint32_t w_ = blockIdx.x / 16 * 4 + (threadIdx.x >> 6); \
+            for (int k_ = 0; k_ < kTraceSlots; ++k_) {                    \
+                g_trace[w_ * kTraceSlots + k_] = s_trace[threadIdx.x >> 6][k_][0];                   \
+                g_trace[64 * 4 * kTraceSlots + w_ * kTraceSlots + k_] = s_trace[threadIdx.x >> 6][k_][1]; \
+            }                                                             \
+        }                                                                 \
     } while (0)
 #else
+#define ERAY_TRACE_CLEAR() \
+    do {                   \
+    } while (0)
+#define ERAY_TRACE_FLUSH() \
+    do {                   \
+    } while (0)
 #define ERAY_TRACE_VAL(slot, v) \
     do {                        \
     } while (0)
@@ -342,6 +377,21 @@ __device__ __forceinline__ T lds_uniform(const T* ptr) {
     return out;
 }
 
+// The frame kernel's first reads, passed as leading scalar kernel arguments: the compiler
+// preloads them into SGPRs (-amdgpu-kernarg-preload-count, build.py), so the scene preload's
+// loads issue without a kernel-argument round trip first.
+struct FrameHot {
+    const ObjectDesc* objects;
+    const LightDesc* lights;
+    const TriCull* cull;
+    const TriHot* tris;
+    const TriShade* shade;
+    uint32_t counts;      // nobj | nlights << 16
+    uint32_t total_tris;
+    uint32_t total_sub;   // detail sub-blocks
+    uint32_t grid;        // workgroups launched
+};
+
 struct SceneGlobal {
     const FrameParams& p;
     __device__ ObjGeom geom(uint32_t i) const { return load_const(&p.objects[i].g, 0); }
@@ -349,6 +399,7 @@ struct SceneGlobal {
     __device__ LightDesc light(uint32_t i) const { return load_const(p.lights, i); }
     __device__ TriCull cull(uint32_t g) const { return p.cull[g]; }        // per lane
     __device__ TriHot hot(uint32_t g) const { return load_const(p.tris, g); }  // uniform
+    __device__ TriHot hot_lane(uint32_t g) const { return as_global_rec(p.tris + g); }  // per lane
     __device__ TriShade shade(uint32_t g) const { return p.shade[g]; }     // per lane
 };
 
@@ -363,13 +414,16 @@ struct SceneLds {
     __device__ LightDesc light(uint32_t i) const { return lds_uniform(lights + i); }
     __device__ TriCull cull(uint32_t g) const { return culls[g]; }
     __device__ TriHot hot(uint32_t g) const { return hots[g]; }  // broadcast read (VGPRs)
+    __device__ TriHot hot_lane(uint32_t g) const { return hots[g]; }
     __device__ TriShade shade(uint32_t g) const { return shades[g]; }
 };
 
 // Copies the scene into LDS (layout: scene_lds_layout, internal.hpp): every 16-byte word is
 // loaded before any is stored, four per thread per pass, so a small scene costs one round trip.
-__device__ SceneLds preload_scene(const FrameParams& p, char* dyn) {
-    const SceneLdsLayout L = scene_lds_layout(p.nobj, p.nlights, p.total_tris, p.cull != nullptr);
+// `meanwhile()` runs once while the first pass's loads are in flight.
+template <typename Meanwhile>
+__device__ SceneLds preload_scene(const FrameHot& p, char* dyn, Meanwhile&& meanwhile) {
+    const SceneLdsLayout L = scene_lds_layout(p.counts & 0xffffu, p.counts >> 16, p.total_tris, p.cull != nullptr);
     const uint32_t n_obj = L.lights / 16, n_light = (L.cull - L.lights) / 16;
     const uint32_t n_cull = (L.hot - L.cull) / 16, n_hot = (L.shade - L.hot) / 16;
     const uint32_t total = L.bytes / 16;
@@ -384,23 +438,17 @@ __device__ SceneLds preload_scene(const FrameParams& p, char* dyn) {
     for (uint32_t base = 0; base < total; base += 4 * kWG) {
         v4 v[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            uint32_t i = base + k * kWG + threadIdx.x;
-            if (i >= total) continue;
-            gv4* src;
-            if (i < n_obj) {
-                src = src_obj + i;
-            } else if ((i -= n_obj) < n_light) {
-                src = src_light + i;
-            } else if ((i -= n_light) < n_cull) {
-                src = src_cull + i;
-            } else if ((i -= n_cull) < n_hot) {
-                src = src_hot + i;
-            } else {
-                src = src_shade + (i - n_hot);
-            }
+        for (int k = 0; k < 4; ++k) {  // branch-free (clamped index): the loads issue back to back
+            const uint32_t i = min(base + k * kWG + threadIdx.x, total - 1);
+            const uint32_t i1 = i - n_obj, i2 = i1 - n_light, i3 = i2 - n_cull, i4 = i3 - n_hot;
+            gv4* src = i < n_obj ? src_obj + i
+                     : i1 < n_light ? src_light + i1
+                     : i2 < n_cull ? src_cull + i2
+                     : i3 < n_hot ? src_hot + i3
+                     : src_shade + i4;
             v[k] = *src;
         }
+        if (base == 0) meanwhile();
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t i = base + k * kWG + threadIdx.x;
@@ -410,6 +458,42 @@ __device__ SceneLds preload_scene(const FrameParams& p, char* dyn) {
     return SceneLds{reinterpret_cast<const ObjectDesc*>(dyn + L.objs), reinterpret_cast<const LightDesc*>(dyn + L.lights),
                     reinterpret_cast<const TriCull*>(dyn + L.cull), reinterpret_cast<const TriHot*>(dyn + L.hot),
                     reinterpret_cast<const TriShade*>(dyn + L.shade)};
+}
+
+// Lanes whose Triangle::intersects could pass: the det and t conditions of exact_test, from the
+// same expressions (so the same values).  t = dot(ao, n) * (1 / det) is >= 0 exactly when
+// dot(ao, n) >= 0, except where the product underflows to -0 or 1 / det is 0 — those lanes are
+// kept.  A lane that fails here fails the exact test; a face no lane keeps is skipped.
+__device__ __forceinline__ bool plane_may_hit(f3 n, f3 a, f3 o, f3 d) {
+    const float det = -dot0(d, n);
+    const float dn = dot0(sub(o, a), n);
+    return (det >= 1e-6f) & !((dn < -1e-18f) & (det < 1e19f));
+}
+
+// Faces [0, n) (n <= 64; lane j holds face j's record) that some searching lane may hit
+// (plane_may_hit), as a bit mask.  The planes are broadcast from the lanes that hold them, four
+// faces per step.
+__device__ __forceinline__ unsigned long long plane_mask(const TriHot& mine, uint32_t n, bool searching, f3 o, f3 d) {
+    const float pn[6] = {mine.q1.z, mine.q1.w, mine.q2.x, mine.q2.y, mine.q2.z, mine.q2.w};
+    unsigned long long mask = 0;
+    for (uint32_t i = 0; i < n; i += 4) {
+        bool keep[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t f = min(i + k, n - 1);
+            const f3 nn = mk3(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(pn[0]), f)),
+                              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pn[1]), f)),
+                              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pn[2]), f)));
+            const f3 a = mk3(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(pn[3]), f)),
+                             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pn[4]), f)),
+                             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pn[5]), f)));
+            keep[k] = searching && plane_may_hit(nn, a, o, d);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            if (i + k < n && __any(keep[k])) mask |= 1ull << (i + k);
+    }
+    return mask;
 }
 
 // --------------------------------------------------------------------- first hit -----------
@@ -466,7 +550,7 @@ __device__ __forceinline__ bool test_candidates(unsigned long long mask, Face&& 
 // resolved by activate(), which must generate its direction (into `d`) and return the
 // bounding-box verdict (object.rs:59-61).  `found` receives the face index relative to
 // `begin`, or stays -1.  kLds: every thread of the workgroup must call it.
-template <bool kCull, bool kLds, typename Scene, typename Activate>
+template <bool kCull, bool kLds, bool kPlane = false, typename Scene, typename Activate>
 __device__ void first_hit(const FrameParams& p, const Scene& sc, uint32_t begin, uint32_t count, int& st,
                           const f3& o, const f3& d, const Bundle& bd, TriHot* s_hot, TriCull* s_cull,
                           Activate&& activate, int& found, float& hu, float& hv, float& ht) {
@@ -488,6 +572,10 @@ __device__ void first_hit(const FrameParams& p, const Scene& sc, uint32_t begin,
                 bool keep = false;
                 if (j < count) keep = !cull_rejects(sc.cull(begin + j), bd.xlo, bd.xhi, bd.ylo, bd.yhi);
                 mask = __ballot(keep);
+                ERAY_TRACE(10);
+            } else if (kPlane) {  // rays already resolved (shadow rays): faces some lane may hit
+                const uint32_t n = min(64u, count - base);
+                mask = plane_mask(sc.hot_lane(begin + base + min(lane, n - 1)), n, st == kSearching, o, d);
             } else {
                 const uint32_t n = min(64u, count - base);
                 mask = n == 64 ? ~0ull : ((1ull << n) - 1ull);
@@ -671,13 +759,15 @@ __device__ __forceinline__ uint32_t mod_size(uint32_t i, uint32_t n) {
     return (n & (n - 1)) == 0 ? (i & (n - 1)) : i % n;
 }
 
-__device__ __forceinline__ bool tex_value(const TexView& tv, float x, float y, float& out) {
-    if (!tv.data) return false;
+// Image::mod_get's texel (image.rs:36-38) for uv (x, y) of a `comps`-float texture, or nullptr
+// when the material has no such output (Material::get's default then stands).
+__device__ __forceinline__ const float* texel(const TexView& tv, float x, float y, uint32_t comps) {
+    if (!tv.data) return nullptr;
     const uint32_t ix = mod_size(sat_u32(x * (float)tv.w), tv.w);
     const uint32_t iy = mod_size(sat_u32(y * (float)tv.h), tv.h);
-    out = as_global(tv.data)[(size_t)iy * tv.w + ix];
-    return true;
+    return tv.data + comps * ((size_t)iy * tv.w + ix);
 }
+__device__ const float g_texel_dummy[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 
 // Camera::pixel_to_ray(x / W, y / H).dir (engine.rs:100-109, camera.rs:57-76, Ray::new)
 __device__ __forceinline__ f3 camera_dir(const FrameParams& p, uint32_t px, uint32_t y) {
@@ -800,7 +890,7 @@ __device__ __forceinline__ bool rect_meets(const ObjGeom& ob, const FrameParams&
 template <bool kCull, bool kLdsTiles, bool kSpecPow, typename Scene>
 __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc, uint32_t wx0, uint32_t py0,
                                            bool active, TriHot* s_hot, TriCull* s_cull, char* s_bins, float4* s_rgb,
-                                           uint32_t* s_ppm, bool aligned) {
+                                           uint32_t* s_ppm, bool aligned, const f3* given_d = nullptr) {
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const f3 C = mk3(p.cx, p.cy, p.cz);
     const uint32_t px = wx0 + (lane % kSubW), ly = lane / kSubW;
@@ -810,8 +900,8 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
     const Bundle bd = make_bundle(p, wx0, min(wx0 + kSubW - 1, p.cam_w - 1), py0, min(py0 + kBlkH - 1, p.rows - 1));
 
     // ---- cast_ray (engine.rs:112-216): closest object among first hits -----------
-    f3 d = mk3(0.0f, 0.0f, 0.0f);
-    bool ray_ready = false;
+    f3 d = given_d ? *given_d : mk3(0.0f, 0.0f, 0.0f);  // the camera ray, when the caller has it
+    bool ray_ready = given_d != nullptr;
     bool have = false;
     float closest = 0.0f, bu = 0.0f, bv = 0.0f, bt = 0.0f;
     uint32_t best_obj = 0;
@@ -819,6 +909,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
     for (uint32_t oi = 0; oi < p.nobj; ++oi) {
         const ObjGeom ob = sc.geom(oi);  // uniform
         const bool direct = !kLdsTiles || ob.tri_count <= kDirectMax;
+        ERAY_TRACE(9);
         // outside the object's pixel rectangle no primary ray can hit it (only where skipping
         // keeps the workgroup's barriers uniform)
         if (kCull && direct && !rect_meets(ob, p, wx0, py0)) continue;
@@ -828,8 +919,11 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
                 asm volatile("" : "+v"(pxo), "+v"(yo));
                 d = camera_dir(p, pxo, yo);
                 ray_ready = true;
+                ERAY_TRACE(11);
             }
-            return bbox_hit(ob, C, d);
+            const bool bb = bbox_hit(ob, C, d);
+            ERAY_TRACE(14);
+            return bb;
         };
         int st = valid ? kUndecided : kDone, f = -1;
         float u, v, t;
@@ -860,9 +954,12 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
 
     ERAY_TRACE(2);
     // ---- hit data and Material::get (material.rs:56-94) --------------------------
+    // The object loop only finds each lane's texel addresses; the loads are issued once after
+    // it and first used by the shading, so their latency overlaps the shadow rays.
     f3 P = mk3(0.0f, 0.0f, 0.0f), N = mk3(0.0f, 0.0f, 0.0f);
     rgb color{0.0f, 0.0f, 0.0f};
     float kd = 0.5f, ks = 0.5f, sp = 1.0f;
+    const float *tc = nullptr, *tkd = nullptr, *tks = nullptr, *tsp = nullptr;  // texels, if any
     for (uint32_t oi = 0; oi < p.nobj; ++oi) {  // per-lane object, read from uniform copies
         if (!__any(have && best_obj == oi)) continue;
         const ObjGeom ob = sc.geom(oi);
@@ -885,17 +982,30 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
                         wv * omf + mat.ex_b * mat.ex_factor};
             kd = wv;
         }
-        if (mat.color.data) {
-            const TexView& tv = mat.color;
-            const uint32_t ix = mod_size(sat_u32(uv0 * (float)tv.w), tv.w);
-            const uint32_t iy = mod_size(sat_u32(uv1 * (float)tv.h), tv.h);
-            const auto* c = as_global(tv.data) + 3 * ((size_t)iy * tv.w + ix);
-            color = rgb{c[0], c[1], c[2]};
-        }
-        tex_value(mat.diffuse, uv0, uv1, kd);
-        tex_value(mat.specular, uv0, uv1, ks);
-        if (kSpecPow) tex_value(mat.specular_power, uv0, uv1, sp);
+        tc = texel(mat.color, uv0, uv1, 3);
+        tkd = texel(mat.diffuse, uv0, uv1, 1);
+        tks = texel(mat.specular, uv0, uv1, 1);
+        if (kSpecPow) tsp = texel(mat.specular_power, uv0, uv1, 1);
     }
+    // every lane loads (a lane without the texture reads a dummy word); Material::get's values
+    // are selected where the shading first needs them
+    const auto* tcg = as_global(tc ? tc : g_texel_dummy);
+    const float vc0 = tcg[0], vc1 = tcg[1], vc2 = tcg[2];
+    const float vkd = *as_global(tkd ? tkd : g_texel_dummy);
+    const float vks = *as_global(tks ? tks : g_texel_dummy);
+    const float vsp = kSpecPow ? *as_global(tsp ? tsp : g_texel_dummy) : 1.0f;
+    bool resolved = false;
+    auto material = [&]() {
+        if (resolved) return;
+        resolved = true;
+        if (tc) color = rgb{vc0, vc1, vc2};
+        if (tkd) kd = vkd;
+        if (tks) ks = vks;
+        if (kSpecPow && tsp) sp = vsp;
+    };
+#ifdef ERAY_AB_EARLY_MATERIAL
+    material();
+#endif
 
     ERAY_TRACE(3);
     bool any = false;  // the lighting list as a running left fold (color.rs:82-87)
@@ -908,39 +1018,58 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
             any = true;
         }
     };
-    for (uint32_t li = 0; li < p.nlights; ++li) {
-        const LightDesc L = sc.light(li);
-        if (L.variant == 1) continue;  // point lights first (engine.rs:274-279)
-        const f3 Lp = mk3(L.pos[0], L.pos[1], L.pos[2]);
-        // reaches_light(Ray::new(P + N * 0.1, Lp - P)) (engine.rs:280-286, 218-228)
-        f3 S = mk3(0.0f, 0.0f, 0.0f);
-        f3 sd = mk3(0.0f, 0.0f, 1.0f);
-        float dist = 0.0f;
-        if (have) {
-            S = add(P, mul(N, 0.1f));
-            sd = normalize(sub(Lp, P));
-            dist = len(sub(Lp, S));
-        }
-        bool reached = true, decided = false;
-        for (uint32_t oj = 0; oj < p.nobj; ++oj) {
-            const ObjGeom ob = sc.geom(oj);
-            int st = (have && !decided && bbox_hit(ob, S, sd)) ? kSearching : kDone;
-            int f = -1;
-            float u, v, t;
-            auto never = []() { return false; };
-            if (!kLdsTiles || ob.tri_count <= kDirectMax)
-                first_hit<false, false>(p, sc, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot, s_cull, never, f, u,
-                                        v, t);
-            else
-                first_hit<false, kLdsTiles>(p, sc, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot, s_cull, never,
-                                            f, u, v, t);
-            if (f >= 0) {
-                const f3 hp = add(S, mul(sd, t));
-                reached = len(sub(hp, S)) > dist;
-                decided = true;
+    // Point lights first (engine.rs:274-279), 32 at a time: every light's shadow ray, then the
+    // shading of the lights that reach the hit, in list order.  The texture loads above are
+    // still in flight during the first shadow scan; the shading is their first use.
+    for (uint32_t li0 = 0; li0 < p.nlights; li0 += 32) {
+        const uint32_t li1 = min(p.nlights, li0 + 32);
+        uint32_t lit = 0;  // bit li - li0: point light li reaches the lane's hit
+        for (uint32_t li = li0; li < li1; ++li) {
+            const LightDesc L = sc.light(li);
+            if (L.variant == 1 || (!kLdsTiles && !__any(have))) continue;  // (LDS tiles: barriers)
+            const f3 Lp = mk3(L.pos[0], L.pos[1], L.pos[2]);
+            // reaches_light(Ray::new(P + N * 0.1, Lp - P)) (engine.rs:280-286, 218-228)
+            f3 S = mk3(0.0f, 0.0f, 0.0f);
+            f3 sd = mk3(0.0f, 0.0f, 1.0f);
+            float dist = 0.0f;
+            if (have) {
+                S = add(P, mul(N, 0.1f));
+                sd = normalize(sub(Lp, P));
+                dist = len(sub(Lp, S));
             }
+            bool reached = true, decided = false;
+            for (uint32_t oj = 0; oj < p.nobj; ++oj) {
+                const ObjGeom ob = sc.geom(oj);
+                int st = (have && !decided && bbox_hit(ob, S, sd)) ? kSearching : kDone;
+                int f = -1;
+                float u, v, t;
+                auto never = []() { return false; };
+#ifdef ERAY_AB_PLANE_OFF
+                constexpr bool kPlaneTest = false;
+#else
+                constexpr bool kPlaneTest = true;
+#endif
+                if (!kLdsTiles || ob.tri_count <= kDirectMax)
+                    first_hit<false, false, kPlaneTest>(p, sc, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot, s_cull,
+                                                  never, f, u, v, t);
+                else
+                    first_hit<false, kLdsTiles>(p, sc, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot, s_cull,
+                                                never, f, u, v, t);
+                ERAY_TRACE(15);
+                if (f >= 0) {
+                    const f3 hp = add(S, mul(sd, t));
+                    reached = len(sub(hp, S)) > dist;
+                    decided = true;
+                }
+            }
+            if (have && reached) lit |= 1u << (li - li0);
         }
-        if (have && reached) {  // engine.rs:287-322
+        if (!__any(lit != 0)) continue;
+        material();
+        for (uint32_t li = li0; li < li1; ++li) {
+            const LightDesc L = sc.light(li);
+            if (L.variant == 1 || !((lit >> (li - li0)) & 1u)) continue;  // engine.rs:287-322
+            const f3 Lp = mk3(L.pos[0], L.pos[1], L.pos[2]);
             const f3 LmP = sub(Lp, P);
             float prod = rust_clamp(dot0(N, LmP), 0.0f, 1.0f);
             if (prod != prod) prod = 0.0f;
@@ -960,6 +1089,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
         }
     }
     if (have) {
+        material();
         for (uint32_t li = 0; li < p.nlights; ++li) {  // ambient lights (engine.rs:341-352)
             const LightDesc L = sc.light(li);
             if (L.variant != 1) continue;
@@ -1038,7 +1168,11 @@ __device__ __forceinline__ bool inside(const SubRect& r, int32_t sx, int32_t sy)
 }
 
 template <bool kCull, bool kLdsTiles, bool kSpecPow, bool kLdsScene>
-__global__ void __launch_bounds__(kWG) frame_kernel(FrameParams p) {
+__global__ void __launch_bounds__(kWG)
+    frame_kernel(const ObjectDesc* h_objects, const LightDesc* h_lights, const TriCull* h_cull, const TriHot* h_tris,
+                 const TriShade* h_shade, uint32_t h_counts, uint32_t h_total_tris, uint32_t h_total_sub,
+                 uint32_t h_grid, FrameParams p) {
+    const FrameHot hot{h_objects, h_lights, h_cull, h_tris, h_shade, h_counts, h_total_tris, h_total_sub, h_grid};
     // large objects: LDS tiles (shadow rays, brute force) and, aliased, the per-wave binned
     // primary search (first_hit ends its tile loop on a barrier, so the two never overlap)
     constexpr size_t kTileBytes = kTriTile * (sizeof(TriHot) + ((kCull && kLdsTiles) ? sizeof(TriCull) : 0));
@@ -1052,38 +1186,58 @@ __global__ void __launch_bounds__(kWG) frame_kernel(FrameParams p) {
     extern __shared__ __attribute__((aligned(16))) char dyn[];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t nwaves = kWG / 64;
-    const bool aligned = (p.img_w % 16) == 0 &&
-                         ((reinterpret_cast<uintptr_t>(p.out_rgb) | reinterpret_cast<uintptr_t>(p.out_ppm) |
-                           reinterpret_cast<uintptr_t>(p.out_face)) & 15) == 0;
-    const uint32_t total = p.total_sub;  // detail sub-blocks
+    const bool aligned = p.aligned != 0;  // (a kernel-argument read where it is used)
+    const uint32_t total = hot.total_sub;  // detail sub-blocks
+    const uint32_t grid = hot.grid;        // == gridDim.x, without the implicit-argument load
     // workgroups [0, nd) render the detail sub-blocks, the others write the background; when
     // every workgroup has detail work, all of them fill afterwards
-    const uint32_t nd = min(gridDim.x, (total + nwaves - 1) / nwaves);
+    const uint32_t nd = min(grid, (total + nwaves - 1) / nwaves);
+    ERAY_TRACE_CLEAR();
     ERAY_TRACE(0);
 
     // ---- detail sub-blocks -------------------------------------------------------------------
     if (blockIdx.x < nd) {
-        auto detail = [&](const auto& sc) {
-            for (uint32_t c = blockIdx.x * nwaves; c < total; c += gridDim.x * nwaves) {  // workgroup-uniform
-                uint32_t j = c + wave;
-                bool active = j < total;
-                int32_t sx = 0, sy = 0;
-                if (active) {
-                    // the rectangles are disjoint (host): find j's by area
-                    for (uint32_t k = 0; k < p.nrect; ++k) {
-                        const SubRect r = frame_rect(p, k);
-                        const uint32_t w = (uint32_t)(r.sx1 - r.sx0 + 1);
-                        const uint32_t a = w * (uint32_t)(r.sy1 - r.sy0 + 1);
-                        if (j < a) {
-                            sx = r.sx0 + (int32_t)(j % w);
-                            sy = r.sy0 + (int32_t)(j / w);
-                            break;
-                        }
-                        j -= a;
-                    }
+        // detail sub-block j (enumeration order) -> sub-block coordinates
+        auto locate = [&](uint32_t j, int32_t& sx, int32_t& sy) {
+            for (uint32_t k = 0; k < p.nrect; ++k) {  // the rectangles are disjoint (host): by area
+                const SubRect r = frame_rect(p, k);
+                const uint32_t w = (uint32_t)(r.sx1 - r.sx0 + 1);
+                const uint32_t a = w * (uint32_t)(r.sy1 - r.sy0 + 1);
+                if (j < a) {
+                    sx = r.sx0 + (int32_t)(j % w);
+                    sy = r.sy0 + (int32_t)(j / w);
+                    return;
                 }
+                j -= a;
+            }
+        };
+        // the wave's first sub-block and its camera rays, before the scene is in: the kernel
+        // arguments' scalar loads and the ray arithmetic overlap the preload's round trip
+        const uint32_t c0 = blockIdx.x * nwaves;
+        int32_t sx0 = 0, sy0 = 0;
+        f3 d0;
+#ifdef ERAY_AB_LAZY_RAY
+        constexpr bool kGivenRay = false;
+        auto first_rays = [&]() {
+            if (c0 + wave < total) locate(c0 + wave, sx0, sy0);
+        };
+#else
+        constexpr bool kGivenRay = true;
+        auto first_rays = [&]() {
+            if (c0 + wave < total) locate(c0 + wave, sx0, sy0);
+            d0 = camera_dir(p, (uint32_t)sx0 * kSubW + lane % kSubW, p.row0 + (uint32_t)sy0 * kBlkH + lane / kSubW);
+            asm volatile("" : "+v"(d0.x), "+v"(d0.y), "+v"(d0.z));  // here, not after the barrier
+        };
+#endif
+        auto detail = [&](const auto& sc) {
+            for (uint32_t c = c0; c < total; c += grid * nwaves) {  // workgroup-uniform
+                const uint32_t j = c + wave;
+                const bool active = j < total;
+                int32_t sx = sx0, sy = sy0;
+                if (c != c0 && active) locate(j, sx, sy);
                 render_sub<kCull, kLdsTiles, kSpecPow>(p, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH, active,
-                                                       s_hot, s_cull, s_bins, s_rgb, s_ppm, aligned);
+                                                       s_hot, s_cull, s_bins, s_rgb, s_ppm, aligned,
+                                                       (kGivenRay && c == c0) ? &d0 : nullptr);
 #ifdef ERAY_PHASE_TRACE_REPEAT  // diagnostics: the same sub-block again, instruction cache warm
                 ERAY_TRACE(6);
                 render_sub<kCull, kLdsTiles, kSpecPow>(p, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH, active,
@@ -1092,22 +1246,26 @@ __global__ void __launch_bounds__(kWG) frame_kernel(FrameParams p) {
             }
         };
         if constexpr (kLdsScene) {
-            const SceneLds sc = preload_scene(p, dyn);
+            const SceneLds sc = preload_scene(hot, dyn, first_rays);
             __syncthreads();
             ERAY_TRACE(1);
             detail(sc);
         } else {
             const SceneGlobal sc{p};
+            first_rays();
             ERAY_TRACE(1);
             detail(sc);
         }
         ERAY_TRACE(7);
-        if (nd < gridDim.x) return;
+        if (nd < grid) {
+            ERAY_TRACE_FLUSH();
+            return;
+        }
     }
 
     // ---- background of the non-detail sub-blocks ---------------------------------------------
-    const uint32_t nf = nd < gridDim.x ? gridDim.x - nd : gridDim.x;  // filling workgroups
-    const uint32_t f = nd < gridDim.x ? blockIdx.x - nd : blockIdx.x;
+    const uint32_t nf = nd < grid ? grid - nd : grid;  // filling workgroups
+    const uint32_t f = nd < grid ? blockIdx.x - nd : blockIdx.x;
     const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
     for (uint32_t blk = wave * nf + f; blk < nblk; blk += nf * nwaves) {
         const uint32_t bx = blk % p.tiles_x, by = blk / p.tiles_x;
@@ -1129,6 +1287,7 @@ __global__ void __launch_bounds__(kWG) frame_kernel(FrameParams p) {
         }
     }
     ERAY_TRACE(8);
+    ERAY_TRACE_FLUSH();
 }
 
 // Image<Color>::save_as_ppm body: byte row k = image row h-1-k.
@@ -1200,7 +1359,8 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
     }();
     const int wg_cu = cap > 0 && cap < per_cu ? cap : per_cu;
     const uint32_t grid = min(want, (uint32_t)(wg_cu * cus));
-    frame_kernel<C, L, S, K><<<grid, kWG, dyn, s>>>(p);
+    frame_kernel<C, L, S, K><<<grid, kWG, dyn, s>>>(p.objects, p.lights, p.cull, p.tris, p.shade,
+                                                    p.nobj | (p.nlights << 16), p.total_tris, p.total_sub, grid, p);
     return hipGetLastError();
 }
 

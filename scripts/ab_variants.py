@@ -1,0 +1,62 @@
+"""A/B timing of frame-kernel design choices (diagnostics, not part of the product).
+
+`python scripts/ab_variants.py build` compiles lib/liberay_hip_<name>.so for each variant below
+(here, no GPU); `python scripts/ab_variants.py run` times the C2 frame (and a 4-row frame) with
+each library in a child process on the GPU box.
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+VARIANTS = {
+    "base": (),
+    "lazyray": ("ERAY_AB_LAZY_RAY",),
+    "earlymat": ("ERAY_AB_EARLY_MATERIAL",),
+    "lazy_early": ("ERAY_AB_LAZY_RAY", "ERAY_AB_EARLY_MATERIAL"),
+    "noplane": ("ERAY_AB_PLANE_OFF",),
+}
+
+CHILD = r"""
+import os, sys, time
+sys.path.insert(0, os.environ["ROOT"])
+import numpy as np, torch
+from eray_amd import capi
+from eray_amd.frame import MainScene
+from eray_amd.objfile import load_obj_file
+W, H = 1920, 1080
+mesh = load_obj_file(os.path.join(os.environ["ROOT"], "objects", "cube.obj"))
+ctx = capi.Context(0)
+rgb = ctx.empty((H, W, 3), np.float32); ppm = ctx.empty((H, W, 3), np.uint8)
+sc = MainScene(ctx, *mesh, W, H)
+out = []
+for row0, rows in ((0, H), (538, 4)):
+    kw = dict(row0=row0, rows=rows, out_rgb=rgb.ptr, out_ppm=ppm.ptr)
+    ctx.render_frames(64, W, H, prepare_only=True, **kw)
+    ctx.render_frames(64, W, H, **kw); ctx.synchronize()
+    best = min(ctx.render_frames(640, W, H, timed=True, **kw) for _ in range(5))
+    out.append(f"{rows:5d} rows {best * 1e3:7.2f} us")
+print(os.environ["ERAY_LIB"].split("_hip")[-1], " | ".join(out), flush=True)
+"""
+
+
+def main():
+    mode = sys.argv[1] if len(sys.argv) > 1 else "run"
+    names = sys.argv[2:] or list(VARIANTS)
+    if mode == "build":
+        from eray_amd.build import build
+        for n in names:
+            print(build(variant=n, defines=VARIANTS[n]), flush=True)
+        return
+    env = dict(os.environ, ROOT=ROOT)
+    for n in names:
+        env["ERAY_LIB"] = os.path.join(ROOT, "eray_amd", "lib", f"liberay_hip_{n}.so")
+        r = subprocess.run([sys.executable, "-c", CHILD], env=env, timeout=300)
+        if r.returncode != 0:
+            sys.exit(r.returncode)
+
+
+if __name__ == "__main__":
+    main()

@@ -3,7 +3,7 @@
 Renders the bench frame (cube, main.rs scene, 1920x1080) and prints, for workgroups
 0, 16, ..., 1008, each wave's phase timestamps (s_memrealtime, 10 ns ticks) relative to the earliest
 kernel-entry stamp: 0 entry, 1 caches ready, 2 primary hits, 3 material, 4 lighting,
-5 sub-block stored, 7 detail done, 8 kernel end.
+5 sub-block stored, 7 detail done, 8 kernel end; 14 camera ray and bounding box, 15 shadow scan.
 """
 import ctypes as C
 import os
@@ -45,14 +45,24 @@ if sel.any():
     ghz = ((clk[:, :, 7] - clk[:, :, 1])[sel] / ((t[:, :, 7] - t[:, :, 1])[sel] * 10.0)).mean()
     print(f"shader clock (detail waves) ~ {ghz:.2f} GHz")
 t0 = t[:, :, 0][t[:, :, 0] > 0].min()
-names = {0: "entry", 1: "caches", 2: "primary", 3: "material", 4: "light", 5: "stored", 6: "repeat", 7: "detail", 8: "end"}
+names = {0: "entry", 1: "caches", 9: "geom", 10: "cull", 11: "ray", 14: "bbox", 2: "primary", 3: "material", 15: "shadow", 4: "light", 5: "stored",
+         6: "repeat", 7: "detail", 8: "end"}
 print(f"rows {row0}..{row0 + rows}; ticks of 10 ns from the first entry")
-print("  wg.w " + " ".join(f"{names[k]:>8s}" for k in sorted(names)))
+order = [0, 1, 6, 9, 10, 11, 14, 2, 3, 15, 4, 5, 7]
+print("  wg.w " + " ".join(f"{names[k]:>8s}" for k in order))
 for g in range(64):
     for w in range(4):
         row = t[g, w]
         if row[0] == 0:
             continue
-        print(f"{16 * g:4d}.{w} " + " ".join(f"{(row[k] - t0) if row[k] else -1:8d}" for k in sorted(names))
+        print(f"{16 * g:4d}.{w} " + " ".join(f"{(row[k] - t0) if row[k] else -1:8d}" for k in order)
               + f"   heavy bin: list {row[9]:6d} pairs {row[10]:6d} chunks {row[11]:4d} "
               f"scan {(row[13] - row[12]) if row[12] else -1:6d}")
+print("shader cycles from each detail wave's entry (s_memtime)")
+print("  wg.w " + " ".join(f"{names[k]:>8s}" for k in order))
+for g in range(64):
+    for w in range(4):
+        row, ck = t[g, w], clk[g, w]
+        if row[0] == 0 or row[1] == 0 or row[7] == 0:
+            continue
+        print(f"{16 * g:4d}.{w} " + " ".join(f"{(ck[k] - ck[0]) if ck[k] else -1:8d}" for k in order))
