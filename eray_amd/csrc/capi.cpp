@@ -70,6 +70,7 @@ struct eray_ctx {
     std::vector<float> h_raw;
     uint32_t total_tris = 0;
     bool spec_pow = false;     // some material has a specular-power output
+    bool example_mat = false;  // some material is main.rs's graph evaluated per hit
 };
 
 namespace {
@@ -174,6 +175,7 @@ int sync_scene(eray_ctx* ctx, bool need_cull) {
         ctx->h_objs.clear();
         uint32_t begin = 0;
         ctx->spec_pow = false;
+        ctx->example_mat = false;
         for (auto& o : ctx->objects) {
             ObjectDesc d{};
             d.g.tri_begin = begin;
@@ -201,6 +203,7 @@ int sync_scene(eray_ctx* ctx, bool need_cull) {
             }
             ctx->h_objs.push_back(d);
             ctx->spec_pow |= o.mat.specular_power.data != nullptr;
+            ctx->example_mat |= d.mat.example != 0;
             begin += o.T;
         }
         ctx->h_lights.clear();
@@ -611,6 +614,9 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     for (auto& o : ctx->objects) p.max_object_tris = o.T > p.max_object_tris ? o.T : p.max_object_tris;
     p.total_tris = ctx->total_tris;
     p.lds_scene = (ctx->total_tris <= kCacheTris && p.nobj <= kCacheObjects && p.nlights <= kCacheLights) ? 1u : 0u;
+#ifdef ERAY_AB_NO_LDS_SCENE
+    p.lds_scene = 0;
+#endif
     // detail rectangles in sub-block units (16 px x 4 rank-local rows); brute force: the frame
     const int32_t rows_i = (int32_t)rp->rows, w_i = (int32_t)W;
     p.nrect = 0;
@@ -662,6 +668,7 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
         p.total_sub += (uint32_t)(r[1] - r[0] + 1) * (uint32_t)(r[3] - r[2] + 1);
     }
     p.spec_pow = ctx->spec_pow ? 1u : 0u;
+    p.example_mat = ctx->example_mat ? 1u : 0u;
     p.tiles_x = (W + 63) / 64;
     p.bins_x = (W + kBinW - 1) / kBinW;
     p.bin_phase = rp->row0 % kBinH;

@@ -110,6 +110,7 @@ struct FrameParams {
     uint32_t total_sub;        // inclusive) and the number of sub-blocks they cover, counting
     int32_t rects[kMaxRects][4];  // overlaps once: x0, x1, y0, y1
     uint32_t spec_pow;         // some material has a specular-power output (powf != identity)
+    uint32_t example_mat;      // some material evaluates main.rs's graph per hit (example)
     uint32_t tiles_x;    // 64 x 4 pixel blocks per row
     uint32_t bins_x;     // screen bins per row
     uint32_t bin_phase;  // bins start at camera rows bin_phase + k * kBinH (row0 % kBinH)

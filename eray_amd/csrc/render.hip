@@ -108,6 +108,17 @@ __shared__ uint64_t s_trace[4][kTraceSlots][2];
             }                                                             \
         }                                                                 \
     } while (0)
+#elif defined(ERAY_ISA_MARKS)  // static instruction profile (scripts/isa_profile.py): asm comments
+#define ERAY_TRACE(slot) asm volatile("; ERAY_MARK " #slot)
+#define ERAY_TRACE_VAL(slot, v) \
+    do {                        \
+    } while (0)
+#define ERAY_TRACE_CLEAR() \
+    do {                   \
+    } while (0)
+#define ERAY_TRACE_FLUSH() \
+    do {                   \
+    } while (0)
 #else
 #define ERAY_TRACE_CLEAR() \
     do {                   \
@@ -409,9 +420,17 @@ struct SceneLds {
     const TriCull* culls;
     const TriHot* hots;
     const TriShade* shades;
+    const ObjectDesc* g_objs;  // the device arrays (scalar loads of uniform records)
+    const LightDesc* g_lights;
+#ifdef ERAY_AB_SLOAD_UNIFORM
+    __device__ ObjGeom geom(uint32_t i) const { return load_const(&g_objs[i].g, 0); }
+    __device__ MaterialDesc mat(uint32_t i) const { return load_const(&g_objs[i].mat, 0); }
+    __device__ LightDesc light(uint32_t i) const { return load_const(g_lights, i); }
+#else
     __device__ ObjGeom geom(uint32_t i) const { return lds_uniform(&objs[i].g); }
     __device__ MaterialDesc mat(uint32_t i) const { return lds_uniform(&objs[i].mat); }
     __device__ LightDesc light(uint32_t i) const { return lds_uniform(lights + i); }
+#endif
     __device__ TriCull cull(uint32_t g) const { return culls[g]; }
     __device__ TriHot hot(uint32_t g) const { return hots[g]; }  // broadcast read (VGPRs)
     __device__ TriHot hot_lane(uint32_t g) const { return hots[g]; }
@@ -448,7 +467,10 @@ __device__ SceneLds preload_scene(const FrameHot& p, char* dyn, Meanwhile&& mean
                      : src_shade + i4;
             v[k] = *src;
         }
-        if (base == 0) meanwhile();
+        if (base == 0) {
+            ERAY_TRACE(13);
+            meanwhile();
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t i = base + k * kWG + threadIdx.x;
@@ -457,7 +479,7 @@ __device__ SceneLds preload_scene(const FrameHot& p, char* dyn, Meanwhile&& mean
     }
     return SceneLds{reinterpret_cast<const ObjectDesc*>(dyn + L.objs), reinterpret_cast<const LightDesc*>(dyn + L.lights),
                     reinterpret_cast<const TriCull*>(dyn + L.cull), reinterpret_cast<const TriHot*>(dyn + L.hot),
-                    reinterpret_cast<const TriShade*>(dyn + L.shade)};
+                    reinterpret_cast<const TriShade*>(dyn + L.shade), p.objects, p.lights};
 }
 
 // Lanes whose Triangle::intersects could pass: the det and t conditions of exact_test, from the
@@ -496,6 +518,85 @@ __device__ __forceinline__ unsigned long long plane_mask(const TriHot& mine, uin
     return mask;
 }
 
+// Wave-wide min and max of six floats at once (lanes that must not count pass +inf / -inf):
+// the floats as order-preserving integer keys, DPP row shifts and row broadcasts (an invalid
+// source lane reads the identity), the six reductions interleaved; results in SGPRs.
+__device__ __forceinline__ int32_t float_key(float x) {
+    const int32_t b = __float_as_int(x);
+    return b ^ ((b >> 31) & 0x7fffffff);  // signed order of keys = numeric order of floats
+}
+__device__ __forceinline__ float key_float(int32_t k) { return __int_as_float(k ^ ((k >> 31) & 0x7fffffff)); }
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ void dpp_minmax_step(int32_t (&v)[6]) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const int32_t id = i < 3 ? 0x7fffffff : (int32_t)0x80000000;  // identity: fuses into v_min/max_dpp
+        const int32_t o = __builtin_amdgcn_update_dpp(id, v[i], kCtrl, kRowMask, 0xf, false);
+        v[i] = i < 3 ? min(v[i], o) : max(v[i], o);
+    }
+}
+// v[0..2]: values to minimise, v[3..5]: values to maximise
+__device__ __forceinline__ void wave_minmax6(const float (&in)[6], float (&out)[6]) {
+    int32_t v[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) v[i] = float_key(in[i]);
+    dpp_minmax_step<0x111, 0xf>(v);  // row_shr:1
+    dpp_minmax_step<0x112, 0xf>(v);  // row_shr:2
+    dpp_minmax_step<0x114, 0xf>(v);  // row_shr:4
+    dpp_minmax_step<0x118, 0xf>(v);  // row_shr:8: lane 15 of each row holds the row's
+    dpp_minmax_step<0x142, 0xa>(v);  // row_bcast:15
+    dpp_minmax_step<0x143, 0xc>(v);  // row_bcast:31: lane 63 holds the wave's
+#pragma unroll
+    for (int i = 0; i < 6; ++i) out[i] = key_float(__builtin_amdgcn_readlane(v[i], 63));
+}
+
+// The box of the wave's hit points P (lanes with a hit), for the shadow rays' face bounds.
+struct HitBox {
+    float lo[3], hi[3];
+    bool ok;  // some lane has a hit and every hit lane's P and N are finite
+};
+__device__ __forceinline__ HitBox hit_box(bool have, f3 P, f3 N) {
+    const float inf = __builtin_inff();
+    const bool finite = __builtin_isfinite(P.x) && __builtin_isfinite(P.y) && __builtin_isfinite(P.z) &&
+                        __builtin_isfinite(N.x) && __builtin_isfinite(N.y) && __builtin_isfinite(N.z);
+    const bool use = have && finite;
+    const float in[6] = {use ? P.x : inf, use ? P.y : inf, use ? P.z : inf,
+                         use ? P.x : -inf, use ? P.y : -inf, use ? P.z : -inf};
+    float out[6];
+    wave_minmax6(in, out);
+    HitBox b;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        b.lo[k] = out[k];
+        b.hi[k] = out[3 + k];
+    }
+    b.ok = __any(have) && !__any(have && !finite);
+    return b;
+}
+
+// Can a shadow ray Ray::new(P + N * 0.1, Lp - P) of a hit point P in box `b` pass this face's
+// det and t conditions (primitives.rs:47-66)?  det >= 1e-6 needs dot(P - Lp, n) > 0 and t >= 0
+// needs dot(S - a, n) >= 0 for the origin S, which lies within 0.1 (|N| = 1) of the box; both
+// are linear, so their maxima over the box decide.  The tolerance (1e-4 of the terms'
+// magnitudes) dwarfs the f32 rounding of every quantity involved, so a face some lane's exact
+// test accepts is never dropped; non-finite bounds keep the face.
+__device__ __forceinline__ bool shadow_box_may_hit(const TriHot& r, f3 Lp, const HitBox& b) {
+    const float n[3] = {r.q1.z, r.q1.w, r.q2.x}, a[3] = {r.q2.y, r.q2.z, r.q2.w};
+    const float lp[3] = {Lp.x, Lp.y, Lp.z};
+    const float g = 0.1001f;
+    float m1 = 0.0f, m2 = 0.0f, mag = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const bool pos = n[k] >= 0.0f;
+        m1 += n[k] * ((pos ? b.hi[k] : b.lo[k]) - lp[k]);
+        m2 += n[k] * ((pos ? b.hi[k] + g : b.lo[k] - g) - a[k]);
+        mag += __builtin_fabsf(n[k]) *
+               (__builtin_fabsf(b.lo[k]) + __builtin_fabsf(b.hi[k]) + __builtin_fabsf(lp[k]) + __builtin_fabsf(a[k]) + 1.0f);
+    }
+    const float tol = 1e-4f * mag + 1e-30f;
+    return ((m1 >= -tol) & (m2 >= -tol)) | !(mag < 1e30f);
+}
+
 // --------------------------------------------------------------------- first hit -----------
 // Per-ray search state: kUndecided (ray and bounding-box test not evaluated yet), kSearching,
 // kDone (hit found, bbox rejected, or not a pixel of the image).
@@ -508,7 +609,37 @@ constexpr int kUndecided = 0, kSearching = 1, kDone = 2;
 // dependent chains, division included, overlap).
 constexpr int kBatch = 4;
 
-// Tests the candidates of `mask` in index order, kBatch at a time: bit i stands for face
+// Tests the next kB candidates of `mask` (kB <= its population) in index order.
+template <int kB, typename Face, typename Hot>
+__device__ __forceinline__ void test_step(unsigned long long& mask, Face&& face, Hot&& hot, int& st, const f3& o,
+                                          const f3& d, int& found, float& hu, float& hv, float& ht) {
+    uint32_t ids[kB];
+    bool has[kB];
+    TriHot h[kB];
+#pragma unroll
+    for (int k = 0; k < kB; ++k) {  // (fewer than kB left only with ERAY_AB_BATCH_FIXED)
+        has[k] = mask != 0;
+        ids[k] = has[k] ? (uint32_t)(__ffsll(mask) - 1) : 0u;
+        mask &= mask - 1;
+        h[k] = hot(ids[k]);
+    }
+    bool hit[kB];
+    float u[kB], v[kB], t[kB];
+#pragma unroll
+    for (int k = 0; k < kB; ++k) hit[k] = has[k] && exact_test_flat(h[k], o, d, u[k], v[k], t[k]);
+#pragma unroll
+    for (int k = 0; k < kB; ++k) {
+        if (st == kSearching && hit[k]) {
+            found = (int)face(ids[k]);
+            hu = u[k];
+            hv = v[k];
+            ht = t[k];
+            st = kDone;
+        }
+    }
+}
+
+// Tests the candidates of `mask` in index order, up to kBatch at a time: bit i stands for face
 // face(i) (relative to the object) whose record is hot(i).  Returns false once no lane is
 // searching.
 template <typename Face, typename Hot>
@@ -516,30 +647,17 @@ __device__ __forceinline__ bool test_candidates(unsigned long long mask, Face&& 
                                                 const f3& o, const f3& d, int& found, float& hu, float& hv,
                                                 float& ht) {
     while (mask) {
-        uint32_t ids[kBatch];
-        bool has[kBatch];
-        TriHot h[kBatch];
-#pragma unroll
-        for (int k = 0; k < kBatch; ++k) {
-            has[k] = mask != 0;
-            ids[k] = has[k] ? (uint32_t)(__ffsll(mask) - 1) : 0u;
-            mask &= mask - 1;
-            h[k] = hot(ids[k]);
-        }
-        bool hit[kBatch];
-        float u[kBatch], v[kBatch], t[kBatch];
-#pragma unroll
-        for (int k = 0; k < kBatch; ++k) hit[k] = has[k] && exact_test_flat(h[k], o, d, u[k], v[k], t[k]);
-#pragma unroll
-        for (int k = 0; k < kBatch; ++k) {
-            if (st == kSearching && hit[k]) {
-                found = (int)face(ids[k]);
-                hu = u[k];
-                hv = v[k];
-                ht = t[k];
-                st = kDone;
-            }
-        }
+#ifdef ERAY_AB_BATCH_FIXED
+        const int n = kBatch;
+#else
+        const int n = __popcll(mask);
+#endif
+        if (n >= kBatch)
+            test_step<kBatch>(mask, face, hot, st, o, d, found, hu, hv, ht);
+        else if (n >= 2)
+            test_step<2>(mask, face, hot, st, o, d, found, hu, hv, ht);
+        else
+            test_step<1>(mask, face, hot, st, o, d, found, hu, hv, ht);
         if (!__any(st == kSearching)) return false;
     }
     return true;
@@ -887,10 +1005,15 @@ __device__ __forceinline__ bool rect_meets(const ObjGeom& ob, const FrameParams&
 
 // Engine::cast_ray for the 16 x 4 pixels at (wx0, py0) (rank-local rows), one pixel per lane;
 // `active` false: the wave only takes part in the workgroup's LDS-tile barriers.
-template <bool kCull, bool kLdsTiles, bool kSpecPow, typename Scene>
+// kMat: material features some object of the scene uses — kMatSpecPow (a specular-power output:
+// powf is not the identity), kMatExample (main.rs's graph evaluated per hit texel); a kernel
+// without them carries none of their code or registers.
+constexpr int kMatSpecPow = 1, kMatExample = 2;
+template <bool kCull, bool kLdsTiles, int kMat, typename Scene>
 __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc, uint32_t wx0, uint32_t py0,
                                            bool active, TriHot* s_hot, TriCull* s_cull, char* s_bins, float4* s_rgb,
                                            uint32_t* s_ppm, bool aligned, const f3* given_d = nullptr) {
+    constexpr bool kSpecPow = (kMat & kMatSpecPow) != 0, kExample = (kMat & kMatExample) != 0;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const f3 C = mk3(p.cx, p.cy, p.cz);
     const uint32_t px = wx0 + (lane % kSubW), ly = lane / kSubW;
@@ -973,7 +1096,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
         const float w = 1.0f - bu - bv;
         const float uv0 = ((sh.s2.y * w) + (sh.s2.w * bu)) + (sh.s3.y * bv);
         const float uv1 = ((sh.s2.z * w) + (sh.s3.x * bu)) + (sh.s3.z * bv);
-        if (mat.example) {  // main.rs's graph at the texel Material::get would read
+        if (kExample && mat.example) {  // main.rs's graph at the texel Material::get would read
             const uint32_t ix = mod_size(sat_u32(uv0 * (float)mat.ex_w), mat.ex_w);
             const uint32_t iy = mod_size(sat_u32(uv1 * (float)mat.ex_h), mat.ex_h);
             const float wv = __builtin_fabsf(libm::cosf_glibc(((float)ix * mat.ex_xf + (float)iy * mat.ex_yf) / 10.0f));
@@ -989,6 +1112,10 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
     }
     // every lane loads (a lane without the texture reads a dummy word); Material::get's values
     // are selected where the shading first needs them
+#ifdef ERAY_AB_X_NO_TEXTURE  // diagnostics only (wrong images): the texture fetch's cost
+    tc = tkd = tks = tsp = nullptr;
+#endif
+    const bool has_c = tc, has_kd = tkd, has_ks = tks, has_sp = kSpecPow && tsp;
     const auto* tcg = as_global(tc ? tc : g_texel_dummy);
     const float vc0 = tcg[0], vc1 = tcg[1], vc2 = tcg[2];
     const float vkd = *as_global(tkd ? tkd : g_texel_dummy);
@@ -998,10 +1125,10 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
     auto material = [&]() {
         if (resolved) return;
         resolved = true;
-        if (tc) color = rgb{vc0, vc1, vc2};
-        if (tkd) kd = vkd;
-        if (tks) ks = vks;
-        if (kSpecPow && tsp) sp = vsp;
+        if (has_c) color = rgb{vc0, vc1, vc2};
+        if (has_kd) kd = vkd;
+        if (has_ks) ks = vks;
+        if (has_sp) sp = vsp;
     };
 #ifdef ERAY_AB_EARLY_MATERIAL
     material();
@@ -1018,6 +1145,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
             any = true;
         }
     };
+    const HitBox hb = hit_box(have, P, N);  // (wave-uniform; shadow-ray face bounds)
     // Point lights first (engine.rs:274-279), 32 at a time: every light's shadow ray, then the
     // shading of the lights that reach the hit, in list order.  The texture loads above are
     // still in flight during the first shadow scan; the shading is their first use.
@@ -1032,29 +1160,55 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
             f3 S = mk3(0.0f, 0.0f, 0.0f);
             f3 sd = mk3(0.0f, 0.0f, 1.0f);
             float dist = 0.0f;
-            if (have) {
-                S = add(P, mul(N, 0.1f));
-                sd = normalize(sub(Lp, P));
-                dist = len(sub(Lp, S));
-            }
             bool reached = true, decided = false;
+            bool ray = false;  // S, sd, dist computed
+            auto shadow_ray = [&]() {
+                if (ray) return;
+                ray = true;
+                if (have) {
+                    S = add(P, mul(N, 0.1f));
+                    sd = normalize(sub(Lp, P));
+                    dist = len(sub(Lp, S));
+                }
+            };
+#ifdef ERAY_AB_X_NO_SHADOW  // diagnostics only (wrong images): the shadow scan's cost
+            if (p.nobj != 12345) decided = true;
+#endif
             for (uint32_t oj = 0; oj < p.nobj; ++oj) {
+#ifdef ERAY_AB_X_NO_SHADOW
+                if (p.nobj != 12345) break;
+#endif
                 const ObjGeom ob = sc.geom(oj);
-                int st = (have && !decided && bbox_hit(ob, S, sd)) ? kSearching : kDone;
                 int f = -1;
                 float u, v, t;
-                auto never = []() { return false; };
-#ifdef ERAY_AB_PLANE_OFF
-                constexpr bool kPlaneTest = false;
-#else
-                constexpr bool kPlaneTest = true;
-#endif
-                if (!kLdsTiles || ob.tri_count <= kDirectMax)
-                    first_hit<false, false, kPlaneTest>(p, sc, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot, s_cull,
-                                                  never, f, u, v, t);
-                else
+                if (!kLdsTiles || ob.tri_count <= kDirectMax) {
+                    // faces some hit point's shadow ray may pass (box bounds, lane-parallel),
+                    // then the exact tests in index order; the ray itself only when needed
+                    int st = kDone;
+                    bool opened = false;
+                    for (uint32_t base = 0; base < ob.tri_count; base += 64) {
+                        const uint32_t n = min(64u, ob.tri_count - base);
+                        bool keep = lane < n;
+                        if (keep && hb.ok) keep = shadow_box_may_hit(sc.hot_lane(ob.tri_begin + base + lane), Lp, hb);
+                        const unsigned long long mask = __ballot(keep);
+                        if (!mask) continue;
+                        if (!opened) {
+                            opened = true;
+                            shadow_ray();
+                            st = (have && !decided && bbox_hit(ob, S, sd)) ? kSearching : kDone;
+                        }
+                        if (!__any(st == kSearching)) break;
+                        auto face = [&](uint32_t i) { return base + i; };
+                        auto hot = [&](uint32_t i) { return sc.hot(ob.tri_begin + base + i); };
+                        if (!test_candidates(mask, face, hot, st, S, sd, f, u, v, t)) break;
+                    }
+                } else {
+                    shadow_ray();
+                    int st = (have && !decided && bbox_hit(ob, S, sd)) ? kSearching : kDone;
+                    auto never = []() { return false; };
                     first_hit<false, kLdsTiles>(p, sc, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot, s_cull,
                                                 never, f, u, v, t);
+                }
                 ERAY_TRACE(15);
                 if (f >= 0) {
                     const f3 hp = add(S, mul(sd, t));
@@ -1167,8 +1321,8 @@ __device__ __forceinline__ bool inside(const SubRect& r, int32_t sx, int32_t sy)
     return sx >= r.sx0 && sx <= r.sx1 && sy >= r.sy0 && sy <= r.sy1;
 }
 
-template <bool kCull, bool kLdsTiles, bool kSpecPow, bool kLdsScene>
-__global__ void __launch_bounds__(kWG)
+template <bool kCull, bool kLdsTiles, int kMat, bool kLdsScene>
+__global__ void __launch_bounds__(kWG, (kLdsTiles || (kMat & kMatSpecPow)) ? 1 : 3)  // 3 workgroups per CU where that fits
     frame_kernel(const ObjectDesc* h_objects, const LightDesc* h_lights, const TriCull* h_cull, const TriHot* h_tris,
                  const TriShade* h_shade, uint32_t h_counts, uint32_t h_total_tris, uint32_t h_total_sub,
                  uint32_t h_grid, FrameParams p) {
@@ -1197,6 +1351,9 @@ __global__ void __launch_bounds__(kWG)
 
     // ---- detail sub-blocks -------------------------------------------------------------------
     if (blockIdx.x < nd) {
+#ifdef ERAY_AB_X_NO_DETAIL  // diagnostics only (wrong images): the fill alone, same grid
+        if (nd < grid) return;
+#endif
         // detail sub-block j (enumeration order) -> sub-block coordinates
         auto locate = [&](uint32_t j, int32_t& sx, int32_t& sy) {
             for (uint32_t k = 0; k < p.nrect; ++k) {  // the rectangles are disjoint (host): by area
@@ -1235,18 +1392,19 @@ __global__ void __launch_bounds__(kWG)
                 const bool active = j < total;
                 int32_t sx = sx0, sy = sy0;
                 if (c != c0 && active) locate(j, sx, sy);
-                render_sub<kCull, kLdsTiles, kSpecPow>(p, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH, active,
+                render_sub<kCull, kLdsTiles, kMat>(p, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH, active,
                                                        s_hot, s_cull, s_bins, s_rgb, s_ppm, aligned,
                                                        (kGivenRay && c == c0) ? &d0 : nullptr);
 #ifdef ERAY_PHASE_TRACE_REPEAT  // diagnostics: the same sub-block again, instruction cache warm
                 ERAY_TRACE(6);
-                render_sub<kCull, kLdsTiles, kSpecPow>(p, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH, active,
+                render_sub<kCull, kLdsTiles, kMat>(p, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH, active,
                                                        s_hot, s_cull, s_bins, s_rgb, s_ppm, aligned);
 #endif
             }
         };
         if constexpr (kLdsScene) {
             const SceneLds sc = preload_scene(hot, dyn, first_rays);
+            ERAY_TRACE(12);
             __syncthreads();
             ERAY_TRACE(1);
             detail(sc);
@@ -1264,6 +1422,9 @@ __global__ void __launch_bounds__(kWG)
     }
 
     // ---- background of the non-detail sub-blocks ---------------------------------------------
+#ifdef ERAY_AB_X_NO_FILL  // diagnostics only (wrong images): the detail work alone
+    if (p.nobj != 12345) return;
+#endif
     const uint32_t nf = nd < grid ? grid - nd : grid;  // filling workgroups
     const uint32_t f = nd < grid ? blockIdx.x - nd : blockIdx.x;
     const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
@@ -1338,7 +1499,7 @@ hipError_t launch_tri_rect(const TriCull* cull, uint32_t T, uint32_t cam_w, uint
 namespace {
 // Persistent grid: as many workgroups as are resident at once (occupancy API), capped by the
 // work (fill blocks or detail sub-blocks, whichever needs more workgroups).
-template <bool C, bool L, bool S, bool K>
+template <bool C, bool L, int M, bool K>
 hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, hipStream_t s) {
     static int per_cu = -1, cus = 0;
     static size_t per_cu_dyn = 0;
@@ -1347,7 +1508,7 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, frame_kernel<C, L, S, K>, kWG, dyn) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, frame_kernel<C, L, M, K>, kWG, dyn) !=
                 hipSuccess ||
             per_cu <= 0)
             per_cu = 1;
@@ -1359,21 +1520,21 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
     }();
     const int wg_cu = cap > 0 && cap < per_cu ? cap : per_cu;
     const uint32_t grid = min(want, (uint32_t)(wg_cu * cus));
-    frame_kernel<C, L, S, K><<<grid, kWG, dyn, s>>>(p.objects, p.lights, p.cull, p.tris, p.shade,
+    frame_kernel<C, L, M, K><<<grid, kWG, dyn, s>>>(p.objects, p.lights, p.cull, p.tris, p.shade,
                                                     p.nobj | (p.nlights << 16), p.total_tris, p.total_sub, grid, p);
     return hipGetLastError();
 }
 
-template <bool C, bool S>
+template <bool C, int M>
 hipError_t launch_frame_cs(const FrameParams& p, uint32_t want, hipStream_t s) {
     // small scenes are preloaded into LDS whole (no object then needs the LDS tiles); otherwise
     // everything is read from the device arrays
     if (p.lds_scene) {
         const size_t dyn = scene_lds_layout(p.nobj, p.nlights, p.total_tris, C).bytes;
-        return launch_frame_kernel<C, false, S, true>(p, want, dyn, s);
+        return launch_frame_kernel<C, false, M, true>(p, want, dyn, s);
     }
-    if (p.max_object_tris > kDirectMax) return launch_frame_kernel<C, true, S, false>(p, want, 0, s);
-    return launch_frame_kernel<C, false, S, false>(p, want, 0, s);
+    if (p.max_object_tris > kDirectMax) return launch_frame_kernel<C, true, M, false>(p, want, 0, s);
+    return launch_frame_kernel<C, false, M, false>(p, want, 0, s);
 }
 }  // namespace
 
@@ -1383,8 +1544,21 @@ hipError_t launch_render(const FrameParams& p, hipStream_t s) {
     if (!nblk) return hipSuccess;
     // enough workgroups for one fill block or one round of detail sub-blocks per wave
     const uint32_t want = max((nblk + 3) / 4, (p.total_sub + 3) / 4);
-    if (p.cull) return p.spec_pow ? launch_frame_cs<true, true>(p, want, s) : launch_frame_cs<true, false>(p, want, s);
-    return p.spec_pow ? launch_frame_cs<false, true>(p, want, s) : launch_frame_cs<false, false>(p, want, s);
+    const int mat = (p.spec_pow ? kMatSpecPow : 0) | (p.example_mat ? kMatExample : 0);
+    if (p.cull) {
+        switch (mat) {
+            case 0: return launch_frame_cs<true, 0>(p, want, s);
+            case kMatSpecPow: return launch_frame_cs<true, kMatSpecPow>(p, want, s);
+            case kMatExample: return launch_frame_cs<true, kMatExample>(p, want, s);
+            default: return launch_frame_cs<true, kMatSpecPow | kMatExample>(p, want, s);
+        }
+    }
+    switch (mat) {
+        case 0: return launch_frame_cs<false, 0>(p, want, s);
+        case kMatSpecPow: return launch_frame_cs<false, kMatSpecPow>(p, want, s);
+        case kMatExample: return launch_frame_cs<false, kMatExample>(p, want, s);
+        default: return launch_frame_cs<false, kMatSpecPow | kMatExample>(p, want, s);
+    }
 }
 
 hipError_t launch_pack_ppm(const float* rgb, uint32_t w, uint32_t h, uint8_t* out, hipStream_t s) {

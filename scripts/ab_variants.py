@@ -13,10 +13,16 @@ sys.path.insert(0, ROOT)
 
 VARIANTS = {
     "base": (),
+    "batch4": ("ERAY_AB_BATCH_FIXED",),
     "lazyray": ("ERAY_AB_LAZY_RAY",),
-    "earlymat": ("ERAY_AB_EARLY_MATERIAL",),
-    "lazy_early": ("ERAY_AB_LAZY_RAY", "ERAY_AB_EARLY_MATERIAL"),
-    "noplane": ("ERAY_AB_PLANE_OFF",),
+    "sload": ("ERAY_AB_SLOAD_UNIFORM",),
+    "sload_lazy": ("ERAY_AB_SLOAD_UNIFORM", "ERAY_AB_LAZY_RAY"),
+    "global": ("ERAY_AB_NO_LDS_SCENE",),
+    "x_noshadow": ("ERAY_AB_X_NO_SHADOW",),
+    "x_notex": ("ERAY_AB_X_NO_TEXTURE",),
+    "x_neither": ("ERAY_AB_X_NO_SHADOW", "ERAY_AB_X_NO_TEXTURE"),
+    "x_nofill": ("ERAY_AB_X_NO_FILL",),
+    "x_nodetail": ("ERAY_AB_X_NO_DETAIL",),
 }
 
 CHILD = r"""
@@ -42,12 +48,36 @@ print(os.environ["ERAY_LIB"].split("_hip")[-1], " | ".join(out), flush=True)
 """
 
 
+def build_head(rev="HEAD"):
+    """lib/liberay_hip_head.so from the committed sources (the control of an A/B run)."""
+    import shutil
+    import tempfile
+    from eray_amd import build as B
+    tmp = tempfile.mkdtemp(prefix="eray_head_")
+    subprocess.run(f"git -C {ROOT} archive {rev} eray_amd/csrc include | tar -x -C {tmp}", shell=True, check=True)
+    csrc, inc = os.path.join(tmp, "eray_amd", "csrc"), os.path.join(tmp, "include")
+    flags = [f if not f.startswith("-I") else "-I" + inc for f in B.CXXFLAGS]
+    objs = []
+    for src in B.SOURCES:
+        o = os.path.join(tmp, src + ".o")
+        lang = [] if src.endswith(".hip") else ["-x", "hip"]
+        subprocess.run([B.hipcc(), *flags, *lang, "-c", os.path.join(csrc, src), "-o", o], check=True)
+        objs.append(o)
+    out = os.path.join(B.LIB_DIR, "liberay_hip_head.so")
+    subprocess.run([B.hipcc(), f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", out, *objs], check=True)
+    shutil.rmtree(tmp)
+    return out
+
+
 def main():
     mode = sys.argv[1] if len(sys.argv) > 1 else "run"
     names = sys.argv[2:] or list(VARIANTS)
     if mode == "build":
         from eray_amd.build import build
         for n in names:
+            if n == "head":
+                print(build_head(), flush=True)
+                continue
             print(build(variant=n, defines=VARIANTS[n]), flush=True)
         return
     env = dict(os.environ, ROOT=ROOT)

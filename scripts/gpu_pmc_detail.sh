@@ -2,17 +2,19 @@
 # Counter passes over scripts/pmc_detail.py (each pass its own run, kernel trace only).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out/pmcd
+OUT=${OUT:-gpurun_out/pmcd}
+mkdir -p $OUT
 export TMPDIR=/tmp
 pass() {
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex 'frame_kernel' --output-format csv \
-      -d gpurun_out/pmcd/$name -o $name -- python scripts/pmc_detail.py > gpurun_out/pmcd/$name.log 2>&1
+      -d $OUT/$name -o $name -- python scripts/pmc_detail.py > $OUT/$name.log 2>&1
   local rc=$?
   echo "=== pmc $name rc=$rc"
-  if [ $rc -ne 0 ]; then tail -20 gpurun_out/pmcd/$name.log; exit $rc; fi
+  if [ $rc -ne 0 ]; then tail -20 $OUT/$name.log; exit $rc; fi
 }
 pass a SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM
 pass b SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR
-pass c SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INST_CYCLES_VMEM_RD SQ_BUSY_CYCLES
-python scripts/pmc_detail.py report gpurun_out/pmcd
+pass c SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY
+pass d SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC
+python scripts/pmc_detail.py report $OUT

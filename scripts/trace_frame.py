@@ -45,10 +45,10 @@ if sel.any():
     ghz = ((clk[:, :, 7] - clk[:, :, 1])[sel] / ((t[:, :, 7] - t[:, :, 1])[sel] * 10.0)).mean()
     print(f"shader clock (detail waves) ~ {ghz:.2f} GHz")
 t0 = t[:, :, 0][t[:, :, 0] > 0].min()
-names = {0: "entry", 1: "caches", 9: "geom", 10: "cull", 11: "ray", 14: "bbox", 2: "primary", 3: "material", 15: "shadow", 4: "light", 5: "stored",
+names = {0: "entry", 13: "issued", 12: "stored", 1: "caches", 9: "geom", 10: "cull", 11: "ray", 14: "bbox", 2: "primary", 3: "material", 15: "shadow", 4: "light", 5: "out",
          6: "repeat", 7: "detail", 8: "end"}
 print(f"rows {row0}..{row0 + rows}; ticks of 10 ns from the first entry")
-order = [0, 1, 6, 9, 10, 11, 14, 2, 3, 15, 4, 5, 7]
+order = [0, 13, 12, 1, 9, 10, 14, 2, 3, 15, 4, 5, 7]
 print("  wg.w " + " ".join(f"{names[k]:>8s}" for k in order))
 for g in range(64):
     for w in range(4):
