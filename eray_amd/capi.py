@@ -78,7 +78,7 @@ class RenderParams(C.Structure):
     _fields_ = [("image_width", C.c_uint32), ("image_height", C.c_uint32), ("row0", C.c_uint32),
                 ("rows", C.c_uint32), ("bounces", C.c_uint32), ("anti_aliasing", C.c_uint32),
                 ("out_rgb", C.c_void_p), ("out_ppm", C.c_void_p), ("out_face", C.c_void_p),
-                ("flags", C.c_uint32)]
+                ("flags", C.c_uint32), ("aa_seed", C.c_uint64)]
 
 
 # Every exported symbol of include/eray_hip.h with its (restype, argtypes).
@@ -324,21 +324,22 @@ class Context:
         return idx.value
 
     def render(self, image_width, image_height, row0=0, rows=None, out_rgb=None, out_ppm=None,
-               out_face=None, bounces=0, anti_aliasing=0, flags=RENDER_DEFAULT) -> None:
+               out_face=None, bounces=0, anti_aliasing=0, flags=RENDER_DEFAULT, aa_seed=0) -> None:
         if rows is None:
             rows = image_height - row0
         p = RenderParams(image_width, image_height, row0, rows, bounces, anti_aliasing,
-                         out_rgb or None, out_ppm or None, out_face or None, flags)
+                         out_rgb or None, out_ppm or None, out_face or None, flags, aa_seed)
         self._check(lib().eray_render(self._h, C.byref(p)))
 
     def render_frames(self, frames, image_width, image_height, row0=0, rows=None, out_rgb=None,
-                      out_ppm=None, out_face=None, flags=RENDER_DEFAULT, timed=False, prepare_only=False):
+                      out_ppm=None, out_face=None, flags=RENDER_DEFAULT, timed=False, prepare_only=False,
+                      bounces=0, anti_aliasing=0, aa_seed=0):
         """`frames` back-to-back renders (replayed from a cached HIP graph); returns the mean
         device ms per frame when `timed`.  `prepare_only` builds the launch plan and returns."""
         if rows is None:
             rows = image_height - row0
-        p = RenderParams(image_width, image_height, row0, rows, 0, 0, out_rgb or None, out_ppm or None,
-                         out_face or None, flags)
+        p = RenderParams(image_width, image_height, row0, rows, bounces, anti_aliasing, out_rgb or None,
+                         out_ppm or None, out_face or None, flags, aa_seed)
         if prepare_only:
             self._check(lib().eray_render_prepare(self._h, C.byref(p), frames))
             return None

@@ -554,14 +554,15 @@ namespace {
 int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out, bool* empty) {
     if (int st = use_device(ctx)) return st;
     if (!rp) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "params is null");
-    if (rp->anti_aliasing != 0)
-        return set_error(ctx, ERAY_E_UNSUPPORTED,
-                         "anti_aliasing > 0 uses rand::thread_rng (engine.rs:49,62-69); not supported");
-    if (rp->bounces > 0)
-        for (auto& o : ctx->objects)
-            if (o.mat.reflection.data)
-                return set_error(ctx, ERAY_E_UNSUPPORTED,
-                                 "reflection bounces (engine.rs:181-191) are not supported yet");
+    // anti-aliasing and reflection bounces take the general tracer (trace.hip); bounces only
+    // matter when some material has a reflection output (engine.rs:181-182)
+    bool reflective = false;
+    for (auto& o : ctx->objects) reflective |= o.mat.reflection.data != nullptr;
+    const uint32_t bounces = reflective ? rp->bounces : 0u;
+    if (bounces > kMaxBounces)
+        return set_error(ctx, ERAY_E_UNSUPPORTED, "bounces = %u: at most %u reflection levels", rp->bounces,
+                         kMaxBounces);
+    const bool general = rp->anti_aliasing > 0 || bounces > 0;
     uint32_t W, H;
     eray_camera_size(&ctx->camera, &W, &H);
     if ((uint64_t)rp->row0 + rp->rows > H)
@@ -576,7 +577,7 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     if (rp->out_ppm && (W != rp->image_width || H != rp->image_height))
         return set_error(ctx, ERAY_E_INVALID_ARGUMENT,
                          "fused PPM output needs camera size == image size; use eray_pack_ppm");
-    const bool cull = !(rp->flags & ERAY_RENDER_BRUTE_FORCE);
+    const bool cull = !general && !(rp->flags & ERAY_RENDER_BRUTE_FORCE);
     if (int st = sync_scene(ctx, cull)) return st;
     if (cull)
         if (int st = sync_bins(ctx, rp->row0 % kBinH)) return st;
@@ -672,6 +673,10 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     p.tiles_x = (W + 63) / 64;
     p.bins_x = (W + kBinW - 1) / kBinW;
     p.bin_phase = rp->row0 % kBinH;
+    p.aa = rp->anti_aliasing;
+    p.bounces = bounces;
+    p.seed_lo = (uint32_t)rp->aa_seed;
+    p.seed_hi = (uint32_t)(rp->aa_seed >> 32);
     return ERAY_OK;
 }
 

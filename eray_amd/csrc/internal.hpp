@@ -54,6 +54,8 @@ constexpr uint32_t kDirectMax = 256;
 constexpr uint32_t kBinW = 16, kBinH = 4;
 // Detail rectangles carried in the kernel arguments (more objects: merged into the last one).
 constexpr int kMaxRects = 8;
+// Deepest reflection recursion the general tracer keeps frames for (Engine::bounces).
+constexpr uint32_t kMaxBounces = 16;
 
 struct ObjGeom {  // what the triangle scans need of an object, 80 B
     uint32_t tri_begin, tri_count;
@@ -114,6 +116,10 @@ struct FrameParams {
     uint32_t tiles_x;    // 64 x 4 pixel blocks per row
     uint32_t bins_x;     // screen bins per row
     uint32_t bin_phase;  // bins start at camera rows bin_phase + k * kBinH (row0 % kBinH)
+    // general tracer (trace.hip): anti-aliasing rays per pixel, reflection depth, jitter seed;
+    // aa == 0 && bounces == 0 selects the frame kernel
+    uint32_t aa, bounces;
+    uint32_t seed_lo, seed_hi;
 };
 
 // Byte offsets of the LDS scene copy: [ObjectDesc x nobj | LightDesc x nl | TriCull x n (if
@@ -142,7 +148,9 @@ hipError_t launch_tri_cull(const TriHot* hot, uint32_t T, float cx, float cy, fl
 // updated by atomicMax: (~x0, x1 + 1, ~y0, y1 + 1); a1 == 0 means empty.
 hipError_t launch_tri_rect(const TriCull* cull, uint32_t T, uint32_t cam_w, uint32_t cam_h,
                            uint32_t* acc, hipStream_t s);
+// The frame kernel, or the general tracer (trace.hip) when p.aa or p.bounces is set.
 hipError_t launch_render(const FrameParams& p, hipStream_t s);
+hipError_t launch_trace(const FrameParams& p, hipStream_t s);
 
 struct ObjBins {  // device arrays of one object's bins (owned by the context)
     uint32_t* start = nullptr;

@@ -1,0 +1,269 @@
+// trace.hip — the general tracer on gfx950: Engine::render with anti-aliasing and reflection
+// bounces (src/lib/engine.rs:46-81, 112-228).
+//
+// The frame kernel (render.hip) is specialised for what the reference's default engine does —
+// one primary ray per pixel at the integer pixel corner, no recursion — and its culling
+// records, pixel rectangles and screen bins all assume those rays.  Jittered anti-aliasing
+// rays and reflected rays go anywhere, so this kernel is the plain form of the same semantics:
+// one thread per pixel (a 256-thread workgroup owns a 64 x 4 pixel tile, each wave a 64-pixel
+// row segment), every ray scans every object's faces in index order (Object::intersects,
+// object.rs:58-81: bbox test, then the FIRST face whose Triangle::intersects passes), with the
+// triangle records read through L1/L2 (TriHot, 48 B).  It runs only when the caller asks for
+// anti_aliasing > 0, or for bounces > 0 on a scene with a reflection output; the reference's
+// default engine never takes it.
+//
+// Recursion.  cast_ray returns a Vec<Color> whose nested bounce lists are flattened into the
+// parent's (`lighting.extend(cast_ray(..).map(|c| c * reflection))`, engine.rs:187-190) and
+// the pixel value is the left fold of the flattened list (color.rs:82-87).  So the pixel is
+// one running sum over a depth-first walk: an element produced at depth k is multiplied by the
+// reflection factors of depths k-1, ..., 0, in that order, and added.  Only the closest
+// object's elements survive a level (`lighting.clear()` on a closer hit, engine.rs:119-126),
+// so each level first finds its closest hit, then emits.  The walk keeps one frame per depth
+// (hit point, normal, ray direction, material, next light) — bounces <= kMaxBounces.
+//
+// Anti-aliasing.  engine.rs:62-69 draws two gen_range(-1.0..1.0) values per extra ray from
+// rand::thread_rng (ChaCha12, OS-seeded: not reproducible).  Here the stream is Philox4x32-10
+// keyed by the caller's seed with counter (x, y, sample, 0) — words 0 and 1 are the x and y
+// draws — mapped to [-1, 1) exactly as rand 0.8's UniformFloat::sample_single does.  The
+// oracle uses the same stream (oracle_render_aa), so results are comparable bit for bit.
+#include "device_math.hpp"
+#include "glibc_cosf.hpp"
+#include "hit.hpp"
+#include "internal.hpp"
+
+namespace eray {
+namespace gpu {
+namespace {
+
+using namespace eray::dev;
+
+// Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11; Random123's philox4x32 with 10 rounds).
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int round = 0; round < 10; ++round) {
+        if (round) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+        const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+        c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+    }
+    return c;
+}
+
+// rand 0.8 UniformFloat::<f32>::sample_single(-1.0, 1.0) from one 32-bit word: 23 bits as a
+// float in [1, 2), minus 1, times the range (2), plus low (-1); never reaches high, so one draw.
+__device__ __forceinline__ float jitter(uint32_t word) {
+    const float value0_1 = __uint_as_float((word >> 9) | 0x3F800000u) - 1.0f;
+    return value0_1 * 2.0f + -1.0f;
+}
+
+// Camera::pixel_to_ray(x', y').dir (camera.rs:57-76, Ray::new normalises)
+__device__ __forceinline__ f3 camera_ray_dir(const FrameParams& p, float xf, float yf) {
+    const f3 C = mk3(p.cx, p.cy, p.cz);
+    const float vw = p.ratio * 2.0f;
+    const f3 horizontal = mk3(vw, 0.0f, 0.0f), vertical = mk3(0.0f, 2.0f, 0.0f);
+    const f3 botleft = sub(sub(sub(C, divs(horizontal, 2.0f)), divs(vertical, 2.0f)), mk3(0.0f, 0.0f, p.z_dist));
+    return normalize(sub(add(add(botleft, mul(horizontal, xf)), mul(vertical, yf)), C));
+}
+
+// Object<Built>::intersects up to the face (object.rs:58-78): bbox, then the first face in
+// index order; u, v, t of that face.
+__device__ __forceinline__ int first_face(const TriHot* tris, const ObjGeom& ob, f3 o, f3 d, float& u, float& v,
+                                          float& t) {
+    if (!bbox_hit(ob, o, d)) return -1;
+    const TriHot* r = tris + ob.tri_begin;
+    for (uint32_t f = 0; f < ob.tri_count; ++f)
+        if (exact_test(r[f], o, d, u, v, t)) return (int)f;
+    return -1;
+}
+
+// One level of cast_ray: the closest object's hit and the Material::get values at it.
+struct Level {
+    f3 P, N, d;  // hit point, interpolated normal, the (normalised) ray direction
+    rgb color;
+    float kd, ks, sp, refl;
+    uint32_t li;  // next light of the per-light loop (engine.rs:130-192)
+};
+
+// The closest object's first hit along Ray(o, d) — strict `<` on |P - camera|² in object order
+// (engine.rs:116-126) — and its material (Triangle::intersects' P and N, primitives.rs:60-69;
+// RaycastHit's UV and Material::get, object.rs:70-74, material.rs:56-94).  False on a miss.
+__device__ bool surface(const FrameParams& p, f3 o, f3 d, Level& L, int32_t* face_out) {
+    const f3 C = mk3(p.cx, p.cy, p.cz);
+    bool have = false;
+    float best = 0.0f, bu = 0.0f, bv = 0.0f, bt = 0.0f;
+    uint32_t bo = 0;
+    int bf = -1;
+    for (uint32_t oi = 0; oi < p.nobj; ++oi) {
+        const ObjGeom ob = p.objects[oi].g;
+        float u, v, t;
+        const int f = first_face(p.tris, ob, o, d, u, v, t);
+        if (f < 0) continue;
+        const float dsq = len_sq(sub(add(o, mul(d, t)), C));
+        if (!have || dsq < best) {
+            have = true;
+            best = dsq;
+            bo = oi;
+            bf = f;
+            bu = u;
+            bv = v;
+            bt = t;
+        }
+    }
+    if (!have) return false;
+    if (face_out) *face_out = bf;
+    const ObjectDesc& od = p.objects[bo];
+    const TriShade sh = p.shade[od.g.tri_begin + (uint32_t)bf];
+    L.P = add(o, mul(d, bt));
+    const f3 na = mk3(sh.s0.x, sh.s0.y, sh.s0.z), nb = mk3(sh.s0.w, sh.s1.x, sh.s1.y);
+    const f3 nc = mk3(sh.s1.z, sh.s1.w, sh.s2.x);
+    L.N = normalize(add(add(mul(na, bu), mul(nb, bv)), mul(nc, bt)));  // (t, not w: primitives.rs:63)
+    L.d = d;
+    const float w = 1.0f - bu - bv;
+    const float uv0 = ((sh.s2.y * w) + (sh.s2.w * bu)) + (sh.s3.y * bv);
+    const float uv1 = ((sh.s2.z * w) + (sh.s3.x * bu)) + (sh.s3.z * bv);
+    const MaterialDesc& mat = od.mat;
+    // defaults at use (engine.rs:128,155,160,164,181)
+    L.color = rgb{0.0f, 0.0f, 0.0f};
+    L.kd = 0.5f;
+    L.ks = 0.5f;
+    L.sp = 1.0f;
+    L.refl = 0.0f;
+    if (mat.example) {  // main.rs's graph at the texel Material::get reads
+        const uint32_t ix = mod_size(sat_u32(uv0 * (float)mat.ex_w), mat.ex_w);
+        const uint32_t iy = mod_size(sat_u32(uv1 * (float)mat.ex_h), mat.ex_h);
+        const float wv = __builtin_fabsf(libm::cosf_glibc(((float)ix * mat.ex_xf + (float)iy * mat.ex_yf) / 10.0f));
+        const float omf = 1.0f - mat.ex_factor;
+        L.color = rgb{wv * omf + mat.ex_r * mat.ex_factor, wv * omf + mat.ex_g * mat.ex_factor,
+                      wv * omf + mat.ex_b * mat.ex_factor};
+        L.kd = wv;
+    }
+    if (const float* c = texel(mat.color, uv0, uv1, 3)) L.color = rgb{c[0], c[1], c[2]};
+    if (const float* c = texel(mat.diffuse, uv0, uv1, 1)) L.kd = *c;
+    if (const float* c = texel(mat.specular, uv0, uv1, 1)) L.ks = *c;
+    if (const float* c = texel(mat.specular_power, uv0, uv1, 1)) L.sp = *c;
+    if (const float* c = texel(mat.reflection, uv0, uv1, 1)) L.refl = *c;
+    L.li = 0;
+    return true;
+}
+
+// Engine::reaches_light (engine.rs:218-228): the FIRST object with any hit decides.
+__device__ bool reaches_light(const FrameParams& p, f3 S, f3 sd, f3 Lp) {
+    const float dist = len(sub(Lp, S));
+    for (uint32_t oi = 0; oi < p.nobj; ++oi) {
+        const ObjGeom ob = p.objects[oi].g;
+        float u, v, t;
+        if (first_face(p.tris, ob, S, sd, u, v, t) >= 0) return len(sub(add(S, mul(sd, t)), S)) > dist;
+    }
+    return true;
+}
+
+// diffuse + specular of one point light that reaches the hit (engine.rs:143-176)
+__device__ __forceinline__ rgb shade(const Level& L, const LightDesc& Ld) {
+    const f3 Lp = mk3(Ld.pos[0], Ld.pos[1], Ld.pos[2]);
+    const f3 LmP = sub(Lp, L.P);
+    float prod = rust_clamp(dot0(L.N, LmP), 0.0f, 1.0f);
+    if (prod != prod) prod = 0.0f;
+    const float falloff = 1.0f / len(LmP);
+    const rgb lc{Ld.color[0], Ld.color[1], Ld.color[2]};
+    const rgb diffusion = cmul(cmul(cmul(cmul(cmulc(L.color, lc), L.kd), prod), Ld.brightness), falloff);
+    const f3 reflected = sub(L.d, mul(mul(L.N, 2.0f), dot0(L.d, L.N)));
+    const float res =
+        rust_clamp(L.ks * Ld.brightness * powf_ref(dot0(normalize(reflected), normalize(LmP)), L.sp), 0.0f, 1.0f);
+    const float sf = rust_clamp(powf_ref(falloff, L.sp), 0.0f, 1.0f);
+    return cadd(diffusion, rgb{res * sf, res * sf, res * sf});
+}
+
+// Engine::cast_ray(ray, 0).sum() (engine.rs:112-216, color.rs:82-87) as a depth-first walk.
+__device__ rgb cast_ray(const FrameParams& p, f3 o, f3 d, int32_t* face_out) {
+    Level st[kMaxBounces + 1];
+    bool any = false;
+    rgb acc{0.0f, 0.0f, 0.0f};
+    auto emit = [&](rgb c, int depth) {  // c * refl[depth-1] * ... * refl[0], then the fold
+        for (int j = depth - 1; j >= 0; --j) c = cmul(c, st[j].refl);
+        acc = any ? cadd(acc, c) : c;
+        any = true;
+    };
+    const rgb miss{0.1f, 0.1f, 0.2f};  // engine.rs:211-213
+    if (!surface(p, o, d, st[0], face_out)) {
+        emit(miss, 0);
+        return acc;
+    }
+    int depth = 0;
+    while (depth >= 0) {
+        Level& L = st[depth];
+        if (L.li < p.nlights) {
+            const LightDesc Ld = p.lights[L.li++];
+            if (Ld.variant == 1) continue;  // ambient lights come after the loop
+            const f3 Lp = mk3(Ld.pos[0], Ld.pos[1], Ld.pos[2]);
+            const f3 S = add(L.P, mul(L.N, 0.1f));
+            if (reaches_light(p, S, normalize(sub(Lp, L.P)), Lp)) emit(shade(L, Ld), depth);
+            if ((uint32_t)depth < p.bounces && L.refl != 0.0f) {  // engine.rs:181-191
+                const f3 rd = normalize(sub(L.d, mul(mul(L.N, 2.0f), dot0(L.d, L.N))));
+                if (surface(p, S, rd, st[depth + 1], nullptr))
+                    ++depth;
+                else
+                    emit(miss, depth + 1);
+            }
+        } else {
+            for (uint32_t li = 0; li < p.nlights; ++li) {  // ambient lights (engine.rs:197-208)
+                const LightDesc A = p.lights[li];
+                if (A.variant != 1) continue;
+                const rgb m{rust_min(A.color[0], L.color.r), rust_min(A.color[1], L.color.g),
+                            rust_min(A.color[2], L.color.b)};
+                emit(cmul(cmul(m, L.kd), A.brightness), depth);
+            }
+            --depth;
+        }
+    }
+    return acc;
+}
+
+__global__ void __launch_bounds__(256) trace_kernel(FrameParams p) {
+    const uint32_t px = blockIdx.x * 64 + (threadIdx.x & 63);
+    const uint32_t py = blockIdx.y * 4 + (threadIdx.x >> 6);  // rank-local row
+    if (px >= p.cam_w || py >= p.rows) return;
+    const uint32_t y = p.row0 + py;
+    const f3 C = mk3(p.cx, p.cy, p.cz);
+    int32_t face = -1;
+    // cast_ray_from_camera(x as f32, y as f32) (engine.rs:60, 100-109)
+    rgb avg = cast_ray(p, C, camera_ray_dir(p, (float)px / (float)p.cam_w, (float)y / (float)p.cam_h), &face);
+    for (uint32_t s = 0; s < p.aa; ++s) {  // engine.rs:62-69
+        const uint4 r = philox4x32_10(make_uint4(px, y, s, 0u), p.seed_lo, p.seed_hi);
+        const float xf = ((float)px + jitter(r.x)) / (float)p.cam_w;
+        const float yf = ((float)y + jitter(r.y)) / (float)p.cam_h;
+        avg = cadd(avg, cast_ray(p, C, camera_ray_dir(p, xf, yf), nullptr));
+    }
+    if (p.aa) {  // (average / aa as f32).clamp() (engine.rs:71-73)
+        const float n = (float)p.aa;
+        avg = rgb{rust_clamp(avg.r / n, 0.0f, 1.0f), rust_clamp(avg.g / n, 0.0f, 1.0f),
+                  rust_clamp(avg.b / n, 0.0f, 1.0f)};
+    }
+    const size_t idx = (size_t)py * p.img_w + px;
+    if (p.out_rgb) {
+        float* o = p.out_rgb + 3 * idx;
+        o[0] = avg.r;
+        o[1] = avg.g;
+        o[2] = avg.b;
+    }
+    if (p.out_ppm) {  // Color::as_bytes, rows bottom-up (image.rs:48-74, color.rs:31-37)
+        uint8_t* o = p.out_ppm + 3 * ((size_t)(p.rows - 1 - py) * p.img_w + px);
+        o[0] = (uint8_t)sat_u8(avg.r * 255.0f);
+        o[1] = (uint8_t)sat_u8(avg.g * 255.0f);
+        o[2] = (uint8_t)sat_u8(avg.b * 255.0f);
+    }
+    if (p.out_face) p.out_face[idx] = face;
+}
+
+}  // namespace
+
+hipError_t launch_trace(const FrameParams& p, hipStream_t s) {
+    const dim3 grid((p.cam_w + 63) / 64, (p.rows + 3) / 4);
+    hipLaunchKernelGGL(trace_kernel, grid, dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+}  // namespace gpu
+}  // namespace eray

@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <random>
 #include <sstream>
 
 #include "eray/engine.hpp"
@@ -230,7 +231,11 @@ Scene& Scene::add_object(Object<Built> object) {
 
 // ------------------------------------------------------------------------------ Engine -----
 Engine::Engine(std::pair<uint32_t, uint32_t> size, uint32_t bounces, uint32_t anti_aliasing)
-    : image_(size.first, size.second, Color()), bounces_(bounces), anti_aliasing_(anti_aliasing) {}
+    : image_(size.first, size.second, Color()), bounces_(bounces), anti_aliasing_(anti_aliasing) {
+    // rand::thread_rng is seeded from the OS (engine.rs:49): so is the jitter stream by default
+    std::random_device rd;
+    aa_seed_ = ((uint64_t)rd() << 32) | rd();
+}
 
 void Engine::upload() {
     Device& d = Device::current();
@@ -283,7 +288,7 @@ const Image<Color>& Engine::render() {  // engine.rs:46-81
     d.check(eray_memset(d.ctx(), rgb_->data(), 0, 12 * n));
     const uint32_t h = scene_.camera_.size().second;
     eray_render_params p{image_.width, image_.height, 0, h, bounces_, anti_aliasing_,
-                         static_cast<float*>(rgb_->data()), nullptr, nullptr, ERAY_RENDER_DEFAULT};
+                         static_cast<float*>(rgb_->data()), nullptr, nullptr, ERAY_RENDER_DEFAULT, aa_seed_};
     d.check(eray_render(d.ctx(), &p));
     d.check(eray_copy_to_host(d.ctx(), image_.pixels.data(), rgb_->data(), 12 * n));
     return image_;

@@ -126,12 +126,18 @@ public:
     const Image<Color>& render();
     // engine.rs:86-98: render + save_as_ppm (the PPM bytes come from the device, fused)
     const Image<Color>& render_to_path(const std::string& path);
+    // The anti-aliasing jitter stream's key (eray_render_params::aa_seed).  The reference draws
+    // from the OS-seeded thread_rng; a new Engine picks a random seed likewise, and fixing it
+    // makes anti-aliased renders reproducible.
+    void set_aa_seed(uint64_t seed) { aa_seed_ = seed; }
+    uint64_t aa_seed() const { return aa_seed_; }
 
 private:
     void upload();
     Image<Color> image_;
     Scene scene_;
     uint32_t bounces_, anti_aliasing_;
+    uint64_t aa_seed_ = 0;
     std::shared_ptr<DeviceBuffer> rgb_, ppm_;
 };
 

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define ERAY_ABI_VERSION 1
+#define ERAY_ABI_VERSION 2
 
 typedef enum eray_status {
     ERAY_OK = 0,
@@ -190,8 +190,8 @@ typedef struct eray_render_params {
     uint32_t image_height;
     uint32_t row0;                  /* render camera rows [row0, row0 + rows)               */
     uint32_t rows;
-    uint32_t bounces;               /* Engine::bounces (reflection recursion depth)         */
-    uint32_t anti_aliasing;         /* Engine::anti_aliasing; only 0 is supported           */
+    uint32_t bounces;               /* Engine::bounces (reflection recursion depth, <= 16)  */
+    uint32_t anti_aliasing;         /* Engine::anti_aliasing: extra jittered rays per pixel */
     float* out_rgb;                 /* device or NULL: rows x image_width x 3 f32, pixel
                                        (x, row0 + j) at ((j * image_width) + x) * 3         */
     uint8_t* out_ppm;               /* device or NULL: the PPM body bytes of these rows, in
@@ -200,6 +200,9 @@ typedef struct eray_render_params {
     int32_t* out_face;              /* device or NULL: rows x image_width, the face index of
                                        the closest object's first hit, -1 for a miss        */
     uint32_t flags;                 /* ERAY_RENDER_* */
+    uint64_t aa_seed;               /* anti-aliasing jitter stream: Philox4x32-10 keyed by
+                                       aa_seed, counter (x, y, sample, 0) — replaces the
+                                       reference's OS-seeded rand::thread_rng (engine.rs:49) */
 } eray_render_params;
 
 #define ERAY_RENDER_DEFAULT 0u

@@ -518,10 +518,50 @@ int oracle_example_material(uint32_t w, uint32_t h, float x_fac, float y_fac, fl
     return ORACLE_OK;
 }
 
+void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]};
+    uint32_t k0 = key[0], k1 = key[1];
+    for (int round = 0; round < 10; ++round) {
+        if (round) {
+            k0 += 0x9E3779B9u;  // Weyl key schedule
+            k1 += 0xBB67AE85u;
+        }
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+        c[0] = n0;
+        c[1] = lo1;
+        c[2] = n2;
+        c[3] = lo0;
+    }
+    std::memcpy(out, c, sizeof c);
+}
+
+float oracle_jitter(uint32_t word) {
+    // rand 0.8 UniformFloat::<f32>::sample_single(-1.0, 1.0): 23 random bits as a float in
+    // [1, 2), minus 1, times the range, plus low (value0_1 * scale + low, unfused)
+    uint32_t bits = (word >> 9) | 0x3F800000u;
+    float value1_2;
+    std::memcpy(&value1_2, &bits, sizeof bits);
+    const float value0_1 = value1_2 - 1.0f;
+    return value0_1 * 2.0f + -1.0f;
+}
+
 int oracle_render(const oracle_object* objects, uint32_t object_count, const oracle_light* lights,
                   uint32_t light_count, const oracle_camera* cam, uint32_t image_width,
                   uint32_t image_height, uint32_t row0, uint32_t rows, uint32_t bounces,
                   float* out_rgb, int32_t* out_face, int32_t* out_object, oracle_stats* stats) {
+    return oracle_render_aa(objects, object_count, lights, light_count, cam, image_width, image_height,
+                            row0, rows, bounces, 0, 0, out_rgb, out_face, out_object, stats);
+}
+
+int oracle_render_aa(const oracle_object* objects, uint32_t object_count, const oracle_light* lights,
+                     uint32_t light_count, const oracle_camera* cam, uint32_t image_width,
+                     uint32_t image_height, uint32_t row0, uint32_t rows, uint32_t bounces,
+                     uint32_t anti_aliasing, uint64_t seed, float* out_rgb, int32_t* out_face,
+                     int32_t* out_object, oracle_stats* stats) {
     Engine e;
     e.camera = to_camera(cam);
     e.bounces = bounces;
@@ -562,7 +602,26 @@ int oracle_render(const oracle_object* objects, uint32_t object_count, const ora
             int32_t face = -1, obj = -1;
             e.cast_ray(ray, 0, lighting, &face, &obj);
             if (face >= 0) ++e.stats.hit_pixels;
-            Color average = color_sum(lighting);  // anti_aliasing == 0: stored unclamped
+            Color average = color_sum(lighting);
+            // engine.rs:62-69: anti_aliasing more rays at (x + jx, y + jy), jx and jy drawn
+            // from gen_range(-1.0..1.0) in that order.  thread_rng (ChaCha12, OS-seeded) is
+            // replaced by Philox4x32-10 keyed by `seed`, counter (x, y, sample, 0): words 0
+            // and 1 are the two draws.
+            for (uint32_t s = 0; s < anti_aliasing; ++s) {
+                const uint32_t ctr[4] = {x, y, s, 0u};
+                const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+                uint32_t r[4];
+                oracle_philox4x32_10(ctr, key, r);
+                const float jx = oracle_jitter(r[0]), jy = oracle_jitter(r[1]);
+                Ray aa_ray = pixel_to_ray(e.camera, ((float)x + jx) / (float)width, ((float)y + jy) / (float)height);
+                e.cast_ray(aa_ray, 0, lighting, nullptr, nullptr);
+                average = cadd(average, color_sum(lighting));  // AddAssign (color.rs:12)
+            }
+            if (anti_aliasing > 0) {  // (average / aa as f32).clamp() (engine.rs:71-73); else raw
+                const float n = (float)anti_aliasing;
+                average = Color{rust_clamp(average.r / n, 0.0f, 1.0f), rust_clamp(average.g / n, 0.0f, 1.0f),
+                                rust_clamp(average.b / n, 0.0f, 1.0f)};
+            }
             size_t idx = (size_t)(y - row0) * image_width + x;
             out_rgb[3 * idx + 0] = average.r;
             out_rgb[3 * idx + 1] = average.g;

@@ -112,6 +112,19 @@ int oracle_render(const oracle_object* objects, uint32_t object_count,
                   uint32_t bounces, float* out_rgb, int32_t* out_face, int32_t* out_object,
                   oracle_stats* stats);
 
+/* The same with Engine::anti_aliasing = `anti_aliasing` (engine.rs:59-77): the reference's
+ * OS-seeded thread_rng is replaced by Philox4x32-10 (key = seed, counter = (x, y, sample, 0));
+ * each draw maps a 32-bit word to [-1, 1) as rand 0.8's gen_range(-1.0..1.0) does.           */
+int oracle_render_aa(const oracle_object* objects, uint32_t object_count,
+                     const oracle_light* lights, uint32_t light_count, const oracle_camera* cam,
+                     uint32_t image_width, uint32_t image_height, uint32_t row0, uint32_t rows,
+                     uint32_t bounces, uint32_t anti_aliasing, uint64_t seed, float* out_rgb,
+                     int32_t* out_face, int32_t* out_object, oracle_stats* stats);
+/* Philox4x32-10 (Salmon et al., SC'11; Random123's philox4x32 with 10 rounds) and the
+ * gen_range(-1.0..1.0) mapping of one of its words. */
+void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+float oracle_jitter(uint32_t word);
+
 /* Image<Color>::save_as_ppm body bytes (image.rs:48-74): rows bottom-up, sat-u8 bytes. */
 int oracle_ppm_bytes(const float* rgb, uint32_t width, uint32_t height, uint8_t* out);
 /* "P6 {w} {h} 255\n" (image.rs:56); returns header length. */

@@ -68,6 +68,8 @@ def lib():
         L.oracle_powf.restype = C.c_float
         L.oracle_powf.argtypes = [C.c_float, C.c_float]
         L.oracle_ppm_header.restype = C.c_size_t
+        L.oracle_jitter.restype = C.c_float
+        L.oracle_jitter.argtypes = [C.c_uint32]
         _lib = L
     return _lib
 
@@ -220,7 +222,7 @@ class Scene:
 
 
 def render(scene: Scene, cam: Camera, image_width=None, image_height=None, row0=0, rows=None,
-           bounces=0, want_faces=False):
+           bounces=0, want_faces=False, anti_aliasing=0, seed=0):
     W, H = camera_size(cam)
     image_width = W if image_width is None else image_width
     image_height = H if image_height is None else image_height
@@ -230,14 +232,27 @@ def render(scene: Scene, cam: Camera, image_width=None, image_height=None, row0=
     objs = (Object * max(1, len(scene.objects)))(*scene.objects)
     lights = (Light * max(1, len(scene.lights)))(*scene.lights)
     st = Stats()
-    rc = lib().oracle_render(objs, len(scene.objects), lights, len(scene.lights), C.byref(cam),
-                             image_width, image_height, row0, rows, bounces, _fp(out),
+    rc = lib().oracle_render_aa(objs, len(scene.objects), lights, len(scene.lights), C.byref(cam),
+                                image_width, image_height, row0, rows, bounces, anti_aliasing,
+                                C.c_uint64(seed), _fp(out),
                              faces.ctypes.data_as(C.POINTER(C.c_int32)) if want_faces else None,
                              None, C.byref(st))
     if rc:
         raise ValueError(f"oracle_render status {rc}")
     stats = dict(primary_tests=st.primary_tests, shadow_tests=st.shadow_tests, hit_pixels=st.hit_pixels)
     return (out, faces, stats) if want_faces else (out, stats)
+
+
+def philox4x32_10(ctr, key):
+    """Philox4x32-10 block (the anti-aliasing jitter stream, oracle_render_aa)."""
+    c, k, o = (C.c_uint32 * 4)(*ctr), (C.c_uint32 * 2)(*key), (C.c_uint32 * 4)()
+    lib().oracle_philox4x32_10(c, k, o)
+    return list(o)
+
+
+def jitter(word: int) -> float:
+    """rand 0.8 gen_range(-1.0..1.0) for f32 from one 32-bit word."""
+    return lib().oracle_jitter(word)
 
 
 def ppm_bytes(rgb: np.ndarray) -> bytes:

@@ -171,9 +171,6 @@ def test_render_errors(gpu, cube):
     sc = MainScene(gpu, *cube, 64, 64)
     buf = gpu.empty((64, 64, 3), np.float32)
     with pytest.raises(capi.ErayError) as e:
-        gpu.render(64, 64, out_rgb=buf.ptr, anti_aliasing=2)
-    assert e.value.status == capi.E_UNSUPPORTED
-    with pytest.raises(capi.ErayError) as e:
         gpu.render(64, 64, row0=60, rows=10, out_rgb=buf.ptr)
     assert e.value.status == capi.E_INVALID_ARGUMENT
     with pytest.raises(capi.ErayError) as e:  # camera 64x64 does not fit a 64x32 engine image

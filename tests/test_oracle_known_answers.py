@@ -83,3 +83,32 @@ def test_triangle_intersects_edge_semantics(oracle):
     assert b[0] == 0.5 and b[1] == 0.0 and np.signbit(b[1])
     # backface: same triangle seen from behind
     assert oracle.triangle_intersects(pos, nrm, (0, 0, -5), (0, 0, 1)) is None
+
+
+def test_philox_known_answers(oracle):
+    """The anti-aliasing jitter stream: Philox4x32-10 against Random123's kat_vectors."""
+    assert oracle.philox4x32_10([0, 0, 0, 0], [0, 0]) == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    assert oracle.philox4x32_10([0xFFFFFFFF] * 4, [0xFFFFFFFF] * 2) == [0x408F276D, 0x41C83B0E, 0xA20BC7C6,
+                                                                       0x6D5451FD]
+    assert oracle.philox4x32_10([0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344], [0xA4093822, 0x299F31D0]) == [
+        0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+
+
+def test_jitter_is_rand_gen_range(oracle):
+    """rand 0.8 gen_range(-1.0..1.0) for f32: (word >> 9) as the mantissa of [1, 2), minus 1,
+    times 2, minus 1 — the 2^23 outcomes are exactly -1 + k * 2^-22."""
+    assert oracle.jitter(0) == -1.0
+    assert oracle.jitter(0x1FF) == -1.0  # the low 9 bits are discarded
+    assert oracle.jitter(0x200) == -1.0 + 2.0 ** -22
+    assert oracle.jitter(0x80000000) == 0.0
+    assert oracle.jitter(0xFFFFFFFF) == 1.0 - 2.0 ** -22
+
+
+def test_anti_aliasing_zero_is_the_plain_render(oracle, cube):
+    s = oracle.main_rs_scene(*cube, texture=64)
+    cam = oracle.camera(width=24)
+    a, _ = oracle.render(s, cam)
+    b, _ = oracle.render(s, cam, anti_aliasing=0, seed=1234)
+    c, _ = oracle.render(s, cam, anti_aliasing=1, seed=1234)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert not np.array_equal(a, c) and c.max() <= 1.0
