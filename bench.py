@@ -6,13 +6,18 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 Workload (BASELINE.json configs[1]): objects/cube.obj with src/main.rs's scene
-and material graph, 1920x1080 per GPU.  One step = one frame: every rank renders its 1080-row
-tile of a 1920 x (1080*N) frame (camera rays, first-hit triangle scan, shading with shadow rays)
-with the f32 image and the PPM bytes written by the fused kernel.  For N > 1 the job ends with the
-final RCCL gather (xGMI) of the PPM rows to rank 0 inside the timed region (north_star: "a final
-RCCL gather"); --gather-every-frame gathers after every frame instead.  Inputs (mesh, material
+and material graph, 1920x1080 per GPU.  One step = one frame (camera rays, first-hit triangle
+scan, shading with shadow rays) with the f32 image and the PPM bytes written by the fused kernel.
+
+Multi-GPU (row tiles).  Default, weak scaling: N GPUs render a (1920*N) x 1080
+frame — C2 widened at the same pixel pitch (the camera's Fov ratio grows with the width, the
+viewport height and focal length stay main.rs's), so every rank renders 1080/N rows of 1920*N
+pixels, the same 2,073,600 rays per GPU, and N = 1 is exactly C2.  --scaling strong splits one
+fixed --width x --height frame (C4, C5) instead.  For N > 1 the job ends with the final RCCL
+gather (xGMI) of the PPM rows to rank 0 inside the timed region (north_star: "a final RCCL
+gather"); --gather-every-frame gathers after every frame instead.  Inputs (mesh, material
 textures) are resident in HBM before timing; the material graph is evaluated once, as
-Material::update is (reported separately).  Per-GPU work is fixed as N grows (weak scaling).
+Material::update is (reported separately).
 
 Prints ONE JSON line on rank 0 (metric "Mrays/s": primary rays of all ranks / wall time).
 """
@@ -36,13 +41,24 @@ from eray_amd.dist import gather_ppm_rows, row_block  # noqa: E402
 from eray_amd.frame import MainScene  # noqa: E402
 from eray_amd.objfile import load_obj_file  # noqa: E402
 
-WIDTH, HEIGHT_PER_GPU, TEXTURE = 1920, 1080, 1024  # C2 (defaults; --width / --rows-per-gpu)
+WIDTH, HEIGHT, TEXTURE = 1920, 1080, 1024  # C2 (defaults; --width / --height)
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
 def frame_camera_fov(width: int, height: int) -> tuple[float, float]:
-    """Fov giving Camera::size() == (width, height) exactly (Fov(16, 9) for 16:9 frames)."""
-    for fov in ((16.0, 9.0 * height * 16 / (9.0 * width)), (16.0, 9.0), (float(width), float(height))):
+    """Fov giving Camera::size() == (width, height) exactly: Fov(16, 9) for 16:9 frames (SURVEY.md
+    §8), Fov(60, 60) for square ones, otherwise Fov(width, height) with fov1 nudged by a few ulps
+    until (width as f32 / (fov0 / fov1)) as u32 == height."""
+    cands = [(16.0, 9.0), (60.0, 60.0)]
+    f1 = np.float32(height)
+    for _ in range(8):
+        cands += [(float(width), float(f1))]
+        f1 = np.nextafter(f1, np.float32(np.inf))
+    f1 = np.float32(height)
+    for _ in range(8):
+        f1 = np.nextafter(f1, np.float32(0))
+        cands += [(float(width), float(f1))]
+    for fov in cands:
         cam = capi.make_camera((0.0, 0.0, 5.0), fov, width, 1.0)
         if capi.camera_size(cam) == (width, height):
             return fov
@@ -113,8 +129,11 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--mesh", default=os.path.join(ROOT, "objects", "cube.obj"))
-    ap.add_argument("--width", type=int, default=WIDTH, help="frame width (C2: 1920)")
-    ap.add_argument("--rows-per-gpu", type=int, default=HEIGHT_PER_GPU, help="frame rows per GPU (C2: 1080)")
+    ap.add_argument("--width", type=int, default=WIDTH,
+                    help="frame width per GPU (weak) or of the whole frame (strong); C2: 1920")
+    ap.add_argument("--height", type=int, default=HEIGHT, help="frame height (C2: 1080)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="weak: a (width*N) x height frame; strong: one width x height frame split N ways")
     ap.add_argument("--brute-force", action="store_true", help="disable the exact wave culling")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -149,8 +168,11 @@ def main() -> None:
     stream = torch.cuda.Stream()  # one stream shared by the library, torch and RCCL
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
-    width, per_gpu = args.width, args.rows_per_gpu
-    H_total = per_gpu * world
+    width = args.width * world if args.scaling == "weak" else args.width
+    H_total = args.height
+    if H_total % world:
+        raise SystemExit(f"--height {H_total} does not split into {world} equal row tiles")
+    per_gpu = H_total // world
     t_mat0 = time.perf_counter()
     scene = MainScene(ctx, *mesh, width, H_total, texture=TEXTURE, fov=frame_camera_fov(width, H_total))
     torch.cuda.synchronize()
@@ -220,6 +242,9 @@ def main() -> None:
         gather_ms = (time.perf_counter() - g0) * 1e3
 
     if rank == 0:
+        # the configuration profiles/pmc_traffic.json was collected on (C2, or C2 widened for N > 1)
+        is_c2 = (args.width, args.height, args.scaling) == (WIDTH, HEIGHT, "weak") and args.mesh.endswith(
+            "objects/cube.obj") and not args.brute_force
         pixels = width * rows
         ms_per_step = elapsed / args.steps * 1e3
         rays = width * H_total * args.steps
@@ -235,17 +260,18 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 6),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": (f"synthetic scene of src/main.rs around {os.path.relpath(args.mesh, ROOT)}"
                      + (" (the reference's own file)" if args.mesh.endswith("objects/cube.obj") else "")
                      + ", procedural material graph"),
             "config": {
-                "workload": f"{'C2: ' if (width, per_gpu) == (1920, 1080) and args.mesh.endswith('objects/cube.obj') else ''}"
-                            f"{os.path.basename(args.mesh)}, {width}x{per_gpu} per GPU, main.rs scene + material graph; step = "
-                            "one frame (camera rays, first-hit scan, shading + shadow rays, f32 image "
-                            "and PPM bytes); N > 1: row tiles, final RCCL gather of the PPM rows to rank 0",
+                "workload": f"{'C2' + (f' widened x{world}' if world > 1 else '') + ': ' if is_c2 else ''}"
+                            f"{os.path.basename(args.mesh)}, {width}x{H_total} frame, {width}x{per_gpu} rows per GPU, "
+                            "main.rs scene + material graph; step = one frame (camera rays, first-hit scan, "
+                            "shading + shadow rays, f32 image and PPM bytes); N > 1: row tiles, final RCCL "
+                            "gather of the PPM rows to rank 0",
                 "mesh": os.path.relpath(args.mesh, ROOT),
                 "triangles": int(len(mesh[0])),
                 "frame": [width, H_total],
@@ -268,7 +294,7 @@ def main() -> None:
                 "peak": PEAK_HBM_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4),
-                "traffic": pmc_traffic(),
+                "traffic": pmc_traffic() if is_c2 and world == 1 else None,
                 "kernel": "frame_kernel (eray_amd/csrc/render.hip)",
                 "algorithmic_bytes_per_launch": alg,
                 "kernel_ms": round(kernel_ms, 6),

@@ -601,7 +601,9 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     p.out_rgb = rp->out_rgb;
     p.out_ppm = rp->out_ppm;
     p.out_face = rp->out_face;
-    p.aligned = (p.img_w % 16) == 0 &&
+    // 16-byte row stores: 16-byte aligned rows, and byte offsets of the largest output (f32 RGB)
+    // within 32 bits (the kernels store through buffer resources, render.hip stream16)
+    p.aligned = (p.img_w % 16) == 0 && (uint64_t)p.rows * p.img_w * 12u < (1ull << 32) &&
                 ((reinterpret_cast<uintptr_t>(p.out_rgb) | reinterpret_cast<uintptr_t>(p.out_ppm) |
                   reinterpret_cast<uintptr_t>(p.out_face)) & 15) == 0;
     p.tris = ctx->d_hot;

@@ -23,6 +23,7 @@ VARIANTS = {
     "x_neither": ("ERAY_AB_X_NO_SHADOW", "ERAY_AB_X_NO_TEXTURE"),
     "x_nofill": ("ERAY_AB_X_NO_FILL",),
     "x_nodetail": ("ERAY_AB_X_NO_DETAIL",),
+    "st_nt": ("ERAY_AB_STORE_NT",),
 }
 
 CHILD = r"""
