@@ -53,11 +53,14 @@ struct eray_ctx {
     size_t objs_cap = 0;
     LightDesc* d_lights = nullptr;
     size_t lights_cap = 0;
-    // launch plan of eray_render_frames: a HIP graph of kGraphFrames frame launches, cached
-    // for the frame parameters + stream it was captured with
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t graph_exec = nullptr;
-    std::vector<unsigned char> graph_key;
+    // launch plan of eray_render_frames: HIP graphs of back-to-back frame launches — [0] a
+    // chunk of up to kGraphFrames frames, [1] the remainder of the last call's frame count —
+    // each cached for the frame parameters + stream + length it was captured with
+    struct FrameGraph {
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+        std::vector<unsigned char> key;
+    } graphs[2];
     uint32_t* d_rect = nullptr;  // per-object pixel-rectangle accumulators (4 x uint32)
     size_t rect_cap = 0;
     std::vector<uint32_t> h_rect;
@@ -348,8 +351,10 @@ int eray_ctx_destroy(eray_ctx* ctx) {
     void* bufs[] = {ctx->d_hot, ctx->d_shade, ctx->d_cull, ctx->d_raw, ctx->d_objs, ctx->d_lights, ctx->d_rect};
     for (void* b : bufs)
         if (b) hipFree(b);
-    if (ctx->graph_exec) hipGraphExecDestroy(ctx->graph_exec);
-    if (ctx->graph) hipGraphDestroy(ctx->graph);
+    for (auto& g : ctx->graphs) {
+        if (g.exec) hipGraphExecDestroy(g.exec);
+        if (g.graph) hipGraphDestroy(g.graph);
+    }
     if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
     delete ctx;
     return ERAY_OK;
@@ -696,40 +701,50 @@ int eray_render(eray_ctx* ctx, const eray_render_params* rp) {
 namespace {
 constexpr uint32_t kGraphFrames = 64;
 
-// (Re)builds the cached graph of min(frames, kGraphFrames) back-to-back frame launches.
-// Returns the graph's frame count, 0 when the plain launch path must be used.
-int ensure_plan(eray_ctx* ctx, const FrameParams& p, uint32_t frames, uint32_t* chunk) {
-    *chunk = 0;
-    if (!ctx->stream || frames < 2) return ERAY_OK;  // the null stream cannot be captured
-    const uint32_t n = frames < kGraphFrames ? frames : kGraphFrames;
+// (Re)builds graph `slot` of n back-to-back frame launches unless it is cached for (p, n, stream).
+int ensure_graph(eray_ctx* ctx, const FrameParams& p, uint32_t n, int slot) {
+    auto& G = ctx->graphs[slot];
     std::vector<unsigned char> key(sizeof p + sizeof n + sizeof ctx->stream);
     std::memcpy(key.data(), &p, sizeof p);
     std::memcpy(key.data() + sizeof p, &n, sizeof n);
     std::memcpy(key.data() + sizeof p + sizeof n, &ctx->stream, sizeof ctx->stream);
-    if (ctx->graph_exec && key == ctx->graph_key) {
-        *chunk = n;
-        return ERAY_OK;
-    }
-    if (ctx->graph_exec) hipGraphExecDestroy(ctx->graph_exec);
-    if (ctx->graph) hipGraphDestroy(ctx->graph);
-    ctx->graph_exec = nullptr;
-    ctx->graph = nullptr;
-    ctx->graph_key.clear();
+    if (G.exec && key == G.key) return ERAY_OK;
+    if (G.exec) hipGraphExecDestroy(G.exec);
+    if (G.graph) hipGraphDestroy(G.graph);
+    G.exec = nullptr;
+    G.graph = nullptr;
+    G.key.clear();
     HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
     hipError_t e = hipSuccess;
     for (uint32_t f = 0; f < n && e == hipSuccess; ++f) e = launch_render(p, ctx->stream);
     hipGraph_t g = nullptr;
     const hipError_t e2 = hipStreamEndCapture(ctx->stream, &g);
     if (e == hipSuccess) e = e2;
-    if (e == hipSuccess) e = hipGraphInstantiate(&ctx->graph_exec, g, nullptr, nullptr, 0);
+    if (e == hipSuccess) e = hipGraphInstantiate(&G.exec, g, nullptr, nullptr, 0);
     if (e != hipSuccess) {
         if (g) hipGraphDestroy(g);
-        ctx->graph_exec = nullptr;
+        G.exec = nullptr;
         return set_error(ctx, ERAY_E_HIP, "frame graph capture: %s", hipGetErrorString(e));
     }
-    ctx->graph = g;
-    ctx->graph_key = std::move(key);
+    G.graph = g;
+    G.key = std::move(key);
+    return ERAY_OK;
+}
+
+// The launch plan of `frames` frames: graph 0 of `chunk` = min(frames, kGraphFrames) frames,
+// replayed frames / chunk times, and graph 1 of the remainder (no plain launches, whose host
+// cost can exceed a frame's device time).  chunk = 0: plain launches (null stream, 1 frame).
+int ensure_plan(eray_ctx* ctx, const FrameParams& p, uint32_t frames, uint32_t* chunk, uint32_t* rest) {
+    *chunk = *rest = 0;
+    if (!ctx->stream || frames < 2) return ERAY_OK;  // the null stream cannot be captured
+    const uint32_t n = frames < kGraphFrames ? frames : kGraphFrames;
+    if (int st = ensure_graph(ctx, p, n, 0)) return st;
     *chunk = n;
+    const uint32_t r = frames % n;
+    if (r > 1) {
+        if (int st = ensure_graph(ctx, p, r, 1)) return st;
+        *rest = r;
+    }
     return ERAY_OK;
 }
 }  // namespace
@@ -738,8 +753,8 @@ int eray_render_prepare(eray_ctx* ctx, const eray_render_params* rp, uint32_t fr
     FrameParams p;
     bool empty = false;
     if (int st = prepare_render(ctx, rp, &p, &empty)) return st;
-    uint32_t chunk;
-    return empty ? ERAY_OK : ensure_plan(ctx, p, frames, &chunk);
+    uint32_t chunk, rest;
+    return empty ? ERAY_OK : ensure_plan(ctx, p, frames, &chunk, &rest);
 }
 
 int eray_render_frames(eray_ctx* ctx, const eray_render_params* rp, uint32_t frames,
@@ -749,8 +764,8 @@ int eray_render_frames(eray_ctx* ctx, const eray_render_params* rp, uint32_t fra
     if (int st = prepare_render(ctx, rp, &p, &empty)) return st;
     if (mean_frame_ms) *mean_frame_ms = 0.0f;
     if (empty || !frames) return ERAY_OK;
-    uint32_t chunk = 0;
-    if (int st = ensure_plan(ctx, p, frames, &chunk)) return st;
+    uint32_t chunk = 0, rest = 0;
+    if (int st = ensure_plan(ctx, p, frames, &chunk, &rest)) return st;
     hipEvent_t ev[2] = {nullptr, nullptr};
     if (mean_frame_ms) {
         for (auto& e : ev) {
@@ -761,11 +776,15 @@ int eray_render_frames(eray_ctx* ctx, const eray_render_params* rp, uint32_t fra
             }
         }
     }
-    // replay the cached graph (back-to-back frame kernels); plain launches for the remainder
+    // replay the cached graphs (back-to-back frame kernels)
     hipError_t he = mean_frame_ms ? hipEventRecord(ev[0], ctx->stream) : hipSuccess;
     uint32_t done = 0;
     for (; chunk && done + chunk <= frames && he == hipSuccess; done += chunk)
-        he = hipGraphLaunch(ctx->graph_exec, ctx->stream);
+        he = hipGraphLaunch(ctx->graphs[0].exec, ctx->stream);
+    if (rest && done + rest == frames && he == hipSuccess) {
+        he = hipGraphLaunch(ctx->graphs[1].exec, ctx->stream);
+        done += rest;
+    }
     for (; done < frames && he == hipSuccess; ++done) he = launch_frame(ctx, p);
     if (mean_frame_ms && he == hipSuccess) {
         he = hipEventRecord(ev[1], ctx->stream);
