@@ -96,6 +96,30 @@ __global__ void __launch_bounds__(256) bin_start_kernel(const uint32_t* __restri
     for (uint32_t t = lo; t <= hi && t <= nbins; ++t) start[t] = i;
 }
 
+// The pixel rectangle of the non-empty bins (camera pixels), accumulated as tri_rect_kernel's:
+// (~x0, x1 + 1, ~y0, y1 + 1) by atomicMax into zeroed words.
+__global__ void __launch_bounds__(256) bins_rect_kernel(const uint32_t* __restrict__ start, uint32_t bins_x,
+                                                        uint32_t nbins, uint32_t W, uint32_t H, uint32_t phase,
+                                                        uint32_t* __restrict__ acc) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t a[4] = {0u, 0u, 0u, 0u};
+    if (b < nbins && start[b + 1] > start[b]) {
+        const uint32_t bx = b % bins_x, by = b / bins_x;
+        const int32_t y0 = (int32_t)(by * kBinH + phase) - (int32_t)kBinH;
+        const uint32_t x0 = bx * kBinW, x1 = min(x0 + kBinW, W) - 1;
+        const uint32_t r0 = (uint32_t)max(y0, 0), r1 = (uint32_t)min(y0 + (int32_t)kBinH, (int32_t)H) - 1;
+        a[0] = ~x0;
+        a[1] = x1 + 1u;
+        a[2] = ~r0;
+        a[3] = r1 + 1u;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        for (int off = 32; off > 0; off >>= 1) a[k] = max(a[k], (uint32_t)__shfl_xor((int)a[k], off));
+    if ((threadIdx.x & 63) == 0 && a[1])
+        for (int k = 0; k < 4; ++k) atomicMax(acc + k, a[k]);
+}
+
 template <typename T>
 hipError_t grow(T** p, size_t* cap, size_t need) {
     if (*p && *cap >= need) return hipSuccess;
@@ -110,7 +134,84 @@ hipError_t grow(T** p, size_t* cap, size_t need) {
     return e;
 }
 
+// Sub-block s = sy * (4 * tiles_x) + sx (padded rows: a 64 x 4 block's four sub-blocks are four
+// consecutive threads): listed when some object can be hit there (see build_detail_list).
+__global__ void __launch_bounds__(256) detail_flags_kernel(const ObjectDesc* __restrict__ objs, uint32_t nobj,
+                                                           uint32_t cam_w, uint32_t row0, uint32_t rows,
+                                                           uint32_t bins_x, uint32_t phase, uint32_t tiles_x,
+                                                           uint32_t n, uint8_t* __restrict__ flags,
+                                                           uint32_t* __restrict__ packed, uint8_t* __restrict__ occ) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t row_subs = 4 * tiles_x;
+    const uint32_t sx = s % row_subs, sy = s / row_subs;
+    bool hit = false;
+    if (s < n && sx * kBinW < cam_w) {
+        const int32_t x0 = (int32_t)(sx * kBinW), x1 = x0 + (int32_t)kBinW - 1;
+        const int32_t y0 = (int32_t)(row0 + sy * kBinH), y1 = min(y0 + (int32_t)kBinH, (int32_t)(row0 + rows)) - 1;
+        for (uint32_t oi = 0; oi < nobj && !hit; ++oi) {
+            const ObjGeom& g = objs[oi].g;
+            if (!g.tri_count) continue;
+            if (g.bin_start) {  // the frame kernel's bin of this sub-block (first_hit_binned)
+                const uint32_t bin = ((row0 + sy * kBinH + kBinH - phase) / kBinH) * bins_x + sx;
+                hit = g.bin_start[bin + 1] > g.bin_start[bin];
+            } else {
+                hit = x0 <= g.rect[1] && x1 >= g.rect[0] && y0 <= g.rect[3] && y1 >= g.rect[2];
+            }
+        }
+    }
+    if (s < n) {
+        flags[s] = hit ? 1 : 0;
+        packed[s] = (sy << 16) | sx;
+    }
+    // the block's four flags: lanes 4b .. 4b + 3 of the wave (row_subs is a multiple of 4)
+    const unsigned long long bal = __ballot(hit);
+    if (s < n && (threadIdx.x & 3) == 0) occ[s / 4] = (uint8_t)((bal >> (threadIdx.x & 63)) & 0xfu);
+}
+
 }  // namespace
+
+hipError_t build_detail_list(const ObjectDesc* objs, uint32_t nobj, uint32_t cam_w, uint32_t row0, uint32_t rows,
+                             uint32_t bins_x, uint32_t phase, uint32_t tiles_x, uint32_t* list, uint8_t* occ,
+                             uint32_t* count, hipStream_t s) {
+    const uint32_t subs_y = (rows + kBinH - 1) / kBinH;
+    const uint32_t n = 4 * tiles_x * subs_y;
+    *count = 0;
+    if (!n) return hipSuccess;
+    uint8_t* flags = nullptr;
+    uint32_t *packed = nullptr, *d_count = nullptr;
+    void* temp = nullptr;
+    auto done = [&](hipError_t err) {
+        for (void* q : {(void*)flags, (void*)packed, (void*)d_count, temp})
+            if (q) hipFree(q);
+        return err;
+    };
+    hipError_t e;
+    if ((e = hipMalloc((void**)&flags, n)) != hipSuccess) return done(e);
+    if ((e = hipMalloc((void**)&packed, sizeof(uint32_t) * n)) != hipSuccess) return done(e);
+    if ((e = hipMalloc((void**)&d_count, sizeof(uint32_t))) != hipSuccess) return done(e);
+    detail_flags_kernel<<<(n + 255) / 256, 256, 0, s>>>(objs, nobj, cam_w, row0, rows, bins_x, phase, tiles_x, n,
+                                                        flags, packed, occ);
+    if ((e = hipGetLastError()) != hipSuccess) return done(e);
+    size_t temp_bytes = 0;
+    if ((e = hipcub::DeviceSelect::Flagged(nullptr, temp_bytes, packed, flags, list, d_count, (int)n, s)) !=
+        hipSuccess)
+        return done(e);
+    if ((e = hipMalloc(&temp, temp_bytes ? temp_bytes : 1)) != hipSuccess) return done(e);
+    if ((e = hipcub::DeviceSelect::Flagged(temp, temp_bytes, packed, flags, list, d_count, (int)n, s)) != hipSuccess)
+        return done(e);
+    if ((e = hipMemcpyAsync(count, d_count, sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (e = hipStreamSynchronize(s)) != hipSuccess)
+        return done(e);
+    return done(hipSuccess);
+}
+
+hipError_t launch_bins_rect(const uint32_t* start, uint32_t bins_x, uint32_t bins_y, uint32_t W, uint32_t H,
+                            uint32_t phase, uint32_t* acc, hipStream_t s) {
+    const uint32_t nbins = bins_x * bins_y;
+    if (!nbins) return hipSuccess;
+    bins_rect_kernel<<<(nbins + 255) / 256, 256, 0, s>>>(start, bins_x, nbins, W, H, phase, acc);
+    return hipGetLastError();
+}
 
 hipError_t build_bins(const TriCull* cull, const TriHot* hot, uint32_t T, uint32_t W, uint32_t H, uint32_t phase,
                       uint32_t bins_x, uint32_t bins_y, ObjBins* out, hipStream_t s) {

@@ -6,6 +6,7 @@
 // CPU path: without a usable GPU the calls fail loudly.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -62,12 +63,21 @@ struct eray_ctx {
         std::vector<unsigned char> key;
     } graphs[2];
     uint32_t* d_rect = nullptr;  // per-object pixel-rectangle accumulators (4 x uint32)
+    std::vector<int32_t> face_rects;  // per object: the union of its faces' rectangles (4 x int32)
     size_t rect_cap = 0;
     std::vector<uint32_t> h_rect;
     // screen bins of the large objects' faces (bins.hip), per object; valid for bins_phase
     std::vector<ObjBins> bins;
     bool bins_dirty = true;
     uint32_t bins_phase = 0;
+    uint64_t bins_gen = 0;  // bumped whenever the bins (and the rectangles) are rebuilt
+    // detail sub-block list of the last rendered rows (scenes with binned objects)
+    uint32_t* d_detail_list = nullptr;
+    size_t detail_list_cap = 0;
+    uint8_t* d_detail_occ = nullptr;
+    size_t detail_occ_cap = 0;
+    std::vector<uint64_t> detail_key;
+    uint32_t detail_count = 0;
     std::vector<ObjectDesc> h_objs;  // kept alive for the async uploads
     std::vector<LightDesc> h_lights;
     std::vector<float> h_raw;
@@ -266,6 +276,8 @@ int sync_scene(eray_ctx* ctx, bool need_cull) {
                     r[3] = (int32_t)a[3] - 1;
                 }
             }
+            ctx->face_rects.resize(4 * nobj);
+            for (size_t i = 0; i < nobj; ++i) std::memcpy(&ctx->face_rects[4 * i], ctx->h_objs[i].g.rect, 16);
             HIP_TRY(ctx, hipMemcpyAsync(ctx->d_objs, ctx->h_objs.data(), sizeof(ObjectDesc) * nobj,
                                         hipMemcpyHostToDevice, ctx->stream));
         }
@@ -301,10 +313,67 @@ int sync_bins(eray_ctx* ctx, uint32_t phase) {
         g.bin_mask = ctx->bins[i].mask;
         g.bin_hot = ctx->bins[i].hot;
     }
+    // A binned object's pixel rectangle narrows to its non-empty bins: a pixel of an empty bin has
+    // no face whose culling bounds can pass there (bin_pixels), so no primary ray hits the object.
+    // Face rectangles alone can be far too wide (a near-silhouette face's bounds may span the
+    // frame), which would make the frame kernel search empty bins.
+    const size_t nobj = ctx->objects.size();
+    if (int st = ensure(ctx, &ctx->d_rect, &ctx->rect_cap, 4 * nobj)) return st;
+    HIP_TRY(ctx, hipMemsetAsync(ctx->d_rect, 0, sizeof(uint32_t) * 4 * nobj, ctx->stream));
+    for (size_t i = 0; i < nobj; ++i)
+        if (ctx->objects[i].T > kDirectMax)
+            HIP_TRY(ctx, launch_bins_rect(ctx->bins[i].start, bins_x, bins_y, W, H, phase, ctx->d_rect + 4 * i,
+                                          ctx->stream));
+    ctx->h_rect.assign(4 * nobj, 0u);
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_rect.data(), ctx->d_rect, sizeof(uint32_t) * 4 * nobj, hipMemcpyDeviceToHost,
+                                ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (size_t i = 0; i < nobj; ++i) {
+        int32_t* r = ctx->h_objs[i].g.rect;
+        const int32_t* f = &ctx->face_rects[4 * i];
+        if (ctx->objects[i].T <= kDirectMax) {
+            std::memcpy(r, f, 16);
+            continue;
+        }
+        const uint32_t* a = &ctx->h_rect[4 * i];
+        if (a[1] == 0) {  // every bin is empty
+            r[0] = r[2] = 1;
+            r[1] = r[3] = 0;
+            continue;
+        }
+        r[0] = std::max(f[0], (int32_t)~a[0]);
+        r[1] = std::min(f[1], (int32_t)a[1] - 1);
+        r[2] = std::max(f[2], (int32_t)~a[2]);
+        r[3] = std::min(f[3], (int32_t)a[3] - 1);
+    }
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_objs, ctx->h_objs.data(), sizeof(ObjectDesc) * ctx->h_objs.size(),
                                 hipMemcpyHostToDevice, ctx->stream));
     ctx->bins_dirty = false;
     ctx->bins_phase = phase;
+    ++ctx->bins_gen;
+    return ERAY_OK;
+}
+
+// The detail sub-block list of the rendered rows when some object is binned: only sub-blocks
+// where a binned object's bin is non-empty (or a small object's rectangle reaches) get a detail
+// wave; everything else is background.  Rebuilt when the rows or the bins change.
+int sync_detail(eray_ctx* ctx, FrameParams& p) {
+    const uint32_t subs_y = (p.rows + kBinH - 1) / kBinH;
+    const size_t nsub = 4 * (size_t)p.tiles_x * subs_y, nblk = (size_t)p.tiles_x * subs_y;
+    std::vector<uint64_t> key{p.cam_w, p.cam_h, p.row0, p.rows, p.bin_phase, ctx->bins_gen};
+    if (int st = ensure(ctx, &ctx->d_detail_list, &ctx->detail_list_cap, nsub)) return st;
+    if (int st = ensure(ctx, &ctx->d_detail_occ, &ctx->detail_occ_cap, nblk)) return st;
+    if (key != ctx->detail_key) {
+        ctx->detail_key.clear();
+        HIP_TRY(ctx, build_detail_list(ctx->d_objs, (uint32_t)ctx->objects.size(), p.cam_w, p.row0, p.rows, p.bins_x,
+                                       p.bin_phase, p.tiles_x, ctx->d_detail_list, ctx->d_detail_occ,
+                                       &ctx->detail_count, ctx->stream));
+        ctx->detail_key = std::move(key);
+    }
+    p.detail_list = ctx->d_detail_list;
+    p.detail_occ = ctx->d_detail_occ;
+    p.total_sub = ctx->detail_count;
+    p.nrect = 0;
     return ERAY_OK;
 }
 
@@ -348,7 +417,9 @@ int eray_ctx_destroy(eray_ctx* ctx) {
         if (b.mask) hipFree(b.mask);
         if (b.hot) hipFree(b.hot);
     }
-    void* bufs[] = {ctx->d_hot, ctx->d_shade, ctx->d_cull, ctx->d_raw, ctx->d_objs, ctx->d_lights, ctx->d_rect};
+    void* bufs[] = {ctx->d_hot,  ctx->d_shade,         ctx->d_cull,        ctx->d_raw,
+                    ctx->d_objs, ctx->d_lights,        ctx->d_rect,        ctx->d_detail_list,
+                    ctx->d_detail_occ};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (auto& g : ctx->graphs) {
@@ -684,6 +755,10 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     p.bounces = bounces;
     p.seed_lo = (uint32_t)rp->aa_seed;
     p.seed_hi = (uint32_t)(rp->aa_seed >> 32);
+    bool binned = false;
+    for (auto& o : ctx->objects) binned |= o.T > kDirectMax;
+    if (cull && binned)
+        if (int st = sync_detail(ctx, p)) return st;
     return ERAY_OK;
 }
 
@@ -819,3 +894,41 @@ int eray_ppm_header(uint32_t w, uint32_t h, char* buf, size_t cap, size_t* len) 
 }
 
 }  // extern "C"
+
+// Diagnostics (not part of include/eray_hip.h): the screen bins of object `index` as built for
+// the last render — out[0] bins, out[1] entries, out[2] (face, pixel) pairs (mask bits),
+// out[3] most entries in one bin, out[4] non-empty bins, out[5] most pairs in one bin,
+// out[6..9] the object's pixel rectangle (x0, x1, y0, y1; int32 as uint64).
+extern "C" int eray_debug_bin_stats(eray_ctx* ctx, uint32_t index, uint64_t* out) {
+    if (!ctx || !out || index >= ctx->bins.size() || !ctx->bins[index].start) return ERAY_E_INVALID_ARGUMENT;
+    const ObjBins& b = ctx->bins[index];
+    uint32_t W, H;
+    eray_camera_size(&ctx->camera, &W, &H);
+    const uint32_t bins_x = (W + kBinW - 1) / kBinW;
+    const uint32_t bins_y = H ? (H - 1 + kBinH - ctx->bins_phase) / kBinH + 1 : 1;
+    const size_t nb = (size_t)bins_x * bins_y;
+    std::vector<uint32_t> start(nb + 1);
+    std::vector<unsigned long long> mask(b.n);
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess ||
+        hipMemcpy(start.data(), b.start, start.size() * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+        (b.n && hipMemcpy(mask.data(), b.mask, b.n * 8, hipMemcpyDeviceToHost) != hipSuccess))
+        return set_error(ctx, ERAY_E_HIP, "bin stats copy failed");
+    uint64_t pairs = 0, most = 0, nonempty = 0, most_pairs = 0;
+    for (size_t i = 0; i < nb; ++i) {
+        const uint64_t e = start[i + 1] - start[i];
+        most = e > most ? e : most;
+        nonempty += e != 0;
+        uint64_t pb = 0;
+        for (uint32_t j = start[i]; j < start[i + 1]; ++j) pb += (uint64_t)__builtin_popcountll(mask[j]);
+        pairs += pb;
+        most_pairs = pb > most_pairs ? pb : most_pairs;
+    }
+    out[0] = nb;
+    out[1] = b.n;
+    out[2] = pairs;
+    out[3] = most;
+    out[4] = nonempty;
+    out[5] = most_pairs;
+    for (int k = 0; k < 4; ++k) out[6 + k] = (uint64_t)(int64_t)ctx->h_objs[index].g.rect[k];
+    return ERAY_OK;
+}

@@ -65,10 +65,13 @@ __device__ inline bool face_rect(const TriCull& c, uint32_t W, uint32_t H, int32
 
 // Where condition k of a culling record can pass along a camera row, in pixels: from
 // K + A xf + B yf >= -T (the culling bound at the pixel's own f32 viewport coordinates), solved
-// for xf in double: x >= c0 - c1 yf (A > 0) or x <= c0 - c1 yf (A < 0), widened by a pixel (the
-// f32 xf = x/W is within 2^-24 of x/W; the double solve within ~1e-15 of a pixel).  A condition
-// nearly independent of x is decided per row from its x-free part (kind 3); a disabled one
-// (T = +inf) does not narrow the interval (kind 0).
+// for xf in double: x >= c0 - c1 yf (A > 0) or x <= c0 - c1 yf (A < 0), widened by `tol` pixels:
+// the f32 xf = x/W is within a relative 2^-24 of x/W (at most W * 2^-24 < 1e-3 pixel for any
+// W < 16.7M) and the double solve is within ~1e-15 (|c0| + |c1|) pixels, so 1e-3 + 1e-12 (|c0| +
+// |c1|) contains every pixel whose bound can pass, without the whole-pixel widening that would
+// add false (face, pixel) pairs around every small face.  A condition nearly independent of x is
+// decided per row from its x-free part (kind 3); a disabled one (T = +inf) does not narrow the
+// interval (kind 0).
 struct CondLine {
     double c0, c1, tol;
     int kind;  // 0 none, 1 lower bound x >= c0 - c1 yf, 2 upper bound, 3 flat: fails if c0 - c1 yf > tol
@@ -88,6 +91,7 @@ __device__ inline CondLine cond_line(float A, float B, float K, float T, uint32_
     const double inv = (double)W / (double)A;
     l.c0 = -((double)K + (double)T) * inv;
     l.c1 = (double)B * inv;
+    l.tol = 1e-3 + 1e-12 * (fabs(l.c0) + fabs(l.c1));
     l.kind = A > 0.0f ? 1 : 2;
     return l;
 }
@@ -100,10 +104,10 @@ __device__ inline void apply_line(const CondLine& l, double yf, int32_t& xl, int
             xr = 0;
         }
     } else if (l.kind == 1) {
-        const double lo = floor(q) - 1.0;
+        const double lo = ceil(q - l.tol);
         if (lo > (double)xl) xl = lo > 2e9 ? 2000000000 : (int32_t)lo;
     } else {
-        const double hi = ceil(q) + 1.0;
+        const double hi = floor(q + l.tol);
         if (hi < (double)xr) xr = hi < -2e9 ? -2000000000 : (int32_t)hi;
     }
 }

@@ -116,6 +116,12 @@ struct FrameParams {
     uint32_t tiles_x;    // 64 x 4 pixel blocks per row
     uint32_t bins_x;     // screen bins per row
     uint32_t bin_phase;  // bins start at camera rows bin_phase + k * kBinH (row0 % kBinH)
+    // Detail sub-block list (scenes with binned objects, built by build_detail_list): the j-th
+    // detail sub-block is detail_list[j] = sy << 16 | sx (sub-block units, rank-local rows) and
+    // bit i of detail_occ[block] marks sub-block i of 64 x 4 block `block` as listed.  Null: the
+    // detail sub-blocks are those of the rectangles above.
+    const uint32_t* detail_list;
+    const uint8_t* detail_occ;
     // general tracer (trace.hip): anti-aliasing rays per pixel, reflection depth, jitter seed;
     // aa == 0 && bounces == 0 selects the frame kernel
     uint32_t aa, bounces;
@@ -163,6 +169,18 @@ struct ObjBins {  // device arrays of one object's bins (owned by the context)
 // bins of kBinW x kBinH pixels starting at camera row phase - kBinH.  Synchronises `s`.
 hipError_t build_bins(const TriCull* cull, const TriHot* hot, uint32_t T, uint32_t W, uint32_t H, uint32_t phase, uint32_t bins_x,
                       uint32_t bins_y, ObjBins* out, hipStream_t s);
+// The pixel rectangle (camera pixels) of the non-empty bins of `start` (bins_x x bins_y bins of
+// build_bins' layout), accumulated like launch_tri_rect into 4 zeroed words.
+hipError_t launch_bins_rect(const uint32_t* start, uint32_t bins_x, uint32_t bins_y, uint32_t W, uint32_t H,
+                            uint32_t phase, uint32_t* acc, hipStream_t s);
+// The detail sub-blocks of rank-local rows [row0, row0 + rows) of a cam_w-wide frame: those
+// where some binned object's bin is non-empty or some other object's pixel rectangle reaches
+// (objs: the device descriptors).  Writes the compacted list (sy << 16 | sx, in raster order) and
+// the per-block occupancy bytes (see FrameParams::detail_list); *count receives the list length
+// (the call synchronises s).
+hipError_t build_detail_list(const ObjectDesc* objs, uint32_t nobj, uint32_t cam_w, uint32_t row0, uint32_t rows,
+                             uint32_t bins_x, uint32_t phase, uint32_t tiles_x, uint32_t* list, uint8_t* occ,
+                             uint32_t* count, hipStream_t s);
 hipError_t launch_pack_ppm(const float* rgb, uint32_t w, uint32_t h, uint8_t* out, hipStream_t s);
 
 hipError_t launch_wave(uint32_t w, uint32_t h, float xf, float yf, float* out, hipStream_t s);

@@ -76,7 +76,7 @@ __device__ __forceinline__ T load_const(const T* base, size_t i) {
 // boundaries.  Stamps go to LDS (no vector-memory counter the kernel's own waits would include)
 // and are copied out when the wave ends (ERAY_TRACE_FLUSH).
 #ifdef ERAY_PHASE_TRACE
-constexpr int kTraceSlots = 16;
+constexpr int kTraceSlots = 24;
 __device__ uint64_t g_trace[2 * 64 * 4 * kTraceSlots];  // [realtime | shader clock]
 __shared__ uint64_t s_trace[4][kTraceSlots][2];
 #define ERAY_TRACE_ON() ((threadIdx.x & 63) == 0 && blockIdx.x % 16 == 0 && blockIdx.x < 1024)
@@ -729,7 +729,9 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
     constexpr uint32_t kWaves = kWG / 64;
     BinLds& L = *reinterpret_cast<BinLds*>(s_bins + wave * kBinLdsBytes);
     uint32_t* s_range = reinterpret_cast<uint32_t*>(s_bins + kWaves * kBinLdsBytes);  // [lo, hi] per wave
+    ERAY_TRACE(16);
     uint32_t lo = load_const(ob.bin_start, bin), hi = load_const(ob.bin_start, bin + 1);
+    ERAY_TRACE_VAL(23, hi - lo);
     if (lo != hi && __any(st == kUndecided)) {  // every pixel's ray and bbox verdict, up front
         const bool a = activate();
         if (st == kUndecided) st = a ? kSearching : kDone;
@@ -744,6 +746,7 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
         s_range[2 * wave + 1] = hi;
     }
     __syncthreads();
+    ERAY_TRACE(17);
     uint32_t chunks[kWaves], total = 0;
 #pragma unroll
     for (uint32_t w = 0; w < kWaves; ++w) {
@@ -771,6 +774,9 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // wide candidates (many pixels): the whole wave tests them, each lane its own pixel
         unsigned long long wide = __ballot(cnt > kWide);
+#ifdef ERAY_AB_X_NO_WIDE  // diagnostics only (wrong images)
+        wide = 0;
+#endif
         while (wide) {
             const uint32_t s = (uint32_t)(__ffsll(wide) - 1);
             wide &= wide - 1;
@@ -803,6 +809,9 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#ifdef ERAY_AB_X_NO_PAIRS  // diagnostics only (wrong images): compaction without the tests
+        if (p.nobj != 12345) continue;
+#endif
         for (uint32_t q = 0; q < npairs; q += 64) {
             if (q + lane < npairs) {
                 const uint32_t pr = L.pairs[q + lane];
@@ -819,7 +828,9 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
         __builtin_amdgcn_wave_barrier();  // L.cand / L.pairs are rewritten by the next chunk
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    ERAY_TRACE(18);
     __syncthreads();  // every chunk of every sub-block is done
+    ERAY_TRACE(19);
     const uint32_t mine = L.best[lane];
     if (st == kSearching && mine != 0xffffffffu) {
         float u, v, t;
@@ -1167,11 +1178,13 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
                         if (!test_candidates(mask, face, hot, st, S, sd, f, u, v, t)) break;
                     }
                 } else {
+                    ERAY_TRACE(20);
                     shadow_ray();
                     int st = (have && !decided && bbox_hit(ob, S, sd)) ? kSearching : kDone;
                     auto never = []() { return false; };
                     first_hit<false, kLdsTiles>(p, sc, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot, s_cull,
                                                 never, f, u, v, t);
+                    ERAY_TRACE(21);
                 }
                 ERAY_TRACE(15);
                 if (f >= 0) {
@@ -1320,6 +1333,12 @@ __global__ void __launch_bounds__(kWG, (kLdsTiles || (kMat & kMatSpecPow)) ? 1 :
 #endif
         // detail sub-block j (enumeration order) -> sub-block coordinates
         auto locate = [&](uint32_t j, int32_t& sx, int32_t& sy) {
+            if (p.detail_list) {
+                const uint32_t e = p.detail_list[j];
+                sx = (int32_t)(e & 0xffffu);
+                sy = (int32_t)(e >> 16);
+                return;
+            }
             for (uint32_t k = 0; k < p.nrect; ++k) {  // the rectangles are disjoint (host): by area
                 const SubRect r = frame_rect(p, k);
                 const uint32_t w = (uint32_t)(r.sx1 - r.sx0 + 1);
@@ -1395,7 +1414,8 @@ __global__ void __launch_bounds__(kWG, (kLdsTiles || (kMat & kMatSpecPow)) ? 1 :
     for (uint32_t blk = wave * nf + f; blk < nblk; blk += nf * nwaves) {
         const uint32_t bx = blk % p.tiles_x, by = blk / p.tiles_x;
         uint32_t mask = 0;  // detail sub-blocks of this block
-        for (uint32_t k = 0; k < p.nrect; ++k) {
+        if (p.detail_occ) mask = p.detail_occ[blk];
+        for (uint32_t k = 0; k < p.nrect && !p.detail_occ; ++k) {
             const SubRect r = frame_rect(p, k);
             if ((int32_t)by < r.sy0 || (int32_t)by > r.sy1) continue;
 #pragma unroll

@@ -24,6 +24,9 @@ VARIANTS = {
     "x_nofill": ("ERAY_AB_X_NO_FILL",),
     "x_nodetail": ("ERAY_AB_X_NO_DETAIL",),
     "st_nt": ("ERAY_AB_STORE_NT",),
+    "x_nowide": ("ERAY_AB_X_NO_WIDE",),
+    "x_nopairs": ("ERAY_AB_X_NO_PAIRS",),
+    "x_nobinwork": ("ERAY_AB_X_NO_WIDE", "ERAY_AB_X_NO_PAIRS"),
 }
 
 CHILD = r"""
@@ -33,13 +36,14 @@ import numpy as np, torch
 from eray_amd import capi
 from eray_amd.frame import MainScene
 from eray_amd.objfile import load_obj_file
-W, H = 1920, 1080
-mesh = load_obj_file(os.path.join(os.environ["ROOT"], "objects", "cube.obj"))
+W, H = int(os.environ.get("ERAY_AB_W", 1920)), int(os.environ.get("ERAY_AB_H", 1080))
+mesh = load_obj_file(os.environ.get("ERAY_AB_MESH") or os.path.join(os.environ["ROOT"], "objects", "cube.obj"))
 ctx = capi.Context(0)
 rgb = ctx.empty((H, W, 3), np.float32); ppm = ctx.empty((H, W, 3), np.uint8)
-sc = MainScene(ctx, *mesh, W, H)
+from bench import frame_camera_fov
+sc = MainScene(ctx, *mesh, W, H, fov=frame_camera_fov(W, H))
 out = []
-for row0, rows in ((0, H), (538, 4)):
+for row0, rows in ((0, H), (H // 2 - 2, 4)):
     kw = dict(row0=row0, rows=rows, out_rgb=rgb.ptr, out_ppm=ppm.ptr)
     ctx.render_frames(64, W, H, prepare_only=True, **kw)
     ctx.render_frames(64, W, H, **kw); ctx.synchronize()

@@ -19,22 +19,24 @@ from eray_amd import capi  # noqa: E402
 from eray_amd.frame import MainScene  # noqa: E402
 from eray_amd.objfile import load_obj_file  # noqa: E402
 
-W, H = 1920, 1080
+W, H = int(os.environ.get("ERAY_TRACE_W", 1920)), int(os.environ.get("ERAY_TRACE_H", 1080))
 rows = int(sys.argv[1]) if len(sys.argv) > 1 else H
 row0 = (H - rows) // 2
 mesh = load_obj_file(sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "objects", "cube.obj"))
 ctx = capi.Context(0)
 rgb = ctx.empty((H, W, 3), np.float32)
 ppm = ctx.empty((H, W, 3), np.uint8)
-sc = MainScene(ctx, *mesh, W, H)
+from bench import frame_camera_fov  # noqa: E402
+sc = MainScene(ctx, *mesh, W, H, fov=frame_camera_fov(W, H))
 for _ in range(30):
     ctx.render(W, H, row0=row0, rows=rows, out_rgb=rgb.ptr, out_ppm=ppm.ptr)
 ctx.synchronize()
 lib = capi.lib()
-buf = (C.c_uint64 * (2 * 64 * 4 * 16))()
+NS = 24
+buf = (C.c_uint64 * (2 * 64 * 4 * NS))()
 lib.eray_debug_trace.argtypes = [C.c_void_p, C.c_size_t]
 assert lib.eray_debug_trace(buf, len(buf)) == 0
-tt = np.frombuffer(buf, dtype=np.uint64).reshape(2, 64, 4, 16).astype(np.int64)
+tt = np.frombuffer(buf, dtype=np.uint64).reshape(2, 64, 4, NS).astype(np.int64)
 t, clk = tt[0], tt[1]
 sel = (t[:, :, 0] > 0) & (t[:, :, 8] > 0)
 if sel.any():
@@ -45,10 +47,10 @@ if sel.any():
     ghz = ((clk[:, :, 7] - clk[:, :, 1])[sel] / ((t[:, :, 7] - t[:, :, 1])[sel] * 10.0)).mean()
     print(f"shader clock (detail waves) ~ {ghz:.2f} GHz")
 t0 = t[:, :, 0][t[:, :, 0] > 0].min()
-names = {0: "entry", 13: "issued", 12: "stored", 1: "caches", 9: "geom", 10: "cull", 11: "ray", 14: "bbox", 2: "primary", 3: "material", 15: "shadow", 4: "light", 5: "out",
+names = {16: "bin_in", 17: "bin_sync", 18: "bin_loop", 19: "bin_out", 20: "sh_in", 21: "sh_out", 0: "entry", 13: "issued", 12: "stored", 1: "caches", 9: "geom", 10: "cull", 11: "ray", 14: "bbox", 2: "primary", 3: "material", 15: "shadow", 4: "light", 5: "out",
          6: "repeat", 7: "detail", 8: "end"}
 print(f"rows {row0}..{row0 + rows}; ticks of 10 ns from the first entry")
-order = [0, 13, 12, 1, 9, 10, 14, 2, 3, 15, 4, 5, 7]
+order = [0, 13, 12, 1, 16, 14, 17, 18, 19, 2, 3, 20, 21, 15, 4, 5, 7]
 print("  wg.w " + " ".join(f"{names[k]:>8s}" for k in order))
 for g in range(64):
     for w in range(4):
@@ -56,8 +58,7 @@ for g in range(64):
         if row[0] == 0:
             continue
         print(f"{16 * g:4d}.{w} " + " ".join(f"{(row[k] - t0) if row[k] else -1:8d}" for k in order)
-              + f"   heavy bin: list {row[9]:6d} pairs {row[10]:6d} chunks {row[11]:4d} "
-              f"scan {(row[13] - row[12]) if row[12] else -1:6d}")
+              + f"   bin entries {row[23]:5d}")
 print("shader cycles from each detail wave's entry (s_memtime)")
 print("  wg.w " + " ".join(f"{names[k]:>8s}" for k in order))
 for g in range(64):

@@ -348,6 +348,48 @@ def test_c3_full_size_rows_match_oracle(gpu, oracle, standin70k):
     sc.close()
 
 
+def test_binned_and_small_objects_row_tiles(gpu, oracle, cube):
+    """A binned object (8k faces, general bounding box) beside small ones (the cube, a random
+    mesh), rendered whole and in row tiles of every row phase: the detail sub-block list (non-empty
+    bins + the small objects' rectangles) and its occupancy bitmap for the fill must give the
+    brute-force frame bit for bit, and the oracle's on the tiles."""
+    v, n, t, fv, ft, fn = meshgen.displaced_sphere(8000, 3)
+    big = (np.ascontiguousarray(v[fv].reshape(-1, 9)) * np.float32(0.6) + np.float32([-0.9, 0.3, 0.0] * 3),
+           np.ascontiguousarray(n[fn].reshape(-1, 9)), np.ascontiguousarray(t[ft].reshape(-1, 6)))
+    rng = np.random.default_rng(5)
+    small = random_mesh(rng, 40, scale=0.3, center=(0.9, -0.4, 0.5))
+    W, H = 320, 180
+    cam_center = (0.1, -0.05, 4.0)
+    gpu.scene_reset()
+    gpu.set_camera(capi.make_camera(cam_center, (16.0, 9.0), W, 1.0))
+    s = oracle.Scene()
+    tex = rng.uniform(0, 1, (16, 16, 3)).astype(np.float32)
+    dt = gpu.to_device(tex)
+    cube_s = (cube[0] * np.float32(0.4) + np.float32([0.8, 0.5, -0.5] * 3), cube[1], cube[2])
+    for pos, nrm, uv in (big, cube_s, small):
+        lo, hi = pos.reshape(-1, 3).min(0), pos.reshape(-1, 3).max(0)
+        gpu.add_object(pos, nrm, uv, tuple(lo), tuple(hi), color=dt.image())
+        s.add_object(pos, nrm, uv, tuple(lo), tuple(hi), color=tex)
+    for p, var, col, b in (((0.0, 2.0, 0.0), "ambient", (1.0, 1.0, 1.0), 0.2),
+                           ((1.0, 1.0, 2.0), "point", (1.0, 1.0, 1.0), 1.0)):
+        gpu.add_light(capi.make_light(p, var, col, b))
+        s.add_light(p, var, col, b)
+    full, full_face, _ = gpu_render(gpu, W, H)
+    brute, brute_face, _ = gpu_render(gpu, W, H, flags=capi.RENDER_BRUTE_FORCE)
+    assert (full_face >= 0).sum() > 800
+    assert np.array_equal(full_face, brute_face)
+    assert_bit_equal(full, brute, "binned + small vs brute force")
+    ocam = oracle.camera(cam_center, (16.0, 9.0), W, 1.0)
+    for row0, rows in ((0, 45), (45, 46), (91, 43), (134, 46), (61, 7)):
+        part, part_face, _ = gpu_render(gpu, W, H, row0=row0, rows=rows, ppm=False)
+        assert np.array_equal(part_face, full_face[row0:row0 + rows])
+        assert_bit_equal(part, full[row0:row0 + rows], f"tile {row0}+{rows}")
+    ref, ref_face, _ = oracle.render(s, ocam, row0=85, rows=12, want_faces=True)
+    assert np.array_equal(full_face[85:97], ref_face)
+    assert_bit_equal(full[85:97], ref, "binned + small vs oracle")
+    dt.free()
+
+
 def test_example_material_errors(gpu, cube):
     sc = MainScene(gpu, *cube, 64, 64, texture=16)
     with pytest.raises(capi.ErayError) as e:
