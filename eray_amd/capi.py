@@ -69,6 +69,27 @@ class Object(C.Structure):
                 ("bbox_max", C.c_float * 3), ("material", Material)]
 
 
+TEXEL_WAVE, TEXEL_RGB, TEXEL_FLAT_COLOR, TEXEL_MIX_COLOR = 0, 1, 2, 3
+
+
+class TexelNode(C.Structure):  # eray_texel_node
+    _fields_ = [("kind", C.c_uint32), ("width", C.c_uint32), ("height", C.c_uint32),
+                ("param", C.c_float * 3), ("input", C.c_int32 * 3)]
+
+
+class TexelGraph(C.Structure):  # eray_texel_graph
+    _fields_ = [("nodes", C.POINTER(TexelNode)), ("count", C.c_uint32), ("color", C.c_int32),
+                ("diffuse", C.c_int32), ("specular", C.c_int32), ("specular_power", C.c_int32),
+                ("reflection", C.c_int32)]
+
+
+def texel_node(kind, width, height, param=(0.0, 0.0, 0.0), inputs=(-1, -1, -1)) -> TexelNode:
+    """One shaderlib node of a per-texel material graph (eray_texel_node)."""
+    p = list(param) + [0.0] * (3 - len(param))
+    q = list(inputs) + [-1] * (3 - len(inputs))
+    return TexelNode(kind, width, height, (C.c_float * 3)(*p), (C.c_int32 * 3)(*q))
+
+
 class ExampleMaterial(C.Structure):  # eray_material_example_params
     _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("x_fac", C.c_float), ("y_fac", C.c_float),
                 ("r", C.c_float), ("g", C.c_float), ("b", C.c_float), ("factor", C.c_float)]
@@ -107,6 +128,7 @@ SIGNATURES = {
     "eray_scene_set_camera": (C.c_int, [_P, C.POINTER(Camera)]),
     "eray_scene_add_light": (C.c_int, [_P, C.POINTER(Light)]),
     "eray_scene_set_object_example_material": (C.c_int, [_P, _U, C.POINTER(ExampleMaterial)]),
+    "eray_scene_set_object_texel_graph": (C.c_int, [_P, _U, C.POINTER(TexelGraph)]),
     "eray_scene_add_object": (C.c_int, [_P, C.POINTER(Object), C.POINTER(_U)]),
     "eray_camera_size": (C.c_int, [C.POINTER(Camera), C.POINTER(_U), C.POINTER(_U)]),
     "eray_render": (C.c_int, [_P, C.POINTER(RenderParams)]),
@@ -304,6 +326,17 @@ class Context:
     def set_object_example_material(self, index, width, height, x_fac, y_fac, r, g, b, factor) -> None:
         m = ExampleMaterial(width, height, x_fac, y_fac, r, g, b, factor)
         self._check(lib().eray_scene_set_object_example_material(self._h, index, C.byref(m)))
+
+    def set_object_texel_graph(self, index, nodes, color=-1, diffuse=-1, specular=-1, specular_power=-1,
+                               reflection=-1) -> None:
+        """Material outputs of object `index` from a shaderlib graph evaluated per hit texel;
+        nodes=None removes it."""
+        if nodes is None:
+            self._check(lib().eray_scene_set_object_texel_graph(self._h, index, None))
+            return
+        arr = (TexelNode * max(1, len(nodes)))(*nodes)
+        g = TexelGraph(arr, len(nodes), color, diffuse, specular, specular_power, reflection)
+        self._check(lib().eray_scene_set_object_texel_graph(self._h, index, C.byref(g)))
 
     def add_object(self, positions, normals, uvs, bbox_min=(0.0, 0.0, 0.0), bbox_max=(0.0, 0.0, 0.0),
                    color: Image | None = None, diffuse: Image | None = None,

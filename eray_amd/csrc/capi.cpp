@@ -30,7 +30,45 @@ struct HostObject {
     eray_material mat{};
     bool example = false;  // color + diffuse from main.rs's graph at the hit texel
     eray_material_example_params ex{};
+    std::vector<eray_texel_node> tnodes;  // a shader graph per hit texel (texel_graph)
+    int32_t tout[5] = {-1, -1, -1, -1, -1};
 };
+
+// Node types of the shaderlib outputs: wave's is IValue, rgb / flat_color / mix_color's IColor.
+bool texel_is_color(uint32_t kind) { return kind != ERAY_TEXEL_WAVE; }
+
+// Expands node `idx` of `nodes` (evaluated at a texel derived from instruction `parent` by
+// `xform`) into pre-order instructions; indices are relative to `first`.
+uint32_t texel_emit(const std::vector<eray_texel_node>& nodes, uint32_t idx, uint32_t parent, uint32_t xform,
+                    size_t first, std::vector<TexelInstr>& ins) {
+    const eray_texel_node& nd = nodes[idx];
+    const uint32_t k = (uint32_t)(ins.size() - first);
+    TexelInstr t{};
+    t.kind = nd.kind;
+    t.w = nd.width;
+    t.h = nd.height;
+    t.parent = parent;
+    t.xform = xform;
+    for (int j = 0; j < 3; ++j) t.p[j] = nd.param[j];
+    ins.push_back(t);
+    if (ins.size() - first > kTexelMaxNodes) return k;  // the caller reports the size
+    if (nd.kind == ERAY_TEXEL_RGB) {
+        uint32_t c[3];
+        for (int j = 0; j < 3; ++j) {
+            int same = -1;  // rgb's inputs at the same node read the same pixel index: share
+            for (int q = 0; q < j; ++q)
+                if (nd.input[q] == nd.input[j]) same = q;
+            c[j] = same >= 0 ? c[same] : texel_emit(nodes, (uint32_t)nd.input[j], k, kTexelIndex, first, ins);
+        }
+        for (int j = 0; j < 3; ++j) ins[first + k].c[j] = c[j];
+    } else if (nd.kind == ERAY_TEXEL_MIX_COLOR) {
+        const uint32_t l = texel_emit(nodes, (uint32_t)nd.input[0], k, kTexelMod, first, ins);
+        const uint32_t r = texel_emit(nodes, (uint32_t)nd.input[1], k, kTexelMod, first, ins);
+        ins[first + k].c[0] = l;
+        ins[first + k].c[1] = r;
+    }
+    return k;
+}
 }  // namespace
 
 struct eray_ctx {
@@ -78,6 +116,9 @@ struct eray_ctx {
     size_t detail_occ_cap = 0;
     std::vector<uint64_t> detail_key;
     uint32_t detail_count = 0;
+    uint32_t* d_prog = nullptr;  // every object's texel program (MaterialDesc::prog), concatenated
+    size_t prog_cap = 0;
+    std::vector<uint32_t> h_prog;
     std::vector<ObjectDesc> h_objs;  // kept alive for the async uploads
     std::vector<LightDesc> h_lights;
     std::vector<float> h_raw;
@@ -189,7 +230,37 @@ int sync_scene(eray_ctx* ctx, bool need_cull) {
         uint32_t begin = 0;
         ctx->spec_pow = false;
         ctx->example_mat = false;
-        for (auto& o : ctx->objects) {
+        // texel programs: per object a header + its outputs' expression trees (48-B records)
+        ctx->h_prog.clear();
+        std::vector<size_t> prog_at(ctx->objects.size(), SIZE_MAX);
+        for (size_t i = 0; i < ctx->objects.size(); ++i) {
+            const HostObject& o = ctx->objects[i];
+            if (o.tnodes.empty()) continue;
+            std::vector<TexelInstr> ins;
+            uint32_t head[kTexelHeaderWords] = {};
+            for (int out = 0; out < 5; ++out) {
+                const int32_t idx = o.tout[out];
+                if (idx < 0 || texel_is_color(o.tnodes[idx].kind) != (out == 0)) continue;  // kept / None
+                const size_t first = ins.size();
+                texel_emit(o.tnodes, (uint32_t)idx, 0, kTexelMod, first, ins);
+                if (ins.size() - first > kTexelMaxNodes)
+                    return set_error(ctx, ERAY_E_UNSUPPORTED, "object %zu: output %d expands to more than %u texel nodes",
+                                     i, out, kTexelMaxNodes);
+                head[out] = (uint32_t)first;
+                head[5 + out] = (uint32_t)(ins.size() - first);
+            }
+            prog_at[i] = ctx->h_prog.size();
+            ctx->h_prog.insert(ctx->h_prog.end(), head, head + kTexelHeaderWords);
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(ins.data());
+            ctx->h_prog.insert(ctx->h_prog.end(), w, w + ins.size() * (sizeof(TexelInstr) / 4));
+        }
+        if (!ctx->h_prog.empty()) {
+            if ((st = ensure(ctx, &ctx->d_prog, &ctx->prog_cap, ctx->h_prog.size()))) return st;
+            HIP_TRY(ctx, hipMemcpyAsync(ctx->d_prog, ctx->h_prog.data(), 4 * ctx->h_prog.size(), hipMemcpyHostToDevice,
+                                        ctx->stream));
+        }
+        for (size_t i = 0; i < ctx->objects.size(); ++i) {
+            const HostObject& o = ctx->objects[i];
             ObjectDesc d{};
             d.g.tri_begin = begin;
             d.g.tri_count = o.T;
@@ -214,8 +285,17 @@ int sync_scene(eray_ctx* ctx, bool need_cull) {
                 d.mat.ex_b = o.ex.b;
                 d.mat.ex_factor = o.ex.factor;
             }
+            if (prog_at[i] != SIZE_MAX) {  // graph outputs replace the textures (None: defaults)
+                d.mat.prog = ctx->d_prog + prog_at[i];
+                TexView* tv[5] = {&d.mat.color, &d.mat.diffuse, &d.mat.specular, &d.mat.specular_power,
+                                  &d.mat.reflection};
+                for (int out = 0; out < 5; ++out)
+                    if (o.tout[out] >= 0) *tv[out] = TexView{nullptr, 0, 0};
+                ctx->example_mat = true;
+                if (o.tout[3] >= 0 && !texel_is_color(o.tnodes[o.tout[3]].kind)) ctx->spec_pow = true;
+            }
             ctx->h_objs.push_back(d);
-            ctx->spec_pow |= o.mat.specular_power.data != nullptr;
+            ctx->spec_pow |= d.mat.specular_power.data != nullptr;
             ctx->example_mat |= d.mat.example != 0;
             begin += o.T;
         }
@@ -419,7 +499,7 @@ int eray_ctx_destroy(eray_ctx* ctx) {
     }
     void* bufs[] = {ctx->d_hot,  ctx->d_shade,         ctx->d_cull,        ctx->d_raw,
                     ctx->d_objs, ctx->d_lights,        ctx->d_rect,        ctx->d_detail_list,
-                    ctx->d_detail_occ};
+                    ctx->d_detail_occ, ctx->d_prog};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (auto& g : ctx->graphs) {
@@ -587,6 +667,50 @@ int eray_scene_set_object_example_material(eray_ctx* ctx, uint32_t index, const 
     return ERAY_OK;
 }
 
+int eray_scene_set_object_texel_graph(eray_ctx* ctx, uint32_t index, const eray_texel_graph* g) {
+    if (!ctx) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "null context");
+    if (index >= ctx->objects.size())
+        return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "object %u out of range (%zu objects)", index,
+                         ctx->objects.size());
+    HostObject& o = ctx->objects[index];
+    if (!g) {
+        o.tnodes.clear();
+        std::fill(o.tout, o.tout + 5, -1);
+        ctx->desc_dirty = true;
+        return ERAY_OK;
+    }
+    if (g->count && !g->nodes) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "nodes is null");
+    for (uint32_t i = 0; i < g->count; ++i) {
+        const eray_texel_node& n = g->nodes[i];
+        if (n.kind > ERAY_TEXEL_MIX_COLOR) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "node %u: kind %u", i, n.kind);
+        // every image a Material::get lookup can reach is indexed by mod_get or by pixel index:
+        // a zero-sized one panics there (image.rs:36-38)
+        if (!n.width || !n.height)
+            return set_error(ctx, ERAY_E_OUT_OF_BOUNDS, "node %u: zero width or height", i);
+        const int inputs = n.kind == ERAY_TEXEL_RGB ? 3 : n.kind == ERAY_TEXEL_MIX_COLOR ? 2 : 0;
+        for (int j = 0; j < inputs; ++j) {
+            const int32_t in = n.input[j];
+            if (in < 0 || (uint32_t)in >= i)  // unconnected (MissingMany) or not an earlier node
+                return set_error(ctx, ERAY_E_MISSING_MANY, "node %u: input %d is not an earlier node", i, j);
+            const eray_texel_node& src = g->nodes[in];
+            // rgb takes IValue images, mix_color IColor ones (get_sv!, shader.rs:140-178)
+            if (texel_is_color(src.kind) != (n.kind == ERAY_TEXEL_MIX_COLOR))
+                return set_error(ctx, ERAY_E_INVALID_TYPE, "node %u: input %d has the wrong image type", i, j);
+            // rgb reads pixels[y * width + x] of each input (rgb.rs:89-95): it panics past the end
+            if (n.kind == ERAY_TEXEL_RGB && (uint64_t)src.width * src.height < (uint64_t)n.width * n.height)
+                return set_error(ctx, ERAY_E_OUT_OF_BOUNDS, "node %u: input %d has fewer pixels than the node", i, j);
+        }
+    }
+    const int32_t outs[5] = {g->color, g->diffuse, g->specular, g->specular_power, g->reflection};
+    for (int k = 0; k < 5; ++k)
+        if (outs[k] < -1 || outs[k] >= (int32_t)g->count)
+            return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "output %d: node %d out of range", k, outs[k]);
+    o.tnodes.assign(g->nodes, g->nodes + g->count);
+    std::copy(outs, outs + 5, o.tout);
+    ctx->desc_dirty = true;
+    return ERAY_OK;
+}
+
 int eray_scene_add_object(eray_ctx* ctx, const eray_object* obj, uint32_t* index) {
     if (!ctx || !obj) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "null argument");
     const uint32_t T = obj->triangle_count;
@@ -633,7 +757,10 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     // anti-aliasing and reflection bounces take the general tracer (trace.hip); bounces only
     // matter when some material has a reflection output (engine.rs:181-182)
     bool reflective = false;
-    for (auto& o : ctx->objects) reflective |= o.mat.reflection.data != nullptr;
+    for (auto& o : ctx->objects) {
+        const int32_t r = o.tout[4];  // a graph output replaces the texture (None if mistyped)
+        reflective |= r >= 0 ? !texel_is_color(o.tnodes[r].kind) : o.mat.reflection.data != nullptr;
+    }
     const uint32_t bounces = reflective ? rp->bounces : 0u;
     if (bounces > kMaxBounces)
         return set_error(ctx, ERAY_E_UNSUPPORTED, "bounces = %u: at most %u reflection levels", rp->bounces,

@@ -4,6 +4,7 @@
 #pragma once
 
 #include "device_math.hpp"
+#include "glibc_cosf.hpp"
 #include "internal.hpp"
 
 namespace eray {
@@ -64,6 +65,60 @@ __device__ __forceinline__ const float* texel(const TexView& tv, float x, float 
     const uint32_t ix = mod_size(sat_u32(x * (float)tv.w), tv.w);
     const uint32_t iy = mod_size(sat_u32(y * (float)tv.h), tv.h);
     return tv.data + comps * ((size_t)iy * tv.w + ix);
+}
+
+// Material output `out` (0 color .. 4 reflection) of a texel program (MaterialDesc::prog) at uv:
+// the value Material::get would read from the texture Graph::run makes (material.rs:56-94).
+// Returns false when the output is not a program output.  First the texel of every tree node,
+// top-down (the root's is Material::get's mod_get texel), then the values, bottom-up:
+//   wave  |cos((x as f32 * x_fac + y as f32 * y_fac) / 10)|     (wave.rs:127)
+//   rgb   (red[i], green[i], blue[i]) at the node's own index  (rgb.rs:89-95)
+//   flat  (r, g, b)                                            (flat_color.rs:88)
+//   mix   l * (1 - factor) + r * factor per channel            (mix_color.rs:85-91)
+__device__ __noinline__ bool texel_program(const uint32_t* prog, uint32_t out, float u, float v, float (&val)[3]) {
+    const uint32_t first = prog[out], n = prog[5 + out];
+    if (!n) return false;
+    const TexelInstr* ins = reinterpret_cast<const TexelInstr*>(prog + kTexelHeaderWords) + first;
+    uint32_t cx[kTexelMaxNodes], cy[kTexelMaxNodes];
+    float vr[kTexelMaxNodes], vg[kTexelMaxNodes], vb[kTexelMaxNodes];
+    cx[0] = mod_size(sat_u32(u * (float)ins[0].w), ins[0].w);
+    cy[0] = mod_size(sat_u32(v * (float)ins[0].h), ins[0].h);
+    for (uint32_t k = 1; k < n; ++k) {
+        const TexelInstr& t = ins[k];
+        const uint32_t q = t.parent;
+        if (t.xform == kTexelMod) {
+            cx[k] = cx[q] % t.w;
+            cy[k] = cy[q] % t.h;
+        } else {
+            const uint64_t i = (uint64_t)cy[q] * ins[q].w + cx[q];
+            cx[k] = (uint32_t)(i % t.w);
+            cy[k] = (uint32_t)(i / t.w);
+        }
+    }
+    for (uint32_t k = n; k-- > 0;) {
+        const TexelInstr& t = ins[k];
+        if (t.kind == 0) {  // wave
+            vr[k] = __builtin_fabsf(libm::cosf_glibc(((float)cx[k] * t.p[0] + (float)cy[k] * t.p[1]) / 10.0f));
+        } else if (t.kind == 1) {  // rgb
+            vr[k] = vr[t.c[0]];
+            vg[k] = vr[t.c[1]];
+            vb[k] = vr[t.c[2]];
+        } else if (t.kind == 2) {  // flat_color
+            vr[k] = t.p[0];
+            vg[k] = t.p[1];
+            vb[k] = t.p[2];
+        } else {  // mix_color
+            const float f = t.p[0];
+            const uint32_t l = t.c[0], r = t.c[1];
+            vr[k] = vr[l] * (1.0f - f) + vr[r] * f;
+            vg[k] = vg[l] * (1.0f - f) + vg[r] * f;
+            vb[k] = vb[l] * (1.0f - f) + vb[r] * f;
+        }
+    }
+    val[0] = vr[0];
+    val[1] = vg[0];
+    val[2] = vb[0];
+    return true;
 }
 }  // namespace
 }  // namespace gpu

@@ -38,12 +38,35 @@ struct TexView {
     uint32_t w, h;
 };
 
+// One node of a material output's expression tree, evaluated per hit texel (hit.hpp
+// texel_program): the host expands the shader graph (eray_texel_graph) per output into a tree in
+// pre-order — a node shared along different paths is evaluated at each path's texel — where
+// every node's texel derives from its parent's.
+struct TexelInstr {  // 48 B
+    uint32_t kind;    // eray_texel_node_kind
+    uint32_t w, h;    // the node's image size
+    uint32_t parent;  // instruction index of the parent (0: the root itself)
+    uint32_t xform;   // kTexelMod: parent texel mod (w, h) (mix's mod_get); kTexelIndex: the
+                      // parent's pixel index y * w_parent + x as (i % w, i / w) (rgb's pixels[i])
+    float p[3];
+    uint32_t c[3];    // children (later instructions; rgb's identical inputs share one)
+    uint32_t pad;
+};
+constexpr uint32_t kTexelMod = 0, kTexelIndex = 1;
+constexpr uint32_t kTexelMaxNodes = 32;  // per output tree
+// Program header (uint32 words): first instruction and count per Material output (color,
+// diffuse, specular, specular_power, reflection), count 0 = not a program output; then the
+// instructions from word kTexelHeaderWords (48-B records).
+constexpr uint32_t kTexelHeaderWords = 12;
+
 struct MaterialDesc {
     TexView color;  // IColor, 3 floats per texel
     TexView diffuse, specular, specular_power, reflection;  // IValue
     // example: 1 = color and diffuse are main.rs's graph evaluated at the hit texel
     uint32_t example, ex_w, ex_h;
     float ex_xf, ex_yf, ex_r, ex_g, ex_b, ex_factor;
+    // a shader graph per hit texel (eray_scene_set_object_texel_graph), or null
+    const uint32_t* prog;
 };
 
 // Scenes up to these sizes are preloaded whole into each frame workgroup's LDS.

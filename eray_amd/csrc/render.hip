@@ -1080,6 +1080,13 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
                         wv * omf + mat.ex_b * mat.ex_factor};
             kd = wv;
         }
+        if (kExample && mat.prog) {  // a shader graph at the texel (its outputs have no texture)
+            float t3[3];
+            if (texel_program(mat.prog, 0, uv0, uv1, t3)) color = rgb{t3[0], t3[1], t3[2]};
+            if (texel_program(mat.prog, 1, uv0, uv1, t3)) kd = t3[0];
+            if (texel_program(mat.prog, 2, uv0, uv1, t3)) ks = t3[0];
+            if (kSpecPow && texel_program(mat.prog, 3, uv0, uv1, t3)) sp = t3[0];
+        }
         tc = texel(mat.color, uv0, uv1, 3);
         tkd = texel(mat.diffuse, uv0, uv1, 1);
         tks = texel(mat.specular, uv0, uv1, 1);

@@ -140,6 +140,14 @@ __device__ bool surface(const FrameParams& p, f3 o, f3 d, Level& L, int32_t* fac
                       wv * omf + mat.ex_b * mat.ex_factor};
         L.kd = wv;
     }
+    if (mat.prog) {  // a shader graph at the texel (its outputs have no texture)
+        float t3[3];
+        if (texel_program(mat.prog, 0, uv0, uv1, t3)) L.color = rgb{t3[0], t3[1], t3[2]};
+        if (texel_program(mat.prog, 1, uv0, uv1, t3)) L.kd = t3[0];
+        if (texel_program(mat.prog, 2, uv0, uv1, t3)) L.ks = t3[0];
+        if (texel_program(mat.prog, 3, uv0, uv1, t3)) L.sp = t3[0];
+        if (texel_program(mat.prog, 4, uv0, uv1, t3)) L.refl = t3[0];
+    }
     if (const float* c = texel(mat.color, uv0, uv1, 3)) L.color = rgb{c[0], c[1], c[2]};
     if (const float* c = texel(mat.diffuse, uv0, uv1, 1)) L.kd = *c;
     if (const float* c = texel(mat.specular, uv0, uv1, 1)) L.ks = *c;

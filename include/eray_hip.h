@@ -18,6 +18,9 @@
  *                           all four nodes fused into one pass)
  *   eray_scene_*            lib/scene.rs:39-54 (add_object / add_light / set_camera) and
  *                           lib/object.rs:213-230 (Object::build -> device triangle arrays);
+ *                           eray_scene_set_object_texel_graph: lib/material.rs:35-94 +
+ *                           lib/shader/graph.rs:499-609 (Material::update's Graph::run over the
+ *                           shaderlib nodes, evaluated at the texel Material::get reads);
  *                           eray_scene_set_object_example_material: lib/material.rs:56-94
  *                           (Material::get) over main.rs:80-144's graph, per hit texel
  *   eray_render             lib/engine.rs:46-81 (Engine::render: camera rays, first-hit
@@ -172,6 +175,37 @@ typedef struct eray_material_example_params {
     float factor;                   /* mix_color input */
 } eray_material_example_params;
 
+/* A material shader graph of the four shaderlib nodes, evaluated at the hit texel instead of
+ * sampled from the textures Graph::run would produce (graph.rs:499-609, material.rs:35-94).
+ * Material::get reads texel ((u*W) as u32 % W, (v*H) as u32 % H) of an output's W x H image; a
+ * node's value at a texel depends only on its inputs' values at texels its own formula picks —
+ * mix_color's mod_get (mix_color.rs:85-91: the input's (x % w, y % h)), rgb's pixel index
+ * (rgb.rs:89-95: pixels[y * W + x] of each input), wave's (x, y) (wave.rs:127) — so evaluating
+ * the graph at that one texel is bit-identical to the texture path, with no image at all.     */
+typedef enum eray_texel_node_kind {
+    ERAY_TEXEL_WAVE = 0,            /* IValue; param = x_fac, y_fac (wave.rs:100-137)          */
+    ERAY_TEXEL_RGB = 1,             /* IColor; input = red, green, blue (IValue nodes)         */
+    ERAY_TEXEL_FLAT_COLOR = 2,      /* IColor; param = r, g, b (flat_color.rs:65-95)           */
+    ERAY_TEXEL_MIX_COLOR = 3        /* IColor; input = left, right (IColor nodes), param[0] =
+                                       factor (default 0.5 is the caller's: mix_color.rs:83)   */
+} eray_texel_node_kind;
+
+typedef struct eray_texel_node {
+    uint32_t kind;                  /* eray_texel_node_kind */
+    uint32_t width, height;         /* the node's width / height inputs (as u32)               */
+    float param[3];
+    int32_t input[3];               /* indices of EARLIER nodes of the array (a DAG in order)   */
+} eray_texel_node;
+
+typedef struct eray_texel_graph {
+    const eray_texel_node* nodes;
+    uint32_t count;
+    /* node index of each Material output, or -1 to keep the object's texture / default; an
+     * output whose node has the wrong type reads as None (Material::get, material.rs:61-88:
+     * the default then applies, as in the reference) */
+    int32_t color, diffuse, specular, specular_power, reflection;
+} eray_texel_graph;
+
 int eray_scene_reset(eray_ctx* ctx);
 int eray_scene_set_camera(eray_ctx* ctx, const eray_camera* camera);
 int eray_scene_add_light(eray_ctx* ctx, const eray_light* light);
@@ -181,6 +215,13 @@ int eray_scene_add_object(eray_ctx* ctx, const eray_object* object, uint32_t* ob
  * eray_material_example_params); its other outputs stay as given. */
 int eray_scene_set_object_example_material(eray_ctx* ctx, uint32_t object_index,
                                            const eray_material_example_params* params);
+/* The object's material outputs named by `graph` become that graph evaluated per hit texel
+ * (see eray_texel_graph); the others stay as given.  Errors: a node input that is not an
+ * earlier node or has the wrong type (shader::Error::InvalidType), a zero-sized mix input
+ * (`% 0`) or an rgb input with fewer pixels than the rgb image (rgb.rs indexes past the end:
+ * ERAY_E_OUT_OF_BOUNDS), more than 32 nodes in one output's expansion (ERAY_E_UNSUPPORTED).
+ * graph == NULL removes a previous graph. */
+int eray_scene_set_object_texel_graph(eray_ctx* ctx, uint32_t object_index, const eray_texel_graph* graph);
 /* Camera::size(): (width, (width as f32 / (fov0/fov1)) as u32) */
 int eray_camera_size(const eray_camera* camera, uint32_t* width, uint32_t* height);
 

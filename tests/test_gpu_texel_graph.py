@@ -1,0 +1,249 @@
+"""GPU parity of per-texel shader graphs (eray_scene_set_object_texel_graph):
+a material graph of the four shaderlib nodes evaluated at the hit texel must render exactly what
+the texture path renders — Graph::run's images (here the oracle's node functions, and the GPU's
+own node kernels) sampled by Material::get (material.rs:56-94).
+
+Bar: bit-identical f32 RGB and faces (powf with a specular-power output: RGB_TOL, the device
+evaluates pow in double).
+"""
+import numpy as np
+import pytest
+
+from eray_amd import capi
+from eray_amd.frame import fov_for
+from tests.helpers import RGB_TOL, assert_bit_equal, random_mesh
+
+pytestmark = pytest.mark.gpu
+
+W, H = 192, 108
+
+
+def random_graph(rng, n_nodes=7):
+    """A random DAG of shaderlib nodes with assorted sizes (mix inputs of other sizes wrap by
+    mod_get; rgb inputs are at least the rgb node's pixel count)."""
+    nodes = []  # (kind, w, h, param, inputs)
+    for i in range(n_nodes):
+        waves = [j for j, n in enumerate(nodes) if n[0] == capi.TEXEL_WAVE]
+        colors = [j for j, n in enumerate(nodes) if n[0] != capi.TEXEL_WAVE]
+        choices = [capi.TEXEL_WAVE, capi.TEXEL_FLAT_COLOR]
+        if waves:
+            choices.append(capi.TEXEL_RGB)
+        if len(colors) >= 1:
+            choices.append(capi.TEXEL_MIX_COLOR)
+        kind = int(rng.choice(choices)) if i >= 2 else [capi.TEXEL_WAVE, capi.TEXEL_FLAT_COLOR][i]
+        w, h = int(rng.integers(3, 40)), int(rng.integers(3, 40))
+        if kind == capi.TEXEL_WAVE:
+            nodes.append((kind, w, h, (float(rng.uniform(-3, 3)), float(rng.uniform(-3, 3))), ()))
+        elif kind == capi.TEXEL_FLAT_COLOR:
+            nodes.append((kind, w, h, tuple(float(x) for x in rng.uniform(0, 1.2, 3)), ()))
+        elif kind == capi.TEXEL_RGB:
+            ins = [int(rng.choice(waves)) for _ in range(3)]
+            if rng.uniform() < 0.3:
+                ins = [ins[0]] * 3
+            # rgb indexes its inputs' pixel vectors with its own index: they must be no smaller
+            w = min(w, min(nodes[j][1] for j in ins))
+            h = min(h, min(nodes[j][1] * nodes[j][2] for j in ins) // w)
+            nodes.append((kind, w, max(h, 1), (), tuple(ins)))
+        else:
+            l, r = int(rng.choice(colors)), int(rng.choice(colors))
+            nodes.append((kind, w, h, (float(rng.uniform(-0.2, 1.2)),), (l, r)))
+    return nodes
+
+
+def oracle_images(oracle, nodes):
+    """Graph::run: every node's image, by the oracle's node functions."""
+    img = []
+    for kind, w, h, param, ins in nodes:
+        if kind == capi.TEXEL_WAVE:
+            img.append(oracle.node_wave(w, h, param[0], param[1]))
+        elif kind == capi.TEXEL_FLAT_COLOR:
+            img.append(oracle.node_flat_color(w, h, param[0], param[1], param[2]))
+        elif kind == capi.TEXEL_RGB:
+            img.append(oracle.node_rgb(w, h, img[ins[0]], img[ins[1]], img[ins[2]]))
+        else:
+            img.append(oracle.node_mix_color(w, h, img[ins[0]], img[ins[1]], param[0]))
+    return img
+
+
+def to_texel_nodes(nodes):
+    return [capi.texel_node(k, w, h, p, ins) for k, w, h, p, ins in nodes]
+
+
+def scene_with(gpu, oracle, mesh, material_gpu, material_oracle, lights, texel=None, cam_center=(0.0, 0.0, 5.0)):
+    gpu.scene_reset()
+    gpu.set_camera(capi.make_camera(cam_center, fov_for(W, H), W, 1.0))
+    lo, hi = (0.0, 0.0, 0.0), (0.0, 0.0, 0.0)
+    gpu.add_object(*mesh, lo, hi, **material_gpu)
+    if texel is not None:
+        gpu.set_object_texel_graph(0, texel[0], **texel[1])
+    s = oracle.Scene()
+    s.add_object(*mesh, lo, hi, **material_oracle)
+    for p, var, col, b in lights:
+        gpu.add_light(capi.make_light(p, var, col, b))
+        s.add_light(p, var, col, b)
+    return s, oracle.camera(cam_center, fov_for(W, H), W, 1.0)
+
+
+LIGHTS = [((0.0, 2.0, 0.0), "ambient", (1.0, 0.9, 0.8), 0.2), ((1.0, 1.0, 2.0), "point", (1.0, 1.0, 1.0), 1.0)]
+
+
+def render(gpu, bounces=0):
+    rgb = gpu.empty((H, W, 3), np.float32)
+    face = gpu.empty((H, W), np.int32)
+    gpu.render(W, H, out_rgb=rgb.ptr, out_face=face.ptr, bounces=bounces)
+    out = rgb.numpy(), face.numpy()
+    rgb.free()
+    face.free()
+    return out
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_random_graph_matches_textures(gpu, oracle, cube, seed):
+    rng = np.random.default_rng(seed)
+    nodes = random_graph(rng)
+    imgs = oracle_images(oracle, nodes)
+    colors = [j for j, n in enumerate(nodes) if n[0] != capi.TEXEL_WAVE]
+    waves = [j for j, n in enumerate(nodes) if n[0] == capi.TEXEL_WAVE]
+    out = dict(color=colors[-1], diffuse=waves[-1], specular=waves[0])
+    s, cam = scene_with(gpu, oracle, cube, {}, {"color": imgs[out["color"]], "diffuse": imgs[out["diffuse"]],
+                                                "specular": imgs[out["specular"]]},
+                        LIGHTS, texel=(to_texel_nodes(nodes), out))
+    got, got_face = render(gpu)
+    ref, ref_face, _ = oracle.render(s, cam, want_faces=True)
+    assert (got_face >= 0).sum() > 400
+    assert np.array_equal(got_face, ref_face)
+    assert_bit_equal(got, ref, f"graph seed {seed}")
+
+
+def test_graph_equals_gpu_texture_path(gpu, cube):
+    """The same graph through the GPU node kernels (Material::update's textures) and per texel."""
+    rng = np.random.default_rng(9)
+    nodes = random_graph(rng, 8)
+    dev = []
+    for kind, w, h, param, ins in nodes:
+        if kind == capi.TEXEL_WAVE:
+            a = gpu.empty((h, w), np.float32)
+            gpu.node_wave(w, h, param[0], param[1], a.ptr)
+        else:
+            a = gpu.empty((h, w, 3), np.float32)
+            if kind == capi.TEXEL_FLAT_COLOR:
+                gpu.node_flat_color(w, h, *param, a.ptr)
+            elif kind == capi.TEXEL_RGB:
+                gpu.node_rgb(w, h, dev[ins[0]].image(), dev[ins[1]].image(), dev[ins[2]].image(), a.ptr)
+            else:
+                gpu.node_mix_color(w, h, dev[ins[0]].image(), dev[ins[1]].image(), param[0], a.ptr)
+        dev.append(a)
+    colors = [j for j, n in enumerate(nodes) if n[0] != capi.TEXEL_WAVE]
+    waves = [j for j, n in enumerate(nodes) if n[0] == capi.TEXEL_WAVE]
+    gpu.scene_reset()
+    gpu.set_camera(capi.make_camera((0.2, 0.1, 4.5), fov_for(W, H), W, 1.0))
+    gpu.add_object(*cube, color=dev[colors[-1]].image(), diffuse=dev[waves[-1]].image())
+    for p, var, col, b in LIGHTS:
+        gpu.add_light(capi.make_light(p, var, col, b))
+    a, fa = render(gpu)
+    gpu.set_object_texel_graph(0, to_texel_nodes(nodes), color=colors[-1], diffuse=waves[-1])
+    b, fb = render(gpu)
+    gpu.set_object_texel_graph(0, None)
+    c, _ = render(gpu)
+    for x in dev:
+        x.free()
+    assert np.array_equal(fa, fb)
+    assert_bit_equal(a, b, "texture path vs texel graph")
+    assert_bit_equal(a, c, "graph removed")
+
+
+def test_main_rs_graph_as_texel_graph(gpu, oracle, cube):
+    """main.rs:80-144 written as a texel graph equals the fused example material and the oracle."""
+    T = 64
+    nodes = [capi.texel_node(capi.TEXEL_WAVE, T, T, (1.0, 1.0)),
+             capi.texel_node(capi.TEXEL_RGB, T, T, (), (0, 0, 0)),
+             capi.texel_node(capi.TEXEL_FLAT_COLOR, T, T, (1.0, 0.0, 0.0)),
+             capi.texel_node(capi.TEXEL_MIX_COLOR, T, T, (0.5,), (1, 2))]
+    color, diffuse = oracle.example_material(T, T)
+    s, cam = scene_with(gpu, oracle, cube, {}, {"color": color, "diffuse": diffuse}, LIGHTS,
+                        texel=(nodes, dict(color=3, diffuse=0)))
+    a, fa = render(gpu)
+    gpu.set_object_texel_graph(0, None)
+    gpu.set_object_example_material(0, T, T, 1.0, 1.0, 1.0, 0.0, 0.0, 0.5)
+    b, _ = render(gpu)
+    ref, ref_face, _ = oracle.render(s, cam, want_faces=True)
+    assert np.array_equal(fa, ref_face)
+    assert_bit_equal(a, ref, "main.rs graph per texel")
+    assert_bit_equal(b, ref, "example material")
+
+
+def test_mistyped_output_reads_as_none(gpu, oracle, cube):
+    """Material::get counts only an IColor color and IValue scalars (material.rs:61-88): a wave as
+    the colour output, or a colour node as diffuse, is None and the default applies."""
+    nodes = [capi.texel_node(capi.TEXEL_WAVE, 8, 8, (0.7, 0.2)),
+             capi.texel_node(capi.TEXEL_FLAT_COLOR, 8, 8, (0.3, 0.6, 0.9))]
+    s, cam = scene_with(gpu, oracle, cube, {}, {}, LIGHTS, texel=(nodes, dict(color=0, diffuse=1)))
+    got, _ = render(gpu)
+    ref, _ = oracle.render(s, cam)
+    assert_bit_equal(got, ref, "None outputs")
+
+
+def test_reflection_and_specular_power_outputs(gpu, oracle):
+    """Graph outputs for specular power (powf not the identity: tolerance) and reflection (the
+    general tracer's bounces)."""
+    rng = np.random.default_rng(17)
+    a = random_mesh(rng, 60, scale=0.8, center=(-0.3, 0.0, 0.0))
+    b = random_mesh(rng, 60, scale=0.8, center=(0.4, 0.2, -0.3))
+    nodes = [capi.texel_node(capi.TEXEL_WAVE, 16, 8, (0.3, 0.9)),
+             capi.texel_node(capi.TEXEL_WAVE, 5, 7, (2.0, -1.0)),
+             capi.texel_node(capi.TEXEL_FLAT_COLOR, 3, 3, (0.8, 0.4, 0.1)),
+             capi.texel_node(capi.TEXEL_RGB, 4, 5, (), (0, 1, 0)),
+             capi.texel_node(capi.TEXEL_MIX_COLOR, 9, 4, (0.25,), (3, 2))]
+    imgs = oracle_images(oracle, [(n.kind, n.width, n.height, tuple(n.param), tuple(n.input)) for n in nodes])
+    gpu.scene_reset()
+    cam_center = (0.1, 0.2, 4.0)
+    gpu.set_camera(capi.make_camera(cam_center, fov_for(W, H), W, 1.0))
+    s = oracle.Scene()
+    for mesh in (a, b):
+        lo, hi = mesh[0].reshape(-1, 3).min(0), mesh[0].reshape(-1, 3).max(0)
+        idx = gpu.add_object(*mesh, tuple(lo), tuple(hi))
+        gpu.set_object_texel_graph(idx, nodes, color=4, diffuse=0, specular_power=1, reflection=0)
+        s.add_object(*mesh, tuple(lo), tuple(hi), color=imgs[4], diffuse=imgs[0], specular_power=imgs[1],
+                     reflection=imgs[0])
+    for p, var, col, bb in LIGHTS:
+        gpu.add_light(capi.make_light(p, var, col, bb))
+        s.add_light(p, var, col, bb)
+    cam = oracle.camera(cam_center, fov_for(W, H), W, 1.0)
+    for bounces in (0, 2):
+        got, face = render(gpu, bounces=bounces)
+        ref, ref_face, _ = oracle.render(s, cam, want_faces=True, bounces=bounces)
+        assert np.array_equal(face, ref_face)
+        np.testing.assert_allclose(got, ref, rtol=0, atol=RGB_TOL, err_msg=f"bounces={bounces}")
+
+
+def test_texel_graph_errors(gpu, cube):
+    gpu.scene_reset()
+    gpu.set_camera(capi.make_camera((0.0, 0.0, 5.0), (60.0, 60.0), W, 1.0))
+    gpu.add_object(*cube)
+    wave = capi.texel_node(capi.TEXEL_WAVE, 4, 4, (1.0, 1.0))
+    flat = capi.texel_node(capi.TEXEL_FLAT_COLOR, 4, 4, (1.0, 0.0, 0.0))
+    cases = [
+        ([wave, capi.texel_node(capi.TEXEL_RGB, 4, 4, (), (0, 0, 1))], capi.E_MISSING_MANY),   # not earlier
+        ([flat, capi.texel_node(capi.TEXEL_RGB, 4, 4, (), (0, 0, 0))], capi.E_INVALID_TYPE),   # IColor into rgb
+        ([wave, capi.texel_node(capi.TEXEL_MIX_COLOR, 4, 4, (0.5,), (0, 0))], capi.E_INVALID_TYPE),
+        ([wave, capi.texel_node(capi.TEXEL_RGB, 8, 4, (), (0, 0, 0))], capi.E_OUT_OF_BOUNDS),  # rgb past the end
+        ([capi.texel_node(capi.TEXEL_WAVE, 0, 4, (1.0, 1.0))], capi.E_OUT_OF_BOUNDS),          # mod_get by 0
+    ]
+    for nodes, code in cases:
+        with pytest.raises(capi.ErayError) as e:
+            gpu.set_object_texel_graph(0, nodes, color=len(nodes) - 1)
+        assert e.value.status == code, nodes
+    with pytest.raises(capi.ErayError) as e:
+        gpu.set_object_texel_graph(0, [wave], color=3)
+    assert e.value.status == capi.E_INVALID_ARGUMENT
+    # a mix chain whose expansion exceeds 32 nodes (each level doubles) is reported at render
+    chain = [flat]
+    for i in range(6):
+        chain.append(capi.texel_node(capi.TEXEL_MIX_COLOR, 4, 4, (0.5,), (i, i)))
+    gpu.set_object_texel_graph(0, chain, color=len(chain) - 1)
+    out = gpu.empty((W, W, 3), np.float32)
+    with pytest.raises(capi.ErayError) as e:
+        gpu.render(W, W, out_rgb=out.ptr, rows=1)
+    assert e.value.status == capi.E_UNSUPPORTED
+    gpu.set_object_texel_graph(0, None)
+    out.free()
