@@ -145,6 +145,7 @@ struct FrameParams {
     // detail sub-blocks are those of the rectangles above.
     const uint32_t* detail_list;
     const uint8_t* detail_occ;
+    uint32_t detail_wgs;  // most workgroups of the frame kernel's grid doing detail work (0: all)
     // general tracer (trace.hip): anti-aliasing rays per pixel, reflection depth, jitter seed;
     // aa == 0 && bounces == 0 selects the frame kernel
     uint32_t aa, bounces;

@@ -1327,9 +1327,12 @@ __global__ void __launch_bounds__(kWG, (kLdsTiles || (kMat & kMatSpecPow)) ? 1 :
     const bool aligned = p.aligned != 0;  // (a kernel-argument read where it is used)
     const uint32_t total = hot.total_sub;  // detail sub-blocks
     const uint32_t grid = hot.grid;        // == gridDim.x, without the implicit-argument load
-    // workgroups [0, nd) render the detail sub-blocks, the others write the background; when
-    // every workgroup has detail work, all of them fill afterwards
-    const uint32_t nd = min(grid, (total + nwaves - 1) / nwaves);
+    // workgroups [0, nd) render the detail sub-blocks (persistent: rounds of nd * 4 sub-blocks),
+    // the others write the background at the same time; at most p.detail_wgs detail workgroups
+    // (the launcher keeps a share of the grid for the fill, so a large detail area overlaps the
+    // fill's HBM writes instead of preceding them); when every workgroup has detail work, all of
+    // them fill afterwards
+    const uint32_t nd = min(p.detail_wgs ? p.detail_wgs : grid, (total + nwaves - 1) / nwaves);
     ERAY_TRACE_CLEAR();
     ERAY_TRACE(0);
 
@@ -1377,7 +1380,7 @@ __global__ void __launch_bounds__(kWG, (kLdsTiles || (kMat & kMatSpecPow)) ? 1 :
         };
 #endif
         auto detail = [&](const auto& sc) {
-            for (uint32_t c = c0; c < total; c += grid * nwaves) {  // workgroup-uniform
+            for (uint32_t c = c0; c < total; c += nd * nwaves) {  // workgroup-uniform
                 const uint32_t j = c + wave;
                 const bool active = j < total;
                 int32_t sx = sx0, sy = sy0;
@@ -1418,10 +1421,29 @@ __global__ void __launch_bounds__(kWG, (kLdsTiles || (kMat & kMatSpecPow)) ? 1 :
     const uint32_t nf = nd < grid ? grid - nd : grid;  // filling workgroups
     const uint32_t f = nd < grid ? blockIdx.x - nd : blockIdx.x;
     const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
-    for (uint32_t blk = wave * nf + f; blk < nblk; blk += nf * nwaves) {
-        const uint32_t bx = blk % p.tiles_x, by = blk / p.tiles_x;
+    const uint32_t fstride = nf * nwaves;
+    uint32_t occ = 0;  // detail list: lane i holds the occupancy of this wave's i-th next block
+    uint32_t it = 0;
+    // block coordinates advance incrementally (no integer division per block)
+    const uint32_t first = wave * nf + f, step_y = fstride / p.tiles_x, step_x = fstride - step_y * p.tiles_x;
+    uint32_t by = first / p.tiles_x, bx = first - by * p.tiles_x;
+    for (uint32_t blk = first; blk < nblk; blk += fstride, ++it) {
+        if (it) {
+            bx += step_x;
+            by += step_y;
+            if (bx >= p.tiles_x) {
+                bx -= p.tiles_x;
+                ++by;
+            }
+        }
         uint32_t mask = 0;  // detail sub-blocks of this block
-        if (p.detail_occ) mask = p.detail_occ[blk];
+        if (p.detail_occ) {  // one load per 64 blocks, not a dependent load per block
+            if ((it & 63u) == 0) {
+                const uint32_t b = blk + lane * fstride;
+                occ = b < nblk ? p.detail_occ[b] : 0u;
+            }
+            mask = (uint32_t)__builtin_amdgcn_readlane((int)occ, (int)(it & 63u));
+        }
         for (uint32_t k = 0; k < p.nrect && !p.detail_occ; ++k) {
             const SubRect r = frame_rect(p, k);
             if ((int32_t)by < r.sy0 || (int32_t)by > r.sy1) continue;
@@ -1511,8 +1533,19 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
     }();
     const int wg_cu = cap > 0 && cap < per_cu ? cap : per_cu;
     const uint32_t grid = min(want, (uint32_t)(wg_cu * cus));
-    frame_kernel<C, L, M, K><<<grid, kWG, dyn, s>>>(p.objects, p.lights, p.cull, p.tris, p.shade,
-                                                    p.nobj | (p.nlights << 16), p.total_tris, p.total_sub, grid, p);
+    // Workgroups kept for the fill so that it overlaps a large detail area instead of following
+    // it: one per 64 background blocks, at most 1/share of the grid (fill waves are issue-bound
+    // below ~1000 per frame: at 3840x2160 / 70k, 128 fill workgroups took 52 us, 256 took 31 us,
+    // none 34 us).  Tuning knob ERAY_FILL_SHARE (diagnostics; 0 = no reservation).
+    static const uint32_t share = [] {
+        const char* e = getenv("ERAY_FILL_SHARE");
+        return e ? (uint32_t)atoi(e) : 2u;
+    }();
+    const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
+    FrameParams q = p;
+    q.detail_wgs = share && grid >= 2 ? grid - max(min(grid / share, (nblk + 63) / 64), 1u) : 0u;
+    frame_kernel<C, L, M, K><<<grid, kWG, dyn, s>>>(q.objects, q.lights, q.cull, q.tris, q.shade,
+                                                    q.nobj | (q.nlights << 16), q.total_tris, q.total_sub, grid, q);
     return hipGetLastError();
 }
 
