@@ -199,10 +199,11 @@ def main() -> None:
     t_setup = time.perf_counter() - t_setup0
     hits = int((face >= 0).sum().item())
 
-    for _ in range(args.warmup):
-        scene.render(**render_args())
-    # capture the frame-loop graph and warm the gather outside the timed region
+    # capture the frame-loop graph, then the W warmup frames through the same replayed path as
+    # the timed ones (and the gather warmed) outside the timed region
     scene.ctx.render_frames(args.steps, width, H_total, prepare_only=True, **render_args())
+    if args.warmup:
+        scene.ctx.render_frames(args.warmup, width, H_total, **render_args())
     if world > 1:
         gather_ppm_rows(ppm, frame, world, rank)
     torch.cuda.synchronize()

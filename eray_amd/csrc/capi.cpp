@@ -92,14 +92,17 @@ struct eray_ctx {
     size_t objs_cap = 0;
     LightDesc* d_lights = nullptr;
     size_t lights_cap = 0;
-    // launch plan of eray_render_frames: HIP graphs of back-to-back frame launches — [0] a
-    // chunk of up to kGraphFrames frames, [1] the remainder of the last call's frame count —
-    // each cached for the frame parameters + stream + length it was captured with
+    // launch plans of eray_render_frames: HIP graphs of back-to-back frame launches (chunks of up
+    // to kGraphFrames frames and remainders), each cached for the frame parameters + stream +
+    // length it was captured with; the least recently used is evicted beyond kGraphCache
     struct FrameGraph {
         hipGraph_t graph = nullptr;
         hipGraphExec_t exec = nullptr;
         std::vector<unsigned char> key;
-    } graphs[2];
+        uint64_t used = 0;
+    };
+    std::vector<FrameGraph> graphs;
+    uint64_t graph_clock = 0;
     uint32_t* d_rect = nullptr;  // per-object pixel-rectangle accumulators (4 x uint32)
     std::vector<int32_t> face_rects;  // per object: the union of its faces' rectangles (4 x int32)
     size_t rect_cap = 0;
@@ -903,49 +906,68 @@ int eray_render(eray_ctx* ctx, const eray_render_params* rp) {
 namespace {
 constexpr uint32_t kGraphFrames = 64;
 
-// (Re)builds graph `slot` of n back-to-back frame launches unless it is cached for (p, n, stream).
-int ensure_graph(eray_ctx* ctx, const FrameParams& p, uint32_t n, int slot) {
-    auto& G = ctx->graphs[slot];
+constexpr size_t kGraphCache = 6;
+
+// The graph of n back-to-back frame launches for (p, stream), captured unless cached.
+int ensure_graph(eray_ctx* ctx, const FrameParams& p, uint32_t n, hipGraphExec_t* out) {
     std::vector<unsigned char> key(sizeof p + sizeof n + sizeof ctx->stream);
     std::memcpy(key.data(), &p, sizeof p);
     std::memcpy(key.data() + sizeof p, &n, sizeof n);
     std::memcpy(key.data() + sizeof p + sizeof n, &ctx->stream, sizeof ctx->stream);
-    if (G.exec && key == G.key) return ERAY_OK;
-    if (G.exec) hipGraphExecDestroy(G.exec);
-    if (G.graph) hipGraphDestroy(G.graph);
-    G.exec = nullptr;
-    G.graph = nullptr;
-    G.key.clear();
+    for (auto& G : ctx->graphs)
+        if (G.key == key) {
+            G.used = ++ctx->graph_clock;
+            *out = G.exec;
+            return ERAY_OK;
+        }
+    if (ctx->graphs.size() >= kGraphCache) {  // evict the least recently used
+        size_t lru = 0;
+        for (size_t i = 1; i < ctx->graphs.size(); ++i)
+            if (ctx->graphs[i].used < ctx->graphs[lru].used) lru = i;
+        auto& G = ctx->graphs[lru];
+        if (G.exec) hipGraphExecDestroy(G.exec);
+        if (G.graph) hipGraphDestroy(G.graph);
+        ctx->graphs.erase(ctx->graphs.begin() + (std::ptrdiff_t)lru);
+    }
     HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
     hipError_t e = hipSuccess;
     for (uint32_t f = 0; f < n && e == hipSuccess; ++f) e = launch_render(p, ctx->stream);
     hipGraph_t g = nullptr;
     const hipError_t e2 = hipStreamEndCapture(ctx->stream, &g);
     if (e == hipSuccess) e = e2;
-    if (e == hipSuccess) e = hipGraphInstantiate(&G.exec, g, nullptr, nullptr, 0);
+    hipGraphExec_t exec = nullptr;
+    if (e == hipSuccess) e = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
     if (e != hipSuccess) {
         if (g) hipGraphDestroy(g);
-        G.exec = nullptr;
         return set_error(ctx, ERAY_E_HIP, "frame graph capture: %s", hipGetErrorString(e));
     }
+    eray_ctx::FrameGraph G;
     G.graph = g;
+    G.exec = exec;
     G.key = std::move(key);
+    G.used = ++ctx->graph_clock;
+    ctx->graphs.push_back(std::move(G));
+    *out = exec;
     return ERAY_OK;
 }
 
-// The launch plan of `frames` frames: graph 0 of `chunk` = min(frames, kGraphFrames) frames,
-// replayed frames / chunk times, and graph 1 of the remainder (no plain launches, whose host
+// The launch plan of `frames` frames: a graph of `chunk` = min(frames, kGraphFrames) frames,
+// replayed frames / chunk times, and a graph of the remainder (no plain launches, whose host
 // cost can exceed a frame's device time).  chunk = 0: plain launches (null stream, 1 frame).
-int ensure_plan(eray_ctx* ctx, const FrameParams& p, uint32_t frames, uint32_t* chunk, uint32_t* rest) {
-    *chunk = *rest = 0;
+struct Plan {
+    uint32_t chunk = 0, rest = 0;
+    hipGraphExec_t chunk_exec = nullptr, rest_exec = nullptr;
+};
+int ensure_plan(eray_ctx* ctx, const FrameParams& p, uint32_t frames, Plan* plan) {
+    *plan = Plan{};
     if (!ctx->stream || frames < 2) return ERAY_OK;  // the null stream cannot be captured
     const uint32_t n = frames < kGraphFrames ? frames : kGraphFrames;
-    if (int st = ensure_graph(ctx, p, n, 0)) return st;
-    *chunk = n;
+    if (int st = ensure_graph(ctx, p, n, &plan->chunk_exec)) return st;
+    plan->chunk = n;
     const uint32_t r = frames % n;
     if (r > 1) {
-        if (int st = ensure_graph(ctx, p, r, 1)) return st;
-        *rest = r;
+        if (int st = ensure_graph(ctx, p, r, &plan->rest_exec)) return st;
+        plan->rest = r;
     }
     return ERAY_OK;
 }
@@ -955,8 +977,8 @@ int eray_render_prepare(eray_ctx* ctx, const eray_render_params* rp, uint32_t fr
     FrameParams p;
     bool empty = false;
     if (int st = prepare_render(ctx, rp, &p, &empty)) return st;
-    uint32_t chunk, rest;
-    return empty ? ERAY_OK : ensure_plan(ctx, p, frames, &chunk, &rest);
+    Plan plan;
+    return empty ? ERAY_OK : ensure_plan(ctx, p, frames, &plan);
 }
 
 int eray_render_frames(eray_ctx* ctx, const eray_render_params* rp, uint32_t frames,
@@ -966,8 +988,8 @@ int eray_render_frames(eray_ctx* ctx, const eray_render_params* rp, uint32_t fra
     if (int st = prepare_render(ctx, rp, &p, &empty)) return st;
     if (mean_frame_ms) *mean_frame_ms = 0.0f;
     if (empty || !frames) return ERAY_OK;
-    uint32_t chunk = 0, rest = 0;
-    if (int st = ensure_plan(ctx, p, frames, &chunk, &rest)) return st;
+    Plan plan;
+    if (int st = ensure_plan(ctx, p, frames, &plan)) return st;
     hipEvent_t ev[2] = {nullptr, nullptr};
     if (mean_frame_ms) {
         for (auto& e : ev) {
@@ -981,11 +1003,11 @@ int eray_render_frames(eray_ctx* ctx, const eray_render_params* rp, uint32_t fra
     // replay the cached graphs (back-to-back frame kernels)
     hipError_t he = mean_frame_ms ? hipEventRecord(ev[0], ctx->stream) : hipSuccess;
     uint32_t done = 0;
-    for (; chunk && done + chunk <= frames && he == hipSuccess; done += chunk)
-        he = hipGraphLaunch(ctx->graphs[0].exec, ctx->stream);
-    if (rest && done + rest == frames && he == hipSuccess) {
-        he = hipGraphLaunch(ctx->graphs[1].exec, ctx->stream);
-        done += rest;
+    for (; plan.chunk && done + plan.chunk <= frames && he == hipSuccess; done += plan.chunk)
+        he = hipGraphLaunch(plan.chunk_exec, ctx->stream);
+    if (plan.rest && done + plan.rest == frames && he == hipSuccess) {
+        he = hipGraphLaunch(plan.rest_exec, ctx->stream);
+        done += plan.rest;
     }
     for (; done < frames && he == hipSuccess; ++done) he = launch_frame(ctx, p);
     if (mean_frame_ms && he == hipSuccess) {
