@@ -123,6 +123,13 @@ def cpu_baseline(mesh, width: int, height: int, fov, seconds: float = 10.0) -> d
             "sample": sample + ", single thread, oracle/eray_oracle.cpp (g++ -O2 -ffp-contract=off)"}
 
 
+def mesh_label(path: str) -> str:
+    """The mesh as the JSON line names it: repo-relative when it is in the tree, else the file name
+    (meshes generated on the box by eray_amd.meshgen)."""
+    rel = os.path.relpath(path, ROOT)
+    return os.path.basename(path) if rel.startswith("..") else rel
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -264,7 +271,7 @@ def main() -> None:
             "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
-            "data": (f"synthetic scene of src/main.rs around {os.path.relpath(args.mesh, ROOT)}"
+            "data": (f"synthetic scene of src/main.rs around {mesh_label(args.mesh)}"
                      + (" (the reference's own file)" if args.mesh.endswith("objects/cube.obj") else "")
                      + ", procedural material graph"),
             "config": {
@@ -273,7 +280,7 @@ def main() -> None:
                             "main.rs scene + material graph; step = one frame (camera rays, first-hit scan, "
                             "shading + shadow rays, f32 image and PPM bytes); N > 1: row tiles, final RCCL "
                             "gather of the PPM rows to rank 0",
-                "mesh": os.path.relpath(args.mesh, ROOT),
+                "mesh": mesh_label(args.mesh),
                 "triangles": int(len(mesh[0])),
                 "frame": [width, H_total],
                 "rows_per_gpu": rows,

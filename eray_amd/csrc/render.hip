@@ -1305,8 +1305,13 @@ __device__ __forceinline__ bool inside(const SubRect& r, int32_t sx, int32_t sy)
     return sx >= r.sx0 && sx <= r.sx1 && sy >= r.sy0 && sy <= r.sy1;
 }
 
-template <bool kCull, bool kLdsTiles, int kMat, bool kLdsScene>
-__global__ void __launch_bounds__(kWG, (kLdsTiles || (kMat & kMatSpecPow)) ? 1 : 3)  // 3 workgroups per CU where that fits
+// kDense (large meshes only): 3 workgroups per CU instead of 2 (168 VGPRs, a few spilled), for
+// frames whose detail sub-blocks exceed one round of the 2-per-CU grid — there the detail waves
+// are VALU-issue bound and a second detail wave per SIMD doubles the issue slots (one wave alone
+// issues a VALU instruction every 4 cycles, the SIMD every 2); below one round the spills only
+// lengthen each wave's chain.
+template <bool kCull, bool kLdsTiles, int kMat, bool kLdsScene, bool kDense = false>
+__global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && !kDense) ? 1 : 3)  // 3 workgroups per CU where that fits
     frame_kernel(const ObjectDesc* h_objects, const LightDesc* h_lights, const TriCull* h_cull, const TriHot* h_tris,
                  const TriShade* h_shade, uint32_t h_counts, uint32_t h_total_tris, uint32_t h_total_sub,
                  uint32_t h_grid, FrameParams p) {
@@ -1512,7 +1517,7 @@ hipError_t launch_tri_rect(const TriCull* cull, uint32_t T, uint32_t cam_w, uint
 namespace {
 // Persistent grid: as many workgroups as are resident at once (occupancy API), capped by the
 // work (fill blocks or detail sub-blocks, whichever needs more workgroups).
-template <bool C, bool L, int M, bool K>
+template <bool C, bool L, int M, bool K, bool D = false>
 hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, hipStream_t s) {
     static int per_cu = -1, cus = 0;
     static size_t per_cu_dyn = 0;
@@ -1521,7 +1526,7 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, frame_kernel<C, L, M, K>, kWG, dyn) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, frame_kernel<C, L, M, K, D>, kWG, dyn) !=
                 hipSuccess ||
             per_cu <= 0)
             per_cu = 1;
@@ -1544,7 +1549,7 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
     const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
     FrameParams q = p;
     q.detail_wgs = share && grid >= 2 ? grid - max(min(grid / share, (nblk + 63) / 64), 1u) : 0u;
-    frame_kernel<C, L, M, K><<<grid, kWG, dyn, s>>>(q.objects, q.lights, q.cull, q.tris, q.shade,
+    frame_kernel<C, L, M, K, D><<<grid, kWG, dyn, s>>>(q.objects, q.lights, q.cull, q.tris, q.shade,
                                                     q.nobj | (q.nlights << 16), q.total_tris, q.total_sub, grid, q);
     return hipGetLastError();
 }
@@ -1557,7 +1562,24 @@ hipError_t launch_frame_cs(const FrameParams& p, uint32_t want, hipStream_t s) {
         const size_t dyn = scene_lds_layout(p.nobj, p.nlights, p.total_tris, C).bytes;
         return launch_frame_kernel<C, false, M, true>(p, want, dyn, s);
     }
-    if (p.max_object_tris > kDirectMax) return launch_frame_kernel<C, true, M, false>(p, want, 0, s);
+    if (p.max_object_tris > kDirectMax) {
+        if constexpr (!(M & kMatSpecPow)) {
+            // more detail sub-blocks than the 2-per-CU grid's detail waves (half the grid, four
+            // waves each: launch_frame_kernel) take in one round: the 3-per-CU build
+            const char* e = getenv("ERAY_DENSE_DETAIL");  // tests/diagnostics: 0 never, 1 always
+            const int dense = e ? atoi(e) : -1;
+            static const uint32_t cus = [] {
+                int dev = 0, n = 0;
+                return (hipGetDevice(&dev) == hipSuccess &&
+                        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+                           ? (uint32_t)n
+                           : 256u;
+            }();
+            if (dense == 1 || (dense < 0 && p.total_sub > cus * (kWG / 64)))
+                return launch_frame_kernel<C, true, M, false, true>(p, want, 0, s);
+        }
+        return launch_frame_kernel<C, true, M, false>(p, want, 0, s);
+    }
     return launch_frame_kernel<C, false, M, false>(p, want, 0, s);
 }
 }  // namespace

@@ -316,9 +316,13 @@ def standin70k():
             np.ascontiguousarray(t[ft].reshape(-1, 6)))
 
 
+@pytest.mark.parametrize("dense", ["auto", "0", "1"])
 @pytest.mark.parametrize("material", ["textures", "example"])
-def test_c3_binned_equals_brute_force(gpu, standin70k, material):
-    """Screen bins (bins.hip) for a 70k-face object: bit-identical to the brute-force scan."""
+def test_c3_binned_equals_brute_force(gpu, standin70k, material, dense, monkeypatch):
+    """Screen bins (bins.hip) for a 70k-face object: bit-identical to the brute-force scan, with
+    the large-mesh frame kernel at 2 and at 3 workgroups per CU (ERAY_DENSE_DETAIL)."""
+    if dense != "auto":
+        monkeypatch.setenv("ERAY_DENSE_DETAIL", dense)
     W, H = 480, 270
     sc = MainScene(gpu, *standin70k, W, H, texture=256, fov=(16.0, 9.0), material=material)
     a = gpu_render(gpu, W, H)
@@ -330,9 +334,12 @@ def test_c3_binned_equals_brute_force(gpu, standin70k, material):
     assert np.array_equal(a[2], b[2])
 
 
-def test_c3_full_size_rows_match_oracle(gpu, oracle, standin70k):
+@pytest.mark.parametrize("dense", ["0", "1"])
+def test_c3_full_size_rows_match_oracle(gpu, oracle, standin70k, dense, monkeypatch):
     """C3 at 1920x1080 (bins built for the full camera) against the oracle on a row sample
-    through the object, including row blocks rendered with a row phase (row0 % 4 != 0)."""
+    through the object, including row blocks rendered with a row phase (row0 % 4 != 0); the
+    large-mesh kernel at 2 and at 3 workgroups per CU."""
+    monkeypatch.setenv("ERAY_DENSE_DETAIL", dense)
     W, H = 1920, 1080
     sc = MainScene(gpu, *standin70k, W, H, texture=256, fov=(16.0, 9.0))
     rgb, face, _ = gpu_render(gpu, W, H)
