@@ -1338,11 +1338,14 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     // fill's HBM writes instead of preceding them); when every workgroup has detail work, all of
     // them fill afterwards
     const uint32_t nd = min(p.detail_wgs ? p.detail_wgs : grid, (total + nwaves - 1) / nwaves);
+    // the workgroup's role index: detail roles [0, nd), fill roles [nd, grid); with fill_first
+    // the fill roles go to the first-dispatched (older, VALU-priority) workgroups
+    const uint32_t bid = (p.fill_first && nd < grid) ? (blockIdx.x + nd) % grid : blockIdx.x;
     ERAY_TRACE_CLEAR();
     ERAY_TRACE(0);
 
     // ---- detail sub-blocks -------------------------------------------------------------------
-    if (blockIdx.x < nd) {
+    if (bid < nd) {
 #ifdef ERAY_AB_X_NO_DETAIL  // diagnostics only (wrong images): the fill alone, same grid
         if (nd < grid) return;
 #endif
@@ -1368,7 +1371,7 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
         };
         // the wave's first sub-block and its camera rays, before the scene is in: the kernel
         // arguments' scalar loads and the ray arithmetic overlap the preload's round trip
-        const uint32_t c0 = blockIdx.x * nwaves;
+        const uint32_t c0 = bid * nwaves;
         int32_t sx0 = 0, sy0 = 0;
         f3 d0;
 #ifdef ERAY_AB_LAZY_RAY
@@ -1424,7 +1427,7 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     if (p.nobj != 12345) return;
 #endif
     const uint32_t nf = nd < grid ? grid - nd : grid;  // filling workgroups
-    const uint32_t f = nd < grid ? blockIdx.x - nd : blockIdx.x;
+    const uint32_t f = nd < grid ? bid - nd : bid;
     const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
     const uint32_t fstride = nf * nwaves;
     uint32_t occ = 0;  // detail list: lane i holds the occupancy of this wave's i-th next block
@@ -1539,16 +1542,32 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
     const int wg_cu = cap > 0 && cap < per_cu ? cap : per_cu;
     const uint32_t grid = min(want, (uint32_t)(wg_cu * cus));
     // Workgroups kept for the fill so that it overlaps a large detail area instead of following
-    // it: one per 64 background blocks, at most 1/share of the grid (fill waves are issue-bound
-    // below ~1000 per frame: at 3840x2160 / 70k, 128 fill workgroups took 52 us, 256 took 31 us,
-    // none 34 us).  Tuning knob ERAY_FILL_SHARE (diagnostics; 0 = no reservation).
-    static const uint32_t share = [] {
-        const char* e = getenv("ERAY_FILL_SHARE");
-        return e ? (uint32_t)atoi(e) : 2u;
-    }();
+    // it: one per 64 background blocks, at most 1/share of the grid.  Measured (graph-replayed
+    // frames, profiles/ab/ab_knobs*.log): the fill needs enough store-issuing waves on every CU
+    // (3840x2160 / 70k: 128 fill workgroups 52 us, 256 31 us, none 34 us) and the detail waves'
+    // VALU issue; share 2 with the detail roles first is best for C2, C3 and 3840x2160 / 70k
+    // (27.8 us; share 3 29.4-30.3, share 4 37), while a small-scene frame with more than one
+    // round of detail sub-blocks (the cube at 3840x2160) wants one fill workgroup per CU
+    // dispatched first (share 3, fill_first: 22.8 -> 20.4 us; at C2 fill_first costs 0.7 us).
+    // Diagnostics knobs ERAY_FILL_SHARE (0 = no reservation) and ERAY_FILL_FIRST override.
+    const char* e_share = getenv("ERAY_FILL_SHARE");
+    const char* e_first = getenv("ERAY_FILL_FIRST");
     const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
+    auto detail_wgs = [&](float share) {
+        return share >= 1.0f && grid >= 2 ? grid - max(min((uint32_t)((float)grid / share), (nblk + 63) / 64), 1u)
+                                          : 0u;
+    };
+    float share = 2.0f;
+    uint32_t fill_first = 0;
+    if (!L && p.total_sub > detail_wgs(share) * (kWG / 64)) {
+        share = 3.0f;
+        fill_first = 1;
+    }
+    if (e_share) share = (float)atof(e_share);
+    if (e_first) fill_first = (uint32_t)atoi(e_first);
     FrameParams q = p;
-    q.detail_wgs = share && grid >= 2 ? grid - max(min(grid / share, (nblk + 63) / 64), 1u) : 0u;
+    q.detail_wgs = detail_wgs(share);
+    q.fill_first = fill_first;
     frame_kernel<C, L, M, K, D><<<grid, kWG, dyn, s>>>(q.objects, q.lights, q.cull, q.tris, q.shade,
                                                     q.nobj | (q.nlights << 16), q.total_tris, q.total_sub, grid, q);
     return hipGetLastError();
