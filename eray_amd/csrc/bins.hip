@@ -11,9 +11,15 @@
 // bounds solved per pixel row), so the frame kernel only tests (face, pixel) pairs that can hit.
 //
 // Built once per camera / geometry change (and per row phase of the rendered rows):
-// count covered bins per face -> exclusive scan -> emit (bin, position) pairs in face order ->
-// stable radix sort by bin (LSD: keeps face order within a bin) -> bin start offsets -> faces,
-// pixel masks and intersection records gathered in bin order.
+// each face's bin rectangle -> exclusive scan of the rectangles' areas (the (face, bin) pairs,
+// face-major) -> pixel masks of all pairs, one thread per pair (balanced: a near-silhouette
+// face's rectangle can span the frame's width, thousands of bins that one thread per face
+// walked alone) -> the non-empty pairs compacted in pair order, i.e. (bin, position) in face
+// order -> stable radix sort by bin (LSD: keeps face order within a bin) -> bin start offsets ->
+// faces, pixel masks and intersection records gathered in bin order.
+#include <algorithm>
+#include <cstdlib>
+
 #include <hipcub/hipcub.hpp>
 
 #include "face_rect.hpp"
@@ -23,50 +29,85 @@ namespace eray {
 namespace gpu {
 namespace {
 
-// per face: its bins (face_rect) and how many of them it may actually cover (bin_pixels != 0)
-__global__ void __launch_bounds__(256) bin_count_kernel(const TriCull* __restrict__ cull, uint32_t T, uint32_t W,
-                                                        uint32_t H, uint32_t phase, uint32_t* __restrict__ count,
-                                                        int4* __restrict__ range) {
+// per face: its bin rectangle (face_rect; empty: x0 > x1) and the rectangle's number of bins
+__global__ void __launch_bounds__(256) bin_range_kernel(const TriCull* __restrict__ cull, uint32_t T, uint32_t W,
+                                                        uint32_t H, uint32_t phase, int4* __restrict__ range,
+                                                        unsigned long long* __restrict__ area) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= T) return;
-    const TriCull c = cull[i];
     int32_t r[4];
-    uint32_t n = 0;
     int4 g = make_int4(1, 0, 1, 0);
-    if (face_rect(c, W, H, r)) {
+    unsigned long long a = 0;
+    if (face_rect(cull[i], W, H, r)) {
         // bin row of camera row y: (y + kBinH - phase) / kBinH
         g = make_int4(r[0] / (int32_t)kBinW, r[1] / (int32_t)kBinW,
                       (r[2] + (int32_t)kBinH - (int32_t)phase) / (int32_t)kBinH,
                       (r[3] + (int32_t)kBinH - (int32_t)phase) / (int32_t)kBinH);
-        for (int32_t ty = g.z; ty <= g.w; ++ty)
-            for (int32_t tx = g.x; tx <= g.y; ++tx) n += bin_pixels(c, W, H, phase, (uint32_t)tx, (uint32_t)ty) != 0;
+        a = (unsigned long long)(g.y - g.x + 1) * (unsigned long long)(g.w - g.z + 1);
     }
-    count[i] = n;
     range[i] = g;
+    area[i] = a;
 }
 
-__global__ void __launch_bounds__(256) bin_emit_kernel(const TriCull* __restrict__ cull,
-                                                       const uint32_t* __restrict__ offset,
-                                                       const uint32_t* __restrict__ count,
-                                                       const int4* __restrict__ range, uint32_t T, uint32_t W,
-                                                       uint32_t H, uint32_t phase, uint32_t bins_x,
+// Pair j of [j0, j0 + len) (face-major, each face's bins row-major): its face (the last face
+// whose first pair is <= j), bin and pixel mask.  emit == false: only the number of non-empty
+// pairs, added to *nonempty; emit == true: the pair's mask, bin key and face, and a 0/1 flag.
+template <bool emit>
+__global__ void __launch_bounds__(256) bin_pairs_kernel(const TriCull* __restrict__ cull, const int4* __restrict__ range,
+                                                        const unsigned long long* __restrict__ first, uint32_t T,
+                                                        unsigned long long j0, uint32_t len, uint32_t W, uint32_t H,
+                                                        uint32_t phase, uint32_t bins_x,
+                                                        unsigned long long* __restrict__ nonempty,
+                                                        unsigned long long* __restrict__ pmask,
+                                                        uint32_t* __restrict__ pkey, uint32_t* __restrict__ pface,
+                                                        uint32_t* __restrict__ pflag) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long m = 0;
+    uint32_t key = 0, i = 0;
+    if (k < len) {
+        const unsigned long long j = j0 + k;
+        uint32_t lo = 0, hi = T;  // first face whose first pair is > j
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (first[mid] <= j) lo = mid + 1;
+            else hi = mid;
+        }
+        i = lo - 1;
+        const int4 g = range[i];
+        const uint32_t w = (uint32_t)(g.y - g.x + 1);
+        const uint32_t c = (uint32_t)(j - first[i]);
+        const uint32_t tx = (uint32_t)g.x + c % w, ty = (uint32_t)g.z + c / w;
+        m = bin_pixels(cull[i], W, H, phase, tx, ty);
+        key = ty * bins_x + tx;
+    }
+    if constexpr (emit) {
+        if (k < len) {
+            pmask[k] = m;
+            pkey[k] = key;
+            pface[k] = i;
+            pflag[k] = m != 0;
+        }
+    } else {
+        const unsigned long long b = __ballot(m != 0);
+        if ((threadIdx.x & 63) == 0 && b) atomicAdd(nonempty, (unsigned long long)__popcll(b));
+    }
+}
+
+// the non-empty pairs of a chunk at their compacted positions base + pos (pair order = face order)
+__global__ void __launch_bounds__(256) bin_emit_kernel(const unsigned long long* __restrict__ pmask,
+                                                       const uint32_t* __restrict__ pkey,
+                                                       const uint32_t* __restrict__ pface,
+                                                       const uint32_t* __restrict__ pflag,
+                                                       const uint32_t* __restrict__ pos, uint32_t len, uint32_t base,
                                                        uint32_t* __restrict__ keys, uint32_t* __restrict__ order,
                                                        uint32_t* __restrict__ tri, unsigned long long* __restrict__ mask) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= T || !count[i]) return;
-    const TriCull c = cull[i];
-    uint32_t o = offset[i];
-    const int4 g = range[i];
-    for (int32_t ty = g.z; ty <= g.w; ++ty)
-        for (int32_t tx = g.x; tx <= g.y; ++tx) {
-            const unsigned long long m = bin_pixels(c, W, H, phase, (uint32_t)tx, (uint32_t)ty);
-            if (!m) continue;
-            keys[o] = (uint32_t)ty * bins_x + (uint32_t)tx;
-            order[o] = o;  // emit positions increase with the face index
-            tri[o] = i;
-            mask[o] = m;
-            ++o;
-        }
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= len || !pflag[k]) return;
+    const uint32_t o = base + pos[k];
+    keys[o] = pkey[k];
+    order[o] = o;  // emit positions increase with the face index
+    tri[o] = pface[k];
+    mask[o] = pmask[k];
 }
 
 // entries in bin order: face, pixel mask and intersection record
@@ -218,38 +259,67 @@ hipError_t build_bins(const TriCull* cull, const TriHot* hot, uint32_t T, uint32
     const uint32_t nbins = bins_x * bins_y;
     hipError_t e = grow(&out->start, &out->start_cap, (size_t)nbins + 1);
     if (e != hipSuccess) return e;
-    uint32_t *count = nullptr, *offset = nullptr, *keys = nullptr, *keys2 = nullptr, *order = nullptr,
-             *order2 = nullptr, *tri = nullptr;
-    unsigned long long* mask = nullptr;
+    uint32_t *keys = nullptr, *keys2 = nullptr, *order = nullptr, *order2 = nullptr, *tri = nullptr;
+    uint32_t *pkey = nullptr, *pface = nullptr, *pflag = nullptr, *pos = nullptr;
+    unsigned long long *mask = nullptr, *area = nullptr, *first = nullptr, *d_n = nullptr, *pmask = nullptr;
     int4* range = nullptr;
     void* temp = nullptr;
     size_t n = 0;
+    unsigned long long pairs = 0;  // (face, bin) pairs of the faces' bin rectangles
     auto done = [&](hipError_t err) {
-        for (void* q : {(void*)count, (void*)offset, (void*)keys, (void*)keys2, (void*)order, (void*)order2,
-                        (void*)tri, (void*)mask, (void*)range, temp})
+        for (void* q : {(void*)keys, (void*)keys2, (void*)order, (void*)order2, (void*)tri, (void*)pkey,
+                        (void*)pface, (void*)pflag, (void*)pos, (void*)mask, (void*)area, (void*)first, (void*)d_n,
+                        (void*)pmask, (void*)range, temp})
             if (q) hipFree(q);
         return err;
     };
+    // scratch scans: one temp buffer, grown to the largest request
+    size_t temp_cap = 0;
+    auto temp_for = [&](size_t bytes) -> hipError_t {
+        if (temp && temp_cap >= bytes) return hipSuccess;
+        if (temp) hipFree(temp);
+        temp = nullptr;
+        temp_cap = 0;
+        const hipError_t err = hipMalloc(&temp, bytes ? bytes : 1);
+        if (err == hipSuccess) temp_cap = bytes;
+        return err;
+    };
+    // pairs per pass (24 B of scratch each); tests shrink it (ERAY_BIN_PAIR_CHUNK) to cover the
+    // multi-pass compaction
+    const char* e_chunk = getenv("ERAY_BIN_PAIR_CHUNK");
+    const unsigned long long kPairChunk = e_chunk && atoll(e_chunk) > 0 ? (unsigned long long)atoll(e_chunk) : 1ull << 24;
     if (T) {
-        if ((e = hipMalloc((void**)&count, sizeof(uint32_t) * T)) != hipSuccess) return done(e);
-        if ((e = hipMalloc((void**)&offset, sizeof(uint32_t) * T)) != hipSuccess) return done(e);
         if ((e = hipMalloc((void**)&range, sizeof(int4) * T)) != hipSuccess) return done(e);
-        bin_count_kernel<<<(T + 255) / 256, 256, 0, s>>>(cull, T, W, H, phase, count, range);
+        if ((e = hipMalloc((void**)&area, sizeof(unsigned long long) * T)) != hipSuccess) return done(e);
+        if ((e = hipMalloc((void**)&first, sizeof(unsigned long long) * T)) != hipSuccess) return done(e);
+        if ((e = hipMalloc((void**)&d_n, sizeof(unsigned long long))) != hipSuccess) return done(e);
+        bin_range_kernel<<<(T + 255) / 256, 256, 0, s>>>(cull, T, W, H, phase, range, area);
         if ((e = hipGetLastError()) != hipSuccess) return done(e);
         size_t temp_bytes = 0;
-        if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, temp_bytes, count, offset, T, s)) != hipSuccess)
+        if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, temp_bytes, area, first, T, s)) != hipSuccess ||
+            (e = temp_for(temp_bytes)) != hipSuccess ||
+            (e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, area, first, T, s)) != hipSuccess)
             return done(e);
-        if ((e = hipMalloc(&temp, temp_bytes ? temp_bytes : 1)) != hipSuccess) return done(e);
-        if ((e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, count, offset, T, s)) != hipSuccess)
-            return done(e);
-        uint32_t last[2];
-        if ((e = hipMemcpyAsync(&last[0], offset + T - 1, 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-            (e = hipMemcpyAsync(&last[1], count + T - 1, 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        unsigned long long last[2];
+        if ((e = hipMemcpyAsync(&last[0], first + T - 1, 8, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+            (e = hipMemcpyAsync(&last[1], area + T - 1, 8, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+            (e = hipMemsetAsync(d_n, 0, sizeof(unsigned long long), s)) != hipSuccess ||
             (e = hipStreamSynchronize(s)) != hipSuccess)
             return done(e);
-        n = (size_t)last[0] + last[1];
-        hipFree(temp);
-        temp = nullptr;
+        pairs = last[0] + last[1];
+        // the non-empty pairs (count only)
+        for (unsigned long long j0 = 0; j0 < pairs; j0 += kPairChunk) {
+            const uint32_t len = (uint32_t)std::min(kPairChunk, pairs - j0);
+            bin_pairs_kernel<false><<<(len + 255) / 256, 256, 0, s>>>(cull, range, first, T, j0, len, W, H, phase,
+                                                                      bins_x, d_n, nullptr, nullptr, nullptr, nullptr);
+            if ((e = hipGetLastError()) != hipSuccess) return done(e);
+        }
+        unsigned long long nn = 0;
+        if ((e = hipMemcpyAsync(&nn, d_n, 8, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+            (e = hipStreamSynchronize(s)) != hipSuccess)
+            return done(e);
+        if (nn >= (1ull << 31)) return done(hipErrorOutOfMemory);  // entries are indexed by int (radix sort)
+        n = (size_t)nn;
     }
     if ((e = grow(&out->tri, &out->tri_cap, n)) != hipSuccess) return done(e);
     if ((e = grow(&out->mask, &out->mask_cap, n)) != hipSuccess) return done(e);
@@ -259,17 +329,43 @@ hipError_t build_bins(const TriCull* cull, const TriHot* hot, uint32_t T, uint32
         for (uint32_t** q : {&keys, &keys2, &order, &order2, &tri})
             if ((e = hipMalloc((void**)q, sizeof(uint32_t) * n)) != hipSuccess) return done(e);
         if ((e = hipMalloc((void**)&mask, sizeof(unsigned long long) * n)) != hipSuccess) return done(e);
-        bin_emit_kernel<<<(T + 255) / 256, 256, 0, s>>>(cull, offset, count, range, T, W, H, phase, bins_x, keys,
-                                                        order, tri, mask);
+        const size_t chunk = (size_t)std::min(kPairChunk, pairs);
+        if ((e = hipMalloc((void**)&pmask, sizeof(unsigned long long) * chunk)) != hipSuccess) return done(e);
+        for (uint32_t** q : {&pkey, &pface, &pflag, &pos})
+            if ((e = hipMalloc((void**)q, sizeof(uint32_t) * chunk)) != hipSuccess) return done(e);
+        // the pairs again, now written out, and compacted in pair order (= face order)
+        uint32_t base = 0;
+        for (unsigned long long j0 = 0; j0 < pairs; j0 += kPairChunk) {
+            const uint32_t len = (uint32_t)std::min(kPairChunk, pairs - j0);
+            bin_pairs_kernel<true><<<(len + 255) / 256, 256, 0, s>>>(cull, range, first, T, j0, len, W, H, phase,
+                                                                     bins_x, nullptr, pmask, pkey, pface, pflag);
+            if ((e = hipGetLastError()) != hipSuccess) return done(e);
+            size_t temp_bytes = 0;
+            if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, temp_bytes, pflag, pos, len, s)) != hipSuccess ||
+                (e = temp_for(temp_bytes)) != hipSuccess ||
+                (e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, pflag, pos, len, s)) != hipSuccess)
+                return done(e);
+            bin_emit_kernel<<<(len + 255) / 256, 256, 0, s>>>(pmask, pkey, pface, pflag, pos, len, base, keys, order,
+                                                              tri, mask);
+            if ((e = hipGetLastError()) != hipSuccess) return done(e);
+            if (j0 + len < pairs) {  // the next chunk's base
+                uint32_t last[2];
+                if ((e = hipMemcpyAsync(&last[0], pos + len - 1, 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+                    (e = hipMemcpyAsync(&last[1], pflag + len - 1, 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+                    (e = hipStreamSynchronize(s)) != hipSuccess)
+                    return done(e);
+                base += last[0] + last[1];
+            }
+        }
         if ((e = hipGetLastError()) != hipSuccess) return done(e);
         int end_bit = 1;
         while (end_bit < 32 && (1ull << end_bit) < (unsigned long long)nbins) ++end_bit;
         hipcub::DoubleBuffer<uint32_t> kb(keys, keys2), vb(order, order2);
         size_t temp_bytes = 0;
         if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, kb, vb, (int)n, 0, end_bit, s)) !=
-            hipSuccess)
+                hipSuccess ||
+            (e = temp_for(temp_bytes)) != hipSuccess)
             return done(e);
-        if ((e = hipMalloc(&temp, temp_bytes ? temp_bytes : 1)) != hipSuccess) return done(e);
         if ((e = hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, kb, vb, (int)n, 0, end_bit, s)) != hipSuccess)
             return done(e);
         bin_start_kernel<<<(uint32_t)((n + 1 + 255) / 256), 256, 0, s>>>(kb.Current(), (uint32_t)n, nbins,

@@ -316,13 +316,16 @@ def standin70k():
             np.ascontiguousarray(t[ft].reshape(-1, 6)))
 
 
-@pytest.mark.parametrize("dense", ["auto", "0", "1"])
+@pytest.mark.parametrize("dense,chunk", [("auto", None), ("0", None), ("1", None), ("auto", "9973")])
 @pytest.mark.parametrize("material", ["textures", "example"])
-def test_c3_binned_equals_brute_force(gpu, standin70k, material, dense, monkeypatch):
+def test_c3_binned_equals_brute_force(gpu, standin70k, material, dense, chunk, monkeypatch):
     """Screen bins (bins.hip) for a 70k-face object: bit-identical to the brute-force scan, with
-    the large-mesh frame kernel at 2 and at 3 workgroups per CU (ERAY_DENSE_DETAIL)."""
+    the large-mesh frame kernel at 2 and at 3 workgroups per CU (ERAY_DENSE_DETAIL), and with the
+    (face, bin) pairs compacted in many passes (ERAY_BIN_PAIR_CHUNK)."""
     if dense != "auto":
         monkeypatch.setenv("ERAY_DENSE_DETAIL", dense)
+    if chunk:
+        monkeypatch.setenv("ERAY_BIN_PAIR_CHUNK", chunk)
     W, H = 480, 270
     sc = MainScene(gpu, *standin70k, W, H, texture=256, fov=(16.0, 9.0), material=material)
     a = gpu_render(gpu, W, H)
