@@ -127,14 +127,20 @@ __global__ void __launch_bounds__(256) bin_gather_kernel(const uint32_t* __restr
     hot_out[j] = hot[f];
 }
 
-// start[t] = first position of bin t in the sorted keys (start[nbins] = n)
+// start[t] = first position of bin t in the sorted keys (start[nbins] = n): one thread per bin,
+// a lower bound over the keys (a thread per key filling the gap to the next key left the last
+// thread walking every bin after the last non-empty one: 0.85 ms at 3840x2160)
 __global__ void __launch_bounds__(256) bin_start_kernel(const uint32_t* __restrict__ keys, uint32_t n,
                                                         uint32_t nbins, uint32_t* __restrict__ start) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > n) return;
-    const uint32_t lo = i == 0 ? 0u : keys[i - 1] + 1u;
-    const uint32_t hi = i == n ? nbins : keys[i];
-    for (uint32_t t = lo; t <= hi && t <= nbins; ++t) start[t] = i;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > nbins) return;
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (keys[mid] < t) lo = mid + 1;
+        else hi = mid;
+    }
+    start[t] = lo;
 }
 
 // The pixel rectangle of the non-empty bins (camera pixels), accumulated as tri_rect_kernel's:
@@ -157,8 +163,20 @@ __global__ void __launch_bounds__(256) bins_rect_kernel(const uint32_t* __restri
 #pragma unroll
     for (int k = 0; k < 4; ++k)
         for (int off = 32; off > 0; off >>= 1) a[k] = max(a[k], (uint32_t)__shfl_xor((int)a[k], off));
-    if ((threadIdx.x & 63) == 0 && a[1])
-        for (int k = 0; k < 4; ++k) atomicMax(acc + k, a[k]);
+    // one set of atomics per workgroup (per wave they serialised on the same four words)
+    __shared__ uint32_t s_a[4][4];
+    const uint32_t wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < 4; ++k) s_a[wave][k] = a[k];
+    __syncthreads();
+    if (threadIdx.x < 4) {  // (launched with 256 threads: four waves)
+        uint32_t m = 0, any = 0;
+        for (uint32_t w = 0; w < 4; ++w) {
+            m = max(m, s_a[w][threadIdx.x]);
+            any |= s_a[w][1];  // some bin of the workgroup is non-empty
+        }
+        if (any) atomicMax(acc + threadIdx.x, m);
+    }
 }
 
 template <typename T>
@@ -368,13 +386,12 @@ hipError_t build_bins(const TriCull* cull, const TriHot* hot, uint32_t T, uint32
             return done(e);
         if ((e = hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, kb, vb, (int)n, 0, end_bit, s)) != hipSuccess)
             return done(e);
-        bin_start_kernel<<<(uint32_t)((n + 1 + 255) / 256), 256, 0, s>>>(kb.Current(), (uint32_t)n, nbins,
-                                                                          out->start);
+        bin_start_kernel<<<(nbins + 1 + 255) / 256, 256, 0, s>>>(kb.Current(), (uint32_t)n, nbins, out->start);
         if ((e = hipGetLastError()) != hipSuccess) return done(e);
         bin_gather_kernel<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(vb.Current(), tri, mask, hot, n, out->tri,
                                                                        out->mask, out->hot);
     } else {
-        bin_start_kernel<<<1, 256, 0, s>>>(nullptr, 0, nbins, out->start);
+        bin_start_kernel<<<(nbins + 1 + 255) / 256, 256, 0, s>>>(nullptr, 0, nbins, out->start);
     }
     if ((e = hipGetLastError()) != hipSuccess) return done(e);
     e = hipStreamSynchronize(s);  // the scratch buffers are freed below

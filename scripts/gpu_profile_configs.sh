@@ -11,7 +11,7 @@ python -m eray_amd.meshgen --triangles 1000000 --seed 1234 -o $M/synth1m.obj > /
 prof() {  # name timeout bench-args...
   local name=$1 t=$2; shift 2
   echo "=== $name: $*"
-  timeout -k 10 "$t" rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$name -o run -- \
+  timeout -k 10 "$t" rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$name -o run --output-format csv -- \
       python bench.py --no-cpu-baseline "$@" > gpurun_out/prof_$name.log 2>&1
   local rc=$?
   echo "=== $name rc=$rc"; tail -1 gpurun_out/prof_$name.log | cut -c1-300

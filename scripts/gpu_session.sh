@@ -25,5 +25,5 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
 fi
 run bench 600 python bench.py --steps "$STEPS" --warmup 20 --cpu-seconds 10
 if [ "${SKIP_PROF:-0}" != 1 ]; then
-  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline
+  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline
 fi
