@@ -24,6 +24,7 @@ Prints ONE JSON line on rank 0 (metric "Mrays/s": primary rays of all ranks / wa
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -72,16 +73,20 @@ def algorithmic_bytes(hit_pixels: int, pixels: int, triangles: int) -> int:
     return 15 * pixels + 16 * hit_pixels + (48 + 64 + 64) * triangles
 
 
-def pmc_traffic():
+def pmc_traffic(workload: dict):
     """HBM bytes per frame-kernel launch from the committed rocprofv3 counter summary of this
     workload (scripts/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
-    MI355X_MICROARCH.md), or None when no summary is committed."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        with open(path) as f:
-            return int(json.load(f)["frame_kernel"]["hbm_bytes_per_launch"])
-    except (OSError, KeyError, ValueError):
-        return None
+    MI355X_MICROARCH.md): profiles/pmc_traffic*.json whose "workload" (mesh, frame, rows per
+    GPU, GPUs) equals this run's, or None when no summary of this workload is committed."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json"))):
+        try:
+            with open(path) as f:
+                rec = json.load(f)
+            if rec.get("workload") == workload:
+                return int(rec["frame_kernel"]["hbm_bytes_per_launch"])
+        except (OSError, KeyError, ValueError):
+            continue
+    return None
 
 
 def cpu_baseline(mesh, width: int, height: int, fov, seconds: float = 10.0) -> dict:
@@ -250,7 +255,9 @@ def main() -> None:
         gather_ms = (time.perf_counter() - g0) * 1e3
 
     if rank == 0:
-        # the configuration profiles/pmc_traffic.json was collected on (C2, or C2 widened for N > 1)
+        # the workload a committed counter summary (profiles/pmc_traffic*.json) must match
+        pmc_key = {"mesh": mesh_label(args.mesh), "frame": [width, H_total], "rows_per_gpu": rows,
+                   "n_gpus": world, "brute_force": bool(args.brute_force)}
         is_c2 = (args.width, args.height, args.scaling) == (WIDTH, HEIGHT, "weak") and args.mesh.endswith(
             "objects/cube.obj") and not args.brute_force
         pixels = width * rows
@@ -302,7 +309,7 @@ def main() -> None:
                 "peak": PEAK_HBM_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4),
-                "traffic": pmc_traffic() if is_c2 and world == 1 else None,
+                "traffic": pmc_traffic(pmc_key),
                 "kernel": "frame_kernel (eray_amd/csrc/render.hip)",
                 "algorithmic_bytes_per_launch": alg,
                 "kernel_ms": round(kernel_ms, 6),

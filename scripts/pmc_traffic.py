@@ -23,14 +23,20 @@ PROF = os.path.join(ROOT, "profiles")
 
 
 def kernel_stats(tag: str) -> None:
+    csvs = glob.glob(os.path.join(OUT, "prof", "**", "*kernel_stats.csv"), recursive=True)
+    path = os.path.join(PROF, f"{tag}_kernel_stats.csv")
+    if csvs:  # rocprofv3 --output-format csv
+        with open(csvs[0]) as src, open(path, "w") as dst:
+            dst.write(src.read())
+        print("wrote", os.path.relpath(path, ROOT))
+        return
     dbs = glob.glob(os.path.join(OUT, "prof", "**", "*results.db"), recursive=True)
     if not dbs:
-        print("no rocprofv3 stats database under gpurun_out/prof", file=sys.stderr)
+        print("no rocprofv3 stats under gpurun_out/prof", file=sys.stderr)
         return
     con = sqlite3.connect(dbs[0])
     cur = con.execute("select * from top_kernels")
     cols = [d[0] for d in cur.description]
-    path = os.path.join(PROF, f"{tag}_kernel_stats.csv")
     with open(path, "w", newline="") as f:
         w = csv.writer(f)
         w.writerow(cols)
@@ -39,9 +45,9 @@ def kernel_stats(tag: str) -> None:
     print("wrote", os.path.relpath(path, ROOT))
 
 
-def pmc(tag: str) -> None:
+def pmc(tag: str, pmc_dir: str = "pmc", out_name: str = "pmc_traffic.json", workload=None) -> None:
     per = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> values per dispatch
-    for path in glob.glob(os.path.join(OUT, "pmc", "*", "*counter_collection.csv")):
+    for path in glob.glob(os.path.join(OUT, pmc_dir, "*", "*counter_collection.csv")):
         with open(path) as f:
             for row in csv.DictReader(f):
                 name = row["Kernel_Name"]
@@ -54,7 +60,15 @@ def pmc(tag: str) -> None:
     name = max(per, key=lambda k: len(per[k].get("WRITE_SIZE", [])))
     c = {k: statistics.mean(v) for k, v in per[name].items()}
     fetch, write = c.get("FETCH_SIZE", 0.0) * 1024, c.get("WRITE_SIZE", 0.0) * 1024
-    out = {"round": tag, "frame_kernel": {
+    if workload is None:  # the bench line of the counted run (its JSON line in the pass logs)
+        for log in glob.glob(os.path.join(OUT, pmc_dir, "*.log")):
+            for line in open(log):
+                if line.startswith("{"):
+                    d = json.loads(line)
+                    cfg = d["config"]
+                    workload = {"mesh": cfg["mesh"], "frame": cfg["frame"], "rows_per_gpu": cfg["rows_per_gpu"],
+                                "n_gpus": d["n_gpus"], "brute_force": not cfg["culling"]}
+    out = {"round": tag, "workload": workload, "frame_kernel": {
         "kernel": name,
         "dispatches": len(per[name].get("WRITE_SIZE", [])),
         "counters_mean_per_dispatch": c,
@@ -62,14 +76,18 @@ def pmc(tag: str) -> None:
         "write_bytes": write,
         "hbm_bytes_per_launch": int(2 * fetch + write),
     }}
-    path = os.path.join(PROF, "pmc_traffic.json")
+    path = os.path.join(PROF, out_name)
     with open(path, "w") as f:
         json.dump(out, f, indent=2)
     print("wrote", os.path.relpath(path, ROOT), out["frame_kernel"]["hbm_bytes_per_launch"])
 
 
 if __name__ == "__main__":
+    # usage: pmc_traffic.py [tag] [pmc dir under gpurun_out] [output file name under profiles/]
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
     os.makedirs(PROF, exist_ok=True)
-    kernel_stats(tag)
-    pmc(tag)
+    if len(sys.argv) > 2:
+        pmc(tag, sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else f"pmc_traffic_{sys.argv[2]}.json")
+    else:
+        kernel_stats(tag)
+        pmc(tag)
