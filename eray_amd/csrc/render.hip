@@ -700,15 +700,17 @@ constexpr uint32_t kBlkW = 64, kBlkH = 4;  // pixel block
 constexpr uint32_t kSubW = 16;             // sub-block width (x kBlkH rows): one wave's pixels
 static_assert(kSubW == kBinW && kBlkH == kBinH, "a screen bin is one wave's sub-block");
 
+constexpr uint32_t kWide = 16;  // candidates that may cover more pixels are tested by the whole wave
+
 // Per-wave LDS of the binned primary search.
 struct BinLds {
     float dir[3][64];         // each pixel's camera ray (lane = pixel)
     uint32_t best[64];        // each pixel's earliest hit so far: bin position, 0xffffffff = none
     TriHot cand[64];          // the chunk's candidate records (slot = lane that loaded it)
-    uint16_t pairs[64 * 64];  // (candidate slot << 6) | pixel, for every pixel a candidate may hit
+    // (candidate slot << 6) | pixel, for every pixel a narrow candidate (<= kWide pixels) may hit
+    uint16_t pairs[64 * kWide];
 };
 constexpr uint32_t kBinLdsBytes = (sizeof(BinLds) + 15) / 16 * 16;
-constexpr uint32_t kWide = 16;  // candidates that may cover more pixels are tested by the whole wave
 
 // Primary-ray first hit of a binned object (bins.hip), all four waves of the workgroup together
 // (every wave calls it; workgroup-uniform).  The reference's first hit by index is the smallest

@@ -3,7 +3,7 @@
 # and the cube at 3840x2160.
 mkdir -p gpurun_out /tmp/m
 python -m eray_amd.meshgen --triangles 69451 --seed 42 -o /tmp/m/s70k.obj > /dev/null || exit 1
-V="head cur head cur"
+V=${AB_VARIANTS:-"head cur head cur"}
 timeout -k 10 120 python scripts/ab_variants.py run $V || exit 1
 ERAY_AB_MESH=/tmp/m/s70k.obj timeout -k 10 120 python scripts/ab_variants.py run $V || exit 1
 ERAY_AB_MESH=/tmp/m/s70k.obj ERAY_AB_W=3840 ERAY_AB_H=2160 timeout -k 10 120 python scripts/ab_variants.py run $V || exit 1
@@ -12,5 +12,5 @@ if [ "${AB_CUBE4K:-1}" = 1 ]; then
 fi
 if [ "${AB_C5:-0}" = 1 ]; then
   python -m eray_amd.meshgen --triangles 1000000 --seed 1234 -o /tmp/m/s1m.obj > /dev/null || exit 1
-  ERAY_AB_MESH=/tmp/m/s1m.obj ERAY_AB_W=7680 ERAY_AB_H=4320 timeout -k 10 300 python scripts/ab_variants.py run head cur || exit 1
+  ERAY_AB_MESH=/tmp/m/s1m.obj ERAY_AB_W=7680 ERAY_AB_H=4320 timeout -k 10 300 python scripts/ab_variants.py run $V || exit 1
 fi
