@@ -147,6 +147,7 @@ struct FrameParams {
     const uint8_t* detail_occ;
     uint32_t detail_wgs;  // most workgroups of the frame kernel's grid doing detail work (0: all)
     uint32_t fill_first;  // the fill workgroups take the grid's first block indices (dispatched first)
+    uint32_t separate_fill;  // the frame kernel does detail work only; fill_kernel writes the background
     // general tracer (trace.hip): anti-aliasing rays per pixel, reflection depth, jitter seed;
     // aa == 0 && bounces == 0 selects the frame kernel
     uint32_t aa, bounces;

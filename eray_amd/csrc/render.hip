@@ -1307,6 +1307,53 @@ __device__ __forceinline__ bool inside(const SubRect& r, int32_t sx, int32_t sy)
     return sx >= r.sx0 && sx <= r.sx1 && sy >= r.sy0 && sy <= r.sy1;
 }
 
+// The background of the non-detail sub-blocks: fill workgroup f of nf strides over the 64 x 4
+// blocks (shared by the frame kernel's fill roles and fill_kernel).
+__device__ __forceinline__ void fill_blocks(const FrameParams& p, uint32_t f, uint32_t nf, uint32_t wave,
+                                            uint32_t lane, bool aligned) {
+    constexpr uint32_t nwaves = kWG / 64;
+    const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
+    const uint32_t fstride = nf * nwaves;
+    uint32_t occ = 0;  // detail list: lane i holds the occupancy of this wave's i-th next block
+    uint32_t it = 0;
+    // block coordinates advance incrementally (no integer division per block)
+    const uint32_t first = wave * nf + f, step_y = fstride / p.tiles_x, step_x = fstride - step_y * p.tiles_x;
+    uint32_t by = first / p.tiles_x, bx = first - by * p.tiles_x;
+    for (uint32_t blk = first; blk < nblk; blk += fstride, ++it) {
+        if (it) {
+            bx += step_x;
+            by += step_y;
+            if (bx >= p.tiles_x) {
+                bx -= p.tiles_x;
+                ++by;
+            }
+        }
+        uint32_t mask = 0;  // detail sub-blocks of this block
+        if (p.detail_occ) {  // one load per 64 blocks, not a dependent load per block
+            if ((it & 63u) == 0) {
+                const uint32_t b = blk + lane * fstride;
+                occ = b < nblk ? p.detail_occ[b] : 0u;
+            }
+            mask = (uint32_t)__builtin_amdgcn_readlane((int)occ, (int)(it & 63u));
+        }
+        for (uint32_t k = 0; k < p.nrect && !p.detail_occ; ++k) {
+            const SubRect r = frame_rect(p, k);
+            if ((int32_t)by < r.sy0 || (int32_t)by > r.sy1) continue;
+#pragma unroll
+            for (int32_t i = 0; i < 4; ++i) {
+                const int32_t sx = (int32_t)(4 * bx) + i;
+                mask |= (sx >= r.sx0 && sx <= r.sx1) ? (1u << i) : 0u;
+            }
+        }
+        if (!mask) {
+            fill_background<kBlkW>(p, bx * kBlkW, by * kBlkH, aligned, lane);
+        } else if (mask != 0xfu) {
+            for (uint32_t i = 0; i < 4; ++i)
+                if (!((mask >> i) & 1u)) fill_background<kSubW>(p, bx * kBlkW + i * kSubW, by * kBlkH, aligned, lane);
+        }
+    }
+}
+
 // kDense (large meshes only): 3 workgroups per CU instead of 2 (168 VGPRs, a few spilled), for
 // frames whose detail sub-blocks exceed one round of the 2-per-CU grid — there the detail waves
 // are VALU-issue bound and a second detail wave per SIMD doubles the issue slots (one wave alone
@@ -1428,50 +1475,19 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
 #ifdef ERAY_AB_X_NO_FILL  // diagnostics only (wrong images): the detail work alone
     if (p.nobj != 12345) return;
 #endif
+    if (p.separate_fill) return;  // fill_kernel writes the background beside this launch
     const uint32_t nf = nd < grid ? grid - nd : grid;  // filling workgroups
     const uint32_t f = nd < grid ? bid - nd : bid;
-    const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
-    const uint32_t fstride = nf * nwaves;
-    uint32_t occ = 0;  // detail list: lane i holds the occupancy of this wave's i-th next block
-    uint32_t it = 0;
-    // block coordinates advance incrementally (no integer division per block)
-    const uint32_t first = wave * nf + f, step_y = fstride / p.tiles_x, step_x = fstride - step_y * p.tiles_x;
-    uint32_t by = first / p.tiles_x, bx = first - by * p.tiles_x;
-    for (uint32_t blk = first; blk < nblk; blk += fstride, ++it) {
-        if (it) {
-            bx += step_x;
-            by += step_y;
-            if (bx >= p.tiles_x) {
-                bx -= p.tiles_x;
-                ++by;
-            }
-        }
-        uint32_t mask = 0;  // detail sub-blocks of this block
-        if (p.detail_occ) {  // one load per 64 blocks, not a dependent load per block
-            if ((it & 63u) == 0) {
-                const uint32_t b = blk + lane * fstride;
-                occ = b < nblk ? p.detail_occ[b] : 0u;
-            }
-            mask = (uint32_t)__builtin_amdgcn_readlane((int)occ, (int)(it & 63u));
-        }
-        for (uint32_t k = 0; k < p.nrect && !p.detail_occ; ++k) {
-            const SubRect r = frame_rect(p, k);
-            if ((int32_t)by < r.sy0 || (int32_t)by > r.sy1) continue;
-#pragma unroll
-            for (int32_t i = 0; i < 4; ++i) {
-                const int32_t sx = (int32_t)(4 * bx) + i;
-                mask |= (sx >= r.sx0 && sx <= r.sx1) ? (1u << i) : 0u;
-            }
-        }
-        if (!mask) {
-            fill_background<kBlkW>(p, bx * kBlkW, by * kBlkH, aligned, lane);
-        } else if (mask != 0xfu) {
-            for (uint32_t i = 0; i < 4; ++i)
-                if (!((mask >> i) & 1u)) fill_background<kSubW>(p, bx * kBlkW + i * kSubW, by * kBlkH, aligned, lane);
-        }
-    }
+    fill_blocks(p, f, nf, wave, lane, aligned);
     ERAY_TRACE(8);
     ERAY_TRACE_FLUSH();
+}
+
+// The background alone, beside a detail-only frame kernel on another stream (FrameParams::
+// separate_fill): small workgroups that hold few registers, so the fill waves do not take the
+// register budget of the large-mesh detail build.
+__global__ void __launch_bounds__(kWG) fill_kernel(FrameParams p) {
+    fill_blocks(p, blockIdx.x, gridDim.x, threadIdx.x >> 6, threadIdx.x & 63, p.aligned != 0);
 }
 
 // Image<Color>::save_as_ppm body: byte row k = image row h-1-k.
@@ -1570,6 +1586,52 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
     FrameParams q = p;
     q.detail_wgs = detail_wgs(share);
     q.fill_first = fill_first;
+    q.separate_fill = 0;
+    if constexpr (D) {
+        // Separate fill: the dense build does detail work only, at most 2 workgroups per CU, and
+        // fill_kernel's small workgroups (58 VGPRs) write the background beside it from a second
+        // stream (fork / join by events, which a graph capture records as two parallel nodes).
+        // Measured (profiles/ab/ab_sepfill.log): with many rounds of detail sub-blocks the detail
+        // waves get the register budget the fill roles held (C5's frame 216 -> 190 us); with
+        // ~2 rounds the single launch overlaps better (3840x2160 / 70k 27.9 vs 37.8 us).  Used
+        // above 16 detail sub-blocks per CU; knobs ERAY_SEPARATE_FILL (0 never, 1 always),
+        // ERAY_SEP_DETAIL_PER_CU, ERAY_SEP_FILL_PER_CU (diagnostics and tests).
+        const char* e_sep = getenv("ERAY_SEPARATE_FILL");
+        const bool separate = e_sep ? atoi(e_sep) > 0 : p.total_sub > 16u * (uint32_t)cus;
+        if (separate) {
+            const char* e_dpc = getenv("ERAY_SEP_DETAIL_PER_CU");
+            const char* e_fpc = getenv("ERAY_SEP_FILL_PER_CU");
+            const uint32_t dpc = e_dpc ? (uint32_t)atoi(e_dpc) : 2u, fpc = e_fpc ? (uint32_t)atoi(e_fpc) : 2u;
+            int dev = 0;
+            if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+            static hipStream_t side[64];
+            static hipEvent_t fork_ev[64], join_ev[64];
+            hipError_t e = hipSuccess;
+            if (!side[dev]) {
+                if ((e = hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking)) != hipSuccess ||
+                    (e = hipEventCreateWithFlags(&fork_ev[dev], hipEventDisableTiming)) != hipSuccess ||
+                    (e = hipEventCreateWithFlags(&join_ev[dev], hipEventDisableTiming)) != hipSuccess)
+                    return e;
+            }
+            q.separate_fill = 1;
+            q.detail_wgs = 0;
+            q.fill_first = 0;
+            const uint32_t dgrid =
+                max(1u, min(min(grid, max(dpc, 1u) * (uint32_t)cus), (p.total_sub + kWG / 64 - 1) / (kWG / 64)));
+            const uint32_t fgrid = max(1u, min(max(fpc, 1u) * (uint32_t)cus, (nblk + 3) / 4));
+            if ((e = hipEventRecord(fork_ev[dev], s)) != hipSuccess ||
+                (e = hipStreamWaitEvent(side[dev], fork_ev[dev], 0)) != hipSuccess)
+                return e;
+            frame_kernel<C, L, M, K, D><<<dgrid, kWG, dyn, s>>>(q.objects, q.lights, q.cull, q.tris, q.shade,
+                                                             q.nobj | (q.nlights << 16), q.total_tris, q.total_sub,
+                                                             dgrid, q);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            fill_kernel<<<fgrid, kWG, 0, side[dev]>>>(q);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            if ((e = hipEventRecord(join_ev[dev], side[dev])) != hipSuccess) return e;
+            return hipStreamWaitEvent(s, join_ev[dev], 0);
+        }
+    }
     frame_kernel<C, L, M, K, D><<<grid, kWG, dyn, s>>>(q.objects, q.lights, q.cull, q.tris, q.shade,
                                                     q.nobj | (q.nlights << 16), q.total_tris, q.total_sub, grid, q);
     return hipGetLastError();

@@ -316,14 +316,18 @@ def standin70k():
             np.ascontiguousarray(t[ft].reshape(-1, 6)))
 
 
-@pytest.mark.parametrize("dense,chunk", [("auto", None), ("0", None), ("1", None), ("auto", "9973")])
+@pytest.mark.parametrize("dense,chunk,separate", [("auto", None, None), ("0", None, None), ("1", None, "0"),
+                                                  ("1", None, "1"), ("auto", "9973", None)])
 @pytest.mark.parametrize("material", ["textures", "example"])
-def test_c3_binned_equals_brute_force(gpu, standin70k, material, dense, chunk, monkeypatch):
+def test_c3_binned_equals_brute_force(gpu, standin70k, material, dense, chunk, separate, monkeypatch):
     """Screen bins (bins.hip) for a 70k-face object: bit-identical to the brute-force scan, with
-    the large-mesh frame kernel at 2 and at 3 workgroups per CU (ERAY_DENSE_DETAIL), and with the
-    (face, bin) pairs compacted in many passes (ERAY_BIN_PAIR_CHUNK)."""
+    the large-mesh frame kernel at 2 and at 3 workgroups per CU (ERAY_DENSE_DETAIL), the dense
+    build with and without the separate fill kernel (ERAY_SEPARATE_FILL), and with the (face,
+    bin) pairs compacted in many passes (ERAY_BIN_PAIR_CHUNK)."""
     if dense != "auto":
         monkeypatch.setenv("ERAY_DENSE_DETAIL", dense)
+    if separate is not None:
+        monkeypatch.setenv("ERAY_SEPARATE_FILL", separate)
     if chunk:
         monkeypatch.setenv("ERAY_BIN_PAIR_CHUNK", chunk)
     W, H = 480, 270
@@ -337,12 +341,43 @@ def test_c3_binned_equals_brute_force(gpu, standin70k, material, dense, chunk, m
     assert np.array_equal(a[2], b[2])
 
 
-@pytest.mark.parametrize("dense", ["0", "1"])
-def test_c3_full_size_rows_match_oracle(gpu, oracle, standin70k, dense, monkeypatch):
+@pytest.mark.parametrize("separate", ["0", "1"])
+def test_dense_frames_graph_replay(gpu, standin70k, separate, monkeypatch):
+    """The dense large-mesh build replayed from a HIP graph, with the fill in the same launch and
+    as a second kernel on a forked stream (two parallel graph nodes joined by an event): every
+    replayed frame equals eray_render's brute-force frame."""
+    monkeypatch.setenv("ERAY_DENSE_DETAIL", "1")
+    monkeypatch.setenv("ERAY_SEPARATE_FILL", separate)
+    W, H = 480, 270
+    sc = MainScene(gpu, *standin70k, W, H, texture=256, fov=(16.0, 9.0))
+    ref = gpu_render(gpu, W, H, flags=capi.RENDER_BRUTE_FORCE)
+    rgb = gpu.empty((H, W, 3), np.float32)
+    ppm = gpu.empty((H, W, 3), np.uint8)
+    face = gpu.empty((H, W), np.int32)
+    try:
+        for frames in (1, 9):
+            gpu.memset(rgb.ptr, 0, rgb.nbytes)
+            gpu.memset(ppm.ptr, 0, ppm.nbytes)
+            gpu.memset(face.ptr, 0x7F, face.nbytes)
+            gpu.render_frames(frames, W, H, out_rgb=rgb.ptr, out_ppm=ppm.ptr, out_face=face.ptr)
+            gpu.synchronize()
+            assert_bit_equal(rgb.numpy(), ref[0], f"dense render_frames({frames}) separate={separate}")
+            assert np.array_equal(face.numpy(), ref[1])
+            assert np.array_equal(ppm.numpy(), ref[2])
+    finally:
+        for a in (rgb, ppm, face):
+            a.free()
+        sc.close()
+
+
+@pytest.mark.parametrize("dense,separate", [("0", "0"), ("1", "0"), ("1", "1")])
+def test_c3_full_size_rows_match_oracle(gpu, oracle, standin70k, dense, separate, monkeypatch):
     """C3 at 1920x1080 (bins built for the full camera) against the oracle on a row sample
     through the object, including row blocks rendered with a row phase (row0 % 4 != 0); the
-    large-mesh kernel at 2 and at 3 workgroups per CU."""
+    large-mesh kernel at 2 and at 3 workgroups per CU, the latter also beside the separate fill
+    kernel."""
     monkeypatch.setenv("ERAY_DENSE_DETAIL", dense)
+    monkeypatch.setenv("ERAY_SEPARATE_FILL", separate)
     W, H = 1920, 1080
     sc = MainScene(gpu, *standin70k, W, H, texture=256, fov=(16.0, 9.0))
     rgb, face, _ = gpu_render(gpu, W, H)
