@@ -1363,8 +1363,14 @@ template <bool kCull, bool kLdsTiles, int kMat, bool kLdsScene, bool kDense = fa
 __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && !kDense) ? 1 : 3)  // 3 workgroups per CU where that fits
     frame_kernel(const ObjectDesc* h_objects, const LightDesc* h_lights, const TriCull* h_cull, const TriHot* h_tris,
                  const TriShade* h_shade, uint32_t h_counts, uint32_t h_total_tris, uint32_t h_total_sub,
-                 uint32_t h_grid, FrameParams p) {
-    const FrameHot hot{h_objects, h_lights, h_cull, h_tris, h_shade, h_counts, h_total_tris, h_total_sub, h_grid};
+                 uint32_t h_roles, FrameParams p) {
+    // h_roles (a preloaded argument, see frame_roles): the grid size, the detail workgroups and
+    // the role flags, so the role decision — and the scene preload behind it — does not wait for
+    // a kernel-argument load from memory
+    const FrameHot hot{h_objects, h_lights, h_cull, h_tris, h_shade, h_counts, h_total_tris, h_total_sub,
+                       h_roles & 0x7fffu};
+    const uint32_t detail_wgs = (h_roles >> 15) & 0x7fffu;
+    const bool fill_first = (h_roles >> 30) & 1u, separate_fill = (h_roles >> 31) & 1u;
     // large objects: LDS tiles (shadow rays, brute force) and, aliased, the per-wave binned
     // primary search (first_hit ends its tile loop on a barrier, so the two never overlap)
     constexpr size_t kTileBytes = kTriTile * (sizeof(TriHot) + ((kCull && kLdsTiles) ? sizeof(TriCull) : 0));
@@ -1382,14 +1388,14 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     const uint32_t total = hot.total_sub;  // detail sub-blocks
     const uint32_t grid = hot.grid;        // == gridDim.x, without the implicit-argument load
     // workgroups [0, nd) render the detail sub-blocks (persistent: rounds of nd * 4 sub-blocks),
-    // the others write the background at the same time; at most p.detail_wgs detail workgroups
+    // the others write the background at the same time; at most detail_wgs detail workgroups
     // (the launcher keeps a share of the grid for the fill, so a large detail area overlaps the
     // fill's HBM writes instead of preceding them); when every workgroup has detail work, all of
     // them fill afterwards
-    const uint32_t nd = min(p.detail_wgs ? p.detail_wgs : grid, (total + nwaves - 1) / nwaves);
+    const uint32_t nd = min(detail_wgs ? detail_wgs : grid, (total + nwaves - 1) / nwaves);
     // the workgroup's role index: detail roles [0, nd), fill roles [nd, grid); with fill_first
     // the fill roles go to the first-dispatched (older, VALU-priority) workgroups
-    const uint32_t bid = (p.fill_first && nd < grid) ? (blockIdx.x + nd) % grid : blockIdx.x;
+    const uint32_t bid = (fill_first && nd < grid) ? (blockIdx.x + nd) % grid : blockIdx.x;
     ERAY_TRACE_CLEAR();
     ERAY_TRACE(0);
 
@@ -1475,7 +1481,7 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
 #ifdef ERAY_AB_X_NO_FILL  // diagnostics only (wrong images): the detail work alone
     if (p.nobj != 12345) return;
 #endif
-    if (p.separate_fill) return;  // fill_kernel writes the background beside this launch
+    if (separate_fill) return;  // fill_kernel writes the background beside this launch
     const uint32_t nf = nd < grid ? grid - nd : grid;  // filling workgroups
     const uint32_t f = nd < grid ? bid - nd : bid;
     fill_blocks(p, f, nf, wave, lane, aligned);
@@ -1538,6 +1544,12 @@ hipError_t launch_tri_rect(const TriCull* cull, uint32_t T, uint32_t cam_w, uint
 namespace {
 // Persistent grid: as many workgroups as are resident at once (occupancy API), capped by the
 // work (fill blocks or detail sub-blocks, whichever needs more workgroups).
+// frame_kernel's h_roles: grid | detail_wgs << 15 | fill_first << 30 | separate_fill << 31
+uint32_t frame_roles(uint32_t grid, const FrameParams& q) {
+    return (grid & 0x7fffu) | ((q.detail_wgs & 0x7fffu) << 15) | ((q.fill_first ? 1u : 0u) << 30) |
+           ((q.separate_fill ? 1u : 0u) << 31);
+}
+
 template <bool C, bool L, int M, bool K, bool D = false>
 hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, hipStream_t s) {
     static int per_cu = -1, cus = 0;
@@ -1624,7 +1636,7 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
                 return e;
             frame_kernel<C, L, M, K, D><<<dgrid, kWG, dyn, s>>>(q.objects, q.lights, q.cull, q.tris, q.shade,
                                                              q.nobj | (q.nlights << 16), q.total_tris, q.total_sub,
-                                                             dgrid, q);
+                                                             frame_roles(dgrid, q), q);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             fill_kernel<<<fgrid, kWG, 0, side[dev]>>>(q);
             if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1633,7 +1645,8 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
         }
     }
     frame_kernel<C, L, M, K, D><<<grid, kWG, dyn, s>>>(q.objects, q.lights, q.cull, q.tris, q.shade,
-                                                    q.nobj | (q.nlights << 16), q.total_tris, q.total_sub, grid, q);
+                                                    q.nobj | (q.nlights << 16), q.total_tris, q.total_sub,
+                                                    frame_roles(grid, q), q);
     return hipGetLastError();
 }
 
