@@ -1593,6 +1593,7 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
         share = 3.0f;
         fill_first = 1;
     }
+    if (L && !D) fill_first = 1;  // the 2-per-CU large-mesh build (C3): 13.0 -> 12.7-12.9 us
     if (e_share) share = (float)atof(e_share);
     if (e_first) fill_first = (uint32_t)atoi(e_first);
     FrameParams q = p;
