@@ -384,7 +384,11 @@ struct SceneLds {
     const TriShade* shades;
     const ObjectDesc* g_objs;  // the device arrays (scalar loads of uniform records)
     const LightDesc* g_lights;
-#ifdef ERAY_AB_SLOAD_UNIFORM
+    // Wave-uniform records (objects, materials, lights) by scalar loads from the device arrays,
+    // not LDS reads + readfirstlane: C2 8.67 -> 8.40 us per frame (profiles/ab/ab_c2chain.log),
+    // though one wave's chain alone is 0.2 us longer (7.26 -> 7.44 us, a 4-row frame).
+    // ERAY_AB_LDS_UNIFORM (A/B) restores the LDS reads.
+#ifndef ERAY_AB_LDS_UNIFORM
     __device__ ObjGeom geom(uint32_t i) const { return load_const(&g_objs[i].g, 0); }
     __device__ MaterialDesc mat(uint32_t i) const { return load_const(&g_objs[i].mat, 0); }
     __device__ LightDesc light(uint32_t i) const { return load_const(g_lights, i); }

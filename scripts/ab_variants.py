@@ -15,8 +15,7 @@ VARIANTS = {
     "base": (),
     "batch4": ("ERAY_AB_BATCH_FIXED",),
     "lazyray": ("ERAY_AB_LAZY_RAY",),
-    "sload": ("ERAY_AB_SLOAD_UNIFORM",),
-    "sload_lazy": ("ERAY_AB_SLOAD_UNIFORM", "ERAY_AB_LAZY_RAY"),
+    "lds_uniform": ("ERAY_AB_LDS_UNIFORM",),
     "global": ("ERAY_AB_NO_LDS_SCENE",),
     "x_noshadow": ("ERAY_AB_X_NO_SHADOW",),
     "x_notex": ("ERAY_AB_X_NO_TEXTURE",),
