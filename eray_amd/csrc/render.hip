@@ -384,6 +384,7 @@ struct SceneLds {
     const TriShade* shades;
     const ObjectDesc* g_objs;  // the device arrays (scalar loads of uniform records)
     const LightDesc* g_lights;
+    const TriHot* g_tris;
     // Wave-uniform records (objects, materials, lights) by scalar loads from the device arrays,
     // not LDS reads + readfirstlane: C2 8.67 -> 8.40 us per frame (profiles/ab/ab_c2chain.log),
     // though one wave's chain alone is 0.2 us longer (7.26 -> 7.44 us, a 4-row frame).
@@ -398,7 +399,11 @@ struct SceneLds {
     __device__ LightDesc light(uint32_t i) const { return lds_uniform(lights + i); }
 #endif
     __device__ TriCull cull(uint32_t g) const { return culls[g]; }
+#ifdef ERAY_AB_SLOAD_HOT  // A/B: the candidate record by scalar loads (C2 8.38 -> 8.72 us: slower)
+    __device__ TriHot hot(uint32_t g) const { return load_const(g_tris, g); }
+#else
     __device__ TriHot hot(uint32_t g) const { return hots[g]; }  // broadcast read (VGPRs)
+#endif
     __device__ TriHot hot_lane(uint32_t g) const { return hots[g]; }
     __device__ TriShade shade(uint32_t g) const { return shades[g]; }
 };
@@ -445,7 +450,7 @@ __device__ SceneLds preload_scene(const FrameHot& p, char* dyn, Meanwhile&& mean
     }
     return SceneLds{reinterpret_cast<const ObjectDesc*>(dyn + L.objs), reinterpret_cast<const LightDesc*>(dyn + L.lights),
                     reinterpret_cast<const TriCull*>(dyn + L.cull), reinterpret_cast<const TriHot*>(dyn + L.hot),
-                    reinterpret_cast<const TriShade*>(dyn + L.shade), p.objects, p.lights};
+                    reinterpret_cast<const TriShade*>(dyn + L.shade), p.objects, p.lights, p.tris};
 }
 
 // Lanes whose Triangle::intersects could pass: the det and t conditions of exact_test, from the

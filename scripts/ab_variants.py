@@ -16,6 +16,7 @@ VARIANTS = {
     "batch4": ("ERAY_AB_BATCH_FIXED",),
     "lazyray": ("ERAY_AB_LAZY_RAY",),
     "lds_uniform": ("ERAY_AB_LDS_UNIFORM",),
+    "sload_hot": ("ERAY_AB_SLOAD_HOT",),
     "global": ("ERAY_AB_NO_LDS_SCENE",),
     "x_noshadow": ("ERAY_AB_X_NO_SHADOW",),
     "x_notex": ("ERAY_AB_X_NO_TEXTURE",),
