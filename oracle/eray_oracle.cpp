@@ -557,11 +557,14 @@ int oracle_render(const oracle_object* objects, uint32_t object_count, const ora
                             row0, rows, bounces, 0, 0, out_rgb, out_face, out_object, stats);
 }
 
-int oracle_render_aa(const oracle_object* objects, uint32_t object_count, const oracle_light* lights,
-                     uint32_t light_count, const oracle_camera* cam, uint32_t image_width,
-                     uint32_t image_height, uint32_t row0, uint32_t rows, uint32_t bounces,
-                     uint32_t anti_aliasing, uint64_t seed, float* out_rgb, int32_t* out_face,
-                     int32_t* out_object, oracle_stats* stats) {
+// Engine::render restricted to the camera pixels [x0, x0 + cols) x rows [row0, row0 + rows):
+// the same per-pixel loop body (engine.rs:52-78), output pixel (x, y) at (y - row0) * stride +
+// (x - x0).  The whole-frame entry points pass x0 = 0, cols = camera width, stride = image width.
+static int render_region(const oracle_object* objects, uint32_t object_count, const oracle_light* lights,
+                         uint32_t light_count, const oracle_camera* cam, uint32_t image_width,
+                         uint32_t image_height, uint32_t row0, uint32_t rows, uint32_t x0, uint32_t cols,
+                         uint32_t stride, uint32_t bounces, uint32_t anti_aliasing, uint64_t seed, float* out_rgb,
+                         int32_t* out_face, int32_t* out_object, oracle_stats* stats) {
     Engine e;
     e.camera = to_camera(cam);
     e.bounces = bounces;
@@ -595,9 +598,12 @@ int oracle_render_aa(const oracle_object* objects, uint32_t object_count, const 
     if (width > 0 && height > 0 &&
         ((uint64_t)(height - 1) * image_width + (width - 1)) >= (uint64_t)image_width * image_height)
         return ORACLE_E_OOB;
+    if (cols == UINT32_MAX) cols = width;
+    if ((uint64_t)x0 + cols > width) return ORACLE_E_ARG;
+    if (stride == UINT32_MAX) stride = image_width;
     std::vector<Color> lighting;
     for (uint32_t y = row0; y < row0 + rows; ++y) {
-        for (uint32_t x = 0; x < width; ++x) {
+        for (uint32_t x = x0; x < x0 + cols; ++x) {
             Ray ray = pixel_to_ray(e.camera, (float)x / (float)width, (float)y / (float)height);
             int32_t face = -1, obj = -1;
             e.cast_ray(ray, 0, lighting, &face, &obj);
@@ -622,7 +628,7 @@ int oracle_render_aa(const oracle_object* objects, uint32_t object_count, const 
                 average = Color{rust_clamp(average.r / n, 0.0f, 1.0f), rust_clamp(average.g / n, 0.0f, 1.0f),
                                 rust_clamp(average.b / n, 0.0f, 1.0f)};
             }
-            size_t idx = (size_t)(y - row0) * image_width + x;
+            size_t idx = (size_t)(y - row0) * stride + (x - x0);
             out_rgb[3 * idx + 0] = average.r;
             out_rgb[3 * idx + 1] = average.g;
             out_rgb[3 * idx + 2] = average.b;
@@ -632,6 +638,24 @@ int oracle_render_aa(const oracle_object* objects, uint32_t object_count, const 
     }
     if (stats) *stats = e.stats;
     return ORACLE_OK;
+}
+
+int oracle_render_aa(const oracle_object* objects, uint32_t object_count, const oracle_light* lights,
+                     uint32_t light_count, const oracle_camera* cam, uint32_t image_width,
+                     uint32_t image_height, uint32_t row0, uint32_t rows, uint32_t bounces,
+                     uint32_t anti_aliasing, uint64_t seed, float* out_rgb, int32_t* out_face,
+                     int32_t* out_object, oracle_stats* stats) {
+    return render_region(objects, object_count, lights, light_count, cam, image_width, image_height, row0, rows, 0,
+                         UINT32_MAX, UINT32_MAX, bounces, anti_aliasing, seed, out_rgb, out_face, out_object, stats);
+}
+
+int oracle_render_span(const oracle_object* objects, uint32_t object_count, const oracle_light* lights,
+                       uint32_t light_count, const oracle_camera* cam, uint32_t row0, uint32_t rows, uint32_t x0,
+                       uint32_t cols, float* out_rgb, int32_t* out_face, oracle_stats* stats) {
+    uint32_t width, height;
+    camera_size(to_camera(cam), &width, &height);
+    return render_region(objects, object_count, lights, light_count, cam, width, height, row0, rows, x0, cols, cols,
+                         0, 0, 0, out_rgb, out_face, nullptr, stats);
 }
 
 int oracle_ppm_bytes(const float* rgb, uint32_t width, uint32_t height, uint8_t* out) {

@@ -120,6 +120,13 @@ int oracle_render_aa(const oracle_object* objects, uint32_t object_count,
                      uint32_t image_width, uint32_t image_height, uint32_t row0, uint32_t rows,
                      uint32_t bounces, uint32_t anti_aliasing, uint64_t seed, float* out_rgb,
                      int32_t* out_face, int32_t* out_object, oracle_stats* stats);
+/* Engine::render's loop body over the pixel span [x0, x0+cols) x camera rows [row0, row0+rows)
+ * (AA = 0, no bounces): out_rgb is rows x cols x 3 floats, out_face (optional) rows x cols.
+ * Lets a test check a few pixels of a frame whose full oracle render would take minutes. */
+int oracle_render_span(const oracle_object* objects, uint32_t object_count,
+                       const oracle_light* lights, uint32_t light_count, const oracle_camera* cam,
+                       uint32_t row0, uint32_t rows, uint32_t x0, uint32_t cols, float* out_rgb,
+                       int32_t* out_face, oracle_stats* stats);
 /* Philox4x32-10 (Salmon et al., SC'11; Random123's philox4x32 with 10 rounds) and the
  * gen_range(-1.0..1.0) mapping of one of its words. */
 void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);

@@ -243,6 +243,21 @@ def render(scene: Scene, cam: Camera, image_width=None, image_height=None, row0=
     return (out, faces, stats) if want_faces else (out, stats)
 
 
+def render_span(scene: Scene, cam: Camera, row0: int, rows: int, x0: int, cols: int):
+    """Pixels [x0, x0+cols) x camera rows [row0, row0+rows) of the frame (AA = 0, no bounces):
+    returns (rgb rows x cols x 3, faces rows x cols, stats)."""
+    out = np.zeros((rows, cols, 3), np.float32)
+    faces = np.full((rows, cols), -1, np.int32)
+    objs = (Object * max(1, len(scene.objects)))(*scene.objects)
+    lights = (Light * max(1, len(scene.lights)))(*scene.lights)
+    st = Stats()
+    rc = lib().oracle_render_span(objs, len(scene.objects), lights, len(scene.lights), C.byref(cam), row0, rows,
+                                  x0, cols, _fp(out), faces.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(st))
+    if rc:
+        raise ValueError(f"oracle_render_span status {rc}")
+    return out, faces, dict(primary_tests=st.primary_tests, shadow_tests=st.shadow_tests, hit_pixels=st.hit_pixels)
+
+
 def philox4x32_10(ctr, key):
     """Philox4x32-10 block (the anti-aliasing jitter stream, oracle_render_aa)."""
     c, k, o = (C.c_uint32 * 4)(*ctr), (C.c_uint32 * 2)(*key), (C.c_uint32 * 4)()

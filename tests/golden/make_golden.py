@@ -14,6 +14,9 @@ Fixtures
                     headers
   texture_8x4.npz   the example material graph (wave -> rgb -> mix with flat) at 8x4 texels:
                     color and diffuse images
+  c5_spans.npz      C5 (the 1M-face synthetic mesh, meshgen seed 1234, at 7680x4320, main.rs
+                    scene): pixel spans across the silhouette, the mesh centre and the row-tile
+                    boundary of the 8-GPU split (oracle_render_span), f32 RGB and faces
 """
 import hashlib
 import json
@@ -26,6 +29,7 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
+from eray_amd import meshgen  # noqa: E402
 from eray_amd.objfile import load_obj_file  # noqa: E402
 from oracle import pyoracle as O  # noqa: E402
 
@@ -38,11 +42,37 @@ def frame(mesh, w, h, fov):
     return rgb, face, stats
 
 
+# C5 spans (camera row, first column, columns): the 8-GPU split's middle tile boundary (camera
+# rows 2159 | 2160), the mesh centre, the left and right silhouettes, a row near the top of the
+# mesh, and one row block at another tile boundary (all background there, 16 pixels)
+C5_SPANS = [(2159, 3360, 48), (2160, 3360, 48), (2160, 3816, 48), (2160, 4252, 48), (2163, 3830, 20),
+            (1812, 3800, 64), (2507, 3700, 40), (1620, 100, 4)]
+
+
+def c5_mesh():
+    v, n, t, fv, ft, fn = meshgen.displaced_sphere(**meshgen.SYNTH_1M)
+    return (np.ascontiguousarray(v[fv].reshape(-1, 9)), np.ascontiguousarray(n[fn].reshape(-1, 9)),
+            np.ascontiguousarray(t[ft].reshape(-1, 6)))
+
+
+def c5_spans() -> None:
+    scene = O.main_rs_scene(*c5_mesh(), texture=1024)
+    cam = O.camera((0.0, 0.0, 5.0), (16.0, 9.0), 7680, 1.0)
+    assert O.camera_size(cam) == (7680, 4320)
+    out = {"spans": np.array(C5_SPANS, np.int32)}
+    for k, (y, x0, cols) in enumerate(C5_SPANS):
+        rgb, face, _ = O.render_span(scene, cam, y, 1, x0, cols)
+        out[f"rgb{k}"] = rgb[0]
+        out[f"face{k}"] = face[0]
+    np.savez_compressed(os.path.join(HERE, "c5_spans.npz"), **out)
+
+
 def main() -> None:
     mesh = load_obj_file(os.path.join(ROOT, "objects", "cube.obj"))
     digests = {}
     configs = {"c1": (256, 256, (60.0, 60.0)), "c2": (1920, 1080, (16.0, 9.0)),
-               "main_rs": (1024, 1024, (60.0, 60.0))}  # main.rs's own 1024x1024 render
+               "main_rs": (1024, 1024, (60.0, 60.0)),  # main.rs's own 1024x1024 render
+               "c4": (3840, 2160, (16.0, 9.0))}
     for tag, (w, h, fov) in configs.items():
         rgb, face, stats = frame(mesh, w, h, fov)
         full = O.ppm_bytes(rgb)  # the whole P6 file: header + body
@@ -68,6 +98,7 @@ def main() -> None:
                                 hit_rgb=rgb.reshape(-1, 3)[hit].astype(np.float32))
     with open(os.path.join(HERE, "digests.json"), "w") as f:
         json.dump(digests, f, indent=2, sort_keys=True)
+    c5_spans()
     color, diffuse = O.example_material(8, 4)
     np.savez_compressed(os.path.join(HERE, "texture_8x4.npz"), color=color, diffuse=diffuse)
     print("wrote", sorted(os.listdir(HERE)))

@@ -24,7 +24,7 @@ def _sha(a) -> str:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-@pytest.mark.parametrize("tag", ["c1", "c2"])
+@pytest.mark.parametrize("tag", ["c1", "c2", "c4"])
 def test_oracle_reproduces_digests(oracle, cube, tag):
     g = _digests()[tag]
     scene = oracle.main_rs_scene(*cube, texture=1024)
@@ -46,6 +46,19 @@ def test_oracle_reproduces_c1_fixture(oracle, cube):
     assert np.array_equal(rgb.reshape(-1, 3)[fx["hit_index"]], fx["hit_rgb"])
     body = oracle.ppm_bytes(rgb)[len(b"P6 256 256 255\n"):]
     assert np.array_equal(np.frombuffer(body, np.uint8).reshape(256, 256, 3), fx["ppm"])
+
+
+def test_oracle_reproduces_c5_span_fixture(oracle):
+    """Two of the C5 spans (1M faces at 7680x4320): the mesh centre and the right silhouette."""
+    from tests.golden.make_golden import c5_mesh
+    fx = np.load(os.path.join(GOLDEN, "c5_spans.npz"))
+    scene = oracle.main_rs_scene(*c5_mesh(), texture=1024)
+    cam = oracle.camera((0.0, 0.0, 5.0), (16.0, 9.0), 7680, 1.0)
+    for k in (3, 4):
+        y, x0, cols = (int(v) for v in fx["spans"][k])
+        rgb, face, _ = oracle.render_span(scene, cam, y, 1, x0, cols)
+        assert np.array_equal(face[0], fx[f"face{k}"])
+        assert rgb[0].view(np.uint32).tobytes() == fx[f"rgb{k}"].view(np.uint32).tobytes()
 
 
 def test_oracle_reproduces_texture_fixture(oracle):
