@@ -24,7 +24,7 @@ OBJ = os.path.join(PKG, "_obj")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "liberay_hip.so")
 
-SOURCES = ["render.hip", "trace.hip", "bins.hip", "shaderlib.hip", "capi.cpp"]
+SOURCES = ["render.hip", "setup.hip", "trace.hip", "bins.hip", "shaderlib.hip", "capi.cpp"]
 ARCH = "gfx950"
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
             f"--offload-arch={ARCH}", "-I" + os.path.join(ROOT, "include"),
@@ -52,19 +52,11 @@ def _headers() -> list[str]:
     return hs
 
 
-def build(jobs: int = 4, verbose: bool = False, force: bool = False, trace: bool = False,
-          variant: str = "", defines: tuple = ()) -> str:
-    """Build the product library; `trace` builds the diagnostic variant
-    lib/liberay_hip_trace.so instead (frame-kernel phase timestamps, ERAY_PHASE_TRACE).
-    `variant` + `defines`: a diagnostic A/B build lib/liberay_hip_<variant>.so with extra -D macros
-    (scripts/ab_variants.py); never the product library."""
-    tag = "trace" if trace else variant
-    obj_dir = os.path.join(OBJ, tag) if tag else OBJ
-    lib_path = LIB.replace(".so", f"_{tag}.so") if tag else LIB
-    extra = ["-DERAY_PHASE_TRACE"] if trace else []
-    extra += [f"-D{d}" for d in defines]
-    if trace and os.environ.get("ERAY_TRACE_REPEAT"):
-        extra.append("-DERAY_PHASE_TRACE_REPEAT")
+def build(jobs: int = 4, verbose: bool = False, force: bool = False) -> str:
+    """Build the product library (the only build: no diagnostic variants of the kernels)."""
+    obj_dir = OBJ
+    lib_path = LIB
+    extra: list[str] = []
     os.makedirs(obj_dir, exist_ok=True)
     os.makedirs(LIB_DIR, exist_ok=True)
     cc = hipcc()
@@ -149,10 +141,9 @@ def main() -> None:
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--force", action="store_true")
-    ap.add_argument("--trace", action="store_true", help="build the diagnostic phase-trace variant")
     ap.add_argument("--host", action="store_true", help="also build the C++ host (liberay_host.so, bin/)")
     a = ap.parse_args()
-    print(build(a.jobs, a.verbose, a.force, a.trace))
+    print(build(a.jobs, a.verbose, a.force))
     if a.host:
         print("\n".join(build_host(a.jobs, a.verbose, a.force)))
 

@@ -32,6 +32,10 @@ E_CYCLE = -12
 
 RENDER_DEFAULT = 0
 RENDER_BRUTE_FORCE = 1
+RENDER_DENSE_DETAIL = 2
+RENDER_NO_DENSE_DETAIL = 4
+RENDER_SEPARATE_FILL = 8
+RENDER_NO_SEPARATE_FILL = 16
 
 LIGHT_POINT = 0
 LIGHT_AMBIENT = 1
@@ -134,8 +138,18 @@ SIGNATURES = {
     "eray_render": (C.c_int, [_P, C.POINTER(RenderParams)]),
     "eray_render_frames": (C.c_int, [_P, C.POINTER(RenderParams), _U, C.POINTER(C.c_float)]),
     "eray_render_prepare": (C.c_int, [_P, C.POINTER(RenderParams), _U]),
+    "eray_render_camera_path": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(Camera), _U,
+                                          C.POINTER(C.c_float)]),
     "eray_pack_ppm": (C.c_int, [_P, _P, _U, _U, _P]),
     "eray_ppm_header": (C.c_int, [_U, _U, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+}
+
+# Diagnostics exported beside the header's API (not part of include/eray_hip.h).
+DEBUG_SIGNATURES = {
+    "eray_debug_bin_stats": (C.c_int, [_P, _U, C.POINTER(C.c_uint64)]),
+    "eray_debug_set_bin_capacity": (C.c_int, [_P, C.c_uint64]),
+    "eray_debug_bin_capacity": (C.c_uint64, [_P]),
+    "eray_debug_setup_state": (C.c_int, [_P, _U, _P, C.POINTER(C.c_int32)]),
 }
 
 _lib = None
@@ -169,6 +183,10 @@ def lib():
         _preload_hip_runtime()
         L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
         for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        for name, (res, args) in DEBUG_SIGNATURES.items():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
@@ -378,6 +396,21 @@ class Context:
             return None
         ms = C.c_float()
         self._check(lib().eray_render_frames(self._h, C.byref(p), frames, C.byref(ms) if timed else None))
+        return ms.value if timed else None
+
+    def render_camera_path(self, cameras, image_width, image_height, row0=0, rows=None, out_rgb=None,
+                           out_ppm=None, out_face=None, flags=RENDER_DEFAULT, timed=False, bounces=0,
+                           anti_aliasing=0, aa_seed=0):
+        """One frame per camera (Scene::set_camera + Engine::render each), the per-camera setup on
+        the device; returns the mean device ms per frame (setup included) when `timed`."""
+        if rows is None:
+            rows = image_height - row0
+        p = RenderParams(image_width, image_height, row0, rows, bounces, anti_aliasing, out_rgb or None,
+                         out_ppm or None, out_face or None, flags, aa_seed)
+        cams = (Camera * max(1, len(cameras)))(*cameras)
+        ms = C.c_float()
+        self._check(lib().eray_render_camera_path(self._h, C.byref(p), cams, len(cameras),
+                                                  C.byref(ms) if timed else None))
         return ms.value if timed else None
 
     def pack_ppm(self, rgb_ptr, w, h, out_ptr) -> None:

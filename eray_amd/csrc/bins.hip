@@ -1,24 +1,29 @@
-// bins.hip — screen bins of a large object's faces for the frame kernel's primary-ray scan.
-// A bin is one 16 x 4 pixel sub-block: exactly one wave's pixels.
+// bins.hip — screen bins of the large objects' faces for the frame kernel's primary-ray scan,
+// rebuilt per camera entirely on the device.  A bin is one 16 x 4 pixel sub-block: exactly one
+// wave's pixels.
 //
-// The per-face pixel rectangles (face_rect.hpp) say which pixel bins a face can be hit
-// in.  For objects too large to scan per wave (> kDirectMax faces) the frame kernel reads, for
-// its sub-block's bin, the list of those faces in INCREASING FACE INDEX (the reference's
-// first-hit order, object.rs:63-78) and runs the exact culling + tests on that list only: a face
-// outside the list cannot be hit by any ray of the bin, so the first hit is the reference's.
+// The per-face pixel rectangles (face_rect.hpp, setup.hip) say which bins a face can be hit in.
+// For objects too large to scan per wave (> kDirectMax faces) the frame kernel reads, for its
+// sub-block's bin, the faces that can be hit there and runs the exact tests on those only: a face
+// outside the bin's list cannot be hit by any ray of the bin.  The list need not be in index
+// order: the frame kernel keeps, per pixel, the smallest face index whose Triangle::intersects
+// passes, which is the reference's first hit (object.rs:63-78).
 //
 // Each entry also carries the bin's pixels the face may cover (bin_pixels: the four culling
 // bounds solved per pixel row), so the frame kernel only tests (face, pixel) pairs that can hit.
 //
-// Built once per camera / geometry change (and per row phase of the rendered rows):
-// each face's bin rectangle -> exclusive scan of the rectangles' areas (the (face, bin) pairs,
-// face-major) -> pixel masks of all pairs, one thread per pair (balanced: a near-silhouette
-// face's rectangle can span the frame's width, thousands of bins that one thread per face
-// walked alone) -> the non-empty pairs compacted in pair order, i.e. (bin, position) in face
-// order -> stable radix sort by bin (LSD: keeps face order within a bin) -> bin start offsets ->
-// faces, pixel masks and intersection records gathered in bin order.
+// Per camera, after camera_setup_kernel (each binned face's bin rectangle and its number of bins):
+//   exclusive scan of the rectangles' areas -> one thread per (face, bin) pair (a wave-uniform
+//   grid-stride loop over the total read on the device; the face found by binary search — a
+//   near-silhouette face's rectangle can span thousands of bins) computes the pair's pixel mask
+//   and appends the non-empty pairs (wave-aggregated slot counter) with a per-bin count ->
+//   exclusive scan of the counts -> each entry scattered to its bin (the per-bin count counted
+//   back down to zero for the next camera) -> the binned objects' rectangles narrowed to their
+//   non-empty bins, their bin views in the descriptors -> the detail sub-block list.
+// Buffers are preallocated (bins_alloc); if the pairs exceed the capacity the bins are dropped
+// for that camera (the frame kernel scans those objects through LDS tiles instead, still exact)
+// and CamState reports the count, so the host can grow the capacity.
 #include <algorithm>
-#include <cstdlib>
 
 #include <hipcub/hipcub.hpp>
 
@@ -29,129 +34,106 @@ namespace eray {
 namespace gpu {
 namespace {
 
-// per face: its bin rectangle (face_rect; empty: x0 > x1) and the rectangle's number of bins
-__global__ void __launch_bounds__(256) bin_range_kernel(const TriCull* __restrict__ cull, uint32_t T, uint32_t W,
-                                                        uint32_t H, uint32_t phase, int4* __restrict__ range,
-                                                        unsigned long long* __restrict__ area) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= T) return;
-    int32_t r[4];
-    int4 g = make_int4(1, 0, 1, 0);
-    unsigned long long a = 0;
-    if (face_rect(cull[i], W, H, r)) {
-        // bin row of camera row y: (y + kBinH - phase) / kBinH
-        g = make_int4(r[0] / (int32_t)kBinW, r[1] / (int32_t)kBinW,
-                      (r[2] + (int32_t)kBinH - (int32_t)phase) / (int32_t)kBinH,
-                      (r[3] + (int32_t)kBinH - (int32_t)phase) / (int32_t)kBinH);
-        a = (unsigned long long)(g.y - g.x + 1) * (unsigned long long)(g.w - g.z + 1);
-    }
-    range[i] = g;
-    area[i] = a;
+constexpr int kBinWG = 256;
+constexpr uint32_t kPairGrid = 2048;  // workgroups of the grid-stride pair and scatter loops
+
+__device__ __forceinline__ unsigned long long total_pairs(const unsigned long long* first,
+                                                          const unsigned long long* area, uint32_t T) {
+    return T ? first[T - 1] + area[T - 1] : 0ull;
 }
 
-// Pair j of [j0, j0 + len) (face-major, each face's bins row-major): its face (the last face
-// whose first pair is <= j), bin and pixel mask.  emit == false: only the number of non-empty
-// pairs, added to *nonempty; emit == true: the pair's mask, bin key and face, and a 0/1 flag.
-template <bool emit>
-__global__ void __launch_bounds__(256) bin_pairs_kernel(const TriCull* __restrict__ cull, const int4* __restrict__ range,
-                                                        const unsigned long long* __restrict__ first, uint32_t T,
-                                                        unsigned long long j0, uint32_t len, uint32_t W, uint32_t H,
-                                                        uint32_t phase, uint32_t bins_x,
-                                                        unsigned long long* __restrict__ nonempty,
-                                                        unsigned long long* __restrict__ pmask,
-                                                        uint32_t* __restrict__ pkey, uint32_t* __restrict__ pface,
-                                                        uint32_t* __restrict__ pflag) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    unsigned long long m = 0;
-    uint32_t key = 0, i = 0;
-    if (k < len) {
-        const unsigned long long j = j0 + k;
-        uint32_t lo = 0, hi = T;  // first face whose first pair is > j
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (first[mid] <= j) lo = mid + 1;
-            else hi = mid;
+// (face, bin) pairs of the binned faces' bin rectangles (face-major, each rectangle row-major):
+// the non-empty ones appended to the entry list, counted per bin key
+__global__ void __launch_bounds__(kBinWG) bin_pairs_kernel(const TriCull* __restrict__ cull,
+                                                           const int4* __restrict__ range,
+                                                           const unsigned long long* __restrict__ first,
+                                                           const unsigned long long* __restrict__ area,
+                                                           const uint32_t* __restrict__ fkey, uint32_t T, uint32_t W,
+                                                           uint32_t H, uint32_t phase, uint32_t bins_x, uint32_t nbins,
+                                                           uint32_t cap, uint32_t* __restrict__ n,
+                                                           uint32_t* __restrict__ count, uint32_t* __restrict__ ekey,
+                                                           uint32_t* __restrict__ eface,
+                                                           unsigned long long* __restrict__ emask) {
+    const unsigned long long P = total_pairs(first, area, T);
+    const uint32_t lane = threadIdx.x & 63;
+    const unsigned long long stride = (unsigned long long)gridDim.x * kBinWG;
+    for (unsigned long long base = (unsigned long long)blockIdx.x * kBinWG + (threadIdx.x & ~63u); base < P;
+         base += stride) {  // wave-uniform
+        const unsigned long long j = base + lane;
+        unsigned long long m = 0;
+        uint32_t key = 0, i = 0;
+        if (j < P) {
+            uint32_t lo = 0, hi = T;  // first face whose first pair is > j
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (first[mid] <= j) lo = mid + 1;
+                else hi = mid;
+            }
+            i = lo - 1;
+            const int4 g = range[i];
+            const uint32_t w = (uint32_t)(g.y - g.x + 1);
+            const uint32_t c = (uint32_t)(j - first[i]);
+            const uint32_t tx = (uint32_t)g.x + c % w, ty = (uint32_t)g.z + c / w;
+            m = bin_pixels(cull[i], W, H, phase, tx, ty);
+            key = fkey[i] * nbins + ty * bins_x + tx;
         }
-        i = lo - 1;
-        const int4 g = range[i];
-        const uint32_t w = (uint32_t)(g.y - g.x + 1);
-        const uint32_t c = (uint32_t)(j - first[i]);
-        const uint32_t tx = (uint32_t)g.x + c % w, ty = (uint32_t)g.z + c / w;
-        m = bin_pixels(cull[i], W, H, phase, tx, ty);
-        key = ty * bins_x + tx;
-    }
-    if constexpr (emit) {
-        if (k < len) {
-            pmask[k] = m;
-            pkey[k] = key;
-            pface[k] = i;
-            pflag[k] = m != 0;
+        const unsigned long long bal = __ballot(m != 0);
+        if (!bal) continue;
+        uint32_t slot0 = 0;
+        if (lane == (uint32_t)(__ffsll(bal) - 1)) slot0 = atomicAdd(n, (uint32_t)__popcll(bal));
+        slot0 = (uint32_t)__shfl((int)slot0, __ffsll(bal) - 1);
+        if (m) {
+            const uint32_t slot = slot0 + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+            if (slot < cap) {
+                ekey[slot] = key;
+                eface[slot] = i;
+                emask[slot] = m;
+                atomicAdd(count + key, 1u);
+            }
         }
-    } else {
-        const unsigned long long b = __ballot(m != 0);
-        if ((threadIdx.x & 63) == 0 && b) atomicAdd(nonempty, (unsigned long long)__popcll(b));
     }
 }
 
-// the non-empty pairs of a chunk at their compacted positions base + pos (pair order = face order)
-__global__ void __launch_bounds__(256) bin_emit_kernel(const unsigned long long* __restrict__ pmask,
-                                                       const uint32_t* __restrict__ pkey,
-                                                       const uint32_t* __restrict__ pface,
-                                                       const uint32_t* __restrict__ pflag,
-                                                       const uint32_t* __restrict__ pos, uint32_t len, uint32_t base,
-                                                       uint32_t* __restrict__ keys, uint32_t* __restrict__ order,
-                                                       uint32_t* __restrict__ tri, unsigned long long* __restrict__ mask) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= len || !pflag[k]) return;
-    const uint32_t o = base + pos[k];
-    keys[o] = pkey[k];
-    order[o] = o;  // emit positions increase with the face index
-    tri[o] = pface[k];
-    mask[o] = pmask[k];
-}
-
-// entries in bin order: face, pixel mask and intersection record
-__global__ void __launch_bounds__(256) bin_gather_kernel(const uint32_t* __restrict__ order,
-                                                         const uint32_t* __restrict__ tri_in,
-                                                         const unsigned long long* __restrict__ mask_in,
-                                                         const TriHot* __restrict__ hot, size_t n,
-                                                         uint32_t* __restrict__ tri_out,
-                                                         unsigned long long* __restrict__ mask_out,
-                                                         TriHot* __restrict__ hot_out) {
-    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    const uint32_t pos = order[j];
-    const uint32_t f = tri_in[pos];
-    tri_out[j] = f;
-    mask_out[j] = mask_in[pos];
-    hot_out[j] = hot[f];
-}
-
-// start[t] = first position of bin t in the sorted keys (start[nbins] = n): one thread per bin,
-// a lower bound over the keys (a thread per key filling the gap to the next key left the last
-// thread walking every bin after the last non-empty one: 0.85 ms at 3840x2160)
-__global__ void __launch_bounds__(256) bin_start_kernel(const uint32_t* __restrict__ keys, uint32_t n,
-                                                        uint32_t nbins, uint32_t* __restrict__ start) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t > nbins) return;
-    uint32_t lo = 0, hi = n;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (keys[mid] < t) lo = mid + 1;
-        else hi = mid;
+// every stored entry to its bin: start[key] + (the count, counted down to zero)
+__global__ void __launch_bounds__(kBinWG) bin_scatter_kernel(const uint32_t* __restrict__ n, uint32_t cap,
+                                                             const uint32_t* __restrict__ ekey,
+                                                             const uint32_t* __restrict__ eface,
+                                                             const unsigned long long* __restrict__ emask,
+                                                             const uint32_t* __restrict__ start,
+                                                             uint32_t* __restrict__ count,
+                                                             const uint32_t* __restrict__ kbegin, uint32_t nbins,
+                                                             const TriHot* __restrict__ hot, uint32_t* __restrict__ tri,
+                                                             unsigned long long* __restrict__ mask,
+                                                             TriHot* __restrict__ hot_out) {
+    const uint32_t total = min(*n, cap);
+    for (uint32_t e = blockIdx.x * kBinWG + threadIdx.x; e < total; e += gridDim.x * kBinWG) {
+        const uint32_t key = ekey[e], f = eface[e];
+        const uint32_t pos = start[key] + atomicSub(count + key, 1u) - 1u;
+        tri[pos] = f - kbegin[key / nbins];
+        mask[pos] = emask[e];
+        hot_out[pos] = hot[f];
     }
-    start[t] = lo;
 }
 
-// The pixel rectangle of the non-empty bins (camera pixels), accumulated as tri_rect_kernel's:
-// (~x0, x1 + 1, ~y0, y1 + 1) by atomicMax into zeroed words.
-__global__ void __launch_bounds__(256) bins_rect_kernel(const uint32_t* __restrict__ start, uint32_t bins_x,
-                                                        uint32_t nbins, uint32_t W, uint32_t H, uint32_t phase,
-                                                        uint32_t* __restrict__ acc) {
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t a[4] = {0u, 0u, 0u, 0u};
-    if (b < nbins && start[b + 1] > start[b]) {
-        const uint32_t bx = b % bins_x, by = b / bins_x;
+// The binned objects' non-empty bins -> their pixel rectangles (accumulated as the setup's:
+// (~x0, x1 + 1, ~y0, y1 + 1) by atomicMax); the last workgroup narrows each binned object's
+// rectangle to them, publishes its bin views (none on overflow) and resets the counters.
+__global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(const uint32_t* __restrict__ start, uint32_t nb,
+                                                               uint32_t bins_x, uint32_t nbins, uint32_t W, uint32_t H,
+                                                               uint32_t phase, uint32_t* __restrict__ acc,
+                                                               uint32_t* __restrict__ done, uint32_t* __restrict__ n,
+                                                               uint32_t cap, const uint32_t* __restrict__ kobj,
+                                                               ObjectDesc* __restrict__ objs, uint32_t* tri,
+                                                               unsigned long long* mask, TriHot* hot,
+                                                               CamState* __restrict__ st) {
+    __shared__ uint32_t s_last;
+    const uint32_t b = blockIdx.x * kBinWG + threadIdx.x;
+    const uint32_t keys = nb * nbins;
+    uint32_t a[4] = {0u, 0u, 0u, 0u}, k = 0;
+    if (b < keys && start[b + 1] > start[b]) {
+        k = b / nbins;
+        const uint32_t lb = b - k * nbins;
+        const uint32_t bx = lb % bins_x, by = lb / bins_x;
         const int32_t y0 = (int32_t)(by * kBinH + phase) - (int32_t)kBinH;
         const uint32_t x0 = bx * kBinW, x1 = min(x0 + kBinW, W) - 1;
         const uint32_t r0 = (uint32_t)max(y0, 0), r1 = (uint32_t)min(y0 + (int32_t)kBinH, (int32_t)H) - 1;
@@ -160,46 +142,72 @@ __global__ void __launch_bounds__(256) bins_rect_kernel(const uint32_t* __restri
         a[2] = ~r0;
         a[3] = r1 + 1u;
     }
+    const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k);
+    if (__all(k == k0 || a[1] == 0)) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-        for (int off = 32; off > 0; off >>= 1) a[k] = max(a[k], (uint32_t)__shfl_xor((int)a[k], off));
-    // one set of atomics per workgroup (per wave they serialised on the same four words)
-    __shared__ uint32_t s_a[4][4];
-    const uint32_t wave = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0)
-        for (int k = 0; k < 4; ++k) s_a[wave][k] = a[k];
+        for (int q = 0; q < 4; ++q)
+            for (int off = 32; off > 0; off >>= 1) a[q] = max(a[q], (uint32_t)__shfl_xor((int)a[q], off));
+        if ((threadIdx.x & 63) == 0 && a[1])
+            for (int q = 0; q < 4; ++q) atomicMax(acc + 4 * k0 + q, a[q]);
+    } else if (a[1]) {
+        for (int q = 0; q < 4; ++q) atomicMax(acc + 4 * k + q, a[q]);
+    }
+    __threadfence();
     __syncthreads();
-    if (threadIdx.x < 4) {  // (launched with 256 threads: four waves)
-        uint32_t m = 0, any = 0;
-        for (uint32_t w = 0; w < 4; ++w) {
-            m = max(m, s_a[w][threadIdx.x]);
-            any |= s_a[w][1];  // some bin of the workgroup is non-empty
+    if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    const uint32_t found = *n;
+    const bool overflow = found > cap;
+    for (uint32_t j = threadIdx.x; j < nb; j += kBinWG) {
+        uint32_t w[4];
+        for (int q = 0; q < 4; ++q) w[q] = atomicExch(acc + 4 * j + q, 0u);
+        ObjGeom& g = objs[kobj[j]].g;
+        if (overflow) {  // keep the face rectangles; the frame kernel scans through LDS tiles
+            g.bin_start = nullptr;
+            g.bin_tri = nullptr;
+            g.bin_mask = nullptr;
+            g.bin_hot = nullptr;
+            continue;
         }
-        if (any) atomicMax(acc + threadIdx.x, m);
+        // a pixel of an empty bin has no face whose culling bounds can pass there (bin_pixels),
+        // so no primary ray hits the object: its rectangle narrows to the non-empty bins
+        int32_t* r = g.rect;
+        if (w[1] == 0) {
+            r[0] = r[2] = 1;
+            r[1] = r[3] = 0;
+        } else {
+            r[0] = max(r[0], (int32_t)~w[0]);
+            r[1] = min(r[1], (int32_t)w[1] - 1);
+            r[2] = max(r[2], (int32_t)~w[2]);
+            r[3] = min(r[3], (int32_t)w[3] - 1);
+        }
+        g.bin_start = start + (size_t)j * nbins;
+        g.bin_tri = tri;
+        g.bin_mask = mask;
+        g.bin_hot = hot;
     }
-}
-
-template <typename T>
-hipError_t grow(T** p, size_t* cap, size_t need) {
-    if (*p && *cap >= need) return hipSuccess;
-    if (*p) {
-        hipError_t e = hipFree(*p);
-        if (e != hipSuccess) return e;
-        *p = nullptr;
+    if (threadIdx.x == 0) {
+        *n = 0u;
+        *done = 0u;
+        // the most entries any setup needed since the buffers were allocated (the host grows the
+        // capacity from it), and whether any overflowed
+        st->bin_entries = max(st->bin_entries, found);
+        st->bin_overflow |= overflow ? 1u : 0u;
+        st->nrect = 0u;
     }
-    *cap = 0;
-    hipError_t e = hipMalloc((void**)p, (need ? need : 1) * sizeof(T));
-    if (e == hipSuccess) *cap = need ? need : 1;
-    return e;
 }
 
 // Sub-block s = sy * (4 * tiles_x) + sx (padded rows: a 64 x 4 block's four sub-blocks are four
-// consecutive threads): listed when some object can be hit there (see build_detail_list).
-__global__ void __launch_bounds__(256) detail_flags_kernel(const ObjectDesc* __restrict__ objs, uint32_t nobj,
-                                                           uint32_t cam_w, uint32_t row0, uint32_t rows,
-                                                           uint32_t bins_x, uint32_t phase, uint32_t tiles_x,
-                                                           uint32_t n, uint8_t* __restrict__ flags,
-                                                           uint32_t* __restrict__ packed, uint8_t* __restrict__ occ) {
+// consecutive threads): listed when some object can be hit there — a binned object's bin is
+// non-empty (the frame kernel's bin of the sub-block, first_hit_binned) or another object's pixel
+// rectangle reaches it.
+__global__ void __launch_bounds__(kBinWG) detail_flags_kernel(const ObjectDesc* __restrict__ objs, uint32_t nobj,
+                                                              uint32_t cam_w, uint32_t row0, uint32_t rows,
+                                                              uint32_t bins_x, uint32_t phase, uint32_t tiles_x,
+                                                              uint32_t n, uint8_t* __restrict__ flags,
+                                                              uint32_t* __restrict__ packed, uint8_t* __restrict__ occ) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t row_subs = 4 * tiles_x;
     const uint32_t sx = s % row_subs, sy = s / row_subs;
@@ -210,7 +218,7 @@ __global__ void __launch_bounds__(256) detail_flags_kernel(const ObjectDesc* __r
         for (uint32_t oi = 0; oi < nobj && !hit; ++oi) {
             const ObjGeom& g = objs[oi].g;
             if (!g.tri_count) continue;
-            if (g.bin_start) {  // the frame kernel's bin of this sub-block (first_hit_binned)
+            if (g.bin_start) {
                 const uint32_t bin = ((row0 + sy * kBinH + kBinH - phase) / kBinH) * bins_x + sx;
                 hit = g.bin_start[bin + 1] > g.bin_start[bin];
             } else {
@@ -227,175 +235,103 @@ __global__ void __launch_bounds__(256) detail_flags_kernel(const ObjectDesc* __r
     if (s < n && (threadIdx.x & 3) == 0) occ[s / 4] = (uint8_t)((bal >> (threadIdx.x & 63)) & 0xfu);
 }
 
+template <typename T>
+hipError_t grow(T** p, size_t need) {
+    if (*p) {
+        hipError_t e = hipFree(*p);
+        if (e != hipSuccess) return e;
+        *p = nullptr;
+    }
+    return hipMalloc((void**)p, (need ? need : 1) * sizeof(T));
+}
+
 }  // namespace
 
-hipError_t build_detail_list(const ObjectDesc* objs, uint32_t nobj, uint32_t cam_w, uint32_t row0, uint32_t rows,
-                             uint32_t bins_x, uint32_t phase, uint32_t tiles_x, uint32_t* list, uint8_t* occ,
-                             uint32_t* count, hipStream_t s) {
-    const uint32_t subs_y = (rows + kBinH - 1) / kBinH;
-    const uint32_t n = 4 * tiles_x * subs_y;
-    *count = 0;
-    if (!n) return hipSuccess;
-    uint8_t* flags = nullptr;
-    uint32_t *packed = nullptr, *d_count = nullptr;
-    void* temp = nullptr;
-    auto done = [&](hipError_t err) {
-        for (void* q : {(void*)flags, (void*)packed, (void*)d_count, temp})
-            if (q) hipFree(q);
-        return err;
-    };
-    hipError_t e;
-    if ((e = hipMalloc((void**)&flags, n)) != hipSuccess) return done(e);
-    if ((e = hipMalloc((void**)&packed, sizeof(uint32_t) * n)) != hipSuccess) return done(e);
-    if ((e = hipMalloc((void**)&d_count, sizeof(uint32_t))) != hipSuccess) return done(e);
-    detail_flags_kernel<<<(n + 255) / 256, 256, 0, s>>>(objs, nobj, cam_w, row0, rows, bins_x, phase, tiles_x, n,
-                                                        flags, packed, occ);
-    if ((e = hipGetLastError()) != hipSuccess) return done(e);
-    size_t temp_bytes = 0;
-    if ((e = hipcub::DeviceSelect::Flagged(nullptr, temp_bytes, packed, flags, list, d_count, (int)n, s)) !=
-        hipSuccess)
-        return done(e);
-    if ((e = hipMalloc(&temp, temp_bytes ? temp_bytes : 1)) != hipSuccess) return done(e);
-    if ((e = hipcub::DeviceSelect::Flagged(temp, temp_bytes, packed, flags, list, d_count, (int)n, s)) != hipSuccess)
-        return done(e);
-    if ((e = hipMemcpyAsync(count, d_count, sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess ||
-        (e = hipStreamSynchronize(s)) != hipSuccess)
-        return done(e);
-    return done(hipSuccess);
+void bins_free(BinBuffers& b) {
+    void* ptrs[] = {b.first, b.count,  b.start,  b.kbegin, b.kobj,   b.n,       b.done,    b.acc,   b.ekey,
+                    b.eface, b.emask,  b.tri,    b.mask,   b.hot,    b.dflags,  b.dpacked, b.dlist, b.docc,
+                    b.temp};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+    b = BinBuffers{};
 }
 
-hipError_t launch_bins_rect(const uint32_t* start, uint32_t bins_x, uint32_t bins_y, uint32_t W, uint32_t H,
-                            uint32_t phase, uint32_t* acc, hipStream_t s) {
-    const uint32_t nbins = bins_x * bins_y;
-    if (!nbins) return hipSuccess;
-    bins_rect_kernel<<<(nbins + 255) / 256, 256, 0, s>>>(start, bins_x, nbins, W, H, phase, acc);
-    return hipGetLastError();
-}
-
-hipError_t build_bins(const TriCull* cull, const TriHot* hot, uint32_t T, uint32_t W, uint32_t H, uint32_t phase,
-                      uint32_t bins_x, uint32_t bins_y, ObjBins* out, hipStream_t s) {
-    const uint32_t nbins = bins_x * bins_y;
-    hipError_t e = grow(&out->start, &out->start_cap, (size_t)nbins + 1);
+hipError_t bins_alloc(BinBuffers& b, uint32_t T, uint32_t nb, const uint32_t* kbegin, const uint32_t* kobj, uint32_t W,
+                      uint32_t H, uint32_t phase, uint32_t tiles_x, uint32_t rows, size_t cap, hipStream_t s) {
+    hipError_t e = hipStreamSynchronize(s);  // the buffers may be in use by enqueued work
     if (e != hipSuccess) return e;
-    uint32_t *keys = nullptr, *keys2 = nullptr, *order = nullptr, *order2 = nullptr, *tri = nullptr;
-    uint32_t *pkey = nullptr, *pface = nullptr, *pflag = nullptr, *pos = nullptr;
-    unsigned long long *mask = nullptr, *area = nullptr, *first = nullptr, *d_n = nullptr, *pmask = nullptr;
-    int4* range = nullptr;
-    void* temp = nullptr;
-    size_t n = 0;
-    unsigned long long pairs = 0;  // (face, bin) pairs of the faces' bin rectangles
-    auto done = [&](hipError_t err) {
-        for (void* q : {(void*)keys, (void*)keys2, (void*)order, (void*)order2, (void*)tri, (void*)pkey,
-                        (void*)pface, (void*)pflag, (void*)pos, (void*)mask, (void*)area, (void*)first, (void*)d_n,
-                        (void*)pmask, (void*)range, temp})
-            if (q) hipFree(q);
-        return err;
-    };
-    // scratch scans: one temp buffer, grown to the largest request
-    size_t temp_cap = 0;
-    auto temp_for = [&](size_t bytes) -> hipError_t {
-        if (temp && temp_cap >= bytes) return hipSuccess;
-        if (temp) hipFree(temp);
-        temp = nullptr;
-        temp_cap = 0;
-        const hipError_t err = hipMalloc(&temp, bytes ? bytes : 1);
-        if (err == hipSuccess) temp_cap = bytes;
-        return err;
-    };
-    // pairs per pass (24 B of scratch each); tests shrink it (ERAY_BIN_PAIR_CHUNK) to cover the
-    // multi-pass compaction
-    const char* e_chunk = getenv("ERAY_BIN_PAIR_CHUNK");
-    const unsigned long long kPairChunk = e_chunk && atoll(e_chunk) > 0 ? (unsigned long long)atoll(e_chunk) : 1ull << 24;
-    if (T) {
-        if ((e = hipMalloc((void**)&range, sizeof(int4) * T)) != hipSuccess) return done(e);
-        if ((e = hipMalloc((void**)&area, sizeof(unsigned long long) * T)) != hipSuccess) return done(e);
-        if ((e = hipMalloc((void**)&first, sizeof(unsigned long long) * T)) != hipSuccess) return done(e);
-        if ((e = hipMalloc((void**)&d_n, sizeof(unsigned long long))) != hipSuccess) return done(e);
-        bin_range_kernel<<<(T + 255) / 256, 256, 0, s>>>(cull, T, W, H, phase, range, area);
-        if ((e = hipGetLastError()) != hipSuccess) return done(e);
-        size_t temp_bytes = 0;
-        if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, temp_bytes, area, first, T, s)) != hipSuccess ||
-            (e = temp_for(temp_bytes)) != hipSuccess ||
-            (e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, area, first, T, s)) != hipSuccess)
-            return done(e);
-        unsigned long long last[2];
-        if ((e = hipMemcpyAsync(&last[0], first + T - 1, 8, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-            (e = hipMemcpyAsync(&last[1], area + T - 1, 8, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-            (e = hipMemsetAsync(d_n, 0, sizeof(unsigned long long), s)) != hipSuccess ||
-            (e = hipStreamSynchronize(s)) != hipSuccess)
-            return done(e);
-        pairs = last[0] + last[1];
-        // the non-empty pairs (count only)
-        for (unsigned long long j0 = 0; j0 < pairs; j0 += kPairChunk) {
-            const uint32_t len = (uint32_t)std::min(kPairChunk, pairs - j0);
-            bin_pairs_kernel<false><<<(len + 255) / 256, 256, 0, s>>>(cull, range, first, T, j0, len, W, H, phase,
-                                                                      bins_x, d_n, nullptr, nullptr, nullptr, nullptr);
-            if ((e = hipGetLastError()) != hipSuccess) return done(e);
-        }
-        unsigned long long nn = 0;
-        if ((e = hipMemcpyAsync(&nn, d_n, 8, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-            (e = hipStreamSynchronize(s)) != hipSuccess)
-            return done(e);
-        if (nn >= (1ull << 31)) return done(hipErrorOutOfMemory);  // entries are indexed by int (radix sort)
-        n = (size_t)nn;
+    bins_free(b);
+    b.nb = nb;
+    b.T = T;
+    b.bins_x = (W + kBinW - 1) / kBinW;
+    b.bins_y = H ? (H - 1 + kBinH - phase) / kBinH + 1 : 1;
+    b.nbins = b.bins_x * b.bins_y;
+    b.phase = phase;
+    b.cap = cap;
+    const size_t keys = (size_t)nb * b.nbins;
+    const uint32_t subs_y = (rows + kBinH - 1) / kBinH;
+    b.nsub = 4 * (size_t)tiles_x * subs_y;
+    if ((e = grow(&b.first, T)) != hipSuccess || (e = grow(&b.count, keys + 1)) != hipSuccess ||
+        (e = grow(&b.start, keys + 1)) != hipSuccess || (e = grow(&b.kbegin, nb)) != hipSuccess ||
+        (e = grow(&b.kobj, nb)) != hipSuccess || (e = grow(&b.n, 1)) != hipSuccess ||
+        (e = grow(&b.done, 1)) != hipSuccess || (e = grow(&b.acc, 4 * (size_t)nb)) != hipSuccess ||
+        (e = grow(&b.ekey, cap)) != hipSuccess || (e = grow(&b.eface, cap)) != hipSuccess ||
+        (e = grow(&b.emask, cap)) != hipSuccess || (e = grow(&b.tri, cap)) != hipSuccess ||
+        (e = grow(&b.mask, cap)) != hipSuccess || (e = grow(&b.hot, cap)) != hipSuccess ||
+        (e = grow(&b.dflags, b.nsub)) != hipSuccess || (e = grow(&b.dpacked, b.nsub)) != hipSuccess ||
+        (e = grow(&b.dlist, b.nsub)) != hipSuccess || (e = grow(&b.docc, (size_t)tiles_x * subs_y)) != hipSuccess)
+        return e;
+    // counters zero between builds (each build leaves them so)
+    if ((e = hipMemsetAsync(b.count, 0, sizeof(uint32_t) * (keys + 1), s)) != hipSuccess ||
+        (e = hipMemsetAsync(b.n, 0, sizeof(uint32_t), s)) != hipSuccess ||
+        (e = hipMemsetAsync(b.done, 0, sizeof(uint32_t), s)) != hipSuccess ||
+        (e = hipMemsetAsync(b.acc, 0, sizeof(uint32_t) * 4 * nb, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(b.kbegin, kbegin, sizeof(uint32_t) * nb, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(b.kobj, kobj, sizeof(uint32_t) * nb, hipMemcpyHostToDevice, s)) != hipSuccess)
+        return e;
+    // hipcub scratch: the largest of the three device-wide passes
+    size_t t1 = 0, t2 = 0, t3 = 0;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, t1, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                              (int)std::max<uint32_t>(T, 1u), s)) != hipSuccess ||
+        (e = hipcub::DeviceScan::ExclusiveSum(nullptr, t2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)(keys + 1), s)) !=
+            hipSuccess ||
+        (e = hipcub::DeviceSelect::Flagged(nullptr, t3, (uint32_t*)nullptr, (uint8_t*)nullptr, (uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, (int)std::max<size_t>(b.nsub, 1), s)) != hipSuccess)
+        return e;
+    b.temp_bytes = std::max(std::max(t1, t2), t3);
+    if ((e = hipMalloc(&b.temp, b.temp_bytes ? b.temp_bytes : 1)) != hipSuccess) return e;
+    return hipStreamSynchronize(s);  // the host arrays above are the caller's
+}
+
+hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tiles_x, hipStream_t s) {
+    hipError_t e;
+    const size_t keys = (size_t)b.nb * b.nbins;
+    size_t tb = b.temp_bytes;
+    if (b.T) {
+        if ((e = hipcub::DeviceScan::ExclusiveSum(b.temp, tb, sp.area, b.first, (int)b.T, s)) != hipSuccess) return e;
+        bin_pairs_kernel<<<kPairGrid, kBinWG, 0, s>>>(sp.cull, sp.range, b.first, sp.area, sp.fkey, b.T, sp.W, sp.H,
+                                                      sp.phase, b.bins_x, b.nbins, (uint32_t)b.cap, b.n, b.count,
+                                                      b.ekey, b.eface, b.emask);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    if ((e = grow(&out->tri, &out->tri_cap, n)) != hipSuccess) return done(e);
-    if ((e = grow(&out->mask, &out->mask_cap, n)) != hipSuccess) return done(e);
-    if ((e = grow(&out->hot, &out->hot_cap, n)) != hipSuccess) return done(e);
-    out->n = n;
-    if (n) {
-        for (uint32_t** q : {&keys, &keys2, &order, &order2, &tri})
-            if ((e = hipMalloc((void**)q, sizeof(uint32_t) * n)) != hipSuccess) return done(e);
-        if ((e = hipMalloc((void**)&mask, sizeof(unsigned long long) * n)) != hipSuccess) return done(e);
-        const size_t chunk = (size_t)std::min(kPairChunk, pairs);
-        if ((e = hipMalloc((void**)&pmask, sizeof(unsigned long long) * chunk)) != hipSuccess) return done(e);
-        for (uint32_t** q : {&pkey, &pface, &pflag, &pos})
-            if ((e = hipMalloc((void**)q, sizeof(uint32_t) * chunk)) != hipSuccess) return done(e);
-        // the pairs again, now written out, and compacted in pair order (= face order)
-        uint32_t base = 0;
-        for (unsigned long long j0 = 0; j0 < pairs; j0 += kPairChunk) {
-            const uint32_t len = (uint32_t)std::min(kPairChunk, pairs - j0);
-            bin_pairs_kernel<true><<<(len + 255) / 256, 256, 0, s>>>(cull, range, first, T, j0, len, W, H, phase,
-                                                                     bins_x, nullptr, pmask, pkey, pface, pflag);
-            if ((e = hipGetLastError()) != hipSuccess) return done(e);
-            size_t temp_bytes = 0;
-            if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, temp_bytes, pflag, pos, len, s)) != hipSuccess ||
-                (e = temp_for(temp_bytes)) != hipSuccess ||
-                (e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, pflag, pos, len, s)) != hipSuccess)
-                return done(e);
-            bin_emit_kernel<<<(len + 255) / 256, 256, 0, s>>>(pmask, pkey, pface, pflag, pos, len, base, keys, order,
-                                                              tri, mask);
-            if ((e = hipGetLastError()) != hipSuccess) return done(e);
-            if (j0 + len < pairs) {  // the next chunk's base
-                uint32_t last[2];
-                if ((e = hipMemcpyAsync(&last[0], pos + len - 1, 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-                    (e = hipMemcpyAsync(&last[1], pflag + len - 1, 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-                    (e = hipStreamSynchronize(s)) != hipSuccess)
-                    return done(e);
-                base += last[0] + last[1];
-            }
-        }
-        if ((e = hipGetLastError()) != hipSuccess) return done(e);
-        int end_bit = 1;
-        while (end_bit < 32 && (1ull << end_bit) < (unsigned long long)nbins) ++end_bit;
-        hipcub::DoubleBuffer<uint32_t> kb(keys, keys2), vb(order, order2);
-        size_t temp_bytes = 0;
-        if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, kb, vb, (int)n, 0, end_bit, s)) !=
-                hipSuccess ||
-            (e = temp_for(temp_bytes)) != hipSuccess)
-            return done(e);
-        if ((e = hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, kb, vb, (int)n, 0, end_bit, s)) != hipSuccess)
-            return done(e);
-        bin_start_kernel<<<(nbins + 1 + 255) / 256, 256, 0, s>>>(kb.Current(), (uint32_t)n, nbins, out->start);
-        if ((e = hipGetLastError()) != hipSuccess) return done(e);
-        bin_gather_kernel<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(vb.Current(), tri, mask, hot, n, out->tri,
-                                                                       out->mask, out->hot);
-    } else {
-        bin_start_kernel<<<(nbins + 1 + 255) / 256, 256, 0, s>>>(nullptr, 0, nbins, out->start);
-    }
-    if ((e = hipGetLastError()) != hipSuccess) return done(e);
-    e = hipStreamSynchronize(s);  // the scratch buffers are freed below
-    return done(e);
+    tb = b.temp_bytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(b.temp, tb, b.count, b.start, (int)(keys + 1), s)) != hipSuccess) return e;
+    bin_scatter_kernel<<<kPairGrid, kBinWG, 0, s>>>(b.n, (uint32_t)b.cap, b.ekey, b.eface, b.emask, b.start, b.count,
+                                                    b.kbegin, b.nbins, sp.hot, b.tri, b.mask, b.hot);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const uint32_t fgrid = (uint32_t)std::max<size_t>((keys + kBinWG - 1) / kBinWG, 1);
+    bins_finalize_kernel<<<fgrid, kBinWG, 0, s>>>(b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase, b.acc, b.done,
+                                                  b.n, (uint32_t)b.cap, b.kobj, sp.objs, b.tri, b.mask, b.hot,
+                                                  sp.state);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (!b.nsub) return hipSuccess;
+    const uint32_t n = (uint32_t)b.nsub;
+    detail_flags_kernel<<<(n + kBinWG - 1) / kBinWG, kBinWG, 0, s>>>(sp.objs, sp.nobj, sp.W, sp.row0, sp.rows,
+                                                                    b.bins_x, b.phase, tiles_x, n, b.dflags,
+                                                                    b.dpacked, b.docc);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    tb = b.temp_bytes;
+    return hipcub::DeviceSelect::Flagged(b.temp, tb, b.dpacked, b.dflags, b.dlist, &sp.state->total_sub, (int)n, s);
 }
 
 }  // namespace gpu

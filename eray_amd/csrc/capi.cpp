@@ -81,7 +81,8 @@ struct eray_ctx {
     std::vector<eray_light> lights;
     std::vector<HostObject> objects;
 
-    bool geom_dirty = true, desc_dirty = true, cull_dirty = true;
+    bool geom_dirty = true, desc_dirty = true;
+    uint64_t scene_gen = 0;  // bumped whenever geometry or descriptors are uploaded
     TriHot* d_hot = nullptr;
     TriShade* d_shade = nullptr;
     TriCull* d_cull = nullptr;
@@ -92,9 +93,10 @@ struct eray_ctx {
     size_t objs_cap = 0;
     LightDesc* d_lights = nullptr;
     size_t lights_cap = 0;
-    // launch plans of eray_render_frames: HIP graphs of back-to-back frame launches (chunks of up
-    // to kGraphFrames frames and remainders), each cached for the frame parameters + stream +
-    // length it was captured with; the least recently used is evicted beyond kGraphCache
+    // launch plans of eray_render_frames / eray_render_camera_path: HIP graphs of back-to-back
+    // frames (chunks of up to kGraphFrames frames and remainders), each cached for the frame
+    // parameters + stream + length + kind it was captured with; the least recently used is
+    // evicted beyond kGraphCache
     struct FrameGraph {
         hipGraph_t graph = nullptr;
         hipGraphExec_t exec = nullptr;
@@ -103,31 +105,45 @@ struct eray_ctx {
     };
     std::vector<FrameGraph> graphs;
     uint64_t graph_clock = 0;
-    uint32_t* d_rect = nullptr;  // per-object pixel-rectangle accumulators (4 x uint32)
-    std::vector<int32_t> face_rects;  // per object: the union of its faces' rectangles (4 x int32)
-    size_t rect_cap = 0;
-    std::vector<uint32_t> h_rect;
-    // screen bins of the large objects' faces (bins.hip), per object; valid for bins_phase
-    std::vector<ObjBins> bins;
-    bool bins_dirty = true;
-    uint32_t bins_phase = 0;
-    uint64_t bins_gen = 0;  // bumped whenever the bins (and the rectangles) are rebuilt
-    // detail sub-block list of the last rendered rows (scenes with binned objects)
-    uint32_t* d_detail_list = nullptr;
-    size_t detail_list_cap = 0;
-    uint8_t* d_detail_occ = nullptr;
-    size_t detail_occ_cap = 0;
-    std::vector<uint64_t> detail_key;
-    uint32_t detail_count = 0;
     uint32_t* d_prog = nullptr;  // every object's texel program (MaterialDesc::prog), concatenated
     size_t prog_cap = 0;
     std::vector<uint32_t> h_prog;
     std::vector<ObjectDesc> h_objs;  // kept alive for the async uploads
     std::vector<LightDesc> h_lights;
     std::vector<float> h_raw;
+    std::vector<uint32_t> h_begin;   // obj_begin (nobj + 1) | objkey (nobj), uploaded with the descriptors
     uint32_t total_tris = 0;
     bool spec_pow = false;     // some material has a specular-power output
     bool example_mat = false;  // some material is main.rs's graph evaluated per hit
+    // ---- per-camera setup (setup.hip, bins.hip), all on the device
+    CamDev* d_cam = nullptr;      // the context camera's device slot
+    CamState* d_state = nullptr;  // the last setup's results
+    CamState* h_state = nullptr;  // pinned host copy, valid once state_ev has completed
+    hipEvent_t state_ev = nullptr;
+    bool state_pending = false;   // a copy into h_state is in flight
+    bool state_known = false;     // h_state holds the results of the setup of setup_key
+    std::vector<uint64_t> setup_key;  // camera, size, rows and scene generation of the last setup
+    uint32_t* d_acc = nullptr;    // setup rectangle accumulators (4 x nobj) + done counter
+    size_t acc_cap = 0;
+    uint32_t* d_begin = nullptr;  // obj_begin | objkey
+    size_t begin_cap = 0;
+    int4* d_range = nullptr;      // binned faces' bin rectangles, areas, binned-object index
+    unsigned long long* d_area = nullptr;
+    uint32_t* d_fkey = nullptr;
+    size_t face_cap = 0;
+    BinBuffers bins;
+    std::vector<uint64_t> bins_layout;
+    size_t bin_cap = 0;           // entry capacity to allocate (grown when a setup overflows)
+    // camera paths (eray_render_camera_path): the cameras of the current graph chunk on the
+    // device, the whole path staged in pinned memory
+    CamDev* d_path = nullptr;
+    size_t path_cap = 0;
+    CamDev* d_path_all = nullptr;
+    size_t path_all_cap = 0;
+    CamDev* h_path = nullptr;
+    size_t h_path_cap = 0;
+    hipEvent_t path_ev = nullptr;  // the last path upload (h_path reusable once complete)
+    LaunchCtx lc{nullptr, nullptr, nullptr};  // the separate fill's stream and events
 };
 
 namespace {
@@ -183,7 +199,7 @@ uint32_t sat_u32_host(float f) {
 bool image_ok(const eray_image& im) { return !im.data || (im.width > 0 && im.height > 0); }
 TexView tex(const eray_image& im) { return TexView{im.data, im.width, im.height}; }
 
-int sync_scene(eray_ctx* ctx, bool need_cull) {
+int sync_scene(eray_ctx* ctx) {
     int st;
     // The host staging vectors below feed async copies: drain earlier ones before reuse.
     if (ctx->geom_dirty || ctx->desc_dirty) HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -225,7 +241,6 @@ int sync_scene(eray_ctx* ctx, bool need_cull) {
                                                ctx->d_shade, ctx->stream));
         }
         ctx->geom_dirty = false;
-        ctx->cull_dirty = true;
         ctx->desc_dirty = true;
     }
     if (ctx->desc_dirty) {
@@ -322,141 +337,162 @@ int sync_scene(eray_ctx* ctx, bool need_cull) {
             HIP_TRY(ctx, hipMemcpyAsync(ctx->d_lights, ctx->h_lights.data(),
                                         sizeof(LightDesc) * ctx->h_lights.size(), hipMemcpyHostToDevice,
                                         ctx->stream));
+        // setup.hip's object ranges and binned-object indices
+        const uint32_t nobj = (uint32_t)ctx->objects.size();
+        ctx->h_begin.assign(2 * (size_t)nobj + 1, 0u);
+        uint32_t nb = 0;
+        for (uint32_t i = 0; i < nobj; ++i) {
+            ctx->h_begin[i] = ctx->h_objs[i].g.tri_begin;
+            ctx->h_begin[nobj + 1 + i] = ctx->objects[i].T > kDirectMax ? nb++ : ~0u;
+        }
+        ctx->h_begin[nobj] = ctx->total_tris;
+        if ((st = ensure(ctx, &ctx->d_begin, &ctx->begin_cap, ctx->h_begin.size()))) return st;
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->d_begin, ctx->h_begin.data(), 4 * ctx->h_begin.size(), hipMemcpyHostToDevice,
+                                    ctx->stream));
+        // rectangle accumulators + the setup's workgroup counter, zero between setups
+        if (ctx->acc_cap < 4 * (size_t)nobj + 1 || !ctx->d_acc) {
+            if ((st = ensure(ctx, &ctx->d_acc, &ctx->acc_cap, 4 * (size_t)nobj + 1))) return st;
+            HIP_TRY(ctx, hipMemsetAsync(ctx->d_acc, 0, 4 * ctx->acc_cap, ctx->stream));
+        }
         ctx->desc_dirty = false;
-        ctx->cull_dirty = true;  // the rectangles live in the descriptors just rebuilt
+        ++ctx->scene_gen;
     }
-    if (need_cull && ctx->cull_dirty) {
-        const eray_camera& c = ctx->camera;
-        HIP_TRY(ctx, launch_tri_cull(ctx->d_hot, ctx->total_tris, c.center[0], c.center[1], c.center[2],
-                                     c.fov[0] / c.fov[1], c.z_dist, ctx->d_cull, ctx->stream));
-        // each object's pixel rectangle (where its faces can be hit by a primary ray), read back
-        // once per camera / geometry change and carried in the object descriptors
-        const size_t nobj = ctx->objects.size();
-        uint32_t W, H;
-        eray_camera_size(&c, &W, &H);
-        if (nobj) {
-            if ((st = ensure(ctx, &ctx->d_rect, &ctx->rect_cap, 4 * nobj))) return st;
-            HIP_TRY(ctx, hipMemsetAsync(ctx->d_rect, 0, sizeof(uint32_t) * 4 * nobj, ctx->stream));
-            for (size_t i = 0; i < nobj; ++i)
-                HIP_TRY(ctx, launch_tri_rect(ctx->d_cull + ctx->h_objs[i].g.tri_begin, ctx->h_objs[i].g.tri_count, W, H,
-                                             ctx->d_rect + 4 * i, ctx->stream));
-            ctx->h_rect.assign(4 * nobj, 0u);
-            HIP_TRY(ctx, hipMemcpyAsync(ctx->h_rect.data(), ctx->d_rect, sizeof(uint32_t) * 4 * nobj,
-                                        hipMemcpyDeviceToHost, ctx->stream));
-            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-            for (size_t i = 0; i < nobj; ++i) {
-                const uint32_t* a = &ctx->h_rect[4 * i];
-                int32_t* r = ctx->h_objs[i].g.rect;
-                if (a[1] == 0) {  // no face can be hit
-                    r[0] = 1;
-                    r[1] = 0;
-                    r[2] = 1;
-                    r[3] = 0;
-                } else {
-                    r[0] = (int32_t)~a[0];
-                    r[1] = (int32_t)a[1] - 1;
-                    r[2] = (int32_t)~a[2];
-                    r[3] = (int32_t)a[3] - 1;
-                }
+    return ERAY_OK;
+}
+
+uint32_t binned_objects(const eray_ctx* ctx) {
+    uint32_t nb = 0;
+    for (auto& o : ctx->objects) nb += o.T > kDirectMax;
+    return nb;
+}
+
+// The device buffers of the binned objects' bins for this camera size, row phase and rows
+// (reallocated, with a stream synchronisation, only when that layout or the capacity changes).
+int ensure_bins(eray_ctx* ctx, uint32_t W, uint32_t H, uint32_t row0, uint32_t rows) {
+    const uint32_t nb = binned_objects(ctx);
+    const uint32_t T = ctx->total_tris;
+    if (ctx->face_cap < T || !ctx->d_range) {
+        int st;
+        if ((st = ensure(ctx, &ctx->d_range, &ctx->face_cap, T))) return st;
+        size_t c1 = 0, c2 = 0;
+        if ((st = ensure(ctx, &ctx->d_area, &c1, T)) || (st = ensure(ctx, &ctx->d_fkey, &c2, T))) return st;
+    }
+    size_t binned_tris = 0;
+    for (auto& o : ctx->objects)
+        if (o.T > kDirectMax) binned_tris += o.T;
+    if (!ctx->bin_cap) ctx->bin_cap = std::max<size_t>(2 * binned_tris, 1u << 16);
+    const uint32_t phase = row0 % kBinH, tiles_x = (W + 63) / 64;
+    std::vector<uint64_t> layout{T, nb, W, H, phase, rows, ctx->bin_cap, ctx->scene_gen};
+    if (layout == ctx->bins_layout) return ERAY_OK;
+    std::vector<uint32_t> kbegin, kobj;
+    for (uint32_t i = 0; i < ctx->objects.size(); ++i)
+        if (ctx->objects[i].T > kDirectMax) {
+            kbegin.push_back(ctx->h_objs[i].g.tri_begin);
+            kobj.push_back(i);
+        }
+    HIP_TRY(ctx, bins_alloc(ctx->bins, T, nb, kbegin.data(), kobj.data(), W, H, phase, tiles_x, rows, ctx->bin_cap,
+                            ctx->stream));
+    ctx->bins_layout = std::move(layout);
+    ctx->setup_key.clear();  // the bins must be rebuilt
+    return ERAY_OK;
+}
+
+// Enqueues the per-camera setup of `d_camera` (device) for camera rows [row0, row0 + rows): no
+// host round trip (setup.hip, bins.hip).
+int enqueue_setup(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint32_t H, uint32_t row0, uint32_t rows) {
+    SetupParams sp{};
+    sp.hot = ctx->d_hot;
+    sp.cull = ctx->d_cull;
+    sp.T = ctx->total_tris;
+    sp.objs = ctx->d_objs;
+    sp.nobj = (uint32_t)ctx->objects.size();
+    sp.obj_begin = ctx->d_begin;
+    sp.objkey = ctx->d_begin + sp.nobj + 1;
+    sp.cam = d_camera;
+    sp.state = ctx->d_state;
+    sp.W = W;
+    sp.H = H;
+    sp.row0 = row0;
+    sp.rows = rows;
+    sp.acc = ctx->d_acc;
+    sp.done = ctx->d_acc + 4 * (size_t)sp.nobj;
+    const bool binned = binned_objects(ctx) > 0;
+    sp.binned = binned ? 1u : 0u;
+    if (binned) {
+        sp.range = ctx->d_range;
+        sp.area = ctx->d_area;
+        sp.fkey = ctx->d_fkey;
+        sp.bins_x = ctx->bins.bins_x;
+        sp.phase = ctx->bins.phase;
+    }
+    HIP_TRY(ctx, launch_camera_setup(sp, ctx->stream));
+    if (binned) HIP_TRY(ctx, launch_bins_build(sp, ctx->bins, (W + 63) / 64, ctx->stream));
+    return ERAY_OK;
+}
+
+CamDev cam_dev(const eray_camera& c) {
+    return CamDev{c.center[0], c.center[1], c.center[2], c.fov[0] / c.fov[1], c.z_dist, {0u, 0u, 0u}};
+}
+
+// A copy of the setup state has reached the host (h_state): grow the bins' capacity when some
+// setup since the last reallocation needed more entries (they then fell back to LDS tiles).
+void state_arrived(eray_ctx* ctx) {
+    ctx->state_pending = false;
+    ctx->state_known = true;
+    if (ctx->h_state->bin_entries > ctx->bin_cap) {
+        ctx->bin_cap = 2 * (size_t)ctx->h_state->bin_entries;
+        ctx->state_known = false;
+        ctx->setup_key.clear();  // rebuilt with the larger capacity
+    }
+}
+
+// Makes the per-camera setup of the context camera current for rows [row0, row0 + rows):
+// enqueued when the camera, the rows or the scene changed, its results copied to the host
+// asynchronously.  *known: the host has them (args-mode frames); `wait`: block until it does.
+int sync_setup(eray_ctx* ctx, uint32_t W, uint32_t H, uint32_t row0, uint32_t rows, bool wait, bool* known) {
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        if (ctx->state_pending) {
+            const hipError_t q = hipEventQuery(ctx->state_ev);
+            if (q == hipSuccess) state_arrived(ctx);
+            else if (q != hipErrorNotReady) return set_error(ctx, ERAY_E_HIP, "setup event: %s", hipGetErrorString(q));
+        }
+        auto bins_ready = [&]() -> int {
+            if (!binned_objects(ctx)) return ERAY_OK;
+            const std::vector<uint64_t> before = ctx->bins_layout;
+            if (int st = ensure_bins(ctx, W, H, row0, rows)) return st;
+            if (ctx->bins_layout != before)  // new buffers: the bin statistics start over
+                HIP_TRY(ctx, hipMemsetAsync(ctx->d_state, 0, sizeof(CamState), ctx->stream));
+            return ERAY_OK;
+        };
+        if (int st = bins_ready()) return st;
+        std::vector<uint64_t> key(sizeof(eray_camera) / 4 + 4);
+        std::memcpy(key.data(), &ctx->camera, sizeof(eray_camera));
+        key[key.size() - 4] = row0;
+        key[key.size() - 3] = rows;
+        key[key.size() - 2] = ctx->scene_gen;
+        key[key.size() - 1] = ((uint64_t)W << 32) | H;
+        if (key != ctx->setup_key) {
+            if (ctx->state_pending) {  // h_state is about to be rewritten
+                HIP_TRY(ctx, hipEventSynchronize(ctx->state_ev));
+                state_arrived(ctx);
+                if (int st = bins_ready()) return st;  // (a grown capacity)
             }
-            ctx->face_rects.resize(4 * nobj);
-            for (size_t i = 0; i < nobj; ++i) std::memcpy(&ctx->face_rects[4 * i], ctx->h_objs[i].g.rect, 16);
-            HIP_TRY(ctx, hipMemcpyAsync(ctx->d_objs, ctx->h_objs.data(), sizeof(ObjectDesc) * nobj,
-                                        hipMemcpyHostToDevice, ctx->stream));
+            HIP_TRY(ctx, launch_set_camera(cam_dev(ctx->camera), ctx->d_cam, ctx->stream));
+            if (int st = enqueue_setup(ctx, ctx->d_cam, W, H, row0, rows)) return st;
+            HIP_TRY(ctx, hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(CamState), hipMemcpyDeviceToHost,
+                                        ctx->stream));
+            HIP_TRY(ctx, hipEventRecord(ctx->state_ev, ctx->stream));
+            ctx->setup_key = std::move(key);
+            ctx->state_pending = true;
+            ctx->state_known = false;
         }
-        ctx->cull_dirty = false;
-        ctx->bins_dirty = true;
-    }
-    return ERAY_OK;
-}
-
-// Screen bins for the objects the frame kernel does not scan per wave (> kDirectMax faces),
-// for the camera and the row phase of this render.
-int sync_bins(eray_ctx* ctx, uint32_t phase) {
-    bool need = false;
-    for (auto& o : ctx->objects) need |= o.T > kDirectMax;
-    if (!need || (!ctx->bins_dirty && ctx->bins_phase == phase)) return ERAY_OK;
-    uint32_t W, H;
-    eray_camera_size(&ctx->camera, &W, &H);
-    const uint32_t bins_x = (W + kBinW - 1) / kBinW;
-    const uint32_t bins_y = H ? (H - 1 + kBinH - phase) / kBinH + 1 : 1;
-    if (ctx->bins.size() < ctx->objects.size()) ctx->bins.resize(ctx->objects.size());
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // h_objs is about to change
-    for (size_t i = 0; i < ctx->objects.size(); ++i) {
-        ObjGeom& g = ctx->h_objs[i].g;
-        g.bin_start = nullptr;
-        g.bin_tri = nullptr;
-        g.bin_mask = nullptr;
-        g.bin_hot = nullptr;
-        if (ctx->objects[i].T <= kDirectMax) continue;
-        HIP_TRY(ctx, build_bins(ctx->d_cull + g.tri_begin, ctx->d_hot + g.tri_begin, g.tri_count, W, H, phase, bins_x, bins_y, &ctx->bins[i],
-                                ctx->stream));
-        g.bin_start = ctx->bins[i].start;
-        g.bin_tri = ctx->bins[i].tri;
-        g.bin_mask = ctx->bins[i].mask;
-        g.bin_hot = ctx->bins[i].hot;
-    }
-    // A binned object's pixel rectangle narrows to its non-empty bins: a pixel of an empty bin has
-    // no face whose culling bounds can pass there (bin_pixels), so no primary ray hits the object.
-    // Face rectangles alone can be far too wide (a near-silhouette face's bounds may span the
-    // frame), which would make the frame kernel search empty bins.
-    const size_t nobj = ctx->objects.size();
-    if (int st = ensure(ctx, &ctx->d_rect, &ctx->rect_cap, 4 * nobj)) return st;
-    HIP_TRY(ctx, hipMemsetAsync(ctx->d_rect, 0, sizeof(uint32_t) * 4 * nobj, ctx->stream));
-    for (size_t i = 0; i < nobj; ++i)
-        if (ctx->objects[i].T > kDirectMax)
-            HIP_TRY(ctx, launch_bins_rect(ctx->bins[i].start, bins_x, bins_y, W, H, phase, ctx->d_rect + 4 * i,
-                                          ctx->stream));
-    ctx->h_rect.assign(4 * nobj, 0u);
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_rect.data(), ctx->d_rect, sizeof(uint32_t) * 4 * nobj, hipMemcpyDeviceToHost,
-                                ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    for (size_t i = 0; i < nobj; ++i) {
-        int32_t* r = ctx->h_objs[i].g.rect;
-        const int32_t* f = &ctx->face_rects[4 * i];
-        if (ctx->objects[i].T <= kDirectMax) {
-            std::memcpy(r, f, 16);
-            continue;
+        if (ctx->state_pending && wait) {
+            HIP_TRY(ctx, hipEventSynchronize(ctx->state_ev));
+            state_arrived(ctx);  // (may ask for a larger capacity: set up again)
         }
-        const uint32_t* a = &ctx->h_rect[4 * i];
-        if (a[1] == 0) {  // every bin is empty
-            r[0] = r[2] = 1;
-            r[1] = r[3] = 0;
-            continue;
-        }
-        r[0] = std::max(f[0], (int32_t)~a[0]);
-        r[1] = std::min(f[1], (int32_t)a[1] - 1);
-        r[2] = std::max(f[2], (int32_t)~a[2]);
-        r[3] = std::min(f[3], (int32_t)a[3] - 1);
+        if (ctx->state_known || !wait) break;
     }
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_objs, ctx->h_objs.data(), sizeof(ObjectDesc) * ctx->h_objs.size(),
-                                hipMemcpyHostToDevice, ctx->stream));
-    ctx->bins_dirty = false;
-    ctx->bins_phase = phase;
-    ++ctx->bins_gen;
-    return ERAY_OK;
-}
-
-// The detail sub-block list of the rendered rows when some object is binned: only sub-blocks
-// where a binned object's bin is non-empty (or a small object's rectangle reaches) get a detail
-// wave; everything else is background.  Rebuilt when the rows or the bins change.
-int sync_detail(eray_ctx* ctx, FrameParams& p) {
-    const uint32_t subs_y = (p.rows + kBinH - 1) / kBinH;
-    const size_t nsub = 4 * (size_t)p.tiles_x * subs_y, nblk = (size_t)p.tiles_x * subs_y;
-    std::vector<uint64_t> key{p.cam_w, p.cam_h, p.row0, p.rows, p.bin_phase, ctx->bins_gen};
-    if (int st = ensure(ctx, &ctx->d_detail_list, &ctx->detail_list_cap, nsub)) return st;
-    if (int st = ensure(ctx, &ctx->d_detail_occ, &ctx->detail_occ_cap, nblk)) return st;
-    if (key != ctx->detail_key) {
-        ctx->detail_key.clear();
-        HIP_TRY(ctx, build_detail_list(ctx->d_objs, (uint32_t)ctx->objects.size(), p.cam_w, p.row0, p.rows, p.bins_x,
-                                       p.bin_phase, p.tiles_x, ctx->d_detail_list, ctx->d_detail_occ,
-                                       &ctx->detail_count, ctx->stream));
-        ctx->detail_key = std::move(key);
-    }
-    p.detail_list = ctx->d_detail_list;
-    p.detail_occ = ctx->d_detail_occ;
-    p.total_sub = ctx->detail_count;
-    p.nrect = 0;
+    *known = ctx->state_known;
     return ERAY_OK;
 }
 
@@ -481,8 +517,21 @@ int eray_ctx_create(int device, eray_ctx** out) {
     ctx->device = device;
     e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
+    // the separate fill kernel's stream and fork / join events (render.hip launch_frame_kernel)
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->lc.side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->lc.fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->lc.join, hipEventDisableTiming);
+    // the per-camera setup's device state and its pinned host copy
+    if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_cam, sizeof(CamDev));
+    if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_state, sizeof(CamState));
+    if (e == hipSuccess) e = hipMemset(ctx->d_state, 0, sizeof(CamState));
+    if (e == hipSuccess) e = hipHostMalloc((void**)&ctx->h_state, sizeof(CamState), hipHostMallocDefault);
+    if (e == hipSuccess) std::memset(ctx->h_state, 0, sizeof(CamState));
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->state_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->path_ev, hipEventDisableTiming);
     if (e != hipSuccess) {
-        delete ctx;
+        ctx->stream = ctx->own_stream;
+        eray_ctx_destroy(ctx);
         return set_error(nullptr, ERAY_E_HIP, "context init: %s", hipGetErrorString(e));
     }
     ctx->stream = ctx->own_stream;
@@ -494,21 +543,22 @@ int eray_ctx_destroy(eray_ctx* ctx) {
     if (!ctx) return ERAY_OK;
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
-    for (auto& b : ctx->bins) {
-        if (b.start) hipFree(b.start);
-        if (b.tri) hipFree(b.tri);
-        if (b.mask) hipFree(b.mask);
-        if (b.hot) hipFree(b.hot);
-    }
-    void* bufs[] = {ctx->d_hot,  ctx->d_shade,         ctx->d_cull,        ctx->d_raw,
-                    ctx->d_objs, ctx->d_lights,        ctx->d_rect,        ctx->d_detail_list,
-                    ctx->d_detail_occ, ctx->d_prog};
+    if (ctx->own_stream) hipStreamSynchronize(ctx->own_stream);
+    bins_free(ctx->bins);
+    void* bufs[] = {ctx->d_hot,   ctx->d_shade, ctx->d_cull,  ctx->d_raw,  ctx->d_objs,  ctx->d_lights,
+                    ctx->d_prog,  ctx->d_cam,   ctx->d_state, ctx->d_acc,  ctx->d_begin, ctx->d_range,
+                    ctx->d_area,  ctx->d_fkey,  ctx->d_path,  ctx->d_path_all};
     for (void* b : bufs)
         if (b) hipFree(b);
+    if (ctx->h_state) hipHostFree(ctx->h_state);
+    if (ctx->h_path) hipHostFree(ctx->h_path);
     for (auto& g : ctx->graphs) {
         if (g.exec) hipGraphExecDestroy(g.exec);
         if (g.graph) hipGraphDestroy(g.graph);
     }
+    for (hipEvent_t ev : {ctx->state_ev, ctx->path_ev, ctx->lc.fork, ctx->lc.join})
+        if (ev) hipEventDestroy(ev);
+    if (ctx->lc.side) hipStreamDestroy(ctx->lc.side);
     if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
     delete ctx;
     return ERAY_OK;
@@ -635,15 +685,14 @@ int eray_scene_reset(eray_ctx* ctx) {
     ctx->objects.clear();
     ctx->lights.clear();
     ctx->camera = eray_camera{{0.0f, 0.0f, 0.0f}, {60.0f, 60.0f}, 1024u, 1.0f};
-    ctx->geom_dirty = ctx->desc_dirty = ctx->cull_dirty = true;
+    ctx->geom_dirty = ctx->desc_dirty = true;
     return ERAY_OK;
 }
 
 int eray_scene_set_camera(eray_ctx* ctx, const eray_camera* camera) {
     if (!ctx || !camera) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "null argument");
     if (std::memcmp(&ctx->camera, camera, sizeof(eray_camera)) != 0) {
-        ctx->camera = *camera;
-        ctx->cull_dirty = true;
+        ctx->camera = *camera;  // (the next culled render sets it up: sync_setup)
     }
     return ERAY_OK;
 }
@@ -741,7 +790,7 @@ int eray_scene_add_object(eray_ctx* ctx, const eray_object* obj, uint32_t* index
     h.mat = m;
     ctx->objects.push_back(std::move(h));
     if (index) *index = (uint32_t)(ctx->objects.size() - 1);
-    ctx->geom_dirty = ctx->desc_dirty = ctx->cull_dirty = true;
+    ctx->geom_dirty = ctx->desc_dirty = true;
     return ERAY_OK;
 }
 
@@ -754,7 +803,13 @@ int eray_camera_size(const eray_camera* c, uint32_t* w, uint32_t* h) {
 
 // ------------------------------------------------------------------------ render ------------
 namespace {
-int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out, bool* empty) {
+enum class SetupWait { kNo, kYes };
+// Frame parameters of a render call.  Culled frames need the camera's setup: when its results
+// are on the host (or `wait`), the detail rectangles / count travel in the kernel arguments
+// (args mode); otherwise the frame kernel reads them from the setup's CamState (device-camera
+// mode) and the call never waits for the setup.
+int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out, bool* empty,
+                   SetupWait wait = SetupWait::kNo) {
     if (int st = use_device(ctx)) return st;
     if (!rp) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "params is null");
     // anti-aliasing and reflection bounces take the general tracer (trace.hip); bounces only
@@ -768,6 +823,9 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     if (bounces > kMaxBounces)
         return set_error(ctx, ERAY_E_UNSUPPORTED, "bounces = %u: at most %u reflection levels", rp->bounces,
                          kMaxBounces);
+    const uint32_t known_flags = ERAY_RENDER_BRUTE_FORCE | ERAY_RENDER_DENSE_DETAIL | ERAY_RENDER_NO_DENSE_DETAIL |
+                                 ERAY_RENDER_SEPARATE_FILL | ERAY_RENDER_NO_SEPARATE_FILL;
+    if (rp->flags & ~known_flags) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "unknown render flags 0x%x", rp->flags);
     const bool general = rp->anti_aliasing > 0 || bounces > 0;
     uint32_t W, H;
     eray_camera_size(&ctx->camera, &W, &H);
@@ -784,11 +842,12 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
         return set_error(ctx, ERAY_E_INVALID_ARGUMENT,
                          "fused PPM output needs camera size == image size; use eray_pack_ppm");
     const bool cull = !general && !(rp->flags & ERAY_RENDER_BRUTE_FORCE);
-    if (int st = sync_scene(ctx, cull)) return st;
-    if (cull)
-        if (int st = sync_bins(ctx, rp->row0 % kBinH)) return st;
+    if (int st = sync_scene(ctx)) return st;
     *empty = !rp->rows || !W;
     if (*empty) return ERAY_OK;
+    bool known = true;
+    if (cull)
+        if (int st = sync_setup(ctx, W, H, rp->row0, rp->rows, wait == SetupWait::kYes, &known)) return st;
 
     FrameParams& p = *out;
     std::memset(&p, 0, sizeof p);  // padding too: the launch-plan cache compares the bytes
@@ -823,59 +882,6 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     for (auto& o : ctx->objects) p.max_object_tris = o.T > p.max_object_tris ? o.T : p.max_object_tris;
     p.total_tris = ctx->total_tris;
     p.lds_scene = (ctx->total_tris <= kCacheTris && p.nobj <= kCacheObjects && p.nlights <= kCacheLights) ? 1u : 0u;
-#ifdef ERAY_AB_NO_LDS_SCENE
-    p.lds_scene = 0;
-#endif
-    // detail rectangles in sub-block units (16 px x 4 rank-local rows); brute force: the frame
-    const int32_t rows_i = (int32_t)rp->rows, w_i = (int32_t)W;
-    p.nrect = 0;
-    p.total_sub = 0;
-    auto add_rect = [&](int32_t x0, int32_t x1, int32_t y0, int32_t y1) {  // pixels, local rows
-        x1 = x1 < w_i - 1 ? x1 : w_i - 1;
-        y0 = y0 > 0 ? y0 : 0;
-        y1 = y1 < rows_i - 1 ? y1 : rows_i - 1;
-        if (x0 > x1 || y0 > y1) return;
-        int32_t r[4] = {x0 / 16, x1 / 16, y0 / 4, y1 / 4};
-        if (p.nrect == (uint32_t)kMaxRects) {  // out of slots: widen the last one
-            int32_t* l = p.rects[kMaxRects - 1];
-            l[0] = l[0] < r[0] ? l[0] : r[0];
-            l[1] = l[1] > r[1] ? l[1] : r[1];
-            l[2] = l[2] < r[2] ? l[2] : r[2];
-            l[3] = l[3] > r[3] ? l[3] : r[3];
-            return;
-        }
-        std::memcpy(p.rects[p.nrect++], r, sizeof r);
-    };
-    if (cull) {
-        for (size_t i = 0; i < ctx->h_objs.size(); ++i) {
-            const ObjectDesc& d = ctx->h_objs[i];
-            if (!d.g.tri_count) continue;
-            add_rect(d.g.rect[0], d.g.rect[1], d.g.rect[2] - (int32_t)rp->row0, d.g.rect[3] - (int32_t)rp->row0);
-        }
-    } else if (p.nobj) {
-        add_rect(0, w_i - 1, 0, rows_i - 1);
-    }
-    // the frame kernel wants disjoint rectangles: merge overlapping ones into their bounding box
-    for (bool merged = true; merged;) {
-        merged = false;
-        for (uint32_t a = 0; a < p.nrect && !merged; ++a)
-            for (uint32_t b = a + 1; b < p.nrect && !merged; ++b) {
-                int32_t* ra = p.rects[a];
-                const int32_t* rb = p.rects[b];
-                if (ra[0] > rb[1] || rb[0] > ra[1] || ra[2] > rb[3] || rb[2] > ra[3]) continue;
-                ra[0] = ra[0] < rb[0] ? ra[0] : rb[0];
-                ra[1] = ra[1] > rb[1] ? ra[1] : rb[1];
-                ra[2] = ra[2] < rb[2] ? ra[2] : rb[2];
-                ra[3] = ra[3] > rb[3] ? ra[3] : rb[3];
-                std::memmove(p.rects[b], p.rects[b + 1], sizeof(p.rects[0]) * (p.nrect - b - 1));
-                --p.nrect;
-                merged = true;
-            }
-    }
-    for (uint32_t k = 0; k < p.nrect; ++k) {  // sub-blocks the frame kernel renders in detail
-        const int32_t* r = p.rects[k];
-        p.total_sub += (uint32_t)(r[1] - r[0] + 1) * (uint32_t)(r[3] - r[2] + 1);
-    }
     p.spec_pow = ctx->spec_pow ? 1u : 0u;
     p.example_mat = ctx->example_mat ? 1u : 0u;
     p.tiles_x = (W + 63) / 64;
@@ -885,14 +891,35 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     p.bounces = bounces;
     p.seed_lo = (uint32_t)rp->aa_seed;
     p.seed_hi = (uint32_t)(rp->aa_seed >> 32);
-    bool binned = false;
-    for (auto& o : ctx->objects) binned |= o.T > kDirectMax;
-    if (cull && binned)
-        if (int st = sync_detail(ctx, p)) return st;
+    p.launch_flags = rp->flags & ~ERAY_RENDER_BRUTE_FORCE;
+    if (!cull) {  // every pixel in detail: one rectangle, the frame (sub-block units)
+        if (p.nobj) {
+            p.nrect = 1;
+            p.rects[0][0] = 0;
+            p.rects[0][1] = (int32_t)((W - 1) / 16);
+            p.rects[0][2] = 0;
+            p.rects[0][3] = (int32_t)((rp->rows - 1) / 4);
+            p.total_sub = (uint32_t)(p.rects[0][1] + 1) * (uint32_t)(p.rects[0][3] + 1);
+        }
+        return ERAY_OK;
+    }
+    if (binned_objects(ctx)) {  // the detail sub-block list of the setup
+        p.detail_list = ctx->bins.dlist;
+        p.detail_occ = ctx->bins.docc;
+    }
+    if (known) {  // args mode
+        const CamState& h = *ctx->h_state;
+        p.nrect = h.nrect;
+        p.total_sub = h.total_sub;
+        std::memcpy(p.rects, h.rects, sizeof p.rects);
+    } else {  // device-camera mode (the last known count only steers the launch shape)
+        p.cam_state = ctx->d_state;
+        p.total_sub = ctx->h_state ? ctx->h_state->total_sub : 0u;
+    }
     return ERAY_OK;
 }
 
-hipError_t launch_frame(eray_ctx* ctx, FrameParams& p) { return launch_render(p, ctx->stream); }
+hipError_t launch_frame(eray_ctx* ctx, const FrameParams& p) { return launch_render(p, ctx->lc, ctx->stream); }
 }  // namespace
 
 int eray_render(eray_ctx* ctx, const eray_render_params* rp) {
@@ -903,17 +930,21 @@ int eray_render(eray_ctx* ctx, const eray_render_params* rp) {
     return ERAY_OK;
 }
 
+}  // extern "C"
+
 namespace {
 constexpr uint32_t kGraphFrames = 64;
 
 constexpr size_t kGraphCache = 6;
 
-// The graph of n back-to-back frame launches for (p, stream), captured unless cached.
-int ensure_graph(eray_ctx* ctx, const FrameParams& p, uint32_t n, hipGraphExec_t* out) {
-    std::vector<unsigned char> key(sizeof p + sizeof n + sizeof ctx->stream);
-    std::memcpy(key.data(), &p, sizeof p);
-    std::memcpy(key.data() + sizeof p, &n, sizeof n);
-    std::memcpy(key.data() + sizeof p + sizeof n, &ctx->stream, sizeof ctx->stream);
+// The graph of n back-to-back frames, frame f enqueued by body(f), for `key` (+ n and the
+// stream), captured unless cached.
+template <typename Body>
+int ensure_graph(eray_ctx* ctx, std::vector<unsigned char> key, uint32_t n, Body&& body, hipGraphExec_t* out) {
+    const size_t at = key.size();
+    key.resize(at + sizeof n + sizeof ctx->stream);
+    std::memcpy(key.data() + at, &n, sizeof n);
+    std::memcpy(key.data() + at + sizeof n, &ctx->stream, sizeof ctx->stream);
     for (auto& G : ctx->graphs)
         if (G.key == key) {
             G.used = ++ctx->graph_clock;
@@ -930,11 +961,14 @@ int ensure_graph(eray_ctx* ctx, const FrameParams& p, uint32_t n, hipGraphExec_t
         ctx->graphs.erase(ctx->graphs.begin() + (std::ptrdiff_t)lru);
     }
     HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
-    hipError_t e = hipSuccess;
-    for (uint32_t f = 0; f < n && e == hipSuccess; ++f) e = launch_render(p, ctx->stream);
+    int st = ERAY_OK;
+    for (uint32_t f = 0; f < n && st == ERAY_OK; ++f) st = body(f);
     hipGraph_t g = nullptr;
-    const hipError_t e2 = hipStreamEndCapture(ctx->stream, &g);
-    if (e == hipSuccess) e = e2;
+    hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+    if (st != ERAY_OK) {
+        if (g) hipGraphDestroy(g);
+        return st;
+    }
     hipGraphExec_t exec = nullptr;
     if (e == hipSuccess) e = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
     if (e != hipSuccess) {
@@ -951,6 +985,13 @@ int ensure_graph(eray_ctx* ctx, const FrameParams& p, uint32_t n, hipGraphExec_t
     return ERAY_OK;
 }
 
+std::vector<unsigned char> params_key(const FrameParams& p, uint32_t kind) {
+    std::vector<unsigned char> key(sizeof p + sizeof kind);
+    std::memcpy(key.data(), &p, sizeof p);
+    std::memcpy(key.data() + sizeof p, &kind, sizeof kind);
+    return key;
+}
+
 // The launch plan of `frames` frames: a graph of `chunk` = min(frames, kGraphFrames) frames,
 // replayed frames / chunk times, and a graph of the remainder (no plain launches, whose host
 // cost can exceed a frame's device time).  chunk = 0: plain launches (null stream, 1 frame).
@@ -958,40 +999,28 @@ struct Plan {
     uint32_t chunk = 0, rest = 0;
     hipGraphExec_t chunk_exec = nullptr, rest_exec = nullptr;
 };
-int ensure_plan(eray_ctx* ctx, const FrameParams& p, uint32_t frames, Plan* plan) {
+template <typename Body>
+int ensure_plan(eray_ctx* ctx, const std::vector<unsigned char>& key, uint32_t frames, Body&& body, Plan* plan) {
     *plan = Plan{};
     if (!ctx->stream || frames < 2) return ERAY_OK;  // the null stream cannot be captured
     const uint32_t n = frames < kGraphFrames ? frames : kGraphFrames;
-    if (int st = ensure_graph(ctx, p, n, &plan->chunk_exec)) return st;
+    if (int st = ensure_graph(ctx, key, n, body, &plan->chunk_exec)) return st;
     plan->chunk = n;
     const uint32_t r = frames % n;
     if (r > 1) {
-        if (int st = ensure_graph(ctx, p, r, &plan->rest_exec)) return st;
+        if (int st = ensure_graph(ctx, key, r, body, &plan->rest_exec)) return st;
         plan->rest = r;
     }
     return ERAY_OK;
 }
-}  // namespace
 
-int eray_render_prepare(eray_ctx* ctx, const eray_render_params* rp, uint32_t frames) {
-    FrameParams p;
-    bool empty = false;
-    if (int st = prepare_render(ctx, rp, &p, &empty)) return st;
-    Plan plan;
-    return empty ? ERAY_OK : ensure_plan(ctx, p, frames, &plan);
-}
-
-int eray_render_frames(eray_ctx* ctx, const eray_render_params* rp, uint32_t frames,
-                       float* mean_frame_ms) {
-    FrameParams p;
-    bool empty = false;
-    if (int st = prepare_render(ctx, rp, &p, &empty)) return st;
-    if (mean_frame_ms) *mean_frame_ms = 0.0f;
-    if (empty || !frames) return ERAY_OK;
-    Plan plan;
-    if (int st = ensure_plan(ctx, p, frames, &plan)) return st;
+// Replays `plan` for `frames` frames (before_chunk(first frame, count) runs ahead of each graph
+// launch, plain(f) renders frames the plan does not cover); mean device time per frame when asked.
+template <typename Before, typename Plain>
+int replay(eray_ctx* ctx, const Plan& plan, uint32_t frames, Before&& before_chunk, Plain&& plain, float* mean_ms) {
     hipEvent_t ev[2] = {nullptr, nullptr};
-    if (mean_frame_ms) {
+    if (mean_ms) {
+        *mean_ms = 0.0f;
         for (auto& e : ev) {
             hipError_t he = hipEventCreate(&e);
             if (he != hipSuccess) {
@@ -1000,27 +1029,153 @@ int eray_render_frames(eray_ctx* ctx, const eray_render_params* rp, uint32_t fra
             }
         }
     }
-    // replay the cached graphs (back-to-back frame kernels)
-    hipError_t he = mean_frame_ms ? hipEventRecord(ev[0], ctx->stream) : hipSuccess;
+    int st = ERAY_OK;
+    hipError_t he = mean_ms ? hipEventRecord(ev[0], ctx->stream) : hipSuccess;
     uint32_t done = 0;
-    for (; plan.chunk && done + plan.chunk <= frames && he == hipSuccess; done += plan.chunk)
-        he = hipGraphLaunch(plan.chunk_exec, ctx->stream);
-    if (plan.rest && done + plan.rest == frames && he == hipSuccess) {
-        he = hipGraphLaunch(plan.rest_exec, ctx->stream);
+    for (; plan.chunk && done + plan.chunk <= frames && he == hipSuccess && !st; done += plan.chunk) {
+        st = before_chunk(done, plan.chunk);
+        if (!st) he = hipGraphLaunch(plan.chunk_exec, ctx->stream);
+    }
+    if (plan.rest && done + plan.rest == frames && he == hipSuccess && !st) {
+        st = before_chunk(done, plan.rest);
+        if (!st) he = hipGraphLaunch(plan.rest_exec, ctx->stream);
         done += plan.rest;
     }
-    for (; done < frames && he == hipSuccess; ++done) he = launch_frame(ctx, p);
-    if (mean_frame_ms && he == hipSuccess) {
+    for (; done < frames && he == hipSuccess && !st; ++done) st = plain(done);
+    if (mean_ms && he == hipSuccess && !st) {
         he = hipEventRecord(ev[1], ctx->stream);
         if (he == hipSuccess) he = hipEventSynchronize(ev[1]);
         float ms = 0.0f;
         if (he == hipSuccess) he = hipEventElapsedTime(&ms, ev[0], ev[1]);
-        if (he == hipSuccess) *mean_frame_ms = ms / (float)frames;
+        if (he == hipSuccess) *mean_ms = ms / (float)frames;
     }
     for (auto e : ev)
         if (e) hipEventDestroy(e);
+    if (st) return st;
     if (he != hipSuccess) return set_error(ctx, ERAY_E_HIP, "render loop: %s", hipGetErrorString(he));
     return ERAY_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int eray_render_prepare(eray_ctx* ctx, const eray_render_params* rp, uint32_t frames) {
+    FrameParams p;
+    bool empty = false;
+    if (int st = prepare_render(ctx, rp, &p, &empty, SetupWait::kYes)) return st;
+    if (empty) return ERAY_OK;
+    Plan plan;
+    auto body = [&](uint32_t) -> int {
+        HIP_TRY(ctx, launch_frame(ctx, p));
+        return ERAY_OK;
+    };
+    return ensure_plan(ctx, params_key(p, 0), frames, body, &plan);
+}
+
+int eray_render_frames(eray_ctx* ctx, const eray_render_params* rp, uint32_t frames,
+                       float* mean_frame_ms) {
+    FrameParams p;
+    bool empty = false;
+    if (int st = prepare_render(ctx, rp, &p, &empty, SetupWait::kYes)) return st;
+    if (mean_frame_ms) *mean_frame_ms = 0.0f;
+    if (empty || !frames) return ERAY_OK;
+    Plan plan;
+    auto body = [&](uint32_t) -> int {
+        HIP_TRY(ctx, launch_frame(ctx, p));
+        return ERAY_OK;
+    };
+    if (int st = ensure_plan(ctx, params_key(p, 0), frames, body, &plan)) return st;
+    auto none = [](uint32_t, uint32_t) { return (int)ERAY_OK; };
+    return replay(ctx, plan, frames, none, body, mean_frame_ms);
+}
+
+int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* rp, const eray_camera* cameras, uint32_t n,
+                            float* mean_frame_ms) {
+    if (int st = use_device(ctx)) return st;
+    if (mean_frame_ms) *mean_frame_ms = 0.0f;
+    if (!rp) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "params is null");
+    if (n && !cameras) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "cameras is null");
+    uint32_t W, H;
+    eray_camera_size(&ctx->camera, &W, &H);
+    for (uint32_t f = 0; f < n; ++f) {  // one engine image: every camera has the scene camera's size
+        uint32_t w, h;
+        eray_camera_size(&cameras[f], &w, &h);
+        if (w != W || h != H)
+            return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "camera %u: size %ux%u differs from the scene camera's %ux%u",
+                             f, w, h, W, H);
+    }
+    FrameParams p;
+    bool empty = false;
+    // the scene camera's setup once (scene upload, bins layout, a detail count for the launch shape)
+    if (int st = prepare_render(ctx, rp, &p, &empty, SetupWait::kYes)) return st;
+    if (empty || !n) return ERAY_OK;
+    if (!p.cull) {  // anti-aliasing, bounces, brute force: no per-camera setup, camera in the arguments
+        const eray_camera saved = ctx->camera;
+        for (uint32_t f = 0; f < n; ++f) {
+            ctx->camera = cameras[f];
+            FrameParams q;
+            int st = prepare_render(ctx, rp, &q, &empty);
+            if (!st && !empty) {
+                const hipError_t e = launch_frame(ctx, q);
+                if (e != hipSuccess) st = set_error(ctx, ERAY_E_HIP, "render: %s", hipGetErrorString(e));
+            }
+            if (st) {
+                ctx->camera = saved;
+                return st;
+            }
+        }
+        ctx->camera = saved;
+        if (mean_frame_ms) HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        return ERAY_OK;
+    }
+    // device-camera mode: every frame reads its setup's CamState
+    p.cam_state = ctx->d_state;
+    p.nrect = 0;
+    std::memset(p.rects, 0, sizeof p.rects);
+    // the cameras: staged in pinned memory, copied to the device once per call; each graph chunk
+    // reads its cameras from d_path (a device-to-device copy of its slice before each replay)
+    if (ctx->h_path_cap < n) {
+        HIP_TRY(ctx, hipEventSynchronize(ctx->path_ev));
+        if (ctx->h_path) HIP_TRY(ctx, hipHostFree(ctx->h_path));
+        ctx->h_path = nullptr;
+        HIP_TRY(ctx, hipHostMalloc((void**)&ctx->h_path, sizeof(CamDev) * n, hipHostMallocDefault));
+        ctx->h_path_cap = n;
+    }
+    HIP_TRY(ctx, hipEventSynchronize(ctx->path_ev));  // the previous upload has read h_path
+    for (uint32_t f = 0; f < n; ++f) ctx->h_path[f] = cam_dev(cameras[f]);
+    if (int st = ensure(ctx, &ctx->d_path_all, &ctx->path_all_cap, n)) return st;
+    if (int st = ensure(ctx, &ctx->d_path, &ctx->path_cap, kGraphFrames)) return st;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_path_all, ctx->h_path, sizeof(CamDev) * n, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipEventRecord(ctx->path_ev, ctx->stream));
+    auto frame = [&](const CamDev* cam) -> int {
+        if (int st = enqueue_setup(ctx, cam, W, H, rp->row0, rp->rows)) return st;
+        HIP_TRY(ctx, launch_frame(ctx, p));
+        return ERAY_OK;
+    };
+    auto body = [&](uint32_t f) { return frame(ctx->d_path + f); };
+    std::vector<unsigned char> key = params_key(p, 1);
+    key.insert(key.end(), reinterpret_cast<const unsigned char*>(&ctx->d_path),
+               reinterpret_cast<const unsigned char*>(&ctx->d_path) + sizeof ctx->d_path);
+    Plan plan;
+    if (int st = ensure_plan(ctx, key, n, body, &plan)) return st;
+    auto before = [&](uint32_t first, uint32_t count) -> int {
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->d_path, ctx->d_path_all + first, sizeof(CamDev) * count,
+                                    hipMemcpyDeviceToDevice, ctx->stream));
+        return ERAY_OK;
+    };
+    auto plain = [&](uint32_t f) { return frame(ctx->d_path_all + f); };
+    const int st = replay(ctx, plan, n, before, plain, mean_frame_ms);
+    // the device state now belongs to the path's last camera: the scene camera is set up again
+    // at its next render; the path's bin statistics reach the host with this copy
+    ctx->setup_key.clear();
+    ctx->state_known = false;
+    if (!st) {
+        if (ctx->state_pending) HIP_TRY(ctx, hipEventSynchronize(ctx->state_ev));
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(CamState), hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipEventRecord(ctx->state_ev, ctx->stream));
+        ctx->state_pending = true;
+    }
+    return st;
 }
 
 int eray_pack_ppm(eray_ctx* ctx, const float* rgb, uint32_t w, uint32_t h, uint8_t* out) {
@@ -1045,39 +1200,64 @@ int eray_ppm_header(uint32_t w, uint32_t h, char* buf, size_t cap, size_t* len) 
 }  // extern "C"
 
 // Diagnostics (not part of include/eray_hip.h): the screen bins of object `index` as built for
-// the last render — out[0] bins, out[1] entries, out[2] (face, pixel) pairs (mask bits),
+// the last setup — out[0] bins, out[1] entries, out[2] (face, pixel) pairs (mask bits),
 // out[3] most entries in one bin, out[4] non-empty bins, out[5] most pairs in one bin,
-// out[6..9] the object's pixel rectangle (x0, x1, y0, y1; int32 as uint64).
+// out[6..9] the object's pixel rectangle (x0, x1, y0, y1; int32 as uint64).  Synchronises.
 extern "C" int eray_debug_bin_stats(eray_ctx* ctx, uint32_t index, uint64_t* out) {
-    if (!ctx || !out || index >= ctx->bins.size() || !ctx->bins[index].start) return ERAY_E_INVALID_ARGUMENT;
-    const ObjBins& b = ctx->bins[index];
-    uint32_t W, H;
-    eray_camera_size(&ctx->camera, &W, &H);
-    const uint32_t bins_x = (W + kBinW - 1) / kBinW;
-    const uint32_t bins_y = H ? (H - 1 + kBinH - ctx->bins_phase) / kBinH + 1 : 1;
-    const size_t nb = (size_t)bins_x * bins_y;
-    std::vector<uint32_t> start(nb + 1);
-    std::vector<unsigned long long> mask(b.n);
+    if (!ctx || !out || index >= ctx->objects.size() || ctx->objects[index].T <= kDirectMax || !ctx->bins.start)
+        return ERAY_E_INVALID_ARGUMENT;
+    const BinBuffers& b = ctx->bins;
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < index; ++i) k += ctx->objects[i].T > kDirectMax;
+    std::vector<uint32_t> start(b.nbins + 1);
+    ObjectDesc d{};
     if (hipStreamSynchronize(ctx->stream) != hipSuccess ||
-        hipMemcpy(start.data(), b.start, start.size() * 4, hipMemcpyDeviceToHost) != hipSuccess ||
-        (b.n && hipMemcpy(mask.data(), b.mask, b.n * 8, hipMemcpyDeviceToHost) != hipSuccess))
+        hipMemcpy(start.data(), b.start + (size_t)k * b.nbins, start.size() * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(&d, ctx->d_objs + index, sizeof d, hipMemcpyDeviceToHost) != hipSuccess)
+        return set_error(ctx, ERAY_E_HIP, "bin stats copy failed");
+    const size_t n = start[b.nbins] - start[0];
+    std::vector<unsigned long long> mask(n);
+    if (n && hipMemcpy(mask.data(), b.mask + start[0], n * 8, hipMemcpyDeviceToHost) != hipSuccess)
         return set_error(ctx, ERAY_E_HIP, "bin stats copy failed");
     uint64_t pairs = 0, most = 0, nonempty = 0, most_pairs = 0;
-    for (size_t i = 0; i < nb; ++i) {
+    for (size_t i = 0; i < b.nbins; ++i) {
         const uint64_t e = start[i + 1] - start[i];
         most = e > most ? e : most;
         nonempty += e != 0;
         uint64_t pb = 0;
-        for (uint32_t j = start[i]; j < start[i + 1]; ++j) pb += (uint64_t)__builtin_popcountll(mask[j]);
+        for (uint32_t j = start[i]; j < start[i + 1]; ++j) pb += (uint64_t)__builtin_popcountll(mask[j - start[0]]);
         pairs += pb;
         most_pairs = pb > most_pairs ? pb : most_pairs;
     }
-    out[0] = nb;
-    out[1] = b.n;
+    out[0] = b.nbins;
+    out[1] = n;
     out[2] = pairs;
     out[3] = most;
     out[4] = nonempty;
     out[5] = most_pairs;
-    for (int k = 0; k < 4; ++k) out[6 + k] = (uint64_t)(int64_t)ctx->h_objs[index].g.rect[k];
+    for (int q = 0; q < 4; ++q) out[6 + q] = (uint64_t)(int64_t)d.g.rect[q];
+    return ERAY_OK;
+}
+
+// Diagnostics (not part of include/eray_hip.h): the screen bins' entry capacity.  Setting it
+// reallocates the bins at the next setup; a setup whose entries exceed it renders its binned
+// objects through LDS tiles and the capacity grows once the host sees the count (tests).
+extern "C" int eray_debug_set_bin_capacity(eray_ctx* ctx, uint64_t entries) {
+    if (!ctx || !entries) return ERAY_E_INVALID_ARGUMENT;
+    ctx->bin_cap = (size_t)entries;
+    ctx->setup_key.clear();
+    return ERAY_OK;
+}
+extern "C" uint64_t eray_debug_bin_capacity(const eray_ctx* ctx) { return ctx ? (uint64_t)ctx->bins.cap : 0u; }
+// Diagnostics: the last setup's device state (CamState, 176 B) and object `index`'s pixel
+// rectangle as the frame kernel reads them (synchronises).
+extern "C" int eray_debug_setup_state(eray_ctx* ctx, uint32_t index, void* state_out, int32_t* rect_out) {
+    if (!ctx || !state_out || !rect_out || index >= ctx->objects.size()) return ERAY_E_INVALID_ARGUMENT;
+    ObjectDesc d{};
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess ||
+        hipMemcpy(state_out, ctx->d_state, sizeof(CamState), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(&d, ctx->d_objs + index, sizeof d, hipMemcpyDeviceToHost) != hipSuccess)
+        return set_error(ctx, ERAY_E_HIP, "setup state copy failed");
+    std::memcpy(rect_out, d.g.rect, sizeof d.g.rect);
     return ERAY_OK;
 }

@@ -11,12 +11,27 @@ namespace gpu {
 // Clipping the viewport square by the four half-planes (double precision; each relaxed by 1e-9
 // of its magnitude, far above the clip's rounding, so the computed polygon contains the exact
 // one) and widening its bounding box by 1 pixel (x' is the reference's f32 x/W, within a relative
-// 2^-24 of x/W: far less than a pixel) gives a conservative pixel rectangle per face.  The object's rectangle is the union: no primary ray
-// outside it can hit the object, so those pixels need no test for it.
-__device__ inline bool face_rect(const TriCull& c, uint32_t W, uint32_t H, int32_t (&r)[4]) {
+// 2^-24 of x/W: far less than a pixel) gives a conservative pixel rectangle per face.  The
+// object's rectangle is the union: no primary ray outside it can hit the object, so those pixels
+// need no test for it.
+// The polygon (at most 8 vertices: 4 + one per clip) lives in the caller's LDS workspace `ws`
+// (4 arrays of 8 doubles, element k of array a at ws[(a * 8 + k) * stride]): as private arrays
+// with run-time indices it lived in scratch memory, a chain of memory round trips per clip
+// (tri_rect_kernel took 14.5 us for 12 faces).
+__device__ inline bool face_rect(const TriCull& c, uint32_t W, uint32_t H, int32_t (&r)[4], double* ws,
+                                 uint32_t stride) {
     const float A[4] = {c.A.x, c.A.y, c.A.z, c.A.w}, B[4] = {c.B.x, c.B.y, c.B.z, c.B.w};
     const float K[4] = {c.K.x, c.K.y, c.K.z, c.K.w}, T[4] = {c.T.x, c.T.y, c.T.z, c.T.w};
-    double px[12] = {0.0, 1.0, 1.0, 0.0}, py[12] = {0.0, 0.0, 1.0, 1.0}, qx[12], qy[12];
+    double* px = ws;
+    double* py = ws + 8 * stride;
+    double* qx = ws + 16 * stride;
+    double* qy = ws + 24 * stride;
+    const double sx[4] = {0.0, 1.0, 1.0, 0.0}, sy[4] = {0.0, 0.0, 1.0, 1.0};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        px[i * stride] = sx[i];
+        py[i * stride] = sy[i];
+    }
     int n = 4;
     for (int k = 0; k < 4; ++k) {
         if (T[k] == __builtin_inff()) continue;  // condition disabled (non-finite record)
@@ -25,35 +40,41 @@ __device__ inline bool face_rect(const TriCull& c, uint32_t W, uint32_t H, int32
         const double mag = fabs((double)K[k]) + fabs(a) + fabs(b) + fabs((double)T[k]);
         const double cc = (double)K[k] + (double)T[k] + 1e-9 * mag + 1e-300;
         int m = 0;
+        double xi = px[0], yi = py[0];
+        double fi = a * xi + b * yi + cc;
         for (int i = 0; i < n; ++i) {
             const int j = i + 1 == n ? 0 : i + 1;
-            const double fi = a * px[i] + b * py[i] + cc, fj = a * px[j] + b * py[j] + cc;
+            const double xj = px[j * stride], yj = py[j * stride];
+            const double fj = a * xj + b * yj + cc;
             if (fi >= 0.0) {
-                qx[m] = px[i];
-                qy[m] = py[i];
+                qx[m * stride] = xi;
+                qy[m * stride] = yi;
                 ++m;
             }
             if ((fi >= 0.0) != (fj >= 0.0)) {
                 double t = fi / (fi - fj);
                 t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
-                qx[m] = px[i] + t * (px[j] - px[i]);
-                qy[m] = py[i] + t * (py[j] - py[i]);
+                qx[m * stride] = xi + t * (xj - xi);
+                qy[m * stride] = yi + t * (yj - yi);
                 ++m;
             }
+            xi = xj;
+            yi = yj;
+            fi = fj;
         }
         n = m;
         if (!n) return false;
         for (int i = 0; i < n; ++i) {
-            px[i] = qx[i];
-            py[i] = qy[i];
+            px[i * stride] = qx[i * stride];
+            py[i * stride] = qy[i * stride];
         }
     }
     double xmin = px[0], xmax = px[0], ymin = py[0], ymax = py[0];
     for (int i = 1; i < n; ++i) {
-        xmin = fmin(xmin, px[i]);
-        xmax = fmax(xmax, px[i]);
-        ymin = fmin(ymin, py[i]);
-        ymax = fmax(ymax, py[i]);
+        xmin = fmin(xmin, px[i * stride]);
+        xmax = fmax(xmax, px[i * stride]);
+        ymin = fmin(ymin, py[i * stride]);
+        ymax = fmax(ymax, py[i * stride]);
     }
     r[0] = max((int32_t)floor(xmin * W) - 1, 0);
     r[1] = min((int32_t)ceil(xmax * W) + 1, (int32_t)W - 1);
@@ -61,7 +82,6 @@ __device__ inline bool face_rect(const TriCull& c, uint32_t W, uint32_t H, int32
     r[3] = min((int32_t)ceil(ymax * H) + 1, (int32_t)H - 1);
     return r[0] <= r[1] && r[2] <= r[3];
 }
-
 
 // Where condition k of a culling record can pass along a camera row, in pixels: from
 // K + A xf + B yf >= -T (the culling bound at the pixel's own f32 viewport coordinates), solved

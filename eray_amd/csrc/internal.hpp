@@ -108,6 +108,25 @@ struct LightDesc {
     float brightness;
 };
 
+// A camera as the kernels use it (camera.rs:57-76): centre, Fov ratio fov0 / fov1 (computed on
+// the host in f32, as Fov::ratio does) and z_dist.  Camera::size is fixed per frame plan.
+struct CamDev {
+    float cx, cy, cz, ratio, z_dist;
+    uint32_t pad[3];
+};
+
+// Per-camera frame setup in device memory, written by the setup kernels (setup.hip, bins.hip)
+// and read by the frame kernel in device-camera mode (FrameParams::cam_state): no host round
+// trip between a camera change and its frame.
+struct alignas(16) CamState {
+    CamDev cam;                   // the camera of the setup (copied by the setup kernel)
+    uint32_t nrect;               // detail rectangles (sub-block units, rank-local rows, disjoint)
+    uint32_t total_sub;           // detail sub-blocks (rectangles' area, or the detail list's length)
+    uint32_t bin_entries;         // (face, bin) entries the bins needed (host capacity sizing)
+    uint32_t bin_overflow;        // the bins did not fit: binned objects fall back to LDS tiles
+    int32_t rects[kMaxRects][4];  // x0, x1, y0, y1 (inclusive)
+};
+
 struct FrameParams {
     // camera (camera.rs:57-76)
     float cx, cy, cz;
@@ -148,6 +167,14 @@ struct FrameParams {
     uint32_t detail_wgs;  // most workgroups of the frame kernel's grid doing detail work (0: all)
     uint32_t fill_first;  // the fill workgroups take the grid's first block indices (dispatched first)
     uint32_t separate_fill;  // the frame kernel does detail work only; fill_kernel writes the background
+    // device-camera mode: camera, detail rectangles and detail count come from the setup
+    // kernels' CamState (the host has not read them back); null: the fields above hold them
+    const CamState* cam_state;
+    // device-camera mode's fill reservation (launch_frame_kernel computes it on the host in
+    // args mode): detail workgroups at the default share and at the small-scene share used
+    // when the detail sub-blocks exceed one round (frame_kernel decides from the count)
+    uint32_t detail_wgs_alt;
+    uint32_t launch_flags;  // ERAY_RENDER_* launch overrides (dense / separate fill), part of the plan key
     // general tracer (trace.hip): anti-aliasing rays per pixel, reflection depth, jitter seed;
     // aa == 0 && bounces == 0 selects the frame kernel
     uint32_t aa, bounces;
@@ -174,39 +201,91 @@ static_assert(sizeof(ObjectDesc) % 16 == 0 && sizeof(LightDesc) % 16 == 0, "16-B
 // ------------------------------------------------------------- launchers (.hip files) ------
 hipError_t launch_tri_precompute(const float* pos, const float* nrm, const float* uv, uint32_t T,
                                  TriHot* hot, TriShade* shade, hipStream_t s);
-hipError_t launch_tri_cull(const TriHot* hot, uint32_t T, float cx, float cy, float cz, float ratio,
-                           float z_dist, TriCull* cull, hipStream_t s);
-// Per-object pixel rectangle accumulator: 4 uint32 per object, zeroed before the launch, all
-// updated by atomicMax: (~x0, x1 + 1, ~y0, y1 + 1); a1 == 0 means empty.
-hipError_t launch_tri_rect(const TriCull* cull, uint32_t T, uint32_t cam_w, uint32_t cam_h,
-                           uint32_t* acc, hipStream_t s);
+// ------------------------------------------------------------- per-camera setup (setup.hip)
+// Everything a camera change needs before its frame, enqueued on the stream with no host round
+// trip (so a camera path can be graph-replayed): per triangle the culling record (TriCull) and
+// its conservative pixel rectangle, per object the union of those (ObjGeom::rect, written into
+// the device descriptors), for binned objects each face's bin rectangle (bins.hip), and, for
+// scenes without binned objects, the merged detail rectangles of the rendered rows (CamState).
+struct SetupParams {
+    const TriHot* hot;
+    TriCull* cull;
+    uint32_t T;                 // all triangles of the scene
+    ObjectDesc* objs;           // device descriptors (rect written)
+    uint32_t nobj;
+    const uint32_t* obj_begin;  // nobj + 1: first triangle of each object, then T
+    const uint32_t* objkey;     // nobj: the object's binned-object index, or ~0u
+    const CamDev* cam;          // the camera to set up (device)
+    CamState* state;
+    uint32_t W, H;              // Camera::size
+    uint32_t row0, rows;        // rendered camera rows (the merged rectangles are rank-local)
+    uint32_t* acc;              // 4 x nobj rectangle accumulators, zero between setups
+    uint32_t* done;             // workgroup counter (last-workgroup finalisation), zero between setups
+    uint32_t binned;            // some object is binned: bins.hip narrows rects + builds the detail list
+    // binned objects' faces (bins.hip): bin rectangle and its number of bins per face (zero for
+    // other faces), the binned-object index per face
+    int4* range;
+    unsigned long long* area;
+    uint32_t* fkey;
+    uint32_t bins_x, phase;
+};
+hipError_t launch_camera_setup(const SetupParams& sp, hipStream_t s);
+// Writes `cam` into the device camera slot (kernel arguments: no host staging buffer to race).
+hipError_t launch_set_camera(const CamDev& cam, CamDev* slot, hipStream_t s);
+// Launch overrides of eray_render_params::flags (eray_hip.h ERAY_RENDER_*) the frame launcher reads.
+constexpr uint32_t kLaunchDense = 2u, kLaunchNoDense = 4u, kLaunchSeparateFill = 8u, kLaunchNoSeparateFill = 16u;
+// Per-context launch resources: the separate fill kernel's stream and its fork / join events.
+struct LaunchCtx {
+    hipStream_t side;
+    hipEvent_t fork, join;
+};
 // The frame kernel, or the general tracer (trace.hip) when p.aa or p.bounces is set.
-hipError_t launch_render(const FrameParams& p, hipStream_t s);
+hipError_t launch_render(const FrameParams& p, const LaunchCtx& lc, hipStream_t s);
 hipError_t launch_trace(const FrameParams& p, hipStream_t s);
 
-struct ObjBins {  // device arrays of one object's bins (owned by the context)
-    uint32_t* start = nullptr;
-    uint32_t* tri = nullptr;
+// ------------------------------------------------------------- screen bins (bins.hip)
+// Device arrays of the binned objects' screen bins for one layout (camera size, row phase, the
+// binned objects), all preallocated: a camera's bins are rebuilt on the stream with no host
+// round trip.  Bin key = k * nbins + bin for binned object k; a bin's entries (face relative to
+// the object, pixel mask, intersection record) are unordered — the frame kernel keeps the
+// smallest face index that hits, which is the reference's first hit (object.rs:63-78).
+struct BinBuffers {
+    uint32_t nb = 0, nbins = 0, bins_x = 0, bins_y = 0, phase = 0, T = 0;
+    size_t cap = 0;                       // entry capacity
+    unsigned long long* first = nullptr;  // exclusive scan of SetupParams::area (T)
+    uint32_t* count = nullptr;            // per key (nb * nbins + 1), zero between builds
+    uint32_t* start = nullptr;            // per key + 1
+    uint32_t* kbegin = nullptr;           // tri_begin per binned object
+    uint32_t* kobj = nullptr;             // object index per binned object
+    uint32_t* n = nullptr;                // entries found (device counter, reset by the finaliser)
+    uint32_t* done = nullptr;             // workgroup counter of the finaliser
+    uint32_t* acc = nullptr;              // 4 x nb rectangle accumulators of the non-empty bins
+    uint32_t* ekey = nullptr;             // unscattered entries (cap)
+    uint32_t* eface = nullptr;
+    unsigned long long* emask = nullptr;
+    uint32_t* tri = nullptr;              // bin entries in key order (cap)
     unsigned long long* mask = nullptr;
     TriHot* hot = nullptr;
-    size_t start_cap = 0, tri_cap = 0, mask_cap = 0, hot_cap = 0, n = 0;
+    // detail sub-block list of the rendered rows
+    uint8_t* dflags = nullptr;
+    uint32_t* dpacked = nullptr;
+    uint32_t* dlist = nullptr;
+    uint8_t* docc = nullptr;
+    size_t nsub = 0;
+    void* temp = nullptr;                 // hipcub scratch
+    size_t temp_bytes = 0;
 };
-// Builds `out` for the object's records `cull[0, T)`, `hot[0, T)` and a W x H camera; bins_x x bins_y
-// bins of kBinW x kBinH pixels starting at camera row phase - kBinH.  Synchronises `s`.
-hipError_t build_bins(const TriCull* cull, const TriHot* hot, uint32_t T, uint32_t W, uint32_t H, uint32_t phase, uint32_t bins_x,
-                      uint32_t bins_y, ObjBins* out, hipStream_t s);
-// The pixel rectangle (camera pixels) of the non-empty bins of `start` (bins_x x bins_y bins of
-// build_bins' layout), accumulated like launch_tri_rect into 4 zeroed words.
-hipError_t launch_bins_rect(const uint32_t* start, uint32_t bins_x, uint32_t bins_y, uint32_t W, uint32_t H,
-                            uint32_t phase, uint32_t* acc, hipStream_t s);
-// The detail sub-blocks of rank-local rows [row0, row0 + rows) of a cam_w-wide frame: those
-// where some binned object's bin is non-empty or some other object's pixel rectangle reaches
-// (objs: the device descriptors).  Writes the compacted list (sy << 16 | sx, in raster order) and
-// the per-block occupancy bytes (see FrameParams::detail_list); *count receives the list length
-// (the call synchronises s).
-hipError_t build_detail_list(const ObjectDesc* objs, uint32_t nobj, uint32_t cam_w, uint32_t row0, uint32_t rows,
-                             uint32_t bins_x, uint32_t phase, uint32_t tiles_x, uint32_t* list, uint8_t* occ,
-                             uint32_t* count, hipStream_t s);
+// (Re)allocates `b` for T triangles, nb binned objects (kbegin / kobj: host arrays), a W x H
+// camera, row phase and `rows` rendered rows, entry capacity `cap` (synchronises `s` when it
+// reallocates).
+hipError_t bins_alloc(BinBuffers& b, uint32_t T, uint32_t nb, const uint32_t* kbegin, const uint32_t* kobj, uint32_t W,
+                      uint32_t H, uint32_t phase, uint32_t tiles_x, uint32_t rows, size_t cap, hipStream_t s);
+void bins_free(BinBuffers& b);
+// After launch_camera_setup: the bins of the setup's camera, the binned objects' rectangles
+// narrowed to their non-empty bins and their bin views in the descriptors (or none when the
+// entries overflow the capacity: the frame kernel then scans those objects through LDS tiles),
+// and the detail sub-block list of rows [row0, row0 + rows) with CamState::total_sub.
+hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tiles_x, hipStream_t s);
 hipError_t launch_pack_ppm(const float* rgb, uint32_t w, uint32_t h, uint8_t* out, hipStream_t s);
 
 hipError_t launch_wave(uint32_t w, uint32_t h, float xf, float yf, float* out, hipStream_t s);

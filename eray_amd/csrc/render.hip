@@ -15,7 +15,7 @@
 // ray the reference's test quantities are linear in the (unnormalised) ray direction, and the
 // camera directions of a 16x4 pixel block span a small convex cone.  Per camera, each triangle
 // gets four affine bounds f_k(x', y') of those quantities with float-error margins T_k
-// (tri_cull_kernel, see the derivation there).  A wave evaluates them triangle-parallel —
+// (camera_setup_kernel in setup.hip, see the derivation there).  A wave evaluates them triangle-parallel —
 // lane j takes triangle j of a 64-triangle chunk — and __ballot()s the survivors; only the
 // survivors are tested ray-parallel, in index order, with the reference's exact arithmetic.
 // The margins make the cull conservative: a triangle the exact test could accept for any ray
@@ -24,11 +24,10 @@
 //
 // Shadow rays (engine.rs:136-142, 218-228) go through the same LDS tiles without culling; the
 // reference's degenerate bounding box rejects almost all of them before the scan.
-#include <cstdlib>
+#include <mutex>
 
 #include "device_math.hpp"
 #include "glibc_cosf.hpp"
-#include "face_rect.hpp"
 #include "internal.hpp"
 #include "hit.hpp"
 
@@ -71,70 +70,6 @@ __device__ __forceinline__ T load_const(const T* base, size_t i) {
     return out;
 }
 
-// Diagnostic builds only (python -m eray_amd.build --trace): workgroups 0, 16, ..., 1008 (waves)
-// record s_memrealtime (100 MHz) and s_memtime (shader clock) at the frame kernel's phase
-// boundaries.  Stamps go to LDS (no vector-memory counter the kernel's own waits would include)
-// and are copied out when the wave ends (ERAY_TRACE_FLUSH).
-#ifdef ERAY_PHASE_TRACE
-constexpr int kTraceSlots = 24;
-__device__ uint64_t g_trace[2 * 64 * 4 * kTraceSlots];  // [realtime | shader clock]
-__shared__ uint64_t s_trace[4][kTraceSlots][2];
-#define ERAY_TRACE_ON() ((threadIdx.x & 63) == 0 && blockIdx.x % 16 == 0 && blockIdx.x < 1024)
-#define ERAY_TRACE(slot)                                                  \
-    do {                                                                  \
-        if (ERAY_TRACE_ON()) {                                            \
-            s_trace[threadIdx.x >> 6][slot][0] = __builtin_amdgcn_s_memrealtime(); \
-            s_trace[threadIdx.x >> 6][slot][1] = __builtin_amdgcn_s_memtime();     \
-        }                                                                 \
-    } while (0)
-#define ERAY_TRACE_VAL(slot, v)                                           \
-    do {                                                                  \
-        if (ERAY_TRACE_ON()) {                                            \
-            s_trace[threadIdx.x >> 6][slot][0] = (v);                     \
-            s_trace[threadIdx.x >> 6][slot][1] = 0;                       \
-        }                                                                 \
-    } while (0)
-#define ERAY_TRACE_CLEAR()                                                \
-    do {                                                                  \
-        if (ERAY_TRACE_ON())                                              \
-            for (int k_ = 0; k_ < kTraceSlots; ++k_) s_trace[threadIdx.x >> 6][k_][0] = s_trace[threadIdx.x >> 6][k_][1] = 0; \
-    } while (0)
-#define ERAY_TRACE_FLUSH()                                                \
-    do {                                                                  \
-        if (ERAY_TRACE_ON()) {                                            \
-            const uint32_t w_ = blockIdx.x / 16 * 4 + (threadIdx.x >> 6); \
-            for (int k_ = 0; k_ < kTraceSlots; ++k_) {                    \
-                g_trace[w_ * kTraceSlots + k_] = s_trace[threadIdx.x >> 6][k_][0];                   \
-                g_trace[64 * 4 * kTraceSlots + w_ * kTraceSlots + k_] = s_trace[threadIdx.x >> 6][k_][1]; \
-            }                                                             \
-        }                                                                 \
-    } while (0)
-#elif defined(ERAY_ISA_MARKS)  // static instruction profile (scripts/isa_profile.py): asm comments
-#define ERAY_TRACE(slot) asm volatile("; ERAY_MARK " #slot)
-#define ERAY_TRACE_VAL(slot, v) \
-    do {                        \
-    } while (0)
-#define ERAY_TRACE_CLEAR() \
-    do {                   \
-    } while (0)
-#define ERAY_TRACE_FLUSH() \
-    do {                   \
-    } while (0)
-#else
-#define ERAY_TRACE_CLEAR() \
-    do {                   \
-    } while (0)
-#define ERAY_TRACE_FLUSH() \
-    do {                   \
-    } while (0)
-#define ERAY_TRACE_VAL(slot, v) \
-    do {                        \
-    } while (0)
-#define ERAY_TRACE(slot) \
-    do {                 \
-    } while (0)
-#endif
-
 // --------------------------------------------------------------------- triangle setup ------
 // Triangle::intersects recomputes e1 = b - a, e2 = c - a, n = e1 x e2 for every test
 // (primitives.rs:44-46); they do not depend on the ray, so they are computed once here with
@@ -159,136 +94,6 @@ __global__ void __launch_bounds__(256) tri_precompute_kernel(const float* __rest
     shade[i].s1 = make_float4(N[4], N[5], N[6], N[7]);
     shade[i].s2 = make_float4(N[8], U[0], U[1], U[2]);
     shade[i].s3 = make_float4(U[3], U[4], U[5], 0.0f);
-}
-
-// --------------------------------------------------------------------- culling record ------
-// Derivation (u = 2^-24, all norms are 1-norms of the float inputs; d = normalised direction).
-// The reference computes, in f32 from ao = C - a (C the camera centre),
-//   det = -(d.n),  a_u = e2.(ao x d),  a_v = -(e1.(ao x d)),  u = a_u/det, v = a_v/det,
-//   t = (ao.n)/det,  hit iff det >= 1e-6, t >= 0, u >= 0, v >= 0, u + v <= 1.
-// In real arithmetic on the same float inputs these are linear in d:
-//   det = d.(-n), a_u = d.w_u (w_u = e2 x ao), a_v = d.w_v (w_v = ao x e1), and
-//   det - a_u - a_v = d.w_w (w_w = -(n + w_u + w_v)).
-// Float evaluation errors (|d_i| <= 1 + 4u): |det_f - det| <= E_n = 4u|n|,
-// |a_u_f - a_u| <= 8u|e2||ao|, |a_v_f - a_v| <= 8u|e1||ao|; an a_u within 2^-149|n| of 0 can
-// still round u to -0 (accepted), hence the 2^-149|n| floors.  A hit needs u+v <= 1 after
-// rounding, which implies d.w_w >= -(E_u + E_v + 1.01 E_n + 3.2u|n|).  So condition k certainly
-// fails for direction d when d.w_k < -E_k.
-// The camera's unnormalised direction is D(x', y') = (bl - C) + (vw x', 2y', 0) with bl, vw the
-// reference's float viewport corner and width (camera.rs:57-76), so D.w_k = K + A x' + B y' is
-// affine and its maximum over a pixel rectangle sits at a corner.  The reference's float
-// direction differs from D/|D| by at most 4u S (S = |bl| + vw + 2 + |C|) before and 4u after
-// normalisation, so condition k fails for every pixel of the rectangle when
-//   max_rect (K + A x' + B y') < -T_k,
-//   T_k = 2 * [ (E_k + 4u|w_k|) Dmax + 4u S |w_k| + 6u (|K| + |A| + |B|) ]
-// (Dmax = largest |D| over the frame; factor 2 = safety).  t >= 0 does not depend on d: when
-// ao.n < -2^-149 |n| (or |n|(1+8u) < 1e-6) no camera ray can hit the face and the whole
-// record rejects.  Any non-finite input disables culling for the face (T = +inf).
-__global__ void __launch_bounds__(256) tri_cull_kernel(const TriHot* __restrict__ hot, uint32_t T,
-                                                       float cx, float cy, float cz, float ratio,
-                                                       float z_dist, TriCull* __restrict__ cull) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= T) return;
-    const double u = 0x1p-24;
-    const TriHot h = hot[i];
-    const f3 e1f = mk3(h.q0.x, h.q0.y, h.q0.z), e2f = mk3(h.q0.w, h.q1.x, h.q1.y);
-    const f3 nf = mk3(h.q1.z, h.q1.w, h.q2.x), af = mk3(h.q2.y, h.q2.z, h.q2.w);
-    const f3 Cf = mk3(cx, cy, cz);
-    const f3 aof = sub(Cf, af);        // exactly the reference's `*ray.start() - a`
-    const float atf = dot0(aof, nf);   // exactly the reference's `ao.dot_product(&n)`
-    // camera.rs:57-76 in f32, as the reference computes it
-    const float vw = ratio * 2.0f;
-    const f3 bl = sub(sub(sub(Cf, divs(mk3(vw, 0.0f, 0.0f), 2.0f)), divs(mk3(0.0f, 2.0f, 0.0f), 2.0f)),
-                      mk3(0.0f, 0.0f, z_dist));
-    // doubles from here on
-    const double e1[3] = {e1f.x, e1f.y, e1f.z}, e2[3] = {e2f.x, e2f.y, e2f.z};
-    const double n[3] = {nf.x, nf.y, nf.z}, ao[3] = {aof.x, aof.y, aof.z};
-    const double blc[3] = {(double)bl.x - cx, (double)bl.y - cy, (double)bl.z - cz};
-    auto n1 = [](const double* v) { return fabs(v[0]) + fabs(v[1]) + fabs(v[2]); };
-    auto crs = [](const double* s, const double* o, double* r) {
-        r[0] = s[1] * o[2] - s[2] * o[1];
-        r[1] = s[2] * o[0] - s[0] * o[2];
-        r[2] = s[0] * o[1] - s[1] * o[0];
-    };
-    double wu[3], wv[3], ww[3], wn[3];
-    crs(e2, ao, wu);
-    crs(ao, e1, wv);
-    for (int k = 0; k < 3; ++k) {
-        ww[k] = -(n[k] + wu[k] + wv[k]);
-        wn[k] = -n[k];
-    }
-    const double nn = n1(n), ne1 = n1(e1), ne2 = n1(e2), nao = n1(ao);
-    const double floor_n = nn * 0x1p-149;
-    const double Eu = 8.0 * u * ne2 * nao + floor_n;
-    const double Ev = 8.0 * u * ne1 * nao + floor_n;
-    const double En = 4.0 * u * nn;
-    const double Ew = (8.0 * u * ne2 * nao) + (8.0 * u * ne1 * nao) + 1.01 * En + 3.2 * u * nn + floor_n;
-    // largest |D| over the frame (corners of x', y' in [0, 1]) and the magnitude scale S
-    double dmax = 0.0;
-    for (int cxr = 0; cxr < 2; ++cxr)
-        for (int cyr = 0; cyr < 2; ++cyr) {
-            double D0 = blc[0] + (double)vw * cxr, D1 = blc[1] + 2.0 * cyr, D2 = blc[2];
-            double l = sqrt(D0 * D0 + D1 * D1 + D2 * D2);
-            dmax = l > dmax ? l : dmax;
-        }
-    const double S = fabs((double)bl.x) + fabs((double)bl.y) + fabs((double)bl.z) + fabs((double)vw) + 2.0 +
-                     fabs((double)cx) + fabs((double)cy) + fabs((double)cz);
-    dmax = dmax * (1.0 + 1e-6) + 8.0 * u * S;
-    const double* W[4] = {wu, wv, ww, wn};
-    const double E[4] = {Eu, Ev, Ew, En};
-    float A[4], B[4], K[4], Tt[4];
-    bool finite = true;
-    for (int k = 0; k < 4; ++k) {
-        const double* w = W[k];
-        double Kd = blc[0] * w[0] + blc[1] * w[1] + blc[2] * w[2];
-        double Ad = (double)vw * w[0];
-        double Bd = 2.0 * w[1];
-        double thr = 2.0 * ((E[k] + 4.0 * u * n1(w)) * dmax + 4.0 * u * S * n1(w) +
-                            6.0 * u * (fabs(Kd) + fabs(Ad) + fabs(Bd)));
-        thr = thr * (1.0 + 0x1p-20) + 0x1p-126;  // round the float threshold up
-        A[k] = (float)Ad;
-        B[k] = (float)Bd;
-        K[k] = (float)Kd;
-        Tt[k] = (float)thr;
-        finite = finite && isfinite(A[k]) && isfinite(B[k]) && isfinite(K[k]) && isfinite(Tt[k]);
-    }
-    bool all_finite = finite && isfinite(atf) && isfinite(nn) && isfinite(nao) && isfinite(ne1) &&
-                      isfinite(ne2) && isfinite(dmax);
-    // t >= 0 fails for every camera ray / det >= 1e-6 is unreachable: reject the whole face
-    bool reject_all = all_finite && (((double)atf < -floor_n * 2.0) || (nn * (1.0 + 8.0 * u) < 1e-6));
-    if (!all_finite) {
-        for (int k = 0; k < 4; ++k) {
-            A[k] = B[k] = K[k] = 0.0f;
-            Tt[k] = __builtin_inff();
-        }
-    } else if (reject_all) {
-        A[3] = B[3] = K[3] = 0.0f;
-        Tt[3] = -__builtin_inff();
-    }
-    cull[i].A = make_float4(A[0], A[1], A[2], A[3]);
-    cull[i].B = make_float4(B[0], B[1], B[2], B[3]);
-    cull[i].K = make_float4(K[0], K[1], K[2], K[3]);
-    cull[i].T = make_float4(Tt[0], Tt[1], Tt[2], Tt[3]);
-}
-
-// ------------------------------------------------------------- object pixel rectangle ------
-// Union of the faces' conservative pixel rectangles (face_rect.hpp).
-__global__ void __launch_bounds__(256) tri_rect_kernel(const TriCull* __restrict__ cull, uint32_t T,
-                                                       uint32_t W, uint32_t H, uint32_t* __restrict__ acc) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t a[4] = {0u, 0u, 0u, 0u};
-    int32_t r[4];
-    if (i < T && face_rect(cull[i], W, H, r)) {
-        a[0] = ~(uint32_t)r[0];
-        a[1] = (uint32_t)r[1] + 1u;
-        a[2] = ~(uint32_t)r[2];
-        a[3] = (uint32_t)r[3] + 1u;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        for (int off = 32; off > 0; off >>= 1) a[k] = max(a[k], (uint32_t)__shfl_xor((int)a[k], off));
-    if ((threadIdx.x & 63) == 0 && a[1])
-        for (int k = 0; k < 4; ++k) atomicMax(acc + k, a[k]);
 }
 
 // true when condition k fails for every pixel of [xlo,xhi] x [ylo,yhi]
@@ -388,22 +193,11 @@ struct SceneLds {
     // Wave-uniform records (objects, materials, lights) by scalar loads from the device arrays,
     // not LDS reads + readfirstlane: C2 8.67 -> 8.40 us per frame (profiles/ab/ab_c2chain.log),
     // though one wave's chain alone is 0.2 us longer (7.26 -> 7.44 us, a 4-row frame).
-    // ERAY_AB_LDS_UNIFORM (A/B) restores the LDS reads.
-#ifndef ERAY_AB_LDS_UNIFORM
     __device__ ObjGeom geom(uint32_t i) const { return load_const(&g_objs[i].g, 0); }
     __device__ MaterialDesc mat(uint32_t i) const { return load_const(&g_objs[i].mat, 0); }
     __device__ LightDesc light(uint32_t i) const { return load_const(g_lights, i); }
-#else
-    __device__ ObjGeom geom(uint32_t i) const { return lds_uniform(&objs[i].g); }
-    __device__ MaterialDesc mat(uint32_t i) const { return lds_uniform(&objs[i].mat); }
-    __device__ LightDesc light(uint32_t i) const { return lds_uniform(lights + i); }
-#endif
     __device__ TriCull cull(uint32_t g) const { return culls[g]; }
-#ifdef ERAY_AB_SLOAD_HOT  // A/B: the candidate record by scalar loads (C2 8.38 -> 8.72 us: slower)
-    __device__ TriHot hot(uint32_t g) const { return load_const(g_tris, g); }
-#else
     __device__ TriHot hot(uint32_t g) const { return hots[g]; }  // broadcast read (VGPRs)
-#endif
     __device__ TriHot hot_lane(uint32_t g) const { return hots[g]; }
     __device__ TriShade shade(uint32_t g) const { return shades[g]; }
 };
@@ -439,7 +233,6 @@ __device__ SceneLds preload_scene(const FrameHot& p, char* dyn, Meanwhile&& mean
             v[k] = *src;
         }
         if (base == 0) {
-            ERAY_TRACE(13);
             meanwhile();
         }
 #pragma unroll
@@ -588,7 +381,7 @@ __device__ __forceinline__ void test_step(unsigned long long& mask, Face&& face,
     bool has[kB];
     TriHot h[kB];
 #pragma unroll
-    for (int k = 0; k < kB; ++k) {  // (fewer than kB left only with ERAY_AB_BATCH_FIXED)
+    for (int k = 0; k < kB; ++k) {
         has[k] = mask != 0;
         ids[k] = has[k] ? (uint32_t)(__ffsll(mask) - 1) : 0u;
         mask &= mask - 1;
@@ -618,11 +411,7 @@ __device__ __forceinline__ bool test_candidates(unsigned long long mask, Face&& 
                                                 const f3& o, const f3& d, int& found, float& hu, float& hv,
                                                 float& ht) {
     while (mask) {
-#ifdef ERAY_AB_BATCH_FIXED
-        const int n = kBatch;
-#else
         const int n = __popcll(mask);
-#endif
         if (n >= kBatch)
             test_step<kBatch>(mask, face, hot, st, o, d, found, hu, hv, ht);
         else if (n >= 2)
@@ -661,7 +450,6 @@ __device__ void first_hit(const FrameParams& p, const Scene& sc, uint32_t begin,
                 bool keep = false;
                 if (j < count) keep = !cull_rejects(sc.cull(begin + j), bd.xlo, bd.xhi, bd.ylo, bd.yhi);
                 mask = __ballot(keep);
-                ERAY_TRACE(10);
             } else if (kPlane) {  // rays already resolved (shadow rays): faces some lane may hit
                 const uint32_t n = min(64u, count - base);
                 mask = plane_mask(sc.hot_lane(begin + base + min(lane, n - 1)), n, st == kSearching, o, d);
@@ -714,23 +502,25 @@ constexpr uint32_t kWide = 16;  // candidates that may cover more pixels are tes
 // Per-wave LDS of the binned primary search.
 struct BinLds {
     float dir[3][64];         // each pixel's camera ray (lane = pixel)
-    uint32_t best[64];        // each pixel's earliest hit so far: bin position, 0xffffffff = none
+    uint32_t best[64];        // each pixel's first hit so far: face index, 0xffffffff = none
     TriHot cand[64];          // the chunk's candidate records (slot = lane that loaded it)
+    uint32_t face[64];        // ... and their face indices
     // (candidate slot << 6) | pixel, for every pixel a narrow candidate (<= kWide pixels) may hit
     uint16_t pairs[64 * kWide];
 };
 constexpr uint32_t kBinLdsBytes = (sizeof(BinLds) + 15) / 16 * 16;
 
 // Primary-ray first hit of a binned object (bins.hip), all four waves of the workgroup together
-// (every wave calls it; workgroup-uniform).  The reference's first hit by index is the smallest
-// index among the faces whose Triangle::intersects passes, so each wave's sub-block bin is cut
-// into chunks of 64 entries and the workgroup's chunks are dealt round-robin over its waves — a
-// bin at a dense spot (thousands of faces) is shared four ways.  A chunk is tested as (face,
-// pixel) pairs: each entry carries the pixels where its four culling bounds can pass
-// (bin_pixels), restricted to the sub-block's pixels still without a hit; narrow faces' pairs
-// are compacted in LDS and tested one per lane, wide ones by the whole wave; a hit lowers the
-// pixel's best bin position with an LDS atomicMin (positions grow with the face index).  Work
-// follows the pixels a face can cover, not 64 lanes per face.  Each wave then re-tests its
+// (every wave calls it; workgroup-uniform).  The reference's first hit is the smallest face index
+// whose Triangle::intersects passes (object.rs:63-78); a bin lists its faces in no particular
+// order, so each pixel keeps the smallest hitting face index seen so far (LDS atomicMin).  Each
+// wave's sub-block bin is cut into chunks of 64 entries and the workgroup's chunks are dealt
+// round-robin over its waves — a bin at a dense spot (thousands of faces) is shared four ways.  A
+// chunk is tested as (face, pixel) pairs: each entry carries the pixels where its four culling
+// bounds can pass (bin_pixels), restricted to the pixels whose best face is still above the
+// chunk's smallest face; narrow faces' pairs are compacted in LDS and tested one per lane, wide
+// ones by the whole wave, and a pair whose face is not below the pixel's best so far is skipped.
+// Work follows the pixels a face can cover, not 64 lanes per face.  Each wave then re-tests its
 // pixels' winners for u, v, t.
 template <typename Activate>
 __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32_t bin, int& st, const f3& o,
@@ -740,9 +530,7 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
     constexpr uint32_t kWaves = kWG / 64;
     BinLds& L = *reinterpret_cast<BinLds*>(s_bins + wave * kBinLdsBytes);
     uint32_t* s_range = reinterpret_cast<uint32_t*>(s_bins + kWaves * kBinLdsBytes);  // [lo, hi] per wave
-    ERAY_TRACE(16);
     uint32_t lo = load_const(ob.bin_start, bin), hi = load_const(ob.bin_start, bin + 1);
-    ERAY_TRACE_VAL(23, hi - lo);
     if (lo != hi && __any(st == kUndecided)) {  // every pixel's ray and bbox verdict, up front
         const bool a = activate();
         if (st == kUndecided) st = a ? kSearching : kDone;
@@ -757,7 +545,6 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
         s_range[2 * wave + 1] = hi;
     }
     __syncthreads();
-    ERAY_TRACE(17);
     uint32_t chunks[kWaves], total = 0;
 #pragma unroll
     for (uint32_t w = 0; w < kWaves; ++w) {
@@ -769,36 +556,39 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
         while (c >= chunks[w]) c -= chunks[w++];
         BinLds& T = *reinterpret_cast<BinLds*>(s_bins + w * kBinLdsBytes);  // the chunk's sub-block
         const uint32_t base = s_range[2 * w] + 64 * c, end = s_range[2 * w + 1];
-        // pixels of that sub-block this chunk can still improve: chunks run out of order, so a
-        // pixel stays live while its best position lies beyond the chunk's first entry
-        const unsigned long long live = __ballot(T.best[lane] > base);
-        if (!live) continue;
         const uint32_t j = base + lane;
-        unsigned long long pix = 0;  // live pixels this face may hit
+        uint32_t fj = 0xffffffffu;
+        unsigned long long pm = 0;
         if (j < end) {
-            pix = ob.bin_mask[j] & live;
+            fj = ob.bin_tri[j];
+            pm = ob.bin_mask[j];
             L.cand[lane] = ob.bin_hot[j];
+            L.face[lane] = fj;
         }
+        uint32_t cmin = fj;  // the chunk's smallest face
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) cmin = min(cmin, (uint32_t)__shfl_xor((int)cmin, off));
+        // pixels of that sub-block this chunk can still improve
+        const unsigned long long live = __ballot(T.best[lane] > cmin);
+        if (!live) continue;
+        const unsigned long long pix = pm & live;  // live pixels this face may hit
         const uint32_t cnt = (uint32_t)__popcll(pix);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();  // L.cand of this chunk visible to the wave
+        __builtin_amdgcn_wave_barrier();  // L.cand / L.face of this chunk visible to the wave
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // wide candidates (many pixels): the whole wave tests them, each lane its own pixel
         unsigned long long wide = __ballot(cnt > kWide);
-#ifdef ERAY_AB_X_NO_WIDE  // diagnostics only (wrong images)
-        wide = 0;
-#endif
         while (wide) {
             const uint32_t s = (uint32_t)(__ffsll(wide) - 1);
             wide &= wide - 1;
             const unsigned long long ps =
                 ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pix >> 32), (int)s) << 32) |
                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pix, (int)s);
-            const uint32_t pos = base + s;
-            if (((ps >> lane) & 1ull) && pos < T.best[lane]) {
+            const uint32_t fc = (uint32_t)__builtin_amdgcn_readlane((int)fj, (int)s);
+            if (((ps >> lane) & 1ull) && fc < T.best[lane]) {
                 float u, v, t;
                 const f3 dd = mk3(T.dir[0][lane], T.dir[1][lane], T.dir[2][lane]);
-                if (exact_test(L.cand[s], o, dd, u, v, t)) atomicMin(&T.best[lane], pos);
+                if (exact_test(L.cand[s], o, dd, u, v, t)) atomicMin(&T.best[lane], fc);
             }
         }
         // narrow candidates: (candidate, pixel) pairs compacted in LDS, one test per lane
@@ -820,33 +610,28 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#ifdef ERAY_AB_X_NO_PAIRS  // diagnostics only (wrong images): compaction without the tests
-        if (p.nobj != 12345) continue;
-#endif
         for (uint32_t q = 0; q < npairs; q += 64) {
             if (q + lane < npairs) {
                 const uint32_t pr = L.pairs[q + lane];
                 const uint32_t slot = pr >> 6, px = pr & 63;
-                const uint32_t pos = base + slot;
-                if (pos < T.best[px]) {  // a pixel already hit by an earlier face needs no test
+                const uint32_t fc = L.face[slot];
+                if (fc < T.best[px]) {  // a pixel already hit by an earlier face needs no test
                     float u, v, t;
                     const f3 dd = mk3(T.dir[0][px], T.dir[1][px], T.dir[2][px]);
-                    if (exact_test(L.cand[slot], o, dd, u, v, t)) atomicMin(&T.best[px], pos);
+                    if (exact_test(L.cand[slot], o, dd, u, v, t)) atomicMin(&T.best[px], fc);
                 }
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();  // L.cand / L.pairs are rewritten by the next chunk
+        __builtin_amdgcn_wave_barrier();  // L.cand / L.face / L.pairs are rewritten by the next chunk
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    ERAY_TRACE(18);
     __syncthreads();  // every chunk of every sub-block is done
-    ERAY_TRACE(19);
     const uint32_t mine = L.best[lane];
     if (st == kSearching && mine != 0xffffffffu) {
         float u, v, t;
-        exact_test(ob.bin_hot[mine], o, d, u, v, t);  // the winner again, for its u, v, t
-        found = (int)ob.bin_tri[mine];
+        exact_test(as_global_rec(p.tris + ob.tri_begin + mine), o, d, u, v, t);  // the winner again, for u, v, t
+        found = (int)mine;
         hu = u;
         hv = v;
         ht = t;
@@ -857,15 +642,22 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
 
 __device__ const float g_texel_dummy[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 
+// The frame's camera: the kernel arguments, or the setup kernel's copy in device-camera mode
+// (FrameParams::cam_state; wave-uniform, scalar loads).
+__device__ __forceinline__ CamDev frame_camera(const FrameParams& p) {
+    if (p.cam_state) return load_const(&p.cam_state->cam, 0);
+    return CamDev{p.cx, p.cy, p.cz, p.ratio, p.z_dist, {0u, 0u, 0u}};
+}
+
 // Camera::pixel_to_ray(x / W, y / H).dir (engine.rs:100-109, camera.rs:57-76, Ray::new)
-__device__ __forceinline__ f3 camera_dir(const FrameParams& p, uint32_t px, uint32_t y) {
-    const f3 C = mk3(p.cx, p.cy, p.cz);
+__device__ __forceinline__ f3 camera_dir(const CamDev& cam, const FrameParams& p, uint32_t px, uint32_t y) {
+    const f3 C = mk3(cam.cx, cam.cy, cam.cz);
     const float xf = (float)px / (float)p.cam_w;
     const float yf = (float)y / (float)p.cam_h;
-    const float vw = p.ratio * 2.0f;
+    const float vw = cam.ratio * 2.0f;
     const f3 horizontal = mk3(vw, 0.0f, 0.0f), vertical = mk3(0.0f, 2.0f, 0.0f);
     const f3 botleft = sub(sub(sub(C, divs(horizontal, 2.0f)), divs(vertical, 2.0f)),
-                           mk3(0.0f, 0.0f, p.z_dist));
+                           mk3(0.0f, 0.0f, cam.z_dist));
     return normalize(sub(add(add(botleft, mul(horizontal, xf)), mul(vertical, yf)), C));
 }
 
@@ -906,13 +698,9 @@ constexpr int kStoreSc1 = 16;  // CPol::SC1 (buffer instruction aux bits on gfx9
 template <typename B>
 __device__ __forceinline__ void stream16(B* base, const void* dst, uint4 v) {
     const u32x4 w{v.x, v.y, v.z, v.w};
-#if defined(ERAY_AB_STORE_NT)  // A/B (scripts/ab_variants.py): the non-temporal policy
-    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(const_cast<void*>(dst)));
-#else
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, -1, 0x00020000);
     const uint32_t off = (uint32_t)(reinterpret_cast<const char*>(dst) - reinterpret_cast<const char*>(base));
     __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, kStoreSc1);
-#endif
 }
 template <typename B>
 __device__ __forceinline__ void stream16(B* base, const void* dst, float4 v) {
@@ -996,12 +784,12 @@ __device__ __forceinline__ bool rect_meets(const ObjGeom& ob, const FrameParams&
 // without them carries none of their code or registers.
 constexpr int kMatSpecPow = 1, kMatExample = 2;
 template <bool kCull, bool kLdsTiles, int kMat, typename Scene>
-__device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc, uint32_t wx0, uint32_t py0,
+__device__ __forceinline__ void render_sub(const FrameParams& p, const CamDev& cam, const Scene& sc, uint32_t wx0, uint32_t py0,
                                            bool active, TriHot* s_hot, TriCull* s_cull, char* s_bins, float4* s_rgb,
                                            uint32_t* s_ppm, bool aligned, const f3* given_d = nullptr) {
     constexpr bool kSpecPow = (kMat & kMatSpecPow) != 0, kExample = (kMat & kMatExample) != 0;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const f3 C = mk3(p.cx, p.cy, p.cz);
+    const f3 C = mk3(cam.cx, cam.cy, cam.cz);
     const uint32_t px = wx0 + (lane % kSubW), ly = lane / kSubW;
     const uint32_t py = py0 + ly;
     const bool valid = active && px < p.cam_w && py < p.rows;
@@ -1018,7 +806,6 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
     for (uint32_t oi = 0; oi < p.nobj; ++oi) {
         const ObjGeom ob = sc.geom(oi);  // uniform
         const bool direct = !kLdsTiles || ob.tri_count <= kDirectMax;
-        ERAY_TRACE(9);
         // outside the object's pixel rectangle no primary ray can hit it (only where skipping
         // keeps the workgroup's barriers uniform)
         if (kCull && direct && !rect_meets(ob, p, wx0, py0)) continue;
@@ -1026,12 +813,10 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
             if (!ray_ready) {
                 uint32_t pxo = px, yo = y;  // opaque: keep ray generation on this path
                 asm volatile("" : "+v"(pxo), "+v"(yo));
-                d = camera_dir(p, pxo, yo);
+                d = camera_dir(cam, p, pxo, yo);
                 ray_ready = true;
-                ERAY_TRACE(11);
             }
             const bool bb = bbox_hit(ob, C, d);
-            ERAY_TRACE(14);
             return bb;
         };
         int st = valid ? kUndecided : kDone, f = -1;
@@ -1061,7 +846,6 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
         }
     }
 
-    ERAY_TRACE(2);
     // ---- hit data and Material::get (material.rs:56-94) --------------------------
     // The object loop only finds each lane's texel addresses; the loads are issued once after
     // it and first used by the shading, so their latency overlaps the shadow rays.
@@ -1105,9 +889,6 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
     }
     // every lane loads (a lane without the texture reads a dummy word); Material::get's values
     // are selected where the shading first needs them
-#ifdef ERAY_AB_X_NO_TEXTURE  // diagnostics only (wrong images): the texture fetch's cost
-    tc = tkd = tks = tsp = nullptr;
-#endif
     const bool has_c = tc, has_kd = tkd, has_ks = tks, has_sp = kSpecPow && tsp;
     const auto* tcg = as_global(tc ? tc : g_texel_dummy);
     const float vc0 = tcg[0], vc1 = tcg[1], vc2 = tcg[2];
@@ -1123,11 +904,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
         if (has_ks) ks = vks;
         if (has_sp) sp = vsp;
     };
-#ifdef ERAY_AB_EARLY_MATERIAL
-    material();
-#endif
 
-    ERAY_TRACE(3);
     bool any = false;  // the lighting list as a running left fold (color.rs:82-87)
     rgb acc{0.0f, 0.0f, 0.0f};
     auto push = [&](rgb c) {
@@ -1164,13 +941,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
                     dist = len(sub(Lp, S));
                 }
             };
-#ifdef ERAY_AB_X_NO_SHADOW  // diagnostics only (wrong images): the shadow scan's cost
-            if (p.nobj != 12345) decided = true;
-#endif
             for (uint32_t oj = 0; oj < p.nobj; ++oj) {
-#ifdef ERAY_AB_X_NO_SHADOW
-                if (p.nobj != 12345) break;
-#endif
                 const ObjGeom ob = sc.geom(oj);
                 int f = -1;
                 float u, v, t;
@@ -1196,15 +967,12 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
                         if (!test_candidates(mask, face, hot, st, S, sd, f, u, v, t)) break;
                     }
                 } else {
-                    ERAY_TRACE(20);
                     shadow_ray();
                     int st = (have && !decided && bbox_hit(ob, S, sd)) ? kSearching : kDone;
                     auto never = []() { return false; };
                     first_hit<false, kLdsTiles>(p, sc, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot, s_cull,
                                                 never, f, u, v, t);
-                    ERAY_TRACE(21);
                 }
-                ERAY_TRACE(15);
                 if (f >= 0) {
                     const f3 hp = add(S, mul(sd, t));
                     reached = len(sub(hp, S)) > dist;
@@ -1250,7 +1018,6 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
         push(rgb{0.1f, 0.1f, 0.2f});  // engine.rs:355-357
     }
 
-    ERAY_TRACE(4);
     // ---- outputs: Image::set + Color::as_bytes, rows bottom-up (image.rs:41-74) ---
     const uint32_t b0 = sat_u8(acc.r * 255.0f), b1 = sat_u8(acc.g * 255.0f), b2 = sat_u8(acc.b * 255.0f);
     if (valid && p.out_face) p.out_face[(size_t)py * p.img_w + px] = have ? best_face : -1;
@@ -1302,15 +1069,19 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const Scene& sc
             o[2] = (uint8_t)b2;
         }
     }
-    ERAY_TRACE(5);
 }
 
-// detail rectangle k of the frame (kernel arguments, uniform index: scalar loads)
+// detail rectangle k of the frame (kernel arguments, or the setup's CamState in device-camera
+// mode; uniform index: scalar loads)
 struct SubRect {  // sub-block coordinates (x in kSubW columns, y in kBlkH local rows), inclusive
     int32_t sx0, sx1, sy0, sy1;
 };
 __device__ __forceinline__ SubRect frame_rect(const FrameParams& p, uint32_t k) {
+    if (p.cam_state) return load_const(reinterpret_cast<const SubRect*>(p.cam_state->rects), k);
     return SubRect{p.rects[k][0], p.rects[k][1], p.rects[k][2], p.rects[k][3]};
+}
+__device__ __forceinline__ uint32_t frame_nrect(const FrameParams& p) {
+    return p.cam_state ? load_const(&p.cam_state->nrect, 0) : p.nrect;
 }
 __device__ __forceinline__ bool inside(const SubRect& r, int32_t sx, int32_t sy) {
     return sx >= r.sx0 && sx <= r.sx1 && sy >= r.sy0 && sy <= r.sy1;
@@ -1325,6 +1096,7 @@ __device__ __forceinline__ void fill_blocks(const FrameParams& p, uint32_t f, ui
     const uint32_t fstride = nf * nwaves;
     uint32_t occ = 0;  // detail list: lane i holds the occupancy of this wave's i-th next block
     uint32_t it = 0;
+    const uint32_t nrect = p.detail_occ ? 0u : frame_nrect(p);
     // block coordinates advance incrementally (no integer division per block)
     const uint32_t first = wave * nf + f, step_y = fstride / p.tiles_x, step_x = fstride - step_y * p.tiles_x;
     uint32_t by = first / p.tiles_x, bx = first - by * p.tiles_x;
@@ -1345,7 +1117,7 @@ __device__ __forceinline__ void fill_blocks(const FrameParams& p, uint32_t f, ui
             }
             mask = (uint32_t)__builtin_amdgcn_readlane((int)occ, (int)(it & 63u));
         }
-        for (uint32_t k = 0; k < p.nrect && !p.detail_occ; ++k) {
+        for (uint32_t k = 0; k < nrect; ++k) {
             const SubRect r = frame_rect(p, k);
             if ((int32_t)by < r.sy0 || (int32_t)by > r.sy1) continue;
 #pragma unroll
@@ -1378,8 +1150,9 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     // a kernel-argument load from memory
     const FrameHot hot{h_objects, h_lights, h_cull, h_tris, h_shade, h_counts, h_total_tris, h_total_sub,
                        h_roles & 0x7fffu};
-    const uint32_t detail_wgs = (h_roles >> 15) & 0x7fffu;
-    const bool fill_first = (h_roles >> 30) & 1u, separate_fill = (h_roles >> 31) & 1u;
+    uint32_t detail_wgs = (h_roles >> 15) & 0x7fffu;
+    bool fill_first = (h_roles >> 30) & 1u;
+    const bool separate_fill = (h_roles >> 31) & 1u;
     // large objects: LDS tiles (shadow rays, brute force) and, aliased, the per-wave binned
     // primary search (first_hit ends its tile loop on a barrier, so the two never overlap)
     constexpr size_t kTileBytes = kTriTile * (sizeof(TriHot) + ((kCull && kLdsTiles) ? sizeof(TriCull) : 0));
@@ -1394,7 +1167,13 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t nwaves = kWG / 64;
     const bool aligned = p.aligned != 0;  // (a kernel-argument read where it is used)
-    const uint32_t total = hot.total_sub;  // detail sub-blocks
+    // detail sub-blocks (device-camera mode: counted by the setup kernels, and the small-scene
+    // fill reservation chosen from that count as launch_frame_kernel does from the host's)
+    const uint32_t total = p.cam_state ? load_const(&p.cam_state->total_sub, 0) : hot.total_sub;
+    if (p.cam_state && p.detail_wgs_alt && total > detail_wgs * nwaves) {
+        detail_wgs = p.detail_wgs_alt;
+        fill_first = true;
+    }
     const uint32_t grid = hot.grid;        // == gridDim.x, without the implicit-argument load
     // workgroups [0, nd) render the detail sub-blocks (persistent: rounds of nd * 4 sub-blocks),
     // the others write the background at the same time; at most detail_wgs detail workgroups
@@ -1405,14 +1184,11 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     // the workgroup's role index: detail roles [0, nd), fill roles [nd, grid); with fill_first
     // the fill roles go to the first-dispatched (older, VALU-priority) workgroups
     const uint32_t bid = (fill_first && nd < grid) ? (blockIdx.x + nd) % grid : blockIdx.x;
-    ERAY_TRACE_CLEAR();
-    ERAY_TRACE(0);
 
     // ---- detail sub-blocks -------------------------------------------------------------------
     if (bid < nd) {
-#ifdef ERAY_AB_X_NO_DETAIL  // diagnostics only (wrong images): the fill alone, same grid
-        if (nd < grid) return;
-#endif
+        const uint32_t nrect = p.detail_list ? 0u : frame_nrect(p);
+        const CamDev cam = frame_camera(p);
         // detail sub-block j (enumeration order) -> sub-block coordinates
         auto locate = [&](uint32_t j, int32_t& sx, int32_t& sy) {
             if (p.detail_list) {
@@ -1421,7 +1197,7 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
                 sy = (int32_t)(e >> 16);
                 return;
             }
-            for (uint32_t k = 0; k < p.nrect; ++k) {  // the rectangles are disjoint (host): by area
+            for (uint32_t k = 0; k < nrect; ++k) {  // the rectangles are disjoint (setup): by area
                 const SubRect r = frame_rect(p, k);
                 const uint32_t w = (uint32_t)(r.sx1 - r.sx0 + 1);
                 const uint32_t a = w * (uint32_t)(r.sy1 - r.sy0 + 1);
@@ -1438,64 +1214,42 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
         const uint32_t c0 = bid * nwaves;
         int32_t sx0 = 0, sy0 = 0;
         f3 d0;
-#ifdef ERAY_AB_LAZY_RAY
-        constexpr bool kGivenRay = false;
-        auto first_rays = [&]() {
-            if (c0 + wave < total) locate(c0 + wave, sx0, sy0);
-        };
-#else
         constexpr bool kGivenRay = true;
         auto first_rays = [&]() {
             if (c0 + wave < total) locate(c0 + wave, sx0, sy0);
-            d0 = camera_dir(p, (uint32_t)sx0 * kSubW + lane % kSubW, p.row0 + (uint32_t)sy0 * kBlkH + lane / kSubW);
+            d0 = camera_dir(cam, p, (uint32_t)sx0 * kSubW + lane % kSubW, p.row0 + (uint32_t)sy0 * kBlkH + lane / kSubW);
             asm volatile("" : "+v"(d0.x), "+v"(d0.y), "+v"(d0.z));  // here, not after the barrier
         };
-#endif
         auto detail = [&](const auto& sc) {
             for (uint32_t c = c0; c < total; c += nd * nwaves) {  // workgroup-uniform
                 const uint32_t j = c + wave;
                 const bool active = j < total;
                 int32_t sx = sx0, sy = sy0;
                 if (c != c0 && active) locate(j, sx, sy);
-                render_sub<kCull, kLdsTiles, kMat>(p, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH, active,
+                render_sub<kCull, kLdsTiles, kMat>(p, cam, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH, active,
                                                        s_hot, s_cull, s_bins, s_rgb, s_ppm, aligned,
                                                        (kGivenRay && c == c0) ? &d0 : nullptr);
-#ifdef ERAY_PHASE_TRACE_REPEAT  // diagnostics: the same sub-block again, instruction cache warm
-                ERAY_TRACE(6);
-                render_sub<kCull, kLdsTiles, kMat>(p, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH, active,
-                                                       s_hot, s_cull, s_bins, s_rgb, s_ppm, aligned);
-#endif
             }
         };
         if constexpr (kLdsScene) {
             const SceneLds sc = preload_scene(hot, dyn, first_rays);
-            ERAY_TRACE(12);
             __syncthreads();
-            ERAY_TRACE(1);
             detail(sc);
         } else {
             const SceneGlobal sc{p};
             first_rays();
-            ERAY_TRACE(1);
             detail(sc);
         }
-        ERAY_TRACE(7);
         if (nd < grid) {
-            ERAY_TRACE_FLUSH();
             return;
         }
     }
 
     // ---- background of the non-detail sub-blocks ---------------------------------------------
-#ifdef ERAY_AB_X_NO_FILL  // diagnostics only (wrong images): the detail work alone
-    if (p.nobj != 12345) return;
-#endif
     if (separate_fill) return;  // fill_kernel writes the background beside this launch
     const uint32_t nf = nd < grid ? grid - nd : grid;  // filling workgroups
     const uint32_t f = nd < grid ? bid - nd : bid;
     fill_blocks(p, f, nf, wave, lane, aligned);
-    ERAY_TRACE(8);
-    ERAY_TRACE_FLUSH();
 }
 
 // The background alone, beside a detail-only frame kernel on another stream (FrameParams::
@@ -1529,27 +1283,6 @@ hipError_t launch_tri_precompute(const float* pos, const float* nrm, const float
     return hipGetLastError();
 }
 
-hipError_t launch_tri_cull(const TriHot* hot, uint32_t T, float cx, float cy, float cz, float ratio,
-                           float z_dist, TriCull* cull, hipStream_t s) {
-    if (!T) return hipSuccess;
-    tri_cull_kernel<<<(T + 255) / 256, 256, 0, s>>>(hot, T, cx, cy, cz, ratio, z_dist, cull);
-    return hipGetLastError();
-}
-
-#ifdef ERAY_PHASE_TRACE
-extern "C" int eray_debug_trace(uint64_t* out, size_t n) {
-    if (n > sizeof(g_trace) / sizeof(uint64_t)) n = sizeof(g_trace) / sizeof(uint64_t);
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace), n * sizeof(uint64_t)) == hipSuccess ? 0 : -2;
-}
-#endif
-
-hipError_t launch_tri_rect(const TriCull* cull, uint32_t T, uint32_t cam_w, uint32_t cam_h, uint32_t* acc,
-                           hipStream_t s) {
-    if (!T) return hipSuccess;
-    tri_rect_kernel<<<(T + 255) / 256, 256, 0, s>>>(cull, T, cam_w, cam_h, acc);
-    return hipGetLastError();
-}
-
 namespace {
 // Persistent grid: as many workgroups as are resident at once (occupancy API), capped by the
 // work (fill blocks or detail sub-blocks, whichever needs more workgroups).
@@ -1559,27 +1292,36 @@ uint32_t frame_roles(uint32_t grid, const FrameParams& q) {
            ((q.separate_fill ? 1u : 0u) << 31);
 }
 
-template <bool C, bool L, int M, bool K, bool D = false>
-hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, hipStream_t s) {
-    static int per_cu = -1, cus = 0;
-    static size_t per_cu_dyn = 0;
-    if (per_cu < 0 || per_cu_dyn != dyn) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, frame_kernel<C, L, M, K, D>, kWG, dyn) !=
-                hipSuccess ||
-            per_cu <= 0)
-            per_cu = 1;
-        per_cu_dyn = dyn;
-    }
-    static const int cap = [] {  // tuning knob (diagnostics): workgroups per CU at most
-        const char* e = getenv("ERAY_FRAME_WG_PER_CU");
-        return e ? atoi(e) : 0;
+uint32_t device_cus() {
+    static const uint32_t cus = [] {  // (thread-safe initialisation)
+        int dev = 0, n = 0;
+        return (hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+                   ? (uint32_t)n
+                   : 256u;
     }();
-    const int wg_cu = cap > 0 && cap < per_cu ? cap : per_cu;
-    const uint32_t grid = min(want, (uint32_t)(wg_cu * cus));
+    return cus;
+}
+
+template <bool C, bool L, int M, bool K, bool D = false>
+hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, const LaunchCtx& lc, hipStream_t s) {
+    static std::mutex mu;  // resident workgroups per CU of this build, per dynamic LDS size
+    static int per_cu = -1;
+    static size_t per_cu_dyn = 0;
+    int wg_cu;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        if (per_cu < 0 || per_cu_dyn != dyn) {
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, frame_kernel<C, L, M, K, D>, kWG, dyn) !=
+                    hipSuccess ||
+                per_cu <= 0)
+                per_cu = 1;
+            per_cu_dyn = dyn;
+        }
+        wg_cu = per_cu;
+    }
+    const uint32_t cus = device_cus();
+    const uint32_t grid = min(want, (uint32_t)wg_cu * cus);
     // Workgroups kept for the fill so that it overlaps a large detail area instead of following
     // it: one per 64 background blocks, at most 1/share of the grid.  Measured (graph-replayed
     // frames, profiles/ab/ab_knobs*.log): the fill needs enough store-issuing waves on every CU
@@ -1588,26 +1330,24 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
     // (27.8 us; share 3 29.4-30.3, share 4 37), while a small-scene frame with more than one
     // round of detail sub-blocks (the cube at 3840x2160) wants one fill workgroup per CU
     // dispatched first (share 3, fill_first: 22.8 -> 20.4 us; at C2 fill_first costs 0.7 us).
-    // Diagnostics knobs ERAY_FILL_SHARE (0 = no reservation) and ERAY_FILL_FIRST override.
-    const char* e_share = getenv("ERAY_FILL_SHARE");
-    const char* e_first = getenv("ERAY_FILL_FIRST");
     const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
     auto detail_wgs = [&](float share) {
         return share >= 1.0f && grid >= 2 ? grid - max(min((uint32_t)((float)grid / share), (nblk + 63) / 64), 1u)
                                           : 0u;
     };
-    float share = 2.0f;
-    uint32_t fill_first = 0;
-    if (!L && p.total_sub > detail_wgs(share) * (kWG / 64)) {
-        share = 3.0f;
-        fill_first = 1;
-    }
-    if (L && !D) fill_first = 1;  // the 2-per-CU large-mesh build (C3): 13.0 -> 12.7-12.9 us
-    if (e_share) share = (float)atof(e_share);
-    if (e_first) fill_first = (uint32_t)atoi(e_first);
     FrameParams q = p;
-    q.detail_wgs = detail_wgs(share);
-    q.fill_first = fill_first;
+    q.detail_wgs = detail_wgs(2.0f);
+    q.fill_first = 0;
+    q.detail_wgs_alt = 0;
+    if (!L) {
+        if (p.cam_state) {  // the count is on the device: frame_kernel picks the share
+            q.detail_wgs_alt = detail_wgs(3.0f);
+        } else if (p.total_sub > q.detail_wgs * (kWG / 64)) {
+            q.detail_wgs = detail_wgs(3.0f);
+            q.fill_first = 1;
+        }
+    }
+    if (L && !D) q.fill_first = 1;  // the 2-per-CU large-mesh build (C3): 13.0 -> 12.7-12.9 us
     q.separate_fill = 0;
     if constexpr (D) {
         // Separate fill: the dense build does detail work only, at most 2 workgroups per CU, and
@@ -1616,42 +1356,29 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
         // Measured (profiles/ab/ab_sepfill.log): with many rounds of detail sub-blocks the detail
         // waves get the register budget the fill roles held (C5's frame 216 -> 190 us); with
         // ~2 rounds the single launch overlaps better (3840x2160 / 70k 27.9 vs 37.8 us).  Used
-        // above 16 detail sub-blocks per CU; knobs ERAY_SEPARATE_FILL (0 never, 1 always),
-        // ERAY_SEP_DETAIL_PER_CU, ERAY_SEP_FILL_PER_CU (diagnostics and tests).
-        const char* e_sep = getenv("ERAY_SEPARATE_FILL");
-        const bool separate = e_sep ? atoi(e_sep) > 0 : p.total_sub > 16u * (uint32_t)cus;
+        // above 16 detail sub-blocks per CU (ERAY_RENDER_SEPARATE_FILL / _NO_SEPARATE_FILL force
+        // it on / off).
+        const bool separate = (p.launch_flags & kLaunchSeparateFill)     ? true
+                              : (p.launch_flags & kLaunchNoSeparateFill) ? false
+                                                                         : p.total_sub > 16u * cus;
         if (separate) {
-            const char* e_dpc = getenv("ERAY_SEP_DETAIL_PER_CU");
-            const char* e_fpc = getenv("ERAY_SEP_FILL_PER_CU");
-            const uint32_t dpc = e_dpc ? (uint32_t)atoi(e_dpc) : 2u, fpc = e_fpc ? (uint32_t)atoi(e_fpc) : 2u;
-            int dev = 0;
-            if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-            static hipStream_t side[64];
-            static hipEvent_t fork_ev[64], join_ev[64];
-            hipError_t e = hipSuccess;
-            if (!side[dev]) {
-                if ((e = hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking)) != hipSuccess ||
-                    (e = hipEventCreateWithFlags(&fork_ev[dev], hipEventDisableTiming)) != hipSuccess ||
-                    (e = hipEventCreateWithFlags(&join_ev[dev], hipEventDisableTiming)) != hipSuccess)
-                    return e;
-            }
+            if (!lc.side || !lc.fork || !lc.join) return hipErrorInvalidValue;
             q.separate_fill = 1;
             q.detail_wgs = 0;
             q.fill_first = 0;
-            const uint32_t dgrid =
-                max(1u, min(min(grid, max(dpc, 1u) * (uint32_t)cus), (p.total_sub + kWG / 64 - 1) / (kWG / 64)));
-            const uint32_t fgrid = max(1u, min(max(fpc, 1u) * (uint32_t)cus, (nblk + 3) / 4));
-            if ((e = hipEventRecord(fork_ev[dev], s)) != hipSuccess ||
-                (e = hipStreamWaitEvent(side[dev], fork_ev[dev], 0)) != hipSuccess)
+            const uint32_t dgrid = max(1u, min(min(grid, 2u * cus), (p.total_sub + kWG / 64 - 1) / (kWG / 64)));
+            const uint32_t fgrid = max(1u, min(2u * cus, (nblk + 3) / 4));
+            hipError_t e;
+            if ((e = hipEventRecord(lc.fork, s)) != hipSuccess || (e = hipStreamWaitEvent(lc.side, lc.fork, 0)) != hipSuccess)
                 return e;
             frame_kernel<C, L, M, K, D><<<dgrid, kWG, dyn, s>>>(q.objects, q.lights, q.cull, q.tris, q.shade,
                                                              q.nobj | (q.nlights << 16), q.total_tris, q.total_sub,
                                                              frame_roles(dgrid, q), q);
             if ((e = hipGetLastError()) != hipSuccess) return e;
-            fill_kernel<<<fgrid, kWG, 0, side[dev]>>>(q);
+            fill_kernel<<<fgrid, kWG, 0, lc.side>>>(q);
             if ((e = hipGetLastError()) != hipSuccess) return e;
-            if ((e = hipEventRecord(join_ev[dev], side[dev])) != hipSuccess) return e;
-            return hipStreamWaitEvent(s, join_ev[dev], 0);
+            if ((e = hipEventRecord(lc.join, lc.side)) != hipSuccess) return e;
+            return hipStreamWaitEvent(s, lc.join, 0);
         }
     }
     frame_kernel<C, L, M, K, D><<<grid, kWG, dyn, s>>>(q.objects, q.lights, q.cull, q.tris, q.shade,
@@ -1661,56 +1388,51 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
 }
 
 template <bool C, int M>
-hipError_t launch_frame_cs(const FrameParams& p, uint32_t want, hipStream_t s) {
+hipError_t launch_frame_cs(const FrameParams& p, uint32_t want, const LaunchCtx& lc, hipStream_t s) {
     // small scenes are preloaded into LDS whole (no object then needs the LDS tiles); otherwise
     // everything is read from the device arrays
     if (p.lds_scene) {
         const size_t dyn = scene_lds_layout(p.nobj, p.nlights, p.total_tris, C).bytes;
-        return launch_frame_kernel<C, false, M, true>(p, want, dyn, s);
+        return launch_frame_kernel<C, false, M, true>(p, want, dyn, lc, s);
     }
     if (p.max_object_tris > kDirectMax) {
         if constexpr (!(M & kMatSpecPow)) {
             // more detail sub-blocks than the 2-per-CU grid's detail waves (half the grid, four
             // waves each: launch_frame_kernel) take in one round: the 3-per-CU build
-            const char* e = getenv("ERAY_DENSE_DETAIL");  // tests/diagnostics: 0 never, 1 always
-            const int dense = e ? atoi(e) : -1;
-            static const uint32_t cus = [] {
-                int dev = 0, n = 0;
-                return (hipGetDevice(&dev) == hipSuccess &&
-                        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-                           ? (uint32_t)n
-                           : 256u;
-            }();
-            if (dense == 1 || (dense < 0 && p.total_sub > cus * (kWG / 64)))
-                return launch_frame_kernel<C, true, M, false, true>(p, want, 0, s);
+            // (ERAY_RENDER_DENSE_DETAIL / _NO_DENSE_DETAIL force it on / off)
+            const bool dense = (p.launch_flags & kLaunchDense)     ? true
+                               : (p.launch_flags & kLaunchNoDense) ? false
+                                                                   : p.total_sub > device_cus() * (kWG / 64);
+            if (dense) return launch_frame_kernel<C, true, M, false, true>(p, want, 0, lc, s);
         }
-        return launch_frame_kernel<C, true, M, false>(p, want, 0, s);
+        return launch_frame_kernel<C, true, M, false>(p, want, 0, lc, s);
     }
-    return launch_frame_kernel<C, false, M, false>(p, want, 0, s);
+    return launch_frame_kernel<C, false, M, false>(p, want, 0, lc, s);
 }
 }  // namespace
 
-hipError_t launch_render(const FrameParams& p, hipStream_t s) {
+hipError_t launch_render(const FrameParams& p, const LaunchCtx& lc, hipStream_t s) {
     if (p.aa || p.bounces) return launch_trace(p, s);
     const uint32_t by_n = (p.rows + kBlkH - 1) / kBlkH;
     const uint32_t nblk = p.tiles_x * by_n;
     if (!nblk) return hipSuccess;
-    // enough workgroups for one fill block or one round of detail sub-blocks per wave
-    const uint32_t want = max((nblk + 3) / 4, (p.total_sub + 3) / 4);
+    // enough workgroups for one fill block or one round of detail sub-blocks per wave (device-
+    // camera mode: the detail count is not known here, so as many as fit)
+    const uint32_t want = p.cam_state ? max((nblk + 3) / 4, nblk) : max((nblk + 3) / 4, (p.total_sub + 3) / 4);
     const int mat = (p.spec_pow ? kMatSpecPow : 0) | (p.example_mat ? kMatExample : 0);
     if (p.cull) {
         switch (mat) {
-            case 0: return launch_frame_cs<true, 0>(p, want, s);
-            case kMatSpecPow: return launch_frame_cs<true, kMatSpecPow>(p, want, s);
-            case kMatExample: return launch_frame_cs<true, kMatExample>(p, want, s);
-            default: return launch_frame_cs<true, kMatSpecPow | kMatExample>(p, want, s);
+            case 0: return launch_frame_cs<true, 0>(p, want, lc, s);
+            case kMatSpecPow: return launch_frame_cs<true, kMatSpecPow>(p, want, lc, s);
+            case kMatExample: return launch_frame_cs<true, kMatExample>(p, want, lc, s);
+            default: return launch_frame_cs<true, kMatSpecPow | kMatExample>(p, want, lc, s);
         }
     }
     switch (mat) {
-        case 0: return launch_frame_cs<false, 0>(p, want, s);
-        case kMatSpecPow: return launch_frame_cs<false, kMatSpecPow>(p, want, s);
-        case kMatExample: return launch_frame_cs<false, kMatExample>(p, want, s);
-        default: return launch_frame_cs<false, kMatSpecPow | kMatExample>(p, want, s);
+        case 0: return launch_frame_cs<false, 0>(p, want, lc, s);
+        case kMatSpecPow: return launch_frame_cs<false, kMatSpecPow>(p, want, lc, s);
+        case kMatExample: return launch_frame_cs<false, kMatExample>(p, want, lc, s);
+        default: return launch_frame_cs<false, kMatSpecPow | kMatExample>(p, want, lc, s);
     }
 }
 

@@ -1,0 +1,299 @@
+// setup.hip — per-camera setup of the frame kernel, entirely on the device.
+//
+// A camera change (Scene::set_camera, scene.rs:39-54, before Engine::render, engine.rs:46-81)
+// needs, before its frame: every triangle's culling record for the new camera, the objects'
+// pixel rectangles and the frame's merged detail rectangles.  One kernel does it all and leaves
+// the results in device memory (CamState, the object descriptors): nothing is read back, so the
+// frame kernel can follow at once and a sequence of cameras can be replayed from one HIP graph.
+// The last workgroup to finish (a device-scope counter) reduces the per-object accumulators and
+// resets them and the counter for the next setup.
+#include "device_math.hpp"
+#include "face_rect.hpp"
+#include "internal.hpp"
+
+namespace eray {
+namespace gpu {
+namespace {
+
+using namespace eray::dev;
+
+constexpr int kSetupWG = 128;
+
+// --------------------------------------------------------------------- culling record ------
+// Derivation (u = 2^-24, all norms are 1-norms of the float inputs; d = normalised direction).
+// The reference computes, in f32 from ao = C - a (C the camera centre),
+//   det = -(d.n),  a_u = e2.(ao x d),  a_v = -(e1.(ao x d)),  u = a_u/det, v = a_v/det,
+//   t = (ao.n)/det,  hit iff det >= 1e-6, t >= 0, u >= 0, v >= 0, u + v <= 1.
+// In real arithmetic on the same float inputs these are linear in d:
+//   det = d.(-n), a_u = d.w_u (w_u = e2 x ao), a_v = d.w_v (w_v = ao x e1), and
+//   det - a_u - a_v = d.w_w (w_w = -(n + w_u + w_v)).
+// Float evaluation errors (|d_i| <= 1 + 4u): |det_f - det| <= E_n = 4u|n|,
+// |a_u_f - a_u| <= 8u|e2||ao|, |a_v_f - a_v| <= 8u|e1||ao|; an a_u within 2^-149|n| of 0 can
+// still round u to -0 (accepted), hence the 2^-149|n| floors.  A hit needs u+v <= 1 after
+// rounding, which implies d.w_w >= -(E_u + E_v + 1.01 E_n + 3.2u|n|).  So condition k certainly
+// fails for direction d when d.w_k < -E_k.
+// The camera's unnormalised direction is D(x', y') = (bl - C) + (vw x', 2y', 0) with bl, vw the
+// reference's float viewport corner and width (camera.rs:57-76), so D.w_k = K + A x' + B y' is
+// affine and its maximum over a pixel rectangle sits at a corner.  The reference's float
+// direction differs from D/|D| by at most 4u S (S = |bl| + vw + 2 + |C|) before and 4u after
+// normalisation, so condition k fails for every pixel of the rectangle when
+//   max_rect (K + A x' + B y') < -T_k,
+//   T_k = 2 * [ (E_k + 4u|w_k|) Dmax + 4u S |w_k| + 6u (|K| + |A| + |B|) ]
+// (Dmax = largest |D| over the frame; factor 2 = safety).  t >= 0 does not depend on d: when
+// ao.n < -2^-149 |n| (or |n|(1+8u) < 1e-6) no camera ray can hit the face and the whole
+// record rejects.  Any non-finite input disables culling for the face (T = +inf).
+__device__ TriCull cull_record(const TriHot& h, const CamDev& cam) {
+    const double u = 0x1p-24;
+    const float cx = cam.cx, cy = cam.cy, cz = cam.cz;
+    const f3 e1f = mk3(h.q0.x, h.q0.y, h.q0.z), e2f = mk3(h.q0.w, h.q1.x, h.q1.y);
+    const f3 nf = mk3(h.q1.z, h.q1.w, h.q2.x), af = mk3(h.q2.y, h.q2.z, h.q2.w);
+    const f3 Cf = mk3(cx, cy, cz);
+    const f3 aof = sub(Cf, af);        // exactly the reference's `*ray.start() - a`
+    const float atf = dot0(aof, nf);   // exactly the reference's `ao.dot_product(&n)`
+    // camera.rs:57-76 in f32, as the reference computes it
+    const float vw = cam.ratio * 2.0f;
+    const f3 bl = sub(sub(sub(Cf, divs(mk3(vw, 0.0f, 0.0f), 2.0f)), divs(mk3(0.0f, 2.0f, 0.0f), 2.0f)),
+                      mk3(0.0f, 0.0f, cam.z_dist));
+    // doubles from here on
+    const double e1[3] = {e1f.x, e1f.y, e1f.z}, e2[3] = {e2f.x, e2f.y, e2f.z};
+    const double n[3] = {nf.x, nf.y, nf.z}, ao[3] = {aof.x, aof.y, aof.z};
+    const double blc[3] = {(double)bl.x - cx, (double)bl.y - cy, (double)bl.z - cz};
+    auto n1 = [](const double* v) { return fabs(v[0]) + fabs(v[1]) + fabs(v[2]); };
+    auto crs = [](const double* s, const double* o, double* r) {
+        r[0] = s[1] * o[2] - s[2] * o[1];
+        r[1] = s[2] * o[0] - s[0] * o[2];
+        r[2] = s[0] * o[1] - s[1] * o[0];
+    };
+    double wu[3], wv[3], ww[3], wn[3];
+    crs(e2, ao, wu);
+    crs(ao, e1, wv);
+    for (int k = 0; k < 3; ++k) {
+        ww[k] = -(n[k] + wu[k] + wv[k]);
+        wn[k] = -n[k];
+    }
+    const double nn = n1(n), ne1 = n1(e1), ne2 = n1(e2), nao = n1(ao);
+    const double floor_n = nn * 0x1p-149;
+    const double Eu = 8.0 * u * ne2 * nao + floor_n;
+    const double Ev = 8.0 * u * ne1 * nao + floor_n;
+    const double En = 4.0 * u * nn;
+    const double Ew = (8.0 * u * ne2 * nao) + (8.0 * u * ne1 * nao) + 1.01 * En + 3.2 * u * nn + floor_n;
+    // largest |D| over the frame (corners of x', y' in [0, 1]) and the magnitude scale S
+    double dmax = 0.0;
+    for (int cxr = 0; cxr < 2; ++cxr)
+        for (int cyr = 0; cyr < 2; ++cyr) {
+            double D0 = blc[0] + (double)vw * cxr, D1 = blc[1] + 2.0 * cyr, D2 = blc[2];
+            double l = sqrt(D0 * D0 + D1 * D1 + D2 * D2);
+            dmax = l > dmax ? l : dmax;
+        }
+    const double S = fabs((double)bl.x) + fabs((double)bl.y) + fabs((double)bl.z) + fabs((double)vw) + 2.0 +
+                     fabs((double)cx) + fabs((double)cy) + fabs((double)cz);
+    dmax = dmax * (1.0 + 1e-6) + 8.0 * u * S;
+    const double* W[4] = {wu, wv, ww, wn};
+    const double E[4] = {Eu, Ev, Ew, En};
+    float A[4], B[4], K[4], Tt[4];
+    bool finite = true;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double* w = W[k];
+        double Kd = blc[0] * w[0] + blc[1] * w[1] + blc[2] * w[2];
+        double Ad = (double)vw * w[0];
+        double Bd = 2.0 * w[1];
+        double thr = 2.0 * ((E[k] + 4.0 * u * n1(w)) * dmax + 4.0 * u * S * n1(w) +
+                            6.0 * u * (fabs(Kd) + fabs(Ad) + fabs(Bd)));
+        thr = thr * (1.0 + 0x1p-20) + 0x1p-126;  // round the float threshold up
+        A[k] = (float)Ad;
+        B[k] = (float)Bd;
+        K[k] = (float)Kd;
+        Tt[k] = (float)thr;
+        finite = finite && isfinite(A[k]) && isfinite(B[k]) && isfinite(K[k]) && isfinite(Tt[k]);
+    }
+    bool all_finite = finite && isfinite(atf) && isfinite(nn) && isfinite(nao) && isfinite(ne1) &&
+                      isfinite(ne2) && isfinite(dmax);
+    // t >= 0 fails for every camera ray / det >= 1e-6 is unreachable: reject the whole face
+    bool reject_all = all_finite && (((double)atf < -floor_n * 2.0) || (nn * (1.0 + 8.0 * u) < 1e-6));
+    if (!all_finite) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            A[k] = B[k] = K[k] = 0.0f;
+            Tt[k] = __builtin_inff();
+        }
+    } else if (reject_all) {
+        A[3] = B[3] = K[3] = 0.0f;
+        Tt[3] = -__builtin_inff();
+    }
+    TriCull c;
+    c.A = make_float4(A[0], A[1], A[2], A[3]);
+    c.B = make_float4(B[0], B[1], B[2], B[3]);
+    c.K = make_float4(K[0], K[1], K[2], K[3]);
+    c.T = make_float4(Tt[0], Tt[1], Tt[2], Tt[3]);
+    return c;
+}
+
+// the object owning triangle i (objects are consecutive triangle ranges)
+__device__ __forceinline__ uint32_t object_of(const uint32_t* begin, uint32_t nobj, uint32_t i) {
+    uint32_t lo = 0, hi = nobj;  // last object whose first triangle is <= i
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (begin[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// rectangle accumulator words of one face rectangle: (~x0, x1 + 1, ~y0, y1 + 1), max-reduced
+__device__ __forceinline__ void rect_words(const int32_t (&r)[4], uint32_t (&a)[4]) {
+    a[0] = ~(uint32_t)r[0];
+    a[1] = (uint32_t)r[1] + 1u;
+    a[2] = ~(uint32_t)r[2];
+    a[3] = (uint32_t)r[3] + 1u;
+}
+
+__global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp) {
+    __shared__ double s_poly[32 * kSetupWG];  // face_rect's polygon workspace, 256 B per thread
+    __shared__ int32_t s_rects[kSetupWG][4];
+    __shared__ uint32_t s_last;
+    const CamDev cam = *sp.cam;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t i = blockIdx.x * kSetupWG + tid;
+    uint32_t obj = 0;
+    uint32_t a[4] = {0u, 0u, 0u, 0u};
+    if (i < sp.T) {
+        const TriCull c = cull_record(sp.hot[i], cam);
+        sp.cull[i] = c;
+        obj = object_of(sp.obj_begin, sp.nobj, i);
+        int32_t r[4];
+        const bool any = face_rect(c, sp.W, sp.H, r, s_poly + tid, kSetupWG);
+        if (any) rect_words(r, a);
+        if (sp.range) {  // bins.hip: the face's bin rectangle, if its object is binned
+            const uint32_t k = sp.objkey[obj];
+            int4 g = make_int4(1, 0, 1, 0);
+            unsigned long long ar = 0;
+            if (k != ~0u && any) {
+                // bin row of camera row y: (y + kBinH - phase) / kBinH
+                g = make_int4(r[0] / (int32_t)kBinW, r[1] / (int32_t)kBinW,
+                              (r[2] + (int32_t)kBinH - (int32_t)sp.phase) / (int32_t)kBinH,
+                              (r[3] + (int32_t)kBinH - (int32_t)sp.phase) / (int32_t)kBinH);
+                ar = (unsigned long long)(g.y - g.x + 1) * (unsigned long long)(g.w - g.z + 1);
+            }
+            sp.range[i] = g;
+            sp.area[i] = ar;
+            sp.fkey[i] = k;
+        }
+    }
+    // per-object union: one set of atomics per wave when its faces share one object
+    const uint32_t o0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)obj);
+    if (__all(obj == o0 || i >= sp.T)) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            for (int off = 32; off > 0; off >>= 1) a[k] = max(a[k], (uint32_t)__shfl_xor((int)a[k], off));
+        if (lane == 0 && a[1])
+            for (int k = 0; k < 4; ++k) atomicMax(sp.acc + 4 * o0 + k, a[k]);
+    } else if (a[1]) {
+        for (int k = 0; k < 4; ++k) atomicMax(sp.acc + 4 * obj + k, a[k]);
+    }
+    // the last workgroup finalises
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) s_last = atomicAdd(sp.done, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    for (uint32_t j = tid; j < sp.nobj; j += kSetupWG) {
+        uint32_t w[4];
+        for (int k = 0; k < 4; ++k) w[k] = atomicExch(sp.acc + 4 * j + k, 0u);  // read and reset
+        int32_t r[4];
+        if (w[1] == 0) {  // no face can be hit
+            r[0] = 1;
+            r[1] = 0;
+            r[2] = 1;
+            r[3] = 0;
+        } else {
+            r[0] = (int32_t)~w[0];
+            r[1] = (int32_t)w[1] - 1;
+            r[2] = (int32_t)~w[2];
+            r[3] = (int32_t)w[3] - 1;
+        }
+        if (sp.obj_begin[j + 1] == sp.obj_begin[j]) {  // no faces: no rectangle
+            r[0] = r[2] = 1;
+            r[1] = r[3] = 0;
+        }
+        for (int k = 0; k < 4; ++k) sp.objs[j].g.rect[k] = r[k];
+        if (j < kSetupWG)
+            for (int k = 0; k < 4; ++k) s_rects[j][k] = r[k];
+    }
+    __syncthreads();
+    if (tid != 0) return;
+    *sp.done = 0u;
+    CamState& st = *sp.state;
+    st.cam = cam;
+    if (sp.binned) return;  // bins.hip narrows the rectangles and lists the detail sub-blocks
+    // detail rectangles in sub-block units (16 px x 4 rank-local rows), made disjoint by merging
+    // overlapping ones into their bounding box; more than kMaxRects widen the last one
+    int32_t rects[kMaxRects][4];
+    uint32_t nrect = 0;
+    const int32_t rows_i = (int32_t)sp.rows, w_i = (int32_t)sp.W;
+    for (uint32_t j = 0; j < sp.nobj; ++j) {
+        int32_t r[4];
+        for (int k = 0; k < 4; ++k) r[k] = j < kSetupWG ? s_rects[j][k] : sp.objs[j].g.rect[k];
+        int32_t x0 = r[0], x1 = r[1], y0 = r[2] - (int32_t)sp.row0, y1 = r[3] - (int32_t)sp.row0;
+        x1 = x1 < w_i - 1 ? x1 : w_i - 1;
+        y0 = y0 > 0 ? y0 : 0;
+        y1 = y1 < rows_i - 1 ? y1 : rows_i - 1;
+        if (x0 > x1 || y0 > y1) continue;
+        const int32_t q[4] = {x0 / 16, x1 / 16, y0 / 4, y1 / 4};
+        if (nrect == (uint32_t)kMaxRects) {
+            int32_t* l = rects[kMaxRects - 1];
+            l[0] = min(l[0], q[0]);
+            l[1] = max(l[1], q[1]);
+            l[2] = min(l[2], q[2]);
+            l[3] = max(l[3], q[3]);
+            continue;
+        }
+        for (int k = 0; k < 4; ++k) rects[nrect][k] = q[k];
+        ++nrect;
+    }
+    for (bool merged = true; merged;) {
+        merged = false;
+        for (uint32_t x = 0; x < nrect && !merged; ++x)
+            for (uint32_t y = x + 1; y < nrect && !merged; ++y) {
+                int32_t* ra = rects[x];
+                const int32_t* rb = rects[y];
+                if (ra[0] > rb[1] || rb[0] > ra[1] || ra[2] > rb[3] || rb[2] > ra[3]) continue;
+                ra[0] = min(ra[0], rb[0]);
+                ra[1] = max(ra[1], rb[1]);
+                ra[2] = min(ra[2], rb[2]);
+                ra[3] = max(ra[3], rb[3]);
+                for (uint32_t z = y; z + 1 < nrect; ++z)
+                    for (int k = 0; k < 4; ++k) rects[z][k] = rects[z + 1][k];
+                --nrect;
+                merged = true;
+            }
+    }
+    uint32_t total = 0;
+    for (uint32_t k = 0; k < nrect; ++k) {
+        total += (uint32_t)(rects[k][1] - rects[k][0] + 1) * (uint32_t)(rects[k][3] - rects[k][2] + 1);
+        for (int q = 0; q < 4; ++q) st.rects[k][q] = rects[k][q];
+    }
+    st.nrect = nrect;
+    st.total_sub = total;
+}
+
+__global__ void set_camera_kernel(CamDev cam, CamDev* slot) {
+    if (threadIdx.x == 0) *slot = cam;
+}
+
+}  // namespace
+
+hipError_t launch_camera_setup(const SetupParams& sp, hipStream_t s) {
+    const uint32_t blocks = sp.T ? (sp.T + kSetupWG - 1) / kSetupWG : 1u;
+    camera_setup_kernel<<<blocks, kSetupWG, 0, s>>>(sp);
+    return hipGetLastError();
+}
+
+hipError_t launch_set_camera(const CamDev& cam, CamDev* slot, hipStream_t s) {
+    set_camera_kernel<<<1, 64, 0, s>>>(cam, slot);
+    return hipGetLastError();
+}
+
+}  // namespace gpu
+}  // namespace eray

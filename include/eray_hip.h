@@ -23,6 +23,7 @@
  *                           shaderlib nodes, evaluated at the texel Material::get reads);
  *                           eray_scene_set_object_example_material: lib/material.rs:56-94
  *                           (Material::get) over main.rs:80-144's graph, per hit texel
+ *   eray_render_camera_path lib/scene.rs:39-54 Scene::set_camera + lib/engine.rs:46-81 per frame
  *   eray_render             lib/engine.rs:46-81 (Engine::render: camera rays, first-hit
  *                           Object::intersects object.rs:58-81, Triangle::intersects
  *                           primitives.rs:41-72, cast_ray shading engine.rs:112-216,
@@ -52,7 +53,7 @@
 extern "C" {
 #endif
 
-#define ERAY_ABI_VERSION 2
+#define ERAY_ABI_VERSION 3
 
 typedef enum eray_status {
     ERAY_OK = 0,
@@ -248,6 +249,12 @@ typedef struct eray_render_params {
 
 #define ERAY_RENDER_DEFAULT 0u
 #define ERAY_RENDER_BRUTE_FORCE 1u  /* disable the exact per-wave triangle culling (A/B) */
+/* Launch-shape overrides (tests / tuning; every choice renders the same image).  By default the
+ * library picks them from the frame's detail sub-block count. */
+#define ERAY_RENDER_DENSE_DETAIL 2u      /* large meshes: the 3-workgroups-per-CU detail build      */
+#define ERAY_RENDER_NO_DENSE_DETAIL 4u   /* large meshes: the 2-workgroups-per-CU detail build      */
+#define ERAY_RENDER_SEPARATE_FILL 8u     /* dense build: background fill in a second, parallel kernel */
+#define ERAY_RENDER_NO_SEPARATE_FILL 16u /* dense build: background fill inside the frame kernel     */
 
 int eray_render(eray_ctx* ctx, const eray_render_params* params);
 /* Renders `frames` frames back to back with the same parameters (a serving / animation loop
@@ -261,6 +268,16 @@ int eray_render_frames(eray_ctx* ctx, const eray_render_params* params, uint32_t
 /* Builds (and caches) the launch plan eray_render_frames uses for these parameters and frame
  * count, without rendering: the one-time capture cost stays out of a timed or serving loop. */
 int eray_render_prepare(eray_ctx* ctx, const eray_render_params* params, uint32_t frames);
+/* Renders one frame per camera of `cameras` (host array of n), in order, into the same outputs —
+ * Scene::set_camera + Engine::render per frame (scene.rs:39-54, engine.rs:46-81), e.g. an
+ * animation or a serving loop whose camera moves every frame.  Every camera must have the scene
+ * camera's Camera::size.  Each frame's camera setup (culling records, pixel rectangles, screen
+ * bins, detail list) runs on the device right before its frame, with no host round trip, and the
+ * frames are replayed from cached HIP graphs (the cameras are re-read every call).  When
+ * mean_frame_ms is not NULL the call waits and returns the mean device time per frame, setup
+ * included.  The scene camera (eray_scene_set_camera) is unchanged. */
+int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* params, const eray_camera* cameras,
+                            uint32_t n, float* mean_frame_ms);
 
 /* ------------------------------------------------------------------ PPM ----------------- */
 /* Body bytes of Image<Color>::save_as_ppm for a width x height device image: rows bottom-up,

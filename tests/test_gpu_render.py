@@ -316,23 +316,20 @@ def standin70k():
             np.ascontiguousarray(t[ft].reshape(-1, 6)))
 
 
-@pytest.mark.parametrize("dense,chunk,separate", [("auto", None, None), ("0", None, None), ("1", None, "0"),
-                                                  ("1", None, "1"), ("auto", "9973", None)])
+DENSE = {"auto": 0, "0": capi.RENDER_NO_DENSE_DETAIL, "1": capi.RENDER_DENSE_DETAIL}
+SEPARATE = {None: 0, "0": capi.RENDER_NO_SEPARATE_FILL, "1": capi.RENDER_SEPARATE_FILL}
+
+
+@pytest.mark.parametrize("dense,separate", [("auto", None), ("0", None), ("1", "0"), ("1", "1")])
 @pytest.mark.parametrize("material", ["textures", "example"])
-def test_c3_binned_equals_brute_force(gpu, standin70k, material, dense, chunk, separate, monkeypatch):
+def test_c3_binned_equals_brute_force(gpu, standin70k, material, dense, separate):
     """Screen bins (bins.hip) for a 70k-face object: bit-identical to the brute-force scan, with
-    the large-mesh frame kernel at 2 and at 3 workgroups per CU (ERAY_DENSE_DETAIL), the dense
-    build with and without the separate fill kernel (ERAY_SEPARATE_FILL), and with the (face,
-    bin) pairs compacted in many passes (ERAY_BIN_PAIR_CHUNK)."""
-    if dense != "auto":
-        monkeypatch.setenv("ERAY_DENSE_DETAIL", dense)
-    if separate is not None:
-        monkeypatch.setenv("ERAY_SEPARATE_FILL", separate)
-    if chunk:
-        monkeypatch.setenv("ERAY_BIN_PAIR_CHUNK", chunk)
+    the large-mesh frame kernel at 2 and at 3 workgroups per CU (ERAY_RENDER_(NO_)DENSE_DETAIL)
+    and the dense build with and without the separate fill kernel (ERAY_RENDER_(NO_)SEPARATE_FILL)."""
+    flags = DENSE[dense] | SEPARATE[separate]
     W, H = 480, 270
     sc = MainScene(gpu, *standin70k, W, H, texture=256, fov=(16.0, 9.0), material=material)
-    a = gpu_render(gpu, W, H)
+    a = gpu_render(gpu, W, H, flags=flags)
     b = gpu_render(gpu, W, H, flags=capi.RENDER_BRUTE_FORCE)
     sc.close()
     assert (a[1] >= 0).sum() > 1000
@@ -342,12 +339,12 @@ def test_c3_binned_equals_brute_force(gpu, standin70k, material, dense, chunk, s
 
 
 @pytest.mark.parametrize("separate", ["0", "1"])
-def test_dense_frames_graph_replay(gpu, standin70k, separate, monkeypatch):
+def test_dense_frames_graph_replay(gpu, standin70k, separate):
     """The dense large-mesh build replayed from a HIP graph, with the fill in the same launch and
     as a second kernel on a forked stream (two parallel graph nodes joined by an event): every
-    replayed frame equals eray_render's brute-force frame."""
-    monkeypatch.setenv("ERAY_DENSE_DETAIL", "1")
-    monkeypatch.setenv("ERAY_SEPARATE_FILL", separate)
+    replayed frame equals eray_render's brute-force frame.  The flags are part of the launch-plan
+    key, so each setting captures its own graph."""
+    flags = capi.RENDER_DENSE_DETAIL | SEPARATE[separate]
     W, H = 480, 270
     sc = MainScene(gpu, *standin70k, W, H, texture=256, fov=(16.0, 9.0))
     ref = gpu_render(gpu, W, H, flags=capi.RENDER_BRUTE_FORCE)
@@ -359,7 +356,7 @@ def test_dense_frames_graph_replay(gpu, standin70k, separate, monkeypatch):
             gpu.memset(rgb.ptr, 0, rgb.nbytes)
             gpu.memset(ppm.ptr, 0, ppm.nbytes)
             gpu.memset(face.ptr, 0x7F, face.nbytes)
-            gpu.render_frames(frames, W, H, out_rgb=rgb.ptr, out_ppm=ppm.ptr, out_face=face.ptr)
+            gpu.render_frames(frames, W, H, out_rgb=rgb.ptr, out_ppm=ppm.ptr, out_face=face.ptr, flags=flags)
             gpu.synchronize()
             assert_bit_equal(rgb.numpy(), ref[0], f"dense render_frames({frames}) separate={separate}")
             assert np.array_equal(face.numpy(), ref[1])
@@ -371,23 +368,22 @@ def test_dense_frames_graph_replay(gpu, standin70k, separate, monkeypatch):
 
 
 @pytest.mark.parametrize("dense,separate", [("0", "0"), ("1", "0"), ("1", "1")])
-def test_c3_full_size_rows_match_oracle(gpu, oracle, standin70k, dense, separate, monkeypatch):
+def test_c3_full_size_rows_match_oracle(gpu, oracle, standin70k, dense, separate):
     """C3 at 1920x1080 (bins built for the full camera) against the oracle on a row sample
     through the object, including row blocks rendered with a row phase (row0 % 4 != 0); the
     large-mesh kernel at 2 and at 3 workgroups per CU, the latter also beside the separate fill
     kernel."""
-    monkeypatch.setenv("ERAY_DENSE_DETAIL", dense)
-    monkeypatch.setenv("ERAY_SEPARATE_FILL", separate)
+    flags = DENSE[dense] | SEPARATE[separate]
     W, H = 1920, 1080
     sc = MainScene(gpu, *standin70k, W, H, texture=256, fov=(16.0, 9.0))
-    rgb, face, _ = gpu_render(gpu, W, H)
+    rgb, face, _ = gpu_render(gpu, W, H, flags=flags)
     osc = oracle.main_rs_scene(*standin70k, texture=256)
     ocam = oracle.camera((0.0, 0.0, 5.0), (16.0, 9.0), W, 1.0)
     for row0, rows in ((538, 3), (601, 2)):
         ref, ref_face, _ = oracle.render(osc, ocam, row0=row0, rows=rows, want_faces=True)
         assert np.array_equal(face[row0:row0 + rows], ref_face)
         assert_bit_equal(rgb[row0:row0 + rows], ref, f"c3 rows {row0}+{rows}")
-        part, part_face, _ = gpu_render(gpu, W, H, row0=row0, rows=rows)
+        part, part_face, _ = gpu_render(gpu, W, H, row0=row0, rows=rows, flags=flags)
         assert np.array_equal(part_face, ref_face)
         assert_bit_equal(part, ref, f"c3 row block {row0}+{rows}")
     sc.close()
