@@ -19,6 +19,15 @@ gather"); --gather-every-frame gathers after every frame instead.  Inputs (mesh,
 textures) are resident in HBM before timing; the material graph is evaluated once, as
 Material::update is (reported separately).
 
+The headline `value` replays frames of ONE camera (static camera: the per-camera setup — culling
+records, pixel rectangles, screen bins — runs once before the timed region, as it would for a
+serving loop that renders the same view).  `moving_camera` reports the same frames with a camera
+that moves every frame (a dolly along the view axis: Scene::set_camera + Engine::render per
+frame), every frame's setup on the device inside the timed frames (eray_render_camera_path).
+
+--scaling weak widens the frame with N (C2's pixel pitch, not a BASELINE.json config); --scaling
+strong splits BASELINE's fixed frames (C4: --width 3840 --height 2160, C5: 7680x4320).
+
 Prints ONE JSON line on rank 0 (metric "Mrays/s": primary rays of all ranks / wall time).
 """
 from __future__ import annotations
@@ -38,7 +47,7 @@ import torch  # noqa: E402  (imported before the HIP library: one HIP runtime pe
 import torch.distributed as dist  # noqa: E402
 
 from eray_amd import capi  # noqa: E402
-from eray_amd.dist import gather_ppm_rows, row_block  # noqa: E402
+from eray_amd.dist import RowGather, gather_ppm_rows, row_block  # noqa: E402
 from eray_amd.frame import MainScene  # noqa: E402
 from eray_amd.objfile import load_obj_file  # noqa: E402
 
@@ -89,6 +98,30 @@ def pmc_traffic(workload: dict):
     return None
 
 
+def host_cpu() -> tuple[int, str]:
+    """(logical CPUs of this host, CPU model name) for the cpu_baseline record."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return os.cpu_count() or 0, model
+
+
+def dolly_path(n: int, fov, width: int):
+    """n cameras moving along the view axis (main.rs's camera at (0, 0, 5) +- 0.5, z_dist 1 +- 0.1):
+    every frame a new camera with the same Camera::size.  A loaded mesh's bounding box is the
+    degenerate (0,0,0) box (object.rs:306-315), which only rays from x = y = 0 pass, so the
+    reference's own semantics keep the camera on the axis."""
+    import math
+    return [capi.make_camera((0.0, 0.0, 5.0 + 0.5 * math.sin(2.0 * math.pi * k / max(n, 1))), fov, width,
+                             1.0 + 0.1 * math.cos(2.0 * math.pi * k / max(n, 1))) for k in range(n)]
+
+
 def cpu_baseline(mesh, width: int, height: int, fov, seconds: float = 10.0) -> dict:
     """The single-threaded C++ restatement (oracle/, 'port') on this host, on the bench's own
     frame (width x height, same scene): whole frames (render + PPM byte pack) repeated for
@@ -124,7 +157,9 @@ def cpu_baseline(mesh, width: int, height: int, fov, seconds: float = 10.0) -> d
         rays = done * width
         sample = (f"{done} of the {height} rows of the {width}x{height} frame (every 64th row first), "
                   f"render only, in {el:.1f} s")
+    nproc, model = host_cpu()
     return {"value": rays / el / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
+            "nproc": nproc, "cpu_model": model,
             "sample": sample + ", single thread, oracle/eray_oracle.cpp (g++ -O2 -ffp-contract=off)"}
 
 
@@ -197,6 +232,16 @@ def main() -> None:
     face = torch.empty((rows, width), dtype=torch.int32, device="cuda")
     frame = torch.empty((H_total, width, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
     flags = capi.RENDER_BRUTE_FORCE if args.brute_force else capi.RENDER_DEFAULT
+    # N > 1: the frame gather of the C-ABI (eray_gather_rows, RCCL ncclGather over xGMI); the
+    # one-GPU rehearsal gathers through gloo instead
+    if world > 1 and not rehearsal:
+        rccl = RowGather(ctx, world, rank)
+
+        def gather():
+            rccl(ppm, frame)
+    elif world > 1:
+        def gather():
+            gather_ppm_rows(ppm, frame, world, rank)
 
     def render_args():
         return dict(row0=row0, rows=rows, out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr(), flags=flags)
@@ -217,7 +262,7 @@ def main() -> None:
     if args.warmup:
         scene.ctx.render_frames(args.warmup, width, H_total, **render_args())
     if world > 1:
-        gather_ppm_rows(ppm, frame, world, rank)
+        gather()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -228,11 +273,11 @@ def main() -> None:
     if args.gather_every_frame and world > 1:
         for _ in range(args.steps):
             scene.render(**render_args())
-            gather_ppm_rows(ppm, frame, world, rank)
+            gather()
     else:
         scene.ctx.render_frames(args.steps, width, H_total, **render_args())
         if world > 1:  # the final RCCL gather of the PPM rows to rank 0 (file order)
-            gather_ppm_rows(ppm, frame, world, rank)
+            gather()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -246,13 +291,32 @@ def main() -> None:
     # the library's stream (back-to-back kernels: device time per frame)
     kernel_ms = scene.ctx.render_frames(args.steps, width, H_total, timed=True, **render_args())
     gather_ms = None
-    if world > 1:  # one frame's gather, for the record
+    rank_kernel_ms = [kernel_ms]
+    if world > 1:  # one frame's gather, and every rank's frame-kernel time, for the record
         torch.cuda.synchronize()
         dist.barrier()
         g0 = time.perf_counter()
-        gather_ppm_rows(ppm, frame, world, rank)
+        gather()
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - g0) * 1e3
+        got = [None] * world
+        dist.all_gather_object(got, kernel_ms)
+        rank_kernel_ms = got
+
+    # moving camera: the same frames with a new camera every frame (the setup on the device,
+    # inside each frame); one untimed pass captures the path's graphs
+    path = dolly_path(args.steps, frame_camera_fov(width, H_total), width)
+    scene.ctx.render_camera_path(path, width, H_total, **render_args())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    m0 = time.perf_counter()
+    scene.ctx.render_camera_path(path, width, H_total, **render_args())
+    torch.cuda.synchronize()
+    moving_s = time.perf_counter() - m0
+    if world > 1:
+        moving_s = float(allreduce(moving_s, torch.float64, dist.ReduceOp.MAX))
+    moving_kernel_ms = scene.ctx.render_camera_path(path, width, H_total, timed=True, **render_args())
 
     if rank == 0:
         # the workload a committed counter summary (profiles/pmc_traffic*.json) must match
@@ -293,6 +357,9 @@ def main() -> None:
                 "rows_per_gpu": rows,
                 "texture": TEXTURE,
                 "parallelism": f"row tiles x{world}" if world > 1 else "single GPU",
+                "camera": "static (value); see moving_camera",
+                **({"note": "weak scaling widens the frame to (1920 N) x 1080: not a BASELINE.json config"}
+                   if world > 1 and args.scaling == "weak" else {}),
                 "culling": not args.brute_force,
             },
             "frame_ms": round(ms_per_step, 6),
@@ -300,6 +367,17 @@ def main() -> None:
             "material_graph_s": round(t_mat, 4),
             "scene_setup_ms": round(t_setup * 1e3, 3),
             "gather_ms": None if gather_ms is None else round(gather_ms, 4),
+            "rank_kernel_ms": [round(v, 6) for v in rank_kernel_ms],
+            "moving_camera": {
+                "frame_ms": round(moving_s / args.steps * 1e3, 6),
+                "value": round(width * H_total * args.steps / moving_s / 1e6, 3),
+                "unit": "Mrays/s",
+                "device_ms_per_frame": round(moving_kernel_ms, 6),
+                "frames": args.steps,
+                "camera": "dolly along the view axis, z 5 +- 0.5, z_dist 1 +- 0.1, a new camera every frame",
+                "includes": "per-frame camera setup on the device (culling records, pixel rectangles, merged "
+                            "detail rectangles; screen bins and detail list for meshes over 256 faces) + frame",
+            },
             "gather": ("every frame" if args.gather_every_frame else "final frame") if world > 1 else None,
             **({"rehearsal": "all ranks on GPU 0, gloo collectives: not a measurement"} if rehearsal else {}),
             "hit_pixels": hits_all,
@@ -319,6 +397,8 @@ def main() -> None:
             result["cpu_baseline"] = cpu_baseline(mesh, width, H_total, frame_camera_fov(width, H_total), args.cpu_seconds)
         print(json.dumps(result), flush=True)
 
+    if world > 1 and not rehearsal:
+        rccl.close()
     scene.close()
     ctx.close()
     if world > 1:

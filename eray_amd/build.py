@@ -24,7 +24,7 @@ OBJ = os.path.join(PKG, "_obj")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "liberay_hip.so")
 
-SOURCES = ["render.hip", "setup.hip", "trace.hip", "bins.hip", "shaderlib.hip", "capi.cpp"]
+SOURCES = ["render.hip", "setup.hip", "trace.hip", "bins.hip", "shaderlib.hip", "capi.cpp", "comm.cpp"]
 ARCH = "gfx950"
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
             f"--offload-arch={ARCH}", "-I" + os.path.join(ROOT, "include"),
@@ -83,7 +83,10 @@ def build(jobs: int = 4, verbose: bool = False, force: bool = False) -> str:
             if warn.strip() and verbose:
                 print(warn, file=sys.stderr)
     if force or cmds or not _newer(lib_path, objs):
-        run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib_path, *objs])
+        # RCCL for the multi-GPU gather (comm.cpp); under PyTorch the loader reuses torch's copy
+        # (same SONAME librccl.so.1), so one RCCL serves the process
+        run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib_path, *objs, "-L/opt/rocm/lib", "-lrccl",
+             "-Wl,-rpath,/opt/rocm/lib"])
     return lib_path
 
 

@@ -141,6 +141,10 @@ SIGNATURES = {
     "eray_render_camera_path": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(Camera), _U,
                                           C.POINTER(C.c_float)]),
     "eray_pack_ppm": (C.c_int, [_P, _P, _U, _U, _P]),
+    "eray_comm_unique_id": (C.c_int, [_P]),
+    "eray_comm_init": (C.c_int, [_P, C.c_int, C.c_int, _P, C.POINTER(_P)]),
+    "eray_comm_destroy": (C.c_int, [_P]),
+    "eray_gather_rows": (C.c_int, [_P, _P, _P, _P, _U, _U]),
     "eray_ppm_header": (C.c_int, [_U, _U, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
 }
 
@@ -217,6 +221,20 @@ def make_camera(center=(0.0, 0.0, 5.0), fov=(60.0, 60.0), width=1024, z_dist=1.0
 def make_light(position, variant, color=(1.0, 1.0, 1.0), brightness=1.0) -> Light:
     v = LIGHT_AMBIENT if variant in (LIGHT_AMBIENT, "ambient") else LIGHT_POINT
     return Light((C.c_float * 3)(*position), v, (C.c_float * 3)(*color), brightness)
+
+
+COMM_ID_BYTES = 128
+
+
+def comm_unique_id() -> bytes:
+    """The id of a new RCCL communicator (eray_comm_unique_id), made on rank 0 and sent to the others."""
+    buf = (C.c_uint8 * COMM_ID_BYTES)()
+    check(lib().eray_comm_unique_id(buf))
+    return bytes(buf)
+
+
+def comm_destroy(comm: int) -> None:
+    check(lib().eray_comm_destroy(comm))
 
 
 def ppm_header(width: int, height: int) -> bytes:
@@ -412,6 +430,20 @@ class Context:
         self._check(lib().eray_render_camera_path(self._h, C.byref(p), cams, len(cameras),
                                                   C.byref(ms) if timed else None))
         return ms.value if timed else None
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes) -> int:
+        """An RCCL communicator for this context's GPU (eray_comm_init): every rank passes the id
+        rank 0 got from comm_unique_id().  Returns the ncclComm_t handle."""
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError("unique id must be 128 bytes")
+        buf = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
+        comm = _P()
+        self._check(lib().eray_comm_init(self._h, nranks, rank, buf, C.byref(comm)))
+        return comm.value
+
+    def gather_rows(self, comm: int, local_ptr, frame_ptr, rows: int, width: int) -> None:
+        """eray_gather_rows: every rank's rows x width PPM byte block into rank 0's frame (rank order)."""
+        self._check(lib().eray_gather_rows(self._h, comm, local_ptr, frame_ptr or None, rows, width))
 
     def pack_ppm(self, rgb_ptr, w, h, out_ptr) -> None:
         self._check(lib().eray_pack_ppm(self._h, rgb_ptr, w, h, out_ptr))

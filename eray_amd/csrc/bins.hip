@@ -55,11 +55,14 @@ __global__ void __launch_bounds__(kBinWG) bin_pairs_kernel(const TriCull* __rest
                                                            uint32_t* __restrict__ eface,
                                                            unsigned long long* __restrict__ emask) {
     const unsigned long long P = total_pairs(first, area, T);
-    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __shared__ uint32_t s_cnt[kBinWG / 64];
+    __shared__ uint32_t s_base;
     const unsigned long long stride = (unsigned long long)gridDim.x * kBinWG;
-    for (unsigned long long base = (unsigned long long)blockIdx.x * kBinWG + (threadIdx.x & ~63u); base < P;
-         base += stride) {  // wave-uniform
-        const unsigned long long j = base + lane;
+    // workgroup-uniform loop: one slot-counter atomic per workgroup and pass (a per-wave atomic on
+    // the one counter serialised thousands of times)
+    for (unsigned long long base = (unsigned long long)blockIdx.x * kBinWG; base < P; base += stride) {
+        const unsigned long long j = base + threadIdx.x;
         unsigned long long m = 0;
         uint32_t key = 0, i = 0;
         if (j < P) {
@@ -78,12 +81,18 @@ __global__ void __launch_bounds__(kBinWG) bin_pairs_kernel(const TriCull* __rest
             key = fkey[i] * nbins + ty * bins_x + tx;
         }
         const unsigned long long bal = __ballot(m != 0);
-        if (!bal) continue;
-        uint32_t slot0 = 0;
-        if (lane == (uint32_t)(__ffsll(bal) - 1)) slot0 = atomicAdd(n, (uint32_t)__popcll(bal));
-        slot0 = (uint32_t)__shfl((int)slot0, __ffsll(bal) - 1);
+        if (lane == 0) s_cnt[wave] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kBinWG / 64; ++w) {
+            before += w < wave ? s_cnt[w] : 0u;
+            total += s_cnt[w];
+        }
+        if (threadIdx.x == 0) s_base = total ? atomicAdd(n, total) : 0u;
+        __syncthreads();
         if (m) {
-            const uint32_t slot = slot0 + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+            const uint32_t slot = s_base + before + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
             if (slot < cap) {
                 ekey[slot] = key;
                 eface[slot] = i;
@@ -91,6 +100,7 @@ __global__ void __launch_bounds__(kBinWG) bin_pairs_kernel(const TriCull* __rest
                 atomicAdd(count + key, 1u);
             }
         }
+        __syncthreads();  // s_cnt / s_base are rewritten by the next pass
     }
 }
 
@@ -115,42 +125,59 @@ __global__ void __launch_bounds__(kBinWG) bin_scatter_kernel(const uint32_t* __r
     }
 }
 
-// The binned objects' non-empty bins -> their pixel rectangles (accumulated as the setup's:
-// (~x0, x1 + 1, ~y0, y1 + 1) by atomicMax); the last workgroup narrows each binned object's
-// rectangle to them, publishes its bin views (none on overflow) and resets the counters.
+// The binned objects' non-empty bins -> their pixel rectangles ((~x0, x1 + 1, ~y0, y1 + 1),
+// max-reduced); the last workgroup narrows each binned object's rectangle to them, publishes its
+// bin views (none on overflow) and resets the counters.  Keys are object-major, so a workgroup's
+// 256 keys belong to a run of binned objects [k_first, k_last]: reduced in LDS, the run's two
+// ends published as partials, inner objects' unions stored whole (no contended atomics).
+constexpr uint32_t kFinSpan = 8;    // binned objects per workgroup reduced in LDS (more: atomics)
+constexpr uint32_t kFinTab = 1024;  // binned objects the last workgroup combines in LDS
+
+__device__ __forceinline__ void max4(uint32_t* dst, const uint32_t (&a)[4]) {
+    for (int q = 0; q < 4; ++q) atomicMax(dst + q, a[q]);
+}
+
 __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(const uint32_t* __restrict__ start, uint32_t nb,
                                                                uint32_t bins_x, uint32_t nbins, uint32_t W, uint32_t H,
                                                                uint32_t phase, uint32_t* __restrict__ acc,
+                                                               uint32_t* __restrict__ part,
                                                                uint32_t* __restrict__ done, uint32_t* __restrict__ n,
                                                                uint32_t cap, const uint32_t* __restrict__ kobj,
                                                                ObjectDesc* __restrict__ objs, uint32_t* tri,
                                                                unsigned long long* mask, TriHot* hot,
                                                                CamState* __restrict__ st) {
+    __shared__ uint32_t s_acc[kFinSpan][4];
+    __shared__ uint32_t s_tab[kFinTab][4];
     __shared__ uint32_t s_last;
-    const uint32_t b = blockIdx.x * kBinWG + threadIdx.x;
     const uint32_t keys = nb * nbins;
-    uint32_t a[4] = {0u, 0u, 0u, 0u}, k = 0;
+    const uint32_t b0 = blockIdx.x * kBinWG, b1 = min(b0 + kBinWG, keys);
+    const uint32_t k_first = b0 < b1 ? b0 / nbins : 0u, k_last = b0 < b1 ? (b1 - 1) / nbins : 0u;
+    if (threadIdx.x < kFinSpan * 4) s_acc[threadIdx.x / 4][threadIdx.x % 4] = 0u;
+    __syncthreads();
+    const uint32_t b = b0 + threadIdx.x;
     if (b < keys && start[b + 1] > start[b]) {
-        k = b / nbins;
+        const uint32_t k = b / nbins;
         const uint32_t lb = b - k * nbins;
         const uint32_t bx = lb % bins_x, by = lb / bins_x;
         const int32_t y0 = (int32_t)(by * kBinH + phase) - (int32_t)kBinH;
         const uint32_t x0 = bx * kBinW, x1 = min(x0 + kBinW, W) - 1;
         const uint32_t r0 = (uint32_t)max(y0, 0), r1 = (uint32_t)min(y0 + (int32_t)kBinH, (int32_t)H) - 1;
-        a[0] = ~x0;
-        a[1] = x1 + 1u;
-        a[2] = ~r0;
-        a[3] = r1 + 1u;
+        const uint32_t a[4] = {~x0, x1 + 1u, ~r0, r1 + 1u};
+        if (k - k_first < kFinSpan) max4(s_acc[k - k_first], a);
+        else max4(acc + 4 * k, a);
     }
-    const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k);
-    if (__all(k == k0 || a[1] == 0)) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            for (int off = 32; off > 0; off >>= 1) a[q] = max(a[q], (uint32_t)__shfl_xor((int)a[q], off));
-        if ((threadIdx.x & 63) == 0 && a[1])
-            for (int q = 0; q < 4; ++q) atomicMax(acc + 4 * k0 + q, a[q]);
-    } else if (a[1]) {
-        for (int q = 0; q < 4; ++q) atomicMax(acc + 4 * k + q, a[q]);
+    __syncthreads();
+    const uint32_t span = b0 < b1 ? min(k_last - k_first + 1, kFinSpan) : 0u;
+    if (threadIdx.x < span && threadIdx.x > 0 && k_first + threadIdx.x < k_last)  // inner objects: whole
+        for (int q = 0; q < 4; ++q) acc[4 * (k_first + threadIdx.x) + q] = s_acc[threadIdx.x][q];
+    if (threadIdx.x == 0) {
+        uint32_t* pb = part + 10 * blockIdx.x;
+        pb[0] = b0 < b1 ? k_first : ~0u;
+        pb[5] = b0 < b1 ? k_last : ~0u;
+        for (int q = 0; q < 4; ++q) {
+            pb[1 + q] = s_acc[0][q];
+            pb[6 + q] = b0 < b1 && k_last - k_first < kFinSpan ? s_acc[k_last - k_first][q] : 0u;
+        }
     }
     __threadfence();
     __syncthreads();
@@ -158,11 +185,30 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(const uint32_t* _
     __syncthreads();
     if (!s_last) return;
     __threadfence();
+    const bool in_lds = nb <= kFinTab;
+    if (in_lds) {
+        for (uint32_t j = threadIdx.x; j < nb; j += kBinWG)
+            for (int q = 0; q < 4; ++q) {
+                s_tab[j][q] = acc[4 * j + q];
+                acc[4 * j + q] = 0u;
+            }
+        __syncthreads();
+    }
+    for (uint32_t g = threadIdx.x; g < gridDim.x; g += kBinWG) {
+        const uint32_t* pb = part + 10 * g;
+        for (int e = 0; e < 2; ++e) {
+            if (pb[5 * e] == ~0u) continue;
+            const uint32_t a[4] = {pb[5 * e + 1], pb[5 * e + 2], pb[5 * e + 3], pb[5 * e + 4]};
+            max4(in_lds ? s_tab[pb[5 * e]] : acc + 4 * pb[5 * e], a);
+        }
+    }
+    __threadfence();
+    __syncthreads();
     const uint32_t found = *n;
     const bool overflow = found > cap;
     for (uint32_t j = threadIdx.x; j < nb; j += kBinWG) {
         uint32_t w[4];
-        for (int q = 0; q < 4; ++q) w[q] = atomicExch(acc + 4 * j + q, 0u);
+        for (int q = 0; q < 4; ++q) w[q] = in_lds ? s_tab[j][q] : atomicExch(acc + 4 * j + q, 0u);
         ObjGeom& g = objs[kobj[j]].g;
         if (overflow) {  // keep the face rectangles; the frame kernel scans through LDS tiles
             g.bin_start = nullptr;
@@ -248,7 +294,7 @@ hipError_t grow(T** p, size_t need) {
 }  // namespace
 
 void bins_free(BinBuffers& b) {
-    void* ptrs[] = {b.first, b.count,  b.start,  b.kbegin, b.kobj,   b.n,       b.done,    b.acc,   b.ekey,
+    void* ptrs[] = {b.first, b.count,  b.start,  b.kbegin, b.kobj,   b.n,       b.done,    b.acc,   b.part, b.ekey,
                     b.eface, b.emask,  b.tri,    b.mask,   b.hot,    b.dflags,  b.dpacked, b.dlist, b.docc,
                     b.temp};
     for (void* p : ptrs)
@@ -275,6 +321,7 @@ hipError_t bins_alloc(BinBuffers& b, uint32_t T, uint32_t nb, const uint32_t* kb
         (e = grow(&b.start, keys + 1)) != hipSuccess || (e = grow(&b.kbegin, nb)) != hipSuccess ||
         (e = grow(&b.kobj, nb)) != hipSuccess || (e = grow(&b.n, 1)) != hipSuccess ||
         (e = grow(&b.done, 1)) != hipSuccess || (e = grow(&b.acc, 4 * (size_t)nb)) != hipSuccess ||
+        (e = grow(&b.part, 10 * std::max<size_t>((keys + kBinWG - 1) / kBinWG, 1))) != hipSuccess ||
         (e = grow(&b.ekey, cap)) != hipSuccess || (e = grow(&b.eface, cap)) != hipSuccess ||
         (e = grow(&b.emask, cap)) != hipSuccess || (e = grow(&b.tri, cap)) != hipSuccess ||
         (e = grow(&b.mask, cap)) != hipSuccess || (e = grow(&b.hot, cap)) != hipSuccess ||
@@ -320,7 +367,7 @@ hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tile
                                                     b.kbegin, b.nbins, sp.hot, b.tri, b.mask, b.hot);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t fgrid = (uint32_t)std::max<size_t>((keys + kBinWG - 1) / kBinWG, 1);
-    bins_finalize_kernel<<<fgrid, kBinWG, 0, s>>>(b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase, b.acc, b.done,
+    bins_finalize_kernel<<<fgrid, kBinWG, 0, s>>>(b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase, b.acc, b.part, b.done,
                                                   b.n, (uint32_t)b.cap, b.kobj, sp.objs, b.tri, b.mask, b.hot,
                                                   sp.state);
     if ((e = hipGetLastError()) != hipSuccess) return e;

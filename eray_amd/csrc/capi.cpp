@@ -123,7 +123,7 @@ struct eray_ctx {
     bool state_pending = false;   // a copy into h_state is in flight
     bool state_known = false;     // h_state holds the results of the setup of setup_key
     std::vector<uint64_t> setup_key;  // camera, size, rows and scene generation of the last setup
-    uint32_t* d_acc = nullptr;    // setup rectangle accumulators (4 x nobj) + done counter
+    uint32_t* d_acc = nullptr;    // setup counter, partials and rectangle accumulators (enqueue_setup)
     size_t acc_cap = 0;
     uint32_t* d_begin = nullptr;  // obj_begin | objkey
     size_t begin_cap = 0;
@@ -222,6 +222,7 @@ int sync_scene(eray_ctx* ctx) {
             ctx->d_cull = nullptr;
         }
         HIP_TRY(ctx, hipMalloc((void**)&ctx->d_cull, shade_cap * sizeof(TriCull)));
+
         ctx->h_raw.assign((size_t)T * 24, 0.0f);
         size_t off = 0;
         for (auto& o : ctx->objects) {
@@ -350,8 +351,9 @@ int sync_scene(eray_ctx* ctx) {
         HIP_TRY(ctx, hipMemcpyAsync(ctx->d_begin, ctx->h_begin.data(), 4 * ctx->h_begin.size(), hipMemcpyHostToDevice,
                                     ctx->stream));
         // rectangle accumulators + the setup's workgroup counter, zero between setups
-        if (ctx->acc_cap < 4 * (size_t)nobj + 1 || !ctx->d_acc) {
-            if ((st = ensure(ctx, &ctx->d_acc, &ctx->acc_cap, 4 * (size_t)nobj + 1))) return st;
+        const size_t acc_words = 4 * (size_t)nobj + 1 + 10 * (size_t)kSetupMaxBlocks;
+        if (ctx->acc_cap < acc_words || !ctx->d_acc) {
+            if ((st = ensure(ctx, &ctx->d_acc, &ctx->acc_cap, acc_words))) return st;
             HIP_TRY(ctx, hipMemsetAsync(ctx->d_acc, 0, 4 * ctx->acc_cap, ctx->stream));
         }
         ctx->desc_dirty = false;
@@ -400,6 +402,7 @@ int ensure_bins(eray_ctx* ctx, uint32_t W, uint32_t H, uint32_t row0, uint32_t r
 // Enqueues the per-camera setup of `d_camera` (device) for camera rows [row0, row0 + rows): no
 // host round trip (setup.hip, bins.hip).
 int enqueue_setup(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint32_t H, uint32_t row0, uint32_t rows) {
+    hipStream_t stream = ctx->stream;
     SetupParams sp{};
     sp.hot = ctx->d_hot;
     sp.cull = ctx->d_cull;
@@ -414,8 +417,11 @@ int enqueue_setup(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint32_t H,
     sp.H = H;
     sp.row0 = row0;
     sp.rows = rows;
-    sp.acc = ctx->d_acc;
-    sp.done = ctx->d_acc + 4 * (size_t)sp.nobj;
+    // [done counter | kSetupMaxBlocks x 10 partials | 4 x nobj accumulators]: the counter and the
+    // accumulators are zero between setups whatever the object count (partials are rewritten)
+    sp.done = ctx->d_acc;
+    sp.part = ctx->d_acc + 1;
+    sp.acc = ctx->d_acc + 1 + 10 * (size_t)kSetupMaxBlocks;
     const bool binned = binned_objects(ctx) > 0;
     sp.binned = binned ? 1u : 0u;
     if (binned) {
@@ -425,8 +431,8 @@ int enqueue_setup(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint32_t H,
         sp.bins_x = ctx->bins.bins_x;
         sp.phase = ctx->bins.phase;
     }
-    HIP_TRY(ctx, launch_camera_setup(sp, ctx->stream));
-    if (binned) HIP_TRY(ctx, launch_bins_build(sp, ctx->bins, (W + 63) / 64, ctx->stream));
+    HIP_TRY(ctx, launch_camera_setup(sp, stream));
+    if (binned) HIP_TRY(ctx, launch_bins_build(sp, ctx->bins, (W + 63) / 64, stream));
     return ERAY_OK;
 }
 
@@ -525,6 +531,7 @@ int eray_ctx_create(int device, eray_ctx** out) {
     if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_cam, sizeof(CamDev));
     if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_state, sizeof(CamState));
     if (e == hipSuccess) e = hipMemset(ctx->d_state, 0, sizeof(CamState));
+
     if (e == hipSuccess) e = hipHostMalloc((void**)&ctx->h_state, sizeof(CamState), hipHostMallocDefault);
     if (e == hipSuccess) std::memset(ctx->h_state, 0, sizeof(CamState));
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->state_ev, hipEventDisableTiming);
@@ -962,7 +969,7 @@ int ensure_graph(eray_ctx* ctx, std::vector<unsigned char> key, uint32_t n, Body
     }
     HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
     int st = ERAY_OK;
-    for (uint32_t f = 0; f < n && st == ERAY_OK; ++f) st = body(f);
+    for (uint32_t f = 0; f < n && st == ERAY_OK; ++f) st = body(f, n);
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(ctx->stream, &g);
     if (st != ERAY_OK) {
@@ -1065,7 +1072,7 @@ int eray_render_prepare(eray_ctx* ctx, const eray_render_params* rp, uint32_t fr
     if (int st = prepare_render(ctx, rp, &p, &empty, SetupWait::kYes)) return st;
     if (empty) return ERAY_OK;
     Plan plan;
-    auto body = [&](uint32_t) -> int {
+    auto body = [&](uint32_t, uint32_t) -> int {
         HIP_TRY(ctx, launch_frame(ctx, p));
         return ERAY_OK;
     };
@@ -1080,13 +1087,14 @@ int eray_render_frames(eray_ctx* ctx, const eray_render_params* rp, uint32_t fra
     if (mean_frame_ms) *mean_frame_ms = 0.0f;
     if (empty || !frames) return ERAY_OK;
     Plan plan;
-    auto body = [&](uint32_t) -> int {
+    auto body = [&](uint32_t, uint32_t) -> int {
         HIP_TRY(ctx, launch_frame(ctx, p));
         return ERAY_OK;
     };
     if (int st = ensure_plan(ctx, params_key(p, 0), frames, body, &plan)) return st;
     auto none = [](uint32_t, uint32_t) { return (int)ERAY_OK; };
-    return replay(ctx, plan, frames, none, body, mean_frame_ms);
+    auto plain = [&](uint32_t f) { return body(f, frames); };
+    return replay(ctx, plan, frames, none, plain, mean_frame_ms);
 }
 
 int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* rp, const eray_camera* cameras, uint32_t n,
@@ -1152,7 +1160,7 @@ int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* rp, const e
         HIP_TRY(ctx, launch_frame(ctx, p));
         return ERAY_OK;
     };
-    auto body = [&](uint32_t f) { return frame(ctx->d_path + f); };
+    auto body = [&](uint32_t f, uint32_t) { return frame(ctx->d_path + f); };
     std::vector<unsigned char> key = params_key(p, 1);
     key.insert(key.end(), reinterpret_cast<const unsigned char*>(&ctx->d_path),
                reinterpret_cast<const unsigned char*>(&ctx->d_path) + sizeof ctx->d_path);
@@ -1198,6 +1206,9 @@ int eray_ppm_header(uint32_t w, uint32_t h, char* buf, size_t cap, size_t* len) 
 }
 
 }  // extern "C"
+
+// Error reporting for the other translation units of the library (comm.cpp).
+int eray_internal_error(eray_ctx* ctx, int code, const char* msg) { return set_error(ctx, code, "%s", msg); }
 
 // Diagnostics (not part of include/eray_hip.h): the screen bins of object `index` as built for
 // the last setup — out[0] bins, out[1] entries, out[2] (face, pixel) pairs (mask bits),

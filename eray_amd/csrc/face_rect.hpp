@@ -14,68 +14,70 @@ namespace gpu {
 // 2^-24 of x/W: far less than a pixel) gives a conservative pixel rectangle per face.  The
 // object's rectangle is the union: no primary ray outside it can hit the object, so those pixels
 // need no test for it.
-// The polygon (at most 8 vertices: 4 + one per clip) lives in the caller's LDS workspace `ws`
-// (4 arrays of 8 doubles, element k of array a at ws[(a * 8 + k) * stride]): as private arrays
-// with run-time indices it lived in scratch memory, a chain of memory round trips per clip
-// (tri_rect_kernel took 14.5 us for 12 faces).
+// The polygon (at most 8 vertices: 4 + one per clip) is held in registers (fully unrolled, so
+// every vertex index is a compile-time constant); only a clip's output, whose positions depend on
+// the data, goes through the caller's LDS workspace `ws` (2 arrays of 8 doubles, element k of
+// array a at ws[(a * 8 + k) * stride]) and is read back in one round trip per clip.  (As private
+// arrays with run-time indices the polygon lived in scratch memory, and as an LDS polygon read
+// vertex by vertex each clip was a chain of LDS round trips.)
 __device__ inline bool face_rect(const TriCull& c, uint32_t W, uint32_t H, int32_t (&r)[4], double* ws,
                                  uint32_t stride) {
+    constexpr int kMax = 8;
     const float A[4] = {c.A.x, c.A.y, c.A.z, c.A.w}, B[4] = {c.B.x, c.B.y, c.B.z, c.B.w};
     const float K[4] = {c.K.x, c.K.y, c.K.z, c.K.w}, T[4] = {c.T.x, c.T.y, c.T.z, c.T.w};
-    double* px = ws;
-    double* py = ws + 8 * stride;
-    double* qx = ws + 16 * stride;
-    double* qy = ws + 24 * stride;
-    const double sx[4] = {0.0, 1.0, 1.0, 0.0}, sy[4] = {0.0, 0.0, 1.0, 1.0};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        px[i * stride] = sx[i];
-        py[i * stride] = sy[i];
-    }
+    double* qx = ws;
+    double* qy = ws + kMax * stride;
+    double px[kMax] = {0.0, 1.0, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    double py[kMax] = {0.0, 0.0, 1.0, 1.0, 0.0, 0.0, 0.0, 0.0};
     int n = 4;
+#pragma unroll
     for (int k = 0; k < 4; ++k) {
         if (T[k] == __builtin_inff()) continue;  // condition disabled (non-finite record)
         if (!(T[k] > -__builtin_inff())) return false;  // the face rejects every camera ray
         const double a = A[k], b = B[k];
         const double mag = fabs((double)K[k]) + fabs(a) + fabs(b) + fabs((double)T[k]);
         const double cc = (double)K[k] + (double)T[k] + 1e-9 * mag + 1e-300;
+        double f[kMax];
+#pragma unroll
+        for (int i = 0; i < kMax; ++i) f[i] = a * px[i] + b * py[i] + cc;
         int m = 0;
-        double xi = px[0], yi = py[0];
-        double fi = a * xi + b * yi + cc;
-        for (int i = 0; i < n; ++i) {
-            const int j = i + 1 == n ? 0 : i + 1;
-            const double xj = px[j * stride], yj = py[j * stride];
-            const double fj = a * xj + b * yj + cc;
+#pragma unroll
+        for (int i = 0; i < kMax; ++i) {
+            if (i >= n) break;
+            const bool last = i + 1 == n;  // edge i -> i + 1 (the last edge closes the polygon)
+            const double xj = last ? px[0] : px[(i + 1) % kMax], yj = last ? py[0] : py[(i + 1) % kMax];
+            const double fi = f[i], fj = last ? f[0] : f[(i + 1) % kMax];
             if (fi >= 0.0) {
-                qx[m * stride] = xi;
-                qy[m * stride] = yi;
+                qx[m * stride] = px[i];
+                qy[m * stride] = py[i];
                 ++m;
             }
             if ((fi >= 0.0) != (fj >= 0.0)) {
                 double t = fi / (fi - fj);
                 t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
-                qx[m * stride] = xi + t * (xj - xi);
-                qy[m * stride] = yi + t * (yj - yi);
+                qx[m * stride] = px[i] + t * (xj - px[i]);
+                qy[m * stride] = py[i] + t * (yj - py[i]);
                 ++m;
             }
-            xi = xj;
-            yi = yj;
-            fi = fj;
         }
         n = m;
         if (!n) return false;
-        for (int i = 0; i < n; ++i) {
-            px[i * stride] = qx[i * stride];
-            py[i * stride] = qy[i * stride];
-        }
+#pragma unroll
+        for (int i = 0; i < kMax; ++i)
+            if (i < n) {
+                px[i] = qx[i * stride];
+                py[i] = qy[i * stride];
+            }
     }
     double xmin = px[0], xmax = px[0], ymin = py[0], ymax = py[0];
-    for (int i = 1; i < n; ++i) {
-        xmin = fmin(xmin, px[i * stride]);
-        xmax = fmax(xmax, px[i * stride]);
-        ymin = fmin(ymin, py[i * stride]);
-        ymax = fmax(ymax, py[i * stride]);
-    }
+#pragma unroll
+    for (int i = 1; i < kMax; ++i)
+        if (i < n) {
+            xmin = fmin(xmin, px[i]);
+            xmax = fmax(xmax, px[i]);
+            ymin = fmin(ymin, py[i]);
+            ymax = fmax(ymax, py[i]);
+        }
     r[0] = max((int32_t)floor(xmin * W) - 1, 0);
     r[1] = min((int32_t)ceil(xmax * W) + 1, (int32_t)W - 1);
     r[2] = max((int32_t)floor(ymin * H) - 1, 0);

@@ -207,6 +207,8 @@ hipError_t launch_tri_precompute(const float* pos, const float* nrm, const float
 // its conservative pixel rectangle, per object the union of those (ObjGeom::rect, written into
 // the device descriptors), for binned objects each face's bin rectangle (bins.hip), and, for
 // scenes without binned objects, the merged detail rectangles of the rendered rows (CamState).
+// camera_setup_kernel's grid: at most this many workgroups, each a contiguous chunk of triangles
+constexpr uint32_t kSetupMaxBlocks = 256;
 struct SetupParams {
     const TriHot* hot;
     TriCull* cull;
@@ -221,6 +223,7 @@ struct SetupParams {
     uint32_t row0, rows;        // rendered camera rows (the merged rectangles are rank-local)
     uint32_t* acc;              // 4 x nobj rectangle accumulators, zero between setups
     uint32_t* done;             // workgroup counter (last-workgroup finalisation), zero between setups
+    uint32_t* part;             // kSetupMaxBlocks x 10: each workgroup's boundary objects' partials
     uint32_t binned;            // some object is binned: bins.hip narrows rects + builds the detail list
     // binned objects' faces (bins.hip): bin rectangle and its number of bins per face (zero for
     // other faces), the binned-object index per face
@@ -260,6 +263,7 @@ struct BinBuffers {
     uint32_t* n = nullptr;                // entries found (device counter, reset by the finaliser)
     uint32_t* done = nullptr;             // workgroup counter of the finaliser
     uint32_t* acc = nullptr;              // 4 x nb rectangle accumulators of the non-empty bins
+    uint32_t* part = nullptr;             // 10 per finaliser workgroup: its end objects' partials
     uint32_t* ekey = nullptr;             // unscattered entries (cap)
     uint32_t* eface = nullptr;
     unsigned long long* emask = nullptr;

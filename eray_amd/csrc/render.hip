@@ -39,6 +39,8 @@ using namespace eray::dev;
 
 constexpr int kWG = 256;
 constexpr int kTriTile = 256;
+// frame_kernel's h_total_sub in device-camera mode: read the count from CamState
+constexpr uint32_t kDeviceCount = 0xffffffffu;
 
 // Scene descriptors and triangle records are read-only for the whole frame: reading them
 // through the constant address space lets wave-uniform reads become scalar (s_load) loads.
@@ -1169,8 +1171,11 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     const bool aligned = p.aligned != 0;  // (a kernel-argument read where it is used)
     // detail sub-blocks (device-camera mode: counted by the setup kernels, and the small-scene
     // fill reservation chosen from that count as launch_frame_kernel does from the host's)
-    const uint32_t total = p.cam_state ? load_const(&p.cam_state->total_sub, 0) : hot.total_sub;
-    if (p.cam_state && p.detail_wgs_alt && total > detail_wgs * nwaves) {
+    // (h_total_sub == kDeviceCount: device-camera mode, decided from a preloaded argument so the
+    // args-mode role decision waits for no kernel-argument load)
+    const bool dev_count = hot.total_sub == kDeviceCount;
+    const uint32_t total = dev_count ? load_const(&p.cam_state->total_sub, 0) : hot.total_sub;
+    if (dev_count && p.detail_wgs_alt && total > detail_wgs * nwaves) {
         detail_wgs = p.detail_wgs_alt;
         fill_first = true;
     }
@@ -1372,7 +1377,8 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
             if ((e = hipEventRecord(lc.fork, s)) != hipSuccess || (e = hipStreamWaitEvent(lc.side, lc.fork, 0)) != hipSuccess)
                 return e;
             frame_kernel<C, L, M, K, D><<<dgrid, kWG, dyn, s>>>(q.objects, q.lights, q.cull, q.tris, q.shade,
-                                                             q.nobj | (q.nlights << 16), q.total_tris, q.total_sub,
+                                                             q.nobj | (q.nlights << 16), q.total_tris,
+                                                             q.cam_state ? kDeviceCount : q.total_sub,
                                                              frame_roles(dgrid, q), q);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             fill_kernel<<<fgrid, kWG, 0, lc.side>>>(q);
@@ -1382,7 +1388,8 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
         }
     }
     frame_kernel<C, L, M, K, D><<<grid, kWG, dyn, s>>>(q.objects, q.lights, q.cull, q.tris, q.shade,
-                                                    q.nobj | (q.nlights << 16), q.total_tris, q.total_sub,
+                                                    q.nobj | (q.nlights << 16), q.total_tris,
+                                                             q.cam_state ? kDeviceCount : q.total_sub,
                                                     frame_roles(grid, q), q);
     return hipGetLastError();
 }

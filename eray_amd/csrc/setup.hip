@@ -17,7 +17,7 @@ namespace {
 
 using namespace eray::dev;
 
-constexpr int kSetupWG = 128;
+constexpr int kSetupWG = 256;
 
 // --------------------------------------------------------------------- culling record ------
 // Derivation (u = 2^-24, all norms are 1-norms of the float inputs; d = normalised direction).
@@ -131,6 +131,7 @@ __device__ TriCull cull_record(const TriHot& h, const CamDev& cam) {
 
 // the object owning triangle i (objects are consecutive triangle ranges)
 __device__ __forceinline__ uint32_t object_of(const uint32_t* begin, uint32_t nobj, uint32_t i) {
+    if (nobj <= 1) return 0u;
     uint32_t lo = 0, hi = nobj;  // last object whose first triangle is <= i
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -148,22 +149,46 @@ __device__ __forceinline__ void rect_words(const int32_t (&r)[4], uint32_t (&a)[
     a[3] = (uint32_t)r[3] + 1u;
 }
 
+// Per-object unions without contended atomics: workgroup b owns the contiguous triangle chunk
+// [b * chunk, (b + 1) * chunk), whose objects are a contiguous run [o_first, o_last].  It reduces
+// its faces' rectangles per object in LDS; an object strictly inside the run belongs to this
+// workgroup alone (its union is final and stored to acc), the run's two end objects may continue
+// in the neighbours (stored as this workgroup's partials).  The last workgroup combines: a scene
+// whose one object spans every workgroup costs one counter increment per workgroup, not four
+// atomics per wave on the same four words (70k faces: 73 -> a few us).
+constexpr uint32_t kSpan = kSetupWG;  // objects per workgroup reduced in LDS (more: global atomics)
+constexpr uint32_t kTab = 2048;       // objects the last workgroup combines in LDS (more: in acc)
+
+__device__ __forceinline__ void max4(uint32_t* dst, const uint32_t (&a)[4]) {
+    for (int k = 0; k < 4; ++k) atomicMax(dst + k, a[k]);
+}
+
 __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp) {
-    __shared__ double s_poly[32 * kSetupWG];  // face_rect's polygon workspace, 256 B per thread
-    __shared__ int32_t s_rects[kSetupWG][4];
+    __shared__ double s_poly[16 * kSetupWG];  // face_rect's clip output, 128 B per thread
+    __shared__ uint32_t s_acc[kSpan][4];      // this workgroup's objects (o - o_first)
+    __shared__ uint32_t s_tab[kTab][4];       // the last workgroup's per-object unions
     __shared__ uint32_t s_last;
     const CamDev cam = *sp.cam;
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
-    const uint32_t i = blockIdx.x * kSetupWG + tid;
-    uint32_t obj = 0;
-    uint32_t a[4] = {0u, 0u, 0u, 0u};
-    if (i < sp.T) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t chunk = (sp.T + gridDim.x - 1) / gridDim.x;
+    const uint32_t lo = min(blockIdx.x * chunk, sp.T), hi = min(lo + chunk, sp.T);
+    const uint32_t o_first = lo < hi ? object_of(sp.obj_begin, sp.nobj, lo) : 0u;
+    const uint32_t o_last = lo < hi ? object_of(sp.obj_begin, sp.nobj, hi - 1) : 0u;
+    for (uint32_t j = tid; j < kSpan; j += kSetupWG)
+        for (int k = 0; k < 4; ++k) s_acc[j][k] = 0u;
+    __syncthreads();
+    for (uint32_t i = lo + tid; i < hi; i += kSetupWG) {
         const TriCull c = cull_record(sp.hot[i], cam);
         sp.cull[i] = c;
-        obj = object_of(sp.obj_begin, sp.nobj, i);
+        const uint32_t obj = object_of(sp.obj_begin, sp.nobj, i);
         int32_t r[4];
         const bool any = face_rect(c, sp.W, sp.H, r, s_poly + tid, kSetupWG);
-        if (any) rect_words(r, a);
+        if (any) {
+            uint32_t a[4];
+            rect_words(r, a);
+            if (obj - o_first < kSpan) max4(s_acc[obj - o_first], a);
+            else max4(sp.acc + 4 * obj, a);  // (a workgroup spanning very many objects)
+        }
         if (sp.range) {  // bins.hip: the face's bin rectangle, if its object is binned
             const uint32_t k = sp.objkey[obj];
             int4 g = make_int4(1, 0, 1, 0);
@@ -180,50 +205,108 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp) 
             sp.fkey[i] = k;
         }
     }
-    // per-object union: one set of atomics per wave when its faces share one object
-    const uint32_t o0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)obj);
-    if (__all(obj == o0 || i >= sp.T)) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            for (int off = 32; off > 0; off >>= 1) a[k] = max(a[k], (uint32_t)__shfl_xor((int)a[k], off));
-        if (lane == 0 && a[1])
-            for (int k = 0; k < 4; ++k) atomicMax(sp.acc + 4 * o0 + k, a[k]);
-    } else if (a[1]) {
-        for (int k = 0; k < 4; ++k) atomicMax(sp.acc + 4 * obj + k, a[k]);
+    __syncthreads();
+    const bool single = gridDim.x == 1;
+    if (!single) {  // publish: inner objects' unions are final, the two end objects' are partial
+        const uint32_t span = lo < hi ? min(o_last - o_first + 1, kSpan) : 0u;
+        for (uint32_t j = tid; j < span; j += kSetupWG) {
+            const uint32_t o = o_first + j;
+            if (o == o_first || o == o_last) continue;
+            for (int k = 0; k < 4; ++k) sp.acc[4 * o + k] = s_acc[j][k];
+        }
+        if (tid == 0) {
+            uint32_t* pb = sp.part + 10 * blockIdx.x;
+            pb[0] = lo < hi ? o_first : ~0u;
+            pb[5] = lo < hi ? o_last : ~0u;
+            for (int k = 0; k < 4; ++k) {
+                pb[1 + k] = s_acc[0][k];
+                pb[6 + k] = lo < hi && o_last - o_first < kSpan ? s_acc[o_last - o_first][k] : 0u;
+            }
+        }
+        __threadfence();
+        __syncthreads();
+        if (tid == 0) s_last = atomicAdd(sp.done, 1u) == gridDim.x - 1;
+        __syncthreads();
+        if (!s_last) return;
+        __threadfence();
     }
-    // the last workgroup finalises
-    __threadfence();
+    // ---- the last workgroup: every object's union
+    const bool in_lds = sp.nobj <= kTab;
+    if (single && sp.nobj <= kSpan) {
+        for (uint32_t j = tid; j < sp.nobj; j += kSetupWG) {
+            uint32_t w[4];
+            for (int k = 0; k < 4; ++k) w[k] = s_acc[j][k];
+            for (int k = 0; k < 4; ++k) s_tab[j][k] = w[k];
+        }
+    } else if (in_lds) {
+        for (uint32_t j = tid; j < sp.nobj; j += kSetupWG)
+            for (int k = 0; k < 4; ++k) {
+                s_tab[j][k] = sp.acc[4 * j + k];
+                sp.acc[4 * j + k] = 0u;  // zero for the next setup
+            }
+        __syncthreads();
+        if (single) {  // more objects than kSpan: the first kSpan are still in s_acc
+            for (uint32_t j = tid; j < min(sp.nobj, kSpan); j += kSetupWG)
+                for (int k = 0; k < 4; ++k) s_tab[j][k] = max(s_tab[j][k], s_acc[j][k]);
+        } else {
+            for (uint32_t b = tid; b < gridDim.x; b += kSetupWG) {
+                const uint32_t* pb = sp.part + 10 * b;
+                if (pb[0] != ~0u) {
+                    uint32_t a[4] = {pb[1], pb[2], pb[3], pb[4]};
+                    max4(s_tab[pb[0]], a);
+                }
+                if (pb[5] != ~0u) {
+                    uint32_t a[4] = {pb[6], pb[7], pb[8], pb[9]};
+                    max4(s_tab[pb[5]], a);
+                }
+            }
+        }
+    } else {  // very many objects: combine in the global accumulators
+        if (single) {
+            for (uint32_t j = tid; j < min(sp.nobj, kSpan); j += kSetupWG) {
+                uint32_t a[4] = {s_acc[j][0], s_acc[j][1], s_acc[j][2], s_acc[j][3]};
+                max4(sp.acc + 4 * j, a);
+            }
+        } else {
+            for (uint32_t b = tid; b < gridDim.x; b += kSetupWG) {
+                const uint32_t* pb = sp.part + 10 * b;
+                if (pb[0] != ~0u) {
+                    uint32_t a[4] = {pb[1], pb[2], pb[3], pb[4]};
+                    max4(sp.acc + 4 * pb[0], a);
+                }
+                if (pb[5] != ~0u) {
+                    uint32_t a[4] = {pb[6], pb[7], pb[8], pb[9]};
+                    max4(sp.acc + 4 * pb[5], a);
+                }
+            }
+        }
+        __threadfence();
+    }
     __syncthreads();
-    if (tid == 0) s_last = atomicAdd(sp.done, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
     for (uint32_t j = tid; j < sp.nobj; j += kSetupWG) {
         uint32_t w[4];
-        for (int k = 0; k < 4; ++k) w[k] = atomicExch(sp.acc + 4 * j + k, 0u);  // read and reset
+        if (in_lds) {
+            for (int k = 0; k < 4; ++k) w[k] = s_tab[j][k];
+        } else {
+            for (int k = 0; k < 4; ++k) w[k] = atomicExch(sp.acc + 4 * j + k, 0u);  // read and reset
+        }
         int32_t r[4];
-        if (w[1] == 0) {  // no face can be hit
-            r[0] = 1;
-            r[1] = 0;
-            r[2] = 1;
-            r[3] = 0;
+        if (w[1] == 0) {  // no face can be hit (or no faces)
+            r[0] = r[2] = 1;
+            r[1] = r[3] = 0;
         } else {
             r[0] = (int32_t)~w[0];
             r[1] = (int32_t)w[1] - 1;
             r[2] = (int32_t)~w[2];
             r[3] = (int32_t)w[3] - 1;
         }
-        if (sp.obj_begin[j + 1] == sp.obj_begin[j]) {  // no faces: no rectangle
-            r[0] = r[2] = 1;
-            r[1] = r[3] = 0;
-        }
         for (int k = 0; k < 4; ++k) sp.objs[j].g.rect[k] = r[k];
-        if (j < kSetupWG)
-            for (int k = 0; k < 4; ++k) s_rects[j][k] = r[k];
+        if (j < kTab)
+            for (int k = 0; k < 4; ++k) s_tab[j][k] = (uint32_t)r[k];
     }
     __syncthreads();
     if (tid != 0) return;
-    *sp.done = 0u;
+    if (!single) *sp.done = 0u;
     CamState& st = *sp.state;
     st.cam = cam;
     if (sp.binned) return;  // bins.hip narrows the rectangles and lists the detail sub-blocks
@@ -234,7 +317,7 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp) 
     const int32_t rows_i = (int32_t)sp.rows, w_i = (int32_t)sp.W;
     for (uint32_t j = 0; j < sp.nobj; ++j) {
         int32_t r[4];
-        for (int k = 0; k < 4; ++k) r[k] = j < kSetupWG ? s_rects[j][k] : sp.objs[j].g.rect[k];
+        for (int k = 0; k < 4; ++k) r[k] = j < kTab ? (int32_t)s_tab[j][k] : sp.objs[j].g.rect[k];
         int32_t x0 = r[0], x1 = r[1], y0 = r[2] - (int32_t)sp.row0, y1 = r[3] - (int32_t)sp.row0;
         x1 = x1 < w_i - 1 ? x1 : w_i - 1;
         y0 = y0 > 0 ? y0 : 0;
@@ -285,7 +368,7 @@ __global__ void set_camera_kernel(CamDev cam, CamDev* slot) {
 }  // namespace
 
 hipError_t launch_camera_setup(const SetupParams& sp, hipStream_t s) {
-    const uint32_t blocks = sp.T ? (sp.T + kSetupWG - 1) / kSetupWG : 1u;
+    const uint32_t blocks = sp.T ? min((sp.T + kSetupWG - 1) / kSetupWG, kSetupMaxBlocks) : 1u;
     camera_setup_kernel<<<blocks, kSetupWG, 0, s>>>(sp);
     return hipGetLastError();
 }

@@ -29,6 +29,7 @@
  *                           primitives.rs:41-72, cast_ray shading engine.rs:112-216,
  *                           reaches_light engine.rs:218-228) fused with the PPM byte pack
  *   eray_pack_ppm           lib/image.rs:48-74 + lib/color.rs:31-37 (save_as_ppm body bytes)
+ *   eray_gather_rows        lib/engine.rs:85-98 + lib/image.rs:48-74 across GPUs (row tiles, RCCL)
  *   eray_ppm_header         lib/image.rs:56
  *   eray_camera_size        lib/camera.rs:36-38
  *
@@ -278,6 +279,24 @@ int eray_render_prepare(eray_ctx* ctx, const eray_render_params* params, uint32_
  * included.  The scene camera (eray_scene_set_camera) is unchanged. */
 int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* params, const eray_camera* cameras,
                             uint32_t n, float* mean_frame_ms);
+
+/* ------------------------------------------------------------------ multi-GPU ----------- *
+ * One process (one context) per GPU; a frame is split into row tiles and gathered on rank 0
+ * (SURVEY.md §8(e)).  Rank r of n renders the r-th block of PPM file rows — camera rows
+ * [H - (r+1)*rows, H - r*rows) with out_ppm set — and eray_gather_rows concatenates the blocks on
+ * rank 0 in rank order, which is the PPM body of Image::save_as_ppm (image.rs:48-74).  The gather
+ * is one RCCL collective (xGMI) on the context's stream.  `nccl_comm` is an ncclComm_t: the
+ * caller's own, or one made with eray_comm_init from an id that rank 0 got from
+ * eray_comm_unique_id and sent to the other ranks by any means. */
+#define ERAY_COMM_ID_BYTES 128
+int eray_comm_unique_id(uint8_t* id /* ERAY_COMM_ID_BYTES */);
+int eray_comm_init(eray_ctx* ctx, int nranks, int rank, const uint8_t* id, void** nccl_comm);
+int eray_comm_destroy(void* nccl_comm);
+/* local: device, rows x width x 3 PPM bytes of this rank's block; frame (rank 0 only): device,
+ * nranks x rows x width x 3 bytes.  Replaces the reference's single-process image write
+ * (engine.rs:85-98 render_to_path -> save_as_ppm). */
+int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8_t* frame, uint32_t rows,
+                     uint32_t width);
 
 /* ------------------------------------------------------------------ PPM ----------------- */
 /* Body bytes of Image<Color>::save_as_ppm for a width x height device image: rows bottom-up,
