@@ -143,6 +143,45 @@ def test_random_multi_object_scene(gpu, oracle, seed):
     assert_bit_equal(rgb_b, ref, f"random scene {seed} brute")
 
 
+def test_specular_power_textures_bit_exact(gpu, oracle):
+    """A specular-power texture (engine.rs:164,171,174: powf not the identity): the frame kernel's
+    restated glibc powf against the oracle's glibc powf, culled and brute force, bit for bit."""
+    rng = np.random.default_rng(23)
+    W, H = 128, 72
+    gpu.scene_reset()
+    cam_center = (0.05, -0.1, 3.5)
+    gpu.set_camera(capi.make_camera(cam_center, (16.0, 9.0), W, 1.0))
+    s = oracle.Scene()
+    keep = []
+    for k in range(2):
+        pos, nrm, uv = random_mesh(rng, 200, scale=0.9, center=rng.uniform(-0.5, 0.5, 3))
+        lo, hi = pos.reshape(-1, 3).min(0), pos.reshape(-1, 3).max(0)
+        color = rng.uniform(0, 1, (6, 5, 3)).astype(np.float32)
+        sp = rng.uniform(0.0, 40.0, (7, 9)).astype(np.float32)  # exponents 0 .. 40
+        sp[0, :3] = [1.0, 0.5, 2.0]
+        spec = rng.uniform(0, 1, (3, 3)).astype(np.float32)
+        dc, dsp, ds = gpu.to_device(color), gpu.to_device(sp), gpu.to_device(spec)
+        keep += [dc, dsp, ds]
+        gpu.add_object(pos, nrm, uv, tuple(lo), tuple(hi), color=dc.image(), specular=ds.image(),
+                       specular_power=dsp.image())
+        s.add_object(pos, nrm, uv, tuple(lo), tuple(hi), color=color, specular=spec, specular_power=sp)
+    for p, var, col, b in (((0.0, 2.0, 0.0), "ambient", (1.0, 1.0, 1.0), 0.2),
+                           ((1.0, 1.0, 2.0), "point", (1.0, 1.0, 1.0), 1.0),
+                           ((-1.5, 0.3, 1.5), "point", (0.6, 0.8, 1.0), 0.8)):
+        gpu.add_light(capi.make_light(p, var, col, b))
+        s.add_light(p, var, col, b)
+    try:
+        ref, ref_face, stats = oracle.render(s, oracle.camera(cam_center, (16.0, 9.0), W, 1.0), want_faces=True)
+        assert stats["hit_pixels"] > 150
+        for flags in (capi.RENDER_DEFAULT, capi.RENDER_BRUTE_FORCE):
+            rgb, face, _ = gpu_render(gpu, W, H, flags=flags)
+            assert np.array_equal(face, ref_face)
+            assert_bit_equal(rgb, ref, f"specular power flags={flags}")
+    finally:
+        for a in keep:
+            a.free()
+
+
 def test_row_tiles_equal_full_frame(gpu, cube):
     W, H = 640, 360
     sc = MainScene(gpu, *cube, W, H)

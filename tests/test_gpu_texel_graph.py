@@ -3,15 +3,15 @@ a material graph of the four shaderlib nodes evaluated at the hit texel must ren
 the texture path renders — Graph::run's images (here the oracle's node functions, and the GPU's
 own node kernels) sampled by Material::get (material.rs:56-94).
 
-Bar: bit-identical f32 RGB and faces (powf with a specular-power output: RGB_TOL, the device
-evaluates pow in double).
+Bar: bit-identical f32 RGB and faces (powf with a specular-power output too: the device runs
+the restated glibc powf, eray_amd/csrc/glibc_powf.hpp).
 """
 import numpy as np
 import pytest
 
 from eray_amd import capi
 from eray_amd.frame import fov_for
-from tests.helpers import RGB_TOL, assert_bit_equal, random_mesh
+from tests.helpers import assert_bit_equal, random_mesh
 
 pytestmark = pytest.mark.gpu
 
@@ -184,8 +184,8 @@ def test_mistyped_output_reads_as_none(gpu, oracle, cube):
 
 
 def test_reflection_and_specular_power_outputs(gpu, oracle):
-    """Graph outputs for specular power (powf not the identity: tolerance) and reflection (the
-    general tracer's bounces)."""
+    """Graph outputs for specular power (powf not the identity: the restated glibc powf, bit for
+    bit) and reflection (the general tracer's bounces)."""
     rng = np.random.default_rng(17)
     a = random_mesh(rng, 60, scale=0.8, center=(-0.3, 0.0, 0.0))
     b = random_mesh(rng, 60, scale=0.8, center=(0.4, 0.2, -0.3))
@@ -213,7 +213,7 @@ def test_reflection_and_specular_power_outputs(gpu, oracle):
         got, face = render(gpu, bounces=bounces)
         ref, ref_face, _ = oracle.render(s, cam, want_faces=True, bounces=bounces)
         assert np.array_equal(face, ref_face)
-        np.testing.assert_allclose(got, ref, rtol=0, atol=RGB_TOL, err_msg=f"bounces={bounces}")
+        assert_bit_equal(got, ref, f"specular power, bounces={bounces}")
 
 
 def test_texel_graph_errors(gpu, cube):
