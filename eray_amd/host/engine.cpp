@@ -27,10 +27,23 @@ std::pair<uint32_t, uint32_t> Camera::size() const {
 Material::Material(Graph<Validated> graph, std::map<StandardMaterialOutput, Name> selected)
     : selected_(std::move(selected)), graph_(std::move(graph)), recompute_(true) {}
 
-Status Material::update() {  // material.rs:35-53 (the debug color.ppm dump is not reproduced)
+Status Material::update() {  // material.rs:35-53
     if (recompute_) {
         if (Status s = run(graph_)) return s;
         recompute_ = false;
+    }
+    // material.rs:41-50 (#[cfg(debug_assertions)]): the Color output's image to color.ppm (the
+    // reference panics when that output is not an IColor)
+    if (debug_dumps()) {
+        auto sel = selected_.find(StandardMaterialOutput::Color);
+        if (sel != selected_.end()) {
+            auto out = graph_.outputs.find(sel->second);
+            if (out != graph_.outputs.end()) {
+                const SocketValue& v = out->second.second;
+                if (v.type() != SocketType::IColor) throw Failure(ERAY_E_INVALID_TYPE, "color output is not an IColor");
+                if (v.as_icolor()) save_as_ppm(v.as_icolor()->to_host(), "color.ppm");
+            }
+        }
     }
     return std::nullopt;
 }

@@ -41,6 +41,16 @@ std::vector<uint8_t> ppm_bytes(const Image<Color>& image) {
     return out;
 }
 
+namespace {
+#ifdef NDEBUG
+bool g_debug_dumps = false;
+#else
+bool g_debug_dumps = true;
+#endif
+}  // namespace
+bool debug_dumps() { return g_debug_dumps; }
+void set_debug_dumps(bool on) { g_debug_dumps = on; }
+
 void save_as_ppm(const Image<Color>& image, const std::string& path) {
     const std::vector<uint8_t> bytes = ppm_bytes(image);
     std::ofstream f(path, std::ios::binary);

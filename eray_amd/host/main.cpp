@@ -3,6 +3,9 @@
 // the two lights, render, write the PPM.
 //
 //   eray_main [--mesh objects/cube.obj] [--width 1024] [--fov 60 60] [--output output.ppm]
+//             [--no-debug-dumps]
+// Like the reference's debug build, the run also writes rgb.ppm (the rgb node, rgb.rs:96) and
+// color.ppm (Material::update, material.rs:41-50) into the working directory.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -22,11 +25,12 @@ int main(int argc, char** argv) {
         if (a == "--mesh" && i + 1 < argc) mesh = argv[++i];
         else if (a == "--output" && i + 1 < argc) output = argv[++i];
         else if (a == "--width" && i + 1 < argc) width = (uint32_t)std::strtoul(argv[++i], nullptr, 10);
+        else if (a == "--no-debug-dumps") set_debug_dumps(false);
         else if (a == "--fov" && i + 2 < argc) {
             fov_a = std::strtof(argv[++i], nullptr);
             fov_b = std::strtof(argv[++i], nullptr);
         } else {
-            std::fprintf(stderr, "usage: %s [--mesh PATH] [--width W] [--fov A B] [--output PATH]\n", argv[0]);
+            std::fprintf(stderr, "usage: %s [--mesh PATH] [--width W] [--fov A B] [--output PATH] [--no-debug-dumps]\n", argv[0]);
             return 2;
         }
     }

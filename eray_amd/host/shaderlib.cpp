@@ -134,6 +134,8 @@ NodeResult node() {
                          d.check(eray_node_rgb(d.ctx(), res.width, res.height, red->as_ivalue()->view(),
                                                green->as_ivalue()->view(), blue->as_ivalue()->view(),
                                                reinterpret_cast<float*>(res.data())));
+                         // rgb.rs:96: the node writes its image to rgb.ppm in the working directory
+                         if (debug_dumps()) save_as_ppm(res.to_host(), "rgb.ppm");
                          out->as_icolor() = res;
                          return std::nullopt;
                      });

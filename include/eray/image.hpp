@@ -37,6 +37,12 @@ struct Image {
     bool operator==(const Image& o) const { return width == o.width && height == o.height && pixels == o.pixels; }
 };
 
+// The reference's debug side-effect files — rgb.ppm written by every rgb node run (rgb.rs:96)
+// and color.ppm by Material::update in debug builds (material.rs:41-50) — into the working
+// directory.  On by default in builds without NDEBUG (as a `cargo run` debug build), settable.
+bool debug_dumps();
+void set_debug_dumps(bool on);
+
 // image.rs:48-74 (Image<Color>::save_as_ppm): "P6 {w} {h} 255\n" + rows y = h-1 .. 0
 std::vector<uint8_t> ppm_bytes(const Image<Color>& image);
 void save_as_ppm(const Image<Color>& image, const std::string& path);

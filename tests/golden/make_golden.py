@@ -9,9 +9,9 @@ oracle change are checked against the same bytes.
 Fixtures
   cube_c1_256.npz   C1 (cube.obj, 256x256, main.rs scene): the PPM body bytes (file order),
                     the hit face per pixel, and the f32 RGB of the hit pixels (indices + values)
-  digests.json      SHA-256 of the PPM body and of the f32 image for C1, C2 (1920x1080) and
-                    main.rs's 1024x1024 output.ppm, the per-frame hit/test counters, and the P6
-                    headers
+  digests.json      SHA-256 of the PPM body and of the f32 image for C1, C2 (1920x1080), C4
+                    (3840x2160) and main.rs's 1024x1024 output.ppm (with its color.ppm and rgb.ppm
+                    debug files), the per-frame hit/test counters, and the P6 headers
   texture_8x4.npz   the example material graph (wave -> rgb -> mix with flat) at 8x4 texels:
                     color and diffuse images
   c5_spans.npz      C5 (the 1M-face synthetic mesh, meshgen seed 1234, at 7680x4320, main.rs
@@ -96,6 +96,15 @@ def main() -> None:
                                 face=face.astype(np.int16),
                                 hit_index=hit,
                                 hit_rgb=rgb.reshape(-1, 3)[hit].astype(np.float32))
+    with open(os.path.join(HERE, "digests.json"), "w") as f:
+        json.dump(digests, f, indent=2, sort_keys=True)
+    # main.rs's debug side-effect files at its 1024x1024 material: color.ppm (Material::update,
+    # material.rs:41-50) and rgb.ppm (the rgb node, rgb.rs:96: rgb(wave, wave, wave))
+    color, _ = O.example_material(1024, 1024)
+    wave = O.node_wave(1024, 1024, 1.0, 1.0)
+    rgb_img = O.node_rgb(1024, 1024, wave, wave, wave)
+    digests["main_rs"]["color_ppm_sha256"] = hashlib.sha256(O.ppm_bytes(color)).hexdigest()
+    digests["main_rs"]["rgb_ppm_sha256"] = hashlib.sha256(O.ppm_bytes(rgb_img)).hexdigest()
     with open(os.path.join(HERE, "digests.json"), "w") as f:
         json.dump(digests, f, indent=2, sort_keys=True)
     c5_spans()

@@ -29,8 +29,9 @@ def _sha(path):
         return hashlib.sha256(f.read()).hexdigest()
 
 
-def test_host_unit_tests_cpu(host_bins):
-    r = subprocess.run([host_bins["test_host"], "--root", ROOT], capture_output=True, text=True, timeout=120)
+def test_host_unit_tests_cpu(host_bins, tmp_path):
+    r = subprocess.run([host_bins["test_host"], "--root", ROOT], capture_output=True, text=True, timeout=120,
+                       cwd=tmp_path)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 failed checks" in r.stdout
 
@@ -39,16 +40,21 @@ def test_host_unit_tests_cpu(host_bins):
 def test_host_unit_tests_gpu(host_bins, tmp_path):
     ppm = str(tmp_path / "c1.ppm")
     r = subprocess.run([host_bins["test_host"], "--gpu", "--root", ROOT, "--ppm", ppm], capture_output=True,
-                       text=True, timeout=300)
+                       text=True, timeout=300, cwd=tmp_path)
     assert r.returncode == 0, r.stdout + r.stderr
     assert _sha(ppm) == _digests()["c1"]["ppm_file_sha256"]
 
 
 @pytest.mark.gpu
 def test_main_rs_cli_output_ppm(host_bins, tmp_path):
-    """eray_main = src/main.rs: cube.obj, the example material graph, 1024x1024 -> output.ppm."""
+    """eray_main = src/main.rs: cube.obj, the example material graph, 1024x1024 -> output.ppm, and
+    the reference's debug side-effect files color.ppm (material.rs:41-50) and rgb.ppm (rgb.rs:96)
+    in the working directory."""
     out = str(tmp_path / "output.ppm")
     r = subprocess.run([host_bins["eray_main"], "--mesh", os.path.join(ROOT, "objects", "cube.obj"), "--output", out],
-                       capture_output=True, text=True, timeout=300)
+                       capture_output=True, text=True, timeout=300, cwd=tmp_path)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert _sha(out) == _digests()["main_rs"]["ppm_file_sha256"]
+    g = _digests()["main_rs"]
+    assert _sha(out) == g["ppm_file_sha256"]
+    assert _sha(str(tmp_path / "color.ppm")) == g["color_ppm_sha256"]
+    assert _sha(str(tmp_path / "rgb.ppm")) == g["rgb_ppm_sha256"]
