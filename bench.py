@@ -47,7 +47,7 @@ import torch  # noqa: E402  (imported before the HIP library: one HIP runtime pe
 import torch.distributed as dist  # noqa: E402
 
 from eray_amd import capi  # noqa: E402
-from eray_amd.dist import RowGather, gather_ppm_rows, row_block  # noqa: E402
+from eray_amd.dist import BAND_ROWS, RowGather, band_split, gather_ppm_rows, row_block  # noqa: E402
 from eray_amd.frame import MainScene  # noqa: E402
 from eray_amd.objfile import load_obj_file  # noqa: E402
 
@@ -184,6 +184,8 @@ def main() -> None:
     ap.add_argument("--brute-force", action="store_true", help="disable the exact wave culling")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--split", choices=("bands", "blocks"), default="bands",
+                    help="N > 1: interleaved 4-row bands (balanced, default) or contiguous row blocks")
     ap.add_argument("--gather-every-frame", action="store_true",
                     help="N > 1: gather the PPM rows to rank 0 after every frame (default: one final gather)")
     args = ap.parse_args()
@@ -225,36 +227,48 @@ def main() -> None:
     torch.cuda.synchronize()
     t_mat = time.perf_counter() - t_mat0
 
-    # rank r renders the r-th block of PPM file rows: camera rows [H - (r+1)*h, H - r*h)
-    row0, rows = row_block(rank, world, per_gpu)
-    rgb = torch.empty((rows, width, 3), dtype=torch.float32, device="cuda")
-    ppm = torch.empty((rows, width, 3), dtype=torch.uint8, device="cuda")
-    face = torch.empty((rows, width), dtype=torch.int32, device="cuda")
+    # rank r renders interleaved 4-row bands r, r + N, ... (every rank an equal share of the scene
+    # wherever it sits; tile timings in DESIGN.md §7) or, --split blocks, the r-th block of PPM file
+    # rows: camera rows [H - (r+1)*h, H - r*h)
+    bands = world > 1 and args.split == "bands"
+    if bands:
+        sp = band_split(rank, world, H_total, BAND_ROWS)
+        row0, rows, alloc_rows = sp["row0"], sp["rows"], sp["alloc_rows"]
+        band_args = dict(band_rows=sp["band_rows"], band_stride=sp["band_stride"])
+    else:
+        row0, rows = row_block(rank, world, per_gpu)
+        alloc_rows, band_args = rows, {}
+    rgb = torch.empty((alloc_rows, width, 3), dtype=torch.float32, device="cuda")
+    ppm = torch.zeros((alloc_rows, width, 3), dtype=torch.uint8, device="cuda")
+    face = torch.empty((alloc_rows, width), dtype=torch.int32, device="cuda")
     frame = torch.empty((H_total, width, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
     flags = capi.RENDER_BRUTE_FORCE if args.brute_force else capi.RENDER_DEFAULT
     # N > 1: the frame gather of the C-ABI (eray_gather_rows, RCCL ncclGather over xGMI); the
     # one-GPU rehearsal gathers through gloo instead
+    band = BAND_ROWS if bands else 0
     if world > 1 and not rehearsal:
         rccl = RowGather(ctx, world, rank)
 
         def gather():
-            rccl(ppm, frame)
+            rccl(ppm, frame, H_total, band)
     elif world > 1:
         def gather():
-            gather_ppm_rows(ppm, frame, world, rank)
+            gather_ppm_rows(ppm, frame, world, rank, band_rows=band)
 
     def render_args():
-        return dict(row0=row0, rows=rows, out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr(), flags=flags)
+        return dict(row0=row0, rows=rows, out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr(), flags=flags, **band_args)
 
     # one untimed instrumented frame: hit count for the algorithmic-bytes model; being the first
     # render of the camera it also builds the per-camera data (culling records, pixel
     # rectangles, screen bins of large meshes): reported as scene_setup_ms
     torch.cuda.synchronize()
     t_setup0 = time.perf_counter()
-    scene.render(out_rgb=rgb.data_ptr(), out_face=face.data_ptr(), row0=row0, rows=rows, flags=flags)
+    face.fill_(-1)
+    scene.ctx.render(width, H_total, out_rgb=rgb.data_ptr(), out_face=face.data_ptr(), row0=row0, rows=rows,
+                     flags=flags, **band_args)
     torch.cuda.synchronize()
     t_setup = time.perf_counter() - t_setup0
-    hits = int((face >= 0).sum().item())
+    hits = int((face[:rows] >= 0).sum().item())
 
     # capture the frame-loop graph, then the W warmup frames through the same replayed path as
     # the timed ones (and the gather warmed) outside the timed region
@@ -349,19 +363,21 @@ def main() -> None:
                 "workload": f"{'C2' + (f' widened x{world}' if world > 1 else '') + ': ' if is_c2 else ''}"
                             f"{os.path.basename(args.mesh)}, {width}x{H_total} frame, {width}x{per_gpu} rows per GPU, "
                             "main.rs scene + material graph; step = one frame (camera rays, first-hit scan, "
-                            "shading + shadow rays, f32 image and PPM bytes); N > 1: row tiles, final RCCL "
-                            "gather of the PPM rows to rank 0",
+                            "shading + shadow rays, f32 image and PPM bytes); N > 1: interleaved 4-row bands "
+                            "per GPU, final RCCL gather of the PPM rows to rank 0",
                 "mesh": mesh_label(args.mesh),
                 "triangles": int(len(mesh[0])),
                 "frame": [width, H_total],
                 "rows_per_gpu": rows,
                 "texture": TEXTURE,
-                "parallelism": f"row tiles x{world}" if world > 1 else "single GPU",
+                "parallelism": (f"row tiles x{world} ({'interleaved 4-row bands' if bands else 'contiguous blocks'})"
+                                if world > 1 else "single GPU"),
                 "camera": "static (value); see moving_camera",
                 **({"note": "weak scaling widens the frame to (1920 N) x 1080: not a BASELINE.json config"}
                    if world > 1 and args.scaling == "weak" else {}),
                 "culling": not args.brute_force,
             },
+            "rows_per_gpu_note": "rank 0's row count (bands: rows of its interleaved bands)" if bands else None,
             "frame_ms": round(ms_per_step, 6),
             "render_kernel_ms": round(kernel_ms, 6),
             "material_graph_s": round(t_mat, 4),

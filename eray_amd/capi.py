@@ -103,7 +103,8 @@ class RenderParams(C.Structure):
     _fields_ = [("image_width", C.c_uint32), ("image_height", C.c_uint32), ("row0", C.c_uint32),
                 ("rows", C.c_uint32), ("bounces", C.c_uint32), ("anti_aliasing", C.c_uint32),
                 ("out_rgb", C.c_void_p), ("out_ppm", C.c_void_p), ("out_face", C.c_void_p),
-                ("flags", C.c_uint32), ("aa_seed", C.c_uint64)]
+                ("flags", C.c_uint32), ("aa_seed", C.c_uint64), ("band_rows", C.c_uint32),
+                ("band_stride", C.c_uint32)]
 
 
 # Every exported symbol of include/eray_hip.h with its (restype, argtypes).
@@ -144,7 +145,8 @@ SIGNATURES = {
     "eray_comm_unique_id": (C.c_int, [_P]),
     "eray_comm_init": (C.c_int, [_P, C.c_int, C.c_int, _P, C.POINTER(_P)]),
     "eray_comm_destroy": (C.c_int, [_P]),
-    "eray_gather_rows": (C.c_int, [_P, _P, _P, _P, _U, _U]),
+    "eray_gather_rows": (C.c_int, [_P, _P, _P, _P, _U, _U, _U]),
+    "eray_band_rows": (_U, [_U, _U, _U, _U]),
     "eray_ppm_header": (C.c_int, [_U, _U, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
 }
 
@@ -154,6 +156,7 @@ DEBUG_SIGNATURES = {
     "eray_debug_set_bin_capacity": (C.c_int, [_P, C.c_uint64]),
     "eray_debug_bin_capacity": (C.c_uint64, [_P]),
     "eray_debug_setup_state": (C.c_int, [_P, _U, _P, C.POINTER(C.c_int32)]),
+    "eray_debug_unband": (C.c_int, [_P, _P, _P, _U, _U, _U, _U]),
 }
 
 _lib = None
@@ -231,6 +234,11 @@ def comm_unique_id() -> bytes:
     buf = (C.c_uint8 * COMM_ID_BYTES)()
     check(lib().eray_comm_unique_id(buf))
     return bytes(buf)
+
+
+def band_rows(height: int, band: int, nranks: int, rank: int) -> int:
+    """Camera rows of `rank` in the interleaved band split (eray_band_rows)."""
+    return lib().eray_band_rows(height, band, nranks, rank)
 
 
 def comm_destroy(comm: int) -> None:
@@ -393,22 +401,23 @@ class Context:
         return idx.value
 
     def render(self, image_width, image_height, row0=0, rows=None, out_rgb=None, out_ppm=None,
-               out_face=None, bounces=0, anti_aliasing=0, flags=RENDER_DEFAULT, aa_seed=0) -> None:
+               out_face=None, bounces=0, anti_aliasing=0, flags=RENDER_DEFAULT, aa_seed=0, band_rows=0,
+               band_stride=0) -> None:
         if rows is None:
             rows = image_height - row0
         p = RenderParams(image_width, image_height, row0, rows, bounces, anti_aliasing,
-                         out_rgb or None, out_ppm or None, out_face or None, flags, aa_seed)
+                         out_rgb or None, out_ppm or None, out_face or None, flags, aa_seed, band_rows, band_stride)
         self._check(lib().eray_render(self._h, C.byref(p)))
 
     def render_frames(self, frames, image_width, image_height, row0=0, rows=None, out_rgb=None,
                       out_ppm=None, out_face=None, flags=RENDER_DEFAULT, timed=False, prepare_only=False,
-                      bounces=0, anti_aliasing=0, aa_seed=0):
+                      bounces=0, anti_aliasing=0, aa_seed=0, band_rows=0, band_stride=0):
         """`frames` back-to-back renders (replayed from a cached HIP graph); returns the mean
         device ms per frame when `timed`.  `prepare_only` builds the launch plan and returns."""
         if rows is None:
             rows = image_height - row0
         p = RenderParams(image_width, image_height, row0, rows, bounces, anti_aliasing, out_rgb or None,
-                         out_ppm or None, out_face or None, flags, aa_seed)
+                         out_ppm or None, out_face or None, flags, aa_seed, band_rows, band_stride)
         if prepare_only:
             self._check(lib().eray_render_prepare(self._h, C.byref(p), frames))
             return None
@@ -418,13 +427,13 @@ class Context:
 
     def render_camera_path(self, cameras, image_width, image_height, row0=0, rows=None, out_rgb=None,
                            out_ppm=None, out_face=None, flags=RENDER_DEFAULT, timed=False, bounces=0,
-                           anti_aliasing=0, aa_seed=0):
+                           anti_aliasing=0, aa_seed=0, band_rows=0, band_stride=0):
         """One frame per camera (Scene::set_camera + Engine::render each), the per-camera setup on
         the device; returns the mean device ms per frame (setup included) when `timed`."""
         if rows is None:
             rows = image_height - row0
         p = RenderParams(image_width, image_height, row0, rows, bounces, anti_aliasing, out_rgb or None,
-                         out_ppm or None, out_face or None, flags, aa_seed)
+                         out_ppm or None, out_face or None, flags, aa_seed, band_rows, band_stride)
         cams = (Camera * max(1, len(cameras)))(*cameras)
         ms = C.c_float()
         self._check(lib().eray_render_camera_path(self._h, C.byref(p), cams, len(cameras),
@@ -441,9 +450,10 @@ class Context:
         self._check(lib().eray_comm_init(self._h, nranks, rank, buf, C.byref(comm)))
         return comm.value
 
-    def gather_rows(self, comm: int, local_ptr, frame_ptr, rows: int, width: int) -> None:
-        """eray_gather_rows: every rank's rows x width PPM byte block into rank 0's frame (rank order)."""
-        self._check(lib().eray_gather_rows(self._h, comm, local_ptr, frame_ptr or None, rows, width))
+    def gather_rows(self, comm: int, local_ptr, frame_ptr, height: int, width: int, band_rows: int = 0) -> None:
+        """eray_gather_rows: every rank's PPM rows into rank 0's height x width frame (file order):
+        equal blocks in rank order (band_rows = 0) or interleaved bands of band_rows rows."""
+        self._check(lib().eray_gather_rows(self._h, comm, local_ptr, frame_ptr or None, height, width, band_rows))
 
     def pack_ppm(self, rgb_ptr, w, h, out_ptr) -> None:
         self._check(lib().eray_pack_ppm(self._h, rgb_ptr, w, h, out_ptr))

@@ -143,6 +143,8 @@ struct eray_ctx {
     CamDev* h_path = nullptr;
     size_t h_path_cap = 0;
     hipEvent_t path_ev = nullptr;  // the last path upload (h_path reusable once complete)
+    uint8_t* d_staging = nullptr;  // eray_gather_rows' banded staging (rank 0)
+    size_t staging_cap = 0;
     LaunchCtx lc{nullptr, nullptr, nullptr};  // the separate fill's stream and events
 };
 
@@ -370,7 +372,14 @@ uint32_t binned_objects(const eray_ctx* ctx) {
 
 // The device buffers of the binned objects' bins for this camera size, row phase and rows
 // (reallocated, with a stream synchronisation, only when that layout or the capacity changes).
-int ensure_bins(eray_ctx* ctx, uint32_t W, uint32_t H, uint32_t row0, uint32_t rows) {
+// The rendered rows of a call: camera rows [row0, row0 + rows), or rows local rows of
+// interleaved bands (eray_render_params::band_rows).
+struct RowSpan {
+    uint32_t row0, rows, band_rows, band_stride;
+};
+
+int ensure_bins(eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs) {
+    const uint32_t row0 = rs.row0, rows = rs.rows;
     const uint32_t nb = binned_objects(ctx);
     const uint32_t T = ctx->total_tris;
     if (ctx->face_cap < T || !ctx->d_range) {
@@ -401,7 +410,7 @@ int ensure_bins(eray_ctx* ctx, uint32_t W, uint32_t H, uint32_t row0, uint32_t r
 
 // Enqueues the per-camera setup of `d_camera` (device) for camera rows [row0, row0 + rows): no
 // host round trip (setup.hip, bins.hip).
-int enqueue_setup(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint32_t H, uint32_t row0, uint32_t rows) {
+int enqueue_setup(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint32_t H, const RowSpan& rs) {
     hipStream_t stream = ctx->stream;
     SetupParams sp{};
     sp.hot = ctx->d_hot;
@@ -415,8 +424,10 @@ int enqueue_setup(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint32_t H,
     sp.state = ctx->d_state;
     sp.W = W;
     sp.H = H;
-    sp.row0 = row0;
-    sp.rows = rows;
+    sp.row0 = rs.row0;
+    sp.rows = rs.rows;
+    sp.band_rows = rs.band_rows;
+    sp.band_stride = rs.band_stride;
     // [done counter | kSetupMaxBlocks x 10 partials | 4 x nobj accumulators]: the counter and the
     // accumulators are zero between setups whatever the object count (partials are rewritten)
     sp.done = ctx->d_acc;
@@ -455,7 +466,7 @@ void state_arrived(eray_ctx* ctx) {
 // Makes the per-camera setup of the context camera current for rows [row0, row0 + rows):
 // enqueued when the camera, the rows or the scene changed, its results copied to the host
 // asynchronously.  *known: the host has them (args-mode frames); `wait`: block until it does.
-int sync_setup(eray_ctx* ctx, uint32_t W, uint32_t H, uint32_t row0, uint32_t rows, bool wait, bool* known) {
+int sync_setup(eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs, bool wait, bool* known) {
     for (int attempt = 0; attempt < 3; ++attempt) {
         if (ctx->state_pending) {
             const hipError_t q = hipEventQuery(ctx->state_ev);
@@ -465,7 +476,7 @@ int sync_setup(eray_ctx* ctx, uint32_t W, uint32_t H, uint32_t row0, uint32_t ro
         auto bins_ready = [&]() -> int {
             if (!binned_objects(ctx)) return ERAY_OK;
             const std::vector<uint64_t> before = ctx->bins_layout;
-            if (int st = ensure_bins(ctx, W, H, row0, rows)) return st;
+            if (int st = ensure_bins(ctx, W, H, rs)) return st;
             if (ctx->bins_layout != before)  // new buffers: the bin statistics start over
                 HIP_TRY(ctx, hipMemsetAsync(ctx->d_state, 0, sizeof(CamState), ctx->stream));
             return ERAY_OK;
@@ -473,8 +484,8 @@ int sync_setup(eray_ctx* ctx, uint32_t W, uint32_t H, uint32_t row0, uint32_t ro
         if (int st = bins_ready()) return st;
         std::vector<uint64_t> key(sizeof(eray_camera) / 4 + 4);
         std::memcpy(key.data(), &ctx->camera, sizeof(eray_camera));
-        key[key.size() - 4] = row0;
-        key[key.size() - 3] = rows;
+        key[key.size() - 4] = ((uint64_t)rs.row0 << 32) | rs.band_rows;
+        key[key.size() - 3] = ((uint64_t)rs.rows << 32) | rs.band_stride;
         key[key.size() - 2] = ctx->scene_gen;
         key[key.size() - 1] = ((uint64_t)W << 32) | H;
         if (key != ctx->setup_key) {
@@ -484,7 +495,7 @@ int sync_setup(eray_ctx* ctx, uint32_t W, uint32_t H, uint32_t row0, uint32_t ro
                 if (int st = bins_ready()) return st;  // (a grown capacity)
             }
             HIP_TRY(ctx, launch_set_camera(cam_dev(ctx->camera), ctx->d_cam, ctx->stream));
-            if (int st = enqueue_setup(ctx, ctx->d_cam, W, H, row0, rows)) return st;
+            if (int st = enqueue_setup(ctx, ctx->d_cam, W, H, rs)) return st;
             HIP_TRY(ctx, hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(CamState), hipMemcpyDeviceToHost,
                                         ctx->stream));
             HIP_TRY(ctx, hipEventRecord(ctx->state_ev, ctx->stream));
@@ -554,7 +565,7 @@ int eray_ctx_destroy(eray_ctx* ctx) {
     bins_free(ctx->bins);
     void* bufs[] = {ctx->d_hot,   ctx->d_shade, ctx->d_cull,  ctx->d_raw,  ctx->d_objs,  ctx->d_lights,
                     ctx->d_prog,  ctx->d_cam,   ctx->d_state, ctx->d_acc,  ctx->d_begin, ctx->d_range,
-                    ctx->d_area,  ctx->d_fkey,  ctx->d_path,  ctx->d_path_all};
+                    ctx->d_area,  ctx->d_fkey,  ctx->d_path,  ctx->d_path_all, ctx->d_staging};
     for (void* b : bufs)
         if (b) hipFree(b);
     if (ctx->h_state) hipHostFree(ctx->h_state);
@@ -836,7 +847,7 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     const bool general = rp->anti_aliasing > 0 || bounces > 0;
     uint32_t W, H;
     eray_camera_size(&ctx->camera, &W, &H);
-    if ((uint64_t)rp->row0 + rp->rows > H)
+    if (!rp->band_rows && (uint64_t)rp->row0 + rp->rows > H)
         return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "rows [%u, %u) exceed the camera height %u", rp->row0,
                          rp->row0 + rp->rows, H);
     // Image::set indexes y * image.width + x and panics past the end (image.rs:41-43)
@@ -848,13 +859,24 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     if (rp->out_ppm && (W != rp->image_width || H != rp->image_height))
         return set_error(ctx, ERAY_E_INVALID_ARGUMENT,
                          "fused PPM output needs camera size == image size; use eray_pack_ppm");
+    if (rp->band_rows) {  // interleaved bands: aligned to the 4-row sub-blocks, inside the camera
+        if (rp->band_rows % 4 || rp->band_stride % 4 || rp->row0 % 4 || rp->band_stride < rp->band_rows)
+            return set_error(ctx, ERAY_E_INVALID_ARGUMENT,
+                             "bands: band_rows (%u), band_stride (%u) and row0 (%u) must be multiples of 4, "
+                             "band_stride >= band_rows", rp->band_rows, rp->band_stride, rp->row0);
+        if (rp->rows && band_camera_row(rp->row0, rp->band_rows, rp->band_stride, rp->rows - 1) >= H)
+            return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "bands: %u local rows reach past the camera height %u",
+                             rp->rows, H);
+    }
     const bool cull = !general && !(rp->flags & ERAY_RENDER_BRUTE_FORCE);
     if (int st = sync_scene(ctx)) return st;
     *empty = !rp->rows || !W;
     if (*empty) return ERAY_OK;
     bool known = true;
     if (cull)
-        if (int st = sync_setup(ctx, W, H, rp->row0, rp->rows, wait == SetupWait::kYes, &known)) return st;
+        if (int st = sync_setup(ctx, W, H, RowSpan{rp->row0, rp->rows, rp->band_rows, rp->band_rows ? rp->band_stride : 0u},
+                                wait == SetupWait::kYes, &known))
+            return st;
 
     FrameParams& p = *out;
     std::memset(&p, 0, sizeof p);  // padding too: the launch-plan cache compares the bytes
@@ -870,6 +892,8 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     p.img_h = rp->image_height;
     p.row0 = rp->row0;
     p.rows = rp->rows;
+    p.band_rows = rp->band_rows;
+    p.band_stride = rp->band_rows ? rp->band_stride : 0u;
     p.out_rgb = rp->out_rgb;
     p.out_ppm = rp->out_ppm;
     p.out_face = rp->out_face;
@@ -1156,7 +1180,9 @@ int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* rp, const e
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_path_all, ctx->h_path, sizeof(CamDev) * n, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipEventRecord(ctx->path_ev, ctx->stream));
     auto frame = [&](const CamDev* cam) -> int {
-        if (int st = enqueue_setup(ctx, cam, W, H, rp->row0, rp->rows)) return st;
+        if (int st = enqueue_setup(ctx, cam, W, H,
+                                   RowSpan{rp->row0, rp->rows, rp->band_rows, rp->band_rows ? rp->band_stride : 0u}))
+            return st;
         HIP_TRY(ctx, launch_frame(ctx, p));
         return ERAY_OK;
     };
@@ -1207,8 +1233,13 @@ int eray_ppm_header(uint32_t w, uint32_t h, char* buf, size_t cap, size_t* len) 
 
 }  // extern "C"
 
-// Error reporting for the other translation units of the library (comm.cpp).
+// Error reporting and the gather's staging buffer for the other translation units (comm.cpp).
 int eray_internal_error(eray_ctx* ctx, int code, const char* msg) { return set_error(ctx, code, "%s", msg); }
+void* eray_internal_staging(eray_ctx* ctx, size_t bytes) {
+    if (!ctx) return nullptr;
+    if (ensure(ctx, &ctx->d_staging, &ctx->staging_cap, bytes)) return nullptr;
+    return ctx->d_staging;
+}
 
 // Diagnostics (not part of include/eray_hip.h): the screen bins of object `index` as built for
 // the last setup — out[0] bins, out[1] entries, out[2] (face, pixel) pairs (mask bits),

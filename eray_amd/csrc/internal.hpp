@@ -136,6 +136,9 @@ struct FrameParams {
     // output
     uint32_t img_w, img_h;
     uint32_t row0, rows;
+    // interleaved row bands (multi-GPU balance): local row j is camera row
+    // row0 + (j / band_rows) * band_stride + j % band_rows; band_rows == 0: row0 + j
+    uint32_t band_rows, band_stride;
     float* out_rgb;
     uint8_t* out_ppm;
     int32_t* out_face;
@@ -181,6 +184,32 @@ struct FrameParams {
     uint32_t seed_lo, seed_hi;
 };
 
+// Camera row of rank-local row j (FrameParams::band_rows).
+__host__ __device__ inline uint32_t band_camera_row(uint32_t row0, uint32_t band_rows, uint32_t band_stride, uint32_t j) {
+    return band_rows ? row0 + (j / band_rows) * band_stride + j % band_rows : row0 + j;
+}
+// The rank-local rows [*lo, *hi] whose camera rows lie in [y0, y1] (empty: *lo > *hi); the
+// mapping is monotonic, so a camera row range is a local row range.
+__host__ __device__ inline void band_local_range(uint32_t row0, uint32_t band_rows, uint32_t band_stride, int32_t y0,
+                                                 int32_t y1, int32_t* lo, int32_t* hi) {
+    if (!band_rows) {
+        *lo = y0 - (int32_t)row0;
+        *hi = y1 - (int32_t)row0;
+        return;
+    }
+    const int64_t B = band_rows, S = band_stride, off = row0;
+    auto floordiv = [](int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); };
+    // first local row at or after camera row y0
+    int64_t i = floordiv((int64_t)y0 - off, S), w = (int64_t)y0 - off - i * S;
+    const int64_t l0 = w < B ? i * B + w : (i + 1) * B;
+    // last local row at or before camera row y1
+    i = floordiv((int64_t)y1 - off, S);
+    w = (int64_t)y1 - off - i * S;
+    const int64_t l1 = w < B ? i * B + w : i * B + B - 1;
+    *lo = (int32_t)(l0 < -1 ? -1 : (l0 > 0x7fffffff ? 0x7fffffff : l0));
+    *hi = (int32_t)(l1 < -1 ? -1 : (l1 > 0x7fffffff ? 0x7fffffff : l1));
+}
+
 // Byte offsets of the LDS scene copy: [ObjectDesc x nobj | LightDesc x nl | TriCull x n (if
 // culling) | TriHot x n | TriShade x n]; every section is a whole number of 16-B words.
 struct SceneLdsLayout {
@@ -221,6 +250,7 @@ struct SetupParams {
     CamState* state;
     uint32_t W, H;              // Camera::size
     uint32_t row0, rows;        // rendered camera rows (the merged rectangles are rank-local)
+    uint32_t band_rows, band_stride;  // interleaved bands (FrameParams), 0: rows [row0, row0 + rows)
     uint32_t* acc;              // 4 x nobj rectangle accumulators, zero between setups
     uint32_t* done;             // workgroup counter (last-workgroup finalisation), zero between setups
     uint32_t* part;             // kSetupMaxBlocks x 10: each workgroup's boundary objects' partials

@@ -678,14 +678,20 @@ __device__ __forceinline__ f3 camera_dir(const CamDev& cam, const FrameParams& p
 //    This is the frame's HBM-write floor.  Keeping it off the detail workgroups matters: their
 //    loads must not wait behind their own stores (a CDNA wave's vmcnt counts both).
 
+// camera row of rank-local row j (interleaved bands or a contiguous block)
+__device__ __forceinline__ uint32_t cam_row(const FrameParams& p, uint32_t j) {
+    return band_camera_row(p.row0, p.band_rows, p.band_stride, j);
+}
+
 __device__ __forceinline__ Bundle make_bundle(const FrameParams& p, uint32_t x0, uint32_t xe,
                                               uint32_t py0, uint32_t pye) {
     // the pixel rectangle in viewport coordinates, widened to contain every pixel's x' = x/W and
     // y' = y/H (approximate reciprocal, then 2^-20 outward; x', y' >= 0)
     const float rw = __builtin_amdgcn_rcpf((float)p.cam_w), rh = __builtin_amdgcn_rcpf((float)p.cam_h);
     const float lo = 1.0f - 0x1p-20f, hi = 1.0f + 0x1p-20f;
-    return Bundle{((float)x0 * rw) * lo, ((float)xe * rw) * hi, ((float)(p.row0 + py0) * rh) * lo,
-                  ((float)(p.row0 + pye) * rh) * hi};
+    const uint32_t y0 = cam_row(p, py0);  // (a sub-block's rows lie in one band)
+    return Bundle{((float)x0 * rw) * lo, ((float)xe * rw) * hi, ((float)y0 * rh) * lo,
+                  ((float)(y0 + (pye - py0)) * rh) * hi};
 }
 
 // Frame outputs are written once and never read back by the kernel: 16-byte buffer stores with
@@ -774,7 +780,7 @@ __device__ __forceinline__ void fill_background(const FrameParams& p, uint32_t x
 
 // the pixel rectangle of `ob` (camera rows) meets the sub-block's pixels
 __device__ __forceinline__ bool rect_meets(const ObjGeom& ob, const FrameParams& p, uint32_t wx0, uint32_t py0) {
-    const int32_t x0 = (int32_t)wx0, y0 = (int32_t)(p.row0 + py0);
+    const int32_t x0 = (int32_t)wx0, y0 = (int32_t)cam_row(p, py0);
     return ob.rect[0] <= x0 + (int32_t)kSubW - 1 && ob.rect[1] >= x0 && ob.rect[2] <= y0 + (int32_t)kBlkH - 1 &&
            ob.rect[3] >= y0;
 }
@@ -795,7 +801,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const CamDev& c
     const uint32_t px = wx0 + (lane % kSubW), ly = lane / kSubW;
     const uint32_t py = py0 + ly;
     const bool valid = active && px < p.cam_w && py < p.rows;
-    const uint32_t y = p.row0 + py;
+    const uint32_t y = cam_row(p, py);
     const Bundle bd = make_bundle(p, wx0, min(wx0 + kSubW - 1, p.cam_w - 1), py0, min(py0 + kBlkH - 1, p.rows - 1));
 
     // ---- cast_ray (engine.rs:112-216): closest object among first hits -----------
@@ -827,7 +833,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const CamDev& c
             first_hit<kCull, false>(p, sc, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull, activate, f, u,
                                     v, t);
         } else if (kCull && ob.bin_start) {  // the workgroup's four sub-blocks together
-            const uint32_t bin = ((p.row0 + py0 + kBinH - p.bin_phase) / kBinH) * p.bins_x + wx0 / kBinW;
+            const uint32_t bin = ((cam_row(p, py0) + kBinH - p.bin_phase) / kBinH) * p.bins_x + wx0 / kBinW;
             first_hit_binned(p, ob, bin, st, C, d, activate, f, u, v, t, s_bins);
         } else {
             first_hit<kCull, kLdsTiles>(p, sc, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull, activate,
@@ -1222,7 +1228,7 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
         constexpr bool kGivenRay = true;
         auto first_rays = [&]() {
             if (c0 + wave < total) locate(c0 + wave, sx0, sy0);
-            d0 = camera_dir(cam, p, (uint32_t)sx0 * kSubW + lane % kSubW, p.row0 + (uint32_t)sy0 * kBlkH + lane / kSubW);
+            d0 = camera_dir(cam, p, (uint32_t)sx0 * kSubW + lane % kSubW, cam_row(p, (uint32_t)sy0 * kBlkH + lane / kSubW));
             asm volatile("" : "+v"(d0.x), "+v"(d0.y), "+v"(d0.z));  // here, not after the barrier
         };
         auto detail = [&](const auto& sc) {

@@ -23,6 +23,30 @@ def row_block(rank: int, world: int, rows_per_rank: int) -> tuple[int, int]:
     return height - (rank + 1) * rows_per_rank, rows_per_rank
 
 
+BAND_ROWS = 4  # interleaved split: one 4-row sub-block band per turn (the finest the kernels take)
+
+
+def band_split(rank: int, world: int, height: int, band: int = BAND_ROWS) -> dict:
+    """Interleaved row bands (load balance): rank r renders camera-row bands r,
+    r + world, ... of `band` rows — wherever the scene sits, every rank gets an equal share of it.
+    Returns the eray_render_params fields (row0, rows, band_rows, band_stride) and `alloc_rows`,
+    the rows each rank's local buffers hold for the gather (rank 0's count, the largest)."""
+    if not 0 <= rank < world:
+        raise ValueError(f"rank {rank} outside world {world}")
+    if band % 4:
+        raise ValueError("bands must be a multiple of 4 rows")
+    bands, tail = divmod(height, band)
+    rows = (bands // world + (1 if rank < bands % world else 0)) * band + (tail if tail and bands % world == rank else 0)
+    rows0 = (bands // world + (1 if 0 < bands % world else 0)) * band + (tail if tail and bands % world == 0 else 0)
+    return dict(row0=rank * band, rows=rows, band_rows=band, band_stride=world * band, alloc_rows=rows0)
+
+
+def band_camera_rows(rank: int, world: int, height: int, band: int = BAND_ROWS) -> list[int]:
+    """The camera rows of rank's local rows, in order (tests)."""
+    sp = band_split(rank, world, height, band)
+    return [sp["row0"] + (j // band) * sp["band_stride"] + j % band for j in range(sp["rows"])]
+
+
 class RowGather:
     """The frame gather through the C-ABI (eray_gather_rows over an RCCL communicator made by
     eray_comm_init); `group` carries rank 0's unique id to the others (any backend)."""
@@ -35,10 +59,12 @@ class RowGather:
             dist.broadcast_object_list(uid, src=0)
         self.comm = ctx.comm_init(world, rank, uid[0])
 
-    def __call__(self, local: torch.Tensor, frame: torch.Tensor | None) -> None:
-        rows, width = local.shape[0], local.shape[1]
+    def __call__(self, local: torch.Tensor, frame: torch.Tensor | None, height: int, band_rows: int = 0) -> None:
+        """local: this rank's fused PPM rows (bands: padded to band_split's alloc_rows); frame:
+        rank 0's height x width x 3 PPM body."""
+        width = local.shape[1]
         self.ctx.gather_rows(self.comm, local.data_ptr(), frame.data_ptr() if frame is not None else None,
-                             rows, width)
+                             height, width, band_rows)
 
     def close(self) -> None:
         from . import capi
@@ -47,18 +73,32 @@ class RowGather:
             self.comm = None
 
 
-def gather_ppm_rows(local: torch.Tensor, frame: torch.Tensor | None, world: int, rank: int) -> None:
-    """Gather every rank's (rows, W, 3) uint8 PPM rows into rank 0's (world*rows, W, 3) `frame`
-    (file order).  Other ranks pass frame=None.  One collective, rank order = file order."""
-    if world == 1:
+def gather_ppm_rows(local: torch.Tensor, frame: torch.Tensor | None, world: int, rank: int,
+                    band_rows: int = 0) -> None:
+    """Gather every rank's PPM rows into rank 0's (H, W, 3) uint8 `frame` (file order) with
+    torch.distributed (the CPU tests' gloo path; GPU jobs use RowGather).  band_rows = 0: equal
+    blocks of file rows in rank order; else interleaved bands (band_split), every rank's local
+    buffer padded to alloc_rows, reordered on rank 0.  Other ranks pass frame=None."""
+    if world == 1 and not band_rows:
         if frame is not None and frame.data_ptr() != local.data_ptr():
             frame.copy_(local)
         return
-    if local.is_cuda and dist.get_backend() == "gloo":  # gloo gathers host tensors
-        host = local.cpu()
+    host = local.cpu() if local.is_cuda else local
+    if world == 1:
+        parts = [host]
+    else:
         parts = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
         dist.gather(host, parts, dst=0)
-        if rank == 0:
-            frame.copy_(torch.cat(parts, 0))
+    if rank != 0:
         return
-    dist.gather(local, list(frame.chunk(world, 0)) if rank == 0 else None, dst=0)
+    if not band_rows:
+        frame.copy_(torch.cat(parts, 0))
+        return
+    H = frame.shape[0]
+    out = torch.empty_like(frame, device="cpu")
+    for r in range(world):
+        n = band_split(r, world, H, band_rows)["rows"]
+        cams = band_camera_rows(r, world, H, band_rows)
+        for k in range(n):  # block row k = local row n - 1 - k (local file order)
+            out[H - 1 - cams[n - 1 - k]] = parts[r][k]
+    frame.copy_(out)

@@ -246,6 +246,13 @@ typedef struct eray_render_params {
     uint64_t aa_seed;               /* anti-aliasing jitter stream: Philox4x32-10 keyed by
                                        aa_seed, counter (x, y, sample, 0) — replaces the
                                        reference's OS-seeded rand::thread_rng (engine.rs:49) */
+    uint32_t band_rows;             /* 0: the rows are camera rows [row0, row0 + rows).  Else
+                                       interleaved bands (a multi-GPU rank's share): local row j
+                                       is camera row row0 + (j / band_rows) * band_stride +
+                                       j % band_rows; band_rows, band_stride and row0 multiples
+                                       of 4.  The outputs hold the local rows (out_ppm in local
+                                       file order: byte row k = local row rows - 1 - k). */
+    uint32_t band_stride;
 } eray_render_params;
 
 #define ERAY_RENDER_DEFAULT 0u
@@ -292,11 +299,19 @@ int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* params, con
 int eray_comm_unique_id(uint8_t* id /* ERAY_COMM_ID_BYTES */);
 int eray_comm_init(eray_ctx* ctx, int nranks, int rank, const uint8_t* id, void** nccl_comm);
 int eray_comm_destroy(void* nccl_comm);
-/* local: device, rows x width x 3 PPM bytes of this rank's block; frame (rank 0 only): device,
- * nranks x rows x width x 3 bytes.  Replaces the reference's single-process image write
- * (engine.rs:85-98 render_to_path -> save_as_ppm). */
-int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8_t* frame, uint32_t rows,
-                     uint32_t width);
+/* The PPM body of a height x width frame on rank 0 (frame: device, height x width x 3 bytes),
+ * from every rank's fused out_ppm rows (local: device).  band_rows == 0: rank r rendered the
+ * r-th of nranks equal blocks of file rows (camera rows [H - (r+1) h, H - r h), h = height /
+ * nranks), and the gather is a concatenation in rank order.  band_rows > 0: rank r rendered the
+ * interleaved bands r, r + nranks, ... of band_rows camera rows (eray_render_params row0 =
+ * r * band_rows, band_stride = nranks * band_rows) — equal work per rank wherever the scene
+ * sits — into a local buffer of eray_band_rows(height, band_rows, nranks, 0) rows (rank 0 has
+ * the most), and rank 0 puts the rows in file order after the collective.  Replaces the
+ * reference's single-process image write (engine.rs:85-98 render_to_path -> save_as_ppm). */
+int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8_t* frame, uint32_t height,
+                     uint32_t width, uint32_t band_rows);
+/* Camera rows of rank `rank` in the interleaved band split of a frame of `height` rows. */
+uint32_t eray_band_rows(uint32_t height, uint32_t band_rows, uint32_t nranks, uint32_t rank);
 
 /* ------------------------------------------------------------------ PPM ----------------- */
 /* Body bytes of Image<Color>::save_as_ppm for a width x height device image: rows bottom-up,

@@ -37,19 +37,43 @@ def _render_block(row0, rows):
     return np.frombuffer(body[len(header):], np.uint8).reshape(rows, W, 3).copy()
 
 
-def _worker(rank, world, port, out_path):
+def _render_rows(camera_rows):
+    """The PPM bytes of the given camera rows, in local file order (last row first), as the
+    fused out_ppm of a banded eray_render writes them."""
+    rows = [_render_block(y, 1)[0] for y in camera_rows]
+    return np.stack(rows[::-1]) if rows else np.zeros((0, W, 3), np.uint8)
+
+
+def _worker(rank, world, port, out_path, bands):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from eray_amd.dist import gather_ppm_rows
+    from eray_amd.dist import band_camera_rows, band_split, gather_ppm_rows
 
-    row0, rows = row_block(rank, world, ROWS)
-    local = torch.from_numpy(_render_block(row0, rows))
-    frame = torch.empty((world * ROWS, W, 3), dtype=torch.uint8) if rank == 0 else None
-    gather_ppm_rows(local, frame, world, rank)
+    H = world * ROWS
+    if bands:
+        sp = band_split(rank, world, H, bands)
+        local = np.zeros((sp["alloc_rows"], W, 3), np.uint8)
+        local[: sp["rows"]] = _render_rows(band_camera_rows(rank, world, H, bands))
+        local = torch.from_numpy(local)
+    else:
+        row0, rows = row_block(rank, world, ROWS)
+        local = torch.from_numpy(_render_block(row0, rows))
+    frame = torch.empty((H, W, 3), dtype=torch.uint8) if rank == 0 else None
+    gather_ppm_rows(local, frame, world, rank, band_rows=bands)
     if rank == 0:
         np.save(out_path, frame.numpy())
     dist.barrier()
     dist.destroy_process_group()
+
+
+def test_band_split_covers_every_row_once():
+    from eray_amd.dist import band_camera_rows, band_split
+    for H, N, B in ((1080, 8, 4), (4320, 8, 4), (1081, 3, 4), (10, 3, 4), (2160, 4, 8)):
+        rows = [y for r in range(N) for y in band_camera_rows(r, N, H, B)]
+        assert sorted(rows) == list(range(H)), (H, N, B)
+        assert max(band_split(r, N, H, B)["rows"] for r in range(N)) == band_split(0, N, H, B)["alloc_rows"]
+    with pytest.raises(ValueError):
+        band_split(0, 2, 100, 6)
 
 
 def test_row_block_partition():
@@ -59,9 +83,12 @@ def test_row_block_partition():
         row_block(2, 2, 10)
 
 
-def test_two_rank_gather_equals_single_frame(tmp_path):
+@pytest.mark.parametrize("bands", [0, 4, 8])
+def test_two_rank_gather_equals_single_frame(tmp_path, bands):
+    """Contiguous blocks and interleaved bands (band_split: every rank an equal share of the
+    cube's rows) gather into the single-process frame."""
     out = str(tmp_path / "frame.npy")
-    mp.start_processes(_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(2, _free_port(), out, bands), nprocs=2, join=True, start_method="spawn")
     got = np.load(out)
     want = _render_block(0, 2 * ROWS)
     assert got.shape == want.shape and np.array_equal(got, want)

@@ -17,6 +17,7 @@ import numpy as np
 import pytest
 
 from eray_amd import capi, dist, meshgen
+from eray_amd.dist import band_camera_rows, band_split
 from eray_amd.frame import MainScene
 from tests.helpers import assert_bit_equal
 
@@ -77,6 +78,39 @@ def _tiles_concatenate(fr, W, H, world, full):
     assert np.array_equal(np.concatenate(got_ppm, 0), ppm), "gathered PPM body != full frame"
 
 
+def _bands_assemble(gpu, W, H, world, full, band=dist.BAND_ROWS):
+    """The interleaved-band split (dist.band_split): every rank's bands rendered with
+    eray_render(row0, rows, band_rows, band_stride) must hold the full frame's pixels at its camera
+    rows, and rank 0's reordering step of the banded gather (eray_debug_unband over the ranks'
+    padded PPM blocks, as ncclGather leaves them) must give the full frame's PPM body."""
+    rgb, face, ppm = full
+    alloc = band_split(0, world, H, band)["alloc_rows"]
+    staging = gpu.empty((world * alloc, W, 3), np.uint8)
+    out = Frame(gpu, W, alloc)
+    frame = gpu.empty((H, W, 3), np.uint8)
+    try:
+        gpu.memset(staging.ptr, 0, staging.nbytes)
+        for r in range(world):
+            sp = band_split(r, world, H, band)
+            n = sp["rows"]
+            for a, v in ((out.rgb, 0), (out.face, 0x7F), (out.ppm, 0)):
+                gpu.memset(a.ptr, v, a.nbytes)
+            gpu.render(W, H, row0=sp["row0"], rows=n, band_rows=sp["band_rows"], band_stride=sp["band_stride"],
+                       out_rgb=out.rgb.ptr, out_face=out.face.ptr, out_ppm=out.ppm.ptr)
+            cams = np.array(band_camera_rows(r, world, H, band))
+            t_rgb = out.rgb.numpy().reshape(-1)[: 3 * n * W].reshape(n, W, 3)
+            t_face = out.face.numpy().reshape(-1)[: n * W].reshape(n, W)
+            assert np.array_equal(t_face, face[cams]), f"band rank {r} faces"
+            assert_bit_equal(t_rgb, rgb[cams], f"band rank {r} rgb")
+            gpu.copy_to_device(staging.ptr + r * alloc * W * 3, out.ppm.numpy().reshape(-1)[: 3 * n * W])
+        assert capi.lib().eray_debug_unband(gpu.handle, staging.ptr, frame.ptr, H, W, band, world) == 0
+        assert np.array_equal(frame.numpy(), ppm), "banded gather != full frame PPM"
+    finally:
+        out.free()
+        staging.free()
+        frame.free()
+
+
 def test_c3_full_frame_binned_equals_brute_force(gpu):
     """C3 at 1920x1080 (69,451-face stand-in): the binned frame equals the brute-force scan over the
     whole frame, bit for bit, for both material paths."""
@@ -118,6 +152,7 @@ def test_c4_cube_4k_matches_oracle_and_row_tiles(gpu, oracle, cube):
         assert_bit_equal(rgb, ref, "c4 frame vs oracle")
         assert int((face >= 0).sum()) == stats["hit_pixels"] == g["hit_pixels"]
         _tiles_concatenate(fr, W, H, 4, full)
+        _bands_assemble(gpu, W, H, 4, full)
     finally:
         fr.free()
         sc.close()
@@ -147,6 +182,7 @@ def test_c5_8k_1m_tiles_spans_and_brute_force(gpu, synth1m):
             assert np.array_equal(face[y, x0:x0 + cols], fx[f"face{k}"]), f"span {k} faces"
             assert_bit_equal(rgb[y, x0:x0 + cols], fx[f"rgb{k}"], f"span {k} ({y}, {x0}+{cols})")
         _tiles_concatenate(fr, W, H, 8, full)
+        _bands_assemble(gpu, W, H, 8, full)
         boundaries = [540 * r for r in range(1, 8)]
         for y0, n in [(b - 2, 4) for b in boundaries] + [(2156, 8), (2161, 3), (1763, 5)]:
             for flags in (capi.RENDER_DEFAULT, capi.RENDER_BRUTE_FORCE):  # binned at row phase y0 % 4
