@@ -28,8 +28,8 @@ SOURCES = ["render.hip", "setup.hip", "trace.hip", "bins.hip", "shaderlib.hip", 
 ARCH = "gfx950"
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
             f"--offload-arch={ARCH}", "-I" + os.path.join(ROOT, "include"),
-            # the first 14 kernel-argument dwords arrive in SGPRs (frame_kernel's FrameHot)
-            "-mllvm", "-amdgpu-kernarg-preload-count=14"]
+            # the first 15 kernel-argument dwords arrive in SGPRs (frame_kernel's FrameHot + band word)
+            "-mllvm", "-amdgpu-kernarg-preload-count=15"]
 
 
 def hipcc() -> str:

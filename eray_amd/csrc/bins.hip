@@ -251,7 +251,8 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(const uint32_t* _
 // rectangle reaches it.
 __global__ void __launch_bounds__(kBinWG) detail_flags_kernel(const ObjectDesc* __restrict__ objs, uint32_t nobj,
                                                               uint32_t cam_w, uint32_t row0, uint32_t rows,
-                                                              uint32_t band_rows, uint32_t band_stride,
+                                                              uint32_t band_shift, uint32_t band_mask,
+                                                              uint32_t band_stride,
                                                               uint32_t bins_x, uint32_t phase, uint32_t tiles_x,
                                                               uint32_t n, uint8_t* __restrict__ flags,
                                                               uint32_t* __restrict__ packed, uint8_t* __restrict__ occ) {
@@ -261,8 +262,8 @@ __global__ void __launch_bounds__(kBinWG) detail_flags_kernel(const ObjectDesc* 
     bool hit = false;
     if (s < n && sx * kBinW < cam_w) {
         const int32_t x0 = (int32_t)(sx * kBinW), x1 = x0 + (int32_t)kBinW - 1;
-        // the sub-block's camera rows (one band: band_rows is a multiple of kBinH)
-        const int32_t y0 = (int32_t)band_camera_row(row0, band_rows, band_stride, sy * kBinH);
+        // the sub-block's camera rows (one band: bands are multiples of kBinH rows)
+        const int32_t y0 = (int32_t)band_camera_row(row0, band_shift, band_mask, band_stride, sy * kBinH);
         const int32_t y1 = y0 + (int32_t)min(kBinH, rows - sy * kBinH) - 1;
         for (uint32_t oi = 0; oi < nobj && !hit; ++oi) {
             const ObjGeom& g = objs[oi].g;
@@ -377,7 +378,7 @@ hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tile
     if (!b.nsub) return hipSuccess;
     const uint32_t n = (uint32_t)b.nsub;
     detail_flags_kernel<<<(n + kBinWG - 1) / kBinWG, kBinWG, 0, s>>>(sp.objs, sp.nobj, sp.W, sp.row0, sp.rows,
-                                                                    sp.band_rows, sp.band_stride,
+                                                                    sp.band_shift, sp.band_mask, sp.band_stride,
                                                                     b.bins_x, b.phase, tiles_x, n, b.dflags,
                                                                     b.dpacked, b.docc);
     if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -375,8 +375,15 @@ uint32_t binned_objects(const eray_ctx* ctx) {
 // The rendered rows of a call: camera rows [row0, row0 + rows), or rows local rows of
 // interleaved bands (eray_render_params::band_rows).
 struct RowSpan {
-    uint32_t row0, rows, band_rows, band_stride;
+    uint32_t row0, rows, band_shift, band_mask, band_stride;
 };
+// eray_render_params' band fields as FrameParams encodes them (contiguous: shift 31)
+RowSpan row_span(const eray_render_params* rp) {
+    if (!rp->band_rows) return RowSpan{rp->row0, rp->rows, 31u, 0x7fffffffu, 0u};
+    uint32_t shift = 0;
+    while ((1u << shift) < rp->band_rows) ++shift;
+    return RowSpan{rp->row0, rp->rows, shift, rp->band_rows - 1u, rp->band_stride};
+}
 
 int ensure_bins(eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs) {
     const uint32_t row0 = rs.row0, rows = rs.rows;
@@ -426,7 +433,8 @@ int enqueue_setup(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint32_t H,
     sp.H = H;
     sp.row0 = rs.row0;
     sp.rows = rs.rows;
-    sp.band_rows = rs.band_rows;
+    sp.band_shift = rs.band_shift;
+    sp.band_mask = rs.band_mask;
     sp.band_stride = rs.band_stride;
     // [done counter | kSetupMaxBlocks x 10 partials | 4 x nobj accumulators]: the counter and the
     // accumulators are zero between setups whatever the object count (partials are rewritten)
@@ -484,7 +492,7 @@ int sync_setup(eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs, bool wa
         if (int st = bins_ready()) return st;
         std::vector<uint64_t> key(sizeof(eray_camera) / 4 + 4);
         std::memcpy(key.data(), &ctx->camera, sizeof(eray_camera));
-        key[key.size() - 4] = ((uint64_t)rs.row0 << 32) | rs.band_rows;
+        key[key.size() - 4] = ((uint64_t)rs.row0 << 32) | rs.band_shift;
         key[key.size() - 3] = ((uint64_t)rs.rows << 32) | rs.band_stride;
         key[key.size() - 2] = ctx->scene_gen;
         key[key.size() - 1] = ((uint64_t)W << 32) | H;
@@ -860,11 +868,14 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
         return set_error(ctx, ERAY_E_INVALID_ARGUMENT,
                          "fused PPM output needs camera size == image size; use eray_pack_ppm");
     if (rp->band_rows) {  // interleaved bands: aligned to the 4-row sub-blocks, inside the camera
-        if (rp->band_rows % 4 || rp->band_stride % 4 || rp->row0 % 4 || rp->band_stride < rp->band_rows)
+        if (rp->band_rows % 4 || (rp->band_rows & (rp->band_rows - 1)) || rp->band_stride % 4 || rp->row0 % 4 ||
+            rp->band_stride < rp->band_rows)
             return set_error(ctx, ERAY_E_INVALID_ARGUMENT,
-                             "bands: band_rows (%u), band_stride (%u) and row0 (%u) must be multiples of 4, "
-                             "band_stride >= band_rows", rp->band_rows, rp->band_stride, rp->row0);
-        if (rp->rows && band_camera_row(rp->row0, rp->band_rows, rp->band_stride, rp->rows - 1) >= H)
+                             "bands: band_rows (%u) must be a power of two >= 4, band_stride (%u) and row0 (%u) "
+                             "multiples of 4, band_stride >= band_rows", rp->band_rows, rp->band_stride, rp->row0);
+        const RowSpan rs = row_span(rp);
+        if (rp->rows && (uint64_t)rp->row0 + (uint64_t)((rp->rows - 1) >> rs.band_shift) * rp->band_stride +
+                                ((rp->rows - 1) & rs.band_mask) >= H)
             return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "bands: %u local rows reach past the camera height %u",
                              rp->rows, H);
     }
@@ -874,7 +885,7 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     if (*empty) return ERAY_OK;
     bool known = true;
     if (cull)
-        if (int st = sync_setup(ctx, W, H, RowSpan{rp->row0, rp->rows, rp->band_rows, rp->band_rows ? rp->band_stride : 0u},
+        if (int st = sync_setup(ctx, W, H, row_span(rp),
                                 wait == SetupWait::kYes, &known))
             return st;
 
@@ -892,8 +903,10 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     p.img_h = rp->image_height;
     p.row0 = rp->row0;
     p.rows = rp->rows;
-    p.band_rows = rp->band_rows;
-    p.band_stride = rp->band_rows ? rp->band_stride : 0u;
+    const RowSpan span = row_span(rp);
+    p.band_shift = span.band_shift;
+    p.band_mask = span.band_mask;
+    p.band_stride = span.band_stride;
     p.out_rgb = rp->out_rgb;
     p.out_ppm = rp->out_ppm;
     p.out_face = rp->out_face;
@@ -1181,7 +1194,7 @@ int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* rp, const e
     HIP_TRY(ctx, hipEventRecord(ctx->path_ev, ctx->stream));
     auto frame = [&](const CamDev* cam) -> int {
         if (int st = enqueue_setup(ctx, cam, W, H,
-                                   RowSpan{rp->row0, rp->rows, rp->band_rows, rp->band_rows ? rp->band_stride : 0u}))
+                                   row_span(rp)))
             return st;
         HIP_TRY(ctx, launch_frame(ctx, p));
         return ERAY_OK;

@@ -137,8 +137,9 @@ struct FrameParams {
     uint32_t img_w, img_h;
     uint32_t row0, rows;
     // interleaved row bands (multi-GPU balance): local row j is camera row
-    // row0 + (j / band_rows) * band_stride + j % band_rows; band_rows == 0: row0 + j
-    uint32_t band_rows, band_stride;
+    // row0 + (j >> band_shift) * band_stride + (j & band_mask) (band_rows = 1 << band_shift, a
+    // power of two); a contiguous block is band_shift = 31, band_mask = 0x7fffffff (row0 + j)
+    uint32_t band_shift, band_mask, band_stride;
     float* out_rgb;
     uint8_t* out_ppm;
     int32_t* out_face;
@@ -184,20 +185,22 @@ struct FrameParams {
     uint32_t seed_lo, seed_hi;
 };
 
-// Camera row of rank-local row j (FrameParams::band_rows).
-__host__ __device__ inline uint32_t band_camera_row(uint32_t row0, uint32_t band_rows, uint32_t band_stride, uint32_t j) {
-    return band_rows ? row0 + (j / band_rows) * band_stride + j % band_rows : row0 + j;
+// Camera row of rank-local row j (FrameParams::band_shift; shifts and masks: no division in the
+// kernels' per-pixel paths).
+__host__ __device__ inline uint32_t band_camera_row(uint32_t row0, uint32_t band_shift, uint32_t band_mask,
+                                                    uint32_t band_stride, uint32_t j) {
+    return row0 + (j >> band_shift) * band_stride + (j & band_mask);
 }
 // The rank-local rows [*lo, *hi] whose camera rows lie in [y0, y1] (empty: *lo > *hi); the
 // mapping is monotonic, so a camera row range is a local row range.
-__host__ __device__ inline void band_local_range(uint32_t row0, uint32_t band_rows, uint32_t band_stride, int32_t y0,
+__host__ __device__ inline void band_local_range(uint32_t row0, uint32_t band_shift, uint32_t band_stride, int32_t y0,
                                                  int32_t y1, int32_t* lo, int32_t* hi) {
-    if (!band_rows) {
+    if (band_shift >= 31) {
         *lo = y0 - (int32_t)row0;
         *hi = y1 - (int32_t)row0;
         return;
     }
-    const int64_t B = band_rows, S = band_stride, off = row0;
+    const int64_t B = (int64_t)1 << band_shift, S = band_stride, off = row0;
     auto floordiv = [](int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); };
     // first local row at or after camera row y0
     int64_t i = floordiv((int64_t)y0 - off, S), w = (int64_t)y0 - off - i * S;
@@ -250,7 +253,7 @@ struct SetupParams {
     CamState* state;
     uint32_t W, H;              // Camera::size
     uint32_t row0, rows;        // rendered camera rows (the merged rectangles are rank-local)
-    uint32_t band_rows, band_stride;  // interleaved bands (FrameParams), 0: rows [row0, row0 + rows)
+    uint32_t band_shift, band_mask, band_stride;  // interleaved bands (FrameParams)
     uint32_t* acc;              // 4 x nobj rectangle accumulators, zero between setups
     uint32_t* done;             // workgroup counter (last-workgroup finalisation), zero between setups
     uint32_t* part;             // kSetupMaxBlocks x 10: each workgroup's boundary objects' partials

@@ -39,8 +39,6 @@ using namespace eray::dev;
 
 constexpr int kWG = 256;
 constexpr int kTriTile = 256;
-// frame_kernel's h_total_sub in device-camera mode: read the count from CamState
-constexpr uint32_t kDeviceCount = 0xffffffffu;
 
 // Scene descriptors and triangle records are read-only for the whole frame: reading them
 // through the constant address space lets wave-uniform reads become scalar (s_load) loads.
@@ -646,8 +644,9 @@ __device__ const float g_texel_dummy[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 
 // The frame's camera: the kernel arguments, or the setup kernel's copy in device-camera mode
 // (FrameParams::cam_state; wave-uniform, scalar loads).
+template <bool kDev>
 __device__ __forceinline__ CamDev frame_camera(const FrameParams& p) {
-    if (p.cam_state) return load_const(&p.cam_state->cam, 0);
+    if (kDev) return load_const(&p.cam_state->cam, 0);
     return CamDev{p.cx, p.cy, p.cz, p.ratio, p.z_dist, {0u, 0u, 0u}};
 }
 
@@ -678,18 +677,22 @@ __device__ __forceinline__ f3 camera_dir(const CamDev& cam, const FrameParams& p
 //    This is the frame's HBM-write floor.  Keeping it off the detail workgroups matters: their
 //    loads must not wait behind their own stores (a CDNA wave's vmcnt counts both).
 
-// camera row of rank-local row j (interleaved bands or a contiguous block)
-__device__ __forceinline__ uint32_t cam_row(const FrameParams& p, uint32_t j) {
-    return band_camera_row(p.row0, p.band_rows, p.band_stride, j);
+// Rank-local row -> camera row (interleaved bands or a contiguous block), from the frame kernel's
+// preloaded band word (h_band: shift | stride << 5) and row0.
+struct RowMap {
+    uint32_t row0, shift, stride;
+};
+__device__ __forceinline__ uint32_t cam_row(const RowMap& m, uint32_t j) {
+    return band_camera_row(m.row0, m.shift, 0xffffffffu >> (32u - m.shift), m.stride, j);
 }
 
-__device__ __forceinline__ Bundle make_bundle(const FrameParams& p, uint32_t x0, uint32_t xe,
+__device__ __forceinline__ Bundle make_bundle(const FrameParams& p, const RowMap& rm, uint32_t x0, uint32_t xe,
                                               uint32_t py0, uint32_t pye) {
     // the pixel rectangle in viewport coordinates, widened to contain every pixel's x' = x/W and
     // y' = y/H (approximate reciprocal, then 2^-20 outward; x', y' >= 0)
     const float rw = __builtin_amdgcn_rcpf((float)p.cam_w), rh = __builtin_amdgcn_rcpf((float)p.cam_h);
     const float lo = 1.0f - 0x1p-20f, hi = 1.0f + 0x1p-20f;
-    const uint32_t y0 = cam_row(p, py0);  // (a sub-block's rows lie in one band)
+    const uint32_t y0 = cam_row(rm, py0);  // (a sub-block's rows lie in one band)
     return Bundle{((float)x0 * rw) * lo, ((float)xe * rw) * hi, ((float)y0 * rh) * lo,
                   ((float)(y0 + (pye - py0)) * rh) * hi};
 }
@@ -779,8 +782,8 @@ __device__ __forceinline__ void fill_background(const FrameParams& p, uint32_t x
 }
 
 // the pixel rectangle of `ob` (camera rows) meets the sub-block's pixels
-__device__ __forceinline__ bool rect_meets(const ObjGeom& ob, const FrameParams& p, uint32_t wx0, uint32_t py0) {
-    const int32_t x0 = (int32_t)wx0, y0 = (int32_t)cam_row(p, py0);
+__device__ __forceinline__ bool rect_meets(const ObjGeom& ob, const RowMap& rm, uint32_t wx0, uint32_t py0) {
+    const int32_t x0 = (int32_t)wx0, y0 = (int32_t)cam_row(rm, py0);
     return ob.rect[0] <= x0 + (int32_t)kSubW - 1 && ob.rect[1] >= x0 && ob.rect[2] <= y0 + (int32_t)kBlkH - 1 &&
            ob.rect[3] >= y0;
 }
@@ -792,7 +795,8 @@ __device__ __forceinline__ bool rect_meets(const ObjGeom& ob, const FrameParams&
 // without them carries none of their code or registers.
 constexpr int kMatSpecPow = 1, kMatExample = 2;
 template <bool kCull, bool kLdsTiles, int kMat, typename Scene>
-__device__ __forceinline__ void render_sub(const FrameParams& p, const CamDev& cam, const Scene& sc, uint32_t wx0, uint32_t py0,
+__device__ __forceinline__ void render_sub(const FrameParams& p, const CamDev& cam, const RowMap& rm, const Scene& sc,
+                                           uint32_t wx0, uint32_t py0,
                                            bool active, TriHot* s_hot, TriCull* s_cull, char* s_bins, float4* s_rgb,
                                            uint32_t* s_ppm, bool aligned, const f3* given_d = nullptr) {
     constexpr bool kSpecPow = (kMat & kMatSpecPow) != 0, kExample = (kMat & kMatExample) != 0;
@@ -801,8 +805,8 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const CamDev& c
     const uint32_t px = wx0 + (lane % kSubW), ly = lane / kSubW;
     const uint32_t py = py0 + ly;
     const bool valid = active && px < p.cam_w && py < p.rows;
-    const uint32_t y = cam_row(p, py);
-    const Bundle bd = make_bundle(p, wx0, min(wx0 + kSubW - 1, p.cam_w - 1), py0, min(py0 + kBlkH - 1, p.rows - 1));
+    const uint32_t y = cam_row(rm, py);
+    const Bundle bd = make_bundle(p, rm, wx0, min(wx0 + kSubW - 1, p.cam_w - 1), py0, min(py0 + kBlkH - 1, p.rows - 1));
 
     // ---- cast_ray (engine.rs:112-216): closest object among first hits -----------
     f3 d = given_d ? *given_d : mk3(0.0f, 0.0f, 0.0f);  // the camera ray, when the caller has it
@@ -816,7 +820,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const CamDev& c
         const bool direct = !kLdsTiles || ob.tri_count <= kDirectMax;
         // outside the object's pixel rectangle no primary ray can hit it (only where skipping
         // keeps the workgroup's barriers uniform)
-        if (kCull && direct && !rect_meets(ob, p, wx0, py0)) continue;
+        if (kCull && direct && !rect_meets(ob, rm, wx0, py0)) continue;
         auto activate = [&]() {
             if (!ray_ready) {
                 uint32_t pxo = px, yo = y;  // opaque: keep ray generation on this path
@@ -833,7 +837,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const CamDev& c
             first_hit<kCull, false>(p, sc, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull, activate, f, u,
                                     v, t);
         } else if (kCull && ob.bin_start) {  // the workgroup's four sub-blocks together
-            const uint32_t bin = ((cam_row(p, py0) + kBinH - p.bin_phase) / kBinH) * p.bins_x + wx0 / kBinW;
+            const uint32_t bin = ((cam_row(rm, py0) + kBinH - p.bin_phase) / kBinH) * p.bins_x + wx0 / kBinW;
             first_hit_binned(p, ob, bin, st, C, d, activate, f, u, v, t, s_bins);
         } else {
             first_hit<kCull, kLdsTiles>(p, sc, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull, activate,
@@ -1084,12 +1088,14 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const CamDev& c
 struct SubRect {  // sub-block coordinates (x in kSubW columns, y in kBlkH local rows), inclusive
     int32_t sx0, sx1, sy0, sy1;
 };
+template <bool kDev>
 __device__ __forceinline__ SubRect frame_rect(const FrameParams& p, uint32_t k) {
-    if (p.cam_state) return load_const(reinterpret_cast<const SubRect*>(p.cam_state->rects), k);
+    if (kDev) return load_const(reinterpret_cast<const SubRect*>(p.cam_state->rects), k);
     return SubRect{p.rects[k][0], p.rects[k][1], p.rects[k][2], p.rects[k][3]};
 }
+template <bool kDev>
 __device__ __forceinline__ uint32_t frame_nrect(const FrameParams& p) {
-    return p.cam_state ? load_const(&p.cam_state->nrect, 0) : p.nrect;
+    return kDev ? load_const(&p.cam_state->nrect, 0) : p.nrect;
 }
 __device__ __forceinline__ bool inside(const SubRect& r, int32_t sx, int32_t sy) {
     return sx >= r.sx0 && sx <= r.sx1 && sy >= r.sy0 && sy <= r.sy1;
@@ -1097,6 +1103,7 @@ __device__ __forceinline__ bool inside(const SubRect& r, int32_t sx, int32_t sy)
 
 // The background of the non-detail sub-blocks: fill workgroup f of nf strides over the 64 x 4
 // blocks (shared by the frame kernel's fill roles and fill_kernel).
+template <bool kDev>
 __device__ __forceinline__ void fill_blocks(const FrameParams& p, uint32_t f, uint32_t nf, uint32_t wave,
                                             uint32_t lane, bool aligned) {
     constexpr uint32_t nwaves = kWG / 64;
@@ -1104,7 +1111,7 @@ __device__ __forceinline__ void fill_blocks(const FrameParams& p, uint32_t f, ui
     const uint32_t fstride = nf * nwaves;
     uint32_t occ = 0;  // detail list: lane i holds the occupancy of this wave's i-th next block
     uint32_t it = 0;
-    const uint32_t nrect = p.detail_occ ? 0u : frame_nrect(p);
+    const uint32_t nrect = p.detail_occ ? 0u : frame_nrect<kDev>(p);
     // block coordinates advance incrementally (no integer division per block)
     const uint32_t first = wave * nf + f, step_y = fstride / p.tiles_x, step_x = fstride - step_y * p.tiles_x;
     uint32_t by = first / p.tiles_x, bx = first - by * p.tiles_x;
@@ -1126,7 +1133,7 @@ __device__ __forceinline__ void fill_blocks(const FrameParams& p, uint32_t f, ui
             mask = (uint32_t)__builtin_amdgcn_readlane((int)occ, (int)(it & 63u));
         }
         for (uint32_t k = 0; k < nrect; ++k) {
-            const SubRect r = frame_rect(p, k);
+            const SubRect r = frame_rect<kDev>(p, k);
             if ((int32_t)by < r.sy0 || (int32_t)by > r.sy1) continue;
 #pragma unroll
             for (int32_t i = 0; i < 4; ++i) {
@@ -1148,11 +1155,11 @@ __device__ __forceinline__ void fill_blocks(const FrameParams& p, uint32_t f, ui
 // are VALU-issue bound and a second detail wave per SIMD doubles the issue slots (one wave alone
 // issues a VALU instruction every 4 cycles, the SIMD every 2); below one round the spills only
 // lengthen each wave's chain.
-template <bool kCull, bool kLdsTiles, int kMat, bool kLdsScene, bool kDense = false>
+template <bool kCull, bool kLdsTiles, int kMat, bool kLdsScene, bool kDense = false, bool kDev = false>
 __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && !kDense) ? 1 : 3)  // 3 workgroups per CU where that fits
     frame_kernel(const ObjectDesc* h_objects, const LightDesc* h_lights, const TriCull* h_cull, const TriHot* h_tris,
                  const TriShade* h_shade, uint32_t h_counts, uint32_t h_total_tris, uint32_t h_total_sub,
-                 uint32_t h_roles, FrameParams p) {
+                 uint32_t h_roles, uint32_t h_band, FrameParams p) {
     // h_roles (a preloaded argument, see frame_roles): the grid size, the detail workgroups and
     // the role flags, so the role decision — and the scene preload behind it — does not wait for
     // a kernel-argument load from memory
@@ -1177,11 +1184,8 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     const bool aligned = p.aligned != 0;  // (a kernel-argument read where it is used)
     // detail sub-blocks (device-camera mode: counted by the setup kernels, and the small-scene
     // fill reservation chosen from that count as launch_frame_kernel does from the host's)
-    // (h_total_sub == kDeviceCount: device-camera mode, decided from a preloaded argument so the
-    // args-mode role decision waits for no kernel-argument load)
-    const bool dev_count = hot.total_sub == kDeviceCount;
-    const uint32_t total = dev_count ? load_const(&p.cam_state->total_sub, 0) : hot.total_sub;
-    if (dev_count && p.detail_wgs_alt && total > detail_wgs * nwaves) {
+    const uint32_t total = kDev ? load_const(&p.cam_state->total_sub, 0) : hot.total_sub;
+    if (kDev && p.detail_wgs_alt && total > detail_wgs * nwaves) {
         detail_wgs = p.detail_wgs_alt;
         fill_first = true;
     }
@@ -1198,8 +1202,9 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
 
     // ---- detail sub-blocks -------------------------------------------------------------------
     if (bid < nd) {
-        const uint32_t nrect = p.detail_list ? 0u : frame_nrect(p);
-        const CamDev cam = frame_camera(p);
+        const uint32_t nrect = p.detail_list ? 0u : frame_nrect<kDev>(p);
+        const CamDev cam = frame_camera<kDev>(p);
+        const RowMap rm{p.row0, h_band & 31u, h_band >> 5};
         // detail sub-block j (enumeration order) -> sub-block coordinates
         auto locate = [&](uint32_t j, int32_t& sx, int32_t& sy) {
             if (p.detail_list) {
@@ -1209,7 +1214,7 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
                 return;
             }
             for (uint32_t k = 0; k < nrect; ++k) {  // the rectangles are disjoint (setup): by area
-                const SubRect r = frame_rect(p, k);
+                const SubRect r = frame_rect<kDev>(p, k);
                 const uint32_t w = (uint32_t)(r.sx1 - r.sx0 + 1);
                 const uint32_t a = w * (uint32_t)(r.sy1 - r.sy0 + 1);
                 if (j < a) {
@@ -1228,7 +1233,7 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
         constexpr bool kGivenRay = true;
         auto first_rays = [&]() {
             if (c0 + wave < total) locate(c0 + wave, sx0, sy0);
-            d0 = camera_dir(cam, p, (uint32_t)sx0 * kSubW + lane % kSubW, cam_row(p, (uint32_t)sy0 * kBlkH + lane / kSubW));
+            d0 = camera_dir(cam, p, (uint32_t)sx0 * kSubW + lane % kSubW, cam_row(rm, (uint32_t)sy0 * kBlkH + lane / kSubW));
             asm volatile("" : "+v"(d0.x), "+v"(d0.y), "+v"(d0.z));  // here, not after the barrier
         };
         auto detail = [&](const auto& sc) {
@@ -1237,7 +1242,7 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
                 const bool active = j < total;
                 int32_t sx = sx0, sy = sy0;
                 if (c != c0 && active) locate(j, sx, sy);
-                render_sub<kCull, kLdsTiles, kMat>(p, cam, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH, active,
+                render_sub<kCull, kLdsTiles, kMat>(p, cam, rm, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH, active,
                                                        s_hot, s_cull, s_bins, s_rgb, s_ppm, aligned,
                                                        (kGivenRay && c == c0) ? &d0 : nullptr);
             }
@@ -1260,14 +1265,15 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     if (separate_fill) return;  // fill_kernel writes the background beside this launch
     const uint32_t nf = nd < grid ? grid - nd : grid;  // filling workgroups
     const uint32_t f = nd < grid ? bid - nd : bid;
-    fill_blocks(p, f, nf, wave, lane, aligned);
+    fill_blocks<kDev>(p, f, nf, wave, lane, aligned);
 }
 
 // The background alone, beside a detail-only frame kernel on another stream (FrameParams::
 // separate_fill): small workgroups that hold few registers, so the fill waves do not take the
 // register budget of the large-mesh detail build.
+template <bool kDev>
 __global__ void __launch_bounds__(kWG) fill_kernel(FrameParams p) {
-    fill_blocks(p, blockIdx.x, gridDim.x, threadIdx.x >> 6, threadIdx.x & 63, p.aligned != 0);
+    fill_blocks<kDev>(p, blockIdx.x, gridDim.x, threadIdx.x >> 6, threadIdx.x & 63, p.aligned != 0);
 }
 
 // Image<Color>::save_as_ppm body: byte row k = image row h-1-k.
@@ -1303,6 +1309,9 @@ uint32_t frame_roles(uint32_t grid, const FrameParams& q) {
            ((q.separate_fill ? 1u : 0u) << 31);
 }
 
+// frame_kernel's h_band: the band shift and stride of the row mapping in one preloaded dword
+uint32_t band_word(const FrameParams& q) { return (q.band_shift & 31u) | (q.band_stride << 5); }
+
 uint32_t device_cus() {
     static const uint32_t cus = [] {  // (thread-safe initialisation)
         int dev = 0, n = 0;
@@ -1314,7 +1323,7 @@ uint32_t device_cus() {
     return cus;
 }
 
-template <bool C, bool L, int M, bool K, bool D = false>
+template <bool C, bool L, int M, bool K, bool D = false, bool V = false>
 hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, const LaunchCtx& lc, hipStream_t s) {
     static std::mutex mu;  // resident workgroups per CU of this build, per dynamic LDS size
     static int per_cu = -1;
@@ -1323,7 +1332,7 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
     {
         std::lock_guard<std::mutex> lock(mu);
         if (per_cu < 0 || per_cu_dyn != dyn) {
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, frame_kernel<C, L, M, K, D>, kWG, dyn) !=
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, frame_kernel<C, L, M, K, D, V>, kWG, dyn) !=
                     hipSuccess ||
                 per_cu <= 0)
                 per_cu = 1;
@@ -1382,31 +1391,29 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
             hipError_t e;
             if ((e = hipEventRecord(lc.fork, s)) != hipSuccess || (e = hipStreamWaitEvent(lc.side, lc.fork, 0)) != hipSuccess)
                 return e;
-            frame_kernel<C, L, M, K, D><<<dgrid, kWG, dyn, s>>>(q.objects, q.lights, q.cull, q.tris, q.shade,
+            frame_kernel<C, L, M, K, D, V><<<dgrid, kWG, dyn, s>>>(q.objects, q.lights, q.cull, q.tris, q.shade,
                                                              q.nobj | (q.nlights << 16), q.total_tris,
-                                                             q.cam_state ? kDeviceCount : q.total_sub,
-                                                             frame_roles(dgrid, q), q);
+                                                             q.total_sub, frame_roles(dgrid, q), band_word(q), q);
             if ((e = hipGetLastError()) != hipSuccess) return e;
-            fill_kernel<<<fgrid, kWG, 0, lc.side>>>(q);
+            fill_kernel<V><<<fgrid, kWG, 0, lc.side>>>(q);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if ((e = hipEventRecord(lc.join, lc.side)) != hipSuccess) return e;
             return hipStreamWaitEvent(s, lc.join, 0);
         }
     }
-    frame_kernel<C, L, M, K, D><<<grid, kWG, dyn, s>>>(q.objects, q.lights, q.cull, q.tris, q.shade,
+    frame_kernel<C, L, M, K, D, V><<<grid, kWG, dyn, s>>>(q.objects, q.lights, q.cull, q.tris, q.shade,
                                                     q.nobj | (q.nlights << 16), q.total_tris,
-                                                             q.cam_state ? kDeviceCount : q.total_sub,
-                                                    frame_roles(grid, q), q);
+                                                    q.total_sub, frame_roles(grid, q), band_word(q), q);
     return hipGetLastError();
 }
 
-template <bool C, int M>
+template <bool C, int M, bool V>
 hipError_t launch_frame_cs(const FrameParams& p, uint32_t want, const LaunchCtx& lc, hipStream_t s) {
     // small scenes are preloaded into LDS whole (no object then needs the LDS tiles); otherwise
     // everything is read from the device arrays
     if (p.lds_scene) {
         const size_t dyn = scene_lds_layout(p.nobj, p.nlights, p.total_tris, C).bytes;
-        return launch_frame_kernel<C, false, M, true>(p, want, dyn, lc, s);
+        return launch_frame_kernel<C, false, M, true, false, V>(p, want, dyn, lc, s);
     }
     if (p.max_object_tris > kDirectMax) {
         if constexpr (!(M & kMatSpecPow)) {
@@ -1416,11 +1423,11 @@ hipError_t launch_frame_cs(const FrameParams& p, uint32_t want, const LaunchCtx&
             const bool dense = (p.launch_flags & kLaunchDense)     ? true
                                : (p.launch_flags & kLaunchNoDense) ? false
                                                                    : p.total_sub > device_cus() * (kWG / 64);
-            if (dense) return launch_frame_kernel<C, true, M, false, true>(p, want, 0, lc, s);
+            if (dense) return launch_frame_kernel<C, true, M, false, true, V>(p, want, 0, lc, s);
         }
-        return launch_frame_kernel<C, true, M, false>(p, want, 0, lc, s);
+        return launch_frame_kernel<C, true, M, false, false, V>(p, want, 0, lc, s);
     }
-    return launch_frame_kernel<C, false, M, false>(p, want, 0, lc, s);
+    return launch_frame_kernel<C, false, M, false, false, V>(p, want, 0, lc, s);
 }
 }  // namespace
 
@@ -1433,19 +1440,29 @@ hipError_t launch_render(const FrameParams& p, const LaunchCtx& lc, hipStream_t 
     // camera mode: the detail count is not known here, so as many as fit)
     const uint32_t want = p.cam_state ? max((nblk + 3) / 4, nblk) : max((nblk + 3) / 4, (p.total_sub + 3) / 4);
     const int mat = (p.spec_pow ? kMatSpecPow : 0) | (p.example_mat ? kMatExample : 0);
+    // device-camera mode (the setup's CamState) is a separate build: args-mode frames carry no
+    // branch or load for it
+    if (p.cull && p.cam_state) {
+        switch (mat) {
+            case 0: return launch_frame_cs<true, 0, true>(p, want, lc, s);
+            case kMatSpecPow: return launch_frame_cs<true, kMatSpecPow, true>(p, want, lc, s);
+            case kMatExample: return launch_frame_cs<true, kMatExample, true>(p, want, lc, s);
+            default: return launch_frame_cs<true, kMatSpecPow | kMatExample, true>(p, want, lc, s);
+        }
+    }
     if (p.cull) {
         switch (mat) {
-            case 0: return launch_frame_cs<true, 0>(p, want, lc, s);
-            case kMatSpecPow: return launch_frame_cs<true, kMatSpecPow>(p, want, lc, s);
-            case kMatExample: return launch_frame_cs<true, kMatExample>(p, want, lc, s);
-            default: return launch_frame_cs<true, kMatSpecPow | kMatExample>(p, want, lc, s);
+            case 0: return launch_frame_cs<true, 0, false>(p, want, lc, s);
+            case kMatSpecPow: return launch_frame_cs<true, kMatSpecPow, false>(p, want, lc, s);
+            case kMatExample: return launch_frame_cs<true, kMatExample, false>(p, want, lc, s);
+            default: return launch_frame_cs<true, kMatSpecPow | kMatExample, false>(p, want, lc, s);
         }
     }
     switch (mat) {
-        case 0: return launch_frame_cs<false, 0>(p, want, lc, s);
-        case kMatSpecPow: return launch_frame_cs<false, kMatSpecPow>(p, want, lc, s);
-        case kMatExample: return launch_frame_cs<false, kMatExample>(p, want, lc, s);
-        default: return launch_frame_cs<false, kMatSpecPow | kMatExample>(p, want, lc, s);
+        case 0: return launch_frame_cs<false, 0, false>(p, want, lc, s);
+        case kMatSpecPow: return launch_frame_cs<false, kMatSpecPow, false>(p, want, lc, s);
+        case kMatExample: return launch_frame_cs<false, kMatExample, false>(p, want, lc, s);
+        default: return launch_frame_cs<false, kMatSpecPow | kMatExample, false>(p, want, lc, s);
     }
 }
 

@@ -319,7 +319,7 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp) 
         int32_t r[4];
         for (int k = 0; k < 4; ++k) r[k] = j < kTab ? (int32_t)s_tab[j][k] : sp.objs[j].g.rect[k];
         int32_t x0 = r[0], x1 = r[1], y0, y1;  // camera rows -> rank-local rows
-        band_local_range(sp.row0, sp.band_rows, sp.band_stride, r[2], r[3], &y0, &y1);
+        band_local_range(sp.row0, sp.band_shift, sp.band_stride, r[2], r[3], &y0, &y1);
         x1 = x1 < w_i - 1 ? x1 : w_i - 1;
         y0 = y0 > 0 ? y0 : 0;
         y1 = y1 < rows_i - 1 ? y1 : rows_i - 1;

@@ -233,7 +233,7 @@ __global__ void __launch_bounds__(256) trace_kernel(FrameParams p) {
     const uint32_t px = blockIdx.x * 64 + (threadIdx.x & 63);
     const uint32_t py = blockIdx.y * 4 + (threadIdx.x >> 6);  // rank-local row
     if (px >= p.cam_w || py >= p.rows) return;
-    const uint32_t y = band_camera_row(p.row0, p.band_rows, p.band_stride, py);
+    const uint32_t y = band_camera_row(p.row0, p.band_shift, p.band_mask, p.band_stride, py);
     const f3 C = mk3(p.cx, p.cy, p.cz);
     int32_t face = -1;
     // cast_ray_from_camera(x as f32, y as f32) (engine.rs:60, 100-109)

@@ -33,8 +33,8 @@ def band_split(rank: int, world: int, height: int, band: int = BAND_ROWS) -> dic
     the rows each rank's local buffers hold for the gather (rank 0's count, the largest)."""
     if not 0 <= rank < world:
         raise ValueError(f"rank {rank} outside world {world}")
-    if band % 4:
-        raise ValueError("bands must be a multiple of 4 rows")
+    if band < 4 or band & (band - 1):
+        raise ValueError("bands must be a power of two of at least 4 rows")
     bands, tail = divmod(height, band)
     rows = (bands // world + (1 if rank < bands % world else 0)) * band + (tail if tail and bands % world == rank else 0)
     rows0 = (bands // world + (1 if 0 < bands % world else 0)) * band + (tail if tail and bands % world == 0 else 0)

@@ -249,8 +249,8 @@ typedef struct eray_render_params {
     uint32_t band_rows;             /* 0: the rows are camera rows [row0, row0 + rows).  Else
                                        interleaved bands (a multi-GPU rank's share): local row j
                                        is camera row row0 + (j / band_rows) * band_stride +
-                                       j % band_rows; band_rows, band_stride and row0 multiples
-                                       of 4.  The outputs hold the local rows (out_ppm in local
+                                       j % band_rows; band_rows a power of two >= 4,
+                                       band_stride and row0 multiples of 4.  The outputs hold the local rows (out_ppm in local
                                        file order: byte row k = local row rows - 1 - k). */
     uint32_t band_stride;
 } eray_render_params;
