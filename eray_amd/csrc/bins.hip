@@ -137,7 +137,10 @@ __device__ __forceinline__ void max4(uint32_t* dst, const uint32_t (&a)[4]) {
     for (int q = 0; q < 4; ++q) atomicMax(dst + q, a[q]);
 }
 
-__global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(const uint32_t* __restrict__ start, uint32_t nb,
+// kFinal false: each workgroup reduces its 256 keys and publishes; true: one workgroup combines
+// the nparts workgroups' partials (no device-scope fence and counter per workgroup).
+template <bool kFinal>
+__global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t nparts, const uint32_t* __restrict__ start, uint32_t nb,
                                                                uint32_t bins_x, uint32_t nbins, uint32_t W, uint32_t H,
                                                                uint32_t phase, uint32_t* __restrict__ acc,
                                                                uint32_t* __restrict__ part,
@@ -148,14 +151,13 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(const uint32_t* _
                                                                CamState* __restrict__ st) {
     __shared__ uint32_t s_acc[kFinSpan][4];
     __shared__ uint32_t s_tab[kFinTab][4];
-    __shared__ uint32_t s_last;
     const uint32_t keys = nb * nbins;
     const uint32_t b0 = blockIdx.x * kBinWG, b1 = min(b0 + kBinWG, keys);
     const uint32_t k_first = b0 < b1 ? b0 / nbins : 0u, k_last = b0 < b1 ? (b1 - 1) / nbins : 0u;
     if (threadIdx.x < kFinSpan * 4) s_acc[threadIdx.x / 4][threadIdx.x % 4] = 0u;
     __syncthreads();
     const uint32_t b = b0 + threadIdx.x;
-    if (b < keys && start[b + 1] > start[b]) {
+    if (!kFinal && b < keys && start[b + 1] > start[b]) {
         const uint32_t k = b / nbins;
         const uint32_t lb = b - k * nbins;
         const uint32_t bx = lb % bins_x, by = lb / bins_x;
@@ -167,10 +169,10 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(const uint32_t* _
         else max4(acc + 4 * k, a);
     }
     __syncthreads();
-    const uint32_t span = b0 < b1 ? min(k_last - k_first + 1, kFinSpan) : 0u;
+    const uint32_t span = !kFinal && b0 < b1 ? min(k_last - k_first + 1, kFinSpan) : 0u;
     if (threadIdx.x < span && threadIdx.x > 0 && k_first + threadIdx.x < k_last)  // inner objects: whole
         for (int q = 0; q < 4; ++q) acc[4 * (k_first + threadIdx.x) + q] = s_acc[threadIdx.x][q];
-    if (threadIdx.x == 0) {
+    if (!kFinal && threadIdx.x == 0) {
         uint32_t* pb = part + 10 * blockIdx.x;
         pb[0] = b0 < b1 ? k_first : ~0u;
         pb[5] = b0 < b1 ? k_last : ~0u;
@@ -179,12 +181,7 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(const uint32_t* _
             pb[6 + q] = b0 < b1 && k_last - k_first < kFinSpan ? s_acc[k_last - k_first][q] : 0u;
         }
     }
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
+    if (!kFinal) return;
     const bool in_lds = nb <= kFinTab;
     if (in_lds) {
         for (uint32_t j = threadIdx.x; j < nb; j += kBinWG)
@@ -194,7 +191,7 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(const uint32_t* _
             }
         __syncthreads();
     }
-    for (uint32_t g = threadIdx.x; g < gridDim.x; g += kBinWG) {
+    for (uint32_t g = threadIdx.x; g < nparts; g += kBinWG) {
         const uint32_t* pb = part + 10 * g;
         for (int e = 0; e < 2; ++e) {
             if (pb[5 * e] == ~0u) continue;
@@ -236,7 +233,6 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(const uint32_t* _
     }
     if (threadIdx.x == 0) {
         *n = 0u;
-        *done = 0u;
         // the most entries any setup needed since the buffers were allocated (the host grows the
         // capacity from it), and whether any overflowed
         st->bin_entries = max(st->bin_entries, found);
@@ -371,9 +367,13 @@ hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tile
                                                     b.kbegin, b.nbins, sp.hot, b.tri, b.mask, b.hot);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t fgrid = (uint32_t)std::max<size_t>((keys + kBinWG - 1) / kBinWG, 1);
-    bins_finalize_kernel<<<fgrid, kBinWG, 0, s>>>(b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase, b.acc, b.part, b.done,
-                                                  b.n, (uint32_t)b.cap, b.kobj, sp.objs, b.tri, b.mask, b.hot,
-                                                  sp.state);
+    bins_finalize_kernel<false><<<fgrid, kBinWG, 0, s>>>(fgrid, b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase,
+                                                         b.acc, b.part, b.done, b.n, (uint32_t)b.cap, b.kobj, sp.objs,
+                                                         b.tri, b.mask, b.hot, sp.state);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    bins_finalize_kernel<true><<<1, kBinWG, 0, s>>>(fgrid, b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase, b.acc,
+                                                    b.part, b.done, b.n, (uint32_t)b.cap, b.kobj, sp.objs, b.tri, b.mask,
+                                                    b.hot, sp.state);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (!b.nsub) return hipSuccess;
     const uint32_t n = (uint32_t)b.nsub;

@@ -163,11 +163,15 @@ __device__ __forceinline__ void max4(uint32_t* dst, const uint32_t (&a)[4]) {
     for (int k = 0; k < 4; ++k) atomicMax(dst + k, a[k]);
 }
 
-__global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp) {
+// kMode 0: one workgroup does everything (small scenes); kMode 1: the chunks' workgroups reduce
+// and publish (no finalisation); kMode 2: one workgroup combines the nparts workgroups' partials.
+// (A last-workgroup finalisation inside kMode 1 cost every workgroup a device-scope fence — an
+// L2 write-back on this multi-XCD part — and a contended counter: 59 us at 70k faces.)
+template <int kMode>
+__global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp, uint32_t nparts) {
     __shared__ double s_poly[16 * kSetupWG];  // face_rect's clip output, 128 B per thread
     __shared__ uint32_t s_acc[kSpan][4];      // this workgroup's objects (o - o_first)
     __shared__ uint32_t s_tab[kTab][4];       // the last workgroup's per-object unions
-    __shared__ uint32_t s_last;
     const CamDev cam = *sp.cam;
     const uint32_t tid = threadIdx.x;
     const uint32_t chunk = (sp.T + gridDim.x - 1) / gridDim.x;
@@ -177,7 +181,7 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp) 
     for (uint32_t j = tid; j < kSpan; j += kSetupWG)
         for (int k = 0; k < 4; ++k) s_acc[j][k] = 0u;
     __syncthreads();
-    for (uint32_t i = lo + tid; i < hi; i += kSetupWG) {
+    for (uint32_t i = lo + tid; i < hi && kMode != 2; i += kSetupWG) {
         const TriCull c = cull_record(sp.hot[i], cam);
         sp.cull[i] = c;
         const uint32_t obj = object_of(sp.obj_begin, sp.nobj, i);
@@ -206,8 +210,8 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp) 
         }
     }
     __syncthreads();
-    const bool single = gridDim.x == 1;
-    if (!single) {  // publish: inner objects' unions are final, the two end objects' are partial
+    constexpr bool single = kMode == 0;
+    if (kMode == 1) {  // publish: inner objects' unions are final, the two end objects' are partial
         const uint32_t span = lo < hi ? min(o_last - o_first + 1, kSpan) : 0u;
         for (uint32_t j = tid; j < span; j += kSetupWG) {
             const uint32_t o = o_first + j;
@@ -223,14 +227,9 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp) 
                 pb[6 + k] = lo < hi && o_last - o_first < kSpan ? s_acc[o_last - o_first][k] : 0u;
             }
         }
-        __threadfence();
-        __syncthreads();
-        if (tid == 0) s_last = atomicAdd(sp.done, 1u) == gridDim.x - 1;
-        __syncthreads();
-        if (!s_last) return;
-        __threadfence();
+        return;
     }
-    // ---- the last workgroup: every object's union
+    // ---- one workgroup: every object's union
     const bool in_lds = sp.nobj <= kTab;
     if (single && sp.nobj <= kSpan) {
         for (uint32_t j = tid; j < sp.nobj; j += kSetupWG) {
@@ -249,7 +248,7 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp) 
             for (uint32_t j = tid; j < min(sp.nobj, kSpan); j += kSetupWG)
                 for (int k = 0; k < 4; ++k) s_tab[j][k] = max(s_tab[j][k], s_acc[j][k]);
         } else {
-            for (uint32_t b = tid; b < gridDim.x; b += kSetupWG) {
+            for (uint32_t b = tid; b < nparts; b += kSetupWG) {
                 const uint32_t* pb = sp.part + 10 * b;
                 if (pb[0] != ~0u) {
                     uint32_t a[4] = {pb[1], pb[2], pb[3], pb[4]};
@@ -268,7 +267,7 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp) 
                 max4(sp.acc + 4 * j, a);
             }
         } else {
-            for (uint32_t b = tid; b < gridDim.x; b += kSetupWG) {
+            for (uint32_t b = tid; b < nparts; b += kSetupWG) {
                 const uint32_t* pb = sp.part + 10 * b;
                 if (pb[0] != ~0u) {
                     uint32_t a[4] = {pb[1], pb[2], pb[3], pb[4]};
@@ -306,7 +305,6 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp) 
     }
     __syncthreads();
     if (tid != 0) return;
-    if (!single) *sp.done = 0u;
     CamState& st = *sp.state;
     st.cam = cam;
     if (sp.binned) return;  // bins.hip narrows the rectangles and lists the detail sub-blocks
@@ -370,7 +368,14 @@ __global__ void set_camera_kernel(CamDev cam, CamDev* slot) {
 
 hipError_t launch_camera_setup(const SetupParams& sp, hipStream_t s) {
     const uint32_t blocks = sp.T ? min((sp.T + kSetupWG - 1) / kSetupWG, kSetupMaxBlocks) : 1u;
-    camera_setup_kernel<<<blocks, kSetupWG, 0, s>>>(sp);
+    if (blocks == 1) {
+        camera_setup_kernel<0><<<1, kSetupWG, 0, s>>>(sp, 1u);
+        return hipGetLastError();
+    }
+    camera_setup_kernel<1><<<blocks, kSetupWG, 0, s>>>(sp, blocks);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    camera_setup_kernel<2><<<1, kSetupWG, 0, s>>>(sp, blocks);
     return hipGetLastError();
 }
 
