@@ -87,7 +87,9 @@ def pmc_traffic(workload: dict):
     workload (scripts/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
     MI355X_MICROARCH.md): profiles/pmc_traffic*.json whose "workload" (mesh, frame, rows per
     GPU, GPUs) equals this run's, or None when no summary of this workload is committed."""
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json"))):
+    # the newest round's summaries first (profiles/rNN/pmc_traffic*.json), then older ones
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic*.json")), reverse=True)
+    for path in paths + sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json"))):
         try:
             with open(path) as f:
                 rec = json.load(f)
@@ -170,6 +172,33 @@ def mesh_label(path: str) -> str:
     return os.path.basename(path) if rel.startswith("..") else rel
 
 
+def moving_camera(scene, args, width, height, render_args, world, allreduce) -> dict:
+    """The bench's frames with a camera that moves every frame (dolly_path): eray_render_camera_path
+    runs each frame's camera setup on the device right before it.  Returns the moving_camera record."""
+    path = dolly_path(args.steps, frame_camera_fov(width, height), width)
+    scene.ctx.render_camera_path(path, width, height, **render_args())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    m0 = time.perf_counter()
+    scene.ctx.render_camera_path(path, width, height, **render_args())
+    torch.cuda.synchronize()
+    moving_s = time.perf_counter() - m0
+    if world > 1:
+        moving_s = float(allreduce(moving_s, torch.float64, dist.ReduceOp.MAX))
+    device_ms = scene.ctx.render_camera_path(path, width, height, timed=True, **render_args())
+    return {
+        "frame_ms": round(moving_s / args.steps * 1e3, 6),
+        "value": round(width * height * args.steps / moving_s / 1e6, 3),
+        "unit": "Mrays/s",
+        "device_ms_per_frame": round(device_ms, 6),
+        "frames": args.steps,
+        "camera": "dolly along the view axis, z 5 +- 0.5, z_dist 1 +- 0.1, a new camera every frame",
+        "includes": "per-frame camera setup on the device (culling records, pixel rectangles, merged detail "
+                    "rectangles; screen bins and detail list for meshes over 256 faces) + frame",
+    }
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -184,6 +213,7 @@ def main() -> None:
     ap.add_argument("--brute-force", action="store_true", help="disable the exact wave culling")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-moving-camera", action="store_true", help="skip the moving-camera line (counter runs)")
     ap.add_argument("--split", choices=("bands", "blocks"), default="bands",
                     help="N > 1: interleaved 4-row bands (balanced, default) or contiguous row blocks")
     ap.add_argument("--gather-every-frame", action="store_true",
@@ -319,18 +349,7 @@ def main() -> None:
 
     # moving camera: the same frames with a new camera every frame (the setup on the device,
     # inside each frame); one untimed pass captures the path's graphs
-    path = dolly_path(args.steps, frame_camera_fov(width, H_total), width)
-    scene.ctx.render_camera_path(path, width, H_total, **render_args())
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    m0 = time.perf_counter()
-    scene.ctx.render_camera_path(path, width, H_total, **render_args())
-    torch.cuda.synchronize()
-    moving_s = time.perf_counter() - m0
-    if world > 1:
-        moving_s = float(allreduce(moving_s, torch.float64, dist.ReduceOp.MAX))
-    moving_kernel_ms = scene.ctx.render_camera_path(path, width, H_total, timed=True, **render_args())
+    moving = None if args.no_moving_camera else moving_camera(scene, args, width, H_total, render_args, world, allreduce)
 
     if rank == 0:
         # the workload a committed counter summary (profiles/pmc_traffic*.json) must match
@@ -384,16 +403,7 @@ def main() -> None:
             "scene_setup_ms": round(t_setup * 1e3, 3),
             "gather_ms": None if gather_ms is None else round(gather_ms, 4),
             "rank_kernel_ms": [round(v, 6) for v in rank_kernel_ms],
-            "moving_camera": {
-                "frame_ms": round(moving_s / args.steps * 1e3, 6),
-                "value": round(width * H_total * args.steps / moving_s / 1e6, 3),
-                "unit": "Mrays/s",
-                "device_ms_per_frame": round(moving_kernel_ms, 6),
-                "frames": args.steps,
-                "camera": "dolly along the view axis, z 5 +- 0.5, z_dist 1 +- 0.1, a new camera every frame",
-                "includes": "per-frame camera setup on the device (culling records, pixel rectangles, merged "
-                            "detail rectangles; screen bins and detail list for meshes over 256 faces) + frame",
-            },
+            "moving_camera": moving,
             "gather": ("every frame" if args.gather_every_frame else "final frame") if world > 1 else None,
             **({"rehearsal": "all ranks on GPU 0, gloo collectives: not a measurement"} if rehearsal else {}),
             "hit_pixels": hits_all,

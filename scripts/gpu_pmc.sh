@@ -5,11 +5,11 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 D=${PMC_DIR:-pmc}  # output directory under gpurun_out/
 mkdir -p gpurun_out/$D
 export TMPDIR=/tmp
-ARGS=${BENCH_ARGS:---steps 50 --warmup 5 --no-cpu-baseline}
+ARGS=${BENCH_ARGS:---steps 50 --warmup 5 --no-cpu-baseline --no-moving-camera}
 pass() {  # name counters...
   local name=$1; shift
   echo "=== pmc $name: $*"
-  timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex 'frame_kernel' \
+  timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex 'frame_kernel|fill_kernel' \
       --output-format csv -d gpurun_out/$D/$name -o $name -- python bench.py $ARGS \
       > gpurun_out/$D/$name.log 2>&1
   local rc=$?

@@ -51,15 +51,24 @@ def pmc(tag: str, pmc_dir: str = "pmc", out_name: str = "pmc_traffic.json", work
         with open(path) as f:
             for row in csv.DictReader(f):
                 name = row["Kernel_Name"]
-                if "frame_kernel" not in name:
+                if "frame_kernel" not in name and "fill_kernel" not in name:
                     continue
                 per[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
     if not per:
         print("no frame_kernel counters under gpurun_out/pmc", file=sys.stderr)
         return
-    name = max(per, key=lambda k: len(per[k].get("WRITE_SIZE", [])))
+    frames = [k for k in per if "frame_kernel" in k]
+    name = max(frames, key=lambda k: len(per[k].get("WRITE_SIZE", [])))
     c = {k: statistics.mean(v) for k, v in per[name].items()}
     fetch, write = c.get("FETCH_SIZE", 0.0) * 1024, c.get("WRITE_SIZE", 0.0) * 1024
+    # frames whose background comes from the separate fill_kernel (dense large-mesh builds): one
+    # fill launch per frame launch, its bytes belong to the frame
+    fills = [k for k in per if "fill_kernel" in k]
+    if fills:
+        f = {k: statistics.mean(v) for k, v in per[fills[0]].items()}
+        fetch += f.get("FETCH_SIZE", 0.0) * 1024
+        write += f.get("WRITE_SIZE", 0.0) * 1024
+        name = name + " + " + fills[0]
     if workload is None:  # the bench line of the counted run (its JSON line in the pass logs)
         for log in glob.glob(os.path.join(OUT, pmc_dir, "*.log")):
             for line in open(log):
