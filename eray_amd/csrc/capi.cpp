@@ -143,6 +143,14 @@ struct eray_ctx {
     CamDev* h_path = nullptr;
     size_t h_path_cap = 0;
     hipEvent_t path_ev = nullptr;  // the last path upload (h_path reusable once complete)
+    // batched setups of a path chunk's cameras (scenes without binned objects): per camera slot
+    // its culling records, object descriptors and setup state
+    TriCull* d_bcull = nullptr;
+    size_t bcull_cap = 0;
+    ObjectDesc* d_bobjs = nullptr;
+    size_t bobjs_cap = 0;
+    CamState* d_bstate = nullptr;
+    size_t bstate_cap = 0;
     uint8_t* d_staging = nullptr;  // eray_gather_rows' banded staging (rank 0)
     size_t staging_cap = 0;
     LaunchCtx lc{nullptr, nullptr, nullptr};  // the separate fill's stream and events
@@ -417,8 +425,7 @@ int ensure_bins(eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs) {
 
 // Enqueues the per-camera setup of `d_camera` (device) for camera rows [row0, row0 + rows): no
 // host round trip (setup.hip, bins.hip).
-int enqueue_setup(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint32_t H, const RowSpan& rs) {
-    hipStream_t stream = ctx->stream;
+SetupParams setup_params(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint32_t H, const RowSpan& rs) {
     SetupParams sp{};
     sp.hot = ctx->d_hot;
     sp.cull = ctx->d_cull;
@@ -450,9 +457,24 @@ int enqueue_setup(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint32_t H,
         sp.bins_x = ctx->bins.bins_x;
         sp.phase = ctx->bins.phase;
     }
-    HIP_TRY(ctx, launch_camera_setup(sp, stream));
-    if (binned) HIP_TRY(ctx, launch_bins_build(sp, ctx->bins, (W + 63) / 64, stream));
+    return sp;
+}
+
+int enqueue_setup(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint32_t H, const RowSpan& rs) {
+    const SetupParams sp = setup_params(ctx, d_camera, W, H, rs);
+    HIP_TRY(ctx, launch_camera_setup(sp, ctx->stream));
+    if (sp.binned) HIP_TRY(ctx, launch_bins_build(sp, ctx->bins, (W + 63) / 64, ctx->stream));
     return ERAY_OK;
+}
+
+// Camera paths of scenes without binned objects set up a whole graph chunk's cameras in one
+// launch (one workgroup per camera, into per-camera slots) instead of one setup per frame: the
+// setup of a small scene is one workgroup's latency chain (culling records, the double-precision
+// clip of face_rect, the rectangle merge), which as its own launch per frame cost about as much
+// as the frame.  Up to kBatchTris triangles (the slots hold kGraphFrames x T culling records).
+constexpr uint32_t kBatchTris = 16384;
+bool batch_setup_ok(const eray_ctx* ctx) {
+    return !binned_objects(ctx) && ctx->objects.size() <= kSetupBatchMaxObjects && ctx->total_tris <= kBatchTris;
 }
 
 CamDev cam_dev(const eray_camera& c) {
@@ -573,7 +595,8 @@ int eray_ctx_destroy(eray_ctx* ctx) {
     bins_free(ctx->bins);
     void* bufs[] = {ctx->d_hot,   ctx->d_shade, ctx->d_cull,  ctx->d_raw,  ctx->d_objs,  ctx->d_lights,
                     ctx->d_prog,  ctx->d_cam,   ctx->d_state, ctx->d_acc,  ctx->d_begin, ctx->d_range,
-                    ctx->d_area,  ctx->d_fkey,  ctx->d_path,  ctx->d_path_all, ctx->d_staging};
+                    ctx->d_area,  ctx->d_fkey,  ctx->d_path,  ctx->d_path_all, ctx->d_staging,
+                    ctx->d_bcull, ctx->d_bobjs, ctx->d_bstate};
     for (void* b : bufs)
         if (b) hipFree(b);
     if (ctx->h_state) hipHostFree(ctx->h_state);
@@ -1192,17 +1215,45 @@ int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* rp, const e
     if (int st = ensure(ctx, &ctx->d_path, &ctx->path_cap, kGraphFrames)) return st;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_path_all, ctx->h_path, sizeof(CamDev) * n, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipEventRecord(ctx->path_ev, ctx->stream));
+    const bool batched = batch_setup_ok(ctx);
+    const uint32_t T = ctx->total_tris, nobj = (uint32_t)ctx->objects.size();
+    if (batched) {
+        if (int st = ensure(ctx, &ctx->d_bcull, &ctx->bcull_cap, (size_t)kGraphFrames * T)) return st;
+        if (int st = ensure(ctx, &ctx->d_bobjs, &ctx->bobjs_cap, (size_t)kGraphFrames * nobj)) return st;
+        if (int st = ensure(ctx, &ctx->d_bstate, &ctx->bstate_cap, kGraphFrames)) return st;
+    }
+    // frame `slot` of a batch whose setups started at camera `cams` (count cameras) — the batch
+    // is enqueued with its first frame
+    auto batch_frame = [&](const CamDev* cams, uint32_t slot, uint32_t count) -> int {
+        if (slot == 0) {
+            SetupParams sp = setup_params(ctx, cams, W, H, row_span(rp));
+            sp.cull = ctx->d_bcull;
+            sp.objs = ctx->d_bobjs;
+            sp.objs_src = ctx->d_objs;
+            sp.state = ctx->d_bstate;
+            HIP_TRY(ctx, launch_camera_setup_batch(sp, count, ctx->stream));
+        }
+        FrameParams q = p;
+        q.cam_state = ctx->d_bstate + slot;
+        q.cull = ctx->d_bcull + (size_t)slot * T;
+        q.objects = ctx->d_bobjs + (size_t)slot * nobj;
+        HIP_TRY(ctx, launch_frame(ctx, q));
+        return ERAY_OK;
+    };
     auto frame = [&](const CamDev* cam) -> int {
-        if (int st = enqueue_setup(ctx, cam, W, H,
-                                   row_span(rp)))
-            return st;
+        if (batched) return batch_frame(cam, 0, 1);
+        if (int st = enqueue_setup(ctx, cam, W, H, row_span(rp))) return st;
         HIP_TRY(ctx, launch_frame(ctx, p));
         return ERAY_OK;
     };
-    auto body = [&](uint32_t f, uint32_t) { return frame(ctx->d_path + f); };
-    std::vector<unsigned char> key = params_key(p, 1);
-    key.insert(key.end(), reinterpret_cast<const unsigned char*>(&ctx->d_path),
-               reinterpret_cast<const unsigned char*>(&ctx->d_path) + sizeof ctx->d_path);
+    auto body = [&](uint32_t f, uint32_t count) {
+        return batched ? batch_frame(ctx->d_path, f, count) : frame(ctx->d_path + f);
+    };
+    std::vector<unsigned char> key = params_key(p, batched ? 2 : 1);
+    for (const void* ptr : {(const void*)ctx->d_path, (const void*)ctx->d_bcull, (const void*)ctx->d_bobjs,
+                            (const void*)ctx->d_bstate})
+        key.insert(key.end(), reinterpret_cast<const unsigned char*>(&ptr),
+                   reinterpret_cast<const unsigned char*>(&ptr) + sizeof ptr);
     Plan plan;
     if (int st = ensure_plan(ctx, key, n, body, &plan)) return st;
     auto before = [&](uint32_t first, uint32_t count) -> int {

@@ -264,8 +264,15 @@ struct SetupParams {
     unsigned long long* area;
     uint32_t* fkey;
     uint32_t bins_x, phase;
+    const ObjectDesc* objs_src;  // batched setups: the scene's descriptors, copied into each slot
 };
 hipError_t launch_camera_setup(const SetupParams& sp, hipStream_t s);
+// The setups of `ncam` cameras sp.cam[0 .. ncam) at once, one workgroup each, into per-camera
+// slots: culling records sp.cull + k * T, descriptors sp.objs + k * nobj (sp.objs_src with the
+// camera's rectangles), state sp.state + k.  Scenes without binned objects and at most
+// kSetupBatchMaxObjects objects (every object's union stays in the workgroup's LDS).
+constexpr uint32_t kSetupBatchMaxObjects = 256;
+hipError_t launch_camera_setup_batch(const SetupParams& sp, uint32_t ncam, hipStream_t s);
 // Writes `cam` into the device camera slot (kernel arguments: no host staging buffer to race).
 hipError_t launch_set_camera(const CamDev& cam, CamDev* slot, hipStream_t s);
 // Launch overrides of eray_render_params::flags (eray_hip.h ERAY_RENDER_*) the frame launcher reads.

@@ -158,13 +158,15 @@ __device__ __forceinline__ void rect_words(const int32_t (&r)[4], uint32_t (&a)[
 // atomics per wave on the same four words (70k faces: 73 -> a few us).
 constexpr uint32_t kSpan = kSetupWG;  // objects per workgroup reduced in LDS (more: global atomics)
 constexpr uint32_t kTab = 2048;       // objects the last workgroup combines in LDS (more: in acc)
+static_assert(kSetupBatchMaxObjects <= kSpan, "a batched setup keeps every object's union in LDS");
 
 __device__ __forceinline__ void max4(uint32_t* dst, const uint32_t (&a)[4]) {
     for (int k = 0; k < 4; ++k) atomicMax(dst + k, a[k]);
 }
 
 // kMode 0: one workgroup does everything (small scenes); kMode 1: the chunks' workgroups reduce
-// and publish (no finalisation); kMode 2: one workgroup combines the nparts workgroups' partials.
+// and publish (no finalisation); kMode 2: one workgroup combines the nparts workgroups' partials;
+// kMode 3: workgroup k does kMode 0's work for camera k of a batch, into its own slots.
 // (A last-workgroup finalisation inside kMode 1 cost every workgroup a device-scope fence — an
 // L2 write-back on this multi-XCD part — and a contended counter: 59 us at 70k faces.)
 template <int kMode>
@@ -172,10 +174,16 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp, 
     __shared__ double s_poly[16 * kSetupWG];  // face_rect's clip output, 128 B per thread
     __shared__ uint32_t s_acc[kSpan][4];      // this workgroup's objects (o - o_first)
     __shared__ uint32_t s_tab[kTab][4];       // the last workgroup's per-object unions
+    if (kMode == 3) {  // camera blockIdx.x of the batch: its slots
+        sp.cam += blockIdx.x;
+        sp.cull += (size_t)blockIdx.x * sp.T;
+        sp.objs += (size_t)blockIdx.x * sp.nobj;
+        sp.state += blockIdx.x;
+    }
     const CamDev cam = *sp.cam;
     const uint32_t tid = threadIdx.x;
-    const uint32_t chunk = (sp.T + gridDim.x - 1) / gridDim.x;
-    const uint32_t lo = min(blockIdx.x * chunk, sp.T), hi = min(lo + chunk, sp.T);
+    const uint32_t chunk = kMode == 3 ? sp.T : (sp.T + gridDim.x - 1) / gridDim.x;
+    const uint32_t lo = kMode == 3 ? 0u : min(blockIdx.x * chunk, sp.T), hi = min(lo + chunk, sp.T);
     const uint32_t o_first = lo < hi ? object_of(sp.obj_begin, sp.nobj, lo) : 0u;
     const uint32_t o_last = lo < hi ? object_of(sp.obj_begin, sp.nobj, hi - 1) : 0u;
     for (uint32_t j = tid; j < kSpan; j += kSetupWG)
@@ -210,7 +218,7 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp, 
         }
     }
     __syncthreads();
-    constexpr bool single = kMode == 0;
+    constexpr bool single = kMode == 0 || kMode == 3;
     if (kMode == 1) {  // publish: inner objects' unions are final, the two end objects' are partial
         const uint32_t span = lo < hi ? min(o_last - o_first + 1, kSpan) : 0u;
         for (uint32_t j = tid; j < span; j += kSetupWG) {
@@ -299,6 +307,7 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp, 
             r[2] = (int32_t)~w[2];
             r[3] = (int32_t)w[3] - 1;
         }
+        if (kMode == 3) sp.objs[j] = sp.objs_src[j];  // the slot's descriptor, then its rectangle
         for (int k = 0; k < 4; ++k) sp.objs[j].g.rect[k] = r[k];
         if (j < kTab)
             for (int k = 0; k < 4; ++k) s_tab[j][k] = (uint32_t)r[k];
@@ -376,6 +385,13 @@ hipError_t launch_camera_setup(const SetupParams& sp, hipStream_t s) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     camera_setup_kernel<2><<<1, kSetupWG, 0, s>>>(sp, blocks);
+    return hipGetLastError();
+}
+
+hipError_t launch_camera_setup_batch(const SetupParams& sp, uint32_t ncam, hipStream_t s) {
+    if (sp.binned || sp.nobj > kSetupBatchMaxObjects) return hipErrorInvalidValue;
+    if (!ncam) return hipSuccess;
+    camera_setup_kernel<3><<<ncam, kSetupWG, 0, s>>>(sp, 1u);
     return hipGetLastError();
 }
 
