@@ -137,6 +137,86 @@ __device__ __forceinline__ void max4(uint32_t* dst, const uint32_t (&a)[4]) {
     for (int q = 0; q < 4; ++q) atomicMax(dst + q, a[q]);
 }
 
+// The scatter leaves a bin's entries in no particular order.  The frame kernel's result does not
+// depend on it (each pixel keeps its smallest hitting face), but its work does: a bin is searched
+// in chunks of 64 entries, and a chunk whose faces all come after every live pixel's best hit so
+// far is skipped — in face order, the later chunks of a dense bin mostly are.  So each bin with
+// more than one chunk (and at most kSortMax entries; longer ones stay as they are) is sorted by
+// face index (bin_sort_kernel, one wave per bin).  The frame kernel relies on it: in a bin of 65 to kBinSortMax entries the
+// position order is the face order (render.hip first_hit_binned).
+constexpr uint32_t kSortMax = kBinSortMax;
+constexpr uint32_t kSortPer = kSortMax / 64;  // entries per lane
+constexpr uint32_t kSortGrid = 1024;          // workgroups of the sort kernel's grid-stride loop
+
+// The bins to sort, appended to a work list (one counter atomic per wave), so that the sort
+// kernel spreads them over all its waves: the dense bins sit next to each other on the screen.
+__device__ __forceinline__ void queue_sort(const uint32_t* __restrict__ start, uint32_t b, uint32_t keys,
+                                           uint32_t* __restrict__ sortq, uint32_t* __restrict__ nsort) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t cnt = b < keys ? start[b + 1] - start[b] : 0u;
+    const bool want = cnt > 64 && cnt <= kSortMax;
+    const unsigned long long bal = __ballot(want);
+    if (!bal) return;
+    const uint32_t first = (uint32_t)(__ffsll(bal) - 1);
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(nsort, (uint32_t)__popcll(bal));
+    base = (uint32_t)__shfl((int)base, (int)first);
+    if (want) sortq[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = b;
+}
+
+// One wave per queued bin: its entries staged in LDS, each entry's rank = the number of the bin's
+// faces below its own (a face appears at most once per bin), each entry written back at its rank.
+__global__ void __launch_bounds__(kBinWG) bin_sort_kernel(const uint32_t* __restrict__ sortq,
+                                                          const uint32_t* __restrict__ nsort,
+                                                          const uint32_t* __restrict__ start,
+                                                          uint32_t* __restrict__ tri,
+                                                          unsigned long long* __restrict__ mask,
+                                                          TriHot* __restrict__ hot) {
+    __shared__ uint32_t s_tri[kBinWG / 64][kSortMax];
+    __shared__ unsigned long long s_mask[kBinWG / 64][kSortMax];
+    __shared__ TriHot s_hot[kBinWG / 64][kSortMax];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t items = *nsort;
+    uint32_t* st = s_tri[wave];
+    for (uint32_t it = blockIdx.x * (kBinWG / 64) + wave; it < items; it += gridDim.x * (kBinWG / 64)) {
+        const uint32_t key = sortq[it];  // wave-uniform
+        const uint32_t s0 = start[key], n = start[key + 1] - s0;
+        uint32_t v[kSortPer], r[kSortPer];
+#pragma unroll
+        for (uint32_t q = 0; q < kSortPer; ++q) {
+            const uint32_t e = lane + 64 * q;
+            v[q] = 0xffffffffu;
+            r[q] = 0;
+            if (e < n) {
+                v[q] = tri[s0 + e];
+                st[e] = v[q];
+                s_mask[wave][e] = mask[s0 + e];
+                s_hot[wave][e] = hot[s0 + e];
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t j = 0; j < n; ++j) {
+            const uint32_t f = st[j];
+#pragma unroll
+            for (uint32_t q = 0; q < kSortPer; ++q) r[q] += f < v[q] ? 1u : 0u;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kSortPer; ++q) {
+            const uint32_t e = lane + 64 * q;
+            if (e < n) {
+                tri[s0 + r[q]] = v[q];
+                mask[s0 + r[q]] = s_mask[wave][e];
+                hot[s0 + r[q]] = s_hot[wave][e];
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // the LDS is rewritten by the next bin
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
 // kFinal false: each workgroup reduces its 256 keys and publishes; true: one workgroup combines
 // the nparts workgroups' partials (no device-scope fence and counter per workgroup).
 template <bool kFinal>
@@ -148,6 +228,7 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t nparts, 
                                                                uint32_t cap, const uint32_t* __restrict__ kobj,
                                                                ObjectDesc* __restrict__ objs, uint32_t* tri,
                                                                unsigned long long* mask, TriHot* hot,
+                                                               uint32_t* __restrict__ sortq, uint32_t* __restrict__ nsort,
                                                                CamState* __restrict__ st) {
     __shared__ uint32_t s_acc[kFinSpan][4];
     __shared__ uint32_t s_tab[kFinTab][4];
@@ -169,6 +250,7 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t nparts, 
         else max4(acc + 4 * k, a);
     }
     __syncthreads();
+    if constexpr (!kFinal) queue_sort(start, b, keys, sortq, nsort);
     const uint32_t span = !kFinal && b0 < b1 ? min(k_last - k_first + 1, kFinSpan) : 0u;
     if (threadIdx.x < span && threadIdx.x > 0 && k_first + threadIdx.x < k_last)  // inner objects: whole
         for (int q = 0; q < 4; ++q) acc[4 * (k_first + threadIdx.x) + q] = s_acc[threadIdx.x][q];
@@ -233,6 +315,7 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t nparts, 
     }
     if (threadIdx.x == 0) {
         *n = 0u;
+        *nsort = 0u;  // (bin_sort_kernel has run)
         // the most entries any setup needed since the buffers were allocated (the host grows the
         // capacity from it), and whether any overflowed
         st->bin_entries = max(st->bin_entries, found);
@@ -296,7 +379,7 @@ hipError_t grow(T** p, size_t need) {
 void bins_free(BinBuffers& b) {
     void* ptrs[] = {b.first, b.count,  b.start,  b.kbegin, b.kobj,   b.n,       b.done,    b.acc,   b.part, b.ekey,
                     b.eface, b.emask,  b.tri,    b.mask,   b.hot,    b.dflags,  b.dpacked, b.dlist, b.docc,
-                    b.temp};
+                    b.sortq, b.nsort,  b.temp};
     for (void* p : ptrs)
         if (p) hipFree(p);
     b = BinBuffers{};
@@ -326,11 +409,13 @@ hipError_t bins_alloc(BinBuffers& b, uint32_t T, uint32_t nb, const uint32_t* kb
         (e = grow(&b.emask, cap)) != hipSuccess || (e = grow(&b.tri, cap)) != hipSuccess ||
         (e = grow(&b.mask, cap)) != hipSuccess || (e = grow(&b.hot, cap)) != hipSuccess ||
         (e = grow(&b.dflags, b.nsub)) != hipSuccess || (e = grow(&b.dpacked, b.nsub)) != hipSuccess ||
-        (e = grow(&b.dlist, b.nsub)) != hipSuccess || (e = grow(&b.docc, (size_t)tiles_x * subs_y)) != hipSuccess)
+        (e = grow(&b.dlist, b.nsub)) != hipSuccess || (e = grow(&b.docc, (size_t)tiles_x * subs_y)) != hipSuccess ||
+        (e = grow(&b.sortq, std::max<size_t>(keys, 1))) != hipSuccess || (e = grow(&b.nsort, 1)) != hipSuccess)
         return e;
     // counters zero between builds (each build leaves them so)
     if ((e = hipMemsetAsync(b.count, 0, sizeof(uint32_t) * (keys + 1), s)) != hipSuccess ||
         (e = hipMemsetAsync(b.n, 0, sizeof(uint32_t), s)) != hipSuccess ||
+        (e = hipMemsetAsync(b.nsort, 0, sizeof(uint32_t), s)) != hipSuccess ||
         (e = hipMemsetAsync(b.done, 0, sizeof(uint32_t), s)) != hipSuccess ||
         (e = hipMemsetAsync(b.acc, 0, sizeof(uint32_t) * 4 * nb, s)) != hipSuccess ||
         (e = hipMemcpyAsync(b.kbegin, kbegin, sizeof(uint32_t) * nb, hipMemcpyHostToDevice, s)) != hipSuccess ||
@@ -369,11 +454,13 @@ hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tile
     const uint32_t fgrid = (uint32_t)std::max<size_t>((keys + kBinWG - 1) / kBinWG, 1);
     bins_finalize_kernel<false><<<fgrid, kBinWG, 0, s>>>(fgrid, b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase,
                                                          b.acc, b.part, b.done, b.n, (uint32_t)b.cap, b.kobj, sp.objs,
-                                                         b.tri, b.mask, b.hot, sp.state);
+                                                         b.tri, b.mask, b.hot, b.sortq, b.nsort, sp.state);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    bin_sort_kernel<<<kSortGrid, kBinWG, 0, s>>>(b.sortq, b.nsort, b.start, b.tri, b.mask, b.hot);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     bins_finalize_kernel<true><<<1, kBinWG, 0, s>>>(fgrid, b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase, b.acc,
                                                     b.part, b.done, b.n, (uint32_t)b.cap, b.kobj, sp.objs, b.tri, b.mask,
-                                                    b.hot, sp.state);
+                                                    b.hot, b.sortq, b.nsort, sp.state);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (!b.nsub) return hipSuccess;
     const uint32_t n = (uint32_t)b.nsub;

@@ -75,6 +75,9 @@ constexpr uint32_t kCacheTris = 256, kCacheObjects = 16, kCacheLights = 16;
 constexpr uint32_t kDirectMax = 256;
 // Screen bins of large objects' faces: kBinW x kBinH pixels (one wave's 16 x 4 sub-block).
 constexpr uint32_t kBinW = 16, kBinH = 4;
+// Bins of at most this many entries are sorted by face index (bins.hip sort_bins); longer ones
+// keep the scatter's order.
+constexpr uint32_t kBinSortMax = 256;
 // Detail rectangles carried in the kernel arguments (more objects: merged into the last one).
 constexpr int kMaxRects = 8;
 // Deepest reflection recursion the general tracer keeps frames for (Engine::bounces).
@@ -315,6 +318,8 @@ struct BinBuffers {
     uint32_t* dpacked = nullptr;
     uint32_t* dlist = nullptr;
     uint8_t* docc = nullptr;
+    uint32_t* sortq = nullptr;            // bins to sort by face index (bins.hip bin_sort_kernel)
+    uint32_t* nsort = nullptr;            // their count, zero between builds
     size_t nsub = 0;
     void* temp = nullptr;                 // hipcub scratch
     size_t temp_bytes = 0;

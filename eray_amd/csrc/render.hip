@@ -502,9 +502,11 @@ constexpr uint32_t kWide = 16;  // candidates that may cover more pixels are tes
 // Per-wave LDS of the binned primary search.
 struct BinLds {
     float dir[3][64];         // each pixel's camera ray (lane = pixel)
-    uint32_t best[64];        // each pixel's first hit so far: face index, 0xffffffff = none
+    // each pixel's first hit so far as an order key, 0xffffffff = none: its bin position in a
+    // sorted bin (positions grow with the face index), its face index in a longer one
+    uint32_t best[64];
     TriHot cand[64];          // the chunk's candidate records (slot = lane that loaded it)
-    uint32_t face[64];        // ... and their face indices
+    uint32_t key[64];         // ... and their order keys
     // (candidate slot << 6) | pixel, for every pixel a narrow candidate (<= kWide pixels) may hit
     uint16_t pairs[64 * kWide];
 };
@@ -512,14 +514,19 @@ constexpr uint32_t kBinLdsBytes = (sizeof(BinLds) + 15) / 16 * 16;
 
 // Primary-ray first hit of a binned object (bins.hip), all four waves of the workgroup together
 // (every wave calls it; workgroup-uniform).  The reference's first hit is the smallest face index
-// whose Triangle::intersects passes (object.rs:63-78); a bin lists its faces in no particular
-// order, so each pixel keeps the smallest hitting face index seen so far (LDS atomicMin).  Each
-// wave's sub-block bin is cut into chunks of 64 entries and the workgroup's chunks are dealt
-// round-robin over its waves — a bin at a dense spot (thousands of faces) is shared four ways.  A
-// chunk is tested as (face, pixel) pairs: each entry carries the pixels where its four culling
-// bounds can pass (bin_pixels), restricted to the pixels whose best face is still above the
-// chunk's smallest face; narrow faces' pairs are compacted in LDS and tested one per lane, wide
-// ones by the whole wave, and a pair whose face is not below the pixel's best so far is skipped.
+// whose Triangle::intersects passes (object.rs:63-78), so each pixel keeps the smallest hitting
+// face seen so far (LDS atomicMin of an order key).  A bin of 65 to kBinSortMax entries lists its
+// faces in index order (bins.hip sort_bins): the key is the bin position, and a chunk none of
+// whose pixels is still without a hit before the chunk's first position is skipped before its
+// entries are read.  Other bins are in no particular order (one chunk, or too long to sort): the
+// key is the face index, and a chunk is skipped when every pixel's best face is below the
+// chunk's smallest.  Each wave's
+// sub-block bin is cut into chunks of 64 entries and the workgroup's chunks are dealt round-robin
+// over its waves — a bin at a dense spot (thousands of faces) is shared four ways.  A chunk is
+// tested as (face, pixel) pairs: each entry carries the pixels where its four culling bounds can
+// pass (bin_pixels), restricted to the live pixels; narrow faces' pairs are compacted in LDS and
+// tested one per lane, wide ones by the whole wave, and a pair whose key is not below the pixel's
+// best so far is skipped.
 // Work follows the pixels a face can cover, not 64 lanes per face.  Each wave then re-tests its
 // pixels' winners for u, v, t.
 template <typename Activate>
@@ -555,26 +562,39 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
         uint32_t w = 0, c = item;
         while (c >= chunks[w]) c -= chunks[w++];
         BinLds& T = *reinterpret_cast<BinLds*>(s_bins + w * kBinLdsBytes);  // the chunk's sub-block
-        const uint32_t base = s_range[2 * w] + 64 * c, end = s_range[2 * w + 1];
+        const uint32_t lo_w = s_range[2 * w], end = s_range[2 * w + 1];
+        const uint32_t base = lo_w + 64 * c;
+        const bool sorted = end - lo_w > 64 && end - lo_w <= kBinSortMax;  // workgroup-uniform
         const uint32_t j = base + lane;
-        uint32_t fj = 0xffffffffu;
+        uint32_t fj = 0xffffffffu;  // the entry's order key
         unsigned long long pm = 0;
-        if (j < end) {
-            fj = ob.bin_tri[j];
-            pm = ob.bin_mask[j];
-            L.cand[lane] = ob.bin_hot[j];
-            L.face[lane] = fj;
-        }
-        uint32_t cmin = fj;  // the chunk's smallest face
+        unsigned long long live;  // pixels of that sub-block this chunk can still improve
+        if (sorted) {
+            live = __ballot(T.best[lane] > base);
+            if (!live) continue;
+            if (j < end) {
+                fj = j;
+                pm = ob.bin_mask[j];
+                L.cand[lane] = ob.bin_hot[j];
+                L.key[lane] = j;
+            }
+        } else {
+            if (j < end) {
+                fj = ob.bin_tri[j];
+                pm = ob.bin_mask[j];
+                L.cand[lane] = ob.bin_hot[j];
+                L.key[lane] = fj;
+            }
+            uint32_t cmin = fj;  // the chunk's smallest face
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) cmin = min(cmin, (uint32_t)__shfl_xor((int)cmin, off));
-        // pixels of that sub-block this chunk can still improve
-        const unsigned long long live = __ballot(T.best[lane] > cmin);
-        if (!live) continue;
+            for (int off = 32; off > 0; off >>= 1) cmin = min(cmin, (uint32_t)__shfl_xor((int)cmin, off));
+            live = __ballot(T.best[lane] > cmin);
+            if (!live) continue;
+        }
         const unsigned long long pix = pm & live;  // live pixels this face may hit
         const uint32_t cnt = (uint32_t)__popcll(pix);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();  // L.cand / L.face of this chunk visible to the wave
+        __builtin_amdgcn_wave_barrier();  // L.cand / L.key of this chunk visible to the wave
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // wide candidates (many pixels): the whole wave tests them, each lane its own pixel
         unsigned long long wide = __ballot(cnt > kWide);
@@ -614,7 +634,7 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
             if (q + lane < npairs) {
                 const uint32_t pr = L.pairs[q + lane];
                 const uint32_t slot = pr >> 6, px = pr & 63;
-                const uint32_t fc = L.face[slot];
+                const uint32_t fc = L.key[slot];
                 if (fc < T.best[px]) {  // a pixel already hit by an earlier face needs no test
                     float u, v, t;
                     const f3 dd = mk3(T.dir[0][px], T.dir[1][px], T.dir[2][px]);
@@ -623,15 +643,20 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();  // L.cand / L.face / L.pairs are rewritten by the next chunk
+        __builtin_amdgcn_wave_barrier();  // L.cand / L.key / L.pairs are rewritten by the next chunk
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     __syncthreads();  // every chunk of every sub-block is done
     const uint32_t mine = L.best[lane];
     if (st == kSearching && mine != 0xffffffffu) {
         float u, v, t;
-        exact_test(as_global_rec(p.tris + ob.tri_begin + mine), o, d, u, v, t);  // the winner again, for u, v, t
-        found = (int)mine;
+        if (hi - lo > 64 && hi - lo <= kBinSortMax) {  // the winner again, for u, v, t
+            exact_test(ob.bin_hot[mine], o, d, u, v, t);
+            found = (int)ob.bin_tri[mine];
+        } else {
+            exact_test(as_global_rec(p.tris + ob.tri_begin + mine), o, d, u, v, t);
+            found = (int)mine;
+        }
         hu = u;
         hv = v;
         ht = t;
