@@ -53,6 +53,7 @@ from eray_amd.objfile import load_obj_file  # noqa: E402
 
 WIDTH, HEIGHT, TEXTURE = 1920, 1080, 1024  # C2 (defaults; --width / --height)
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PEAK_VALU_TOPS = 78.6  # non-FMA FP32 VALU: 256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz
 
 
 def frame_camera_fov(width: int, height: int) -> tuple[float, float]:
@@ -82,10 +83,9 @@ def algorithmic_bytes(hit_pixels: int, pixels: int, triangles: int) -> int:
     return 15 * pixels + 16 * hit_pixels + (48 + 64 + 64) * triangles
 
 
-def pmc_traffic(workload: dict):
-    """HBM bytes per frame-kernel launch from the committed rocprofv3 counter summary of this
-    workload (scripts/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
-    MI355X_MICROARCH.md): profiles/pmc_traffic*.json whose "workload" (mesh, frame, rows per
+def pmc_record(workload: dict):
+    """The committed rocprofv3 counter summary of this workload's frame kernel
+    (scripts/pmc_traffic.py): profiles/pmc_traffic*.json whose "workload" (mesh, frame, rows per
     GPU, GPUs) equals this run's, or None when no summary of this workload is committed."""
     # the newest round's summaries first (profiles/rNN/pmc_traffic*.json), then older ones
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic*.json")), reverse=True)
@@ -93,11 +93,34 @@ def pmc_traffic(workload: dict):
         try:
             with open(path) as f:
                 rec = json.load(f)
-            if rec.get("workload") == workload:
-                return int(rec["frame_kernel"]["hbm_bytes_per_launch"])
+            if rec.get("workload") == workload and "frame_kernel" in rec:
+                return rec["frame_kernel"]
         except (OSError, KeyError, ValueError):
             continue
     return None
+
+
+def counter_figures(rec, kernel_ms: float) -> dict:
+    """From a counter summary: HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, the gfx950
+    correction of MI355X_MICROARCH.md), the HBM-read fraction (north_star's figure: corrected fetch
+    bytes / kernel time / peak) and the VALU fraction (SURVEY.md §8(d)'s binding figure for the
+    intersection: SQ_INSTS_VALU x 64 lanes / kernel time / the 78.6 T ops/s non-FMA FP32 peak; it
+    counts every VALU instruction of the frame kernel — rays, tests, shading, fill addressing)."""
+    if not rec:
+        return {"traffic": None}
+    out = {"traffic": int(rec["hbm_bytes_per_launch"])}
+    sec = kernel_ms * 1e-3
+    fetch = rec.get("fetch_bytes_corrected")
+    if fetch is not None and sec > 0:
+        gbs = fetch / sec / 1e9
+        out["hbm_read"] = {"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                           "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": int(fetch)}
+    valu = rec.get("counters_mean_per_dispatch", {}).get("SQ_INSTS_VALU")
+    if valu is not None and sec > 0:
+        tops = valu * 64 / sec / 1e12
+        out["valu"] = {"achieved": round(tops, 2), "peak": PEAK_VALU_TOPS, "unit": "TOP/s",
+                       "frac": round(tops / PEAK_VALU_TOPS, 4), "instructions_per_launch": int(valu)}
+    return out
 
 
 def host_cpu() -> tuple[int, str]:
@@ -415,7 +438,7 @@ def main() -> None:
                 "peak": PEAK_HBM_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4),
-                "traffic": pmc_traffic(pmc_key),
+                **counter_figures(pmc_record(pmc_key), kernel_ms),
                 "kernel": "frame_kernel (eray_amd/csrc/render.hip)",
                 "algorithmic_bytes_per_launch": alg,
                 "kernel_ms": round(kernel_ms, 6),

@@ -60,6 +60,7 @@ def pmc(tag: str, pmc_dir: str = "pmc", out_name: str = "pmc_traffic.json", work
     frames = [k for k in per if "frame_kernel" in k]
     name = max(frames, key=lambda k: len(per[k].get("WRITE_SIZE", [])))
     c = {k: statistics.mean(v) for k, v in per[name].items()}
+    dispatches = len(per[name].get("WRITE_SIZE", []))
     fetch, write = c.get("FETCH_SIZE", 0.0) * 1024, c.get("WRITE_SIZE", 0.0) * 1024
     # frames whose background comes from the separate fill_kernel (dense large-mesh builds): one
     # fill launch per frame launch, its bytes belong to the frame
@@ -79,7 +80,7 @@ def pmc(tag: str, pmc_dir: str = "pmc", out_name: str = "pmc_traffic.json", work
                                 "n_gpus": d["n_gpus"], "brute_force": not cfg["culling"]}
     out = {"round": tag, "workload": workload, "frame_kernel": {
         "kernel": name,
-        "dispatches": len(per[name].get("WRITE_SIZE", [])),
+        "dispatches": dispatches,
         "counters_mean_per_dispatch": c,
         "fetch_bytes_corrected": 2 * fetch,
         "write_bytes": write,
