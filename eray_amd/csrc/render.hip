@@ -692,7 +692,7 @@ __device__ __forceinline__ f3 camera_dir(const CamDev& cam, const FrameParams& p
 // sub-block inside one of the frame's detail rectangles (FrameParams::rects: the objects' pixel
 // rectangles, ObjectDesc::rect, in sub-block units) is "detail": one wave runs Engine::cast_ray
 // for its 64 pixels, one pixel per lane.  Every other sub-block is background
-// (engine.rs:355-357) with no test at all.  One persistent launch does both:
+// (engine.rs:208-213) with no test at all.  One persistent launch does both:
 //  * detail: the detail sub-blocks are enumerated rectangle by rectangle (the host makes the
 //    rectangles disjoint) and dealt out round-robin over the first
 //    workgroups, four consecutive ones per workgroup, so the latency-bound shading is spread
@@ -743,7 +743,7 @@ __device__ __forceinline__ void stream16(B* base, const void* dst, float4 v) {
     stream16(base, dst, make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)));
 }
 
-// background (engine.rs:355-357) and its bytes: sat_u8(0.1*255) = 25, sat_u8(0.2*255) = 51
+// background (engine.rs:208-213) and its bytes: sat_u8(0.1*255) = 25, sat_u8(0.2*255) = 51
 __device__ __forceinline__ float4 bg_rgb4(uint32_t phase) {  // 16-byte word at float offset 4c
     const float a = 0.1f, b = 0.2f;
     return phase == 0 ? make_float4(a, a, b, a) : phase == 1 ? make_float4(a, b, a, a) : make_float4(b, a, a, b);
@@ -1052,7 +1052,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const CamDev& c
             push(cmul(cmul(m, kd), L.brightness));
         }
     } else {
-        push(rgb{0.1f, 0.1f, 0.2f});  // engine.rs:355-357
+        push(rgb{0.1f, 0.1f, 0.2f});  // engine.rs:208-213
     }
 
     // ---- outputs: Image::set + Color::as_bytes, rows bottom-up (image.rs:41-74) ---
