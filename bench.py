@@ -224,6 +224,24 @@ def moving_camera(scene, args, width, height, render_args, world, allreduce) -> 
     }
 
 
+AA_SAMPLES = 4
+AA_MAX_TRIANGLES = 4096  # the general tracer scans every face per ray: small scenes only
+
+
+def anti_aliasing_line(scene, args, width, height, render_args) -> dict:
+    """The general tracer (trace.hip: anti-aliasing, engine.rs:59-77) on the bench's frames:
+    AA_SAMPLES jittered rays per pixel plus the centre ray, every face scanned per ray.  Device
+    time per frame over graph-replayed frames; rays counted as the reference casts them."""
+    frames = max(2, min(args.steps, 20))
+    kw = dict(render_args(), anti_aliasing=AA_SAMPLES, aa_seed=12345)
+    scene.ctx.render_frames(frames, width, height, prepare_only=True, **kw)
+    ms = scene.ctx.render_frames(frames, width, height, timed=True, **kw)
+    rays = width * height * (AA_SAMPLES + 1)
+    return {"anti_aliasing": AA_SAMPLES, "frames": frames, "frame_ms": round(ms, 6),
+            "value": round(rays / (ms * 1e-3) / 1e6, 3), "unit": "Mrays/s (all AA rays)",
+            "kernel": "trace_kernel (eray_amd/csrc/trace.hip), brute force per ray"}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -375,6 +393,10 @@ def main() -> None:
     # moving camera: the same frames with a new camera every frame (the setup on the device,
     # inside each frame); one untimed pass captures the path's graphs
     moving = None if args.no_moving_camera else moving_camera(scene, args, width, H_total, render_args, world, allreduce)
+    # the general tracer (anti-aliasing) on the same frames, rank 0 of one GPU, small scenes
+    aa_line = None
+    if world == 1 and not args.no_moving_camera and len(mesh[0]) <= AA_MAX_TRIANGLES:
+        aa_line = anti_aliasing_line(scene, args, width, H_total, render_args)
 
     if rank == 0:
         # the workload a committed counter summary (profiles/pmc_traffic*.json) must match
@@ -429,6 +451,7 @@ def main() -> None:
             "gather_ms": None if gather_ms is None else round(gather_ms, 4),
             "rank_kernel_ms": [round(v, 6) for v in rank_kernel_ms],
             "moving_camera": moving,
+            "anti_aliased": aa_line,
             "gather": ("every frame" if args.gather_every_frame else "final frame") if world > 1 else None,
             **({"rehearsal": "all ranks on GPU 0, gloo collectives: not a measurement"} if rehearsal else {}),
             "hit_pixels": hits_all,
