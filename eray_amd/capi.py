@@ -157,6 +157,7 @@ DEBUG_SIGNATURES = {
     "eray_debug_bin_capacity": (C.c_uint64, [_P]),
     "eray_debug_setup_state": (C.c_int, [_P, _U, _P, C.POINTER(C.c_int32)]),
     "eray_debug_unband": (C.c_int, [_P, _P, _P, _U, _U, _U, _U]),
+    "eray_debug_coded_unband": (C.c_int, [_P, _P, _P, _U, _U, _U, _U]),
 }
 
 _lib = None

@@ -4,12 +4,15 @@
 // a node, one process (one eray context) per GPU: rank r renders the r-th block of PPM file rows
 // (camera rows [H - (r+1) h, H - r h); eray_render's fused out_ppm writes them in file order), and
 // one gather concatenates the blocks on rank 0 in rank order — the PPM body Image::save_as_ppm
-// writes (image.rs:48-74).  One collective per frame, over xGMI: u8 rows, 4x fewer bytes than f32.
+// writes (image.rs:48-74).  u8 rows, 4x fewer bytes than f32.  With interleaved bands (equal work
+// per rank) the rows travel coded (uniform 64-pixel segments as one word) by point-to-point
+// transfers into rank 0, which writes each file row from them.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <cstdio>
 #include <cstring>
+#include <vector>
 
 #include "../../include/eray_hip.h"
 
@@ -50,6 +53,209 @@ __global__ void __launch_bounds__(256) unband_rows_kernel(const uint8_t* __restr
     }
 }
 
+// ---- coded transport of the banded gather -------------------------------------------------
+// A frame is mostly rows of the same colour (engine.rs:212's miss colour, wherever no face is
+// hit), so each rank sends its rows as 64-pixel segments: a uniform segment as one code word
+// (flag bit + its pixel's 3 bytes), any other as its 192 bytes, packed.  Rank 0 receives every
+// rank's code words (4 B per segment) and packed segments and writes each file row from them.
+// At C2's pixel pitch about 1 segment in 30 is not uniform: 6.2 MB of rows per rank become
+// ~0.2 MB, and the gather into rank 0 is no longer bound by its xGMI links.
+constexpr uint32_t kSegPx = 64, kSegBytes = 3 * kSegPx;
+constexpr uint32_t kUniform = 0x80000000u;
+constexpr int kMaxCodedRanks = 64;
+struct RankOffsets {
+    uint32_t v[kMaxCodedRanks];  // first packed segment of each rank in rank 0's staging
+};
+
+// segment g = q * S + s: block row q of the rank's local rows (rows_r valid of rows_max), pixels
+// [64 s, min(64 s + 64, W)).  Its code word: kUniform | b0 | b1 << 8 | b2 << 16 when all its pixels
+// equal the first, else the index of its slot in `packed`, where its bytes are copied (slots
+// taken with one counter atomic per workgroup: in no particular order, the code word says where).
+// *count ends as the number of packed segments (zero on entry).
+// Rows of 16-byte multiples (W % 16 == 0) on 16-byte aligned buffers: 16 lanes per segment, each
+// comparing one 16-byte word with the first pixel's repeating pattern (coalesced, a ballot per
+// segment), then copying the words of the workgroup's non-uniform segments to their slots;
+// otherwise one lane per segment, byte by byte.
+__device__ __forceinline__ void pattern_words(uint32_t c, uint32_t (&d)[3]) {  // the 12-byte period
+    const uint32_t b0 = c & 0xffu, b1 = (c >> 8) & 0xffu, b2 = (c >> 16) & 0xffu;
+    d[0] = b0 | (b1 << 8) | (b2 << 16) | (b0 << 24);
+    d[1] = b1 | (b2 << 8) | (b0 << 16) | (b1 << 24);
+    d[2] = b2 | (b0 << 8) | (b1 << 16) | (b2 << 24);
+}
+// one slot per set bit of `want` (lanes of the wave), from the shared counter
+__device__ __forceinline__ uint32_t wave_slot(unsigned long long want, uint32_t lane, uint32_t* count) {
+    if (!want) return 0u;
+    const uint32_t first = (uint32_t)(__ffsll(want) - 1);
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(count, (uint32_t)__popcll(want));
+    base = (uint32_t)__shfl((int)base, (int)first);
+    return base + (uint32_t)__popcll(want & ((1ull << lane) - 1ull));
+}
+constexpr uint32_t kBlkSegs = 64;  // segments per workgroup of the wide encoder: one slot atomic each
+__global__ void __launch_bounds__(256) seg_encode_wide_kernel(const uint8_t* __restrict__ local, uint32_t rows_r,
+                                                              uint32_t rows_max, uint32_t W, uint32_t S,
+                                                              uint32_t* __restrict__ code, uint8_t* __restrict__ packed,
+                                                              uint32_t* __restrict__ count) {
+    __shared__ uint32_t s_code[kBlkSegs];  // uniform code, or ~0u for a segment to pack
+    __shared__ uint32_t s_slot[kBlkSegs];
+    const uint32_t G = rows_max * S;
+    const uint32_t k = threadIdx.x & 15u, lane = threadIdx.x & 63u;
+    // pass 1: 16 lanes per segment compare its 16-byte words with the first pixel's pattern
+    for (uint32_t it = 0; it < kBlkSegs / 16; ++it) {
+        const uint32_t i = it * 16 + (threadIdx.x >> 4), g = blockIdx.x * kBlkSegs + i;
+        const bool in = g < G;
+        const uint32_t q = in ? g / S : 0u, s = in ? g - q * S : 0u;
+        const bool live = in && q < rows_r;  // (padding rows of a rank with fewer bands: never decoded)
+        const uint32_t words = live ? min(kSegPx, W - s * kSegPx) * 3u / 16u : 0u;
+        const uint4* seg = reinterpret_cast<const uint4*>(local + (size_t)q * W * 3u + (size_t)s * kSegBytes);
+        uint32_t c = 0;
+        bool bad = false;
+        if (live) {
+            c = reinterpret_cast<const uint32_t*>(seg)[0] & 0xffffffu;
+            if (k < words) {
+                uint32_t d[3];
+                pattern_words(c, d);
+                const uint4 v = seg[k];  // dword 4k + j of the segment is period word (k + j) % 3
+                bad = v.x != d[k % 3] || v.y != d[(k + 1) % 3] || v.z != d[(k + 2) % 3] || v.w != d[k % 3];
+            }
+        }
+        const unsigned long long m = __ballot(bad);
+        if (k == 0) s_code[i] = ((m >> (lane & ~15u)) & 0xffffull) ? ~0u : (kUniform | c);
+    }
+    __syncthreads();
+    // one slot atomic for the workgroup's packed segments
+    if (threadIdx.x < kBlkSegs) {
+        const bool want = s_code[threadIdx.x] == ~0u;
+        const unsigned long long bal = __ballot(want);
+        uint32_t base = 0;
+        if (threadIdx.x == 0 && bal) base = atomicAdd(count, (uint32_t)__popcll(bal));
+        base = (uint32_t)__shfl((int)base, 0);
+        s_slot[threadIdx.x] = base + (uint32_t)__popcll(bal & ((1ull << threadIdx.x) - 1ull));
+    }
+    __syncthreads();
+    // pass 2: the code words, and the packed segments' bytes (L2-resident since pass 1)
+    for (uint32_t it = 0; it < kBlkSegs / 16; ++it) {
+        const uint32_t i = it * 16 + (threadIdx.x >> 4), g = blockIdx.x * kBlkSegs + i;
+        if (g >= G) continue;
+        const uint32_t cw = s_code[i];
+        if (cw != ~0u) {
+            if (k == 0) code[g] = cw;
+            continue;
+        }
+        const uint32_t q = g / S, s = g - q * S;
+        const uint32_t words = min(kSegPx, W - s * kSegPx) * 3u / 16u;
+        const uint32_t slot = s_slot[i];
+        if (k == 0) code[g] = slot;
+        if (k < words)
+            reinterpret_cast<uint4*>(packed + (size_t)slot * kSegBytes)[k] =
+                reinterpret_cast<const uint4*>(local + (size_t)q * W * 3u + (size_t)s * kSegBytes)[k];
+    }
+}
+__global__ void __launch_bounds__(256) seg_encode_kernel(const uint8_t* __restrict__ local, uint32_t rows_r,
+                                                         uint32_t rows_max, uint32_t W, uint32_t S,
+                                                         uint32_t* __restrict__ code, uint8_t* __restrict__ packed,
+                                                         uint32_t* __restrict__ count) {
+    const uint32_t g = blockIdx.x * 256u + threadIdx.x, lane = threadIdx.x & 63u;
+    const bool in = g < rows_max * S;
+    const uint32_t q = in ? g / S : 0u, s = in ? g - q * S : 0u;
+    const bool live = in && q < rows_r;
+    const uint8_t* p = local + (size_t)q * W * 3u + (size_t)s * kSegBytes;
+    const uint32_t n = live ? min(kSegPx, W - s * kSegPx) * 3u : 0u;
+    uint32_t b0 = 0, b1 = 0, b2 = 0;
+    bool uniform = true;
+    if (live) {
+        b0 = p[0];
+        b1 = p[1];
+        b2 = p[2];
+        for (uint32_t k = 3; k < n; k += 3) uniform &= p[k] == b0 && p[k + 1] == b1 && p[k + 2] == b2;
+    }
+    const uint32_t slot = wave_slot(__ballot(live && !uniform), lane, count);
+    if (!in) return;
+    if (live && !uniform) {
+        uint8_t* dst = packed + (size_t)slot * kSegBytes;
+        for (uint32_t k = 0; k < n; ++k) dst[k] = p[k];
+        code[g] = slot;
+    } else {
+        code[g] = kUniform | b0 | (b1 << 8) | (b2 << 16);
+    }
+}
+
+// Rank 0: file row F of the frame (camera row Y = H - 1 - F) from rank r = (Y / B) % N, local row
+// j = (Y / (N B)) B + Y % B at that rank's block row rows_r - 1 - j (as unband_rows_kernel), each
+// segment from its code word: the colour repeated, or the packed bytes.
+__device__ __forceinline__ uint8_t code_byte(uint32_t c, uint32_t i) { return (uint8_t)(c >> (8u * (i % 3u))); }
+__global__ void __launch_bounds__(256) seg_decode_kernel(const uint32_t* __restrict__ codes,
+                                                         const uint8_t* __restrict__ packed, RankOffsets off,
+                                                         uint8_t* __restrict__ frame, uint32_t H, uint32_t W,
+                                                         uint32_t S, uint32_t B, uint32_t N, uint32_t rows_max) {
+    const uint32_t F = blockIdx.x;
+    const uint32_t Y = H - 1 - F;
+    const uint32_t r = (Y / B) % N;
+    const uint32_t j = (Y / (N * B)) * B + Y % B;
+    const uint32_t q = band_rows_of(H, B, N, r) - 1 - j;
+    const uint32_t* cr = codes + ((size_t)r * rows_max + q) * S;
+    const uint8_t* pr = packed + (size_t)off.v[r] * kSegBytes;
+    const uint32_t row_bytes = W * 3u;
+    uint8_t* dst = frame + (size_t)F * row_bytes;
+    if ((row_bytes % 16) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0 &&
+        (reinterpret_cast<uintptr_t>(packed) & 15) == 0) {
+        for (uint32_t k = threadIdx.x; k < row_bytes / 16; k += blockDim.x) {
+            const uint32_t s = k / (kSegBytes / 16), w = k - s * (kSegBytes / 16);
+            const uint32_t c = cr[s];
+            uint4 v;
+            if (c & kUniform) {  // dword 4w + t of the segment is period word (w + t) % 3
+                uint32_t d[3];
+                pattern_words(c, d);
+                const uint32_t ph = w % 3u;
+                v = make_uint4(d[ph], d[(ph + 1) % 3u], d[(ph + 2) % 3u], d[ph]);
+            } else {
+                v = reinterpret_cast<const uint4*>(pr + (size_t)c * kSegBytes)[w];
+            }
+            reinterpret_cast<uint4*>(dst)[k] = v;
+        }
+    } else {
+        for (uint32_t k = threadIdx.x; k < row_bytes; k += blockDim.x) {
+            const uint32_t s = k / kSegBytes, i = k - s * kSegBytes;
+            const uint32_t c = cr[s];
+            dst[k] = (c & kUniform) ? code_byte(c, i) : pr[(size_t)c * kSegBytes + i];
+        }
+    }
+}
+
+// Device buffers of one rank's coded gather, carved from one staging allocation (rank 0: a code
+// block and packed room for every rank).
+struct CodedBufs {
+    uint32_t *code, *count, *counts;
+    uint8_t* packed;
+};
+bool coded_bufs(eray_ctx* ctx, uint32_t G, uint32_t slots, uint32_t nranks, CodedBufs* b) {
+    auto up = [](size_t x) { return (x + 255) / 256 * 256; };
+    const size_t n_code = up((size_t)slots * G * 4), n_cnt = up(4u * (nranks + 1));
+    const size_t n_packed = (size_t)slots * G * kSegBytes;
+    uint8_t* base = static_cast<uint8_t*>(eray_internal_staging(ctx, n_code + n_cnt + n_packed));
+    if (!base) return false;
+    b->code = reinterpret_cast<uint32_t*>(base);
+    b->count = reinterpret_cast<uint32_t*>(base + n_code);
+    b->counts = b->count + 1;
+    b->packed = base + n_code + n_cnt;
+    return true;
+}
+
+// Encodes `rows_r` local block rows (of rows_max) into code (G words) and packed; the count of
+// packed segments into *b.count.
+hipError_t encode_rows(const uint8_t* local, uint32_t rows_r, uint32_t rows_max, uint32_t W, uint32_t S,
+                       uint32_t* code, uint8_t* packed, const CodedBufs& b, hipStream_t s) {
+    const uint32_t G = rows_max * S;
+    hipError_t e = hipMemsetAsync(b.count, 0, 4, s);
+    if (e != hipSuccess) return e;
+    const bool wide = (W % 16u) == 0 && ((reinterpret_cast<uintptr_t>(local) | reinterpret_cast<uintptr_t>(packed)) & 15) == 0;
+    if (wide)
+        seg_encode_wide_kernel<<<(G + kBlkSegs - 1) / kBlkSegs, 256, 0, s>>>(local, rows_r, rows_max, W, S, code, packed,
+                                                                             b.count);
+    else
+        seg_encode_kernel<<<(G + 255) / 256, 256, 0, s>>>(local, rows_r, rows_max, W, S, code, packed, b.count);
+    return hipGetLastError();
+}
 
 int nccl_error(eray_ctx* ctx, const char* what, ncclResult_t r) {
     char buf[256];
@@ -118,8 +324,55 @@ int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8
         if (r != ncclSuccess) return nccl_error(ctx, "ncclGather", r);
         return ERAY_OK;
     }
-    // bands: every rank sends rows_max rows (rank 0's count; the others' buffers are padded), rank
-    // 0 gathers them into its staging buffer and puts each row at its file row
+    hipError_t he;
+    if (nranks <= kMaxCodedRanks) {
+        // bands, coded (see seg_classify_kernel): every rank encodes its rows; the packed counts
+        // reach every host (one all-gather of a word each, then a stream synchronisation: the
+        // point-to-point sizes must be known to post them); rank 0 receives every rank's code
+        // words and packed segments and decodes the frame
+        const uint32_t S = (width + kSegPx - 1) / kSegPx, G = rows * S;
+        const uint32_t mine = band_rows_of(height, band_rows, (uint32_t)nranks, (uint32_t)rank);
+        CodedBufs b;
+        if (!coded_bufs(ctx, G, rank == 0 ? (uint32_t)nranks : 1u, (uint32_t)nranks, &b))
+            return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "gather: staging buffer");
+        if ((he = encode_rows(local, mine, rows, width, S, b.code, b.packed, b, s)) != hipSuccess)
+            return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+        r = ncclAllGather(b.count, b.counts, 1, ncclUint32, c, s);
+        if (r != ncclSuccess) return nccl_error(ctx, "ncclAllGather", r);
+        std::vector<uint32_t> counts((size_t)nranks);
+        if ((he = hipMemcpyAsync(counts.data(), b.counts, 4u * (size_t)nranks, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+            (he = hipStreamSynchronize(s)) != hipSuccess)
+            return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+        RankOffsets off{};
+        for (int k = 1; k < nranks; ++k) off.v[k] = off.v[k - 1] + counts[(size_t)k - 1];
+        if (nranks > 1) {
+            if ((r = ncclGroupStart()) != ncclSuccess) return nccl_error(ctx, "ncclGroupStart", r);
+            if (rank == 0) {
+                for (int k = 1; k < nranks && r == ncclSuccess; ++k) {
+                    r = ncclRecv(b.code + (size_t)k * G, G, ncclUint32, k, c, s);
+                    if (r == ncclSuccess && counts[(size_t)k])
+                        r = ncclRecv(b.packed + (size_t)off.v[k] * kSegBytes, (size_t)counts[(size_t)k] * kSegBytes,
+                                     ncclUint8, k, c, s);
+                }
+            } else {
+                r = ncclSend(b.code, G, ncclUint32, 0, c, s);
+                if (r == ncclSuccess && counts[(size_t)rank])
+                    r = ncclSend(b.packed, (size_t)counts[(size_t)rank] * kSegBytes, ncclUint8, 0, c, s);
+            }
+            const ncclResult_t r2 = ncclGroupEnd();
+            if (r != ncclSuccess) return nccl_error(ctx, "ncclSend/ncclRecv", r);
+            if (r2 != ncclSuccess) return nccl_error(ctx, "ncclGroupEnd", r2);
+        }
+        if (rank == 0) {
+            seg_decode_kernel<<<height, 256, 0, s>>>(b.code, b.packed, off, frame, height, width, S, band_rows,
+                                                     (uint32_t)nranks, rows);
+            if ((he = hipGetLastError()) != hipSuccess) return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+        }
+        return ERAY_OK;
+    }
+    // bands, more ranks than the coded offsets hold: every rank sends rows_max rows (rank 0's
+    // count; the others' buffers are padded), rank 0 gathers them into its staging buffer and
+    // puts each row at its file row
     uint8_t* staging = nullptr;
     if (rank == 0) {
         staging = static_cast<uint8_t*>(eray_internal_staging(ctx, bytes * (size_t)nranks));
@@ -134,6 +387,36 @@ int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8
         if (e != hipSuccess) return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(e));
     }
     return ERAY_OK;
+}
+
+// Diagnostics (tests): the coded banded gather of N ranks on one GPU — staging holds the N ranks'
+// padded local PPM blocks; each is encoded into rank 0's code / packed layout as the point-to-
+// point transfers would leave it, then decoded into frame.
+int eray_debug_coded_unband(eray_ctx* ctx, const uint8_t* staging, uint8_t* frame, uint32_t height, uint32_t width,
+                            uint32_t band_rows, uint32_t nranks) {
+    if (!ctx || !staging || !frame || !band_rows || band_rows % 4 || !nranks || nranks > (uint32_t)kMaxCodedRanks)
+        return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "coded unband: bad arguments");
+    if (!height || !width) return ERAY_OK;
+    hipStream_t s = (hipStream_t)eray_get_stream(ctx);
+    const uint32_t rows = band_rows_of(height, band_rows, nranks, 0);
+    const uint32_t S = (width + kSegPx - 1) / kSegPx, G = rows * S;
+    CodedBufs b;
+    if (!coded_bufs(ctx, G, nranks, nranks, &b))
+        return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "coded unband: staging buffer");
+    RankOffsets off{};
+    std::vector<uint32_t> counts(nranks);
+    for (uint32_t k = 0; k < nranks; ++k) {
+        if (k) off.v[k] = off.v[k - 1] + counts[k - 1];
+        const uint8_t* local = staging + (size_t)k * rows * width * 3u;
+        hipError_t e = encode_rows(local, band_rows_of(height, band_rows, nranks, k), rows, width, S,
+                                   b.code + (size_t)k * G, b.packed + (size_t)off.v[k] * kSegBytes, b, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(&counts[k], b.count, 4, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(e));
+    }
+    seg_decode_kernel<<<height, 256, 0, s>>>(b.code, b.packed, off, frame, height, width, S, band_rows, nranks, rows);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? ERAY_OK : eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(e));
 }
 
 // Diagnostics (tests): rank 0's reordering step of the banded gather alone — staging holds the N

@@ -306,8 +306,12 @@ int eray_comm_destroy(void* nccl_comm);
  * interleaved bands r, r + nranks, ... of band_rows camera rows (eray_render_params row0 =
  * r * band_rows, band_stride = nranks * band_rows) — equal work per rank wherever the scene
  * sits — into a local buffer of eray_band_rows(height, band_rows, nranks, 0) rows (rank 0 has
- * the most), and rank 0 puts the rows in file order after the collective.  Replaces the
- * reference's single-process image write (engine.rs:85-98 render_to_path -> save_as_ppm). */
+ * the most), and rank 0 puts the rows in file order.  With bands the rows travel coded: each
+ * 64-pixel row segment whose pixels are all equal as one 4-byte word, the others as their bytes
+ * (a frame is mostly the miss colour, engine.rs:212), so the transfer into rank 0 shrinks with
+ * the background; the packed sizes are exchanged first and the call synchronises the context's
+ * stream once (not capturable in a graph).  Replaces the reference's single-process image
+ * write (engine.rs:85-98 render_to_path -> save_as_ppm). */
 int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8_t* frame, uint32_t height,
                      uint32_t width, uint32_t band_rows);
 /* Camera rows of rank `rank` in the interleaved band split of a frame of `height` rows. */

@@ -105,6 +105,9 @@ def _bands_assemble(gpu, W, H, world, full, band=dist.BAND_ROWS):
             gpu.copy_to_device(staging.ptr + r * alloc * W * 3, out.ppm.numpy().reshape(-1)[: 3 * n * W])
         assert capi.lib().eray_debug_unband(gpu.handle, staging.ptr, frame.ptr, H, W, band, world) == 0
         assert np.array_equal(frame.numpy(), ppm), "banded gather != full frame PPM"
+        gpu.memset(frame.ptr, 0, frame.nbytes)  # the coded transport eray_gather_rows uses
+        assert capi.lib().eray_debug_coded_unband(gpu.handle, staging.ptr, frame.ptr, H, W, band, world) == 0
+        assert np.array_equal(frame.numpy(), ppm), "coded banded gather != full frame PPM"
     finally:
         out.free()
         staging.free()

@@ -2,7 +2,10 @@
 eray_comm_init), on the one GPU of the box: a one-rank communicator gathers a rendered block into
 the frame buffer (and in place).  More ranks need one GPU each (RCCL puts one rank per device):
 the 2-rank split and gather order are covered on CPU (tests/test_dist_rows.py) and the tiles'
-pixels on the GPU (tests/test_gpu_configs.py)."""
+pixels on the GPU (tests/test_gpu_configs.py).  The banded gather's coded transport (uniform
+64-pixel segments as one word, comm.cpp) is checked here rank by rank: N ranks' padded blocks
+encoded into rank 0's layout and decoded (eray_debug_coded_unband) against the plain reorder and a
+numpy restatement of the band split."""
 import numpy as np
 import pytest
 
@@ -32,6 +35,69 @@ def test_one_rank_gather_through_rccl(gpu, cube):
         assert np.array_equal(local.numpy(), want)
         with pytest.raises(capi.ErayError):
             gpu.gather_rows(comm, local.ptr, None, H, W)  # rank 0 needs the frame
+    finally:
+        if comm:
+            capi.comm_destroy(comm)
+        local.free()
+        frame.free()
+        sc.close()
+
+
+def _banded_blocks(frame, H, W, band, world):
+    """Each rank's padded local PPM block (local file order) of a file-order frame, as
+    eray_render writes it for dist.band_split (numpy restatement of eray_band_rows' split)."""
+    cam = frame[::-1]  # camera rows
+    rows_max = len(range(0, H, band * world)) * band
+    blocks = np.zeros((world, rows_max, W, 3), np.uint8)
+    for r in range(world):
+        mine = [y for y in range(H) if (y // band) % world == r]
+        blocks[r, :len(mine)] = cam[mine][::-1]
+    return blocks
+
+
+@pytest.mark.parametrize("W,H,band,world", [(192, 64, 4, 1), (192, 64, 4, 2), (208, 68, 4, 3), (37, 40, 8, 2),
+                                            (1920, 120, 4, 8), (70, 12, 4, 5), (64, 30, 4, 3)])
+def test_coded_banded_gather_layout(gpu, W, H, band, world):
+    rng = np.random.default_rng(W * 7 + H + world)
+    frame = np.empty((H, W, 3), np.uint8)
+    frame[:] = (25, 25, 51)  # mostly the miss colour, uniform segments
+    for _ in range(6):  # patches of noise (non-uniform segments), some at the right edge
+        y, x = rng.integers(0, H), rng.integers(0, W)
+        frame[y:y + rng.integers(1, 9), x:x + rng.integers(1, 90)] = rng.integers(0, 256, (1, 1, 3), dtype=np.uint8)
+        frame[y, x] = rng.integers(0, 256, 3, dtype=np.uint8)
+    frame[H // 2, :] = rng.integers(0, 256, (W, 3), dtype=np.uint8)
+    frame[1] = (7, 8, 9)  # a uniform row of another colour
+    blocks = _banded_blocks(frame, H, W, band, world)
+    assert blocks.shape[1] == capi.lib().eray_band_rows(H, band, world, 0)
+    staging = gpu.to_device(np.ascontiguousarray(blocks))
+    out = gpu.empty((H, W, 3), np.uint8)
+    try:
+        for fn in ("eray_debug_unband", "eray_debug_coded_unband"):
+            gpu.memset(out.ptr, 0, out.nbytes)
+            assert getattr(capi.lib(), fn)(gpu.handle, staging.ptr, out.ptr, H, W, band, world) == 0
+            gpu.synchronize()
+            assert np.array_equal(out.numpy(), frame), fn
+    finally:
+        staging.free()
+        out.free()
+
+
+def test_one_rank_banded_gather_through_rccl(gpu, cube):
+    """eray_gather_rows with bands on a one-rank communicator: the coded transport end to end
+    (encode, the count all-gather, decode) gives the rendered frame."""
+    W, H = 320, 180
+    sc = MainScene(gpu, *cube, W, H, texture=64, fov=(16.0, 9.0))
+    local = gpu.empty((H, W, 3), np.uint8)
+    frame = gpu.empty((H, W, 3), np.uint8)
+    comm = None
+    try:
+        gpu.render(W, H, out_ppm=local.ptr)
+        comm = gpu.comm_init(1, 0, capi.comm_unique_id())
+        for band in (4, 8):
+            gpu.memset(frame.ptr, 0, frame.nbytes)
+            gpu.gather_rows(comm, local.ptr, frame.ptr, H, W, band_rows=band)
+            gpu.synchronize()
+            assert np.array_equal(frame.numpy(), local.numpy()), band
     finally:
         if comm:
             capi.comm_destroy(comm)
