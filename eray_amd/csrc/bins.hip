@@ -321,13 +321,15 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t nparts, 
         st->bin_entries = max(st->bin_entries, found);
         st->bin_overflow |= overflow ? 1u : 0u;
         st->nrect = 0u;
+        st->total_sub = 0u;  // counted by detail_list_kernel
     }
 }
 
 // Sub-block s = sy * (4 * tiles_x) + sx (padded rows: a 64 x 4 block's four sub-blocks are four
 // consecutive threads): listed when some object can be hit there — a binned object's bin is
 // non-empty (the frame kernel's bin of the sub-block, first_hit_binned) or another object's pixel
-// rectangle reaches it.
+// rectangle reaches it.  Ordered form (one-camera setups): flags, then a device-wide compaction
+// in raster order.
 __global__ void __launch_bounds__(kBinWG) detail_flags_kernel(const ObjectDesc* __restrict__ objs, uint32_t nobj,
                                                               uint32_t cam_w, uint32_t row0, uint32_t rows,
                                                               uint32_t band_shift, uint32_t band_mask,
@@ -362,6 +364,58 @@ __global__ void __launch_bounds__(kBinWG) detail_flags_kernel(const ObjectDesc* 
     // the block's four flags: lanes 4b .. 4b + 3 of the wave (row_subs is a multiple of 4)
     const unsigned long long bal = __ballot(hit);
     if (s < n && (threadIdx.x & 3) == 0) occ[s / 4] = (uint8_t)((bal >> (threadIdx.x & 63)) & 0xfu);
+}
+
+// Appended form (camera paths: one launch instead of four): the same flags, the listed sub-blocks
+// appended with one counter atomic per workgroup (raster order within a workgroup's 256
+// sub-blocks; the frame kernel needs no order, though the raster order is 2 % faster at
+// 3840x2160 / 70k, so one-camera setups keep it); the count lands in CamState::total_sub (zeroed
+// by the finaliser).  (Carrying the bin range in the entry,
+// one scalar load fewer per sub-block, measured slower: C3 +0.3 us, 3840x2160 / 70k +1 us.)
+__global__ void __launch_bounds__(kBinWG) detail_list_kernel(const ObjectDesc* __restrict__ objs, uint32_t nobj,
+                                                             uint32_t cam_w, uint32_t row0, uint32_t rows,
+                                                             uint32_t band_shift, uint32_t band_mask,
+                                                             uint32_t band_stride, uint32_t bins_x, uint32_t phase,
+                                                             uint32_t tiles_x, uint32_t n,
+                                                             uint32_t* __restrict__ list, uint8_t* __restrict__ occ,
+                                                             uint32_t* __restrict__ total) {
+    __shared__ uint32_t s_cnt[kBinWG / 64];
+    __shared__ uint32_t s_base;
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t row_subs = 4 * tiles_x;
+    const uint32_t sx = s % row_subs, sy = s / row_subs;
+    bool hit = false;
+    if (s < n && sx * kBinW < cam_w) {
+        const int32_t x0 = (int32_t)(sx * kBinW), x1 = x0 + (int32_t)kBinW - 1;
+        // the sub-block's camera rows (one band: bands are multiples of kBinH rows)
+        const int32_t y0 = (int32_t)band_camera_row(row0, band_shift, band_mask, band_stride, sy * kBinH);
+        const int32_t y1 = y0 + (int32_t)min(kBinH, rows - sy * kBinH) - 1;
+        for (uint32_t oi = 0; oi < nobj && !hit; ++oi) {
+            const ObjGeom& g = objs[oi].g;
+            if (!g.tri_count) continue;
+            if (g.bin_start) {
+                const uint32_t bin = (((uint32_t)y0 + kBinH - phase) / kBinH) * bins_x + sx;
+                hit = g.bin_start[bin + 1] > g.bin_start[bin];
+            } else {
+                hit = x0 <= g.rect[1] && x1 >= g.rect[0] && y0 <= g.rect[3] && y1 >= g.rect[2];
+            }
+        }
+    }
+    // the block's four flags: lanes 4b .. 4b + 3 of the wave (row_subs is a multiple of 4)
+    const unsigned long long bal = __ballot(hit);
+    if (s < n && (threadIdx.x & 3) == 0) occ[s / 4] = (uint8_t)((bal >> (threadIdx.x & 63)) & 0xfu);
+    if (lane == 0) s_cnt[wave] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kBinWG / 64; ++w) {
+        before += w < wave ? s_cnt[w] : 0u;
+        all += s_cnt[w];
+    }
+    if (threadIdx.x == 0) s_base = all ? atomicAdd(total, all) : 0u;
+    __syncthreads();
+    if (hit) list[s_base + before + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = (sy << 16) | sx;
 }
 
 template <typename T>
@@ -435,7 +489,7 @@ hipError_t bins_alloc(BinBuffers& b, uint32_t T, uint32_t nb, const uint32_t* kb
     return hipStreamSynchronize(s);  // the host arrays above are the caller's
 }
 
-hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tiles_x, hipStream_t s) {
+hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tiles_x, bool ordered, hipStream_t s) {
     hipError_t e;
     const size_t keys = (size_t)b.nb * b.nbins;
     size_t tb = b.temp_bytes;
@@ -464,13 +518,20 @@ hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tile
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (!b.nsub) return hipSuccess;
     const uint32_t n = (uint32_t)b.nsub;
-    detail_flags_kernel<<<(n + kBinWG - 1) / kBinWG, kBinWG, 0, s>>>(sp.objs, sp.nobj, sp.W, sp.row0, sp.rows,
-                                                                    sp.band_shift, sp.band_mask, sp.band_stride,
-                                                                    b.bins_x, b.phase, tiles_x, n, b.dflags,
-                                                                    b.dpacked, b.docc);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    tb = b.temp_bytes;
-    return hipcub::DeviceSelect::Flagged(b.temp, tb, b.dpacked, b.dflags, b.dlist, &sp.state->total_sub, (int)n, s);
+    if (ordered) {
+        detail_flags_kernel<<<(n + kBinWG - 1) / kBinWG, kBinWG, 0, s>>>(sp.objs, sp.nobj, sp.W, sp.row0, sp.rows,
+                                                                        sp.band_shift, sp.band_mask, sp.band_stride,
+                                                                        b.bins_x, b.phase, tiles_x, n, b.dflags,
+                                                                        b.dpacked, b.docc);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        tb = b.temp_bytes;
+        return hipcub::DeviceSelect::Flagged(b.temp, tb, b.dpacked, b.dflags, b.dlist, &sp.state->total_sub, (int)n, s);
+    }
+    detail_list_kernel<<<(n + kBinWG - 1) / kBinWG, kBinWG, 0, s>>>(sp.objs, sp.nobj, sp.W, sp.row0, sp.rows,
+                                                                   sp.band_shift, sp.band_mask, sp.band_stride,
+                                                                   b.bins_x, b.phase, tiles_x, n, b.dlist, b.docc,
+                                                                   &sp.state->total_sub);
+    return hipGetLastError();
 }
 
 }  // namespace gpu

@@ -460,10 +460,12 @@ SetupParams setup_params(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint
     return sp;
 }
 
-int enqueue_setup(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint32_t H, const RowSpan& rs) {
+// ordered: the detail list in raster order (one-camera setups, whose list serves many frames);
+// camera paths append it in one launch instead (bins.hip detail_list_kernel)
+int enqueue_setup(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint32_t H, const RowSpan& rs, bool ordered) {
     const SetupParams sp = setup_params(ctx, d_camera, W, H, rs);
     HIP_TRY(ctx, launch_camera_setup(sp, ctx->stream));
-    if (sp.binned) HIP_TRY(ctx, launch_bins_build(sp, ctx->bins, (W + 63) / 64, ctx->stream));
+    if (sp.binned) HIP_TRY(ctx, launch_bins_build(sp, ctx->bins, (W + 63) / 64, ordered, ctx->stream));
     return ERAY_OK;
 }
 
@@ -525,7 +527,7 @@ int sync_setup(eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs, bool wa
                 if (int st = bins_ready()) return st;  // (a grown capacity)
             }
             HIP_TRY(ctx, launch_set_camera(cam_dev(ctx->camera), ctx->d_cam, ctx->stream));
-            if (int st = enqueue_setup(ctx, ctx->d_cam, W, H, rs)) return st;
+            if (int st = enqueue_setup(ctx, ctx->d_cam, W, H, rs, true)) return st;
             HIP_TRY(ctx, hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(CamState), hipMemcpyDeviceToHost,
                                         ctx->stream));
             HIP_TRY(ctx, hipEventRecord(ctx->state_ev, ctx->stream));
@@ -1242,7 +1244,7 @@ int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* rp, const e
     };
     auto frame = [&](const CamDev* cam) -> int {
         if (batched) return batch_frame(cam, 0, 1);
-        if (int st = enqueue_setup(ctx, cam, W, H, row_span(rp))) return st;
+        if (int st = enqueue_setup(ctx, cam, W, H, row_span(rp), false)) return st;
         HIP_TRY(ctx, launch_frame(ctx, p));
         return ERAY_OK;
     };

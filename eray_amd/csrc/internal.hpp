@@ -165,10 +165,10 @@ struct FrameParams {
     uint32_t tiles_x;    // 64 x 4 pixel blocks per row
     uint32_t bins_x;     // screen bins per row
     uint32_t bin_phase;  // bins start at camera rows bin_phase + k * kBinH (row0 % kBinH)
-    // Detail sub-block list (scenes with binned objects, built by build_detail_list): the j-th
+    // Detail sub-block list (scenes with binned objects, bins.hip detail_list_kernel): the j-th
     // detail sub-block is detail_list[j] = sy << 16 | sx (sub-block units, rank-local rows) and
     // bit i of detail_occ[block] marks sub-block i of 64 x 4 block `block` as listed.  Null: the
-    // detail sub-blocks are those of the rectangles above.
+    // detail rectangles enumerate the sub-blocks.
     const uint32_t* detail_list;
     const uint8_t* detail_occ;
     uint32_t detail_wgs;  // most workgroups of the frame kernel's grid doing detail work (0: all)
@@ -334,7 +334,7 @@ void bins_free(BinBuffers& b);
 // narrowed to their non-empty bins and their bin views in the descriptors (or none when the
 // entries overflow the capacity: the frame kernel then scans those objects through LDS tiles),
 // and the detail sub-block list of rows [row0, row0 + rows) with CamState::total_sub.
-hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tiles_x, hipStream_t s);
+hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tiles_x, bool ordered, hipStream_t s);
 hipError_t launch_pack_ppm(const float* rgb, uint32_t w, uint32_t h, uint8_t* out, hipStream_t s);
 
 hipError_t launch_wave(uint32_t w, uint32_t h, float xf, float yf, float* out, hipStream_t s);
