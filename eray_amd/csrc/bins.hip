@@ -37,24 +37,26 @@ namespace {
 constexpr int kBinWG = 256;
 constexpr uint32_t kPairGrid = 2048;  // workgroups of the grid-stride pair and scatter loops
 
-__device__ __forceinline__ unsigned long long total_pairs(const unsigned long long* first,
-                                                          const unsigned long long* area, uint32_t T) {
-    return T ? first[T - 1] + area[T - 1] : 0ull;
-}
 
 // (face, bin) pairs of the binned faces' bin rectangles (face-major, each rectangle row-major):
 // the non-empty ones appended to the entry list, counted per bin key
 __global__ void __launch_bounds__(kBinWG) bin_pairs_kernel(const TriCull* __restrict__ cull,
                                                            const int4* __restrict__ range,
-                                                           const unsigned long long* __restrict__ first,
-                                                           const unsigned long long* __restrict__ area,
+                                                           const unsigned long long* __restrict__ first_local,
+                                                           const unsigned long long* __restrict__ boff,
+                                                           uint32_t nparts, uint32_t chunk,
                                                            const uint32_t* __restrict__ fkey, uint32_t T, uint32_t W,
                                                            uint32_t H, uint32_t phase, uint32_t bins_x, uint32_t nbins,
                                                            uint32_t cap, uint32_t* __restrict__ n,
                                                            uint32_t* __restrict__ count, uint32_t* __restrict__ ekey,
                                                            uint32_t* __restrict__ eface,
                                                            unsigned long long* __restrict__ emask) {
-    const unsigned long long P = total_pairs(first, area, T);
+    // face i's first pair: its setup chunk's offset + its place in the chunk's own scan
+    __shared__ unsigned long long s_boff[kSetupMaxBlocks + 1];
+    for (uint32_t b = threadIdx.x; b <= nparts; b += kBinWG) s_boff[b] = boff[b];
+    __syncthreads();
+    auto first = [&](uint32_t i) { return s_boff[i / chunk] + first_local[i]; };
+    const unsigned long long P = s_boff[nparts];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     __shared__ uint32_t s_cnt[kBinWG / 64];
     __shared__ uint32_t s_base;
@@ -69,13 +71,13 @@ __global__ void __launch_bounds__(kBinWG) bin_pairs_kernel(const TriCull* __rest
             uint32_t lo = 0, hi = T;  // first face whose first pair is > j
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (first[mid] <= j) lo = mid + 1;
+                if (first(mid) <= j) lo = mid + 1;
                 else hi = mid;
             }
             i = lo - 1;
             const int4 g = range[i];
             const uint32_t w = (uint32_t)(g.y - g.x + 1);
-            const uint32_t c = (uint32_t)(j - first[i]);
+            const uint32_t c = (uint32_t)(j - first(i));
             const uint32_t tx = (uint32_t)g.x + c % w, ty = (uint32_t)g.z + c / w;
             m = bin_pixels(cull[i], W, H, phase, tx, ty);
             key = fkey[i] * nbins + ty * bins_x + tx;
@@ -431,7 +433,7 @@ hipError_t grow(T** p, size_t need) {
 }  // namespace
 
 void bins_free(BinBuffers& b) {
-    void* ptrs[] = {b.first, b.count,  b.start,  b.kbegin, b.kobj,   b.n,       b.done,    b.acc,   b.part, b.ekey,
+    void* ptrs[] = {b.first, b.boff, b.count,  b.start,  b.kbegin, b.kobj,   b.n,       b.done,    b.acc,   b.part, b.ekey,
                     b.eface, b.emask,  b.tri,    b.mask,   b.hot,    b.dflags,  b.dpacked, b.dlist, b.docc,
                     b.sortq, b.nsort,  b.temp};
     for (void* p : ptrs)
@@ -454,7 +456,7 @@ hipError_t bins_alloc(BinBuffers& b, uint32_t T, uint32_t nb, const uint32_t* kb
     const size_t keys = (size_t)nb * b.nbins;
     const uint32_t subs_y = (rows + kBinH - 1) / kBinH;
     b.nsub = 4 * (size_t)tiles_x * subs_y;
-    if ((e = grow(&b.first, T)) != hipSuccess || (e = grow(&b.count, keys + 1)) != hipSuccess ||
+    if ((e = grow(&b.first, T)) != hipSuccess || (e = grow(&b.boff, kSetupMaxBlocks + 1)) != hipSuccess || (e = grow(&b.count, keys + 1)) != hipSuccess ||
         (e = grow(&b.start, keys + 1)) != hipSuccess || (e = grow(&b.kbegin, nb)) != hipSuccess ||
         (e = grow(&b.kobj, nb)) != hipSuccess || (e = grow(&b.n, 1)) != hipSuccess ||
         (e = grow(&b.done, 1)) != hipSuccess || (e = grow(&b.acc, 4 * (size_t)nb)) != hipSuccess ||
@@ -475,11 +477,9 @@ hipError_t bins_alloc(BinBuffers& b, uint32_t T, uint32_t nb, const uint32_t* kb
         (e = hipMemcpyAsync(b.kbegin, kbegin, sizeof(uint32_t) * nb, hipMemcpyHostToDevice, s)) != hipSuccess ||
         (e = hipMemcpyAsync(b.kobj, kobj, sizeof(uint32_t) * nb, hipMemcpyHostToDevice, s)) != hipSuccess)
         return e;
-    // hipcub scratch: the largest of the three device-wide passes
+    // hipcub scratch: the larger of the two device-wide passes
     size_t t1 = 0, t2 = 0, t3 = 0;
-    if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, t1, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                              (int)std::max<uint32_t>(T, 1u), s)) != hipSuccess ||
-        (e = hipcub::DeviceScan::ExclusiveSum(nullptr, t2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)(keys + 1), s)) !=
+    if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, t2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)(keys + 1), s)) !=
             hipSuccess ||
         (e = hipcub::DeviceSelect::Flagged(nullptr, t3, (uint32_t*)nullptr, (uint8_t*)nullptr, (uint32_t*)nullptr,
                                            (uint32_t*)nullptr, (int)std::max<size_t>(b.nsub, 1), s)) != hipSuccess)
@@ -494,8 +494,8 @@ hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tile
     const size_t keys = (size_t)b.nb * b.nbins;
     size_t tb = b.temp_bytes;
     if (b.T) {
-        if ((e = hipcub::DeviceScan::ExclusiveSum(b.temp, tb, sp.area, b.first, (int)b.T, s)) != hipSuccess) return e;
-        bin_pairs_kernel<<<kPairGrid, kBinWG, 0, s>>>(sp.cull, sp.range, b.first, sp.area, sp.fkey, b.T, sp.W, sp.H,
+        const uint32_t nparts = setup_blocks(b.T), chunk = (b.T + nparts - 1) / nparts;  // as camera_setup_kernel
+        bin_pairs_kernel<<<kPairGrid, kBinWG, 0, s>>>(sp.cull, sp.range, b.first, b.boff, nparts, chunk, sp.fkey, b.T, sp.W, sp.H,
                                                       sp.phase, b.bins_x, b.nbins, (uint32_t)b.cap, b.n, b.count,
                                                       b.ekey, b.eface, b.emask);
         if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -456,6 +456,8 @@ SetupParams setup_params(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint
         sp.fkey = ctx->d_fkey;
         sp.bins_x = ctx->bins.bins_x;
         sp.phase = ctx->bins.phase;
+        sp.first_local = ctx->bins.first;
+        sp.boff = ctx->bins.boff;
     }
     return sp;
 }

@@ -244,6 +244,12 @@ hipError_t launch_tri_precompute(const float* pos, const float* nrm, const float
 // scenes without binned objects, the merged detail rectangles of the rendered rows (CamState).
 // camera_setup_kernel's grid: at most this many workgroups, each a contiguous chunk of triangles
 constexpr uint32_t kSetupMaxBlocks = 256;
+// camera_setup_kernel's chunk workgroups for T triangles (each a contiguous chunk of
+// ceil(T / blocks) faces)
+inline uint32_t setup_blocks(uint32_t T) {
+    const uint32_t b = (T + 255u) / 256u;
+    return T ? (b < kSetupMaxBlocks ? b : kSetupMaxBlocks) : 1u;
+}
 struct SetupParams {
     const TriHot* hot;
     TriCull* cull;
@@ -268,6 +274,11 @@ struct SetupParams {
     uint32_t* fkey;
     uint32_t bins_x, phase;
     const ObjectDesc* objs_src;  // batched setups: the scene's descriptors, copied into each slot
+    // binned faces' first (face, bin) pair: the exclusive scan of `area`, as each chunk
+    // workgroup's own scan (first_local) plus its chunk's offset boff[b] (kSetupMaxBlocks + 1
+    // entries; boff[nparts] = all pairs) — bins.hip bin_pairs_kernel reads them
+    unsigned long long* first_local;
+    unsigned long long* boff;
 };
 hipError_t launch_camera_setup(const SetupParams& sp, hipStream_t s);
 // The setups of `ncam` cameras sp.cam[0 .. ncam) at once, one workgroup each, into per-camera
@@ -298,7 +309,9 @@ hipError_t launch_trace(const FrameParams& p, hipStream_t s);
 struct BinBuffers {
     uint32_t nb = 0, nbins = 0, bins_x = 0, bins_y = 0, phase = 0, T = 0;
     size_t cap = 0;                       // entry capacity
-    unsigned long long* first = nullptr;  // exclusive scan of SetupParams::area (T)
+    unsigned long long* first = nullptr;  // SetupParams::first_local (T)
+    unsigned long long* boff = nullptr;   // SetupParams::boff (kSetupMaxBlocks + 1)
+    uint32_t nparts = 0, chunk = 0;       // the setup's chunk workgroups and faces per chunk
     uint32_t* count = nullptr;            // per key (nb * nbins + 1), zero between builds
     uint32_t* start = nullptr;            // per key + 1
     uint32_t* kbegin = nullptr;           // tri_begin per binned object

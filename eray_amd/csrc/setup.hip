@@ -160,6 +160,30 @@ constexpr uint32_t kSpan = kSetupWG;  // objects per workgroup reduced in LDS (m
 constexpr uint32_t kTab = 2048;       // objects the last workgroup combines in LDS (more: in acc)
 static_assert(kSetupBatchMaxObjects <= kSpan, "a batched setup keeps every object's union in LDS");
 
+// exclusive scan of v over the workgroup (thread order); *total gets the sum.  s_w: 4 words of
+// LDS, free on entry and on return.
+__device__ __forceinline__ unsigned long long block_exclusive_scan(unsigned long long v, unsigned long long* s_w,
+                                                                   unsigned long long* total) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned long long incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned long long y = __shfl_up(incl, off);
+        if ((int)lane >= off) incl += y;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    unsigned long long before = 0, all = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kSetupWG / 64; ++w) {
+        before += w < wave ? s_w[w] : 0ull;
+        all += s_w[w];
+    }
+    *total = all;
+    __syncthreads();
+    return before + incl - v;
+}
+
 __device__ __forceinline__ void max4(uint32_t* dst, const uint32_t (&a)[4]) {
     for (int k = 0; k < 4; ++k) atomicMax(dst + k, a[k]);
 }
@@ -174,6 +198,7 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp, 
     __shared__ double s_poly[16 * kSetupWG];  // face_rect's clip output, 128 B per thread
     __shared__ uint32_t s_acc[kSpan][4];      // this workgroup's objects (o - o_first)
     __shared__ uint32_t s_tab[kTab][4];       // the last workgroup's per-object unions
+    __shared__ unsigned long long s_scan[kSetupWG / 64];
     if (kMode == 3) {  // camera blockIdx.x of the batch: its slots
         sp.cam += blockIdx.x;
         sp.cull += (size_t)blockIdx.x * sp.T;
@@ -189,33 +214,51 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp, 
     for (uint32_t j = tid; j < kSpan; j += kSetupWG)
         for (int k = 0; k < 4; ++k) s_acc[j][k] = 0u;
     __syncthreads();
-    for (uint32_t i = lo + tid; i < hi && kMode != 2; i += kSetupWG) {
-        const TriCull c = cull_record(sp.hot[i], cam);
-        sp.cull[i] = c;
-        const uint32_t obj = object_of(sp.obj_begin, sp.nobj, i);
-        int32_t r[4];
-        const bool any = face_rect(c, sp.W, sp.H, r, s_poly + tid, kSetupWG);
-        if (any) {
-            uint32_t a[4];
-            rect_words(r, a);
-            if (obj - o_first < kSpan) max4(s_acc[obj - o_first], a);
-            else max4(sp.acc + 4 * obj, a);  // (a workgroup spanning very many objects)
-        }
-        if (sp.range) {  // bins.hip: the face's bin rectangle, if its object is binned
-            const uint32_t k = sp.objkey[obj];
-            int4 g = make_int4(1, 0, 1, 0);
-            unsigned long long ar = 0;
-            if (k != ~0u && any) {
-                // bin row of camera row y: (y + kBinH - phase) / kBinH
-                g = make_int4(r[0] / (int32_t)kBinW, r[1] / (int32_t)kBinW,
-                              (r[2] + (int32_t)kBinH - (int32_t)sp.phase) / (int32_t)kBinH,
-                              (r[3] + (int32_t)kBinH - (int32_t)sp.phase) / (int32_t)kBinH);
-                ar = (unsigned long long)(g.y - g.x + 1) * (unsigned long long)(g.w - g.z + 1);
+    unsigned long long run = 0;  // binned faces: pairs of this chunk's faces so far
+    for (uint32_t i0 = lo; i0 < hi && kMode != 2; i0 += kSetupWG) {  // workgroup-uniform
+        const uint32_t i = i0 + tid;
+        unsigned long long ar = 0;
+        if (i < hi) {
+            const TriCull c = cull_record(sp.hot[i], cam);
+            sp.cull[i] = c;
+            const uint32_t obj = object_of(sp.obj_begin, sp.nobj, i);
+            int32_t r[4];
+            const bool any = face_rect(c, sp.W, sp.H, r, s_poly + tid, kSetupWG);
+            if (any) {
+                uint32_t a[4];
+                rect_words(r, a);
+                if (obj - o_first < kSpan) max4(s_acc[obj - o_first], a);
+                else max4(sp.acc + 4 * obj, a);  // (a workgroup spanning very many objects)
             }
-            sp.range[i] = g;
-            sp.area[i] = ar;
-            sp.fkey[i] = k;
+            if (sp.range) {  // bins.hip: the face's bin rectangle, if its object is binned
+                const uint32_t k = sp.objkey[obj];
+                int4 g = make_int4(1, 0, 1, 0);
+                if (k != ~0u && any) {
+                    // bin row of camera row y: (y + kBinH - phase) / kBinH
+                    g = make_int4(r[0] / (int32_t)kBinW, r[1] / (int32_t)kBinW,
+                                  (r[2] + (int32_t)kBinH - (int32_t)sp.phase) / (int32_t)kBinH,
+                                  (r[3] + (int32_t)kBinH - (int32_t)sp.phase) / (int32_t)kBinH);
+                    ar = (unsigned long long)(g.y - g.x + 1) * (unsigned long long)(g.w - g.z + 1);
+                }
+                sp.range[i] = g;
+                sp.area[i] = ar;
+                sp.fkey[i] = k;
+            }
         }
+        if (sp.range) {  // the chunk's exclusive scan of the areas, in face order
+            unsigned long long all = 0;
+            const unsigned long long ex = block_exclusive_scan(ar, s_scan, &all);
+            if (i < hi) sp.first_local[i] = run + ex;
+            run += all;
+        }
+    }
+    if (kMode == 1 && sp.range && tid == 0) sp.boff[blockIdx.x] = run;  // the chunk's total
+    if (kMode == 2 && sp.range) {  // chunk totals -> chunk offsets, and all pairs at [nparts]
+        unsigned long long all = 0;
+        const unsigned long long v = tid < nparts ? sp.boff[tid] : 0ull;
+        const unsigned long long ex = block_exclusive_scan(v, s_scan, &all);
+        if (tid < nparts) sp.boff[tid] = ex;
+        if (tid == 0) sp.boff[nparts] = all;
     }
     __syncthreads();
     constexpr bool single = kMode == 0 || kMode == 3;
@@ -376,8 +419,8 @@ __global__ void set_camera_kernel(CamDev cam, CamDev* slot) {
 }  // namespace
 
 hipError_t launch_camera_setup(const SetupParams& sp, hipStream_t s) {
-    const uint32_t blocks = sp.T ? min((sp.T + kSetupWG - 1) / kSetupWG, kSetupMaxBlocks) : 1u;
-    if (blocks == 1) {
+    const uint32_t blocks = setup_blocks(sp.T);
+    if (blocks == 1 && !sp.range) {  // (binned faces' pair offsets come from the two-kernel form)
         camera_setup_kernel<0><<<1, kSetupWG, 0, s>>>(sp, 1u);
         return hipGetLastError();
     }
