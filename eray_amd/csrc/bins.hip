@@ -68,10 +68,20 @@ __global__ void __launch_bounds__(kBinWG) bin_pairs_kernel(const TriCull* __rest
         unsigned long long m = 0;
         uint32_t key = 0, i = 0;
         if (j < P) {
-            uint32_t lo = 0, hi = T;  // first face whose first pair is > j
+            // the chunk: the last one starting at or before j (in LDS; an empty chunk never is, the
+            // next one starts at the same pair) ...
+            uint32_t cb = 0, ce = nparts;
+            while (ce - cb > 1) {
+                const uint32_t mid = (cb + ce) >> 1;
+                if (s_boff[mid] <= j) cb = mid;
+                else ce = mid;
+            }
+            // ... then, inside it, the last face whose first pair is <= j
+            const unsigned long long jl = j - s_boff[cb];
+            uint32_t lo = cb * chunk, hi = min(lo + chunk, T);
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (first(mid) <= j) lo = mid + 1;
+                if (first_local[mid] <= jl) lo = mid + 1;
                 else hi = mid;
             }
             i = lo - 1;

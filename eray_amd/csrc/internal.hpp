@@ -244,7 +244,7 @@ hipError_t launch_tri_precompute(const float* pos, const float* nrm, const float
 // the device descriptors), for binned objects each face's bin rectangle (bins.hip), and, for
 // scenes without binned objects, the merged detail rectangles of the rendered rows (CamState).
 // camera_setup_kernel's grid: at most this many workgroups, each a contiguous chunk of triangles
-constexpr uint32_t kSetupMaxBlocks = 256;
+constexpr uint32_t kSetupMaxBlocks = 1024;
 // camera_setup_kernel's chunk workgroups for T triangles (each a contiguous chunk of
 // ceil(T / blocks) faces)
 inline uint32_t setup_blocks(uint32_t T) {

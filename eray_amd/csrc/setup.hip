@@ -197,7 +197,7 @@ template <int kMode>
 __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp, uint32_t nparts) {
     __shared__ double s_poly[16 * kSetupWG];  // face_rect's clip output, 128 B per thread
     __shared__ uint32_t s_acc[kSpan][4];      // this workgroup's objects (o - o_first)
-    __shared__ uint32_t s_tab[kTab][4];       // the last workgroup's per-object unions
+    __shared__ uint32_t s_tab[kMode == 1 ? 1 : kTab][4];  // the combining workgroup's per-object unions
     __shared__ unsigned long long s_scan[kSetupWG / 64];
     if (kMode == 3) {  // camera blockIdx.x of the batch: its slots
         sp.cam += blockIdx.x;
@@ -254,10 +254,22 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp, 
     }
     if (kMode == 1 && sp.range && tid == 0) sp.boff[blockIdx.x] = run;  // the chunk's total
     if (kMode == 2 && sp.range) {  // chunk totals -> chunk offsets, and all pairs at [nparts]
+        constexpr uint32_t kPer = kSetupMaxBlocks / kSetupWG;  // chunks per thread, consecutive
+        unsigned long long v[kPer], sum = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) {
+            const uint32_t b = tid * kPer + k;
+            v[k] = b < nparts ? sp.boff[b] : 0ull;
+            sum += v[k];
+        }
         unsigned long long all = 0;
-        const unsigned long long v = tid < nparts ? sp.boff[tid] : 0ull;
-        const unsigned long long ex = block_exclusive_scan(v, s_scan, &all);
-        if (tid < nparts) sp.boff[tid] = ex;
+        unsigned long long ex = block_exclusive_scan(sum, s_scan, &all);
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) {
+            const uint32_t b = tid * kPer + k;
+            if (b < nparts) sp.boff[b] = ex;
+            ex += v[k];
+        }
         if (tid == 0) sp.boff[nparts] = all;
     }
     __syncthreads();
