@@ -520,10 +520,8 @@ hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tile
                                                          b.acc, b.part, b.done, b.n, (uint32_t)b.cap, b.kobj, sp.objs,
                                                          b.tri, b.mask, b.hot, b.sortq, b.nsort, sp.state);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (ordered) {  // camera paths skip the sort (their frames key the search by face index)
-        bin_sort_kernel<<<kSortGrid, kBinWG, 0, s>>>(b.sortq, b.nsort, b.start, b.tri, b.mask, b.hot);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
+    bin_sort_kernel<<<kSortGrid, kBinWG, 0, s>>>(b.sortq, b.nsort, b.start, b.tri, b.mask, b.hot);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     bins_finalize_kernel<true><<<1, kBinWG, 0, s>>>(fgrid, b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase, b.acc,
                                                     b.part, b.done, b.n, (uint32_t)b.cap, b.kobj, sp.objs, b.tri, b.mask,
                                                     b.hot, b.sortq, b.nsort, sp.state);

@@ -1200,9 +1200,8 @@ int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* rp, const e
         if (mean_frame_ms) HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         return ERAY_OK;
     }
-    // device-camera mode: every frame reads its setup's CamState; the bins are left unsorted
+    // device-camera mode: every frame reads its setup's CamState
     p.cam_state = ctx->d_state;
-    p.bins_unsorted = 1;
     p.nrect = 0;
     std::memset(p.rects, 0, sizeof p.rects);
     // the cameras: staged in pinned memory, copied to the device once per call; each graph chunk

@@ -171,7 +171,6 @@ struct FrameParams {
     // detail rectangles enumerate the sub-blocks.
     const uint32_t* detail_list;
     const uint8_t* detail_occ;
-    uint32_t bins_unsorted;  // the bins of 65..kBinSortMax entries are not sorted (camera paths)
     uint32_t detail_wgs;  // most workgroups of the frame kernel's grid doing detail work (0: all)
     uint32_t fill_first;  // the fill workgroups take the grid's first block indices (dispatched first)
     uint32_t separate_fill;  // the frame kernel does detail work only; fill_kernel writes the background

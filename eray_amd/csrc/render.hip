@@ -564,7 +564,7 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
         BinLds& T = *reinterpret_cast<BinLds*>(s_bins + w * kBinLdsBytes);  // the chunk's sub-block
         const uint32_t lo_w = s_range[2 * w], end = s_range[2 * w + 1];
         const uint32_t base = lo_w + 64 * c;
-        const bool sorted = !p.bins_unsorted && end - lo_w > 64 && end - lo_w <= kBinSortMax;  // workgroup-uniform
+        const bool sorted = end - lo_w > 64 && end - lo_w <= kBinSortMax;  // workgroup-uniform
         const uint32_t j = base + lane;
         uint32_t fj = 0xffffffffu;  // the entry's order key
         unsigned long long pm = 0;
@@ -650,7 +650,7 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
     const uint32_t mine = L.best[lane];
     if (st == kSearching && mine != 0xffffffffu) {
         float u, v, t;
-        if (!p.bins_unsorted && hi - lo > 64 && hi - lo <= kBinSortMax) {  // the winner again, for u, v, t
+        if (hi - lo > 64 && hi - lo <= kBinSortMax) {  // the winner again, for u, v, t
             exact_test(ob.bin_hot[mine], o, d, u, v, t);
             found = (int)ob.bin_tri[mine];
         } else {
