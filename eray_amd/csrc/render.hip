@@ -31,6 +31,13 @@
 #include "internal.hpp"
 #include "hit.hpp"
 
+// Per-workgroup timestamps for a diagnostics build (scripts/microbench/render_trace.hip defines
+// it before including this file); nothing in the product build.
+#ifndef ERAY_TRACE_POINT
+#define ERAY_TRACE_POINT(k)
+#define ERAY_TRACE_WAVE0(k)
+#endif
+
 namespace eray {
 namespace gpu {
 namespace {
@@ -834,6 +841,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const CamDev& c
     const Bundle bd = make_bundle(p, rm, wx0, min(wx0 + kSubW - 1, p.cam_w - 1), py0, min(py0 + kBlkH - 1, p.rows - 1));
 
     // ---- cast_ray (engine.rs:112-216): closest object among first hits -----------
+    ERAY_TRACE_WAVE0(4);
     f3 d = given_d ? *given_d : mk3(0.0f, 0.0f, 0.0f);  // the camera ray, when the caller has it
     bool ray_ready = given_d != nullptr;
     bool have = false;
@@ -883,6 +891,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const CamDev& c
         }
     }
 
+    ERAY_TRACE_WAVE0(5);
     // ---- hit data and Material::get (material.rs:56-94) --------------------------
     // The object loop only finds each lane's texel addresses; the loads are issued once after
     // it and first used by the shading, so their latency overlaps the shadow rays.
@@ -1055,6 +1064,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const CamDev& c
         push(rgb{0.1f, 0.1f, 0.2f});  // engine.rs:208-213
     }
 
+    ERAY_TRACE_WAVE0(6);
     // ---- outputs: Image::set + Color::as_bytes, rows bottom-up (image.rs:41-74) ---
     const uint32_t b0 = sat_u8(acc.r * 255.0f), b1 = sat_u8(acc.g * 255.0f), b2 = sat_u8(acc.b * 255.0f);
     if (valid && p.out_face) p.out_face[(size_t)py * p.img_w + px] = have ? best_face : -1;
@@ -1106,6 +1116,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const CamDev& c
             o[2] = (uint8_t)b2;
         }
     }
+    ERAY_TRACE_WAVE0(7);
 }
 
 // detail rectangle k of the frame (kernel arguments, or the setup's CamState in device-camera
@@ -1225,6 +1236,7 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     // the fill roles go to the first-dispatched (older, VALU-priority) workgroups
     const uint32_t bid = (fill_first && nd < grid) ? (blockIdx.x + nd) % grid : blockIdx.x;
 
+    ERAY_TRACE_POINT(0);
     // ---- detail sub-blocks -------------------------------------------------------------------
     if (bid < nd) {
         const uint32_t nrect = p.detail_list ? 0u : frame_nrect<kDev>(p);
@@ -1281,6 +1293,7 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
             first_rays();
             detail(sc);
         }
+        ERAY_TRACE_POINT(1);
         if (nd < grid) {
             return;
         }
@@ -1290,7 +1303,9 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     if (separate_fill) return;  // fill_kernel writes the background beside this launch
     const uint32_t nf = nd < grid ? grid - nd : grid;  // filling workgroups
     const uint32_t f = nd < grid ? bid - nd : bid;
+    ERAY_TRACE_POINT(2);
     fill_blocks<kDev>(p, f, nf, wave, lane, aligned);
+    ERAY_TRACE_POINT(3);
 }
 
 // The background alone, beside a detail-only frame kernel on another stream (FrameParams::
