@@ -340,19 +340,24 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t nparts, 
 // Sub-block s = sy * (4 * tiles_x) + sx (padded rows: a 64 x 4 block's four sub-blocks are four
 // consecutive threads): listed when some object can be hit there — a binned object's bin is
 // non-empty (the frame kernel's bin of the sub-block, first_hit_binned) or another object's pixel
-// rectangle reaches it.  Ordered form (one-camera setups): flags, then a device-wide compaction
-// in raster order.
+// rectangle reaches it.  Ordered form (one-camera setups): flags, then device-wide compactions in
+// raster order — first the heavy sub-blocks (a bin of more than one 64-entry chunk), then the
+// others.  The frame kernel deals the list out in rounds of one sub-block per detail wave, so the
+// heavy ones go in the first round and the last round holds only one-chunk sub-blocks
+// (3840x2160 / 70k: two rounds, and the second one's slowest workgroups set the frame's end,
+// profiles/r02/trace/).  Any order gives the same image.
 __global__ void __launch_bounds__(kBinWG) detail_flags_kernel(const ObjectDesc* __restrict__ objs, uint32_t nobj,
                                                               uint32_t cam_w, uint32_t row0, uint32_t rows,
                                                               uint32_t band_shift, uint32_t band_mask,
                                                               uint32_t band_stride,
                                                               uint32_t bins_x, uint32_t phase, uint32_t tiles_x,
                                                               uint32_t n, uint8_t* __restrict__ flags,
+                                                              uint8_t* __restrict__ flags_light,
                                                               uint32_t* __restrict__ packed, uint8_t* __restrict__ occ) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t row_subs = 4 * tiles_x;
     const uint32_t sx = s % row_subs, sy = s / row_subs;
-    bool hit = false;
+    bool hit = false, heavy = false;
     if (s < n && sx * kBinW < cam_w) {
         const int32_t x0 = (int32_t)(sx * kBinW), x1 = x0 + (int32_t)kBinW - 1;
         // the sub-block's camera rows (one band: bands are multiples of kBinH rows)
@@ -364,13 +369,15 @@ __global__ void __launch_bounds__(kBinWG) detail_flags_kernel(const ObjectDesc* 
             if (g.bin_start) {
                 const uint32_t bin = (((uint32_t)y0 + kBinH - phase) / kBinH) * bins_x + sx;
                 hit = g.bin_start[bin + 1] > g.bin_start[bin];
+                heavy = g.bin_start[bin + 1] - g.bin_start[bin] > 64u;
             } else {
                 hit = x0 <= g.rect[1] && x1 >= g.rect[0] && y0 <= g.rect[3] && y1 >= g.rect[2];
             }
         }
     }
     if (s < n) {
-        flags[s] = hit ? 1 : 0;
+        flags[s] = (hit && heavy) ? 1 : 0;
+        flags_light[s] = (hit && !heavy) ? 1 : 0;
         packed[s] = (sy << 16) | sx;
     }
     // the block's four flags: lanes 4b .. 4b + 3 of the wave (row_subs is a multiple of 4)
@@ -430,6 +437,16 @@ __global__ void __launch_bounds__(kBinWG) detail_list_kernel(const ObjectDesc* _
     if (hit) list[s_base + before + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = (sy << 16) | sx;
 }
 
+// The light sub-blocks after the heavy ones (ordered detail list); the list's length into CamState.
+__global__ void __launch_bounds__(kBinWG) detail_append_kernel(const uint32_t* __restrict__ light,
+                                                               const uint32_t* __restrict__ counts,
+                                                               uint32_t* __restrict__ list, CamState* st) {
+    const uint32_t heavy = counts[0], nl = counts[1];
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += gridDim.x * blockDim.x)
+        list[heavy + i] = light[i];
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->total_sub = heavy + nl;
+}
+
 template <typename T>
 hipError_t grow(T** p, size_t need) {
     if (*p) {
@@ -445,7 +462,7 @@ hipError_t grow(T** p, size_t need) {
 void bins_free(BinBuffers& b) {
     void* ptrs[] = {b.first, b.boff, b.count,  b.start,  b.kbegin, b.kobj,   b.n,       b.done,    b.acc,   b.part, b.ekey,
                     b.eface, b.emask,  b.tri,    b.mask,   b.hot,    b.dflags,  b.dpacked, b.dlist, b.docc,
-                    b.sortq, b.nsort,  b.temp};
+                    b.sortq, b.nsort,  b.temp,   b.dflags_light, b.dlight, b.dcount};
     for (void* p : ptrs)
         if (p) hipFree(p);
     b = BinBuffers{};
@@ -475,6 +492,8 @@ hipError_t bins_alloc(BinBuffers& b, uint32_t T, uint32_t nb, const uint32_t* kb
         (e = grow(&b.emask, cap)) != hipSuccess || (e = grow(&b.tri, cap)) != hipSuccess ||
         (e = grow(&b.mask, cap)) != hipSuccess || (e = grow(&b.hot, cap)) != hipSuccess ||
         (e = grow(&b.dflags, b.nsub)) != hipSuccess || (e = grow(&b.dpacked, b.nsub)) != hipSuccess ||
+        (e = grow(&b.dflags_light, b.nsub)) != hipSuccess || (e = grow(&b.dlight, b.nsub)) != hipSuccess ||
+        (e = grow(&b.dcount, 2)) != hipSuccess ||
         (e = grow(&b.dlist, b.nsub)) != hipSuccess || (e = grow(&b.docc, (size_t)tiles_x * subs_y)) != hipSuccess ||
         (e = grow(&b.sortq, std::max<size_t>(keys, 1))) != hipSuccess || (e = grow(&b.nsort, 1)) != hipSuccess)
         return e;
@@ -532,10 +551,19 @@ hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tile
         detail_flags_kernel<<<(n + kBinWG - 1) / kBinWG, kBinWG, 0, s>>>(sp.objs, sp.nobj, sp.W, sp.row0, sp.rows,
                                                                         sp.band_shift, sp.band_mask, sp.band_stride,
                                                                         b.bins_x, b.phase, tiles_x, n, b.dflags,
-                                                                        b.dpacked, b.docc);
+                                                                        b.dflags_light, b.dpacked, b.docc);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         tb = b.temp_bytes;
-        return hipcub::DeviceSelect::Flagged(b.temp, tb, b.dpacked, b.dflags, b.dlist, &sp.state->total_sub, (int)n, s);
+        if ((e = hipcub::DeviceSelect::Flagged(b.temp, tb, b.dpacked, b.dflags, b.dlist, b.dcount, (int)n, s)) !=
+            hipSuccess)
+            return e;
+        tb = b.temp_bytes;
+        if ((e = hipcub::DeviceSelect::Flagged(b.temp, tb, b.dpacked, b.dflags_light, b.dlight, b.dcount + 1, (int)n,
+                                               s)) != hipSuccess)
+            return e;
+        detail_append_kernel<<<std::max<uint32_t>(1u, std::min<uint32_t>(1024u, (n + kBinWG - 1) / kBinWG)), kBinWG, 0,
+                               s>>>(b.dlight, b.dcount, b.dlist, sp.state);
+        return hipGetLastError();
     }
     detail_list_kernel<<<(n + kBinWG - 1) / kBinWG, kBinWG, 0, s>>>(sp.objs, sp.nobj, sp.W, sp.row0, sp.rows,
                                                                    sp.band_shift, sp.band_mask, sp.band_stride,

@@ -327,9 +327,12 @@ struct BinBuffers {
     unsigned long long* mask = nullptr;
     TriHot* hot = nullptr;
     // detail sub-block list of the rendered rows
-    uint8_t* dflags = nullptr;
+    uint8_t* dflags = nullptr;            // listed sub-blocks whose bin holds more than one chunk
+    uint8_t* dflags_light = nullptr;      // ... and the other listed ones
     uint32_t* dpacked = nullptr;
     uint32_t* dlist = nullptr;
+    uint32_t* dlight = nullptr;           // the light ones, appended to dlist after the heavy ones
+    uint32_t* dcount = nullptr;           // [heavy, light] counts
     uint8_t* docc = nullptr;
     uint32_t* sortq = nullptr;            // bins to sort by face index (bins.hip bin_sort_kernel)
     uint32_t* nsort = nullptr;            // their count, zero between builds
