@@ -962,6 +962,7 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     p.bounces = bounces;
     p.seed_lo = (uint32_t)rp->aa_seed;
     p.seed_hi = (uint32_t)(rp->aa_seed >> 32);
+    p.trace_skip = (rp->flags & ERAY_RENDER_BRUTE_FORCE) ? 0u : 1u;
     p.launch_flags = rp->flags & ~ERAY_RENDER_BRUTE_FORCE;
     if (!cull) {  // every pixel in detail: one rectangle, the frame (sub-block units)
         if (p.nobj) {

@@ -186,6 +186,7 @@ struct FrameParams {
     // aa == 0 && bounces == 0 selects the frame kernel
     uint32_t aa, bounces;
     uint32_t seed_lo, seed_hi;
+    uint32_t trace_skip;  // trace_kernel skips waves no camera ray of which can hit a face
 };
 
 // Camera row of rank-local row j (FrameParams::band_shift; shifts and masks: no division in the

@@ -26,6 +26,7 @@
 // reference's degenerate bounding box rejects almost all of them before the scan.
 #include <mutex>
 
+#include "cull_record.hpp"
 #include "device_math.hpp"
 #include "glibc_cosf.hpp"
 #include "internal.hpp"
@@ -101,23 +102,6 @@ __global__ void __launch_bounds__(256) tri_precompute_kernel(const float* __rest
     shade[i].s1 = make_float4(N[4], N[5], N[6], N[7]);
     shade[i].s2 = make_float4(N[8], U[0], U[1], U[2]);
     shade[i].s3 = make_float4(U[3], U[4], U[5], 0.0f);
-}
-
-// true when condition k fails for every pixel of [xlo,xhi] x [ylo,yhi]
-__device__ __forceinline__ bool cull_one(float A, float B, float K, float T, float xlo, float xhi,
-                                         float ylo, float yhi) {
-    float ax = __builtin_fmaxf(A * xlo, A * xhi);
-    float by = __builtin_fmaxf(B * ylo, B * yhi);
-    float fmax = (K + ax) + by;
-    return fmax < -T;
-}
-__device__ __forceinline__ bool cull_rejects(const TriCull c, float xlo, float xhi, float ylo,
-                                             float yhi) {
-    // all four conditions, no short-circuit: the record is one 64-byte load
-    return cull_one(c.A.x, c.B.x, c.K.x, c.T.x, xlo, xhi, ylo, yhi) |
-           cull_one(c.A.y, c.B.y, c.K.y, c.T.y, xlo, xhi, ylo, yhi) |
-           cull_one(c.A.z, c.B.z, c.K.z, c.T.z, xlo, xhi, ylo, yhi) |
-           cull_one(c.A.w, c.B.w, c.K.w, c.T.w, xlo, xhi, ylo, yhi);
 }
 
 // --------------------------------------------------------------------- exact test ----------

@@ -26,6 +26,7 @@
 // keyed by the caller's seed with counter (x, y, sample, 0) — words 0 and 1 are the x and y
 // draws — mapped to [-1, 1) exactly as rand 0.8's UniformFloat::sample_single does.  The
 // oracle uses the same stream (oracle_render_aa), so results are comparable bit for bit.
+#include "cull_record.hpp"
 #include "device_math.hpp"
 #include "glibc_cosf.hpp"
 #include "hit.hpp"
@@ -185,7 +186,8 @@ __device__ __forceinline__ rgb shade(const Level& L, const LightDesc& Ld) {
 }
 
 // Engine::cast_ray(ray, 0).sum() (engine.rs:112-216, color.rs:82-87) as a depth-first walk.
-__device__ rgb cast_ray(const FrameParams& p, f3 o, f3 d, int32_t* face_out) {
+// `miss_known`: the caller knows the ray hits nothing (trace_kernel's background skip).
+__device__ rgb cast_ray(const FrameParams& p, f3 o, f3 d, int32_t* face_out, bool miss_known) {
     Level st[kMaxBounces + 1];
     bool any = false;
     rgb acc{0.0f, 0.0f, 0.0f};
@@ -195,7 +197,7 @@ __device__ rgb cast_ray(const FrameParams& p, f3 o, f3 d, int32_t* face_out) {
         any = true;
     };
     const rgb miss{0.1f, 0.1f, 0.2f};  // engine.rs:211-213
-    if (!surface(p, o, d, st[0], face_out)) {
+    if (miss_known || !surface(p, o, d, st[0], face_out)) {
         emit(miss, 0);
         return acc;
     }
@@ -229,20 +231,58 @@ __device__ rgb cast_ray(const FrameParams& p, f3 o, f3 d, int32_t* face_out) {
     return acc;
 }
 
+// Background skip.  Every ray a wave casts from the camera — its 64 primary rays and their
+// jittered anti-aliasing rays — goes through the viewport rectangle [x0 - 1, x0 + 64] x
+// [y - 1, y + 1] / (W, H) (jitter in [-1, 1), engine.rs:62-69).  For scenes of at most
+// kSkipTris triangles the workgroup computes every triangle's culling record for this camera
+// (cull_record.hpp, the frame kernel's conservative bounds, with the viewport range widened to
+// the jittered rays') into LDS; a wave none of whose records survives its rectangle cannot hit
+// any face with any camera ray, so every one of its rays is the reference's miss
+// (engine.rs:208-213) — cast_ray's own miss path, the same float sums — and the shadow and
+// reflected rays, which start only at a hit, never exist.  Bit-identical to the brute-force
+// scan (ERAY_RENDER_BRUTE_FORCE turns the skip off; tests/test_gpu_trace.py compares them).
+constexpr uint32_t kSkipTris = 256;
+
+__device__ __forceinline__ float widen_down(float v) { return v >= 0.0f ? v * (1.0f - 0x1p-20f) : v * (1.0f + 0x1p-20f); }
+__device__ __forceinline__ float widen_up(float v) { return v >= 0.0f ? v * (1.0f + 0x1p-20f) : v * (1.0f - 0x1p-20f); }
+
 __global__ void __launch_bounds__(256) trace_kernel(FrameParams p) {
-    const uint32_t px = blockIdx.x * 64 + (threadIdx.x & 63);
+    __shared__ TriCull s_cull[kSkipTris];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t px = blockIdx.x * 64 + lane;
     const uint32_t py = blockIdx.y * 4 + (threadIdx.x >> 6);  // rank-local row
-    if (px >= p.cam_w || py >= p.rows) return;
     const uint32_t y = band_camera_row(p.row0, p.band_shift, p.band_mask, p.band_stride, py);
+    bool skip = false;
+    if (p.trace_skip && p.total_tris <= kSkipTris) {  // workgroup-uniform
+        const CamDev cam{p.cx, p.cy, p.cz, p.ratio, p.z_dist, {0u, 0u, 0u}};
+        const double xa = -2.0 / (double)p.cam_w, ya = -2.0 / (double)p.cam_h;  // (rays reach -1/W, -1/H)
+        for (uint32_t i = threadIdx.x; i < p.total_tris; i += 256)
+            s_cull[i] = cull_record(p.tris[i], cam, xa, 1.0, ya, 1.0);
+        __syncthreads();
+        const float rw = 1.0f / (float)p.cam_w, rh = 1.0f / (float)p.cam_h;
+        const float x0 = (float)(blockIdx.x * 64);
+        // (x' <= 1, y' <= 1: the rays reach at most x = W, y = H; the bounds assume |x'|, |y'| <= 1)
+        const float xe = __builtin_fminf(x0 + 64.0f, (float)p.cam_w), ye = __builtin_fminf((float)y + 1.0f, (float)p.cam_h);
+        const float xlo = widen_down((x0 - 1.0f) * rw), xhi = widen_up(xe * rw);
+        const float ylo = widen_down(((float)y - 1.0f) * rh), yhi = widen_up(ye * rh);
+        bool alive = false;
+        for (uint32_t f = lane; f < p.total_tris; f += 64) alive |= !cull_rejects(s_cull[f], xlo, xhi, ylo, yhi);
+        skip = __ballot(alive) == 0;
+    }
+    if (px >= p.cam_w || py >= p.rows) return;
     const f3 C = mk3(p.cx, p.cy, p.cz);
     int32_t face = -1;
     // cast_ray_from_camera(x as f32, y as f32) (engine.rs:60, 100-109)
-    rgb avg = cast_ray(p, C, camera_ray_dir(p, (float)px / (float)p.cam_w, (float)y / (float)p.cam_h), &face);
+    rgb avg = cast_ray(p, C, camera_ray_dir(p, (float)px / (float)p.cam_w, (float)y / (float)p.cam_h), &face, skip);
     for (uint32_t s = 0; s < p.aa; ++s) {  // engine.rs:62-69
+        if (skip) {  // the jitter only moves a ray that misses anyway
+            avg = cadd(avg, cast_ray(p, C, f3{}, nullptr, true));
+            continue;
+        }
         const uint4 r = philox4x32_10(make_uint4(px, y, s, 0u), p.seed_lo, p.seed_hi);
         const float xf = ((float)px + jitter(r.x)) / (float)p.cam_w;
         const float yf = ((float)y + jitter(r.y)) / (float)p.cam_h;
-        avg = cadd(avg, cast_ray(p, C, camera_ray_dir(p, xf, yf), nullptr));
+        avg = cadd(avg, cast_ray(p, C, camera_ray_dir(p, xf, yf), nullptr, false));
     }
     if (p.aa) {  // (average / aa as f32).clamp() (engine.rs:71-73)
         const float n = (float)p.aa;

@@ -256,7 +256,7 @@ typedef struct eray_render_params {
 } eray_render_params;
 
 #define ERAY_RENDER_DEFAULT 0u
-#define ERAY_RENDER_BRUTE_FORCE 1u  /* disable the exact per-wave triangle culling (A/B) */
+#define ERAY_RENDER_BRUTE_FORCE 1u  /* disable the exact per-wave triangle culling and the general tracer's background skip (A/B) */
 /* Launch-shape overrides (tests / tuning; every choice renders the same image).  By default the
  * library picks them from the frame's detail sub-block count. */
 #define ERAY_RENDER_DENSE_DETAIL 2u      /* large meshes: the 3-workgroups-per-CU detail build      */

@@ -156,3 +156,52 @@ def test_too_many_bounces_is_reported(gpu, oracle):
     out.free()
     for x in keep:
         x.free()
+
+
+@pytest.mark.parametrize("seed,n_tris", [(51, 40), (52, 120), (53, 300)])
+def test_background_skip_is_exact(gpu, oracle, seed, n_tris):
+    """trace_kernel's background skip (waves no jittered camera ray of which can reach a face,
+    from the culling records) against the brute-force scan (ERAY_RENDER_BRUTE_FORCE) and the
+    oracle: small objects near the frame's corners and edges, so many waves sit next to a face
+    within a jitter's reach.  300 faces exceed the skip's LDS table (plain scan)."""
+    rng = np.random.default_rng(seed)
+    W, H = 160, 96
+    cam_center = (0.05, -0.03, 4.0)
+    s = oracle.Scene()
+    gpu.scene_reset()
+    gpu.set_camera(capi.make_camera(cam_center, (3.0, 2.0), W, 1.0))
+    keep = []
+    for k, c in enumerate([(-1.35, 0.85, 0.3), (1.3, -0.9, 0.0), (0.0, 0.0, -0.5)]):
+        T = n_tris // 3 + (n_tris % 3 if k == 0 else 0)
+        pos, nrm, uv = random_mesh(rng, T, scale=0.12 + 0.05 * k, center=c)
+        lo, hi = pos.reshape(-1, 3).min(0), pos.reshape(-1, 3).max(0)
+        color = rng.uniform(0, 1.2, (5, 7, 3)).astype(np.float32)
+        refl = rng.uniform(0, 0.9, (3, 4)).astype(np.float32)
+        dev = [gpu.to_device(a) for a in (color, refl)]
+        keep += dev
+        gpu.add_object(pos, nrm, uv, tuple(lo), tuple(hi), color=dev[0].image(), reflection=dev[1].image())
+        s.add_object(pos, nrm, uv, tuple(lo), tuple(hi), color=color, reflection=refl)
+    for p, var, col, b in [((0.0, 2.0, 0.0), "ambient", (0.9, 0.5, 1.0), 0.3),
+                           ((1.0, 1.0, 2.0), "point", (1.0, 1.0, 1.0), 1.0)]:
+        gpu.add_light(capi.make_light(p, var, col, b))
+        s.add_light(p, var, col, b)
+    outs = []
+    for flags in (capi.RENDER_DEFAULT, capi.RENDER_BRUTE_FORCE):
+        rgb = gpu.empty((H, W, 3), np.float32)
+        face = gpu.empty((H, W), np.int32)
+        gpu.render(W, H, out_rgb=rgb.ptr, out_face=face.ptr, anti_aliasing=3, bounces=1, aa_seed=seed,
+                   flags=flags)
+        outs.append((rgb.numpy(), face.numpy()))
+        rgb.free()
+        face.free()
+    for a in keep:
+        a.free()
+    (rgb, face), (brute, brute_face) = outs
+    assert_bit_equal(rgb, brute, "skip vs brute force")
+    assert np.array_equal(face, brute_face)
+    ref, ref_face, _ = oracle.render(s, oracle.camera(cam_center, (3.0, 2.0), W, 1.0), want_faces=True,
+                                     bounces=1, anti_aliasing=3, seed=seed)
+    assert_bit_equal(rgb, ref, "aa=3, bounces=1")
+    assert np.array_equal(face, ref_face)
+    hit = face >= 0
+    assert 0 < hit.sum() < hit.size // 4  # small objects: most waves are background
