@@ -165,7 +165,7 @@ def test_background_skip_is_exact(gpu, oracle, seed, n_tris):
     oracle: small objects near the frame's corners and edges, so many waves sit next to a face
     within a jitter's reach.  300 faces exceed the skip's LDS table (plain scan)."""
     rng = np.random.default_rng(seed)
-    W, H = 160, 96
+    W, H = 144, 96  # (Camera::size of fov 3 x 2)
     cam_center = (0.05, -0.03, 4.0)
     s = oracle.Scene()
     gpu.scene_reset()
