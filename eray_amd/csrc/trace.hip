@@ -71,10 +71,28 @@ __device__ __forceinline__ f3 camera_ray_dir(const FrameParams& p, float xf, flo
 
 // Object<Built>::intersects up to the face (object.rs:58-78): bbox, then the first face in
 // index order; u, v, t of that face.
+// `live` (camera rays of a scene of at most kSkipTris faces, else null): bit f of the
+// wave-uniform mask is clear when face f's culling record rejects every camera ray of the wave —
+// its exact test cannot pass, so skipping it leaves the first passing face unchanged.
 __device__ __forceinline__ int first_face(const TriHot* tris, const ObjGeom& ob, f3 o, f3 d, float& u, float& v,
-                                          float& t) {
+                                          float& t, const uint64_t* live) {
     if (!bbox_hit(ob, o, d)) return -1;
     const TriHot* r = tris + ob.tri_begin;
+    if (live) {
+        if (!ob.tri_count) return -1;
+        const uint32_t b = ob.tri_begin, e = ob.tri_begin + ob.tri_count;
+        for (uint32_t w = b >> 6; w <= (e - 1) >> 6; ++w) {
+            uint64_t m = live[w];
+            if (w == (b >> 6)) m &= ~0ull << (b & 63);
+            if (w == ((e - 1) >> 6) && (e & 63)) m &= ~(~0ull << (e & 63));
+            while (m) {
+                const uint32_t f = w * 64 + (uint32_t)__builtin_ctzll(m) - b;
+                m &= m - 1;
+                if (exact_test(r[f], o, d, u, v, t)) return (int)f;
+            }
+        }
+        return -1;
+    }
     for (uint32_t f = 0; f < ob.tri_count; ++f)
         if (exact_test(r[f], o, d, u, v, t)) return (int)f;
     return -1;
@@ -91,7 +109,7 @@ struct Level {
 // The closest object's first hit along Ray(o, d) — strict `<` on |P - camera|² in object order
 // (engine.rs:116-126) — and its material (Triangle::intersects' P and N, primitives.rs:60-69;
 // RaycastHit's UV and Material::get, object.rs:70-74, material.rs:56-94).  False on a miss.
-__device__ bool surface(const FrameParams& p, f3 o, f3 d, Level& L, int32_t* face_out) {
+__device__ bool surface(const FrameParams& p, f3 o, f3 d, Level& L, int32_t* face_out, const uint64_t* live) {
     const f3 C = mk3(p.cx, p.cy, p.cz);
     bool have = false;
     float best = 0.0f, bu = 0.0f, bv = 0.0f, bt = 0.0f;
@@ -100,7 +118,7 @@ __device__ bool surface(const FrameParams& p, f3 o, f3 d, Level& L, int32_t* fac
     for (uint32_t oi = 0; oi < p.nobj; ++oi) {
         const ObjGeom ob = p.objects[oi].g;
         float u, v, t;
-        const int f = first_face(p.tris, ob, o, d, u, v, t);
+        const int f = first_face(p.tris, ob, o, d, u, v, t, live);
         if (f < 0) continue;
         const float dsq = len_sq(sub(add(o, mul(d, t)), C));
         if (!have || dsq < best) {
@@ -164,7 +182,7 @@ __device__ bool reaches_light(const FrameParams& p, f3 S, f3 sd, f3 Lp) {
     for (uint32_t oi = 0; oi < p.nobj; ++oi) {
         const ObjGeom ob = p.objects[oi].g;
         float u, v, t;
-        if (first_face(p.tris, ob, S, sd, u, v, t) >= 0) return len(sub(add(S, mul(sd, t)), S)) > dist;
+        if (first_face(p.tris, ob, S, sd, u, v, t, nullptr) >= 0) return len(sub(add(S, mul(sd, t)), S)) > dist;
     }
     return true;
 }
@@ -186,8 +204,9 @@ __device__ __forceinline__ rgb shade(const Level& L, const LightDesc& Ld) {
 }
 
 // Engine::cast_ray(ray, 0).sum() (engine.rs:112-216, color.rs:82-87) as a depth-first walk.
-// `miss_known`: the caller knows the ray hits nothing (trace_kernel's background skip).
-__device__ rgb cast_ray(const FrameParams& p, f3 o, f3 d, int32_t* face_out, bool miss_known) {
+// `miss_known`: the caller knows the ray hits nothing (trace_kernel's background skip); `live`:
+// the faces a camera ray of the wave can hit (first_face), for the first level only.
+__device__ rgb cast_ray(const FrameParams& p, f3 o, f3 d, int32_t* face_out, bool miss_known, const uint64_t* live) {
     Level st[kMaxBounces + 1];
     bool any = false;
     rgb acc{0.0f, 0.0f, 0.0f};
@@ -197,7 +216,7 @@ __device__ rgb cast_ray(const FrameParams& p, f3 o, f3 d, int32_t* face_out, boo
         any = true;
     };
     const rgb miss{0.1f, 0.1f, 0.2f};  // engine.rs:211-213
-    if (miss_known || !surface(p, o, d, st[0], face_out)) {
+    if (miss_known || !surface(p, o, d, st[0], face_out, live)) {
         emit(miss, 0);
         return acc;
     }
@@ -212,7 +231,7 @@ __device__ rgb cast_ray(const FrameParams& p, f3 o, f3 d, int32_t* face_out, boo
             if (reaches_light(p, S, normalize(sub(Lp, L.P)), Lp)) emit(shade(L, Ld), depth);
             if ((uint32_t)depth < p.bounces && L.refl != 0.0f) {  // engine.rs:181-191
                 const f3 rd = normalize(sub(L.d, mul(mul(L.N, 2.0f), dot0(L.d, L.N))));
-                if (surface(p, S, rd, st[depth + 1], nullptr))
+                if (surface(p, S, rd, st[depth + 1], nullptr, nullptr))
                     ++depth;
                 else
                     emit(miss, depth + 1);
@@ -239,7 +258,8 @@ __device__ rgb cast_ray(const FrameParams& p, f3 o, f3 d, int32_t* face_out, boo
 // the jittered rays') into LDS; a wave none of whose records survives its rectangle cannot hit
 // any face with any camera ray, so every one of its rays is the reference's miss
 // (engine.rs:208-213) — cast_ray's own miss path, the same float sums — and the shadow and
-// reflected rays, which start only at a hit, never exist.  Bit-identical to the brute-force
+// reflected rays, which start only at a hit, never exist.  The other waves keep the survivors'
+// bits (live_mask): their camera rays test only those faces, in index order.  Bit-identical to the brute-force
 // scan (ERAY_RENDER_BRUTE_FORCE turns the skip off; tests/test_gpu_trace.py compares them).
 constexpr uint32_t kSkipTris = 256;
 
@@ -253,6 +273,8 @@ __global__ void __launch_bounds__(256) trace_kernel(FrameParams p) {
     const uint32_t py = blockIdx.y * 4 + (threadIdx.x >> 6);  // rank-local row
     const uint32_t y = band_camera_row(p.row0, p.band_shift, p.band_mask, p.band_stride, py);
     bool skip = false;
+    uint64_t live_mask[kSkipTris / 64];
+    const uint64_t* live = nullptr;
     if (p.trace_skip && p.total_tris <= kSkipTris) {  // workgroup-uniform
         const CamDev cam{p.cx, p.cy, p.cz, p.ratio, p.z_dist, {0u, 0u, 0u}};
         const double xa = -2.0 / (double)p.cam_w, ya = -2.0 / (double)p.cam_h;  // (rays reach -1/W, -1/H)
@@ -265,24 +287,30 @@ __global__ void __launch_bounds__(256) trace_kernel(FrameParams p) {
         const float xe = __builtin_fminf(x0 + 64.0f, (float)p.cam_w), ye = __builtin_fminf((float)y + 1.0f, (float)p.cam_h);
         const float xlo = widen_down((x0 - 1.0f) * rw), xhi = widen_up(xe * rw);
         const float ylo = widen_down(((float)y - 1.0f) * rh), yhi = widen_up(ye * rh);
-        bool alive = false;
-        for (uint32_t f = lane; f < p.total_tris; f += 64) alive |= !cull_rejects(s_cull[f], xlo, xhi, ylo, yhi);
-        skip = __ballot(alive) == 0;
+        uint64_t any = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kSkipTris / 64; ++w) {
+            const uint32_t f = w * 64 + lane;
+            live_mask[w] = __ballot(f < p.total_tris && !cull_rejects(s_cull[f], xlo, xhi, ylo, yhi));
+            any |= live_mask[w];
+        }
+        skip = any == 0;
+        live = live_mask;
     }
     if (px >= p.cam_w || py >= p.rows) return;
     const f3 C = mk3(p.cx, p.cy, p.cz);
     int32_t face = -1;
     // cast_ray_from_camera(x as f32, y as f32) (engine.rs:60, 100-109)
-    rgb avg = cast_ray(p, C, camera_ray_dir(p, (float)px / (float)p.cam_w, (float)y / (float)p.cam_h), &face, skip);
+    rgb avg = cast_ray(p, C, camera_ray_dir(p, (float)px / (float)p.cam_w, (float)y / (float)p.cam_h), &face, skip, live);
     for (uint32_t s = 0; s < p.aa; ++s) {  // engine.rs:62-69
         if (skip) {  // the jitter only moves a ray that misses anyway
-            avg = cadd(avg, cast_ray(p, C, f3{}, nullptr, true));
+            avg = cadd(avg, cast_ray(p, C, f3{}, nullptr, true, nullptr));
             continue;
         }
         const uint4 r = philox4x32_10(make_uint4(px, y, s, 0u), p.seed_lo, p.seed_hi);
         const float xf = ((float)px + jitter(r.x)) / (float)p.cam_w;
         const float yf = ((float)y + jitter(r.y)) / (float)p.cam_h;
-        avg = cadd(avg, cast_ray(p, C, camera_ray_dir(p, xf, yf), nullptr, false));
+        avg = cadd(avg, cast_ray(p, C, camera_ray_dir(p, xf, yf), nullptr, false, live));
     }
     if (p.aa) {  // (average / aa as f32).clamp() (engine.rs:71-73)
         const float n = (float)p.aa;
