@@ -86,6 +86,7 @@ struct eray_ctx {
     TriHot* d_hot = nullptr;
     TriShade* d_shade = nullptr;
     TriCull* d_cull = nullptr;
+    TriCull* d_tcull = nullptr;  // kTraceSkipTris records: trace.hip's background skip
     size_t tri_cap = 0;
     float* d_raw = nullptr;
     size_t raw_cap = 0;
@@ -232,6 +233,8 @@ int sync_scene(eray_ctx* ctx) {
             ctx->d_cull = nullptr;
         }
         HIP_TRY(ctx, hipMalloc((void**)&ctx->d_cull, shade_cap * sizeof(TriCull)));
+        if (!ctx->d_tcull)  // the general tracer's per-frame culling records (small scenes)
+            HIP_TRY(ctx, hipMalloc((void**)&ctx->d_tcull, kTraceSkipTris * sizeof(TriCull)));
 
         ctx->h_raw.assign((size_t)T * 24, 0.0f);
         size_t off = 0;
@@ -600,7 +603,7 @@ int eray_ctx_destroy(eray_ctx* ctx) {
     void* bufs[] = {ctx->d_hot,   ctx->d_shade, ctx->d_cull,  ctx->d_raw,  ctx->d_objs,  ctx->d_lights,
                     ctx->d_prog,  ctx->d_cam,   ctx->d_state, ctx->d_acc,  ctx->d_begin, ctx->d_range,
                     ctx->d_area,  ctx->d_fkey,  ctx->d_path,  ctx->d_path_all, ctx->d_staging,
-                    ctx->d_bcull, ctx->d_bobjs, ctx->d_bstate};
+                    ctx->d_bcull, ctx->d_bobjs, ctx->d_bstate, ctx->d_tcull};
     for (void* b : bufs)
         if (b) hipFree(b);
     if (ctx->h_state) hipHostFree(ctx->h_state);
@@ -962,7 +965,8 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     p.bounces = bounces;
     p.seed_lo = (uint32_t)rp->aa_seed;
     p.seed_hi = (uint32_t)(rp->aa_seed >> 32);
-    p.trace_skip = (rp->flags & ERAY_RENDER_BRUTE_FORCE) ? 0u : 1u;
+    p.trace_cull = (general && !(rp->flags & ERAY_RENDER_BRUTE_FORCE) && ctx->total_tris <= kTraceSkipTris)
+                       ? ctx->d_tcull : nullptr;
     p.launch_flags = rp->flags & ~ERAY_RENDER_BRUTE_FORCE;
     if (!cull) {  // every pixel in detail: one rectangle, the frame (sub-block units)
         if (p.nobj) {

@@ -130,6 +130,8 @@ struct alignas(16) CamState {
     int32_t rects[kMaxRects][4];  // x0, x1, y0, y1 (inclusive)
 };
 
+constexpr uint32_t kTraceSkipTris = 256;  // general tracer: largest scene with the background skip
+
 struct FrameParams {
     // camera (camera.rs:57-76)
     float cx, cy, cz;
@@ -186,7 +188,9 @@ struct FrameParams {
     // aa == 0 && bounces == 0 selects the frame kernel
     uint32_t aa, bounces;
     uint32_t seed_lo, seed_hi;
-    uint32_t trace_skip;  // trace_kernel skips waves no camera ray of which can hit a face
+    // trace_kernel's culling records for this camera (scenes of at most kTraceSkipTris faces;
+    // null: no background skip), written by trace_cull_kernel before the frame
+    TriCull* trace_cull;
 };
 
 // Camera row of rank-local row j (FrameParams::band_shift; shifts and masks: no division in the

@@ -251,17 +251,28 @@ __device__ rgb cast_ray(const FrameParams& p, f3 o, f3 d, int32_t* face_out, boo
 }
 
 // Background skip.  Every ray a wave casts from the camera — its 64 primary rays and their
-// jittered anti-aliasing rays — goes through the viewport rectangle [x0 - 1, x0 + 64] x
-// [y - 1, y + 1] / (W, H) (jitter in [-1, 1), engine.rs:62-69).  For scenes of at most
-// kSkipTris triangles the workgroup computes every triangle's culling record for this camera
-// (cull_record.hpp, the frame kernel's conservative bounds, with the viewport range widened to
-// the jittered rays') into LDS; a wave none of whose records survives its rectangle cannot hit
-// any face with any camera ray, so every one of its rays is the reference's miss
+// jittered anti-aliasing rays — goes through the viewport rectangle [x0 - 1, x0 + 64] x [y - 1, y
+// + 1] / (W, H) (jitter in [-1, 1), engine.rs:62-69).  For scenes of at most kSkipTris triangles
+// trace_cull_kernel computes every triangle's culling record for this camera (cull_record.hpp, the
+// frame kernel's conservative bounds, with the viewport range widened to the jittered rays') and
+// each workgroup copies them into LDS; a wave none of whose records survives its rectangle cannot
+// hit any face with any camera ray, so every one of its rays is the reference's miss
 // (engine.rs:208-213) — cast_ray's own miss path, the same float sums — and the shadow and
 // reflected rays, which start only at a hit, never exist.  The other waves keep the survivors'
-// bits (live_mask): their camera rays test only those faces, in index order.  Bit-identical to the brute-force
-// scan (ERAY_RENDER_BRUTE_FORCE turns the skip off; tests/test_gpu_trace.py compares them).
-constexpr uint32_t kSkipTris = 256;
+// bits (live_mask): their camera rays test only those faces, in index order.  Bit-identical to the
+// brute-force scan (ERAY_RENDER_BRUTE_FORCE turns the skip off; tests/test_gpu_trace.py compares
+// them).
+constexpr uint32_t kSkipTris = kTraceSkipTris;
+
+// The records, once per frame (one workgroup; the host passes trace_cull only for scenes of at
+// most kSkipTris faces).
+__global__ void __launch_bounds__(256) trace_cull_kernel(FrameParams p) {
+    const uint32_t i = threadIdx.x;
+    if (i >= p.total_tris) return;
+    const CamDev cam{p.cx, p.cy, p.cz, p.ratio, p.z_dist, {0u, 0u, 0u}};
+    const double xa = -2.0 / (double)p.cam_w, ya = -2.0 / (double)p.cam_h;  // (rays reach -1/W, -1/H)
+    p.trace_cull[i] = cull_record(p.tris[i], cam, xa, 1.0, ya, 1.0);
+}
 
 __device__ __forceinline__ float widen_down(float v) { return v >= 0.0f ? v * (1.0f - 0x1p-20f) : v * (1.0f + 0x1p-20f); }
 __device__ __forceinline__ float widen_up(float v) { return v >= 0.0f ? v * (1.0f + 0x1p-20f) : v * (1.0f - 0x1p-20f); }
@@ -275,11 +286,8 @@ __global__ void __launch_bounds__(256) trace_kernel(FrameParams p) {
     bool skip = false;
     uint64_t live_mask[kSkipTris / 64];
     const uint64_t* live = nullptr;
-    if (p.trace_skip && p.total_tris <= kSkipTris) {  // workgroup-uniform
-        const CamDev cam{p.cx, p.cy, p.cz, p.ratio, p.z_dist, {0u, 0u, 0u}};
-        const double xa = -2.0 / (double)p.cam_w, ya = -2.0 / (double)p.cam_h;  // (rays reach -1/W, -1/H)
-        for (uint32_t i = threadIdx.x; i < p.total_tris; i += 256)
-            s_cull[i] = cull_record(p.tris[i], cam, xa, 1.0, ya, 1.0);
+    if (p.trace_cull) {  // workgroup-uniform
+        if (threadIdx.x < p.total_tris) s_cull[threadIdx.x] = p.trace_cull[threadIdx.x];
         __syncthreads();
         const float rw = 1.0f / (float)p.cam_w, rh = 1.0f / (float)p.cam_h;
         const float x0 = (float)(blockIdx.x * 64);
@@ -336,6 +344,10 @@ __global__ void __launch_bounds__(256) trace_kernel(FrameParams p) {
 }  // namespace
 
 hipError_t launch_trace(const FrameParams& p, hipStream_t s) {
+    if (p.trace_cull) {
+        if (p.total_tris > kSkipTris) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(trace_cull_kernel, dim3(1), dim3(256), 0, s, p);
+    }
     const dim3 grid((p.cam_w + 63) / 64, (p.rows + 3) / 4);
     hipLaunchKernelGGL(trace_kernel, grid, dim3(256), 0, s, p);
     return hipGetLastError();
