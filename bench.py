@@ -5,30 +5,28 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json configs[1]): objects/cube.obj with src/main.rs's scene
-and material graph, 1920x1080 per GPU.  One step = one frame (camera rays, first-hit triangle
-scan, shading with shadow rays) with the f32 image and the PPM bytes written by the fused kernel.
+Metric (BASELINE.json): Mrays/s + frame ms at 1920x1080 cube.obj, 1/2/4/8-GPU tile scaling.
+Workload (configs[1]): objects/cube.obj with src/main.rs's scene and material
+graph, a 1920x1080 frame.  One step = one frame: camera rays, first-hit triangle scan, shading
+with shadow rays, the f32 image and the PPM bytes (fused), and for N > 1 the frame assembled on
+rank 0.  Inputs (mesh, material textures) are resident in HBM before timing; the material graph is
+evaluated once, as Material::update is (reported separately).
 
-Multi-GPU (row tiles).  Default, weak scaling: N GPUs render a (1920*N) x 1080
-frame — C2 widened at the same pixel pitch (the camera's Fov ratio grows with the width, the
-viewport height and focal length stay main.rs's), so every rank renders 1080/N rows of 1920*N
-pixels, the same 2,073,600 rays per GPU, and N = 1 is exactly C2.  --scaling strong splits one
-fixed --width x --height frame (C4, C5) instead.  For N > 1 the job ends with the final RCCL
-gather (xGMI) of the PPM rows to rank 0 inside the timed region (north_star: "a final RCCL
-gather"); --gather-every-frame gathers after every frame instead.  Inputs (mesh, material
-textures) are resident in HBM before timing; the material graph is evaluated once, as
-Material::update is (reported separately).
+Frames in flight: a serving loop renders a stream of independent frames, so the frames go
+through a ring of output slots (eray_render_frames_ring) and several frames share one kernel
+launch — the latency-bound shading chains of one frame overlap the others' background stores.
+Every frame is rendered in full into its own slot.  `frame_latency_ms` reports one frame alone
+per launch beside it.
 
-The headline `value` replays frames of ONE camera (static camera: the per-camera setup — culling
-records, pixel rectangles, screen bins — runs once before the timed region, as it would for a
-serving loop that renders the same view).  `moving_camera` reports the same frames with a camera
-that moves every frame (a dolly along the view axis: Scene::set_camera + Engine::render per
-frame), every frame's setup on the device inside the timed frames (eray_render_camera_path).
+Multi-GPU (row tiles), default --scaling strong: the same 1920x1080 frame split over
+the N GPUs in interleaved 4-row bands (equal work wherever the cube sits); N = 1 is exactly C2.
+Every frame is assembled on rank 0 (eray_gather_frames): the ranks render batches of frames into
+one half of a two-half ring while the previous batch's rows travel over xGMI (RCCL point-to-point,
+only the objects' pixel rectangles: ERAY_GATHER_SCENE_CAMERA) on a second stream and rank 0 writes
+the frames.  --scaling weak widens the frame to (1920 N) x 1080 instead (not a BASELINE config).
+C4 (--width 3840 --height 2160) and C5 (7680x4320, a 1M-face mesh) are available by flag.
 
---scaling weak widens the frame with N (C2's pixel pitch, not a BASELINE.json config); --scaling
-strong splits BASELINE's fixed frames (C4: --width 3840 --height 2160, C5: 7680x4320).
-
-Prints ONE JSON line on rank 0 (metric "Mrays/s": primary rays of all ranks / wall time).
+Prints ONE JSON line on rank 0 (metric "Mrays/s": primary rays of all frames / wall time).
 """
 from __future__ import annotations
 
@@ -53,7 +51,10 @@ from eray_amd.objfile import load_obj_file  # noqa: E402
 
 WIDTH, HEIGHT, TEXTURE = 1920, 1080, 1024  # C2 (defaults; --width / --height)
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+ACHIEVABLE_HBM_GBS = 6290.0  # MI355X_MICROARCH.md: 6.29 TB/s measured (float4 copy)
 PEAK_VALU_TOPS = 78.6  # non-FMA FP32 VALU: 256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz
+HIT_TEXEL_BYTES = 16  # Material::get per hit pixel: IColor 12 B + IValue 4 B (material.rs:56-94)
+FACE_RECORD_BYTES = 48 + 64  # the first hit's intersection record (TriHot) + shading record (TriShade)
 
 
 def frame_camera_fov(width: int, height: int) -> tuple[float, float]:
@@ -76,20 +77,21 @@ def frame_camera_fov(width: int, height: int) -> tuple[float, float]:
     raise RuntimeError(f"no Fov gives a {width}x{height} camera")
 
 
-def algorithmic_bytes(hit_pixels: int, pixels: int, triangles: int) -> int:
-    """Bytes the render kernel must move per launch:
-    15 B/pixel written (12 B f32 RGB + 3 B PPM), 16 B of texels read per hit (IColor 12 + IValue 4),
-    and the triangle records once (48 B hot + 64 B culling + 64 B shading)."""
-    return 15 * pixels + 16 * hit_pixels + (48 + 64 + 64) * triangles
+def algorithmic_bytes(pixels: int, hit_pixels: int, hit_faces: int) -> int:
+    """Bytes one frame must move (DESIGN.md §5 roofline): the outputs, 15 B per pixel written
+    (12 B f32 RGB + 3 B PPM); per hit pixel the two texels Material::get reads (16 B); per face
+    that is some pixel's first hit its intersection and shading records (112 B).  Faces that are
+    only candidates, the culling records and the screen bins are work of this implementation,
+    not of the path, and are not counted."""
+    return 15 * pixels + HIT_TEXEL_BYTES * hit_pixels + FACE_RECORD_BYTES * hit_faces
 
 
 def pmc_record(workload: dict):
     """The committed rocprofv3 counter summary of this workload's frame kernel
-    (scripts/pmc_traffic.py): profiles/pmc_traffic*.json whose "workload" (mesh, frame, rows per
-    GPU, GPUs) equals this run's, or None when no summary of this workload is committed."""
-    # the newest round's summaries first (profiles/rNN/pmc_traffic*.json), then older ones
+    (scripts/pmc_traffic.py): profiles/rNN/pmc_traffic*.json whose "workload" equals this run's,
+    or None when no summary of this workload is committed."""
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic*.json")), reverse=True)
-    for path in paths + sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json"))):
+    for path in paths:
         try:
             with open(path) as f:
                 rec = json.load(f)
@@ -100,26 +102,28 @@ def pmc_record(workload: dict):
     return None
 
 
-def counter_figures(rec, kernel_ms: float) -> dict:
-    """From a counter summary: HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, the gfx950
-    correction of MI355X_MICROARCH.md), the HBM-read fraction (north_star's figure: corrected fetch
-    bytes / kernel time / peak) and the VALU fraction (SURVEY.md §8(d)'s binding figure for the
-    intersection: SQ_INSTS_VALU x 64 lanes / kernel time / the 78.6 T ops/s non-FMA FP32 peak; it
-    counts every VALU instruction of the frame kernel — rays, tests, shading, fill addressing)."""
+def counter_figures(rec, launch_ms: float) -> dict:
+    """From a counter summary (per launch of frames_per_launch frames): HBM bytes per launch
+    (2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), the HBM-read
+    fraction (north_star's figure) and the VALU fraction (SQ_INSTS_VALU x 64 lanes / launch time /
+    the 78.6 T ops/s non-FMA FP32 peak; every VALU instruction of the frame kernel), and the share
+    of wave cycles spent waiting (SQ_WAIT_ANY / SQ_WAVE_CYCLES)."""
     if not rec:
         return {"traffic": None}
     out = {"traffic": int(rec["hbm_bytes_per_launch"])}
-    sec = kernel_ms * 1e-3
+    sec = launch_ms * 1e-3
     fetch = rec.get("fetch_bytes_corrected")
     if fetch is not None and sec > 0:
         gbs = fetch / sec / 1e9
         out["hbm_read"] = {"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                            "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": int(fetch)}
-    valu = rec.get("counters_mean_per_dispatch", {}).get("SQ_INSTS_VALU")
-    if valu is not None and sec > 0:
-        tops = valu * 64 / sec / 1e12
+    c = rec.get("counters_mean_per_dispatch", {})
+    if c.get("SQ_INSTS_VALU") is not None and sec > 0:
+        tops = c["SQ_INSTS_VALU"] * 64 / sec / 1e12
         out["valu"] = {"achieved": round(tops, 2), "peak": PEAK_VALU_TOPS, "unit": "TOP/s",
-                       "frac": round(tops / PEAK_VALU_TOPS, 4), "instructions_per_launch": int(valu)}
+                       "frac": round(tops / PEAK_VALU_TOPS, 4), "instructions_per_launch": int(c["SQ_INSTS_VALU"])}
+    if c.get("SQ_WAIT_ANY") and c.get("SQ_WAVE_CYCLES"):
+        out["wave_wait_frac"] = round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4)
     return out
 
 
@@ -195,32 +199,31 @@ def mesh_label(path: str) -> str:
     return os.path.basename(path) if rel.startswith("..") else rel
 
 
-def moving_camera(scene, args, width, height, render_args, world, allreduce) -> dict:
-    """The bench's frames with a camera that moves every frame (dolly_path): eray_render_camera_path
-    runs every frame's camera setup on the device inside the timed loop.  Returns the moving_camera record."""
+def moving_camera(scene, args, width, height, out, ring) -> dict:
+    """The bench's frames with a camera that moves every frame (dolly_path), through the same ring:
+    eray_render_camera_path_ring runs every frame's camera setup on the device inside the timed
+    loop (small scenes: one launch sets up a graph chunk's 64 cameras, frames_per_launch frames
+    per launch, each from its own setup slot).  One GPU."""
     path = dolly_path(args.steps, frame_camera_fov(width, height), width)
-    scene.ctx.render_camera_path(path, width, height, **render_args())
+    scene.ctx.render_camera_path(path, width, height, ring=ring, **out)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
     m0 = time.perf_counter()
-    scene.ctx.render_camera_path(path, width, height, **render_args())
+    scene.ctx.render_camera_path(path, width, height, ring=ring, **out)
     torch.cuda.synchronize()
     moving_s = time.perf_counter() - m0
-    if world > 1:
-        moving_s = float(allreduce(moving_s, torch.float64, dist.ReduceOp.MAX))
-    device_ms = scene.ctx.render_camera_path(path, width, height, timed=True, **render_args())
+    device_ms = scene.ctx.render_camera_path(path, width, height, ring=ring, timed=True, **out)
+    one = scene.ctx.render_camera_path(path, width, height, timed=True, **out)  # one frame per launch
     return {
         "frame_ms": round(moving_s / args.steps * 1e3, 6),
         "value": round(width * height * args.steps / moving_s / 1e6, 3),
         "unit": "Mrays/s",
         "device_ms_per_frame": round(device_ms, 6),
+        "device_ms_per_frame_one_per_launch": round(one, 6),
         "frames": args.steps,
         "camera": "dolly along the view axis, z 5 +- 0.5, z_dist 1 +- 0.1, a new camera every frame",
         "includes": "every frame's camera setup on the device (culling records, pixel rectangles, merged "
-                    "detail rectangles: for scenes without meshes over 256 faces one launch sets up a graph "
-                    "chunk's 64 cameras, one workgroup per camera; otherwise per frame, with the screen bins "
-                    "and detail list) + frame",
+                    "detail rectangles; for meshes over 256 faces the screen bins and detail list, one frame "
+                    "per launch) + frame",
     }
 
 
@@ -228,12 +231,12 @@ AA_SAMPLES = 4
 AA_MAX_TRIANGLES = 4096  # the general tracer scans every face per ray: small scenes only
 
 
-def anti_aliasing_line(scene, args, width, height, render_args) -> dict:
+def anti_aliasing_line(scene, args, width, height, out) -> dict:
     """The general tracer (trace.hip: anti-aliasing, engine.rs:59-77) on the bench's frames:
     AA_SAMPLES jittered rays per pixel plus the centre ray, every face scanned per ray.  Device
     time per frame over graph-replayed frames; rays counted as the reference casts them."""
     frames = max(2, min(args.steps, 20))
-    kw = dict(render_args(), anti_aliasing=AA_SAMPLES, aa_seed=12345)
+    kw = dict(out, anti_aliasing=AA_SAMPLES, aa_seed=12345)
     scene.ctx.render_frames(frames, width, height, prepare_only=True, **kw)
     ms = scene.ctx.render_frames(frames, width, height, timed=True, **kw)
     rays = width * height * (AA_SAMPLES + 1)
@@ -249,18 +252,20 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--mesh", default=os.path.join(ROOT, "objects", "cube.obj"))
     ap.add_argument("--width", type=int, default=WIDTH,
-                    help="frame width per GPU (weak) or of the whole frame (strong); C2: 1920")
+                    help="frame width (strong) or width per GPU (weak); C2: 1920")
     ap.add_argument("--height", type=int, default=HEIGHT, help="frame height (C2: 1080)")
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
-                    help="weak: a (width*N) x height frame; strong: one width x height frame split N ways")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="strong: one width x height frame split N ways (BASELINE); weak: a (width N) x height frame")
+    ap.add_argument("--frames-per-launch", type=int, default=0,
+                    help="frames in flight per kernel launch (0: the library's choice, eray_frames_per_launch)")
     ap.add_argument("--brute-force", action="store_true", help="disable the exact wave culling")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-moving-camera", action="store_true", help="skip the moving-camera line (counter runs)")
+    ap.add_argument("--no-moving-camera", action="store_true", help="skip the moving-camera and AA lines (counter runs)")
     ap.add_argument("--split", choices=("bands", "blocks"), default="bands",
                     help="N > 1: interleaved 4-row bands (balanced, default) or contiguous row blocks")
-    ap.add_argument("--gather-every-frame", action="store_true",
-                    help="N > 1: gather the PPM rows to rank 0 after every frame (default: one final gather)")
+    ap.add_argument("--gather", choices=("scene", "coded"), default="scene",
+                    help="N > 1: only the objects' pixel rectangles travel (scene, sync-free) or the coded rows")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -287,129 +292,175 @@ def main() -> None:
 
     mesh = load_obj_file(args.mesh)
     ctx = capi.Context(device)
-    stream = torch.cuda.Stream()  # one stream shared by the library, torch and RCCL
+    stream = torch.cuda.Stream()  # the render stream: shared by the library and torch
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     width = args.width * world if args.scaling == "weak" else args.width
-    H_total = args.height
-    if H_total % world:
-        raise SystemExit(f"--height {H_total} does not split into {world} equal row tiles")
-    per_gpu = H_total // world
+    H = args.height
     t_mat0 = time.perf_counter()
-    scene = MainScene(ctx, *mesh, width, H_total, texture=TEXTURE, fov=frame_camera_fov(width, H_total))
+    scene = MainScene(ctx, *mesh, width, H, texture=TEXTURE, fov=frame_camera_fov(width, H))
     torch.cuda.synchronize()
     t_mat = time.perf_counter() - t_mat0
 
-    # rank r renders interleaved 4-row bands r, r + N, ... (every rank an equal share of the scene
-    # wherever it sits; tile timings in DESIGN.md §7) or, --split blocks, the r-th block of PPM file
-    # rows: camera rows [H - (r+1)*h, H - r*h)
+    # this rank's rows: interleaved 4-row bands r, r + N, ... (every rank an equal share of the scene
+    # wherever it sits) or, --split blocks, the r-th block of PPM file rows
     bands = world > 1 and args.split == "bands"
     if bands:
-        sp = band_split(rank, world, H_total, BAND_ROWS)
+        sp = band_split(rank, world, H, BAND_ROWS)
         row0, rows, alloc_rows = sp["row0"], sp["rows"], sp["alloc_rows"]
         band_args = dict(band_rows=sp["band_rows"], band_stride=sp["band_stride"])
     else:
-        row0, rows = row_block(rank, world, per_gpu)
+        if H % world:
+            raise SystemExit(f"--height {H} does not split into {world} equal row blocks")
+        row0, rows = row_block(rank, world, H // world)
         alloc_rows, band_args = rows, {}
-    rgb = torch.empty((alloc_rows, width, 3), dtype=torch.float32, device="cuda")
-    ppm = torch.zeros((alloc_rows, width, 3), dtype=torch.uint8, device="cuda")
-    face = torch.empty((alloc_rows, width), dtype=torch.int32, device="cuda")
-    frame = torch.empty((H_total, width, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
-    flags = capi.RENDER_BRUTE_FORCE if args.brute_force else capi.RENDER_DEFAULT
-    # N > 1: the frame gather of the C-ABI (eray_gather_rows, RCCL ncclGather over xGMI); the
-    # one-GPU rehearsal gathers through gloo instead
     band = BAND_ROWS if bands else 0
-    if world > 1 and not rehearsal:
-        rccl = RowGather(ctx, world, rank)
+    flags = capi.RENDER_BRUTE_FORCE if args.brute_force else capi.RENDER_DEFAULT
 
-        def gather():
-            rccl(ppm, frame, H_total, band)
-    elif world > 1:
-        def gather():
-            gather_ppm_rows(ppm, frame, world, rank, band_rows=band)
+    # frames in flight: F frames per launch (the library's choice unless given); N = 1 renders into
+    # a ring of F slots, N > 1 into two halves of G = F slots each (batch b renders into half b % 2
+    # while batch b - 1 is gathered)
+    F = args.frames_per_launch or ctx.frames_per_launch(width, H, rows=rows, slots=64)
+    G = F
+    slots = F if world == 1 else 2 * G
+    slot_px = alloc_rows * width
+    rgb = torch.empty((slots, alloc_rows, width, 3), dtype=torch.float32, device="cuda")
+    ppm = torch.zeros((slots, alloc_rows, width, 3), dtype=torch.uint8, device="cuda")
 
-    def render_args():
-        return dict(row0=row0, rows=rows, out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr(), flags=flags, **band_args)
+    def ring_args(half=0, n=slots):
+        return dict(row0=row0, rows=rows, flags=flags, out_rgb=rgb[half * G].data_ptr(),
+                    out_ppm=ppm[half * G].data_ptr(), ring=capi.frame_ring(n, alloc_rows, width, min(F, n)),
+                    **band_args)
 
-    # one untimed instrumented frame: hit count for the algorithmic-bytes model; being the first
-    # render of the camera it also builds the per-camera data (culling records, pixel
-    # rectangles, screen bins of large meshes): reported as scene_setup_ms
+    # one untimed instrumented frame: hit pixels and hit faces for the algorithmic-bytes model;
+    # being the first render of the camera it also builds the per-camera data (culling records,
+    # pixel rectangles, screen bins of large meshes): reported as scene_setup_ms
+    face = torch.full((alloc_rows, width), -1, dtype=torch.int32, device="cuda")
+    one_rgb = torch.empty((alloc_rows, width, 3), dtype=torch.float32, device="cuda")
     torch.cuda.synchronize()
     t_setup0 = time.perf_counter()
-    face.fill_(-1)
-    scene.ctx.render(width, H_total, out_rgb=rgb.data_ptr(), out_face=face.data_ptr(), row0=row0, rows=rows,
-                     flags=flags, **band_args)
+    ctx.render(width, H, out_rgb=one_rgb.data_ptr(), out_face=face.data_ptr(), row0=row0, rows=rows, flags=flags,
+               **band_args)
     torch.cuda.synchronize()
     t_setup = time.perf_counter() - t_setup0
-    hits = int((face[:rows] >= 0).sum().item())
+    hit = face[:rows][face[:rows] >= 0]
+    hits, hit_faces = int(hit.numel()), int(torch.unique(hit).numel())
+    del face, one_rgb
 
-    # capture the frame-loop graph, then the W warmup frames through the same replayed path as
-    # the timed ones (and the gather warmed) outside the timed region
-    scene.ctx.render_frames(args.steps, width, H_total, prepare_only=True, **render_args())
-    if args.warmup:
-        scene.ctx.render_frames(args.warmup, width, H_total, **render_args())
+    gather = None
+    frames_out = None
     if world > 1:
-        gather()
+        frames_out = torch.empty((G, H, width, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
+        gstream = torch.cuda.Stream()
+        if not rehearsal:
+            rccl = RowGather(ctx, world, rank)
+
+            def gather(half, n):  # frames of ring half `half` -> rank 0's frames, on the gather stream
+                ctx.set_stream(gstream.cuda_stream)
+                ctx.gather_frames(rccl.comm, ppm[half * G].data_ptr(), slot_px * 3,
+                                  frames_out.data_ptr() if frames_out is not None else 0, H * width * 3, n, H, width,
+                                  band_rows=band, scene_camera=args.gather == "scene")
+                ctx.set_stream(stream.cuda_stream)
+        else:
+            def gather(half, n):  # plumbing only: gloo through host memory
+                torch.cuda.synchronize()
+                for k in range(n):
+                    gather_ppm_rows(ppm[half * G + k], frames_out[k] if frames_out is not None else None, world, rank,
+                                    band_rows=band)
+
+    def run(nframes):
+        """nframes frames through the ring (N > 1: batches of G, each gathered while the next renders)."""
+        if world == 1:
+            ctx.render_frames(nframes, width, H, **ring_args())
+            return
+        ev_r, ev_g = [], []
+        b = 0
+        for first in range(0, nframes, G):
+            n = min(G, nframes - first)
+            half = b % 2
+            if b >= 2:  # the gather of batch b - 2 has read this half
+                stream.wait_event(ev_g[b - 2])
+            ctx.render_frames(n, width, H, **ring_args(half, G))
+            e = torch.cuda.Event()
+            e.record(stream)
+            ev_r.append(e)
+            gstream.wait_event(e)
+            with torch.cuda.stream(gstream):
+                gather(half, n)
+                e2 = torch.cuda.Event()
+                e2.record(gstream)
+            ev_g.append(e2)
+            b += 1
+        stream.wait_event(ev_g[-1])
+
+    # launch plans (graphs) of every batch size, the gather plan and buffers, then W warmup frames,
+    # all outside the timed region
+    sizes = {min(G, args.steps)} | ({args.steps % G} if world > 1 and args.steps % G else set())
+    for n in sizes:
+        ctx.render_frames(n, width, H, prepare_only=True, **(ring_args() if world == 1 else ring_args(0, G)))
+    if world == 1:
+        ctx.render_frames(args.steps, width, H, prepare_only=True, **ring_args())
+    run(max(args.warmup, 1))
+    if world > 1:
+        for n in sizes:
+            run(n)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    # every rank renders its row tile of each frame; the frame loop runs inside the library,
-    # replayed from a HIP graph (no per-frame host round trip)
-    if args.gather_every_frame and world > 1:
-        for _ in range(args.steps):
-            scene.render(**render_args())
-            gather()
-    else:
-        scene.ctx.render_frames(args.steps, width, H_total, **render_args())
-        if world > 1:  # the final RCCL gather of the PPM rows to rank 0 (file order)
-            gather()
+    run(args.steps)
+    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
         elapsed = float(allreduce(elapsed, torch.float64, dist.ReduceOp.MAX))
         hits_all = int(allreduce(hits, torch.int64, dist.ReduceOp.SUM))
     else:
         hits_all = hits
-    # the frame kernel's duration: the same frames replayed once more, bracketed by HIP events on
-    # the library's stream (back-to-back kernels: device time per frame)
-    kernel_ms = scene.ctx.render_frames(args.steps, width, H_total, timed=True, **render_args())
-    gather_ms = None
+    # the frame kernel's duration on this rank: the same frames replayed once more, bracketed by
+    # HIP events on the library's stream (mean device time per frame; F frames per launch), and
+    # the latency of one frame alone per launch
+    ring1 = ring_args() if world == 1 else ring_args(0, G)
+    kernel_ms = ctx.render_frames(max(args.steps // F, 1) * F, width, H, timed=True, **ring1)
+    lat_args = dict(ring1)
+    lat_args["ring"] = capi.frame_ring(1, alloc_rows, width, 1)
+    latency_ms = ctx.render_frames(max(min(args.steps, 64), 2), width, H, timed=True, **lat_args)
     rank_kernel_ms = [kernel_ms]
-    if world > 1:  # one frame's gather, and every rank's frame-kernel time, for the record
+    gather_ms = None
+    if world > 1:
         torch.cuda.synchronize()
         dist.barrier()
         g0 = time.perf_counter()
-        gather()
+        with torch.cuda.stream(gstream):
+            gather(0, G)
         torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - g0) * 1e3
+        gather_ms = (time.perf_counter() - g0) * 1e3 / G
         got = [None] * world
         dist.all_gather_object(got, kernel_ms)
         rank_kernel_ms = got
 
-    # moving camera: the same frames with a new camera every frame (the setup on the device,
-    # inside each frame); one untimed pass captures the path's graphs
-    moving = None if args.no_moving_camera else moving_camera(scene, args, width, H_total, render_args, world, allreduce)
-    # the general tracer (anti-aliasing) on the same frames, rank 0 of one GPU, small scenes
+    out1 = dict(row0=row0, rows=rows, flags=flags, out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr(), **band_args)
+    moving = None
     aa_line = None
-    if world == 1 and not args.no_moving_camera and len(mesh[0]) <= AA_MAX_TRIANGLES:
-        aa_line = anti_aliasing_line(scene, args, width, H_total, render_args)
+    if world == 1 and not args.no_moving_camera:
+        moving = moving_camera(scene, args, width, H, out1, capi.frame_ring(slots, alloc_rows, width, F))
+        if len(mesh[0]) <= AA_MAX_TRIANGLES:
+            aa_line = anti_aliasing_line(scene, args, width, H, out1)
 
     if rank == 0:
-        # the workload a committed counter summary (profiles/pmc_traffic*.json) must match
-        pmc_key = {"mesh": mesh_label(args.mesh), "frame": [width, H_total], "rows_per_gpu": rows,
-                   "n_gpus": world, "brute_force": bool(args.brute_force)}
-        is_c2 = (args.width, args.height, args.scaling) == (WIDTH, HEIGHT, "weak") and args.mesh.endswith(
-            "objects/cube.obj") and not args.brute_force
+        # the workload a committed counter summary (profiles/rNN/pmc_traffic*.json) must match
+        pmc_key = {"mesh": mesh_label(args.mesh), "frame": [width, H], "rows_per_gpu": rows, "n_gpus": world,
+                   "brute_force": bool(args.brute_force), "frames_per_launch": F}
+        is_c2 = (width, H) == (WIDTH, HEIGHT) and args.mesh.endswith("objects/cube.obj") and not args.brute_force
         pixels = width * rows
         ms_per_step = elapsed / args.steps * 1e3
-        rays = width * H_total * args.steps
+        rays = width * H * args.steps
         value = rays / elapsed / 1e6
-        alg = algorithmic_bytes(hits, pixels, len(mesh[0]))
-        achieved = alg / (kernel_ms * 1e-3) / 1e9
+        alg = algorithmic_bytes(pixels, hits, hit_faces)
+        gbs = alg / (kernel_ms * 1e-3) / 1e9
+        launch_ms = kernel_ms * F
         result = {
             "metric": "Mrays/s",
             "value": round(value, 3),
@@ -426,52 +477,62 @@ def main() -> None:
                      + (" (the reference's own file)" if args.mesh.endswith("objects/cube.obj") else "")
                      + ", procedural material graph"),
             "config": {
-                "workload": f"{'C2' + (f' widened x{world}' if world > 1 else '') + ': ' if is_c2 else ''}"
-                            f"{os.path.basename(args.mesh)}, {width}x{H_total} frame, {width}x{per_gpu} rows per GPU, "
-                            "main.rs scene + material graph; step = one frame (camera rays, first-hit scan, "
-                            "shading + shadow rays, f32 image and PPM bytes); N > 1: interleaved 4-row bands "
-                            "per GPU, final RCCL gather of the PPM rows to rank 0",
+                "workload": f"{'C2: ' if is_c2 else ''}{os.path.basename(args.mesh)}, {width}x{H} frame, "
+                            f"{width}x{rows} rows on rank 0, main.rs scene + material graph; step = one frame (camera "
+                            "rays, first-hit scan, shading + shadow rays, f32 image and PPM bytes"
+                            + (", assembled on rank 0: scene-camera gather over RCCL point-to-point" if world > 1 else "")
+                            + f"); {F} frames in flight per launch",
                 "mesh": mesh_label(args.mesh),
                 "triangles": int(len(mesh[0])),
-                "frame": [width, H_total],
+                "frame": [width, H],
                 "rows_per_gpu": rows,
                 "texture": TEXTURE,
                 "parallelism": (f"row tiles x{world} ({'interleaved 4-row bands' if bands else 'contiguous blocks'})"
                                 if world > 1 else "single GPU"),
+                "frames_per_launch": F,
+                "ring_slots": slots,
                 "camera": "static (value); see moving_camera",
                 **({"note": "weak scaling widens the frame to (1920 N) x 1080: not a BASELINE.json config"}
                    if world > 1 and args.scaling == "weak" else {}),
                 "culling": not args.brute_force,
             },
-            "rows_per_gpu_note": "rank 0's row count (bands: rows of its interleaved bands)" if bands else None,
             "frame_ms": round(ms_per_step, 6),
             "render_kernel_ms": round(kernel_ms, 6),
+            "frame_latency_ms": round(latency_ms, 6),
             "material_graph_s": round(t_mat, 4),
             "scene_setup_ms": round(t_setup * 1e3, 3),
-            "gather_ms": None if gather_ms is None else round(gather_ms, 4),
+            "gather": ({"kind": f"{args.gather}, every frame, batches of {G} overlapped with rendering",
+                        "ms_per_frame_alone": round(gather_ms, 5)} if world > 1 else None),
             "rank_kernel_ms": [round(v, 6) for v in rank_kernel_ms],
             "moving_camera": moving,
             "anti_aliased": aa_line,
-            "gather": ("every frame" if args.gather_every_frame else "final frame") if world > 1 else None,
             **({"rehearsal": "all ranks on GPU 0, gloo collectives: not a measurement"} if rehearsal else {}),
             "hit_pixels": hits_all,
             "roofline": {
                 "bound": "hbm",
-                "achieved": round(achieved, 1),
+                "achieved": round(gbs, 1),
                 "peak": PEAK_HBM_GBS,
                 "unit": "GB/s",
-                "frac": round(achieved / PEAK_HBM_GBS, 4),
-                **counter_figures(pmc_record(pmc_key), kernel_ms),
+                "frac": round(gbs / PEAK_HBM_GBS, 4),
+                "frac_of_achievable": round(gbs / ACHIEVABLE_HBM_GBS, 4),
+                "achievable": ACHIEVABLE_HBM_GBS,
+                **counter_figures(pmc_record(pmc_key), launch_ms),
                 "kernel": "frame_kernel (eray_amd/csrc/render.hip)",
-                "algorithmic_bytes_per_launch": alg,
-                "kernel_ms": round(kernel_ms, 6),
+                "frames_per_launch": F,
+                "algorithmic_bytes_per_frame": alg,
+                "algorithmic_bytes_per_launch": alg * F,
+                "bytes_model": "15 B/pixel written + 16 B texels per hit pixel + 112 B records per hit face",
+                "hit_faces": hit_faces,
+                "kernel_ms_per_frame": round(kernel_ms, 6),
+                "kernel_ms_per_launch": round(launch_ms, 6),
             },
         }
         if world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline(mesh, width, H_total, frame_camera_fov(width, H_total), args.cpu_seconds)
+            result["cpu_baseline"] = cpu_baseline(mesh, width, H, frame_camera_fov(width, H), args.cpu_seconds)
         print(json.dumps(result), flush=True)
 
     if world > 1 and not rehearsal:
+        torch.cuda.synchronize()
         rccl.close()
     scene.close()
     ctx.close()

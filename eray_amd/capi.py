@@ -37,6 +37,9 @@ RENDER_NO_DENSE_DETAIL = 4
 RENDER_SEPARATE_FILL = 8
 RENDER_NO_SEPARATE_FILL = 16
 
+GATHER_DEFAULT = 0
+GATHER_SCENE_CAMERA = 1
+
 LIGHT_POINT = 0
 LIGHT_AMBIENT = 1
 
@@ -107,6 +110,18 @@ class RenderParams(C.Structure):
                 ("band_stride", C.c_uint32)]
 
 
+class FrameRing(C.Structure):  # eray_frame_ring
+    _fields_ = [("slots", C.c_uint32), ("frames_per_launch", C.c_uint32), ("rgb_stride", C.c_uint64),
+                ("ppm_stride", C.c_uint64), ("face_stride", C.c_uint64)]
+
+
+def frame_ring(slots: int, rows: int, width: int, frames_per_launch: int = 0) -> FrameRing:
+    """A ring of `slots` contiguous output slots of `rows` x `width` pixels (f32 RGB, PPM bytes,
+    face indices: one slot's bytes as the stride; width a multiple of 16 keeps them 16-B aligned)."""
+    px = rows * width
+    return FrameRing(slots, frames_per_launch, 12 * px, 3 * px, 4 * px)
+
+
 # Every exported symbol of include/eray_hip.h with its (restype, argtypes).
 _P = C.c_void_p
 _U = C.c_uint32
@@ -141,11 +156,18 @@ SIGNATURES = {
     "eray_render_prepare": (C.c_int, [_P, C.POINTER(RenderParams), _U]),
     "eray_render_camera_path": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(Camera), _U,
                                           C.POINTER(C.c_float)]),
+    "eray_render_frames_ring": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(FrameRing), _U,
+                                          C.POINTER(C.c_float)]),
+    "eray_render_prepare_ring": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(FrameRing), _U]),
+    "eray_frames_per_launch": (_U, [_P, C.POINTER(RenderParams), _U]),
+    "eray_render_camera_path_ring": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(FrameRing),
+                                               C.POINTER(Camera), _U, C.POINTER(C.c_float)]),
     "eray_pack_ppm": (C.c_int, [_P, _P, _U, _U, _P]),
     "eray_comm_unique_id": (C.c_int, [_P]),
     "eray_comm_init": (C.c_int, [_P, C.c_int, C.c_int, _P, C.POINTER(_P)]),
     "eray_comm_destroy": (C.c_int, [_P]),
     "eray_gather_rows": (C.c_int, [_P, _P, _P, _P, _U, _U, _U]),
+    "eray_gather_frames": (C.c_int, [_P, _P, _P, C.c_uint64, _P, C.c_uint64, _U, _U, _U, _U, _U]),
     "eray_band_rows": (_U, [_U, _U, _U, _U]),
     "eray_ppm_header": (C.c_int, [_U, _U, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
 }
@@ -158,6 +180,7 @@ DEBUG_SIGNATURES = {
     "eray_debug_setup_state": (C.c_int, [_P, _U, _P, C.POINTER(C.c_int32)]),
     "eray_debug_unband": (C.c_int, [_P, _P, _P, _U, _U, _U, _U]),
     "eray_debug_coded_unband": (C.c_int, [_P, _P, _P, _U, _U, _U, _U]),
+    "eray_debug_scene_gather": (C.c_int, [_P, _P, _P, _U, _U, _U, _U]),
 }
 
 _lib = None
@@ -412,23 +435,31 @@ class Context:
 
     def render_frames(self, frames, image_width, image_height, row0=0, rows=None, out_rgb=None,
                       out_ppm=None, out_face=None, flags=RENDER_DEFAULT, timed=False, prepare_only=False,
-                      bounces=0, anti_aliasing=0, aa_seed=0, band_rows=0, band_stride=0):
+                      bounces=0, anti_aliasing=0, aa_seed=0, band_rows=0, band_stride=0, ring=None):
         """`frames` back-to-back renders (replayed from a cached HIP graph); returns the mean
-        device ms per frame when `timed`.  `prepare_only` builds the launch plan and returns."""
+        device ms per frame when `timed`.  `prepare_only` builds the launch plan and returns.
+        ring (FrameRing): frame k into slot k % slots, several frames per launch."""
         if rows is None:
             rows = image_height - row0
         p = RenderParams(image_width, image_height, row0, rows, bounces, anti_aliasing, out_rgb or None,
                          out_ppm or None, out_face or None, flags, aa_seed, band_rows, band_stride)
+        rg = C.byref(ring) if ring is not None else None
         if prepare_only:
-            self._check(lib().eray_render_prepare(self._h, C.byref(p), frames))
+            self._check(lib().eray_render_prepare_ring(self._h, C.byref(p), rg, frames))
             return None
         ms = C.c_float()
-        self._check(lib().eray_render_frames(self._h, C.byref(p), frames, C.byref(ms) if timed else None))
+        self._check(lib().eray_render_frames_ring(self._h, C.byref(p), rg, frames, C.byref(ms) if timed else None))
         return ms.value if timed else None
+
+    def frames_per_launch(self, image_width, image_height, rows=None, slots=64, anti_aliasing=0, bounces=0) -> int:
+        """The frames per launch the library picks for a ring of `slots` (eray_frames_per_launch)."""
+        p = RenderParams(image_width, image_height, 0, image_height if rows is None else rows, bounces,
+                         anti_aliasing, None, None, None, 0, 0, 0, 0)
+        return lib().eray_frames_per_launch(self._h, C.byref(p), slots)
 
     def render_camera_path(self, cameras, image_width, image_height, row0=0, rows=None, out_rgb=None,
                            out_ppm=None, out_face=None, flags=RENDER_DEFAULT, timed=False, bounces=0,
-                           anti_aliasing=0, aa_seed=0, band_rows=0, band_stride=0):
+                           anti_aliasing=0, aa_seed=0, band_rows=0, band_stride=0, ring=None):
         """One frame per camera (Scene::set_camera + Engine::render each), the per-camera setup on
         the device; returns the mean device ms per frame (setup included) when `timed`."""
         if rows is None:
@@ -437,8 +468,8 @@ class Context:
                          out_ppm or None, out_face or None, flags, aa_seed, band_rows, band_stride)
         cams = (Camera * max(1, len(cameras)))(*cameras)
         ms = C.c_float()
-        self._check(lib().eray_render_camera_path(self._h, C.byref(p), cams, len(cameras),
-                                                  C.byref(ms) if timed else None))
+        self._check(lib().eray_render_camera_path_ring(self._h, C.byref(p), C.byref(ring) if ring is not None else None,
+                                                       cams, len(cameras), C.byref(ms) if timed else None))
         return ms.value if timed else None
 
     def comm_init(self, nranks: int, rank: int, uid: bytes) -> int:
@@ -455,6 +486,14 @@ class Context:
         """eray_gather_rows: every rank's PPM rows into rank 0's height x width frame (file order):
         equal blocks in rank order (band_rows = 0) or interleaved bands of band_rows rows."""
         self._check(lib().eray_gather_rows(self._h, comm, local_ptr, frame_ptr or None, height, width, band_rows))
+
+    def gather_frames(self, comm: int, local_ptr, local_stride: int, frames_ptr, frame_stride: int, nframes: int,
+                      height: int, width: int, band_rows: int = 0, scene_camera: bool = False) -> None:
+        """eray_gather_frames: `nframes` frames' rows (local + k * local_stride) into rank 0's frames
+        (frames + k * frame_stride); scene_camera: only the objects' pixel rectangles travel."""
+        self._check(lib().eray_gather_frames(self._h, comm, local_ptr, local_stride, frames_ptr or None, frame_stride,
+                                             nframes, height, width, band_rows,
+                                             GATHER_SCENE_CAMERA if scene_camera else GATHER_DEFAULT))
 
     def pack_ppm(self, rgb_ptr, w, h, out_ptr) -> None:
         self._check(lib().eray_pack_ppm(self._h, rgb_ptr, w, h, out_ptr))

@@ -124,6 +124,13 @@ struct eray_ctx {
     bool state_pending = false;   // a copy into h_state is in flight
     bool state_known = false;     // h_state holds the results of the setup of setup_key
     std::vector<uint64_t> setup_key;  // camera, size, rows and scene generation of the last setup
+    uint64_t setup_gen = 0;       // bumped with every setup of the scene camera (eray_gather_frames' plans)
+    uint32_t setup_span[5] = {0, 0, 0, 0, 0};  // its rows: row0, rows, band_shift, band_mask, band_stride
+    ObjectDesc* h_objs_state = nullptr;  // pinned copy of the descriptors after that setup (pixel rectangles)
+    size_t h_objs_state_cap = 0;
+    // eray_gather_frames' plan (comm.cpp owns it)
+    void* gather_plan = nullptr;
+    void (*gather_plan_free)(void*) = nullptr;
     uint32_t* d_acc = nullptr;    // setup counter, partials and rectangle accumulators (enqueue_setup)
     size_t acc_cap = 0;
     uint32_t* d_begin = nullptr;  // obj_begin | objkey
@@ -134,6 +141,7 @@ struct eray_ctx {
     size_t face_cap = 0;
     BinBuffers bins;
     std::vector<uint64_t> bins_layout;
+    uint64_t bins_gen = 0;        // bumped whenever bins_alloc (re)allocates the bin buffers
     size_t bin_cap = 0;           // entry capacity to allocate (grown when a setup overflows)
     // camera paths (eray_render_camera_path): the cameras of the current graph chunk on the
     // device, the whole path staged in pinned memory
@@ -422,6 +430,7 @@ int ensure_bins(eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs) {
     HIP_TRY(ctx, bins_alloc(ctx->bins, T, nb, kbegin.data(), kobj.data(), W, H, phase, tiles_x, rows, ctx->bin_cap,
                             ctx->stream));
     ctx->bins_layout = std::move(layout);
+    ++ctx->bins_gen;         // graphs that captured the old buffers must not be replayed
     ctx->setup_key.clear();  // the bins must be rebuilt
     return ERAY_OK;
 }
@@ -535,6 +544,22 @@ int sync_setup(eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs, bool wa
             if (int st = enqueue_setup(ctx, ctx->d_cam, W, H, rs, true)) return st;
             HIP_TRY(ctx, hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(CamState), hipMemcpyDeviceToHost,
                                         ctx->stream));
+            // the objects' pixel rectangles of this camera (eray_gather_frames' transfer layout);
+            // no copy into the pinned buffer is in flight here (state_pending was drained above)
+            const size_t nobj = ctx->objects.size();
+            if (ctx->h_objs_state_cap < nobj) {
+                if (ctx->h_objs_state) HIP_TRY(ctx, hipHostFree(ctx->h_objs_state));
+                ctx->h_objs_state = nullptr;
+                ctx->h_objs_state_cap = 0;
+                HIP_TRY(ctx, hipHostMalloc((void**)&ctx->h_objs_state, sizeof(ObjectDesc) * nobj, hipHostMallocDefault));
+                ctx->h_objs_state_cap = nobj;
+            }
+            if (nobj)
+                HIP_TRY(ctx, hipMemcpyAsync(ctx->h_objs_state, ctx->d_objs, sizeof(ObjectDesc) * nobj,
+                                            hipMemcpyDeviceToHost, ctx->stream));
+            ++ctx->setup_gen;
+            const uint32_t span[5] = {rs.row0, rs.rows, rs.band_shift, rs.band_mask, rs.band_stride};
+            std::memcpy(ctx->setup_span, span, sizeof span);
             HIP_TRY(ctx, hipEventRecord(ctx->state_ev, ctx->stream));
             ctx->setup_key = std::move(key);
             ctx->state_pending = true;
@@ -608,6 +633,8 @@ int eray_ctx_destroy(eray_ctx* ctx) {
         if (b) hipFree(b);
     if (ctx->h_state) hipHostFree(ctx->h_state);
     if (ctx->h_path) hipHostFree(ctx->h_path);
+    if (ctx->h_objs_state) hipHostFree(ctx->h_objs_state);
+    if (ctx->gather_plan && ctx->gather_plan_free) ctx->gather_plan_free(ctx->gather_plan);
     for (auto& g : ctx->graphs) {
         if (g.exec) hipGraphExecDestroy(g.exec);
         if (g.graph) hipGraphDestroy(g.graph);
@@ -921,6 +948,7 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
 
     FrameParams& p = *out;
     std::memset(&p, 0, sizeof p);  // padding too: the launch-plan cache compares the bytes
+    p.nframes = 1;
     const eray_camera& c = ctx->camera;
     p.cx = c.center[0];
     p.cy = c.center[1];
@@ -1131,43 +1159,140 @@ int replay(eray_ctx* ctx, const Plan& plan, uint32_t frames, Before&& before_chu
     if (he != hipSuccess) return set_error(ctx, ERAY_E_HIP, "render loop: %s", hipGetErrorString(he));
     return ERAY_OK;
 }
+// Frames in flight (eray_frame_ring): frames of one call are rendered `per_launch` to a kernel
+// launch (FrameParams::nframes), frame k into ring slot k % slots.
+struct Ring {
+    uint32_t slots = 1, per_launch = 1;
+    uint64_t rgb = 0, ppm = 0, face = 0;  // bytes between slots
+};
+// One launch renders at most this many pixels (frames x rows x width) when the library picks the
+// frames per launch: enough frames to overlap the latency-bound detail chains of small frames
+// (C2: 4 frames), one frame of 3840x2160 and more (their fill alone saturates the HBM writes).
+constexpr uint64_t kInFlightPixels = 3840ull * 2160ull;
+constexpr uint32_t kMaxInFlight = 8;
+
+// The library's frames per launch for frames of cam_w x rows pixels and a ring of `slots`.
+uint32_t auto_frames(uint64_t cam_w, uint64_t rows, uint32_t slots) {
+    uint32_t F = 1;
+    while (F * 2 <= kMaxInFlight && F * 2 <= slots && (uint64_t)(F * 2) * cam_w * rows <= kInFlightPixels) F *= 2;
+    return F;
+}
+
+int make_ring(eray_ctx* ctx, const eray_render_params* rp, const FrameParams& p, const eray_frame_ring* r, Ring* out) {
+    *out = Ring{};
+    if (!r) return ERAY_OK;
+    if (!r->slots || r->slots > 64 || (r->slots & (r->slots - 1)))
+        return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "ring: slots (%u) must be a power of two <= 64", r->slots);
+    const uint64_t px = (uint64_t)rp->rows * rp->image_width;
+    const uint64_t need[3] = {px * 12u, px * 3u, px * 4u};
+    const uint64_t stride[3] = {r->rgb_stride, r->ppm_stride, r->face_stride};
+    const void* ptr[3] = {rp->out_rgb, rp->out_ppm, rp->out_face};
+    for (int k = 0; k < 3; ++k) {
+        if (!ptr[k] || r->slots == 1) continue;
+        if (stride[k] % 16 || stride[k] < need[k])
+            return set_error(ctx, ERAY_E_INVALID_ARGUMENT,
+                             "ring: output %d's slot stride %llu must be a multiple of 16 of at least %llu bytes", k,
+                             (unsigned long long)stride[k], (unsigned long long)need[k]);
+    }
+    if (r->frames_per_launch && (r->frames_per_launch > r->slots || (r->frames_per_launch & (r->frames_per_launch - 1))))
+        return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "ring: frames_per_launch (%u) must be a power of two <= slots (%u)",
+                         r->frames_per_launch, r->slots);
+    out->slots = r->slots;
+    out->rgb = r->slots > 1 ? r->rgb_stride : 0;
+    out->ppm = r->slots > 1 ? r->ppm_stride : 0;
+    out->face = r->slots > 1 ? r->face_stride : 0;
+    uint32_t F = 1;
+    if (p.aa || p.bounces || r->slots == 1) {
+        F = 1;  // the general tracer renders one frame per launch
+    } else if (r->frames_per_launch) {
+        F = r->frames_per_launch;
+    } else {
+        F = auto_frames(p.cam_w, p.rows, r->slots);
+    }
+    out->per_launch = F;
+    return ERAY_OK;
+}
+
+// The launch parameters of frames [f, f + count) of a call: ring slot f % slots onwards (slots is
+// a multiple of per_launch, so a launch's frames never wrap).
+FrameParams ring_frames(const FrameParams& p, const Ring& r, uint32_t f, uint32_t count) {
+    FrameParams q = p;
+    const uint64_t slot = f % r.slots;
+    q.nframes = count;
+    q.rgb_stride = r.rgb;
+    q.ppm_stride = r.ppm;
+    q.face_stride = r.face;
+    if (q.out_rgb) q.out_rgb = reinterpret_cast<float*>(reinterpret_cast<char*>(q.out_rgb) + slot * r.rgb);
+    if (q.out_ppm) q.out_ppm += slot * r.ppm;
+    if (q.out_face) q.out_face = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(q.out_face) + slot * r.face);
+    return q;
+}
+
+std::vector<unsigned char> ring_key(std::vector<unsigned char> key, const Ring& r) {
+    const size_t at = key.size();
+    key.resize(at + sizeof r);
+    std::memcpy(key.data() + at, &r, sizeof r);
+    return key;
+}
 }  // namespace
 
 extern "C" {
 
-int eray_render_prepare(eray_ctx* ctx, const eray_render_params* rp, uint32_t frames) {
+int eray_render_prepare_ring(eray_ctx* ctx, const eray_render_params* rp, const eray_frame_ring* ring, uint32_t frames) {
     FrameParams p;
     bool empty = false;
     if (int st = prepare_render(ctx, rp, &p, &empty, SetupWait::kYes)) return st;
     if (empty) return ERAY_OK;
+    Ring r;
+    if (int st = make_ring(ctx, rp, p, ring, &r)) return st;
     Plan plan;
-    auto body = [&](uint32_t, uint32_t) -> int {
-        HIP_TRY(ctx, launch_frame(ctx, p));
+    auto body = [&](uint32_t f, uint32_t n) -> int {
+        if (f % r.per_launch) return ERAY_OK;  // rendered by the launch of frame f - f % per_launch
+        HIP_TRY(ctx, launch_frame(ctx, ring_frames(p, r, f, std::min(r.per_launch, n - f))));
         return ERAY_OK;
     };
-    return ensure_plan(ctx, params_key(p, 0), frames, body, &plan);
+    return ensure_plan(ctx, ring_key(params_key(p, 0), r), frames, body, &plan);
 }
 
-int eray_render_frames(eray_ctx* ctx, const eray_render_params* rp, uint32_t frames,
-                       float* mean_frame_ms) {
+uint32_t eray_frames_per_launch(eray_ctx* ctx, const eray_render_params* rp, uint32_t slots) {
+    if (!ctx || !rp || !slots) return 1u;
+    if (rp->anti_aliasing || rp->bounces) return 1u;
+    uint32_t W, H;
+    eray_camera_size(&ctx->camera, &W, &H);
+    return auto_frames(W, rp->rows, slots);
+}
+
+int eray_render_prepare(eray_ctx* ctx, const eray_render_params* rp, uint32_t frames) {
+    return eray_render_prepare_ring(ctx, rp, nullptr, frames);
+}
+
+int eray_render_frames_ring(eray_ctx* ctx, const eray_render_params* rp, const eray_frame_ring* ring, uint32_t frames,
+                            float* mean_frame_ms) {
     FrameParams p;
     bool empty = false;
-    if (int st = prepare_render(ctx, rp, &p, &empty, SetupWait::kYes)) return st;
     if (mean_frame_ms) *mean_frame_ms = 0.0f;
+    if (int st = prepare_render(ctx, rp, &p, &empty, SetupWait::kYes)) return st;
     if (empty || !frames) return ERAY_OK;
+    Ring r;
+    if (int st = make_ring(ctx, rp, p, ring, &r)) return st;
     Plan plan;
-    auto body = [&](uint32_t, uint32_t) -> int {
-        HIP_TRY(ctx, launch_frame(ctx, p));
+    auto body = [&](uint32_t f, uint32_t n) -> int {
+        if (f % r.per_launch) return ERAY_OK;
+        HIP_TRY(ctx, launch_frame(ctx, ring_frames(p, r, f, std::min(r.per_launch, n - f))));
         return ERAY_OK;
     };
-    if (int st = ensure_plan(ctx, params_key(p, 0), frames, body, &plan)) return st;
+    if (int st = ensure_plan(ctx, ring_key(params_key(p, 0), r), frames, body, &plan)) return st;
     auto none = [](uint32_t, uint32_t) { return (int)ERAY_OK; };
     auto plain = [&](uint32_t f) { return body(f, frames); };
     return replay(ctx, plan, frames, none, plain, mean_frame_ms);
 }
 
-int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* rp, const eray_camera* cameras, uint32_t n,
-                            float* mean_frame_ms) {
+int eray_render_frames(eray_ctx* ctx, const eray_render_params* rp, uint32_t frames, float* mean_frame_ms) {
+    return eray_render_frames_ring(ctx, rp, nullptr, frames, mean_frame_ms);
+}
+
+int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, const eray_frame_ring* ring,
+                                 const eray_camera* cameras, uint32_t n, float* mean_frame_ms) {
     if (int st = use_device(ctx)) return st;
     if (mean_frame_ms) *mean_frame_ms = 0.0f;
     if (!rp) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "params is null");
@@ -1186,23 +1311,43 @@ int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* rp, const e
     // the scene camera's setup once (scene upload, bins layout, a detail count for the launch shape)
     if (int st = prepare_render(ctx, rp, &p, &empty, SetupWait::kYes)) return st;
     if (empty || !n) return ERAY_OK;
+    Ring r;
+    if (int st = make_ring(ctx, rp, p, ring, &r)) return st;
     if (!p.cull) {  // anti-aliasing, bounces, brute force: no per-camera setup, camera in the arguments
         const eray_camera saved = ctx->camera;
+        hipEvent_t ev[2] = {nullptr, nullptr};  // mean device ms per frame, as replay() times it
+        if (mean_frame_ms) {
+            for (auto& e : ev) HIP_TRY(ctx, hipEventCreate(&e));
+            HIP_TRY(ctx, hipEventRecord(ev[0], ctx->stream));
+        }
+        auto drop = [&]() {
+            for (auto e : ev)
+                if (e) hipEventDestroy(e);
+        };
         for (uint32_t f = 0; f < n; ++f) {
             ctx->camera = cameras[f];
             FrameParams q;
             int st = prepare_render(ctx, rp, &q, &empty);
             if (!st && !empty) {
-                const hipError_t e = launch_frame(ctx, q);
+                const hipError_t e = launch_frame(ctx, ring_frames(q, r, f, 1));
                 if (e != hipSuccess) st = set_error(ctx, ERAY_E_HIP, "render: %s", hipGetErrorString(e));
             }
             if (st) {
                 ctx->camera = saved;
+                drop();
                 return st;
             }
         }
         ctx->camera = saved;
-        if (mean_frame_ms) HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        if (mean_frame_ms) {
+            hipError_t e = hipEventRecord(ev[1], ctx->stream);
+            float ms = 0.0f;
+            if (e == hipSuccess) e = hipEventSynchronize(ev[1]);
+            if (e == hipSuccess) e = hipEventElapsedTime(&ms, ev[0], ev[1]);
+            drop();
+            if (e != hipSuccess) return set_error(ctx, ERAY_E_HIP, "camera path timing: %s", hipGetErrorString(e));
+            *mean_frame_ms = ms / (float)n;
+        }
         return ERAY_OK;
     }
     // device-camera mode: every frame reads its setup's CamState
@@ -1225,6 +1370,7 @@ int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* rp, const e
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_path_all, ctx->h_path, sizeof(CamDev) * n, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipEventRecord(ctx->path_ev, ctx->stream));
     const bool batched = batch_setup_ok(ctx);
+    if (!batched) r.per_launch = 1;  // a setup (screen bins) per frame: one frame per launch
     const uint32_t T = ctx->total_tris, nobj = (uint32_t)ctx->objects.size();
     if (batched) {
         if (int st = ensure(ctx, &ctx->d_bcull, &ctx->bcull_cap, (size_t)kGraphFrames * T)) return st;
@@ -1232,8 +1378,10 @@ int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* rp, const e
         if (int st = ensure(ctx, &ctx->d_bstate, &ctx->bstate_cap, kGraphFrames)) return st;
     }
     // frame `slot` of a batch whose setups started at camera `cams` (count cameras) — the batch
-    // is enqueued with its first frame
-    auto batch_frame = [&](const CamDev* cams, uint32_t slot, uint32_t count) -> int {
+    // is enqueued with its first frame; frames in flight: the launch of slot s (s % per_launch ==
+    // 0) renders slots [s, s + per_launch) of the batch, each from its own setup slot; `f` is the
+    // frame's index in the call (its ring slot)
+    auto batch_frame = [&](const CamDev* cams, uint32_t slot, uint32_t count, uint32_t f) -> int {
         if (slot == 0) {
             SetupParams sp = setup_params(ctx, cams, W, H, row_span(rp));
             sp.cull = ctx->d_bcull;
@@ -1242,27 +1390,39 @@ int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* rp, const e
             sp.state = ctx->d_bstate;
             HIP_TRY(ctx, launch_camera_setup_batch(sp, count, ctx->stream));
         }
-        FrameParams q = p;
+        if (slot % r.per_launch) return ERAY_OK;
+        FrameParams q = ring_frames(p, r, f, std::min(r.per_launch, count - slot));
         q.cam_state = ctx->d_bstate + slot;
         q.cull = ctx->d_bcull + (size_t)slot * T;
         q.objects = ctx->d_bobjs + (size_t)slot * nobj;
+        q.dev_slots = 1;
         HIP_TRY(ctx, launch_frame(ctx, q));
         return ERAY_OK;
     };
-    auto frame = [&](const CamDev* cam) -> int {
-        if (batched) return batch_frame(cam, 0, 1);
+    auto frame = [&](const CamDev* cam, uint32_t f) -> int {
+        if (batched) {
+            const Ring keep = r;
+            r.per_launch = 1;
+            const int st = batch_frame(cam, 0, 1, f);
+            r = keep;
+            return st;
+        }
         if (int st = enqueue_setup(ctx, cam, W, H, row_span(rp), false)) return st;
-        HIP_TRY(ctx, launch_frame(ctx, p));
+        HIP_TRY(ctx, launch_frame(ctx, ring_frames(p, r, f, 1)));
         return ERAY_OK;
     };
     auto body = [&](uint32_t f, uint32_t count) {
-        return batched ? batch_frame(ctx->d_path, f, count) : frame(ctx->d_path + f);
+        return batched ? batch_frame(ctx->d_path, f, count, f) : frame(ctx->d_path + f, f);
     };
-    std::vector<unsigned char> key = params_key(p, batched ? 2 : 1);
+    std::vector<unsigned char> key = ring_key(params_key(p, batched ? 2 : 1), r);
     for (const void* ptr : {(const void*)ctx->d_path, (const void*)ctx->d_bcull, (const void*)ctx->d_bobjs,
                             (const void*)ctx->d_bstate})
         key.insert(key.end(), reinterpret_cast<const unsigned char*>(&ptr),
                    reinterpret_cast<const unsigned char*>(&ptr) + sizeof ptr);
+    // the captured setup and bins kernels hold every bin buffer's address: a reallocation (a grown
+    // capacity) must never replay a graph of the old buffers, even if some addresses recur
+    key.insert(key.end(), reinterpret_cast<const unsigned char*>(&ctx->bins_gen),
+               reinterpret_cast<const unsigned char*>(&ctx->bins_gen) + sizeof ctx->bins_gen);
     Plan plan;
     if (int st = ensure_plan(ctx, key, n, body, &plan)) return st;
     auto before = [&](uint32_t first, uint32_t count) -> int {
@@ -1270,11 +1430,12 @@ int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* rp, const e
                                     hipMemcpyDeviceToDevice, ctx->stream));
         return ERAY_OK;
     };
-    auto plain = [&](uint32_t f) { return frame(ctx->d_path_all + f); };
+    auto plain = [&](uint32_t f) { return frame(ctx->d_path_all + f, f); };
     const int st = replay(ctx, plan, n, before, plain, mean_frame_ms);
     // the device state now belongs to the path's last camera: the scene camera is set up again
     // at its next render; the path's bin statistics reach the host with this copy
     ctx->setup_key.clear();
+    ++ctx->setup_gen;
     ctx->state_known = false;
     if (!st) {
         if (ctx->state_pending) HIP_TRY(ctx, hipEventSynchronize(ctx->state_ev));
@@ -1283,6 +1444,11 @@ int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* rp, const e
         ctx->state_pending = true;
     }
     return st;
+}
+
+int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* rp, const eray_camera* cameras, uint32_t n,
+                            float* mean_frame_ms) {
+    return eray_render_camera_path_ring(ctx, rp, nullptr, cameras, n, mean_frame_ms);
 }
 
 int eray_pack_ppm(eray_ctx* ctx, const float* rgb, uint32_t w, uint32_t h, uint8_t* out) {
@@ -1305,6 +1471,36 @@ int eray_ppm_header(uint32_t w, uint32_t h, char* buf, size_t cap, size_t* len) 
 }
 
 }  // extern "C"
+
+// The scene camera's current setup as eray_gather_frames reads it (waits for its host copies).
+int eray_internal_scene_layout(eray_ctx* ctx, SceneLayout* out) {
+    if (!ctx || !out) return ERAY_E_INVALID_ARGUMENT;
+    if (ctx->setup_key.empty())
+        return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "no current setup of the scene camera: render it first");
+    if (ctx->state_pending) {
+        HIP_TRY(ctx, hipEventSynchronize(ctx->state_ev));
+        state_arrived(ctx);
+    }
+    if (!ctx->state_known || ctx->setup_key.empty())
+        return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "the scene camera's setup is not current: render it first");
+    out->gen = ctx->setup_gen;
+    eray_camera_size(&ctx->camera, &out->W, &out->H);
+    out->row0 = ctx->setup_span[0];
+    out->rows = ctx->setup_span[1];
+    out->band_shift = ctx->setup_span[2];
+    out->band_stride = ctx->setup_span[4];
+    out->rects.clear();
+    for (size_t i = 0; i < ctx->objects.size(); ++i) {
+        const int32_t* r = ctx->h_objs_state[i].g.rect;
+        out->rects.push_back({r[0], r[1], r[2], r[3]});
+    }
+    return ERAY_OK;
+}
+void** eray_internal_gather_plan(eray_ctx* ctx, void (*free_fn)(void*)) {
+    ctx->gather_plan_free = free_fn;
+    return &ctx->gather_plan;
+}
+int eray_internal_use_device(eray_ctx* ctx) { return use_device(ctx); }
 
 // Error reporting and the gather's staging buffer for the other translation units (comm.cpp).
 int eray_internal_error(eray_ctx* ctx, int code, const char* msg) { return set_error(ctx, code, "%s", msg); }

@@ -10,17 +10,23 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <vector>
 
 #include "../../include/eray_hip.h"
+#include "internal.hpp"
 
 static_assert(ERAY_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size");
 
-// capi.cpp's error reporting and the context's gather staging buffer
+// capi.cpp's error reporting, the context's gather staging buffer, the scene camera's setup and
+// the context's slot for this file's gather plan
 int eray_internal_error(eray_ctx* ctx, int code, const char* msg);
 void* eray_internal_staging(eray_ctx* ctx, size_t bytes);
+int eray_internal_scene_layout(eray_ctx* ctx, eray::gpu::SceneLayout* out);
+void** eray_internal_gather_plan(eray_ctx* ctx, void (*free_fn)(void*));
+int eray_internal_use_device(eray_ctx* ctx);
 
 namespace {
 // camera rows of `rank` in the interleaved band split (eray_band_rows)
@@ -257,6 +263,182 @@ hipError_t encode_rows(const uint8_t* local, uint32_t rows_r, uint32_t rows_max,
     return hipGetLastError();
 }
 
+// ---- scene-camera gather: only the objects' pixel rectangles travel --------------------------
+// The frame kernel writes engine.rs:212's miss colour at every pixel outside the objects' pixel
+// rectangles (ObjGeom::rect: no primary ray there can hit any face, the same conservative bounds
+// the kernel culls with).  So when every rank's local rows are its renders of the scene camera,
+// the frame on rank 0 is the miss colour except inside those rectangles, and only their bytes need
+// to cross xGMI.  The rectangles are fixed per camera: each rank states its own (rank-local rows,
+// 16-pixel column groups) once, one all-gather exchanges them (the only host synchronisation),
+// and every later gather enqueues a pack kernel, fixed-size point-to-point transfers and, on rank
+// 0, one assembly kernel — no host round trip, so a serving loop can capture it in a graph.
+constexpr int kPlanRects = 8;
+struct GatherRect {        // one rectangle of a rank's rows, 32 B
+    int32_t l0, l1;        // local rows (inclusive)
+    int32_t c0, c1;        // 16-pixel column groups (inclusive)
+    uint32_t off;          // byte offset of its first row in the rank's per-frame pack
+    uint32_t row_bytes;    // 48 * (c1 - c0 + 1)
+    uint32_t first;        // its first packed row among the rank's (pack kernel)
+    uint32_t pad;
+};
+struct RankLayout {        // a rank's rectangles and its share of rank 0's receive buffer
+    GatherRect r[kPlanRects];
+    uint32_t nrect, bytes;  // bytes per frame (a multiple of 48)
+    uint64_t off;           // per-frame offset of the rank's block: its frames start at B * off
+    uint32_t rows, packed_rows;
+    uint32_t pad[2];
+};
+constexpr int kXchgInts = 1 + 4 * kPlanRects;
+
+struct GatherPlan {
+    void* comm = nullptr;
+    uint64_t gen = 0;
+    uint32_t H = 0, W = 0, band = 0, nranks = 0, rank = 0;
+    bool valid = false;
+    std::vector<RankLayout> ranks;
+    uint64_t total = 0;            // every rank's bytes per frame
+    RankLayout* d_ranks = nullptr; // rank 0: the assembly's table
+    uint8_t* buf = nullptr;        // this rank's packed frames (rank 0: the receive buffer of all ranks)
+    size_t buf_cap = 0;
+    int32_t* xchg = nullptr;       // the all-gather of the ranks' rectangles
+};
+void plan_free(void* v) {
+    auto* P = static_cast<GatherPlan*>(v);
+    if (!P) return;
+    if (P->d_ranks) hipFree(P->d_ranks);
+    if (P->buf) hipFree(P->buf);
+    if (P->xchg) hipFree(P->xchg);
+    delete P;
+}
+
+// The local rows of rank `rank` (rows, camera row of local row j): interleaved bands (band > 0)
+// or the rank's block of PPM file rows (camera rows [H - (rank+1) h, H - rank h)).
+struct RankRows {
+    uint32_t row0, rows, shift, stride;
+};
+RankRows rank_rows(uint32_t H, uint32_t band, uint32_t N, uint32_t rank) {
+    if (!band) {
+        const uint32_t h = H / N;
+        return RankRows{H - (rank + 1) * h, h, 31u, 0u};
+    }
+    uint32_t shift = 0;
+    while ((1u << shift) < band) ++shift;
+    return RankRows{rank * band, band_rows_of(H, band, N, rank), shift, N * band};
+}
+
+// This rank's rectangles: the objects' pixel rectangles in its local rows and 16-pixel column
+// groups, overlapping ones merged (as camera_setup_kernel merges the detail rectangles), more than
+// kPlanRects merged into the last.
+std::vector<std::array<int32_t, 4>> my_rects(const eray::gpu::SceneLayout& L, const RankRows& rr, uint32_t W) {
+    std::vector<std::array<int32_t, 4>> out;
+    for (const auto& q : L.rects) {
+        int32_t x0 = std::max(q[0], 0), x1 = std::min(q[1], (int32_t)W - 1), l0, l1;
+        if (x0 > x1 || q[2] > q[3]) continue;
+        eray::gpu::band_local_range(rr.row0, rr.shift, rr.stride, q[2], q[3], &l0, &l1);
+        l0 = std::max(l0, 0);
+        l1 = std::min(l1, (int32_t)rr.rows - 1);
+        if (l0 > l1) continue;
+        std::array<int32_t, 4> r{l0, l1, x0 / 16, x1 / 16};
+        if (out.size() == (size_t)kPlanRects) {
+            auto& z = out.back();
+            z = {std::min(z[0], r[0]), std::max(z[1], r[1]), std::min(z[2], r[2]), std::max(z[3], r[3])};
+        } else {
+            out.push_back(r);
+        }
+    }
+    for (bool merged = true; merged;) {
+        merged = false;
+        for (size_t a = 0; a < out.size() && !merged; ++a)
+            for (size_t b = a + 1; b < out.size() && !merged; ++b) {
+                auto &x = out[a], &y = out[b];
+                if (x[0] > y[1] || y[0] > x[1] || x[2] > y[3] || y[2] > x[3]) continue;
+                x = {std::min(x[0], y[0]), std::max(x[1], y[1]), std::min(x[2], y[2]), std::max(x[3], y[3])};
+                out.erase(out.begin() + (std::ptrdiff_t)b);
+                merged = true;
+            }
+    }
+    return out;
+}
+
+RankLayout layout_of(const int32_t* rec, uint32_t rows) {
+    RankLayout R{};
+    R.nrect = (uint32_t)std::min(std::max(rec[0], 0), kPlanRects);
+    R.rows = rows;
+    uint32_t off = 0, first = 0;
+    for (uint32_t i = 0; i < R.nrect; ++i) {
+        GatherRect& g = R.r[i];
+        g.l0 = rec[1 + 4 * i];
+        g.l1 = rec[2 + 4 * i];
+        g.c0 = rec[3 + 4 * i];
+        g.c1 = rec[4 + 4 * i];
+        g.off = off;
+        g.row_bytes = 48u * (uint32_t)(g.c1 - g.c0 + 1);
+        g.first = first;
+        first += (uint32_t)(g.l1 - g.l0 + 1);
+        off += g.row_bytes * (uint32_t)(g.l1 - g.l0 + 1);
+    }
+    R.bytes = off;
+    R.packed_rows = first;
+    return R;
+}
+
+// Rank r's rows of frame blockIdx.y, rectangle by rectangle, into out + frame * bytes (16-B words:
+// rows of W % 16 == 0 pixels on 16-B aligned buffers, column groups of 48 B).
+__global__ void __launch_bounds__(256) gather_pack_kernel(const uint8_t* __restrict__ local, uint64_t local_stride,
+                                                          uint8_t* __restrict__ out, RankLayout L, uint32_t W) {
+    const uint32_t q = blockIdx.x, k = blockIdx.y;
+    uint32_t i = 0;
+    while (i + 1 < L.nrect && q >= L.r[i + 1].first) ++i;
+    const GatherRect& g = L.r[i];
+    const uint32_t j = (uint32_t)g.l0 + (q - g.first);
+    const uint4* src = reinterpret_cast<const uint4*>(local + k * local_stride + (size_t)(L.rows - 1 - j) * W * 3u +
+                                                      48u * (uint32_t)g.c0);
+    uint4* dst = reinterpret_cast<uint4*>(out + (size_t)k * L.bytes + g.off + (size_t)(q - g.first) * g.row_bytes);
+    for (uint32_t w = threadIdx.x; w < g.row_bytes / 16u; w += blockDim.x) dst[w] = src[w];
+}
+
+// Rank 0: file row blockIdx.x of frame blockIdx.y — the miss colour, except inside the owning
+// rank's rectangles, whose bytes come from that rank's block of the receive buffer.
+__global__ void __launch_bounds__(256) gather_assemble_kernel(const uint8_t* __restrict__ recv,
+                                                              const RankLayout* __restrict__ lay, uint32_t B,
+                                                              uint8_t* __restrict__ frames, uint64_t frame_stride,
+                                                              uint32_t H, uint32_t W, uint32_t band, uint32_t N) {
+    __shared__ RankLayout s_L;
+    const uint32_t F = blockIdx.x, k = blockIdx.y;
+    const uint32_t Y = H - 1 - F;  // camera row
+    uint32_t r, j;
+    if (band) {
+        r = (Y / band) % N;
+        j = (Y / (N * band)) * band + Y % band;
+    } else {
+        const uint32_t h = H / N;
+        r = (H - 1 - Y) / h;
+        j = Y - (H - (r + 1) * h);
+    }
+    if (threadIdx.x < sizeof(RankLayout) / 4)
+        reinterpret_cast<uint32_t*>(&s_L)[threadIdx.x] = reinterpret_cast<const uint32_t*>(lay + r)[threadIdx.x];
+    __syncthreads();
+    uint32_t bg[3];
+    pattern_words(25u | (25u << 8) | (51u << 16), bg);  // sat_u8(0.1 * 255), sat_u8(0.2 * 255)
+    const uint8_t* base = recv + (size_t)B * s_L.off + (size_t)k * s_L.bytes;
+    uint4* dst = reinterpret_cast<uint4*>(frames + k * frame_stride + (size_t)F * W * 3u);
+    for (uint32_t w = threadIdx.x; w < W * 3u / 16u; w += blockDim.x) {
+        const uint32_t c = w / 3u;  // 16-pixel column group (48 B = 3 words)
+        uint4 v;
+        const uint32_t ph = w % 3u;
+        v = make_uint4(bg[ph], bg[(ph + 1) % 3u], bg[(ph + 2) % 3u], bg[ph]);
+        for (uint32_t i = 0; i < s_L.nrect; ++i) {
+            const GatherRect& g = s_L.r[i];
+            if ((int32_t)j >= g.l0 && (int32_t)j <= g.l1 && (int32_t)c >= g.c0 && (int32_t)c <= g.c1) {
+                v = reinterpret_cast<const uint4*>(base + g.off + (size_t)((int32_t)j - g.l0) * g.row_bytes)
+                    [w - 3u * (uint32_t)g.c0];
+                break;
+            }
+        }
+        dst[w] = v;
+    }
+}
+
 int nccl_error(eray_ctx* ctx, const char* what, ncclResult_t r) {
     char buf[256];
     std::snprintf(buf, sizeof buf, "%s: %s", what, ncclGetErrorString(r));
@@ -307,7 +489,8 @@ int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8
     ncclResult_t r = ncclCommCount(c, &nranks);
     if (r == ncclSuccess) r = ncclCommUserRank(c, &rank);
     if (r != ncclSuccess) return nccl_error(ctx, "gather: communicator", r);
-    if (band_rows % 4) return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "gather: band_rows must be a multiple of 4");
+    if (band_rows && (band_rows < 4 || (band_rows & (band_rows - 1))))  // as eray_render's bands (capi.cpp)
+        return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "gather: band_rows must be a power of two >= 4");
     if (!band_rows && height % (uint32_t)nranks)
         return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "gather: height does not split into equal blocks");
     const size_t row_bytes = (size_t)width * 3u;
@@ -388,6 +571,219 @@ int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8
     }
     return ERAY_OK;
 }
+
+}  // extern "C"
+
+namespace {
+// Builds (or reuses) the scene-camera plan of this rank: a collective (every rank calls it at the
+// same point), synchronising the stream once when the camera's setup changed.
+int scene_plan(eray_ctx* ctx, ncclComm_t c, int nranks, int rank, uint32_t H, uint32_t W, uint32_t band,
+               GatherPlan** out) {
+    GatherPlan*& P = *reinterpret_cast<GatherPlan**>(eray_internal_gather_plan(ctx, plan_free));
+    eray::gpu::SceneLayout L;
+    if (int st = eray_internal_scene_layout(ctx, &L)) return st;
+    if (P && P->valid && P->comm == (void*)c && P->gen == L.gen && P->H == H && P->W == W && P->band == band &&
+        P->nranks == (uint32_t)nranks && P->rank == (uint32_t)rank) {
+        *out = P;
+        return ERAY_OK;
+    }
+    if (!P) P = new (std::nothrow) GatherPlan();
+    if (!P) return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "gather plan");
+    P->valid = false;
+    if (L.W != W || L.H != H)
+        return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "scene-camera gather: the frame size is not the scene camera's");
+    const RankRows rr = rank_rows(H, band, (uint32_t)nranks, (uint32_t)rank);
+    if (L.row0 != rr.row0 || L.rows != rr.rows || L.band_shift != rr.shift || (band && L.band_stride != rr.stride))
+        return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT,
+                                   "scene-camera gather: the scene camera's last render covered other rows than this rank's share");
+    const auto mine = my_rects(L, rr, W);
+    int32_t rec[kXchgInts] = {};
+    rec[0] = (int32_t)mine.size();
+    for (size_t i = 0; i < mine.size(); ++i)
+        for (int q = 0; q < 4; ++q) rec[1 + 4 * i + q] = mine[i][q];
+    hipStream_t s = (hipStream_t)eray_get_stream(ctx);
+    hipError_t he;
+    if (!P->xchg && (he = hipMalloc((void**)&P->xchg, sizeof(int32_t) * kXchgInts * (size_t)(kMaxCodedRanks + 1))) != hipSuccess)
+        return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, hipGetErrorString(he));
+    if (nranks > kMaxCodedRanks) return eray_internal_error(ctx, ERAY_E_UNSUPPORTED, "scene-camera gather: more than 64 ranks");
+    std::vector<int32_t> all((size_t)kXchgInts * (size_t)nranks);
+    if ((he = hipMemcpyAsync(P->xchg, rec, sizeof rec, hipMemcpyHostToDevice, s)) != hipSuccess)
+        return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+    const ncclResult_t r = ncclAllGather(P->xchg, P->xchg + kXchgInts, kXchgInts, ncclInt32, c, s);
+    if (r != ncclSuccess) return nccl_error(ctx, "ncclAllGather (gather plan)", r);
+    if ((he = hipMemcpyAsync(all.data(), P->xchg + kXchgInts, sizeof(int32_t) * all.size(), hipMemcpyDeviceToHost, s)) !=
+            hipSuccess ||
+        (he = hipStreamSynchronize(s)) != hipSuccess)
+        return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+    P->ranks.assign((size_t)nranks, RankLayout{});
+    P->total = 0;
+    for (int q = 0; q < nranks; ++q) {
+        RankLayout R = layout_of(all.data() + (size_t)q * kXchgInts, rank_rows(H, band, (uint32_t)nranks, (uint32_t)q).rows);
+        R.off = P->total;
+        P->total += R.bytes;
+        P->ranks[(size_t)q] = R;
+    }
+    if (rank == 0) {
+        if (P->d_ranks) hipFree(P->d_ranks);
+        P->d_ranks = nullptr;
+        if ((he = hipMalloc((void**)&P->d_ranks, sizeof(RankLayout) * (size_t)nranks)) != hipSuccess ||
+            (he = hipMemcpy(P->d_ranks, P->ranks.data(), sizeof(RankLayout) * (size_t)nranks, hipMemcpyHostToDevice)) !=
+                hipSuccess)
+            return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+    }
+    P->comm = (void*)c;
+    P->gen = L.gen;
+    P->H = H;
+    P->W = W;
+    P->band = band;
+    P->nranks = (uint32_t)nranks;
+    P->rank = (uint32_t)rank;
+    P->valid = true;
+    *out = P;
+    return ERAY_OK;
+}
+
+int grow(eray_ctx* ctx, GatherPlan* P, size_t bytes) {
+    if (bytes <= P->buf_cap && P->buf) return ERAY_OK;
+    hipStream_t s = (hipStream_t)eray_get_stream(ctx);
+    hipError_t he = hipStreamSynchronize(s);  // (growth only: the first call of a batch size)
+    if (he == hipSuccess && P->buf) he = hipFree(P->buf);
+    P->buf = nullptr;
+    P->buf_cap = 0;
+    if (he == hipSuccess) he = hipMalloc((void**)&P->buf, std::max<size_t>(bytes, 256));
+    if (he != hipSuccess) return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, hipGetErrorString(he));
+    P->buf_cap = std::max<size_t>(bytes, 256);
+    return ERAY_OK;
+}
+
+// Pack (every rank), transfer, assemble (rank 0) `B` frames with plan P.
+int scene_gather(eray_ctx* ctx, ncclComm_t c, const GatherPlan& P, const uint8_t* local, uint64_t local_stride,
+                 uint8_t* frames, uint64_t frame_stride, uint32_t B) {
+    hipStream_t s = (hipStream_t)eray_get_stream(ctx);
+    const RankLayout& me = P.ranks[P.rank];
+    uint8_t* mine = P.rank == 0 ? P.buf + (size_t)B * me.off : P.buf;
+    hipError_t he;
+    if (me.bytes) {
+        gather_pack_kernel<<<dim3(me.packed_rows, B), 256, 0, s>>>(local, local_stride, mine, me, P.W);
+        if ((he = hipGetLastError()) != hipSuccess) return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+    }
+    if (P.nranks > 1) {
+        ncclResult_t r = ncclGroupStart();
+        if (r != ncclSuccess) return nccl_error(ctx, "ncclGroupStart", r);
+        if (P.rank == 0) {
+            for (uint32_t q = 1; q < P.nranks && r == ncclSuccess; ++q)
+                if (P.ranks[q].bytes)
+                    r = ncclRecv(P.buf + (size_t)B * P.ranks[q].off, (size_t)B * P.ranks[q].bytes, ncclUint8, (int)q, c, s);
+        } else if (me.bytes) {
+            r = ncclSend(mine, (size_t)B * me.bytes, ncclUint8, 0, c, s);
+        }
+        const ncclResult_t r2 = ncclGroupEnd();
+        if (r != ncclSuccess) return nccl_error(ctx, "ncclSend/ncclRecv", r);
+        if (r2 != ncclSuccess) return nccl_error(ctx, "ncclGroupEnd", r2);
+    }
+    if (P.rank == 0) {
+        gather_assemble_kernel<<<dim3(P.H, B), 256, 0, s>>>(P.buf, P.d_ranks, B, frames, frame_stride, P.H, P.W, P.band,
+                                                           P.nranks);
+        if ((he = hipGetLastError()) != hipSuccess) return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+    }
+    return ERAY_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int eray_gather_frames(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint64_t local_stride, uint8_t* frames,
+                       uint64_t frame_stride, uint32_t nframes, uint32_t height, uint32_t width, uint32_t band_rows,
+                       uint32_t flags) {
+    if (!ctx || !nccl_comm) return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "gather: null context or comm");
+    if (flags & ~(uint32_t)ERAY_GATHER_SCENE_CAMERA)
+        return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "gather: unknown flags");
+    if (int st = eray_internal_use_device(ctx)) return st;
+    ncclComm_t c = (ncclComm_t)nccl_comm;
+    int nranks = 0, rank = 0;
+    ncclResult_t r = ncclCommCount(c, &nranks);
+    if (r == ncclSuccess) r = ncclCommUserRank(c, &rank);
+    if (r != ncclSuccess) return nccl_error(ctx, "gather: communicator", r);
+    if (!nframes || !height || !width) return ERAY_OK;
+    const bool aligned = width % 16 == 0 && ((reinterpret_cast<uintptr_t>(local) | reinterpret_cast<uintptr_t>(frames) |
+                                              local_stride | frame_stride) & 15) == 0;
+    const bool rows_ok = band_rows ? band_rows >= 4 && !(band_rows & (band_rows - 1)) : height % (uint32_t)nranks == 0;
+    if ((flags & ERAY_GATHER_SCENE_CAMERA) && aligned && rows_ok && local && (rank != 0 || frames)) {
+        GatherPlan* P = nullptr;
+        if (int st = scene_plan(ctx, c, nranks, rank, height, width, band_rows, &P)) return st;
+        const size_t need = rank == 0 ? (size_t)nframes * P->total : (size_t)nframes * P->ranks[(size_t)rank].bytes;
+        if (int st = grow(ctx, P, need)) return st;
+        return scene_gather(ctx, c, *P, local, local_stride, frames, frame_stride, nframes);
+    }
+    for (uint32_t k = 0; k < nframes; ++k)  // one frame at a time through eray_gather_rows
+        if (int st = eray_gather_rows(ctx, nccl_comm, local ? local + k * local_stride : nullptr,
+                                      frames ? frames + k * frame_stride : nullptr, height, width, band_rows))
+            return st;
+    return ERAY_OK;
+}
+
+// Diagnostics (tests): the scene-camera gather of N ranks simulated on one GPU.  The context has
+// rendered the scene camera's whole frame (its setup's rectangles stand for every rank's);
+// staging holds the N ranks' padded local PPM blocks (rows_max = rank 0's rows, band_rows > 0:
+// bands, 0: blocks); each is packed with its rank's layout into one receive buffer, which is
+// assembled into frame.
+int eray_debug_scene_gather(eray_ctx* ctx, const uint8_t* staging, uint8_t* frame, uint32_t height, uint32_t width,
+                            uint32_t band_rows, uint32_t nranks) {
+    if (!ctx || !staging || !frame || !nranks || nranks > (uint32_t)kMaxCodedRanks || width % 16 ||
+        (band_rows && (band_rows < 4 || (band_rows & (band_rows - 1)))) || (!band_rows && height % nranks))
+        return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "scene gather: bad arguments");
+    eray::gpu::SceneLayout L;
+    if (int st = eray_internal_scene_layout(ctx, &L)) return st;
+    if (L.W != width || L.H != height || L.row0 != 0 || L.rows != height || L.band_shift != 31u)
+        return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "scene gather: render the whole scene-camera frame first");
+    GatherPlan P;
+    P.H = height;
+    P.W = width;
+    P.band = band_rows;
+    P.nranks = nranks;
+    P.rank = 0;
+    const uint32_t rows_max = rank_rows(height, band_rows, nranks, 0).rows;
+    for (uint32_t q = 0; q < nranks; ++q) {
+        const RankRows rr = rank_rows(height, band_rows, nranks, q);
+        const auto mine = my_rects(L, rr, width);
+        int32_t rec[kXchgInts] = {};
+        rec[0] = (int32_t)mine.size();
+        for (size_t i = 0; i < mine.size(); ++i)
+            for (int k = 0; k < 4; ++k) rec[1 + 4 * i + k] = mine[i][k];
+        RankLayout R = layout_of(rec, rr.rows);
+        R.off = P.total;
+        P.total += R.bytes;
+        P.ranks.push_back(R);
+    }
+    hipStream_t s = (hipStream_t)eray_get_stream(ctx);
+    hipError_t he = hipMalloc((void**)&P.d_ranks, sizeof(RankLayout) * nranks);
+    if (he == hipSuccess) he = hipMalloc((void**)&P.buf, std::max<size_t>(P.total, 256));
+    if (he == hipSuccess)
+        he = hipMemcpyAsync(P.d_ranks, P.ranks.data(), sizeof(RankLayout) * nranks, hipMemcpyHostToDevice, s);
+    for (uint32_t q = 0; q < nranks && he == hipSuccess; ++q) {
+        const RankLayout& R = P.ranks[q];
+        if (!R.bytes) continue;
+        gather_pack_kernel<<<dim3(R.packed_rows, 1), 256, 0, s>>>(staging + (size_t)q * rows_max * width * 3u, 0,
+                                                                  P.buf + R.off, R, width);
+        he = hipGetLastError();
+    }
+    if (he == hipSuccess) {
+        gather_assemble_kernel<<<dim3(height, 1), 256, 0, s>>>(P.buf, P.d_ranks, 1, frame, 0, height, width, band_rows,
+                                                              nranks);
+        he = hipGetLastError();
+    }
+    if (he == hipSuccess) he = hipStreamSynchronize(s);
+    if (P.d_ranks) hipFree(P.d_ranks);
+    if (P.buf) hipFree(P.buf);
+    P.d_ranks = nullptr;
+    P.buf = nullptr;
+    P.xchg = nullptr;
+    return he == hipSuccess ? ERAY_OK : eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+}
+
+}  // extern "C"
+
+extern "C" {
 
 // Diagnostics (tests): the coded banded gather of N ranks on one GPU — staging holds the N ranks'
 // padded local PPM blocks; each is encoded into rank 0's code / packed layout as the point-to-

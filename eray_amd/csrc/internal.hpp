@@ -4,6 +4,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <array>
+#include <vector>
+
 namespace eray {
 namespace gpu {
 
@@ -191,6 +194,13 @@ struct FrameParams {
     // trace_kernel's culling records for this camera (scenes of at most kTraceSkipTris faces;
     // null: no background skip), written by trace_cull_kernel before the frame
     TriCull* trace_cull;
+    // Frames in flight: one launch renders `nframes` (>= 1) independent frames, its workgroups
+    // dealt round-robin over them (frame_kernel).  Frame f writes out_* + f * *_stride (bytes,
+    // multiples of 16) and, with dev_slots, reads the batched per-camera setup of slot f
+    // (cam_state + f, cull + f * total_tris, objects + f * nobj: launch_camera_setup_batch).
+    uint32_t nframes;
+    uint32_t dev_slots;
+    uint64_t rgb_stride, ppm_stride, face_stride;
 };
 
 // Camera row of rank-local row j (FrameParams::band_shift; shifts and masks: no division in the
@@ -357,6 +367,17 @@ void bins_free(BinBuffers& b);
 // and the detail sub-block list of rows [row0, row0 + rows) with CamState::total_sub.
 hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tiles_x, bool ordered, hipStream_t s);
 hipError_t launch_pack_ppm(const float* rgb, uint32_t w, uint32_t h, uint8_t* out, hipStream_t s);
+
+// ------------------------------------------------------------- capi.cpp internals for comm.cpp
+// The scene camera's current setup: its generation (changes with every setup), Camera::size, the
+// rendered rows (FrameParams band fields) and every object's pixel rectangle (ObjGeom::rect:
+// x0, x1, y0, y1 inclusive, camera rows; empty when x0 > x1) — outside them the frame kernel
+// writes the background colour.
+struct SceneLayout {
+    uint64_t gen;
+    uint32_t W, H, row0, rows, band_shift, band_stride;
+    std::vector<std::array<int32_t, 4>> rects;
+};
 
 hipError_t launch_wave(uint32_t w, uint32_t h, float xf, float yf, float* out, hipStream_t s);
 hipError_t launch_rgb(uint32_t w, uint32_t h, const float* r, const float* g, const float* b,

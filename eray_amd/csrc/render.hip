@@ -163,10 +163,13 @@ struct FrameHot {
 
 struct SceneGlobal {
     const FrameParams& p;
-    __device__ ObjGeom geom(uint32_t i) const { return load_const(&p.objects[i].g, 0); }
-    __device__ MaterialDesc mat(uint32_t i) const { return load_const(&p.objects[i].mat, 0); }
+    const ObjectDesc* objects;  // the frame's descriptors and culling records (a batched camera
+    const TriCull* culls;       // setup's slot: FrameParams::dev_slots)
+    __device__ ObjGeom geom(uint32_t i) const { return load_const(&objects[i].g, 0); }
+    __device__ MaterialDesc mat(uint32_t i) const { return load_const(&objects[i].mat, 0); }
     __device__ LightDesc light(uint32_t i) const { return load_const(p.lights, i); }
-    __device__ TriCull cull(uint32_t g) const { return p.cull[g]; }        // per lane
+    __device__ TriCull cull(uint32_t g) const { return culls[g]; }          // per lane
+    __device__ const TriCull* cull_array() const { return culls; }
     __device__ TriHot hot(uint32_t g) const { return load_const(p.tris, g); }  // uniform
     __device__ TriHot hot_lane(uint32_t g) const { return as_global_rec(p.tris + g); }  // per lane
     __device__ TriShade shade(uint32_t g) const { return p.shade[g]; }     // per lane
@@ -181,6 +184,7 @@ struct SceneLds {
     const ObjectDesc* g_objs;  // the device arrays (scalar loads of uniform records)
     const LightDesc* g_lights;
     const TriHot* g_tris;
+    const TriCull* g_cull;
     // Wave-uniform records (objects, materials, lights) by scalar loads from the device arrays,
     // not LDS reads + readfirstlane: C2 8.67 -> 8.40 us per frame (profiles/ab/ab_c2chain.log),
     // though one wave's chain alone is 0.2 us longer (7.26 -> 7.44 us, a 4-row frame).
@@ -188,6 +192,7 @@ struct SceneLds {
     __device__ MaterialDesc mat(uint32_t i) const { return load_const(&g_objs[i].mat, 0); }
     __device__ LightDesc light(uint32_t i) const { return load_const(g_lights, i); }
     __device__ TriCull cull(uint32_t g) const { return culls[g]; }
+    __device__ const TriCull* cull_array() const { return g_cull; }
     __device__ TriHot hot(uint32_t g) const { return hots[g]; }  // broadcast read (VGPRs)
     __device__ TriHot hot_lane(uint32_t g) const { return hots[g]; }
     __device__ TriShade shade(uint32_t g) const { return shades[g]; }
@@ -234,7 +239,7 @@ __device__ SceneLds preload_scene(const FrameHot& p, char* dyn, Meanwhile&& mean
     }
     return SceneLds{reinterpret_cast<const ObjectDesc*>(dyn + L.objs), reinterpret_cast<const LightDesc*>(dyn + L.lights),
                     reinterpret_cast<const TriCull*>(dyn + L.cull), reinterpret_cast<const TriHot*>(dyn + L.hot),
-                    reinterpret_cast<const TriShade*>(dyn + L.shade), p.objects, p.lights, p.tris};
+                    reinterpret_cast<const TriShade*>(dyn + L.shade), p.objects, p.lights, p.tris, p.cull};
 }
 
 // Lanes whose Triangle::intersects could pass: the det and t conditions of exact_test, from the
@@ -461,7 +466,7 @@ __device__ void first_hit(const FrameParams& p, const Scene& sc, uint32_t begin,
         const uint32_t n = min((uint32_t)kTriTile, count - base);
         if (threadIdx.x < n) {
             s_hot[threadIdx.x] = p.tris[begin + base + threadIdx.x];
-            if (kCull) s_cull[threadIdx.x] = p.cull[begin + base + threadIdx.x];
+            if (kCull) s_cull[threadIdx.x] = sc.cull_array()[begin + base + threadIdx.x];
         }
         __syncthreads();
         if (!__any(st != kDone)) continue;
@@ -661,8 +666,8 @@ __device__ const float g_texel_dummy[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 // The frame's camera: the kernel arguments, or the setup kernel's copy in device-camera mode
 // (FrameParams::cam_state; wave-uniform, scalar loads).
 template <bool kDev>
-__device__ __forceinline__ CamDev frame_camera(const FrameParams& p) {
-    if (kDev) return load_const(&p.cam_state->cam, 0);
+__device__ __forceinline__ CamDev frame_camera(const FrameParams& p, const CamState* cs) {
+    if (kDev) return load_const(&cs->cam, 0);
     return CamDev{p.cx, p.cy, p.cz, p.ratio, p.z_dist, {0u, 0u, 0u}};
 }
 
@@ -734,6 +739,19 @@ __device__ __forceinline__ void stream16(B* base, const void* dst, float4 v) {
     stream16(base, dst, make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)));
 }
 
+// One frame's output arrays (FrameParams::out_* of the frame: frames in flight write their own).
+struct FrameOut {
+    float* rgb;
+    uint8_t* ppm;
+    int32_t* face;
+};
+__device__ __forceinline__ FrameOut frame_out(const FrameParams& p, uint32_t fr) {
+    return FrameOut{p.out_rgb ? reinterpret_cast<float*>(reinterpret_cast<char*>(p.out_rgb) + fr * p.rgb_stride) : nullptr,
+                    p.out_ppm ? p.out_ppm + fr * p.ppm_stride : nullptr,
+                    p.out_face ? reinterpret_cast<int32_t*>(reinterpret_cast<char*>(p.out_face) + fr * p.face_stride)
+                               : nullptr};
+}
+
 // background (engine.rs:208-213) and its bytes: sat_u8(0.1*255) = 25, sat_u8(0.2*255) = 51
 __device__ __forceinline__ float4 bg_rgb4(uint32_t phase) {  // 16-byte word at float offset 4c
     const float a = 0.1f, b = 0.2f;
@@ -749,28 +767,28 @@ __device__ __forceinline__ uint4 bg_ppm16(uint32_t phase) {  // 16-byte word at 
 
 // Background for the pixels [x0, x0 + w) x rows [py0, py0 + kBlkH) (w = 64 or 16), wave-wide.
 template <uint32_t kW>
-__device__ __forceinline__ void fill_background(const FrameParams& p, uint32_t x0, uint32_t py0, bool aligned,
+__device__ __forceinline__ void fill_background(const FrameParams& p, const FrameOut& o, uint32_t x0, uint32_t py0, bool aligned,
                                                 uint32_t lane) {
     if (aligned && x0 + kW <= p.cam_w && py0 + kBlkH <= p.rows) {
         constexpr uint32_t kRow4 = kW * 3 / 4;    // float4 per RGB row
         constexpr uint32_t kRow16 = kW * 3 / 16;  // 16-byte words per PPM row
         constexpr uint32_t kFace4 = kW / 4;       // int4 per face row
-        if (p.out_rgb) {
+        if (o.rgb) {
 #pragma unroll
             for (uint32_t i = lane; i < kBlkH * kRow4; i += 64) {
                 const uint32_t r = i / kRow4, c = i % kRow4;
-                stream16(p.out_rgb, reinterpret_cast<float4*>(p.out_rgb + 3 * ((size_t)(py0 + r) * p.img_w + x0)) + c,
+                stream16(o.rgb, reinterpret_cast<float4*>(o.rgb + 3 * ((size_t)(py0 + r) * p.img_w + x0)) + c,
                          bg_rgb4(c % 3));
             }
         }
-        if (p.out_ppm && lane < kBlkH * kRow16) {
+        if (o.ppm && lane < kBlkH * kRow16) {
             const uint32_t r = lane / kRow16, c = lane % kRow16;
             const size_t row = (size_t)(p.rows - py0 - kBlkH + r);  // file rows, bottom-up
-            stream16(p.out_ppm, reinterpret_cast<uint4*>(p.out_ppm + 3 * (row * p.img_w + x0)) + c, bg_ppm16(c % 3));
+            stream16(o.ppm, reinterpret_cast<uint4*>(o.ppm + 3 * (row * p.img_w + x0)) + c, bg_ppm16(c % 3));
         }
-        if (p.out_face && lane < kBlkH * kFace4) {
+        if (o.face && lane < kBlkH * kFace4) {
             const uint32_t r = lane / kFace4, c = lane % kFace4;
-            stream16(p.out_face, reinterpret_cast<int4*>(p.out_face + (size_t)(py0 + r) * p.img_w + x0) + c,
+            stream16(o.face, reinterpret_cast<int4*>(o.face + (size_t)(py0 + r) * p.img_w + x0) + c,
                      make_uint4(~0u, ~0u, ~0u, ~0u));
         }
     } else {  // image edge or unaligned output: per pixel
@@ -780,19 +798,19 @@ __device__ __forceinline__ void fill_background(const FrameParams& p, uint32_t x
             const uint32_t px = x0 + k % kW, py = py0 + k / kW;
             if (px >= p.cam_w || py >= p.rows) continue;
             const size_t idx = (size_t)py * p.img_w + px;
-            if (p.out_rgb) {
-                float* o = p.out_rgb + 3 * idx;
-                o[0] = b.x;
-                o[1] = b.y;
-                o[2] = b.z;
+            if (o.rgb) {
+                float* q = o.rgb + 3 * idx;
+                q[0] = b.x;
+                q[1] = b.y;
+                q[2] = b.z;
             }
-            if (p.out_ppm) {
-                uint8_t* o = p.out_ppm + 3 * ((size_t)(p.rows - 1 - py) * p.img_w + px);
-                o[0] = (uint8_t)c01;
-                o[1] = (uint8_t)c01;
-                o[2] = (uint8_t)c02;
+            if (o.ppm) {
+                uint8_t* q = o.ppm + 3 * ((size_t)(p.rows - 1 - py) * p.img_w + px);
+                q[0] = (uint8_t)c01;
+                q[1] = (uint8_t)c01;
+                q[2] = (uint8_t)c02;
             }
-            if (p.out_face) p.out_face[idx] = -1;
+            if (o.face) o.face[idx] = -1;
         }
     }
 }
@@ -811,8 +829,8 @@ __device__ __forceinline__ bool rect_meets(const ObjGeom& ob, const RowMap& rm, 
 // without them carries none of their code or registers.
 constexpr int kMatSpecPow = 1, kMatExample = 2;
 template <bool kCull, bool kLdsTiles, int kMat, typename Scene>
-__device__ __forceinline__ void render_sub(const FrameParams& p, const CamDev& cam, const RowMap& rm, const Scene& sc,
-                                           uint32_t wx0, uint32_t py0,
+__device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut& fo, const CamDev& cam, const RowMap& rm,
+                                           const Scene& sc, uint32_t wx0, uint32_t py0,
                                            bool active, TriHot* s_hot, TriCull* s_cull, char* s_bins, float4* s_rgb,
                                            uint32_t* s_ppm, bool aligned, const f3* given_d = nullptr) {
     constexpr bool kSpecPow = (kMat & kMatSpecPow) != 0, kExample = (kMat & kMatExample) != 0;
@@ -1051,7 +1069,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const CamDev& c
     ERAY_TRACE_WAVE0(6);
     // ---- outputs: Image::set + Color::as_bytes, rows bottom-up (image.rs:41-74) ---
     const uint32_t b0 = sat_u8(acc.r * 255.0f), b1 = sat_u8(acc.g * 255.0f), b2 = sat_u8(acc.b * 255.0f);
-    if (valid && p.out_face) p.out_face[(size_t)py * p.img_w + px] = have ? best_face : -1;
+    if (valid && fo.face) fo.face[(size_t)py * p.img_w + px] = have ? best_face : -1;
     if (active && aligned && wx0 + kSubW <= p.cam_w && py0 + kBlkH <= p.rows) {
         // the wave's 16 x 4 pixels leave through its own LDS slice as 16-B row stores
         constexpr uint32_t kWavePix = kSubW * kBlkH;
@@ -1071,30 +1089,30 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const CamDev& c
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         constexpr uint32_t kRgbRow4 = kSubW * 3 / 4;    // float4 per wave row (12)
         constexpr uint32_t kPpmRow16 = kSubW * 3 / 16;  // 16-byte words per wave row (3)
-        if (p.out_rgb && lane < kBlkH * kRgbRow4) {
+        if (fo.rgb && lane < kBlkH * kRgbRow4) {
             const uint32_t r = lane / kRgbRow4, c = lane % kRgbRow4;
-            float4* dst = reinterpret_cast<float4*>(p.out_rgb + 3 * ((size_t)(py0 + r) * p.img_w + wx0)) + c;
-            stream16(p.out_rgb, dst, reinterpret_cast<const float4*>(wrgb)[lane]);
+            float4* dst = reinterpret_cast<float4*>(fo.rgb + 3 * ((size_t)(py0 + r) * p.img_w + wx0)) + c;
+            stream16(fo.rgb, dst, reinterpret_cast<const float4*>(wrgb)[lane]);
         }
-        if (p.out_ppm && lane < kBlkH * kPpmRow16) {
+        if (fo.ppm && lane < kBlkH * kPpmRow16) {
             const uint32_t r = lane / kPpmRow16, c = lane % kPpmRow16;  // r-th byte row of the block
             const size_t row = (size_t)(p.rows - py0 - kBlkH + r);
-            uint4* dst = reinterpret_cast<uint4*>(p.out_ppm + 3 * (row * p.img_w + wx0)) + c;
-            stream16(p.out_ppm, dst, reinterpret_cast<const uint4*>(wppm)[lane]);
+            uint4* dst = reinterpret_cast<uint4*>(fo.ppm + 3 * (row * p.img_w + wx0)) + c;
+            stream16(fo.ppm, dst, reinterpret_cast<const uint4*>(wppm)[lane]);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next block
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     } else if (valid) {
         const size_t idx = (size_t)py * p.img_w + px;
-        if (p.out_rgb) {
-            float* o = p.out_rgb + 3 * idx;
+        if (fo.rgb) {
+            float* o = fo.rgb + 3 * idx;
             o[0] = acc.r;
             o[1] = acc.g;
             o[2] = acc.b;
         }
-        if (p.out_ppm) {
-            uint8_t* o = p.out_ppm + 3 * ((size_t)(p.rows - 1 - py) * p.img_w + px);
+        if (fo.ppm) {
+            uint8_t* o = fo.ppm + 3 * ((size_t)(p.rows - 1 - py) * p.img_w + px);
             o[0] = (uint8_t)b0;
             o[1] = (uint8_t)b1;
             o[2] = (uint8_t)b2;
@@ -1109,13 +1127,13 @@ struct SubRect {  // sub-block coordinates (x in kSubW columns, y in kBlkH local
     int32_t sx0, sx1, sy0, sy1;
 };
 template <bool kDev>
-__device__ __forceinline__ SubRect frame_rect(const FrameParams& p, uint32_t k) {
-    if (kDev) return load_const(reinterpret_cast<const SubRect*>(p.cam_state->rects), k);
+__device__ __forceinline__ SubRect frame_rect(const FrameParams& p, const CamState* cs, uint32_t k) {
+    if (kDev) return load_const(reinterpret_cast<const SubRect*>(cs->rects), k);
     return SubRect{p.rects[k][0], p.rects[k][1], p.rects[k][2], p.rects[k][3]};
 }
 template <bool kDev>
-__device__ __forceinline__ uint32_t frame_nrect(const FrameParams& p) {
-    return kDev ? load_const(&p.cam_state->nrect, 0) : p.nrect;
+__device__ __forceinline__ uint32_t frame_nrect(const FrameParams& p, const CamState* cs) {
+    return kDev ? load_const(&cs->nrect, 0) : p.nrect;
 }
 __device__ __forceinline__ bool inside(const SubRect& r, int32_t sx, int32_t sy) {
     return sx >= r.sx0 && sx <= r.sx1 && sy >= r.sy0 && sy <= r.sy1;
@@ -1124,14 +1142,15 @@ __device__ __forceinline__ bool inside(const SubRect& r, int32_t sx, int32_t sy)
 // The background of the non-detail sub-blocks: fill workgroup f of nf strides over the 64 x 4
 // blocks (shared by the frame kernel's fill roles and fill_kernel).
 template <bool kDev>
-__device__ __forceinline__ void fill_blocks(const FrameParams& p, uint32_t f, uint32_t nf, uint32_t wave,
+__device__ __forceinline__ void fill_blocks(const FrameParams& p, const FrameOut& o, const CamState* cs, uint32_t f, uint32_t nf,
+                                            uint32_t wave,
                                             uint32_t lane, bool aligned) {
     constexpr uint32_t nwaves = kWG / 64;
     const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
     const uint32_t fstride = nf * nwaves;
     uint32_t occ = 0;  // detail list: lane i holds the occupancy of this wave's i-th next block
     uint32_t it = 0;
-    const uint32_t nrect = p.detail_occ ? 0u : frame_nrect<kDev>(p);
+    const uint32_t nrect = p.detail_occ ? 0u : frame_nrect<kDev>(p, cs);
     // block coordinates advance incrementally (no integer division per block)
     const uint32_t first = wave * nf + f, step_y = fstride / p.tiles_x, step_x = fstride - step_y * p.tiles_x;
     uint32_t by = first / p.tiles_x, bx = first - by * p.tiles_x;
@@ -1153,7 +1172,7 @@ __device__ __forceinline__ void fill_blocks(const FrameParams& p, uint32_t f, ui
             mask = (uint32_t)__builtin_amdgcn_readlane((int)occ, (int)(it & 63u));
         }
         for (uint32_t k = 0; k < nrect; ++k) {
-            const SubRect r = frame_rect<kDev>(p, k);
+            const SubRect r = frame_rect<kDev>(p, cs, k);
             if ((int32_t)by < r.sy0 || (int32_t)by > r.sy1) continue;
 #pragma unroll
             for (int32_t i = 0; i < 4; ++i) {
@@ -1162,11 +1181,24 @@ __device__ __forceinline__ void fill_blocks(const FrameParams& p, uint32_t f, ui
             }
         }
         if (!mask) {
-            fill_background<kBlkW>(p, bx * kBlkW, by * kBlkH, aligned, lane);
+            fill_background<kBlkW>(p, o, bx * kBlkW, by * kBlkH, aligned, lane);
         } else if (mask != 0xfu) {
             for (uint32_t i = 0; i < 4; ++i)
-                if (!((mask >> i) & 1u)) fill_background<kSubW>(p, bx * kBlkW + i * kSubW, by * kBlkH, aligned, lane);
+                if (!((mask >> i) & 1u)) fill_background<kSubW>(p, o, bx * kBlkW + i * kSubW, by * kBlkH, aligned, lane);
         }
+    }
+}
+
+// Fill role q of nf over the launch's frames: virtual roles v (more than nf only when nf < F),
+// frame v % F, its (v / F)-th fill workgroup.
+template <bool kDev>
+__device__ __forceinline__ void fill_frames(const FrameParams& p, uint32_t q, uint32_t nf, uint32_t wave, uint32_t lane,
+                                            bool aligned) {
+    const uint32_t F = p.nframes, roles = max(nf, F);
+    for (uint32_t v = q; v < roles; v += nf) {
+        const uint32_t fr = v % F;
+        fill_blocks<kDev>(p, frame_out(p, fr), p.cam_state + (p.dev_slots ? fr : 0u), v / F, (roles - fr + F - 1) / F,
+                          wave, lane, aligned);
     }
 }
 
@@ -1183,8 +1215,7 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     // h_roles (a preloaded argument, see frame_roles): the grid size, the detail workgroups and
     // the role flags, so the role decision — and the scene preload behind it — does not wait for
     // a kernel-argument load from memory
-    const FrameHot hot{h_objects, h_lights, h_cull, h_tris, h_shade, h_counts, h_total_tris, h_total_sub,
-                       h_roles & 0x7fffu};
+    const uint32_t grid = h_roles & 0x7fffu;  // == gridDim.x, without the implicit-argument load
     uint32_t detail_wgs = (h_roles >> 15) & 0x7fffu;
     bool fill_first = (h_roles >> 30) & 1u;
     const bool separate_fill = (h_roles >> 31) & 1u;
@@ -1202,20 +1233,29 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t nwaves = kWG / 64;
     const bool aligned = p.aligned != 0;  // (a kernel-argument read where it is used)
-    // detail sub-blocks (device-camera mode: counted by the setup kernels, and the small-scene
-    // fill reservation chosen from that count as launch_frame_kernel does from the host's)
-    const uint32_t total = kDev ? load_const(&p.cam_state->total_sub, 0) : hot.total_sub;
-    if (kDev && p.detail_wgs_alt && total > detail_wgs * nwaves) {
+    // Frames in flight: the launch renders F independent frames; detail and fill workgroups are
+    // dealt round-robin over them (frame v % F), so one frame's latency-bound detail chains
+    // overlap the others' fill stores instead of ending the launch alone.
+    const uint32_t F = p.nframes;
+    auto cam_state = [&](uint32_t fr) { return p.cam_state + (p.dev_slots ? fr : 0u); };
+    // detail sub-blocks per frame (device-camera mode: counted by the setup kernels; the most of
+    // any frame sizes the detail roles), and the small-scene fill reservation chosen from that
+    // count as launch_frame_kernel does from the host's
+    uint32_t total_max = h_total_sub;
+    if (kDev) {
+        total_max = 0;
+        for (uint32_t fr = 0; fr < F; ++fr) total_max = max(total_max, load_const(&cam_state(fr)->total_sub, 0));
+    }
+    if (kDev && p.detail_wgs_alt && F * total_max > detail_wgs * nwaves) {
         detail_wgs = p.detail_wgs_alt;
         fill_first = true;
     }
-    const uint32_t grid = hot.grid;        // == gridDim.x, without the implicit-argument load
     // workgroups [0, nd) render the detail sub-blocks (persistent: rounds of nd * 4 sub-blocks),
     // the others write the background at the same time; at most detail_wgs detail workgroups
     // (the launcher keeps a share of the grid for the fill, so a large detail area overlaps the
     // fill's HBM writes instead of preceding them); when every workgroup has detail work, all of
     // them fill afterwards
-    const uint32_t nd = min(detail_wgs ? detail_wgs : grid, (total + nwaves - 1) / nwaves);
+    const uint32_t nd = min(detail_wgs ? detail_wgs : grid, F * ((total_max + nwaves - 1) / nwaves));
     // the workgroup's role index: detail roles [0, nd), fill roles [nd, grid); with fill_first
     // the fill roles go to the first-dispatched (older, VALU-priority) workgroups
     const uint32_t bid = (fill_first && nd < grid) ? (blockIdx.x + nd) % grid : blockIdx.x;
@@ -1223,59 +1263,74 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     ERAY_TRACE_POINT(0);
     // ---- detail sub-blocks -------------------------------------------------------------------
     if (bid < nd) {
-        const uint32_t nrect = p.detail_list ? 0u : frame_nrect<kDev>(p);
-        const CamDev cam = frame_camera<kDev>(p);
         const RowMap rm{p.row0, h_band & 31u, h_band >> 5};
-        // detail sub-block j (enumeration order) -> sub-block coordinates
-        auto locate = [&](uint32_t j, int32_t& sx, int32_t& sy) {
-            if (p.detail_list) {
-                const uint32_t e = p.detail_list[j];
-                sx = (int32_t)(e & 0xffffu);
-                sy = (int32_t)(e >> 16);
-                return;
-            }
-            for (uint32_t k = 0; k < nrect; ++k) {  // the rectangles are disjoint (setup): by area
-                const SubRect r = frame_rect<kDev>(p, k);
-                const uint32_t w = (uint32_t)(r.sx1 - r.sx0 + 1);
-                const uint32_t a = w * (uint32_t)(r.sy1 - r.sy0 + 1);
-                if (j < a) {
-                    sx = r.sx0 + (int32_t)(j % w);
-                    sy = r.sy0 + (int32_t)(j / w);
+        const uint32_t nobj = h_counts & 0xffffu;
+        // virtual detail roles v (more than nd only when nd < F): frame v % F, its (v / F)-th
+        // detail workgroup of nk
+        const uint32_t roles = max(nd, F);
+        for (uint32_t v = bid; v < roles; v += nd) {
+            const uint32_t fr = v % F, kw = v / F, nk = (roles - fr + F - 1) / F;
+            const CamState* cs = cam_state(fr);
+            const uint32_t total = kDev ? load_const(&cs->total_sub, 0) : h_total_sub;
+            const FrameOut fo = frame_out(p, fr);
+            const uint32_t slot = p.dev_slots ? fr : 0u;
+            const ObjectDesc* objs = h_objects + (size_t)slot * nobj;
+            const TriCull* culls = h_cull ? h_cull + (size_t)slot * h_total_tris : nullptr;
+            const uint32_t nrect = p.detail_list ? 0u : frame_nrect<kDev>(p, cs);
+            const CamDev cam = frame_camera<kDev>(p, cs);
+            // detail sub-block j (enumeration order) -> sub-block coordinates
+            auto locate = [&](uint32_t j, int32_t& sx, int32_t& sy) {
+                if (p.detail_list) {
+                    const uint32_t e = p.detail_list[j];
+                    sx = (int32_t)(e & 0xffffu);
+                    sy = (int32_t)(e >> 16);
                     return;
                 }
-                j -= a;
-            }
-        };
-        // the wave's first sub-block and its camera rays, before the scene is in: the kernel
-        // arguments' scalar loads and the ray arithmetic overlap the preload's round trip
-        const uint32_t c0 = bid * nwaves;
-        int32_t sx0 = 0, sy0 = 0;
-        f3 d0;
-        constexpr bool kGivenRay = true;
-        auto first_rays = [&]() {
-            if (c0 + wave < total) locate(c0 + wave, sx0, sy0);
-            d0 = camera_dir(cam, p, (uint32_t)sx0 * kSubW + lane % kSubW, cam_row(rm, (uint32_t)sy0 * kBlkH + lane / kSubW));
-            asm volatile("" : "+v"(d0.x), "+v"(d0.y), "+v"(d0.z));  // here, not after the barrier
-        };
-        auto detail = [&](const auto& sc) {
-            for (uint32_t c = c0; c < total; c += nd * nwaves) {  // workgroup-uniform
-                const uint32_t j = c + wave;
-                const bool active = j < total;
-                int32_t sx = sx0, sy = sy0;
-                if (c != c0 && active) locate(j, sx, sy);
-                render_sub<kCull, kLdsTiles, kMat>(p, cam, rm, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH, active,
-                                                       s_hot, s_cull, s_bins, s_rgb, s_ppm, aligned,
+                for (uint32_t k = 0; k < nrect; ++k) {  // the rectangles are disjoint (setup): by area
+                    const SubRect r = frame_rect<kDev>(p, cs, k);
+                    const uint32_t w = (uint32_t)(r.sx1 - r.sx0 + 1);
+                    const uint32_t a = w * (uint32_t)(r.sy1 - r.sy0 + 1);
+                    if (j < a) {
+                        sx = r.sx0 + (int32_t)(j % w);
+                        sy = r.sy0 + (int32_t)(j / w);
+                        return;
+                    }
+                    j -= a;
+                }
+            };
+            // the wave's first sub-block and its camera rays, before the scene is in: the kernel
+            // arguments' scalar loads and the ray arithmetic overlap the preload's round trip
+            const uint32_t c0 = kw * nwaves;
+            int32_t sx0 = 0, sy0 = 0;
+            f3 d0;
+            constexpr bool kGivenRay = true;
+            auto first_rays = [&]() {
+                if (c0 + wave < total) locate(c0 + wave, sx0, sy0);
+                d0 = camera_dir(cam, p, (uint32_t)sx0 * kSubW + lane % kSubW, cam_row(rm, (uint32_t)sy0 * kBlkH + lane / kSubW));
+                asm volatile("" : "+v"(d0.x), "+v"(d0.y), "+v"(d0.z));  // here, not after the barrier
+            };
+            auto detail = [&](const auto& sc) {
+                for (uint32_t c = c0; c < total; c += nk * nwaves) {  // workgroup-uniform
+                    const uint32_t j = c + wave;
+                    const bool active = j < total;
+                    int32_t sx = sx0, sy = sy0;
+                    if (c != c0 && active) locate(j, sx, sy);
+                    render_sub<kCull, kLdsTiles, kMat>(p, fo, cam, rm, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH,
+                                                       active, s_hot, s_cull, s_bins, s_rgb, s_ppm, aligned,
                                                        (kGivenRay && c == c0) ? &d0 : nullptr);
+                }
+            };
+            if constexpr (kLdsScene) {
+                if (v != bid) __syncthreads();  // the previous frame's reads of the LDS scene are done
+                const FrameHot hf{objs, h_lights, culls, h_tris, h_shade, h_counts, h_total_tris, h_total_sub, grid};
+                const SceneLds sc = preload_scene(hf, dyn, first_rays);
+                __syncthreads();
+                detail(sc);
+            } else {
+                const SceneGlobal sc{p, objs, culls};
+                first_rays();
+                detail(sc);
             }
-        };
-        if constexpr (kLdsScene) {
-            const SceneLds sc = preload_scene(hot, dyn, first_rays);
-            __syncthreads();
-            detail(sc);
-        } else {
-            const SceneGlobal sc{p};
-            first_rays();
-            detail(sc);
         }
         ERAY_TRACE_POINT(1);
         if (nd < grid) {
@@ -1288,7 +1343,7 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     const uint32_t nf = nd < grid ? grid - nd : grid;  // filling workgroups
     const uint32_t f = nd < grid ? bid - nd : bid;
     ERAY_TRACE_POINT(2);
-    fill_blocks<kDev>(p, f, nf, wave, lane, aligned);
+    fill_frames<kDev>(p, f, nf, wave, lane, aligned);
     ERAY_TRACE_POINT(3);
 }
 
@@ -1297,7 +1352,7 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
 // register budget of the large-mesh detail build.
 template <bool kDev>
 __global__ void __launch_bounds__(kWG) fill_kernel(FrameParams p) {
-    fill_blocks<kDev>(p, blockIdx.x, gridDim.x, threadIdx.x >> 6, threadIdx.x & 63, p.aligned != 0);
+    fill_frames<kDev>(p, blockIdx.x, gridDim.x, threadIdx.x >> 6, threadIdx.x & 63, p.aligned != 0);
 }
 
 // Image<Color>::save_as_ppm body: byte row k = image row h-1-k.
@@ -1374,7 +1429,9 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
     // (27.8 us; share 3 29.4-30.3, share 4 37), while a small-scene frame with more than one
     // round of detail sub-blocks (the cube at 3840x2160) wants one fill workgroup per CU
     // dispatched first (share 3, fill_first: 22.8 -> 20.4 us; at C2 fill_first costs 0.7 us).
-    const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
+    // blocks and detail sub-blocks of all the launch's frames (frames in flight)
+    const uint32_t nblk = p.nframes * p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
+    const uint32_t total_sub = p.nframes * p.total_sub;
     auto detail_wgs = [&](float share) {
         return share >= 1.0f && grid >= 2 ? grid - max(min((uint32_t)((float)grid / share), (nblk + 63) / 64), 1u)
                                           : 0u;
@@ -1386,7 +1443,7 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
     if (!L) {
         if (p.cam_state) {  // the count is on the device: frame_kernel picks the share
             q.detail_wgs_alt = detail_wgs(3.0f);
-        } else if (p.total_sub > q.detail_wgs * (kWG / 64)) {
+        } else if (total_sub > q.detail_wgs * (kWG / 64)) {
             q.detail_wgs = detail_wgs(3.0f);
             q.fill_first = 1;
         }
@@ -1404,13 +1461,13 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
         // it on / off).
         const bool separate = (p.launch_flags & kLaunchSeparateFill)     ? true
                               : (p.launch_flags & kLaunchNoSeparateFill) ? false
-                                                                         : p.total_sub > 16u * cus;
+                                                                         : total_sub > 16u * cus;
         if (separate) {
             if (!lc.side || !lc.fork || !lc.join) return hipErrorInvalidValue;
             q.separate_fill = 1;
             q.detail_wgs = 0;
             q.fill_first = 0;
-            const uint32_t dgrid = max(1u, min(min(grid, 2u * cus), (p.total_sub + kWG / 64 - 1) / (kWG / 64)));
+            const uint32_t dgrid = max(1u, min(min(grid, 2u * cus), (total_sub + kWG / 64 - 1) / (kWG / 64)));
             const uint32_t fgrid = max(1u, min(2u * cus, (nblk + 3) / 4));
             hipError_t e;
             if ((e = hipEventRecord(lc.fork, s)) != hipSuccess || (e = hipStreamWaitEvent(lc.side, lc.fork, 0)) != hipSuccess)
@@ -1446,7 +1503,7 @@ hipError_t launch_frame_cs(const FrameParams& p, uint32_t want, const LaunchCtx&
             // (ERAY_RENDER_DENSE_DETAIL / _NO_DENSE_DETAIL force it on / off)
             const bool dense = (p.launch_flags & kLaunchDense)     ? true
                                : (p.launch_flags & kLaunchNoDense) ? false
-                                                                   : p.total_sub > device_cus() * (kWG / 64);
+                                                                   : p.nframes * p.total_sub > device_cus() * (kWG / 64);
             if (dense) return launch_frame_kernel<C, true, M, false, true, V>(p, want, 0, lc, s);
         }
         return launch_frame_kernel<C, true, M, false, false, V>(p, want, 0, lc, s);
@@ -1456,13 +1513,14 @@ hipError_t launch_frame_cs(const FrameParams& p, uint32_t want, const LaunchCtx&
 }  // namespace
 
 hipError_t launch_render(const FrameParams& p, const LaunchCtx& lc, hipStream_t s) {
+    if (p.nframes < 1 || ((p.aa || p.bounces) && p.nframes != 1)) return hipErrorInvalidValue;
     if (p.aa || p.bounces) return launch_trace(p, s);
     const uint32_t by_n = (p.rows + kBlkH - 1) / kBlkH;
     const uint32_t nblk = p.tiles_x * by_n;
     if (!nblk) return hipSuccess;
     // enough workgroups for one fill block or one round of detail sub-blocks per wave (device-
     // camera mode: the detail count is not known here, so as many as fit)
-    const uint32_t want = p.cam_state ? max((nblk + 3) / 4, nblk) : max((nblk + 3) / 4, (p.total_sub + 3) / 4);
+    const uint32_t want = p.nframes * (p.cam_state ? max((nblk + 3) / 4, nblk) : max((nblk + 3) / 4, (p.total_sub + 3) / 4));
     const int mat = (p.spec_pow ? kMatSpecPow : 0) | (p.example_mat ? kMatExample : 0);
     // device-camera mode (the setup's CamState) is a separate build: args-mode frames carry no
     // branch or load for it

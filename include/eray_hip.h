@@ -30,6 +30,7 @@
  *                           reaches_light engine.rs:218-228) fused with the PPM byte pack
  *   eray_pack_ppm           lib/image.rs:48-74 + lib/color.rs:31-37 (save_as_ppm body bytes)
  *   eray_gather_rows        lib/engine.rs:85-98 + lib/image.rs:48-74 across GPUs (row tiles, RCCL)
+ *   eray_gather_frames      the same for a batch of frames (a frame ring), optionally sync-free
  *   eray_ppm_header         lib/image.rs:56
  *   eray_camera_size        lib/camera.rs:36-38
  *
@@ -54,7 +55,7 @@
 extern "C" {
 #endif
 
-#define ERAY_ABI_VERSION 3
+#define ERAY_ABI_VERSION 4
 
 typedef enum eray_status {
     ERAY_OK = 0,
@@ -287,6 +288,36 @@ int eray_render_prepare(eray_ctx* ctx, const eray_render_params* params, uint32_
 int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* params, const eray_camera* cameras,
                             uint32_t n, float* mean_frame_ms);
 
+/* Frames in flight.  A serving or animation loop renders a stream of independent frames; the
+ * ring variants below give frame k of a call its own outputs — ring slot k % slots, at
+ * out_rgb + (k % slots) * rgb_stride (bytes; likewise out_ppm / out_face) — so that several frames
+ * can be rendered by ONE kernel launch (frames_per_launch): one frame's latency-bound shading
+ * chains then overlap the other frames' background stores instead of ending the launch alone.
+ * Every frame is rendered in full, bit-identical to eray_render's; a slot stays valid until frame
+ * k + slots of the same call overwrites it.  The plain eray_render_frames /
+ * eray_render_camera_path are the ring calls with one slot (every frame into the same outputs,
+ * one frame per launch). */
+typedef struct eray_frame_ring {
+    uint32_t slots;                 /* a power of two <= 64 */
+    uint32_t frames_per_launch;     /* a power of two <= slots; 0: the library's choice (frames of
+                                       up to 3840x2160 pixels together per launch, at most 8;
+                                       anti-aliasing / bounces: 1) */
+    uint64_t rgb_stride;            /* bytes between slots of each non-NULL output: a multiple of */
+    uint64_t ppm_stride;            /* 16 and at least one slot's size (ignored when slots == 1) */
+    uint64_t face_stride;
+} eray_frame_ring;
+int eray_render_frames_ring(eray_ctx* ctx, const eray_render_params* params, const eray_frame_ring* ring,
+                            uint32_t frames, float* mean_frame_ms);
+int eray_render_prepare_ring(eray_ctx* ctx, const eray_render_params* params, const eray_frame_ring* ring,
+                             uint32_t frames);
+/* The frames per launch the library picks (frames_per_launch = 0) for these parameters, the scene
+ * camera and a ring of `slots` slots — e.g. to size a ring of exactly that many slots. */
+uint32_t eray_frames_per_launch(eray_ctx* ctx, const eray_render_params* params, uint32_t slots);
+/* Camera paths of scenes whose per-camera setups are batched (no mesh over 256 faces) render
+ * frames_per_launch frames per launch; others one (each camera rebuilds the screen bins). */
+int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* params, const eray_frame_ring* ring,
+                                 const eray_camera* cameras, uint32_t n, float* mean_frame_ms);
+
 /* ------------------------------------------------------------------ multi-GPU ----------- *
  * One process (one context) per GPU; a frame is split into row tiles and gathered on rank 0
  * (SURVEY.md §8(e)).  Rank r of n renders the r-th block of PPM file rows — camera rows
@@ -314,6 +345,25 @@ int eray_comm_destroy(void* nccl_comm);
  * write (engine.rs:85-98 render_to_path -> save_as_ppm). */
 int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8_t* frame, uint32_t height,
                      uint32_t width, uint32_t band_rows);
+/* `nframes` frames at once (frame k: local + k * local_stride on every rank, frames + k *
+ * frame_stride on rank 0), e.g. a ring of eray_render_frames_ring slots gathered while the next
+ * frames render on another stream.  flags:
+ *   ERAY_GATHER_DEFAULT       — eray_gather_rows per frame.
+ *   ERAY_GATHER_SCENE_CAMERA  — the local rows are this context's renders of its scene camera
+ *     (eray_render / eray_render_frames[_ring] without anti-aliasing or bounces, over this rank's
+ *     share: the band or block split above).  The frame kernel writes the miss colour (engine.rs:
+ *     212) at every pixel outside the objects' pixel rectangles, where no primary ray can hit a
+ *     face, so only the bytes inside those rectangles travel: each rank packs them, rank 0
+ *     receives them with fixed-size point-to-point transfers and writes every frame row.  The
+ *     ranks exchange their rectangles once per camera setup (the first call after a new setup
+ *     synchronises the context's stream; a batch size's first call allocates); every later call
+ *     only enqueues kernels and transfers — no host round trip, capturable in a HIP graph.
+ *     Needs width % 16 == 0 and 16-byte aligned buffers and strides (else per-frame gathers). */
+#define ERAY_GATHER_DEFAULT 0u
+#define ERAY_GATHER_SCENE_CAMERA 1u
+int eray_gather_frames(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint64_t local_stride, uint8_t* frames,
+                       uint64_t frame_stride, uint32_t nframes, uint32_t height, uint32_t width, uint32_t band_rows,
+                       uint32_t flags);
 /* Camera rows of rank `rank` in the interleaved band split of a frame of `height` rows. */
 uint32_t eray_band_rows(uint32_t height, uint32_t band_rows, uint32_t nranks, uint32_t rank);
 

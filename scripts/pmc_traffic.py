@@ -77,7 +77,8 @@ def pmc(tag: str, pmc_dir: str = "pmc", out_name: str = "pmc_traffic.json", work
                     d = json.loads(line)
                     cfg = d["config"]
                     workload = {"mesh": cfg["mesh"], "frame": cfg["frame"], "rows_per_gpu": cfg["rows_per_gpu"],
-                                "n_gpus": d["n_gpus"], "brute_force": not cfg["culling"]}
+                                "n_gpus": d["n_gpus"], "brute_force": not cfg["culling"],
+                                "frames_per_launch": cfg.get("frames_per_launch", 1)}
     out = {"round": tag, "workload": workload, "frame_kernel": {
         "kernel": name,
         "dispatches": dispatches,

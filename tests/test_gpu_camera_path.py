@@ -214,3 +214,32 @@ def test_bin_overflow_falls_back_and_grows(gpu, standin70k):
     finally:
         out.free()
         sc.close()
+
+
+def test_path_graph_not_replayed_after_bin_reallocation(gpu, standin70k):
+    """A camera path captured while the bins overflowed, then a render that grows the capacity
+    (every bin buffer reallocated), then the same path again: the path's cached graph holds the
+    old buffers' addresses and must be captured anew (bins generation in the key)."""
+    W, H = 480, 270
+    sc = MainScene(gpu, *standin70k, W, H, texture=256, fov=(16.0, 9.0))
+    out = Out(gpu, W, H)
+    L = capi.lib()
+    try:
+        cam = capi.make_camera((0.1, -0.1, 4.2), (16.0, 9.0), W, 1.0)
+        ref = per_camera(gpu, out, cam, flags=capi.RENDER_BRUTE_FORCE)
+        assert L.eray_debug_set_bin_capacity(gpu.handle, 16) == 0
+        for rep in range(2):
+            out.clear()
+            gpu.render_camera_path([cam, cam, cam], W, H, **out.kw())  # overflowed bins: LDS tiles
+            check(out.get(), ref, f"overflowed path {rep}")
+        out.clear()
+        gpu.render(W, H, **out.kw())  # the count reached the host: capacity grown, buffers reallocated
+        check(out.get(), ref, "render after growth")
+        assert L.eray_debug_bin_capacity(gpu.handle) > 16
+        for rep in range(2):
+            out.clear()
+            gpu.render_camera_path([cam, cam, cam], W, H, **out.kw())
+            check(out.get(), ref, f"path after reallocation {rep}")
+    finally:
+        out.free()
+        sc.close()

@@ -47,16 +47,18 @@ def _banded_blocks(frame, H, W, band, world):
     """Each rank's padded local PPM block (local file order) of a file-order frame, as
     eray_render writes it for dist.band_split (numpy restatement of eray_band_rows' split)."""
     cam = frame[::-1]  # camera rows
-    rows_max = len(range(0, H, band * world)) * band
+    rows_max = capi.band_rows(H, band, world, 0)  # rank 0 holds the most rows (the padded size)
     blocks = np.zeros((world, rows_max, W, 3), np.uint8)
     for r in range(world):
         mine = [y for y in range(H) if (y // band) % world == r]
+        assert len(mine) == capi.band_rows(H, band, world, r)
         blocks[r, :len(mine)] = cam[mine][::-1]
     return blocks
 
 
 @pytest.mark.parametrize("W,H,band,world", [(192, 64, 4, 1), (192, 64, 4, 2), (208, 68, 4, 3), (37, 40, 8, 2),
-                                            (1920, 120, 4, 8), (70, 12, 4, 5), (64, 30, 4, 3)])
+                                            (1920, 120, 4, 8), (70, 12, 4, 5), (64, 30, 4, 3),
+                                            (64, 26, 4, 3)])  # the short tail band on rank 0
 def test_coded_banded_gather_layout(gpu, W, H, band, world):
     rng = np.random.default_rng(W * 7 + H + world)
     frame = np.empty((H, W, 3), np.uint8)
@@ -104,3 +106,96 @@ def test_one_rank_banded_gather_through_rccl(gpu, cube):
         local.free()
         frame.free()
         sc.close()
+
+
+def _blocks_of(frame, H, W, band, world):
+    """Each rank's padded local PPM rows of a file-order frame: interleaved bands, or (band 0)
+    the rank's block of file rows."""
+    if band:
+        return _banded_blocks(frame, H, W, band, world)
+    h = H // world
+    return np.ascontiguousarray(frame.reshape(world, h, W, 3))
+
+
+@pytest.fixture(scope="module")
+def standin70k_gather():
+    from eray_amd import meshgen
+    v, n, t, fv, ft, fn = meshgen.displaced_sphere(**meshgen.STANDIN_70K)
+    return (np.ascontiguousarray(v[fv].reshape(-1, 9)), np.ascontiguousarray(n[fn].reshape(-1, 9)),
+            np.ascontiguousarray(t[ft].reshape(-1, 6)))
+
+
+@pytest.mark.parametrize("mesh", ["cube", "standin70k"])
+def test_scene_camera_gather_layout(gpu, cube, standin70k_gather, mesh):
+    """The scene-camera gather (only the objects' pixel rectangles travel, comm.cpp) of N ranks
+    simulated on one GPU: every rank's rows packed with its own rectangles, then assembled — the
+    frame must be the rendered frame, byte for byte, for bands and blocks."""
+    W, H = (320, 180) if mesh == "cube" else (480, 270)
+    sc = MainScene(gpu, *(cube if mesh == "cube" else standin70k_gather), W, H, texture=64, fov=(16.0, 9.0))
+    ppm = gpu.empty((H, W, 3), np.uint8)
+    out = gpu.empty((H, W, 3), np.uint8)
+    try:
+        gpu.render(W, H, out_ppm=ppm.ptr)
+        frame = ppm.numpy()
+        assert (frame != np.array([25, 25, 51], np.uint8)).any()
+        for world in (1, 2, 3, 5, 8):
+            for band in (0, 4, 8):
+                if not band and H % world:
+                    continue
+                blocks = _blocks_of(frame, H, W, band, world)
+                staging = gpu.to_device(blocks)
+                try:
+                    gpu.memset(out.ptr, 0, out.nbytes)
+                    assert capi.lib().eray_debug_scene_gather(gpu.handle, staging.ptr, out.ptr, H, W, band, world) == 0
+                    assert np.array_equal(out.numpy(), frame), (world, band)
+                finally:
+                    staging.free()
+    finally:
+        ppm.free()
+        out.free()
+        sc.close()
+
+
+def test_one_rank_gather_frames_and_graph_capture(cube):
+    """eray_gather_frames on a one-rank communicator: a ring of rendered frames, gathered per
+    frame (coded path) and scene-camera style, then the scene-camera gather captured in a HIP
+    graph (torch.cuda.CUDAGraph on the context's stream) and replayed — no host synchronisation
+    inside, so the capture succeeds and the replay assembles the frames again."""
+    import torch
+    W, H, S = 320, 180, 4
+    st = torch.cuda.Stream()
+    gpu = capi.Context(0)  # its own context: the stream below outlives nothing else
+    gpu.set_stream(st.cuda_stream)
+    sc = MainScene(gpu, *cube, W, H, texture=64, fov=(16.0, 9.0))
+    ring = capi.frame_ring(S, H, W)
+    rgb = gpu.empty((S, H, W, 3), np.float32)
+    local = gpu.empty((S, H, W, 3), np.uint8)
+    frames = gpu.empty((S, H, W, 3), np.uint8)
+    comm = None
+    try:
+        gpu.render_frames(S, W, H, out_rgb=rgb.ptr, out_ppm=local.ptr, ring=ring)
+        gpu.synchronize()
+        want = local.numpy()
+        assert (want[0] != np.array([25, 25, 51], np.uint8)).any()
+        comm = gpu.comm_init(1, 0, capi.comm_unique_id())
+        slot = H * W * 3
+        for scene_camera in (False, True):
+            gpu.memset(frames.ptr, 0, frames.nbytes)
+            gpu.gather_frames(comm, local.ptr, slot, frames.ptr, slot, S, H, W, scene_camera=scene_camera)
+            gpu.synchronize()
+            assert np.array_equal(frames.numpy(), want), scene_camera
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            gpu.gather_frames(comm, local.ptr, slot, frames.ptr, slot, S, H, W, scene_camera=True)
+        gpu.memset(frames.ptr, 0, frames.nbytes)
+        gpu.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(frames.numpy(), want), "graph replay"
+    finally:
+        if comm:
+            capi.comm_destroy(comm)
+        for a in (rgb, local, frames):
+            a.free()
+        sc.close()
+        gpu.close()
