@@ -1166,15 +1166,20 @@ struct Ring {
     uint64_t rgb = 0, ppm = 0, face = 0;  // bytes between slots
 };
 // One launch renders at most this many pixels (frames x rows x width) when the library picks the
-// frames per launch: enough frames to overlap the latency-bound detail chains of small frames
-// (C2: 4 frames), one frame of 3840x2160 and more (their fill alone saturates the HBM writes).
-constexpr uint64_t kInFlightPixels = 3840ull * 2160ull;
+// frames per launch, at most kMaxInFlight frames.  Measured (scripts/frames_in_flight.py,
+// profiles/r03/frames_in_flight.jsonl, device us per frame by frames per launch): the cube at
+// 1920x1080 9.3 / 7.6 / 5.4 / 5.0 for 1 / 2 / 4 / 8, at 3840x2160 22.9 / 19.6 for 1 / 2; the 70k
+// stand-in (screen bins, heavier detail work) at 1920x1080 14.2 / 9.2 / 8.2 / 9.2, at 3840x2160
+// 29.1 / 34.5 for 1 / 2.  So two frames of 3840x2160 pixels for small scenes, one for scenes with
+// binned meshes.
+constexpr uint64_t kInFlightPixels = 2ull * 3840ull * 2160ull, kInFlightPixelsBinned = 3840ull * 2160ull;
 constexpr uint32_t kMaxInFlight = 8;
 
 // The library's frames per launch for frames of cam_w x rows pixels and a ring of `slots`.
-uint32_t auto_frames(uint64_t cam_w, uint64_t rows, uint32_t slots) {
+uint32_t auto_frames(uint64_t cam_w, uint64_t rows, uint32_t slots, bool binned) {
+    const uint64_t cap = binned ? kInFlightPixelsBinned : kInFlightPixels;
     uint32_t F = 1;
-    while (F * 2 <= kMaxInFlight && F * 2 <= slots && (uint64_t)(F * 2) * cam_w * rows <= kInFlightPixels) F *= 2;
+    while (F * 2 <= kMaxInFlight && F * 2 <= slots && (uint64_t)(F * 2) * cam_w * rows <= cap) F *= 2;
     return F;
 }
 
@@ -1207,7 +1212,7 @@ int make_ring(eray_ctx* ctx, const eray_render_params* rp, const FrameParams& p,
     } else if (r->frames_per_launch) {
         F = r->frames_per_launch;
     } else {
-        F = auto_frames(p.cam_w, p.rows, r->slots);
+        F = auto_frames(p.cam_w, p.rows, r->slots, p.max_object_tris > kDirectMax);
     }
     out->per_launch = F;
     return ERAY_OK;
@@ -1259,7 +1264,9 @@ uint32_t eray_frames_per_launch(eray_ctx* ctx, const eray_render_params* rp, uin
     if (rp->anti_aliasing || rp->bounces) return 1u;
     uint32_t W, H;
     eray_camera_size(&ctx->camera, &W, &H);
-    return auto_frames(W, rp->rows, slots);
+    bool binned = false;
+    for (auto& o : ctx->objects) binned |= o.T > kDirectMax;
+    return auto_frames(W, rp->rows, slots, binned);
 }
 
 int eray_render_prepare(eray_ctx* ctx, const eray_render_params* rp, uint32_t frames) {

@@ -17,6 +17,7 @@ step() {  # name timeout cmd...
 }
 step pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider
 step fif 400 python -u scripts/frames_in_flight.py --big
+TAILN=100 step fill_mlp 200 scripts/microbench/fill_mlp
 TAILN=1 step bench 300 python bench.py --steps 200 --warmup 20 --cpu-seconds 3
 TAILN=1 step bench20 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline
 TAILN=1 step rehearsal_n2 300 env ERAY_BENCH_REHEARSAL=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 40 --warmup 5

@@ -196,3 +196,135 @@ def test_c5_8k_1m_tiles_spans_and_brute_force(gpu, synth1m):
         blk.free()
         fr.free()
         sc.close()
+
+
+def test_north_star_4k_70k_full_frame_binned_equals_brute_force(gpu):
+    """BASELINE north_star: the 69,451-face stand-in at 3840x2160.  The binned frame — the
+    library's own launch choice (the dense 3-per-CU detail build and the heavy-first ordered
+    detail list), the 2-per-CU build, and the dense build with the separate fill kernel — equals
+    the brute-force scan over the whole frame, bit for bit (object.rs:63-78: first hit by index);
+    so do two frames in flight per launch, the 4-band split's ranks and the scene-camera gather of
+    their rows."""
+    mesh = _mesh(**meshgen.STANDIN_70K)
+    W, H = 3840, 2160
+    sc = MainScene(gpu, *mesh, W, H, texture=1024, fov=(16.0, 9.0))
+    fr = Frame(gpu, W, H)
+    try:
+        ref = [x.copy() for x in fr.render(W, H, flags=capi.RENDER_BRUTE_FORCE)]
+        assert (ref[1] >= 0).sum() > 100_000
+        for flags in (capi.RENDER_DEFAULT, capi.RENDER_NO_DENSE_DETAIL,
+                      capi.RENDER_DENSE_DETAIL | capi.RENDER_SEPARATE_FILL):
+            got = fr.render(W, H, flags=flags)
+            assert np.array_equal(got[1], ref[1]), f"faces, flags {flags}"
+            assert_bit_equal(got[0], ref[0], f"4k/70k binned vs brute force, flags {flags}")
+            assert np.array_equal(got[2], ref[2]), f"ppm, flags {flags}"
+        ring_rgb = gpu.empty((2, H, W, 3), np.float32)
+        ring_ppm = gpu.empty((2, H, W, 3), np.uint8)
+        try:
+            gpu.memset(ring_rgb.ptr, 0, ring_rgb.nbytes)
+            gpu.render_frames(2, W, H, out_rgb=ring_rgb.ptr, out_ppm=ring_ppm.ptr, ring=capi.frame_ring(2, H, W, 2))
+            gpu.synchronize()
+            rgb2, ppm2 = ring_rgb.numpy(), ring_ppm.numpy()
+            for s in range(2):
+                assert_bit_equal(rgb2[s], ref[0], f"frame {s} of two in flight")
+                assert np.array_equal(ppm2[s], ref[2])
+        finally:
+            ring_rgb.free()
+            ring_ppm.free()
+        _bands_assemble(gpu, W, H, 4, ref)
+        fr.render(W, H)  # the scene camera's whole frame: its setup's rectangles for the gather
+        staging = gpu.to_device(_band_blocks(ref[2], H, W, 4, 4))
+        out = gpu.empty((H, W, 3), np.uint8)
+        try:
+            assert capi.lib().eray_debug_scene_gather(gpu.handle, staging.ptr, out.ptr, H, W, 4, 4) == 0
+            assert np.array_equal(out.numpy(), ref[2]), "scene-camera gather of the 4 bands"
+        finally:
+            staging.free()
+            out.free()
+    finally:
+        fr.free()
+        sc.close()
+
+
+def _band_blocks(frame, H, W, band, world):
+    """Each rank's padded local PPM rows (local file order) of a file-order frame in the band split."""
+    cam = frame[::-1]
+    rows_max = capi.band_rows(H, band, world, 0)
+    blocks = np.zeros((world, rows_max, W, 3), np.uint8)
+    for r in range(world):
+        mine = [y for y in range(H) if (y // band) % world == r]
+        blocks[r, :len(mine)] = cam[mine][::-1]
+    return blocks
+
+
+def test_c5_every_64th_row_block_equals_brute_force(gpu, synth1m):
+    """C5 (1M faces, 7680x4320): every 64th 4-row block of the binned frame equals the GPU's
+    brute-force scan of the same rows (~5e11 ray-triangle tests), where the culling margins are
+    thinnest (tiny faces, 7680-pixel rows)."""
+    W, H = 7680, 4320
+    sc = MainScene(gpu, *synth1m, W, H, texture=1024, fov=(16.0, 9.0))
+    fr = Frame(gpu, W, H)
+    blk = Frame(gpu, W, 4)
+    try:
+        rgb, face, _ = [x.copy() for x in fr.render(W, H)]
+        checked = 0
+        for y0 in range(0, H, 64 * 4):
+            b_rgb, b_face, _ = blk.render(W, H, row0=y0, rows=4, flags=capi.RENDER_BRUTE_FORCE)
+            assert np.array_equal(b_face, face[y0:y0 + 4]), f"rows {y0}+4"
+            assert_bit_equal(b_rgb, rgb[y0:y0 + 4], f"c5 rows {y0}+4")
+            checked += int((b_face >= 0).sum())
+        assert checked > 5_000
+    finally:
+        blk.free()
+        fr.free()
+        sc.close()
+
+
+def _corner_ray_point(W, H, ratio, x, y, t):
+    """The point at parameter t along the (unnormalised) camera ray through pixel corner (x, y)
+    of main.rs's camera (centre (0, 0, 5), z_dist 1, viewport 2*ratio x 2): camera.rs:57-76."""
+    px = -ratio + 2.0 * ratio * x / W
+    py = -1.0 + 2.0 * y / H
+    return np.array([t * px, t * py, 5.0 - t], np.float64)
+
+
+@pytest.mark.parametrize("faces", [200, 3000])
+def test_culling_margins_on_pixel_corner_rays(gpu, faces):
+    """Adversarial culling: triangles whose vertices lie on pixel-corner camera rays and whose
+    edges pass through pixel corners (the exact rays the frame kernel traces, x/W and y/H), at
+    W = 7680 where a pixel is 1/7680 of the viewport.  The culled frame (per-wave bounds for 200
+    faces, screen bins for 3000) must equal the brute-force scan bit for bit."""
+    W, H = 7680, 4320
+    ratio = 16.0 / 9.0
+    rng = np.random.default_rng(faces)
+    pos = np.empty((faces, 9), np.float32)
+    cx, cy = 3840, 2160  # around the frame centre (the degenerate bbox passes every camera ray)
+    for i in range(faces):
+        x0, y0 = cx + int(rng.integers(-300, 300)), cy + int(rng.integers(-160, 160))
+        t = rng.uniform(4.0, 6.0, 3)
+        if i % 2:  # a small triangle with all three vertices on pixel-corner rays
+            pts = [_corner_ray_point(W, H, ratio, x0 + int(dx), y0 + int(dy), tt)
+                   for (dx, dy), tt in zip([(0, 0), (int(rng.integers(1, 6)), 0), (0, int(rng.integers(1, 6)))], t)]
+        else:  # an edge whose midpoint is on a pixel-corner ray: symmetric about that ray
+            mid = _corner_ray_point(W, H, ratio, x0, y0, t[0])
+            off = rng.normal(size=3) * 2e-3
+            far = _corner_ray_point(W, H, ratio, x0 + int(rng.integers(-4, 5)), y0 + int(rng.integers(2, 6)), t[1])
+            pts = [mid + off, mid - off, far]
+        if rng.integers(2):
+            pts = pts[::-1]  # both windings (backfaces are culled by the test)
+        pos[i] = np.concatenate(pts).astype(np.float32)
+    nrm = rng.normal(size=(faces, 9)).astype(np.float32)
+    uv = rng.uniform(0.0, 1.0, (faces, 6)).astype(np.float32)
+    rows, row0 = 336, 2160 - 168
+    sc = MainScene(gpu, pos, nrm, uv, W, H, texture=64, fov=(16.0, 9.0))
+    blk = Frame(gpu, W, rows)
+    try:
+        a = [x.copy() for x in blk.render(W, H, row0=row0, rows=rows)]
+        b = blk.render(W, H, row0=row0, rows=rows, flags=capi.RENDER_BRUTE_FORCE)
+        assert (b[1] >= 0).sum() > 100
+        assert np.array_equal(a[1], b[1]), "faces"
+        assert_bit_equal(a[0], b[0], "culled vs brute force on pixel-corner geometry")
+        assert np.array_equal(a[2], b[2])
+    finally:
+        blk.free()
+        sc.close()
