@@ -5,7 +5,9 @@ split over the host's cores (ctypes releases the GIL; the oracle keeps no global
 
     python tests/golden/make_c3_digest.py [--threads N]
 
-Adds digests["c3"] with the same fields as the other frames (make_golden.py).
+Adds digests["c3"] with the same fields as the other frames (make_golden.py), and c3_rows.npz:
+camera rows 540 and 541 (through the stand-in's centre) as f32 RGB and faces, which the CPU suite
+re-renders with the oracle in about a second (tests/test_golden.py).  --rows-only writes just those.
 """
 import argparse
 import concurrent.futures as cf
@@ -33,13 +35,25 @@ def c3_mesh():
             np.ascontiguousarray(t[ft].reshape(-1, 6)))
 
 
+ROWS = (540, 2)
+
+
+def c3_rows(scene, cam) -> None:
+    rgb, face, _ = O.render(scene, cam, row0=ROWS[0], rows=ROWS[1], want_faces=True)
+    np.savez_compressed(os.path.join(HERE, "c3_rows.npz"), row0=ROWS[0], rgb=rgb, face=face)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 4)
+    ap.add_argument("--rows-only", action="store_true")
     a = ap.parse_args()
     scene = O.main_rs_scene(*c3_mesh(), texture=1024)
     cam = O.camera((0.0, 0.0, 5.0), FOV, W, 1.0)
     assert O.camera_size(cam) == (W, H)
+    c3_rows(scene, cam)
+    if a.rows_only:
+        return
     chunk = 8
     rgb = np.zeros((H, W, 3), np.float32)
     face = np.full((H, W), -1, np.int32)

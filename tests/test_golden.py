@@ -38,6 +38,24 @@ def test_oracle_reproduces_digests(oracle, cube, tag):
     assert stats == g["stats"]
 
 
+def test_oracle_reproduces_c3_rows(oracle):
+    """C3 (the 69,451-face stand-in at 1920x1080, main.rs's 1024x1024 material): two camera rows
+    through the mesh centre, re-rendered by the oracle, equal the committed rows of the same run
+    that produced digests["c3"] (make_c3_digest.py); the GPU test compares the whole frame with
+    those digests."""
+    from eray_amd import meshgen
+    fx = np.load(os.path.join(GOLDEN, "c3_rows.npz"))
+    v, n, t, fv, ft, fn = meshgen.displaced_sphere(**meshgen.STANDIN_70K)
+    mesh = (v[fv].reshape(-1, 9), n[fn].reshape(-1, 9), t[ft].reshape(-1, 6))
+    scene = oracle.main_rs_scene(*mesh, texture=1024)
+    row0 = int(fx["row0"])
+    rgb, face, _ = oracle.render(scene, oracle.camera((0.0, 0.0, 5.0), (16.0, 9.0), 1920, 1.0), row0=row0,
+                                 rows=fx["face"].shape[0], want_faces=True)
+    assert (face >= 0).sum() > 300
+    assert np.array_equal(face, fx["face"])
+    assert np.array_equal(rgb.view(np.uint32), fx["rgb"].view(np.uint32))
+
+
 def test_oracle_reproduces_c1_fixture(oracle, cube):
     fx = np.load(os.path.join(GOLDEN, "cube_c1_256.npz"))
     scene = oracle.main_rs_scene(*cube, texture=1024)

@@ -116,7 +116,11 @@ def _bands_assemble(gpu, W, H, world, full, band=dist.BAND_ROWS):
 
 def test_c3_full_frame_binned_equals_brute_force(gpu):
     """C3 at 1920x1080 (69,451-face stand-in): the binned frame equals the brute-force scan over the
-    whole frame, bit for bit, for both material paths."""
+    whole frame, bit for bit, for both material paths, and the oracle's whole C3 frame at main.rs's
+    1024x1024 material (its committed digests: tests/golden/make_c3_digest.py, ~1.4e11 tests on the
+    CPU)."""
+    with open(os.path.join(GOLDEN, "digests.json")) as f:
+        g = json.load(f)["c3"]
     mesh = _mesh(**meshgen.STANDIN_70K)
     W, H = 1920, 1080
     fr = Frame(gpu, W, H)
@@ -130,6 +134,11 @@ def test_c3_full_frame_binned_equals_brute_force(gpu):
             assert np.array_equal(a[1], b[1]), material
             assert_bit_equal(a[0], b[0], f"c3 full frame binned vs brute force ({material})")
             assert np.array_equal(a[2], b[2])
+            rgb, face, ppm = a
+            assert int((face >= 0).sum()) == g["hit_pixels"], material
+            assert _sha(face.astype(np.int32)) == g["face_sha256"], f"c3 faces vs oracle ({material})"
+            assert _sha(rgb.astype(np.float32)) == g["rgb_f32_sha256"], f"c3 rgb vs oracle ({material})"
+            assert _sha(ppm) == g["ppm_body_sha256"], f"c3 ppm vs oracle ({material})"
     finally:
         fr.free()
 
