@@ -261,7 +261,8 @@ def main() -> None:
     ap.add_argument("--brute-force", action="store_true", help="disable the exact wave culling")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-moving-camera", action="store_true", help="skip the moving-camera and AA lines (counter runs)")
+    ap.add_argument("--no-moving-camera", action="store_true",
+                    help="skip the moving-camera, AA and one-frame latency lines (counter runs)")
     ap.add_argument("--split", choices=("bands", "blocks"), default="bands",
                     help="N > 1: interleaved 4-row bands (balanced, default) or contiguous row blocks")
     ap.add_argument("--gather", choices=("scene", "coded"), default="scene",
@@ -424,9 +425,11 @@ def main() -> None:
     # the latency of one frame alone per launch
     ring1 = ring_args() if world == 1 else ring_args(0, G)
     kernel_ms = ctx.render_frames(max(args.steps // F, 1) * F, width, H, timed=True, **ring1)
-    lat_args = dict(ring1)
-    lat_args["ring"] = capi.frame_ring(1, alloc_rows, width, 1)
-    latency_ms = ctx.render_frames(max(min(args.steps, 64), 2), width, H, timed=True, **lat_args)
+    latency_ms = None
+    if not args.no_moving_camera:  # (counter runs keep to the measured launches)
+        lat_args = dict(ring1)
+        lat_args["ring"] = capi.frame_ring(1, alloc_rows, width, 1)
+        latency_ms = ctx.render_frames(max(min(args.steps, 64), 2), width, H, timed=True, **lat_args)
     rank_kernel_ms = [kernel_ms]
     gather_ms = None
     if world > 1:
@@ -498,7 +501,7 @@ def main() -> None:
             },
             "frame_ms": round(ms_per_step, 6),
             "render_kernel_ms": round(kernel_ms, 6),
-            "frame_latency_ms": round(latency_ms, 6),
+            "frame_latency_ms": None if latency_ms is None else round(latency_ms, 6),
             "material_graph_s": round(t_mat, 4),
             "scene_setup_ms": round(t_setup * 1e3, 3),
             "gather": ({"kind": f"{args.gather}, every frame, batches of {G} overlapped with rendering",

@@ -36,6 +36,7 @@ RENDER_DENSE_DETAIL = 2
 RENDER_NO_DENSE_DETAIL = 4
 RENDER_SEPARATE_FILL = 8
 RENDER_NO_SEPARATE_FILL = 16
+RENDER_SHARED_DETAIL = 32
 
 GATHER_DEFAULT = 0
 GATHER_SCENE_CAMERA = 1

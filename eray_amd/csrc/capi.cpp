@@ -907,7 +907,7 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
         return set_error(ctx, ERAY_E_UNSUPPORTED, "bounces = %u: at most %u reflection levels", rp->bounces,
                          kMaxBounces);
     const uint32_t known_flags = ERAY_RENDER_BRUTE_FORCE | ERAY_RENDER_DENSE_DETAIL | ERAY_RENDER_NO_DENSE_DETAIL |
-                                 ERAY_RENDER_SEPARATE_FILL | ERAY_RENDER_NO_SEPARATE_FILL;
+                                 ERAY_RENDER_SEPARATE_FILL | ERAY_RENDER_NO_SEPARATE_FILL | ERAY_RENDER_SHARED_DETAIL;
     if (rp->flags & ~known_flags) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "unknown render flags 0x%x", rp->flags);
     const bool general = rp->anti_aliasing > 0 || bounces > 0;
     uint32_t W, H;
@@ -1007,9 +1007,10 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
         }
         return ERAY_OK;
     }
-    if (binned_objects(ctx)) {  // the detail sub-block list of the setup
+    if (binned_objects(ctx)) {  // the detail sub-block list of the setup (ordered: heavy ones first)
         p.detail_list = ctx->bins.dlist;
         p.detail_occ = ctx->bins.docc;
+        p.detail_heavy = ctx->bins.dcount;
     }
     if (known) {  // args mode
         const CamState& h = *ctx->h_state;
@@ -1357,8 +1358,10 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
         }
         return ERAY_OK;
     }
-    // device-camera mode: every frame reads its setup's CamState
+    // device-camera mode: every frame reads its setup's CamState; the per-frame detail lists are
+    // appended unordered (no heavy count)
     p.cam_state = ctx->d_state;
+    p.detail_heavy = nullptr;
     p.nrect = 0;
     std::memset(p.rects, 0, sizeof p.rects);
     // the cameras: staged in pinned memory, copied to the device once per call; each graph chunk

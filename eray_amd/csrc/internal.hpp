@@ -85,6 +85,8 @@ constexpr uint32_t kBinSortMax = 256;
 constexpr int kMaxRects = 8;
 // Deepest reflection recursion the general tracer keeps frames for (Engine::bounces).
 constexpr uint32_t kMaxBounces = 16;
+// Frames one launch may render (eray_frame_ring::frames_per_launch <= slots <= 64).
+constexpr uint32_t kMaxFramesPerLaunch = 64;
 
 struct ObjGeom {  // what the triangle scans need of an object, 80 B
     uint32_t tri_begin, tri_count;
@@ -176,6 +178,9 @@ struct FrameParams {
     // detail rectangles enumerate the sub-blocks.
     const uint32_t* detail_list;
     const uint8_t* detail_occ;
+    // the ordered detail list's heavy sub-blocks (its first detail_heavy[0] entries: a bin of more
+    // than one 64-entry chunk), or null (an unordered list: every sub-block treated as heavy)
+    const uint32_t* detail_heavy;
     uint32_t detail_wgs;  // most workgroups of the frame kernel's grid doing detail work (0: all)
     uint32_t fill_first;  // the fill workgroups take the grid's first block indices (dispatched first)
     uint32_t separate_fill;  // the frame kernel does detail work only; fill_kernel writes the background
@@ -305,7 +310,8 @@ hipError_t launch_camera_setup_batch(const SetupParams& sp, uint32_t ncam, hipSt
 // Writes `cam` into the device camera slot (kernel arguments: no host staging buffer to race).
 hipError_t launch_set_camera(const CamDev& cam, CamDev* slot, hipStream_t s);
 // Launch overrides of eray_render_params::flags (eray_hip.h ERAY_RENDER_*) the frame launcher reads.
-constexpr uint32_t kLaunchDense = 2u, kLaunchNoDense = 4u, kLaunchSeparateFill = 8u, kLaunchNoSeparateFill = 16u;
+constexpr uint32_t kLaunchDense = 2u, kLaunchNoDense = 4u, kLaunchSeparateFill = 8u, kLaunchNoSeparateFill = 16u,
+                   kLaunchSharedDetail = 32u;
 // Per-context launch resources: the separate fill kernel's stream and its fork / join events.
 struct LaunchCtx {
     hipStream_t side;

@@ -368,6 +368,10 @@ constexpr int kUndecided = 0, kSearching = 1, kDone = 2;
 // Candidate triangles tested together per step (independent, branch-free tests: their long
 // dependent chains, division included, overlap).
 constexpr int kBatch = 4;
+#ifndef ERAY_LARGE_TEST_BATCH
+#define ERAY_LARGE_TEST_BATCH 1
+#endif
+constexpr int kLargeTestBatch = ERAY_LARGE_TEST_BATCH;
 
 // Tests the next kB candidates of `mask` (kB <= its population) in index order.
 template <int kB, typename Face, typename Hot>
@@ -402,15 +406,15 @@ __device__ __forceinline__ void test_step(unsigned long long& mask, Face&& face,
 // Tests the candidates of `mask` in index order, up to kBatch at a time: bit i stands for face
 // face(i) (relative to the object) whose record is hot(i).  Returns false once no lane is
 // searching.
-template <typename Face, typename Hot>
+template <int kB = kBatch, typename Face, typename Hot>
 __device__ __forceinline__ bool test_candidates(unsigned long long mask, Face&& face, Hot&& hot, int& st,
                                                 const f3& o, const f3& d, int& found, float& hu, float& hv,
                                                 float& ht) {
     while (mask) {
         const int n = __popcll(mask);
-        if (n >= kBatch)
-            test_step<kBatch>(mask, face, hot, st, o, d, found, hu, hv, ht);
-        else if (n >= 2)
+        if (kB >= 4 && n >= 4)
+            test_step<4>(mask, face, hot, st, o, d, found, hu, hv, ht);
+        else if (kB >= 2 && n >= 2)
             test_step<2>(mask, face, hot, st, o, d, found, hu, hv, ht);
         else
             test_step<1>(mask, face, hot, st, o, d, found, hu, hv, ht);
@@ -424,7 +428,7 @@ __device__ __forceinline__ bool test_candidates(unsigned long long mask, Face&& 
 // resolved by activate(), which must generate its direction (into `d`) and return the
 // bounding-box verdict (object.rs:59-61).  `found` receives the face index relative to
 // `begin`, or stays -1.  kLds: every thread of the workgroup must call it.
-template <bool kCull, bool kLds, bool kPlane = false, typename Scene, typename Activate>
+template <bool kCull, bool kLds, bool kPlane = false, int kB = kBatch, typename Scene, typename Activate>
 __device__ void first_hit(const FrameParams& p, const Scene& sc, uint32_t begin, uint32_t count, int& st,
                           const f3& o, const f3& d, const Bundle& bd, TriHot* s_hot, TriCull* s_cull,
                           Activate&& activate, int& found, float& hu, float& hv, float& ht) {
@@ -457,7 +461,7 @@ __device__ void first_hit(const FrameParams& p, const Scene& sc, uint32_t begin,
             if (!resolve()) break;
             auto face = [&](uint32_t i) { return base + i; };
             auto hot = [&](uint32_t i) { return sc.hot(begin + base + i); };
-            if (!test_candidates(mask, face, hot, st, o, d, found, hu, hv, ht)) return;
+            if (!test_candidates<kB>(mask, face, hot, st, o, d, found, hu, hv, ht)) return;
         }
         return;
     }
@@ -483,7 +487,7 @@ __device__ void first_hit(const FrameParams& p, const Scene& sc, uint32_t begin,
             if (!resolve()) break;
             auto face = [&](uint32_t i) { return base + c + i; };
             auto hot = [&](uint32_t i) { return s_hot[c + i]; };
-            if (!test_candidates(mask, face, hot, st, o, d, found, hu, hv, ht)) break;
+            if (!test_candidates<kB>(mask, face, hot, st, o, d, found, hu, hv, ht)) break;
         }
     }
     __syncthreads();  // the tiles' LDS is reused (aliased by the binned search)
@@ -539,6 +543,7 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
         if (st == kUndecided) st = a ? kSearching : kDone;
     }
     if (!__any(st == kSearching)) hi = lo;  // nothing to search in this sub-block
+    ERAY_TRACE_WAVE0(8);
     L.dir[0][lane] = d.x;
     L.dir[1][lane] = d.y;
     L.dir[2][lane] = d.z;
@@ -548,6 +553,7 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
         s_range[2 * wave + 1] = hi;
     }
     __syncthreads();
+    ERAY_TRACE_WAVE0(9);
     uint32_t chunks[kWaves], total = 0;
 #pragma unroll
     for (uint32_t w = 0; w < kWaves; ++w) {
@@ -642,7 +648,9 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
         __builtin_amdgcn_wave_barrier();  // L.cand / L.key / L.pairs are rewritten by the next chunk
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    ERAY_TRACE_WAVE0(10);
     __syncthreads();  // every chunk of every sub-block is done
+    ERAY_TRACE_WAVE0(11);
     const uint32_t mine = L.best[lane];
     if (st == kSearching && mine != 0xffffffffu) {
         float u, v, t;
@@ -658,7 +666,115 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
         ht = t;
         st = kDone;
     }
+    ERAY_TRACE_WAVE0(12);
     __syncthreads();  // the LDS is reused by the next object / sub-block
+}
+
+// Faces of an object the per-wave binned search takes (its keys pack face << 6 | slot).
+constexpr uint32_t kWaveBinMaxTris = (1u << 26) - 1u;
+
+// Primary-ray first hit of a binned object by ONE wave over its own sub-block's bin, with no
+// workgroup barrier (the light sub-blocks of a frame's ordered detail list: their bins hold at
+// most one 64-entry chunk, so sharing chunks across the workgroup's waves, as first_hit_binned
+// does, buys nothing and its barriers tie four sub-blocks' latency chains together).  The same
+// (face, pixel) pair tests; each pixel keeps the smallest key face << 6 | slot of a hitting pair
+// (LDS atomicMin), so the smallest hitting face index wins (object.rs:63-78) and its record is
+// still in the wave's LDS: the winner's u, v, t are recomputed from there after each chunk,
+// not re-read from memory.
+template <typename Activate>
+__device__ void first_hit_binned_wave(const ObjGeom& ob, uint32_t bin, int& st, const f3& o, const f3& d,
+                                      Activate&& activate, int& found, float& hu, float& hv, float& ht, char* s_bins) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    BinLds& L = *reinterpret_cast<BinLds*>(s_bins + wave * kBinLdsBytes);
+    const uint32_t lo = load_const(ob.bin_start, bin), hi = load_const(ob.bin_start, bin + 1);
+    if (lo == hi) return;
+    if (__any(st == kUndecided)) {  // every pixel's ray and bbox verdict, up front
+        const bool a = activate();
+        if (st == kUndecided) st = a ? kSearching : kDone;
+    }
+    if (!__any(st == kSearching)) return;
+    L.dir[0][lane] = d.x;
+    L.dir[1][lane] = d.y;
+    L.dir[2][lane] = d.z;
+    uint32_t best = st == kSearching ? 0xffffffffu : 0u;  // this lane's pixel: its winning key so far
+    L.best[lane] = best;
+    for (uint32_t base = lo; base < hi; base += 64) {
+        const uint32_t j = base + lane;
+        uint32_t fj = 0xffffffffu;
+        unsigned long long pm = 0;
+        if (j < hi) {
+            fj = ob.bin_tri[j];
+            pm = ob.bin_mask[j];
+            L.cand[lane] = ob.bin_hot[j];
+        }
+        uint32_t cmin = fj;  // the chunk's smallest face
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) cmin = min(cmin, (uint32_t)__shfl_xor((int)cmin, off));
+        const unsigned long long live = __ballot((best >> 6) > cmin);  // pixels this chunk can still improve
+        if (!live) continue;
+        const unsigned long long pix = pm & live;
+        const uint32_t cnt = (uint32_t)__popcll(pix);
+        const uint32_t key = (fj << 6) | lane;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // L.cand / L.dir / L.best visible to the wave
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        unsigned long long wide = __ballot(cnt > kWide);
+        while (wide) {  // wide candidates: the whole wave tests them, each lane its own pixel
+            const uint32_t sl = (uint32_t)(__ffsll(wide) - 1);
+            wide &= wide - 1;
+            const unsigned long long ps =
+                ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pix >> 32), (int)sl) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pix, (int)sl);
+            const uint32_t kc = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)sl);
+            if (((ps >> lane) & 1ull) && kc < L.best[lane]) {
+                float u, v, t;
+                if (exact_test(L.cand[sl], o, d, u, v, t)) atomicMin(&L.best[lane], kc);
+            }
+        }
+        // narrow candidates: (candidate, pixel) pairs compacted in LDS, one test per lane
+        const uint32_t ncnt = cnt > kWide ? 0u : cnt;
+        uint32_t incl = ncnt;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off);
+            if ((int)lane >= off) incl += y;
+        }
+        const uint32_t npairs = __shfl(incl, 63);
+        uint32_t at = incl - ncnt;
+        unsigned long long np = ncnt ? pix : 0ull;
+        while (np) {
+            const uint32_t bpos = (uint32_t)(__ffsll(np) - 1);
+            np &= np - 1;
+            L.pairs[at++] = (uint16_t)((lane << 6) | bpos);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t q = 0; q < npairs; q += 64) {
+            const bool in = q + lane < npairs;
+            const uint32_t pr = in ? L.pairs[q + lane] : 0u;
+            const uint32_t sl = pr >> 6, px = pr & 63;
+            const uint32_t kc = (uint32_t)__shfl((int)key, (int)sl);  // the pair's key, from the lane that loaded it
+            if (in && kc < L.best[px]) {  // a pixel already hit by an earlier face needs no test
+                float u, v, t;
+                const f3 dd = mk3(L.dir[0][px], L.dir[1][px], L.dir[2][px]);
+                if (exact_test(L.cand[sl], o, dd, u, v, t)) atomicMin(&L.best[px], kc);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // every pair of the chunk tested
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t nb = L.best[lane];
+        if (nb != best) {  // improved by this chunk: the winner's record is still L.cand[slot]
+            best = nb;
+            exact_test(L.cand[nb & 63u], o, d, hu, hv, ht);
+            found = (int)(nb >> 6);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // L.cand / L.pairs are rewritten by the next chunk
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (st == kSearching && found >= 0) st = kDone;
 }
 
 __device__ const float g_texel_dummy[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -832,8 +948,14 @@ template <bool kCull, bool kLdsTiles, int kMat, typename Scene>
 __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut& fo, const CamDev& cam, const RowMap& rm,
                                            const Scene& sc, uint32_t wx0, uint32_t py0,
                                            bool active, TriHot* s_hot, TriCull* s_cull, char* s_bins, float4* s_rgb,
-                                           uint32_t* s_ppm, bool aligned, const f3* given_d = nullptr) {
+                                           uint32_t* s_ppm, bool aligned, const f3* given_d = nullptr, bool coop = true) {
+    // coop (workgroup-uniform): the workgroup's four sub-blocks share their large objects' work —
+    // binned chunks dealt over the waves, shadow rays through shared LDS tiles — with barriers;
+    // otherwise (light sub-blocks) every wave searches its own bins and shadow rays alone
     constexpr bool kSpecPow = (kMat & kMatSpecPow) != 0, kExample = (kMat & kMatExample) != 0;
+    // candidates tested together by the per-wave scans (small objects, shadow rays): four for ILP,
+    // one in the large-mesh builds, whose registers bound their resident waves
+    constexpr int kTestB = kLdsTiles ? kLargeTestBatch : kBatch;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const f3 C = mk3(cam.cx, cam.cy, cam.cz);
     const uint32_t px = wx0 + (lane % kSubW), ly = lane / kSubW;
@@ -853,9 +975,10 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
     for (uint32_t oi = 0; oi < p.nobj; ++oi) {
         const ObjGeom ob = sc.geom(oi);  // uniform
         const bool direct = !kLdsTiles || ob.tri_count <= kDirectMax;
+        const bool wave_bins = kCull && !direct && !coop && ob.bin_start && ob.tri_count <= kWaveBinMaxTris;
         // outside the object's pixel rectangle no primary ray can hit it (only where skipping
-        // keeps the workgroup's barriers uniform)
-        if (kCull && direct && !rect_meets(ob, rm, wx0, py0)) continue;
+        // keeps the workgroup's barriers uniform: without coop nothing here has a barrier)
+        if (kCull && (direct || !coop) && !rect_meets(ob, rm, wx0, py0)) continue;
         auto activate = [&]() {
             if (!ray_ready) {
                 uint32_t pxo = px, yo = y;  // opaque: keep ray generation on this path
@@ -869,13 +992,19 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
         int st = valid ? kUndecided : kDone, f = -1;
         float u, v, t;
         if (direct) {
-            first_hit<kCull, false>(p, sc, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull, activate, f, u,
+            first_hit<kCull, false, false, kTestB>(p, sc, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull, activate, f, u,
                                     v, t);
-        } else if (kCull && ob.bin_start) {  // the workgroup's four sub-blocks together
+        } else if (wave_bins) {  // this wave's own bin, no barrier
+            const uint32_t bin = ((cam_row(rm, py0) + kBinH - p.bin_phase) / kBinH) * p.bins_x + wx0 / kBinW;
+            first_hit_binned_wave(ob, bin, st, C, d, activate, f, u, v, t, s_bins);
+        } else if (kCull && ob.bin_start && coop) {  // the workgroup's four sub-blocks together
             const uint32_t bin = ((cam_row(rm, py0) + kBinH - p.bin_phase) / kBinH) * p.bins_x + wx0 / kBinW;
             first_hit_binned(p, ob, bin, st, C, d, activate, f, u, v, t, s_bins);
+        } else if (!coop) {  // no bins (or too many faces for the wave's keys): this wave scans alone
+            first_hit<kCull, false, false, kTestB>(p, sc, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull,
+                                                   activate, f, u, v, t);
         } else {
-            first_hit<kCull, kLdsTiles>(p, sc, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull, activate,
+            first_hit<kCull, kLdsTiles, false, kTestB>(p, sc, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull, activate,
                                         f, u, v, t);
         }
         if (f >= 0) {
@@ -963,6 +1092,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
             any = true;
         }
     };
+    ERAY_TRACE_WAVE0(13);
     const HitBox hb = hit_box(have, P, N);  // (wave-uniform; shadow-ray face bounds)
     // Point lights first (engine.rs:274-279), 32 at a time: every light's shadow ray, then the
     // shading of the lights that reach the hit, in list order.  The texture loads above are
@@ -972,7 +1102,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
         uint32_t lit = 0;  // bit li - li0: point light li reaches the lane's hit
         for (uint32_t li = li0; li < li1; ++li) {
             const LightDesc L = sc.light(li);
-            if (L.variant == 1 || (!kLdsTiles && !__any(have))) continue;  // (LDS tiles: barriers)
+            if (L.variant == 1 || (!(kLdsTiles && coop) && !__any(have))) continue;  // (LDS tiles: barriers)
             const f3 Lp = mk3(L.pos[0], L.pos[1], L.pos[2]);
             // reaches_light(Ray::new(P + N * 0.1, Lp - P)) (engine.rs:280-286, 218-228)
             f3 S = mk3(0.0f, 0.0f, 0.0f);
@@ -1012,13 +1142,19 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
                         if (!__any(st == kSearching)) break;
                         auto face = [&](uint32_t i) { return base + i; };
                         auto hot = [&](uint32_t i) { return sc.hot(ob.tri_begin + base + i); };
-                        if (!test_candidates(mask, face, hot, st, S, sd, f, u, v, t)) break;
+                        if (!test_candidates<kTestB>(mask, face, hot, st, S, sd, f, u, v, t)) break;
                     }
+                } else if (!coop) {  // this wave alone (no barrier): faces its searching lanes may hit
+                    shadow_ray();
+                    int st = (have && !decided && bbox_hit(ob, S, sd)) ? kSearching : kDone;
+                    auto never = []() { return false; };
+                    first_hit<false, false, true, kTestB>(p, sc, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot, s_cull,
+                                                  never, f, u, v, t);
                 } else {
                     shadow_ray();
                     int st = (have && !decided && bbox_hit(ob, S, sd)) ? kSearching : kDone;
                     auto never = []() { return false; };
-                    first_hit<false, kLdsTiles>(p, sc, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot, s_cull,
+                    first_hit<false, kLdsTiles, false, kTestB>(p, sc, ob.tri_begin, ob.tri_count, st, S, sd, bd, s_hot, s_cull,
                                                 never, f, u, v, t);
                 }
                 if (f >= 0) {
@@ -1029,6 +1165,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
             }
             if (have && reached) lit |= 1u << (li - li0);
         }
+        ERAY_TRACE_WAVE0(14);
         if (!__any(lit != 0)) continue;
         material();
         for (uint32_t li = li0; li < li1; ++li) {
@@ -1208,7 +1345,13 @@ __device__ __forceinline__ void fill_frames(const FrameParams& p, uint32_t q, ui
 // issues a VALU instruction every 4 cycles, the SIMD every 2); below one round the spills only
 // lengthen each wave's chain.
 template <bool kCull, bool kLdsTiles, int kMat, bool kLdsScene, bool kDense = false, bool kDev = false>
-__global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && !kDense) ? 1 : 3)  // 3 workgroups per CU where that fits
+#ifndef ERAY_SNAKE_DETAIL
+#define ERAY_SNAKE_DETAIL 1
+#endif
+#ifndef ERAY_DENSE_WGS
+#define ERAY_DENSE_WGS 3
+#endif
+__global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && !kDense) ? 1 : (kDense ? ERAY_DENSE_WGS : 3))  // 3 workgroups per CU where that fits
     frame_kernel(const ObjectDesc* h_objects, const LightDesc* h_lights, const TriCull* h_cull, const TriHot* h_tris,
                  const TriShade* h_shade, uint32_t h_counts, uint32_t h_total_tris, uint32_t h_total_sub,
                  uint32_t h_roles, uint32_t h_band, FrameParams p) {
@@ -1263,6 +1406,11 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     ERAY_TRACE_POINT(0);
     // ---- detail sub-blocks -------------------------------------------------------------------
     if (bid < nd) {
+        // the ordered detail list's heavy count (no count: every iteration shares its work)
+        const uint32_t heavy = (kLdsTiles && p.detail_heavy && !(p.launch_flags & kLaunchSharedDetail))
+                                   ? load_const(p.detail_heavy, 0) : 0xffffffffu;
+        // snake order for the ordered (heavy-first) lists of binned meshes
+        constexpr bool kSnake = kLdsTiles && ERAY_SNAKE_DETAIL;
         const RowMap rm{p.row0, h_band & 31u, h_band >> 5};
         const uint32_t nobj = h_counts & 0xffffu;
         // virtual detail roles v (more than nd only when nd < F): frame v % F, its (v / F)-th
@@ -1310,14 +1458,26 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
                 asm volatile("" : "+v"(d0.x), "+v"(d0.y), "+v"(d0.z));  // here, not after the barrier
             };
             auto detail = [&](const auto& sc) {
-                for (uint32_t c = c0; c < total; c += nk * nwaves) {  // workgroup-uniform
-                    const uint32_t j = c + wave;
+                // Rounds of nk * 4 sub-blocks, dealt in snake order: in odd rounds the last
+                // workgroup takes the first sub-blocks, so the waves whose first sub-block came
+                // from the ordered list's heavy head (the longest chains) take the light tail
+                // of the second round.  (A device-wide atomic work counter instead measured
+                // 2.5x slower at 3840x2160 / 70k: one hot address under the frame's write stream.)
+                const uint32_t round = nk * nwaves;
+                for (uint32_t r = 0;; ++r) {  // workgroup-uniform
+                    const bool odd = (r & 1u) && kSnake;
+                    // the workgroup's first sub-block of round r (odd rounds reversed)
+                    const uint32_t first = r * round + (odd ? round - nwaves - c0 : c0);
+                    if (first >= total) break;
+                    const uint32_t j = odd ? first + (nwaves - 1 - wave) : first + wave;
                     const bool active = j < total;
                     int32_t sx = sx0, sy = sy0;
-                    if (c != c0 && active) locate(j, sx, sy);
+                    if (r != 0 && active) locate(j, sx, sy);
+                    // the ordered detail list's heavy sub-blocks (bins of several chunks) come
+                    // first: an iteration meeting one shares the work across the workgroup
                     render_sub<kCull, kLdsTiles, kMat>(p, fo, cam, rm, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH,
                                                        active, s_hot, s_cull, s_bins, s_rgb, s_ppm, aligned,
-                                                       (kGivenRay && c == c0) ? &d0 : nullptr);
+                                                       (kGivenRay && r == 0) ? &d0 : nullptr, first < heavy);
                 }
             };
             if constexpr (kLdsScene) {
@@ -1437,7 +1597,10 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
                                           : 0u;
     };
     FrameParams q = p;
-    q.detail_wgs = detail_wgs(2.0f);
+#ifndef ERAY_DETAIL_SHARE
+#define ERAY_DETAIL_SHARE 2.0f
+#endif
+    q.detail_wgs = detail_wgs(L && D ? ERAY_DETAIL_SHARE : 2.0f);
     q.fill_first = 0;
     q.detail_wgs_alt = 0;
     if (!L) {
@@ -1449,6 +1612,9 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
         }
     }
     if (L && !D) q.fill_first = 1;  // the 2-per-CU large-mesh build (C3): 13.0 -> 12.7-12.9 us
+#ifdef ERAY_DENSE_FILL_FIRST
+    if (L && D) q.fill_first = 1;
+#endif
     q.separate_fill = 0;
     if constexpr (D) {
         // Separate fill: the dense build does detail work only, at most 2 workgroups per CU, and

@@ -5,9 +5,18 @@ and the PPM body rows are gathered to rank 0.  The PPM body lists camera rows to
 (image.rs:59-72: y = H-1 ... 0), so giving rank r the r-th block of FILE rows makes the gather a
 plain concatenation in rank order: rank r owns camera rows [H - (r+1)*rows, H - r*rows), and the
 library's fused PPM output of those rows is already in file order (eray_render_params.out_ppm).
-No data-path collective other than that gather: on the GPUs it is the library's own C-ABI gather
-(eray_gather_rows, one RCCL ncclGather over xGMI; RowGather below — torch.distributed only carries
-the communicator's id from rank 0 to the others), on CPU tests a gloo gather of the same blocks.
+No data-path collective other than that gather.  On the GPUs it is the library's own C-ABI gather
+over an RCCL communicator (RowGather below; torch.distributed only carries the communicator's id
+from rank 0 to the others):
+  * eray_gather_rows, contiguous blocks: one ncclGather of the u8 rows to rank 0;
+  * eray_gather_rows, interleaved bands (the default split): a coded transport — each rank encodes
+    its rows (a uniform 64-pixel segment as one word), the packed counts are all-gathered and the
+    host synchronises the stream once (point-to-point sizes must be known to post them), then
+    grouped ncclSend / ncclRecv into rank 0 and one decode kernel — so this call blocks the host;
+  * eray_gather_frames with ERAY_GATHER_SCENE_CAMERA (the bench's per-frame assembly): only the
+    objects' pixel rectangles travel, with sizes fixed per camera (one exchange, one host
+    synchronisation per camera setup), so batches of frames are gathered with no host round trip.
+On CPU tests a gloo gather of the same blocks (gather_ppm_rows).
 """
 from __future__ import annotations
 

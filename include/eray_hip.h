@@ -264,6 +264,9 @@ typedef struct eray_render_params {
 #define ERAY_RENDER_NO_DENSE_DETAIL 4u   /* large meshes: the 2-workgroups-per-CU detail build      */
 #define ERAY_RENDER_SEPARATE_FILL 8u     /* dense build: background fill in a second, parallel kernel */
 #define ERAY_RENDER_NO_SEPARATE_FILL 16u /* dense build: background fill inside the frame kernel     */
+#define ERAY_RENDER_SHARED_DETAIL 32u    /* binned meshes: every detail sub-block's search shared by its
+                                            workgroup (default: only the heavy ones; the light ones
+                                            search their own bins without workgroup barriers)     */
 
 int eray_render(eray_ctx* ctx, const eray_render_params* params);
 /* Renders `frames` frames back to back with the same parameters (a serving / animation loop

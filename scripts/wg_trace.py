@@ -26,14 +26,14 @@ lib.eray_debug_read_trace.argtypes = [C.c_void_p, C.c_size_t]
 kw = dict(out_rgb=rgb.ptr, out_ppm=ppm.ptr)
 ctx.render_frames(50, W, H, **kw)
 ctx.synchronize()
-n = 8192 * 8
+n = 8192 * 16
 for rep in range(3):
     assert lib.eray_debug_clear_trace() == 0
     ctx.render_frames(1, W, H, **kw)
     ctx.synchronize()
     buf = (C.c_uint64 * n)()
     assert lib.eray_debug_read_trace(buf, n) == 0
-    t = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
+    t = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 16).astype(np.int64)
     used = t[:, 0] > 0
     t = t[used]
     t0 = t[:, 0].min()
@@ -56,6 +56,16 @@ for rep in range(3):
               f"(p90 {np.percentile(ph[:, 2] - ph[:, 1], 90):.2f}), outputs p50 {np.median(ph[:, 3] - ph[:, 2]):.2f}, "
               f"to workgroup end p50 {np.median(t[det][ok, 1] / 100.0 - ph[:, 3]):.2f}; first start p50 "
               f"{np.median(us(t[det][ok, 4])):.2f}")
+        P = t[det][ok]
+        names = [(4, 8, "range+rays"), (8, 9, "barrier1"), (9, 10, "chunks"), (10, 11, "barrier2"),
+                 (11, 12, "re-test"), (12, 5, "to object-loop end"), (5, 13, "hit records"), (13, 14, "shadow"),
+                 (14, 6, "shading"), (6, 7, "outputs")]
+        parts = []
+        for a, b, nm in names:
+            m = (P[:, a] > 0) & (P[:, b] > 0)
+            if m.any():
+                parts.append(f"{nm} {np.median((P[m, b] - P[m, a]) / 100.0):.2f}")
+        print("  wave 0 phases p50 (us):", ", ".join(parts))
         hist, edges = np.histogram(us(t[det, 1]), bins=12)
         print("  detail end histogram:", " ".join(f"{e:.1f}:{h}" for e, h in zip(edges, hist)))
     if fil.any():

@@ -221,7 +221,8 @@ def test_north_star_4k_70k_full_frame_binned_equals_brute_force(gpu):
     try:
         ref = [x.copy() for x in fr.render(W, H, flags=capi.RENDER_BRUTE_FORCE)]
         assert (ref[1] >= 0).sum() > 100_000
-        for flags in (capi.RENDER_DEFAULT, capi.RENDER_NO_DENSE_DETAIL,
+        for flags in (capi.RENDER_DEFAULT, capi.RENDER_NO_DENSE_DETAIL, capi.RENDER_SHARED_DETAIL,
+                      capi.RENDER_NO_DENSE_DETAIL | capi.RENDER_SHARED_DETAIL,
                       capi.RENDER_DENSE_DETAIL | capi.RENDER_SEPARATE_FILL):
             got = fr.render(W, H, flags=flags)
             assert np.array_equal(got[1], ref[1]), f"faces, flags {flags}"
