@@ -227,6 +227,40 @@ def moving_camera(scene, args, width, height, out, ring) -> dict:
     }
 
 
+def one_shot(mesh_path: str, width: int, height: int) -> dict:
+    """main.rs's own use (main.rs:17-70): load the mesh, build and update the material, set up the
+    scene and render ONE frame to a PPM file's bytes on the host — each step timed, the first thing
+    this process does on the GPU (so code-object loading and first allocations are inside), then
+    the same steps again on a second context (the warm per-scene cost)."""
+    out = {}
+    for tag in ("cold", "warm"):
+        torch.cuda.synchronize()
+        t = [time.perf_counter()]
+        mesh = load_obj_file(mesh_path)  # Object::load_obj (object.rs:101-186)
+        t.append(time.perf_counter())
+        ctx = capi.Context(torch.cuda.current_device())
+        t.append(time.perf_counter())
+        sc = MainScene(ctx, *mesh, width, height, texture=TEXTURE, fov=frame_camera_fov(width, height))
+        ctx.synchronize()  # upload + Material::update (the material graph on the device)
+        t.append(time.perf_counter())
+        ppm = ctx.empty((height, width, 3), np.uint8)
+        ctx.render(width, height, out_ppm=ppm.ptr)  # per-camera setup + frame (Engine::render)
+        ctx.synchronize()
+        t.append(time.perf_counter())
+        body = ppm.numpy()  # PPM body to the host (save_as_ppm's bytes, image.rs:48-74)
+        t.append(time.perf_counter())
+        ppm.free()
+        sc.close()
+        ctx.close()
+        ms = [round((b - a) * 1e3, 3) for a, b in zip(t, t[1:])]
+        out[tag] = {"load_obj_ms": ms[0], "context_ms": ms[1], "upload_and_material_ms": ms[2],
+                    "setup_and_frame_ms": ms[3], "ppm_to_host_ms": ms[4], "total_ms": round((t[-1] - t[0]) * 1e3, 3)}
+        del body
+    out["note"] = ("cold: the process's first GPU work (HIP code-object load, first allocations); warm: a second "
+                   "scene on a new context in the same process")
+    return out
+
+
 AA_SAMPLES = 4
 AA_MAX_TRIANGLES = 4096  # the general tracer scans every face per ray: small scenes only
 
@@ -291,6 +325,8 @@ def main() -> None:
         dist.all_reduce(t, op=op)
         return t.item()
 
+    # main.rs's one-shot use, before anything else touches the GPU (N = 1 only)
+    oneshot = one_shot(args.mesh, args.width, args.height) if world == 1 and not args.no_moving_camera else None
     mesh = load_obj_file(args.mesh)
     ctx = capi.Context(device)
     stream = torch.cuda.Stream()  # the render stream: shared by the library and torch
@@ -508,6 +544,7 @@ def main() -> None:
                         "ms_per_frame_alone": round(gather_ms, 5)} if world > 1 else None),
             "rank_kernel_ms": [round(v, 6) for v in rank_kernel_ms],
             "moving_camera": moving,
+            "one_shot": oneshot,
             "anti_aliased": aa_line,
             **({"rehearsal": "all ranks on GPU 0, gloo collectives: not a measurement"} if rehearsal else {}),
             "hit_pixels": hits_all,

@@ -1611,10 +1611,10 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
             q.fill_first = 1;
         }
     }
-    if (L && !D) q.fill_first = 1;  // the 2-per-CU large-mesh build (C3): 13.0 -> 12.7-12.9 us
-#ifdef ERAY_DENSE_FILL_FIRST
-    if (L && D) q.fill_first = 1;
-#endif
+    // large meshes: the fill roles take the first-dispatched workgroups — the 2-per-CU build (C3):
+    // 13.0 -> 12.7-12.9 us; the dense build (3840x2160 / 70k, spill-free since round 3): 23.4 ->
+    // 22.4 us (profiles/r03/ab/)
+    if (L) q.fill_first = 1;
     q.separate_fill = 0;
     if constexpr (D) {
         // Separate fill: the dense build does detail work only, at most 2 workgroups per CU, and
