@@ -262,12 +262,11 @@ def one_shot(mesh_path: str, width: int, height: int) -> dict:
 
 
 AA_SAMPLES = 4
-AA_MAX_TRIANGLES = 4096  # the general tracer scans every face per ray: small scenes only
 
 
 def anti_aliasing_line(scene, args, width, height, out) -> dict:
     """The general tracer (trace.hip: anti-aliasing, engine.rs:59-77) on the bench's frames:
-    AA_SAMPLES jittered rays per pixel plus the centre ray, every face scanned per ray.  Device
+    AA_SAMPLES jittered rays per pixel plus the centre ray.  Device
     time per frame over graph-replayed frames; rays counted as the reference casts them."""
     frames = max(2, min(args.steps, 20))
     kw = dict(out, anti_aliasing=AA_SAMPLES, aa_seed=12345)
@@ -276,7 +275,9 @@ def anti_aliasing_line(scene, args, width, height, out) -> dict:
     rays = width * height * (AA_SAMPLES + 1)
     return {"anti_aliasing": AA_SAMPLES, "frames": frames, "frame_ms": round(ms, 6),
             "value": round(rays / (ms * 1e-3) / 1e6, 3), "unit": "Mrays/s (all AA rays)",
-            "kernel": "trace_kernel (eray_amd/csrc/trace.hip): waves no camera ray of which can reach a face skip the scan (culling records), the rest brute force per ray"}
+            "kernel": "trace_kernel (eray_amd/csrc/trace.hip): waves no camera ray of which can reach a face skip "
+                      "the scan (culling records / object rectangles); camera rays of large objects read the "
+                      "wave's screen bin (bins.hip, every pair of each face's rectangle); shadow rays every face"}
 
 
 def main() -> None:
@@ -485,8 +486,7 @@ def main() -> None:
     aa_line = None
     if world == 1 and not args.no_moving_camera:
         moving = moving_camera(scene, args, width, H, out1, capi.frame_ring(slots, alloc_rows, width, F))
-        if len(mesh[0]) <= AA_MAX_TRIANGLES:
-            aa_line = anti_aliasing_line(scene, args, width, H, out1)
+        aa_line = anti_aliasing_line(scene, args, width, H, out1)
 
     if rank == 0:
         # the workload a committed counter summary (profiles/rNN/pmc_traffic*.json) must match

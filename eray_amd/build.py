@@ -24,7 +24,7 @@ OBJ = os.path.join(PKG, "_obj")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "liberay_hip.so")
 
-SOURCES = ["render.hip", "setup.hip", "trace.hip", "bins.hip", "shaderlib.hip", "capi.cpp", "comm.cpp"]
+SOURCES = ["render.hip", "setup.hip", "trace.hip", "bins.hip", "shaderlib.hip", "capi.cpp", "comm.cpp", "objload.cpp"]
 ARCH = "gfx950"
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
             f"--offload-arch={ARCH}", "-I" + os.path.join(ROOT, "include"),

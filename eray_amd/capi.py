@@ -127,8 +127,15 @@ def frame_ring(slots: int, rows: int, width: int, frames_per_launch: int = 0) ->
 _P = C.c_void_p
 _U = C.c_uint32
 _F = C.c_float
+class ObjMesh(C.Structure):
+    _fields_ = [("positions", C.POINTER(C.c_float)), ("normals", C.POINTER(C.c_float)),
+                ("uvs", C.POINTER(C.c_float)), ("triangles", C.c_uint32)]
+
+
 SIGNATURES = {
     "eray_abi_version": (C.c_int, []),
+    "eray_obj_load": (C.c_int, [C.c_char_p, C.POINTER(ObjMesh)]),
+    "eray_obj_free": (None, [C.POINTER(ObjMesh)]),
     "eray_ctx_create": (C.c_int, [C.c_int, C.POINTER(_P)]),
     "eray_ctx_destroy": (C.c_int, [_P]),
     "eray_last_error": (C.c_char_p, [_P]),
@@ -275,6 +282,23 @@ def ppm_header(width: int, height: int) -> bytes:
     n = C.c_size_t()
     check(lib().eray_ppm_header(width, height, buf, 64, C.byref(n)))
     return buf.raw[: n.value]
+
+
+def load_obj_native(path: str):
+    """eray_obj_load (objload.cpp): Object::load_obj + build of the file at `path` as
+    (positions (T, 9), normals (T, 9), uvs (T, 6)) float32.  Raises ErayError with the status
+    (E_IO, E_PARSE, E_BUILD)."""
+    m = ObjMesh()
+    st = lib().eray_obj_load(os.fsencode(path), C.byref(m))
+    if st:
+        raise ErayError(st, last_error(None))
+    try:
+        T = m.triangles
+        out = tuple(np.ctypeslib.as_array(ptr, (T, k)).copy() if T else np.zeros((0, k), np.float32)
+                    for ptr, k in ((m.positions, 9), (m.normals, 9), (m.uvs, 6)))
+    finally:
+        lib().eray_obj_free(C.byref(m))
+    return out
 
 
 class DeviceArray:

@@ -11,6 +11,8 @@
 //
 // Each entry also carries the bin's pixels the face may cover (bin_pixels: the four culling
 // bounds solved per pixel row), so the frame kernel only tests (face, pixel) pairs that can hit.
+// The general tracer's setup (SetupParams::keep_all) masks the pixels any of whose jittered
+// anti-aliasing rays may pass instead (bin_pixels_jittered; trace.hip).
 //
 // Per camera, after camera_setup_kernel (each binned face's bin rectangle and its number of bins):
 //   exclusive scan of the rectangles' areas -> one thread per (face, bin) pair (a wave-uniform
@@ -39,7 +41,9 @@ constexpr uint32_t kPairGrid = 2048;  // workgroups of the grid-stride pair and 
 
 
 // (face, bin) pairs of the binned faces' bin rectangles (face-major, each rectangle row-major):
-// the non-empty ones appended to the entry list, counted per bin key
+// the non-empty ones appended to the entry list, counted per bin key.  kJitter: the general
+// tracer's masks (bin_pixels_jittered, SetupParams::keep_all).
+template <bool kJitter>
 __global__ void __launch_bounds__(kBinWG) bin_pairs_kernel(const TriCull* __restrict__ cull,
                                                            const int4* __restrict__ range,
                                                            const unsigned long long* __restrict__ first_local,
@@ -53,6 +57,7 @@ __global__ void __launch_bounds__(kBinWG) bin_pairs_kernel(const TriCull* __rest
                                                            unsigned long long* __restrict__ emask) {
     // face i's first pair: its setup chunk's offset + its place in the chunk's own scan
     __shared__ unsigned long long s_boff[kSetupMaxBlocks + 1];
+    __shared__ double s_poly[kJitter ? 16 * kBinWG : 1];  // clip_box's workspace
     for (uint32_t b = threadIdx.x; b <= nparts; b += kBinWG) s_boff[b] = boff[b];
     __syncthreads();
     auto first = [&](uint32_t i) { return s_boff[i / chunk] + first_local[i]; };
@@ -89,7 +94,8 @@ __global__ void __launch_bounds__(kBinWG) bin_pairs_kernel(const TriCull* __rest
             const uint32_t w = (uint32_t)(g.y - g.x + 1);
             const uint32_t c = (uint32_t)(j - first(i));
             const uint32_t tx = (uint32_t)g.x + c % w, ty = (uint32_t)g.z + c / w;
-            m = bin_pixels(cull[i], W, H, phase, tx, ty);
+            if constexpr (kJitter) m = bin_pixels_jittered(cull[i], W, H, phase, tx, ty, s_poly + threadIdx.x, kBinWG);
+            else m = bin_pixels(cull[i], W, H, phase, tx, ty);
             key = fkey[i] * nbins + ty * bins_x + tx;
         }
         const unsigned long long bal = __ballot(m != 0);
@@ -524,9 +530,9 @@ hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tile
     size_t tb = b.temp_bytes;
     if (b.T) {
         const uint32_t nparts = setup_blocks(b.T), chunk = (b.T + nparts - 1) / nparts;  // as camera_setup_kernel
-        bin_pairs_kernel<<<kPairGrid, kBinWG, 0, s>>>(sp.cull, sp.range, b.first, b.boff, nparts, chunk, sp.fkey, b.T, sp.W, sp.H,
-                                                      sp.phase, b.bins_x, b.nbins, (uint32_t)b.cap, b.n, b.count,
-                                                      b.ekey, b.eface, b.emask);
+        auto* k = sp.keep_all ? bin_pairs_kernel<true> : bin_pairs_kernel<false>;
+        k<<<kPairGrid, kBinWG, 0, s>>>(sp.cull, sp.range, b.first, b.boff, nparts, chunk, sp.fkey, b.T, sp.W, sp.H, sp.phase,
+                                       b.bins_x, b.nbins, (uint32_t)b.cap, b.n, b.count, b.ekey, b.eface, b.emask);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     tb = b.temp_bytes;

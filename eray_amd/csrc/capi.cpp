@@ -476,8 +476,11 @@ SetupParams setup_params(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint
 
 // ordered: the detail list in raster order (one-camera setups, whose list serves many frames);
 // camera paths append it in one launch instead (bins.hip detail_list_kernel)
-int enqueue_setup(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint32_t H, const RowSpan& rs, bool ordered) {
-    const SetupParams sp = setup_params(ctx, d_camera, W, H, rs);
+// keep_all: the general tracer's bins (SetupParams::keep_all)
+int enqueue_setup(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint32_t H, const RowSpan& rs, bool ordered,
+                  bool keep_all = false) {
+    SetupParams sp = setup_params(ctx, d_camera, W, H, rs);
+    sp.keep_all = keep_all ? 1u : 0u;
     HIP_TRY(ctx, launch_camera_setup(sp, ctx->stream));
     if (sp.binned) HIP_TRY(ctx, launch_bins_build(sp, ctx->bins, (W + 63) / 64, ordered, ctx->stream));
     return ERAY_OK;
@@ -512,7 +515,9 @@ void state_arrived(eray_ctx* ctx) {
 // Makes the per-camera setup of the context camera current for rows [row0, row0 + rows):
 // enqueued when the camera, the rows or the scene changed, its results copied to the host
 // asynchronously.  *known: the host has them (args-mode frames); `wait`: block until it does.
-int sync_setup(eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs, bool wait, bool* known) {
+// trace_bins: the general tracer's setup (every pair of each face's bin rectangle binned).
+int sync_setup(eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs, bool wait, bool* known,
+               bool trace_bins = false) {
     for (int attempt = 0; attempt < 3; ++attempt) {
         if (ctx->state_pending) {
             const hipError_t q = hipEventQuery(ctx->state_ev);
@@ -528,8 +533,9 @@ int sync_setup(eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs, bool wa
             return ERAY_OK;
         };
         if (int st = bins_ready()) return st;
-        std::vector<uint64_t> key(sizeof(eray_camera) / 4 + 4);
+        std::vector<uint64_t> key(sizeof(eray_camera) / 4 + 5);
         std::memcpy(key.data(), &ctx->camera, sizeof(eray_camera));
+        key[key.size() - 5] = trace_bins ? 1u : 0u;
         key[key.size() - 4] = ((uint64_t)rs.row0 << 32) | rs.band_shift;
         key[key.size() - 3] = ((uint64_t)rs.rows << 32) | rs.band_stride;
         key[key.size() - 2] = ctx->scene_gen;
@@ -541,7 +547,7 @@ int sync_setup(eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs, bool wa
                 if (int st = bins_ready()) return st;  // (a grown capacity)
             }
             HIP_TRY(ctx, launch_set_camera(cam_dev(ctx->camera), ctx->d_cam, ctx->stream));
-            if (int st = enqueue_setup(ctx, ctx->d_cam, W, H, rs, true)) return st;
+            if (int st = enqueue_setup(ctx, ctx->d_cam, W, H, rs, true, trace_bins)) return st;
             HIP_TRY(ctx, hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(CamState), hipMemcpyDeviceToHost,
                                         ctx->stream));
             // the objects' pixel rectangles of this camera (eray_gather_frames' transfer layout);
@@ -940,11 +946,11 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     if (int st = sync_scene(ctx)) return st;
     *empty = !rp->rows || !W;
     if (*empty) return ERAY_OK;
+    // the general tracer's camera rays scan the binned objects' bins (a setup of its own kind)
+    const bool trace_bins = general && !(rp->flags & ERAY_RENDER_BRUTE_FORCE) && binned_objects(ctx) > 0;
     bool known = true;
-    if (cull)
-        if (int st = sync_setup(ctx, W, H, row_span(rp),
-                                wait == SetupWait::kYes, &known))
-            return st;
+    if (cull || trace_bins)
+        if (int st = sync_setup(ctx, W, H, row_span(rp), wait == SetupWait::kYes, &known, trace_bins)) return st;
 
     FrameParams& p = *out;
     std::memset(&p, 0, sizeof p);  // padding too: the launch-plan cache compares the bytes
@@ -995,6 +1001,7 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     p.seed_hi = (uint32_t)(rp->aa_seed >> 32);
     p.trace_cull = (general && !(rp->flags & ERAY_RENDER_BRUTE_FORCE) && ctx->total_tris <= kTraceSkipTris)
                        ? ctx->d_tcull : nullptr;
+    p.trace_bins = trace_bins ? 1u : 0u;
     p.launch_flags = rp->flags & ~ERAY_RENDER_BRUTE_FORCE;
     if (!cull) {  // every pixel in detail: one rectangle, the frame (sub-block units)
         if (p.nobj) {

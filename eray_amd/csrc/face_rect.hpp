@@ -20,15 +20,17 @@ namespace gpu {
 // array a at ws[(a * 8 + k) * stride]) and is read back in one round trip per clip.  (As private
 // arrays with run-time indices the polygon lived in scratch memory, and as an LDS polygon read
 // vertex by vertex each clip was a chain of LDS round trips.)
-__device__ inline bool face_rect(const TriCull& c, uint32_t W, uint32_t H, int32_t (&r)[4], double* ws,
-                                 uint32_t stride) {
+// The bounding box [xmin, xmax] x [ymin, ymax] of the viewport points of the box [bx0, bx1] x
+// [by0, by1] where every condition of record c can pass; false when there are none.
+__device__ inline bool clip_box(const TriCull& c, double bx0, double bx1, double by0, double by1, double* ws,
+                                uint32_t stride, double& xmin, double& xmax, double& ymin, double& ymax) {
     constexpr int kMax = 8;
     const float A[4] = {c.A.x, c.A.y, c.A.z, c.A.w}, B[4] = {c.B.x, c.B.y, c.B.z, c.B.w};
     const float K[4] = {c.K.x, c.K.y, c.K.z, c.K.w}, T[4] = {c.T.x, c.T.y, c.T.z, c.T.w};
     double* qx = ws;
     double* qy = ws + kMax * stride;
-    double px[kMax] = {0.0, 1.0, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    double py[kMax] = {0.0, 0.0, 1.0, 1.0, 0.0, 0.0, 0.0, 0.0};
+    double px[kMax] = {bx0, bx1, bx1, bx0, 0.0, 0.0, 0.0, 0.0};
+    double py[kMax] = {by0, by0, by1, by1, 0.0, 0.0, 0.0, 0.0};
     int n = 4;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -69,7 +71,10 @@ __device__ inline bool face_rect(const TriCull& c, uint32_t W, uint32_t H, int32
                 py[i] = qy[i * stride];
             }
     }
-    double xmin = px[0], xmax = px[0], ymin = py[0], ymax = py[0];
+    xmin = px[0];
+    xmax = px[0];
+    ymin = py[0];
+    ymax = py[0];
 #pragma unroll
     for (int i = 1; i < kMax; ++i)
         if (i < n) {
@@ -78,6 +83,16 @@ __device__ inline bool face_rect(const TriCull& c, uint32_t W, uint32_t H, int32
             ymin = fmin(ymin, py[i]);
             ymax = fmax(ymax, py[i]);
         }
+    return true;
+}
+
+// (xa, ya): the viewport's lower corner — (0, 0) for the camera rays of the pixel corners; the
+// general tracer's jittered rays reach x' = -1/W, y' = -1/H in column and row 0 (its setup passes
+// (-2/W, -2/H) and records computed for that range, cull_record.hpp).
+__device__ inline bool face_rect(const TriCull& c, uint32_t W, uint32_t H, int32_t (&r)[4], double* ws,
+                                 uint32_t stride, double xa = 0.0, double ya = 0.0) {
+    double xmin, xmax, ymin, ymax;
+    if (!clip_box(c, xa, 1.0, ya, 1.0, ws, stride, xmin, xmax, ymin, ymax)) return false;
     r[0] = max((int32_t)floor(xmin * W) - 1, 0);
     r[1] = min((int32_t)ceil(xmax * W) + 1, (int32_t)W - 1);
     r[2] = max((int32_t)floor(ymin * H) - 1, 0);
@@ -154,6 +169,35 @@ __device__ inline unsigned long long bin_pixels(const TriCull& c, uint32_t W, ui
         apply_line(l1, yf, xl, xr);
         apply_line(l2, yf, xl, xr);
         apply_line(l3, yf, xl, xr);
+        if (xl <= xr) {
+            const uint32_t n = (uint32_t)(xr - xl + 1), s = (uint32_t)(xl - x_lo);
+            pix |= (unsigned long long)((((n >= 32 ? 0xffffffffu : ((1u << n) - 1u)) << s) & 0xffffu)) << (kBinW * r);
+        }
+    }
+    return pix;
+}
+
+// The same for the general tracer's rays (trace.hip): pixel (x, y) casts its corner ray and
+// jittered ones through viewport points x' = fl(fl(x + jx) / W), y' likewise, jx, jy in [-1, 1):
+// x' W within [x - 1, x + 1] up to e = 1e-3 + 2.4e-7 W pixels of rounding.  So pixel x of row y
+// can have a ray whose conditions all pass only if the polygon where they can pass (clip_box,
+// over the row's band [y - 1, y + 1] / H and the bin's columns widened by 1 + e) reaches x - 1 - e
+// .. x + 1 + e: the pixels from ceil(xmin W - 1 - e) to floor(xmax W + 1 + e).  `ws`: clip_box's
+// LDS workspace.
+__device__ inline unsigned long long bin_pixels_jittered(const TriCull& c, uint32_t W, uint32_t H, uint32_t phase,
+                                                         uint32_t bx, uint32_t by, double* ws, uint32_t stride) {
+    const int32_t x_lo = (int32_t)(bx * kBinW), x_hi = min((int32_t)((bx + 1) * kBinW), (int32_t)W) - 1;
+    const double e = 1e-3 + 2.4e-7 * (double)W, dW = (double)W, dH = (double)H;
+    unsigned long long pix = 0;
+    for (uint32_t r = 0; r < kBinH; ++r) {
+        const int32_t y = (int32_t)(by * kBinH + phase + r) - (int32_t)kBinH;
+        if (y < 0 || y >= (int32_t)H) continue;
+        double xmin, xmax, ymin, ymax;
+        if (!clip_box(c, ((double)x_lo - 1.0 - e) / dW, ((double)x_hi + 1.0 + e) / dW, ((double)y - 1.0) / dH - 3e-7,
+                      ((double)y + 1.0) / dH + 3e-7, ws, stride, xmin, xmax, ymin, ymax))
+            continue;
+        const double lo = ceil(xmin * dW - 1.0 - e), hi = floor(xmax * dW + 1.0 + e);
+        const int32_t xl = max(x_lo, (int32_t)fmax(lo, -1.0)), xr = min(x_hi, (int32_t)fmin(hi, 2e9));
         if (xl <= xr) {
             const uint32_t n = (uint32_t)(xr - xl + 1), s = (uint32_t)(xl - x_lo);
             pix |= (unsigned long long)((((n >= 32 ? 0xffffffffu : ((1u << n) - 1u)) << s) & 0xffffu)) << (kBinW * r);

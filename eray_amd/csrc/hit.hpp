@@ -13,6 +13,20 @@ namespace {
 
 using namespace eray::dev;
 
+// A wave-uniform record read through the constant address space: scalar loads (the data was
+// written by an earlier kernel; the scalar cache is invalidated at each kernel's start).
+template <typename T>
+__device__ __forceinline__ T load_const(const T* base, size_t i) {
+    static_assert(sizeof(T) % 4 == 0, "dword-sized records only");
+    using cu32 = const __attribute__((address_space(4))) uint32_t;
+    cu32* src = (cu32*)(base + i);
+    T out;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&out);
+#pragma unroll
+    for (size_t k = 0; k < sizeof(T) / 4; ++k) dst[k] = src[k];
+    return out;
+}
+
 // Triangle::intersects (primitives.rs:41-72) with e1/e2/n precomputed.  The conjunction is
 // evaluated det-first so culled lanes skip the division; the outcome is the same conjunction.
 __device__ __forceinline__ bool exact_test(const TriHot& r, f3 o, f3 d, float& u, float& v,
@@ -29,6 +43,25 @@ __device__ __forceinline__ bool exact_test(const TriHot& r, f3 o, f3 d, float& u
     v = -dot0(e1, dao) * invdet;
     t = dot0(ao, n) * invdet;
     return t >= 0.0f && u >= 0.0f && v >= 0.0f && (u + v) <= 1.0f;
+}
+
+// --------------------------------------------------------------------- exact test ----------
+// The same test without branches: every quantity is computed (a failed det check may divide
+// by zero; its u, v, t are then discarded) and the outcome is the same conjunction, so several
+// tests can be interleaved by the compiler.
+__device__ __forceinline__ bool exact_test_flat(const TriHot& r, f3 o, f3 d, float& u, float& v,
+                                                float& t) {
+    const f3 e1 = mk3(r.q0.x, r.q0.y, r.q0.z), e2 = mk3(r.q0.w, r.q1.x, r.q1.y);
+    const f3 n = mk3(r.q1.z, r.q1.w, r.q2.x), a = mk3(r.q2.y, r.q2.z, r.q2.w);
+    const float nd = dot0(n, d);
+    const float det = -dot0(d, n);
+    const float invdet = 1.0f / det;
+    const f3 ao = sub(o, a);
+    const f3 dao = cross(ao, d);
+    u = dot0(e2, dao) * invdet;
+    v = -dot0(e1, dao) * invdet;
+    t = dot0(ao, n) * invdet;
+    return !(nd > 0.0f) & (det >= 1e-6f) & (t >= 0.0f) & (u >= 0.0f) & (v >= 0.0f) & ((u + v) <= 1.0f);
 }
 
 // BoundingBox::intersects (object.rs:327-379), general box.

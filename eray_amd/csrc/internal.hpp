@@ -199,6 +199,9 @@ struct FrameParams {
     // trace_kernel's culling records for this camera (scenes of at most kTraceSkipTris faces;
     // null: no background skip), written by trace_cull_kernel before the frame
     TriCull* trace_cull;
+    // trace_kernel's camera rays scan the binned objects' screen bins (a setup with
+    // SetupParams::keep_all; the descriptors' bin views and rectangles), else every face
+    uint32_t trace_bins;
     // Frames in flight: one launch renders `nframes` (>= 1) independent frames, its workgroups
     // dealt round-robin over them (frame_kernel).  Frame f writes out_* + f * *_stride (bytes,
     // multiples of 16) and, with dev_slots, reads the batched per-camera setup of slot f
@@ -293,6 +296,10 @@ struct SetupParams {
     unsigned long long* area;
     uint32_t* fkey;
     uint32_t bins_x, phase;
+    // the general tracer's setup (trace.hip): culling records and rectangles over the viewport
+    // its jittered anti-aliasing rays reach, bin masks of the pixels any of whose rays may pass
+    // (face_rect.hpp bin_pixels_jittered)
+    uint32_t keep_all;
     const ObjectDesc* objs_src;  // batched setups: the scene's descriptors, copied into each slot
     // binned faces' first (face, bin) pair: the exclusive scan of `area`, as each chunk
     // workgroup's own scan (first_local) plus its chunk's offset boff[b] (kSetupMaxBlocks + 1

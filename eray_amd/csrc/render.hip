@@ -66,17 +66,6 @@ __device__ __forceinline__ T as_global_rec(const T* ptr) {  // per-lane record r
     for (size_t k = 0; k < sizeof(T) / 16; ++k) dst[k] = src[k];
     return out;
 }
-template <typename T>
-__device__ __forceinline__ T load_const(const T* base, size_t i) {
-    static_assert(sizeof(T) % 4 == 0, "dword-sized records only");
-    using cu32 = const __attribute__((address_space(4))) uint32_t;
-    cu32* src = (cu32*)(base + i);
-    T out;
-    uint32_t* dst = reinterpret_cast<uint32_t*>(&out);
-#pragma unroll
-    for (size_t k = 0; k < sizeof(T) / 4; ++k) dst[k] = src[k];
-    return out;
-}
 
 // --------------------------------------------------------------------- triangle setup ------
 // Triangle::intersects recomputes e1 = b - a, e2 = c - a, n = e1 x e2 for every test
@@ -102,25 +91,6 @@ __global__ void __launch_bounds__(256) tri_precompute_kernel(const float* __rest
     shade[i].s1 = make_float4(N[4], N[5], N[6], N[7]);
     shade[i].s2 = make_float4(N[8], U[0], U[1], U[2]);
     shade[i].s3 = make_float4(U[3], U[4], U[5], 0.0f);
-}
-
-// --------------------------------------------------------------------- exact test ----------
-// The same test without branches: every quantity is computed (a failed det check may divide
-// by zero; its u, v, t are then discarded) and the outcome is the same conjunction, so several
-// tests can be interleaved by the compiler.
-__device__ __forceinline__ bool exact_test_flat(const TriHot& r, f3 o, f3 d, float& u, float& v,
-                                                float& t) {
-    const f3 e1 = mk3(r.q0.x, r.q0.y, r.q0.z), e2 = mk3(r.q0.w, r.q1.x, r.q1.y);
-    const f3 n = mk3(r.q1.z, r.q1.w, r.q2.x), a = mk3(r.q2.y, r.q2.z, r.q2.w);
-    const float nd = dot0(n, d);
-    const float det = -dot0(d, n);
-    const float invdet = 1.0f / det;
-    const f3 ao = sub(o, a);
-    const f3 dao = cross(ao, d);
-    u = dot0(e2, dao) * invdet;
-    v = -dot0(e1, dao) * invdet;
-    t = dot0(ao, n) * invdet;
-    return !(nd > 0.0f) & (det >= 1e-6f) & (t >= 0.0f) & (u >= 0.0f) & (v >= 0.0f) & ((u + v) <= 1.0f);
 }
 
 struct Bundle {  // a wave's pixel rectangle in viewport coordinates

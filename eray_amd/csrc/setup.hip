@@ -110,11 +110,13 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp, 
         const uint32_t i = i0 + tid;
         unsigned long long ar = 0;
         if (i < hi) {
-            const TriCull c = cull_record(sp.hot[i], cam);
+            // (keep_all: the general tracer's viewport, jittered rays reach -1/W and -1/H)
+            const double xa = sp.keep_all ? -2.0 / (double)sp.W : 0.0, ya = sp.keep_all ? -2.0 / (double)sp.H : 0.0;
+            const TriCull c = cull_record(sp.hot[i], cam, xa, 1.0, ya, 1.0);
             sp.cull[i] = c;
             const uint32_t obj = object_of(sp.obj_begin, sp.nobj, i);
             int32_t r[4];
-            const bool any = face_rect(c, sp.W, sp.H, r, s_poly + tid, kSetupWG);
+            const bool any = face_rect(c, sp.W, sp.H, r, s_poly + tid, kSetupWG, xa, ya);
             if (any) {
                 uint32_t a[4];
                 rect_words(r, a);

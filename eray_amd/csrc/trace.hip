@@ -5,10 +5,11 @@
 // one primary ray per pixel at the integer pixel corner, no recursion — and its culling
 // records, pixel rectangles and screen bins all assume those rays.  Jittered anti-aliasing
 // rays and reflected rays go anywhere, so this kernel is the plain form of the same semantics:
-// one thread per pixel (a 256-thread workgroup owns a 64 x 4 pixel tile, each wave a 64-pixel
-// row segment), every ray scans every object's faces in index order (Object::intersects,
-// object.rs:58-81: bbox test, then the FIRST face whose Triangle::intersects passes), with the
-// triangle records read through L1/L2 (TriHot, 48 B).  It runs only when the caller asks for
+// one thread per pixel (a 256-thread workgroup owns a 64 x 4 pixel tile, each wave a 16 x 4
+// sub-block), every ray finds each object's FIRST face whose Triangle::intersects passes
+// (Object::intersects, object.rs:58-81: bbox test, then the faces in index order), with the
+// triangle records read through L1/L2 (TriHot, 48 B) — camera rays from the faces their wave can
+// reach (the background skip below), the others from every face.  It runs only when the caller asks for
 // anti_aliasing > 0, or for bounces > 0 on a scene with a reflection output; the reference's
 // default engine never takes it.
 //
@@ -106,35 +107,25 @@ struct Level {
     uint32_t li;  // next light of the per-light loop (engine.rs:130-192)
 };
 
-// The closest object's first hit along Ray(o, d) — strict `<` on |P - camera|² in object order
-// (engine.rs:116-126) — and its material (Triangle::intersects' P and N, primitives.rs:60-69;
-// RaycastHit's UV and Material::get, object.rs:70-74, material.rs:56-94).  False on a miss.
-__device__ bool surface(const FrameParams& p, f3 o, f3 d, Level& L, int32_t* face_out, const uint64_t* live) {
-    const f3 C = mk3(p.cx, p.cy, p.cz);
-    bool have = false;
-    float best = 0.0f, bu = 0.0f, bv = 0.0f, bt = 0.0f;
-    uint32_t bo = 0;
-    int bf = -1;
-    for (uint32_t oi = 0; oi < p.nobj; ++oi) {
-        const ObjGeom ob = p.objects[oi].g;
-        float u, v, t;
-        const int f = first_face(p.tris, ob, o, d, u, v, t, live);
-        if (f < 0) continue;
-        const float dsq = len_sq(sub(add(o, mul(d, t)), C));
-        if (!have || dsq < best) {
-            have = true;
-            best = dsq;
-            bo = oi;
-            bf = f;
-            bu = u;
-            bv = v;
-            bt = t;
-        }
-    }
-    if (!have) return false;
-    if (face_out) *face_out = bf;
-    const ObjectDesc& od = p.objects[bo];
-    const TriShade sh = p.shade[od.g.tri_begin + (uint32_t)bf];
+// A ray's closest object so far (engine.rs:116-126): the first object whose hit point is strictly
+// closer to the camera (|P - C|²) than every earlier object's replaces it.
+struct Hit {
+    float dsq, u, v, t;
+    int32_t f;    // face relative to the object's first, -1: no hit yet
+    uint32_t o;
+};
+__device__ __forceinline__ void closer(Hit& h, uint32_t oi, int f, float u, float v, float t, f3 o, f3 d, f3 C) {
+    if (f < 0) return;
+    const float dsq = len_sq(sub(add(o, mul(d, t)), C));
+    if (h.f < 0 || dsq < h.dsq) h = Hit{dsq, u, v, t, f, oi};
+}
+
+// The hit's Level: Triangle::intersects' P and N (primitives.rs:60-69), RaycastHit's UV and
+// Material::get (object.rs:70-74, material.rs:56-94).
+__device__ void fill_level(const FrameParams& p, f3 o, f3 d, const Hit& h, Level& L) {
+    const float bu = h.u, bv = h.v, bt = h.t;
+    const ObjectDesc& od = p.objects[h.o];
+    const TriShade sh = p.shade[od.g.tri_begin + (uint32_t)h.f];
     L.P = add(o, mul(d, bt));
     const f3 na = mk3(sh.s0.x, sh.s0.y, sh.s0.z), nb = mk3(sh.s0.w, sh.s1.x, sh.s1.y);
     const f3 nc = mk3(sh.s1.z, sh.s1.w, sh.s2.x);
@@ -173,7 +164,131 @@ __device__ bool surface(const FrameParams& p, f3 o, f3 d, Level& L, int32_t* fac
     if (const float* c = texel(mat.specular_power, uv0, uv1, 1)) L.sp = *c;
     if (const float* c = texel(mat.reflection, uv0, uv1, 1)) L.refl = *c;
     L.li = 0;
+}
+
+// The closest object's first hit along Ray(o, d) (engine.rs:116-126) and its Level; false on a
+// miss.  Every face of every object (reflected rays; camera rays of small scenes via `live`).
+__device__ bool surface(const FrameParams& p, f3 o, f3 d, Level& L, int32_t* face_out, const uint64_t* live) {
+    const f3 C = mk3(p.cx, p.cy, p.cz);
+    Hit h;
+    h.f = -1;
+    for (uint32_t oi = 0; oi < p.nobj; ++oi) {
+        const ObjGeom ob = p.objects[oi].g;
+        float u, v, t;
+        const int f = first_face(p.tris, ob, o, d, u, v, t, live);
+        closer(h, oi, f, u, v, t, o, d, C);
+    }
+    if (h.f < 0) return false;
+    if (face_out) *face_out = h.f;
+    fill_level(p, o, d, h, L);
     return true;
+}
+
+// Camera rays of one pixel, up to kRays at once (the corner ray and anti-aliasing rays), against
+// every object: the closest hit of each (engine.rs:116-126).  Binned objects (p.trace_bins) are
+// searched in one pass over the wave's screen bin `bin` (bins.hip, the tracer's setup) for all the
+// rays together: a camera ray of the bin's pixels — the corner ray or a jittered one, whose
+// viewport point stays inside [-1/W, 1] x [-1/H, 1] — can only hit faces whose entry marks its
+// pixel (face_rect.hpp bin_pixels_jittered), and Object::intersects' first face (object.rs:63-78)
+// is the smallest index that passes: the entries are in no particular order except in bins of 65
+// to kBinSortMax (face order), where a ray stops at its first pass.  One wave is one bin: its
+// lanes load the bin 64 entries at a time into the wave's LDS slot (one round trip per chunk),
+// then every lane reads each entry that marks some searching pixel (LDS broadcasts) and tests
+// its rays.  Every lane of the wave must call (`valid` false: a lane off the frame, no rays).
+// Other objects: first_face per ray.
+constexpr int kRays = 5;  // anti_aliasing = 4 in one pass
+struct BinChunk {         // one wave's LDS slot: a chunk of its bin's entries
+    TriHot hot[64];
+    unsigned long long mask[64];
+    uint32_t tri[64];
+};
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ void camera_hits(const FrameParams& p, f3 C, const f3 (&d)[kRays], uint32_t nr, bool valid, uint32_t bin,
+                            BinChunk& E, Hit (&h)[kRays]) {
+    const uint32_t lane = threadIdx.x & 63;  // = the pixel's bit in a bin mask (row * 16 + column)
+#pragma unroll
+    for (int r = 0; r < kRays; ++r) h[r].f = -1;
+    for (uint32_t oi = 0; oi < p.nobj; ++oi) {
+        const ObjGeom ob = load_const(&p.objects[oi].g, 0);
+        if (!ob.bin_start) {
+#pragma unroll
+            for (uint32_t r = 0; r < (uint32_t)kRays; ++r)
+                if (valid && r < nr) {
+                    float u, v, t;
+                    const int f = first_face(p.tris, ob, C, d[r], u, v, t, nullptr);
+                    closer(h[r], oi, f, u, v, t, C, d[r], C);
+                }
+            continue;
+        }
+        bool in[kRays];
+        uint32_t bf[kRays];
+        float bu[kRays], bv[kRays], bt[kRays];
+        bool any_in = false;
+#pragma unroll
+        for (int r = 0; r < kRays; ++r) {
+            in[r] = valid && (uint32_t)r < nr && bbox_hit(ob, C, d[r]);
+            bf[r] = ~0u;
+            bu[r] = bv[r] = bt[r] = 0.0f;
+            any_in |= in[r];
+        }
+        const unsigned long long act = __ballot(any_in);
+        if (act) {
+            const uint32_t lo = load_const(ob.bin_start, bin), hi = load_const(ob.bin_start, bin + 1);
+            const bool sorted = hi - lo > 64 && hi - lo <= kBinSortMax;
+            for (uint32_t base = lo; base < hi; base += 64) {
+                const uint32_t j = base + lane;
+                bool rel = false;
+                if (j < hi) {
+                    const unsigned long long m = ob.bin_mask[j];
+                    rel = (m & act) != 0;
+                    E.mask[lane] = m;
+                    E.tri[lane] = ob.bin_tri[j];
+                    E.hot[lane] = ob.bin_hot[j];
+                }
+                unsigned long long todo = __ballot(rel);
+                wave_sync();
+                while (todo) {
+                    const uint32_t k = (uint32_t)__builtin_ctzll(todo);
+                    todo &= todo - 1;
+                    const uint32_t f = E.tri[k];
+                    const bool mine = (E.mask[k] >> lane) & 1ull;
+                    const TriHot hh = E.hot[k];
+                    bool hit[kRays];
+                    float uu[kRays], vv[kRays], tt[kRays];
+#pragma unroll
+                    for (int r = 0; r < kRays; ++r) {
+                        hit[r] = false;
+                        if ((uint32_t)r < nr) {  // (wave-uniform)
+                            const bool pass = exact_test_flat(hh, C, d[r], uu[r], vv[r], tt[r]);
+                            hit[r] = mine & in[r] & (f < bf[r]) & pass;
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < kRays; ++r)
+                        if (hit[r]) {
+                            bf[r] = f;
+                            bu[r] = uu[r];
+                            bv[r] = vv[r];
+                            bt[r] = tt[r];
+                        }
+                }
+                wave_sync();  // (the next chunk rewrites the slot)
+                if (sorted) {
+                    bool searching = false;
+#pragma unroll
+                    for (int r = 0; r < kRays; ++r) searching |= in[r] && bf[r] == ~0u;
+                    if (!__any(searching)) break;
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < kRays; ++r)
+            if (bf[r] != ~0u) closer(h[r], oi, (int)bf[r], bu[r], bv[r], bt[r], C, d[r], C);
+    }
 }
 
 // Engine::reaches_light (engine.rs:218-228): the FIRST object with any hit decides.
@@ -203,33 +318,32 @@ __device__ __forceinline__ rgb shade(const Level& L, const LightDesc& Ld) {
     return cadd(diffusion, rgb{res * sf, res * sf, res * sf});
 }
 
-// Engine::cast_ray(ray, 0).sum() (engine.rs:112-216, color.rs:82-87) as a depth-first walk.
-// `miss_known`: the caller knows the ray hits nothing (trace_kernel's background skip); `live`:
-// the faces a camera ray of the wave can hit (first_face), for the first level only.
-__device__ rgb cast_ray(const FrameParams& p, f3 o, f3 d, int32_t* face_out, bool miss_known, const uint64_t* live) {
-    Level st[kMaxBounces + 1];
+// Engine::cast_ray(ray, 0).sum() (engine.rs:112-216, color.rs:82-87) as a depth-first walk from
+// the first level's hit `first`.  kBounce false: no reflection levels (bounces == 0), so the walk
+// needs no per-depth frames.
+template <bool kBounce>
+__device__ rgb walk(const FrameParams& p, const Level& first) {
+    Level st[kBounce ? kMaxBounces + 1 : 1];
+    st[0] = first;
     bool any = false;
     rgb acc{0.0f, 0.0f, 0.0f};
     auto emit = [&](rgb c, int depth) {  // c * refl[depth-1] * ... * refl[0], then the fold
-        for (int j = depth - 1; j >= 0; --j) c = cmul(c, st[j].refl);
+        if (kBounce)
+            for (int j = depth - 1; j >= 0; --j) c = cmul(c, st[j].refl);
         acc = any ? cadd(acc, c) : c;
         any = true;
     };
     const rgb miss{0.1f, 0.1f, 0.2f};  // engine.rs:211-213
-    if (miss_known || !surface(p, o, d, st[0], face_out, live)) {
-        emit(miss, 0);
-        return acc;
-    }
     int depth = 0;
     while (depth >= 0) {
-        Level& L = st[depth];
+        Level& L = st[kBounce ? depth : 0];
         if (L.li < p.nlights) {
             const LightDesc Ld = p.lights[L.li++];
             if (Ld.variant == 1) continue;  // ambient lights come after the loop
             const f3 Lp = mk3(Ld.pos[0], Ld.pos[1], Ld.pos[2]);
             const f3 S = add(L.P, mul(L.N, 0.1f));
             if (reaches_light(p, S, normalize(sub(Lp, L.P)), Lp)) emit(shade(L, Ld), depth);
-            if ((uint32_t)depth < p.bounces && L.refl != 0.0f) {  // engine.rs:181-191
+            if (kBounce && (uint32_t)depth < p.bounces && L.refl != 0.0f) {  // engine.rs:181-191
                 const f3 rd = normalize(sub(L.d, mul(mul(L.N, 2.0f), dot0(L.d, L.N))));
                 if (surface(p, S, rd, st[depth + 1], nullptr, nullptr))
                     ++depth;
@@ -250,18 +364,53 @@ __device__ rgb cast_ray(const FrameParams& p, f3 o, f3 d, int32_t* face_out, boo
     return acc;
 }
 
+// The miss colour (engine.rs:211-213): a ray that hits nothing returns vec![it].
+__device__ __forceinline__ rgb miss_color() { return rgb{0.1f, 0.1f, 0.2f}; }
+
+// Engine::cast_ray(ray, 0).sum() of one ray.  `miss_known`: the caller knows the ray hits
+// nothing (trace_kernel's background skip); `live`: the faces a camera ray of the wave can hit
+// (first_face), for the first level only.
+template <bool kBounce>
+__device__ rgb cast_ray(const FrameParams& p, f3 o, f3 d, int32_t* face_out, bool miss_known, const uint64_t* live) {
+    Level L;
+    if (miss_known || !surface(p, o, d, L, face_out, live)) return miss_color();
+    return walk<kBounce>(p, L);
+}
+
+// Element r of a per-ray array (r < kRays, run time) without a dynamically indexed private array
+// (which would live in scratch memory).
+template <typename T>
+__device__ __forceinline__ T pick(const T (&a)[kRays], uint32_t r) {
+    T out = a[0];
+#pragma unroll
+    for (uint32_t k = 1; k < (uint32_t)kRays; ++k)
+        if (r == k) out = a[k];
+    return out;
+}
+
+// Waves.  A 256-thread workgroup owns a 64 x 4 pixel block and each wave a 16 x 4 sub-block of
+// it, lane = row * 16 + column: one screen bin (bins.hip), so a binned object's camera rays read
+// the same entries in every lane.  (Interleaved bands are multiples of 4 rows: a sub-block's rows
+// are consecutive camera rows.)
+//
 // Background skip.  Every ray a wave casts from the camera — its 64 primary rays and their
-// jittered anti-aliasing rays — goes through the viewport rectangle [x0 - 1, x0 + 64] x [y - 1, y
-// + 1] / (W, H) (jitter in [-1, 1), engine.rs:62-69).  For scenes of at most kSkipTris triangles
-// trace_cull_kernel computes every triangle's culling record for this camera (cull_record.hpp, the
-// frame kernel's conservative bounds, with the viewport range widened to the jittered rays') and
-// each workgroup copies them into LDS; a wave none of whose records survives its rectangle cannot
-// hit any face with any camera ray, so every one of its rays is the reference's miss
+// jittered anti-aliasing rays — goes through the viewport rectangle [x0 - 1, x0 + 16] x [y0 - 1,
+// y0 + 4] / (W, H) (jitter in [-1, 1), engine.rs:62-69).  A wave that can show that none of those
+// rays reaches any face casts none: every one of its rays is the reference's miss
 // (engine.rs:208-213) — cast_ray's own miss path, the same float sums — and the shadow and
-// reflected rays, which start only at a hit, never exist.  The other waves keep the survivors'
-// bits (live_mask): their camera rays test only those faces, in index order.  Bit-identical to the
-// brute-force scan (ERAY_RENDER_BRUTE_FORCE turns the skip off; tests/test_gpu_trace.py compares
-// them).
+// reflected rays, which start only at a hit, never exist.
+//  * Scenes of at most kSkipTris triangles: trace_cull_kernel computes every triangle's culling
+//    record for this camera (cull_record.hpp, the frame kernel's conservative bounds, with the
+//    viewport range widened to the jittered rays') and each workgroup copies them into LDS; a wave
+//    none of whose records survives its rectangle skips, the other waves keep the survivors' bits
+//    (live_mask): their camera rays test only those faces, in index order.
+//  * Scenes with binned objects (p.trace_bins): the per-camera setup's object rectangles
+//    (face_rect.hpp unions over the viewport the jittered rays reach, [-1/W, 1] x [-1/H, 1];
+//    binned objects narrowed to their non-empty bins) hold every pixel whose corner or jittered
+//    ray can hit the object.  A wave whose sub-block meets no object's rectangle skips; in the
+//    others the binned objects' faces come from the wave's bin (first_face_binned).
+// Bit-identical to the brute-force scan (ERAY_RENDER_BRUTE_FORCE turns both off;
+// tests/test_gpu_trace.py compares them).
 constexpr uint32_t kSkipTris = kTraceSkipTris;
 
 // The records, once per frame (one workgroup; the host passes trace_cull only for scenes of at
@@ -277,48 +426,100 @@ __global__ void __launch_bounds__(256) trace_cull_kernel(FrameParams p) {
 __device__ __forceinline__ float widen_down(float v) { return v >= 0.0f ? v * (1.0f - 0x1p-20f) : v * (1.0f + 0x1p-20f); }
 __device__ __forceinline__ float widen_up(float v) { return v >= 0.0f ? v * (1.0f + 0x1p-20f) : v * (1.0f - 0x1p-20f); }
 
+template <bool kBounce>
 __global__ void __launch_bounds__(256) trace_kernel(FrameParams p) {
     __shared__ TriCull s_cull[kSkipTris];
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t px = blockIdx.x * 64 + lane;
-    const uint32_t py = blockIdx.y * 4 + (threadIdx.x >> 6);  // rank-local row
-    const uint32_t y = band_camera_row(p.row0, p.band_shift, p.band_mask, p.band_stride, py);
+    __shared__ uint64_t s_live[4][kSkipTris / 64];  // each wave's live_mask (LDS: run-time indexed)
+    __shared__ BinChunk s_chunk[4];                  // each wave's bin chunk (camera_hits)
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t x0 = blockIdx.x * 64 + wave * 16;  // the wave's sub-block: columns x0 .. x0 + 15
+    const uint32_t px = x0 + (lane & 15);
+    const uint32_t py0 = blockIdx.y * 4, py = py0 + (lane >> 4);  // rank-local rows
+    const uint32_t y0 = band_camera_row(p.row0, p.band_shift, p.band_mask, p.band_stride, py0);
+    const uint32_t y = y0 + (lane >> 4);
     bool skip = false;
-    uint64_t live_mask[kSkipTris / 64];
+    uint64_t* live_mask = s_live[wave];
     const uint64_t* live = nullptr;
     if (p.trace_cull) {  // workgroup-uniform
         if (threadIdx.x < p.total_tris) s_cull[threadIdx.x] = p.trace_cull[threadIdx.x];
         __syncthreads();
         const float rw = 1.0f / (float)p.cam_w, rh = 1.0f / (float)p.cam_h;
-        const float x0 = (float)(blockIdx.x * 64);
         // (x' <= 1, y' <= 1: the rays reach at most x = W, y = H; the bounds assume |x'|, |y'| <= 1)
-        const float xe = __builtin_fminf(x0 + 64.0f, (float)p.cam_w), ye = __builtin_fminf((float)y + 1.0f, (float)p.cam_h);
-        const float xlo = widen_down((x0 - 1.0f) * rw), xhi = widen_up(xe * rw);
-        const float ylo = widen_down(((float)y - 1.0f) * rh), yhi = widen_up(ye * rh);
+        const float xe = __builtin_fminf((float)x0 + 16.0f, (float)p.cam_w);
+        const float ye = __builtin_fminf((float)y0 + 4.0f, (float)p.cam_h);
+        const float xlo = widen_down(((float)x0 - 1.0f) * rw), xhi = widen_up(xe * rw);
+        const float ylo = widen_down(((float)y0 - 1.0f) * rh), yhi = widen_up(ye * rh);
         uint64_t any = 0;
 #pragma unroll
         for (uint32_t w = 0; w < kSkipTris / 64; ++w) {
-            const uint32_t f = w * 64 + lane;
-            live_mask[w] = __ballot(f < p.total_tris && !cull_rejects(s_cull[f], xlo, xhi, ylo, yhi));
-            any |= live_mask[w];
+            const uint64_t m = __ballot(w * 64 + lane < p.total_tris && !cull_rejects(s_cull[w * 64 + lane], xlo, xhi, ylo, yhi));
+            if (lane == 0) live_mask[w] = m;
+            any |= m;
         }
         skip = any == 0;
         live = live_mask;
     }
-    if (px >= p.cam_w || py >= p.rows) return;
+    uint32_t bin = ~0u;
+    if (p.trace_bins) {  // wave-uniform
+        bin = ((y0 + kBinH - p.bin_phase) / kBinH) * p.bins_x + x0 / kBinW;
+        bool meets = false;
+        for (uint32_t oi = 0; oi < p.nobj && !meets; ++oi) {
+            const int32_t* r = p.objects[oi].g.rect;
+            meets = r[0] <= r[1] && r[2] <= r[3] && (int32_t)x0 + 15 >= r[0] && (int32_t)x0 <= r[1] &&
+                    (int32_t)y0 + 3 >= r[2] && (int32_t)y0 <= r[3];
+        }
+        skip = !meets;
+    }
+    const bool valid = px < p.cam_w && py < p.rows;
     const f3 C = mk3(p.cx, p.cy, p.cz);
     int32_t face = -1;
-    // cast_ray_from_camera(x as f32, y as f32) (engine.rs:60, 100-109)
-    rgb avg = cast_ray(p, C, camera_ray_dir(p, (float)px / (float)p.cam_w, (float)y / (float)p.cam_h), &face, skip, live);
-    for (uint32_t s = 0; s < p.aa; ++s) {  // engine.rs:62-69
-        if (skip) {  // the jitter only moves a ray that misses anyway
-            avg = cadd(avg, cast_ray(p, C, f3{}, nullptr, true, nullptr));
-            continue;
-        }
-        const uint4 r = philox4x32_10(make_uint4(px, y, s, 0u), p.seed_lo, p.seed_hi);
+    rgb avg;
+    // ray 0: cast_ray_from_camera(x as f32, y as f32) (engine.rs:60, 100-109); ray 1 + s: the
+    // s-th anti-aliasing ray (engine.rs:62-69); the pixel sums them in that order
+    auto ray_dir = [&](uint32_t i) {
+        if (i == 0) return camera_ray_dir(p, (float)px / (float)p.cam_w, (float)y / (float)p.cam_h);
+        const uint4 r = philox4x32_10(make_uint4(px, y, i - 1, 0u), p.seed_lo, p.seed_hi);
         const float xf = ((float)px + jitter(r.x)) / (float)p.cam_w;
         const float yf = ((float)y + jitter(r.y)) / (float)p.cam_h;
-        avg = cadd(avg, cast_ray(p, C, camera_ray_dir(p, xf, yf), nullptr, false, live));
+        return camera_ray_dir(p, xf, yf);
+    };
+    if (!skip && bin != ~0u) {  // binned objects: the pixel's rays kRays at a time, one pass over the bin each
+        const uint32_t n = 1 + p.aa;
+        for (uint32_t i0 = 0; i0 < n; i0 += kRays) {  // (wave-uniform; every lane, `valid` or not)
+            const uint32_t nr = min((uint32_t)kRays, n - i0);
+            f3 d[kRays];
+#pragma unroll
+            for (uint32_t r = 0; r < (uint32_t)kRays; ++r) d[r] = r < nr ? ray_dir(i0 + r) : mk3(0.0f, 0.0f, -1.0f);
+            Hit h[kRays];
+            camera_hits(p, C, d, nr, valid, bin, s_chunk[wave], h);
+            if (!valid) continue;
+            for (uint32_t r = 0; r < nr; ++r) {
+                const Hit hr = pick(h, r);
+                rgb c = miss_color();
+                if (hr.f >= 0) {
+                    Level L;
+                    fill_level(p, C, pick(d, r), hr, L);
+                    c = walk<kBounce>(p, L);
+                }
+                if (i0 + r == 0) {
+                    avg = c;
+                    face = hr.f;
+                } else {
+                    avg = cadd(avg, c);
+                }
+            }
+        }
+        if (!valid) return;
+    } else {
+        if (!valid) return;
+        if (skip) {  // every camera ray misses (the jitter only moves a ray that misses anyway)
+            avg = miss_color();
+            for (uint32_t s = 0; s < p.aa; ++s) avg = cadd(avg, miss_color());
+        } else {
+            avg = cast_ray<kBounce>(p, C, ray_dir(0), &face, false, live);
+            for (uint32_t s = 0; s < p.aa; ++s)
+                avg = cadd(avg, cast_ray<kBounce>(p, C, ray_dir(1 + s), nullptr, false, live));
+        }
     }
     if (p.aa) {  // (average / aa as f32).clamp() (engine.rs:71-73)
         const float n = (float)p.aa;
@@ -349,7 +550,8 @@ hipError_t launch_trace(const FrameParams& p, hipStream_t s) {
         hipLaunchKernelGGL(trace_cull_kernel, dim3(1), dim3(256), 0, s, p);
     }
     const dim3 grid((p.cam_w + 63) / 64, (p.rows + 3) / 4);
-    hipLaunchKernelGGL(trace_kernel, grid, dim3(256), 0, s, p);
+    if (p.bounces) hipLaunchKernelGGL(trace_kernel<true>, grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(trace_kernel<false>, grid, dim3(256), 0, s, p);
     return hipGetLastError();
 }
 

@@ -1,5 +1,8 @@
 """Wavefront .obj reading/writing in exactly the dialect eray's loader accepts.
 
+`load_obj_file` reads files through the C-ABI loader (eray_obj_load); `load_obj` is the same
+dialect stated in Python for in-memory text, and the check the native loader is tested against.
+
 `load_obj` restates Object::load_obj + Object::build (src/lib/object.rs:101-230,
 396-421) for the Python host; every input that panics in the reference raises ObjError
 with the matching status (E_PARSE for panics, E_BUILD for build()'s Err).  The result is
@@ -125,8 +128,18 @@ def load_obj(text: str | bytes):
 
 
 def load_obj_file(path: str):
-    with open(path, "rb") as f:
-        return load_obj(f.read())
+    """The .obj file at `path` through the C-ABI loader (eray_obj_load, objload.cpp: the same
+    dialect in one native pass); its statuses as ObjError (E_PARSE, E_BUILD) or OSError (E_IO)."""
+    from . import capi
+
+    try:
+        return capi.load_obj_native(path)
+    except capi.ErayError as e:
+        if e.status in (E_PARSE, E_BUILD):
+            raise ObjError(e.status, str(e)) from None
+        if e.status == capi.E_IO:
+            raise OSError(str(e)) from None
+        raise
 
 
 def _fmt(a: np.ndarray) -> list[str]:

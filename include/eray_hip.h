@@ -378,6 +378,20 @@ int eray_pack_ppm(eray_ctx* ctx, const float* rgb, uint32_t width, uint32_t heig
 /* Writes "P6 {width} {height} 255\n" into buf; *len receives its length (buf may be NULL). */
 int eray_ppm_header(uint32_t width, uint32_t height, char* buf, size_t cap, size_t* len);
 
+/* ------------------------------------------------------------------ .obj input ---------- */
+/* Object::load_obj + Object::build (object.rs:101-230, 396-421): the .obj file at `path` in the
+ * reference's dialect, as eray_object's per-face arrays (faces copy their vertices by value).
+ * ERAY_E_IO: unreadable; ERAY_E_PARSE: an input the reference panics on; ERAY_E_BUILD: no
+ * vertices or no normals.  The arrays are malloc'd; release them with eray_obj_free. */
+typedef struct eray_obj_mesh {
+    float* positions;    /* triangles x 9 (a, b, c) */
+    float* normals;      /* triangles x 9 */
+    float* uvs;          /* triangles x 6 */
+    uint32_t triangles;
+} eray_obj_mesh;
+int eray_obj_load(const char* path, eray_obj_mesh* out);
+void eray_obj_free(eray_obj_mesh* mesh);
+
 #ifdef __cplusplus
 }
 #endif

@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 
 from eray_amd import capi, meshgen
-from eray_amd.objfile import ObjError, load_obj
+from eray_amd.objfile import ObjError, load_obj, load_obj_file
 
 GOOD = """# comment
 o Tri
@@ -84,3 +84,44 @@ def test_generated_mesh_roundtrip(oracle, tmp_path):
     p2 = tmp_path / "m2.obj"
     meshgen.generate(str(p2), 3000, 11)
     assert p2.read_text() == txt
+
+
+# ------------------------------------------------------------ the C-ABI loader (objload.cpp)
+def _native(tmp_path, txt, name="x.obj"):
+    p = tmp_path / name
+    p.write_bytes(txt.encode() if isinstance(txt, str) else txt)
+    return load_obj_file(str(p))
+
+
+def test_native_loader_agrees_on_good_files(oracle, tmp_path):
+    crlf = GOOD.replace("\n", "\r\n").replace("v 1.0 0 0", "v 1e0 -0.0 .5").replace("vt 0 0\r", "vt inf NaN\r")
+    for txt in (GOOD, crlf, GOOD.rstrip("\n"), GOOD.replace("f +3/3/1", "f 3/3/1/7")):
+        a = _native(tmp_path, txt)
+        assert same(a, load_obj(txt))
+        assert same(a, oracle.load_obj(txt))
+
+
+@pytest.mark.parametrize("name", sorted(BAD))
+def test_native_loader_rejects_what_panics(tmp_path, name):
+    with pytest.raises(ObjError) as e:
+        _native(tmp_path, BAD[name])
+    assert e.value.status == capi.E_PARSE
+
+
+def test_native_loader_build_and_io_errors(tmp_path):
+    for txt in ("# nothing\n", "v 0 0 0\n"):
+        with pytest.raises(ObjError) as e:
+            _native(tmp_path, txt)
+        assert e.value.status == capi.E_BUILD
+    with pytest.raises(OSError):
+        load_obj_file(str(tmp_path / "missing.obj"))
+
+
+def test_native_loader_generated_mesh(oracle, tmp_path):
+    p = tmp_path / "m.obj"
+    meshgen.generate(str(p), 20000, 5)
+    a = load_obj_file(str(p))
+    assert a[0].shape == (20000, 9)
+    assert same(a, load_obj(p.read_text()))
+    v, n, t, fv, ft, fn = meshgen.displaced_sphere(20000, 5)
+    assert np.array_equal(a[0], v[fv].reshape(-1, 9))
