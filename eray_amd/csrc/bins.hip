@@ -357,7 +357,7 @@ __global__ void __launch_bounds__(kBinWG) detail_flags_kernel(const ObjectDesc* 
                                                               uint32_t band_shift, uint32_t band_mask,
                                                               uint32_t band_stride,
                                                               uint32_t bins_x, uint32_t phase, uint32_t tiles_x,
-                                                              uint32_t n, uint8_t* __restrict__ flags,
+                                                              uint32_t n, uint32_t heavy_min, uint8_t* __restrict__ flags,
                                                               uint8_t* __restrict__ flags_light,
                                                               uint32_t* __restrict__ packed, uint8_t* __restrict__ occ) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -375,7 +375,7 @@ __global__ void __launch_bounds__(kBinWG) detail_flags_kernel(const ObjectDesc* 
             if (g.bin_start) {
                 const uint32_t bin = (((uint32_t)y0 + kBinH - phase) / kBinH) * bins_x + sx;
                 hit = g.bin_start[bin + 1] > g.bin_start[bin];
-                heavy = g.bin_start[bin + 1] - g.bin_start[bin] > 64u;
+                heavy = g.bin_start[bin + 1] - g.bin_start[bin] > heavy_min;
             } else {
                 hit = x0 <= g.rect[1] && x1 >= g.rect[0] && y0 <= g.rect[3] && y1 >= g.rect[2];
             }
@@ -556,7 +556,7 @@ hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tile
     if (ordered) {
         detail_flags_kernel<<<(n + kBinWG - 1) / kBinWG, kBinWG, 0, s>>>(sp.objs, sp.nobj, sp.W, sp.row0, sp.rows,
                                                                         sp.band_shift, sp.band_mask, sp.band_stride,
-                                                                        b.bins_x, b.phase, tiles_x, n, b.dflags,
+                                                                        b.bins_x, b.phase, tiles_x, n, sp.keep_all ? kTraceHeavyMin : 64u, b.dflags,
                                                                         b.dflags_light, b.dpacked, b.docc);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         tb = b.temp_bytes;

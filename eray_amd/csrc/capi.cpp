@@ -1002,6 +1002,11 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     p.trace_cull = (general && !(rp->flags & ERAY_RENDER_BRUTE_FORCE) && ctx->total_tris <= kTraceSkipTris)
                        ? ctx->d_tcull : nullptr;
     p.trace_bins = trace_bins ? 1u : 0u;
+    if (trace_bins) {  // the setup's detail list (trace.hip trace_binned_kernel, trace_heavy_kernel)
+        p.detail_list = ctx->bins.dlist;
+        p.detail_heavy = ctx->bins.dcount;
+        p.detail_occ = ctx->bins.docc;
+    }
     p.launch_flags = rp->flags & ~ERAY_RENDER_BRUTE_FORCE;
     if (!cull) {  // every pixel in detail: one rectangle, the frame (sub-block units)
         if (p.nobj) {
@@ -1530,7 +1535,9 @@ void* eray_internal_staging(eray_ctx* ctx, size_t bytes) {
 // Diagnostics (not part of include/eray_hip.h): the screen bins of object `index` as built for
 // the last setup — out[0] bins, out[1] entries, out[2] (face, pixel) pairs (mask bits),
 // out[3] most entries in one bin, out[4] non-empty bins, out[5] most pairs in one bin,
-// out[6..9] the object's pixel rectangle (x0, x1, y0, y1; int32 as uint64).  Synchronises.
+// out[6..9] the object's pixel rectangle (x0, x1, y0, y1; int32 as uint64), out[10] the bin with
+// the most entries, out[11] / out[12] the bins of more than 64 / kTraceHeavyMin entries (out: 13
+// words).  Synchronises.
 extern "C" int eray_debug_bin_stats(eray_ctx* ctx, uint32_t index, uint64_t* out) {
     if (!ctx || !out || index >= ctx->objects.size() || ctx->objects[index].T <= kDirectMax || !ctx->bins.start)
         return ERAY_E_INVALID_ARGUMENT;
@@ -1547,9 +1554,12 @@ extern "C" int eray_debug_bin_stats(eray_ctx* ctx, uint32_t index, uint64_t* out
     std::vector<unsigned long long> mask(n);
     if (n && hipMemcpy(mask.data(), b.mask + start[0], n * 8, hipMemcpyDeviceToHost) != hipSuccess)
         return set_error(ctx, ERAY_E_HIP, "bin stats copy failed");
-    uint64_t pairs = 0, most = 0, nonempty = 0, most_pairs = 0;
+    uint64_t pairs = 0, most = 0, nonempty = 0, most_pairs = 0, most_at = 0, over64 = 0, over192 = 0;
     for (size_t i = 0; i < b.nbins; ++i) {
         const uint64_t e = start[i + 1] - start[i];
+        over64 += e > 64;
+        over192 += e > kTraceHeavyMin;
+        if (e > most) most_at = i;
         most = e > most ? e : most;
         nonempty += e != 0;
         uint64_t pb = 0;
@@ -1564,6 +1574,31 @@ extern "C" int eray_debug_bin_stats(eray_ctx* ctx, uint32_t index, uint64_t* out
     out[4] = nonempty;
     out[5] = most_pairs;
     for (int q = 0; q < 4; ++q) out[6 + q] = (uint64_t)(int64_t)d.g.rect[q];
+    out[10] = most_at;
+    out[11] = over64;
+    out[12] = over192;
+    return ERAY_OK;
+}
+
+// Diagnostics: the entries of bin `bin` of object `index` (faces relative to the object, pixel
+// masks), at most `cap`; *n = the bin's entry count.  Synchronises.
+extern "C" int eray_debug_bin_dump(eray_ctx* ctx, uint32_t index, uint32_t bin, uint32_t* tri, uint64_t* mask,
+                                   uint32_t cap, uint32_t* n) {
+    if (!ctx || !n || index >= ctx->objects.size() || ctx->objects[index].T <= kDirectMax || !ctx->bins.start ||
+        bin >= ctx->bins.nbins)
+        return ERAY_E_INVALID_ARGUMENT;
+    const BinBuffers& b = ctx->bins;
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < index; ++i) k += ctx->objects[i].T > kDirectMax;
+    uint32_t se[2];
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess ||
+        hipMemcpy(se, b.start + (size_t)k * b.nbins + bin, 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return set_error(ctx, ERAY_E_HIP, "bin dump copy failed");
+    *n = se[1] - se[0];
+    const uint32_t m = std::min(*n, cap);
+    if (m && (hipMemcpy(tri, b.tri + se[0], 4 * (size_t)m, hipMemcpyDeviceToHost) != hipSuccess ||
+              hipMemcpy(mask, b.mask + se[0], 8 * (size_t)m, hipMemcpyDeviceToHost) != hipSuccess))
+        return set_error(ctx, ERAY_E_HIP, "bin dump copy failed");
     return ERAY_OK;
 }
 

@@ -136,6 +136,9 @@ struct alignas(16) CamState {
 };
 
 constexpr uint32_t kTraceSkipTris = 256;  // general tracer: largest scene with the background skip
+// general tracer: a binned sub-block whose bin holds more entries is searched by a whole
+// workgroup (trace.hip; the tracer's setup lists those first, bins.hip detail_flags_kernel)
+constexpr uint32_t kTraceHeavyMin = 192;
 
 struct FrameParams {
     // camera (camera.rs:57-76)
@@ -202,6 +205,12 @@ struct FrameParams {
     // trace_kernel's camera rays scan the binned objects' screen bins (a setup with
     // SetupParams::keep_all; the descriptors' bin views and rectangles), else every face
     uint32_t trace_bins;
+    // ... over the setup's detail list (the sub-blocks some ray of which may hit a face; detail_occ
+    // per 64 x 4 block): trace_heavy_kernel's workgroups take the heavy head of the list, a
+    // workgroup per sub-block; trace_binned_kernel's first trace_fill_wgs workgroups write the
+    // background of the unlisted sub-blocks and the next trace_light_wgs the light list, a wave
+    // per sub-block
+    uint32_t trace_heavy_wgs, trace_fill_wgs, trace_light_wgs;
     // Frames in flight: one launch renders `nframes` (>= 1) independent frames, its workgroups
     // dealt round-robin over them (frame_kernel).  Frame f writes out_* + f * *_stride (bytes,
     // multiples of 16) and, with dev_slots, reads the batched per-camera setup of slot f
@@ -326,7 +335,7 @@ struct LaunchCtx {
 };
 // The frame kernel, or the general tracer (trace.hip) when p.aa or p.bounces is set.
 hipError_t launch_render(const FrameParams& p, const LaunchCtx& lc, hipStream_t s);
-hipError_t launch_trace(const FrameParams& p, hipStream_t s);
+hipError_t launch_trace(const FrameParams& p, const LaunchCtx& lc, hipStream_t s);
 
 // ------------------------------------------------------------- screen bins (bins.hip)
 // Device arrays of the binned objects' screen bins for one layout (camera size, row phase, the

@@ -804,27 +804,6 @@ __device__ __forceinline__ Bundle make_bundle(const FrameParams& p, const RowMap
                   ((float)(y0 + (pye - py0)) * rh) * hi};
 }
 
-// Frame outputs are written once and never read back by the kernel: 16-byte buffer stores with
-// the sc1 (write-through) policy.  An sc1 store leaves no dirty line in the XCD's L2 (the line is
-// dropped once written), so (a) the next dependent kernel boundary does not write back ~31 MB of
-// dirty frame lines (MI355X_MICROARCH.md 'boundary': + B / 6 TB/s), and (b) the frame does not
-// evict the scene and the textures the next frame reads.  Measured at C2: 10.5 -> 8.6 us per
-// frame vs non-temporal stores (which keep the line).  `base` is the wave-uniform output array
-// (the buffer resource); byte offsets fit 32 bits (FrameParams::aligned requires it).
-using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
-constexpr int kStoreSc1 = 16;  // CPol::SC1 (buffer instruction aux bits on gfx940+)
-template <typename B>
-__device__ __forceinline__ void stream16(B* base, const void* dst, uint4 v) {
-    const u32x4 w{v.x, v.y, v.z, v.w};
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, -1, 0x00020000);
-    const uint32_t off = (uint32_t)(reinterpret_cast<const char*>(dst) - reinterpret_cast<const char*>(base));
-    __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, kStoreSc1);
-}
-template <typename B>
-__device__ __forceinline__ void stream16(B* base, const void* dst, float4 v) {
-    stream16(base, dst, make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)));
-}
-
 // One frame's output arrays (FrameParams::out_* of the frame: frames in flight write their own).
 struct FrameOut {
     float* rgb;
@@ -1650,7 +1629,7 @@ hipError_t launch_frame_cs(const FrameParams& p, uint32_t want, const LaunchCtx&
 
 hipError_t launch_render(const FrameParams& p, const LaunchCtx& lc, hipStream_t s) {
     if (p.nframes < 1 || ((p.aa || p.bounces) && p.nframes != 1)) return hipErrorInvalidValue;
-    if (p.aa || p.bounces) return launch_trace(p, s);
+    if (p.aa || p.bounces) return launch_trace(p, lc, s);
     const uint32_t by_n = (p.rows + kBlkH - 1) / kBlkH;
     const uint32_t nblk = p.tiles_x * by_n;
     if (!nblk) return hipSuccess;

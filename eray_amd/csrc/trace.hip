@@ -150,6 +150,7 @@ __device__ void fill_level(const FrameParams& p, f3 o, f3 d, const Hit& h, Level
                       wv * omf + mat.ex_b * mat.ex_factor};
         L.kd = wv;
     }
+#ifndef ERAY_TRACE_NO_PROG  // diagnostics (scripts/build_variants.sh): the texel programs' call frames
     if (mat.prog) {  // a shader graph at the texel (its outputs have no texture)
         float t3[3];
         if (texel_program(mat.prog, 0, uv0, uv1, t3)) L.color = rgb{t3[0], t3[1], t3[2]};
@@ -158,6 +159,7 @@ __device__ void fill_level(const FrameParams& p, f3 o, f3 d, const Hit& h, Level
         if (texel_program(mat.prog, 3, uv0, uv1, t3)) L.sp = t3[0];
         if (texel_program(mat.prog, 4, uv0, uv1, t3)) L.refl = t3[0];
     }
+#endif
     if (const float* c = texel(mat.color, uv0, uv1, 3)) L.color = rgb{c[0], c[1], c[2]};
     if (const float* c = texel(mat.diffuse, uv0, uv1, 1)) L.kd = *c;
     if (const float* c = texel(mat.specular, uv0, uv1, 1)) L.ks = *c;
@@ -186,108 +188,172 @@ __device__ bool surface(const FrameParams& p, f3 o, f3 d, Level& L, int32_t* fac
 
 // Camera rays of one pixel, up to kRays at once (the corner ray and anti-aliasing rays), against
 // every object: the closest hit of each (engine.rs:116-126).  Binned objects (p.trace_bins) are
-// searched in one pass over the wave's screen bin `bin` (bins.hip, the tracer's setup) for all the
-// rays together: a camera ray of the bin's pixels — the corner ray or a jittered one, whose
+// searched in one pass over the sub-block's screen bin `bin` (bins.hip, the tracer's setup) for all
+// its rays together: a camera ray of the bin's pixels — the corner ray or a jittered one, whose
 // viewport point stays inside [-1/W, 1] x [-1/H, 1] — can only hit faces whose entry marks its
 // pixel (face_rect.hpp bin_pixels_jittered), and Object::intersects' first face (object.rs:63-78)
-// is the smallest index that passes: the entries are in no particular order except in bins of 65
-// to kBinSortMax (face order), where a ray stops at its first pass.  One wave is one bin: its
-// lanes load the bin 64 entries at a time into the wave's LDS slot (one round trip per chunk),
-// then every lane reads each entry that marks some searching pixel (LDS broadcasts) and tests
-// its rays.  Every lane of the wave must call (`valid` false: a lane off the frame, no rays).
-// Other objects: first_face per ray.
-constexpr int kRays = 5;  // anti_aliasing = 4 in one pass
-struct BinChunk {         // one wave's LDS slot: a chunk of its bin's entries
+// is the smallest index that passes, whatever order the entries come in.
+// A group of kW waves searches one sub-block (lane = pixel: bit row * 16 + column of a bin mask):
+// each wave loads 64 entries at a time into its LDS chunk (one round trip), an entry marking at
+// most kWide of the searching pixels is tested as (entry, pixel) pairs, compacted in LDS and dealt
+// one per lane — a pole of the mesh, where hundreds of thin faces meet, puts a thousand entries
+// into one bin, each covering a few pixels — and a wider one by the whole wave (lane = pixel).
+// Each (ray, pixel) keeps its smallest passing face in LDS (atomicMin); wave 0 then re-tests its
+// pixels' winners for u, v, t (the same f32 operations: the same values).  kW = 1: every wave its
+// own sub-block; kW = 4: the workgroup on one heavy sub-block (trace_kernel).  Wave 0's lanes
+// hold the pixels' rays `d` and receive the hits; every lane of the group must call (`valid`
+// false: a lane off the frame, no rays).  Objects without bins: first_face per ray.
+constexpr int kRays = 5;    // anti_aliasing = 4 in one pass
+constexpr uint32_t kWide = 16;
+struct BinRays {              // the sub-block's rays and results, shared by the group
+    float dir[kRays][3][64];  // lane = pixel
+    uint32_t best[kRays][64];  // smallest passing face per (ray, pixel), ~0u: none
+    uint32_t in[64];           // bit r: ray r of the pixel passes the object's bounding box
+    unsigned long long act;    // pixels with some ray in the box
+    unsigned long long pad;
+};
+struct BinChunk {             // one wave's chunk of the bin's entries
     TriHot hot[64];
     unsigned long long mask[64];
     uint32_t tri[64];
+    uint16_t pairs[64 * kWide];  // (entry << 6) | pixel
 };
+template <int kW>
+struct BinGroup {
+    BinRays R;
+    BinChunk E[kW];
+};
+
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+template <int kW>
+__device__ __forceinline__ void group_sync() {
+    if (kW == 1) wave_sync();
+    else __syncthreads();
+}
+template <int kW>
 __device__ void camera_hits(const FrameParams& p, f3 C, const f3 (&d)[kRays], uint32_t nr, bool valid, uint32_t bin,
-                            BinChunk& E, Hit (&h)[kRays]) {
-    const uint32_t lane = threadIdx.x & 63;  // = the pixel's bit in a bin mask (row * 16 + column)
+                            BinGroup<kW>& G, Hit (&h)[kRays]) {
+    const uint32_t lane = threadIdx.x & 63, wg = kW == 1 ? 0u : (threadIdx.x >> 6);
+    BinRays& R = G.R;
+    BinChunk& E = G.E[wg];
 #pragma unroll
-    for (int r = 0; r < kRays; ++r) h[r].f = -1;
+    for (int r = 0; r < kRays; ++r) {
+        h[r].f = -1;
+        if (wg == 0) {
+            R.dir[r][0][lane] = d[r].x;
+            R.dir[r][1][lane] = d[r].y;
+            R.dir[r][2][lane] = d[r].z;
+        }
+    }
     for (uint32_t oi = 0; oi < p.nobj; ++oi) {
         const ObjGeom ob = load_const(&p.objects[oi].g, 0);
         if (!ob.bin_start) {
+            if (wg == 0) {
 #pragma unroll
-            for (uint32_t r = 0; r < (uint32_t)kRays; ++r)
-                if (valid && r < nr) {
-                    float u, v, t;
-                    const int f = first_face(p.tris, ob, C, d[r], u, v, t, nullptr);
-                    closer(h[r], oi, f, u, v, t, C, d[r], C);
-                }
+                for (uint32_t r = 0; r < (uint32_t)kRays; ++r)
+                    if (valid && r < nr) {
+                        float u, v, t;
+                        const int f = first_face(p.tris, ob, C, d[r], u, v, t, nullptr);
+                        closer(h[r], oi, f, u, v, t, C, d[r], C);
+                    }
+            }
             continue;
         }
-        bool in[kRays];
-        uint32_t bf[kRays];
-        float bu[kRays], bv[kRays], bt[kRays];
-        bool any_in = false;
+        if (wg == 0) {
+            uint32_t inb = 0;
 #pragma unroll
-        for (int r = 0; r < kRays; ++r) {
-            in[r] = valid && (uint32_t)r < nr && bbox_hit(ob, C, d[r]);
-            bf[r] = ~0u;
-            bu[r] = bv[r] = bt[r] = 0.0f;
-            any_in |= in[r];
+            for (int r = 0; r < kRays; ++r) {
+                if (valid && (uint32_t)r < nr && bbox_hit(ob, C, d[r])) inb |= 1u << r;
+                R.best[r][lane] = ~0u;
+            }
+            R.in[lane] = inb;
+            const unsigned long long a = __ballot(inb != 0);
+            if (lane == 0) R.act = a;
         }
-        const unsigned long long act = __ballot(any_in);
-        if (act) {
-            const uint32_t lo = load_const(ob.bin_start, bin), hi = load_const(ob.bin_start, bin + 1);
-            const bool sorted = hi - lo > 64 && hi - lo <= kBinSortMax;
-            for (uint32_t base = lo; base < hi; base += 64) {
-                const uint32_t j = base + lane;
-                bool rel = false;
-                if (j < hi) {
-                    const unsigned long long m = ob.bin_mask[j];
-                    rel = (m & act) != 0;
-                    E.mask[lane] = m;
-                    E.tri[lane] = ob.bin_tri[j];
-                    E.hot[lane] = ob.bin_hot[j];
+        group_sync<kW>();
+        const unsigned long long act = R.act;
+#ifdef ERAY_TRACE_NO_SEARCH  // diagnostics (scripts/build_variants.sh): the bin search's share
+        group_sync<kW>();
+        continue;
+#endif
+        const uint32_t lo = act ? load_const(ob.bin_start, bin) : 0u, hi = act ? load_const(ob.bin_start, bin + 1) : 0u;
+        for (uint32_t rb = lo; rb < hi; rb += 64 * kW) {
+            const uint32_t j = rb + 64 * wg + lane;
+            unsigned long long m = 0;
+            if (j < hi) {
+                m = ob.bin_mask[j] & act;
+                E.tri[lane] = ob.bin_tri[j];
+                E.hot[lane] = ob.bin_hot[j];
+            }
+            const uint32_t pop = (uint32_t)__popcll(m);
+            const bool narrow = pop && pop <= kWide;
+            // the narrow entries' pairs: exclusive scan of their counts over the lanes
+            uint32_t incl = narrow ? pop : 0u;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)incl, off);
+                if ((int)lane >= off) incl += y;
+            }
+            const uint32_t npairs = (uint32_t)__shfl((int)incl, 63);
+            if (narrow) {
+                uint32_t at = incl - pop;
+                unsigned long long mm = m;
+                while (mm) {
+                    E.pairs[at++] = (uint16_t)((lane << 6) | (uint32_t)__builtin_ctzll(mm));
+                    mm &= mm - 1;
                 }
-                unsigned long long todo = __ballot(rel);
-                wave_sync();
-                while (todo) {
-                    const uint32_t k = (uint32_t)__builtin_ctzll(todo);
-                    todo &= todo - 1;
-                    const uint32_t f = E.tri[k];
-                    const bool mine = (E.mask[k] >> lane) & 1ull;
-                    const TriHot hh = E.hot[k];
-                    bool hit[kRays];
-                    float uu[kRays], vv[kRays], tt[kRays];
+            }
+            unsigned long long wide = __ballot(pop > kWide);
+            E.mask[lane] = m;
+            wave_sync();
+            for (uint32_t i = lane; i < npairs; i += 64) {  // one (entry, pixel) pair per lane
+                const uint32_t pr = E.pairs[i], k = pr >> 6, q = pr & 63u;
+                const uint32_t f = E.tri[k], bits = R.in[q];
+                const TriHot hh = E.hot[k];
 #pragma unroll
-                    for (int r = 0; r < kRays; ++r) {
-                        hit[r] = false;
-                        if ((uint32_t)r < nr) {  // (wave-uniform)
-                            const bool pass = exact_test_flat(hh, C, d[r], uu[r], vv[r], tt[r]);
-                            hit[r] = mine & in[r] & (f < bf[r]) & pass;
-                        }
-                    }
-#pragma unroll
-                    for (int r = 0; r < kRays; ++r)
-                        if (hit[r]) {
-                            bf[r] = f;
-                            bu[r] = uu[r];
-                            bv[r] = vv[r];
-                            bt[r] = tt[r];
-                        }
+                for (uint32_t r = 0; r < (uint32_t)kRays; ++r) {
+                    if (r >= nr) break;
+                    if (!((bits >> r) & 1u) || f >= R.best[r][q]) continue;
+                    float u, v, t;
+                    const f3 dq = mk3(R.dir[r][0][q], R.dir[r][1][q], R.dir[r][2][q]);
+                    if (exact_test_flat(hh, C, dq, u, v, t)) atomicMin(&R.best[r][q], f);
                 }
-                wave_sync();  // (the next chunk rewrites the slot)
-                if (sorted) {
-                    bool searching = false;
+            }
+            const uint32_t bits = R.in[lane];
+            while (wide) {  // a wide entry: every lane tests its own pixel's rays
+                const uint32_t k = (uint32_t)__builtin_ctzll(wide);
+                wide &= wide - 1;
+                const uint32_t f = E.tri[k];
+                if (!((E.mask[k] >> lane) & 1ull)) continue;
+                const TriHot hh = E.hot[k];
 #pragma unroll
-                    for (int r = 0; r < kRays; ++r) searching |= in[r] && bf[r] == ~0u;
-                    if (!__any(searching)) break;
+                for (uint32_t r = 0; r < (uint32_t)kRays; ++r) {
+                    if (r >= nr) break;
+                    float u, v, t;
+                    const f3 dq = mk3(R.dir[r][0][lane], R.dir[r][1][lane], R.dir[r][2][lane]);
+                    if (((bits >> r) & 1u) && f < R.best[r][lane] && exact_test_flat(hh, C, dq, u, v, t))
+                        atomicMin(&R.best[r][lane], f);
+                }
+            }
+            wave_sync();  // (the next chunk rewrites the wave's slot)
+        }
+        group_sync<kW>();  // every wave's results are in
+        if (wg == 0) {  // the winners' u, v, t: the exact test again on the winning face's record
+#pragma unroll
+            for (uint32_t r = 0; r < (uint32_t)kRays; ++r) {
+                const uint32_t f = R.best[r][lane];
+                if (r < nr && f != ~0u) {
+                    float u, v, t;
+                    exact_test_flat(p.tris[ob.tri_begin + f], C, d[r], u, v, t);
+                    closer(h[r], oi, (int)f, u, v, t, C, d[r], C);
                 }
             }
         }
-#pragma unroll
-        for (int r = 0; r < kRays; ++r)
-            if (bf[r] != ~0u) closer(h[r], oi, (int)bf[r], bu[r], bv[r], bt[r], C, d[r], C);
+        group_sync<kW>();  // (R is rewritten for the next object)
     }
 }
 
@@ -404,11 +470,12 @@ __device__ __forceinline__ T pick(const T (&a)[kRays], uint32_t r) {
 //    viewport range widened to the jittered rays') and each workgroup copies them into LDS; a wave
 //    none of whose records survives its rectangle skips, the other waves keep the survivors' bits
 //    (live_mask): their camera rays test only those faces, in index order.
-//  * Scenes with binned objects (p.trace_bins): the per-camera setup's object rectangles
-//    (face_rect.hpp unions over the viewport the jittered rays reach, [-1/W, 1] x [-1/H, 1];
-//    binned objects narrowed to their non-empty bins) hold every pixel whose corner or jittered
-//    ray can hit the object.  A wave whose sub-block meets no object's rectangle skips; in the
-//    others the binned objects' faces come from the wave's bin (first_face_binned).
+//  * Scenes with binned objects (p.trace_bins): the tracer's per-camera setup works over the
+//    viewport the jittered rays reach, [-1/W, 1] x [-1/H, 1]: a binned object's bin lists every
+//    face any ray of the bin's pixels may hit (camera_hits), a small object's rectangle (the
+//    union of face_rect.hpp's) holds every pixel one of whose rays may hit it.  A wave whose bin
+//    is empty for every binned object and whose sub-block meets no small object's rectangle
+//    skips; the others search their bin (camera_hits).
 // Bit-identical to the brute-force scan (ERAY_RENDER_BRUTE_FORCE turns both off;
 // tests/test_gpu_trace.py compares them).
 constexpr uint32_t kSkipTris = kTraceSkipTris;
@@ -426,15 +493,112 @@ __global__ void __launch_bounds__(256) trace_cull_kernel(FrameParams p) {
 __device__ __forceinline__ float widen_down(float v) { return v >= 0.0f ? v * (1.0f - 0x1p-20f) : v * (1.0f + 0x1p-20f); }
 __device__ __forceinline__ float widen_up(float v) { return v >= 0.0f ? v * (1.0f + 0x1p-20f) : v * (1.0f - 0x1p-20f); }
 
+// ray i of pixel (px, camera row y): 0 is cast_ray_from_camera(x as f32, y as f32) (engine.rs:60,
+// 100-109), 1 + s the s-th anti-aliasing ray (engine.rs:62-69); the pixel sums them in that order
+__device__ __forceinline__ f3 pixel_ray(const FrameParams& p, uint32_t px, uint32_t y, uint32_t i) {
+    if (i == 0) return camera_ray_dir(p, (float)px / (float)p.cam_w, (float)y / (float)p.cam_h);
+    const uint4 r = philox4x32_10(make_uint4(px, y, i - 1, 0u), p.seed_lo, p.seed_hi);
+    const float xf = ((float)px + jitter(r.x)) / (float)p.cam_w;
+    const float yf = ((float)y + jitter(r.y)) / (float)p.cam_h;
+    return camera_ray_dir(p, xf, yf);
+}
+
+// (average / aa as f32).clamp() (engine.rs:71-73), then Image::set and the PPM bytes
+// (Color::as_bytes, rows bottom-up: image.rs:48-74, color.rs:31-37) and the first ray's face
+__device__ __forceinline__ void store_pixel(const FrameParams& p, uint32_t px, uint32_t py, rgb avg, int32_t face) {
+    if (p.aa) {
+        const float n = (float)p.aa;
+        avg = rgb{rust_clamp(avg.r / n, 0.0f, 1.0f), rust_clamp(avg.g / n, 0.0f, 1.0f),
+                  rust_clamp(avg.b / n, 0.0f, 1.0f)};
+    }
+    const size_t idx = (size_t)py * p.img_w + px;
+    if (p.out_rgb) {
+        float* o = p.out_rgb + 3 * idx;
+        o[0] = avg.r;
+        o[1] = avg.g;
+        o[2] = avg.b;
+    }
+    if (p.out_ppm) {
+        uint8_t* o = p.out_ppm + 3 * ((size_t)(p.rows - 1 - py) * p.img_w + px);
+        o[0] = (uint8_t)sat_u8(avg.r * 255.0f);
+        o[1] = (uint8_t)sat_u8(avg.g * 255.0f);
+        o[2] = (uint8_t)sat_u8(avg.b * 255.0f);
+    }
+    if (p.out_face) p.out_face[idx] = face;
+}
+
+// The binned search of a sub-block's rays (camera_hits: the wave alone, or with `heavy` the
+// workgroup's four waves together) and, in the pixel's lane of wave 0, the walks of their hits:
+// the pixel's sum and first face.
+template <bool kBounce, bool heavy>
+__device__ void binned_pixel(const FrameParams& p, uint32_t px, uint32_t y, bool valid, uint32_t bin,
+                             unsigned char* lds, rgb& avg, int32_t& face) {
+    const bool lead = !heavy || (threadIdx.x >> 6) == 0;
+    const f3 C = mk3(p.cx, p.cy, p.cz);
+    const uint32_t n = 1 + p.aa;
+    for (uint32_t i0 = 0; i0 < n; i0 += kRays) {  // (wave- / workgroup-uniform)
+        const uint32_t nr = min((uint32_t)kRays, n - i0);
+        f3 d[kRays];
+#pragma unroll
+        for (uint32_t r = 0; r < (uint32_t)kRays; ++r)
+            d[r] = (lead && r < nr) ? pixel_ray(p, px, y, i0 + r) : mk3(0.0f, 0.0f, -1.0f);
+        Hit h[kRays];
+        if constexpr (heavy) camera_hits<4>(p, C, d, nr, valid && lead, bin, *reinterpret_cast<BinGroup<4>*>(lds), h);
+        else camera_hits<1>(p, C, d, nr, valid, bin, *reinterpret_cast<BinGroup<1>*>(lds), h);
+        if (!valid || !lead) continue;
+        for (uint32_t r = 0; r < nr; ++r) {
+            const Hit hr = pick(h, r);
+            rgb c = miss_color();
+            if (hr.f >= 0) {
+#ifndef ERAY_TRACE_NO_SHADE  // diagnostics (scripts/build_variants.sh): the shading walks' share
+                Level L;
+                fill_level(p, C, pick(d, r), hr, L);
+                c = walk<kBounce>(p, L);
+#endif
+            }
+            if (i0 + r == 0) {
+                avg = c;
+                face = hr.f;
+            } else {
+                avg = cadd(avg, c);
+            }
+        }
+    }
+}
+
+
+// Heavy sub-blocks (scenes with binned objects).  A bin of more than kTraceHeavyMin entries (the
+// tracer setup's detail list puts those first, bins.hip) would keep its wave long after the
+// others; trace_binned_kernel's first workgroups take them instead, the whole workgroup on one
+// sub-block (camera_hits<4>).
+template <bool kBounce>
+__device__ void heavy_role(const FrameParams& p, unsigned char* s_raw, uint32_t first, uint32_t stride) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t nheavy = *p.detail_heavy;
+    for (uint32_t hv = first; hv < nheavy; hv += stride) {
+        const uint32_t sub = p.detail_list[hv], sx = sub & 0xffffu, sy = sub >> 16;
+        const uint32_t px = sx * kBinW + (lane & 15), py = sy * kBinH + (lane >> 4);
+        const uint32_t y0 = band_camera_row(p.row0, p.band_shift, p.band_mask, p.band_stride, sy * kBinH);
+        const uint32_t y = y0 + (lane >> 4);
+        const uint32_t bin = ((y0 + kBinH - p.bin_phase) / kBinH) * p.bins_x + sx;
+        const bool valid = px < p.cam_w && py < p.rows;
+        rgb avg{0.0f, 0.0f, 0.0f};
+        int32_t face = -1;
+        binned_pixel<kBounce, true>(p, px, y, valid, bin, s_raw, avg, face);
+        if (wave == 0 && valid) store_pixel(p, px, py, avg, face);
+        __syncthreads();  // (the next sub-block rewrites the group's LDS)
+    }
+}
+
 template <bool kBounce>
 __global__ void __launch_bounds__(256) trace_kernel(FrameParams p) {
-    __shared__ TriCull s_cull[kSkipTris];
+    __shared__ TriCull s_cull[kSkipTris];  // the culling records (scenes of at most kSkipTris faces)
     __shared__ uint64_t s_live[4][kSkipTris / 64];  // each wave's live_mask (LDS: run-time indexed)
-    __shared__ BinChunk s_chunk[4];                  // each wave's bin chunk (camera_hits)
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t x0 = blockIdx.x * 64 + wave * 16;  // the wave's sub-block: columns x0 .. x0 + 15
+    const uint32_t bx = blockIdx.x % p.tiles_x, by = blockIdx.x / p.tiles_x;
+    const uint32_t x0 = bx * 64 + wave * 16;  // the wave's sub-block: columns x0 .. x0 + 15
     const uint32_t px = x0 + (lane & 15);
-    const uint32_t py0 = blockIdx.y * 4, py = py0 + (lane >> 4);  // rank-local rows
+    const uint32_t py0 = by * 4, py = py0 + (lane >> 4);  // rank-local rows
     const uint32_t y0 = band_camera_row(p.row0, p.band_shift, p.band_mask, p.band_stride, py0);
     const uint32_t y = y0 + (lane >> 4);
     bool skip = false;
@@ -459,97 +623,171 @@ __global__ void __launch_bounds__(256) trace_kernel(FrameParams p) {
         skip = any == 0;
         live = live_mask;
     }
-    uint32_t bin = ~0u;
-    if (p.trace_bins) {  // wave-uniform
-        bin = ((y0 + kBinH - p.bin_phase) / kBinH) * p.bins_x + x0 / kBinW;
-        bool meets = false;
-        for (uint32_t oi = 0; oi < p.nobj && !meets; ++oi) {
-            const int32_t* r = p.objects[oi].g.rect;
-            meets = r[0] <= r[1] && r[2] <= r[3] && (int32_t)x0 + 15 >= r[0] && (int32_t)x0 <= r[1] &&
-                    (int32_t)y0 + 3 >= r[2] && (int32_t)y0 <= r[3];
-        }
-        skip = !meets;
-    }
     const bool valid = px < p.cam_w && py < p.rows;
     const f3 C = mk3(p.cx, p.cy, p.cz);
     int32_t face = -1;
-    rgb avg;
-    // ray 0: cast_ray_from_camera(x as f32, y as f32) (engine.rs:60, 100-109); ray 1 + s: the
-    // s-th anti-aliasing ray (engine.rs:62-69); the pixel sums them in that order
-    auto ray_dir = [&](uint32_t i) {
-        if (i == 0) return camera_ray_dir(p, (float)px / (float)p.cam_w, (float)y / (float)p.cam_h);
-        const uint4 r = philox4x32_10(make_uint4(px, y, i - 1, 0u), p.seed_lo, p.seed_hi);
-        const float xf = ((float)px + jitter(r.x)) / (float)p.cam_w;
-        const float yf = ((float)y + jitter(r.y)) / (float)p.cam_h;
-        return camera_ray_dir(p, xf, yf);
-    };
-    if (!skip && bin != ~0u) {  // binned objects: the pixel's rays kRays at a time, one pass over the bin each
-        const uint32_t n = 1 + p.aa;
-        for (uint32_t i0 = 0; i0 < n; i0 += kRays) {  // (wave-uniform; every lane, `valid` or not)
-            const uint32_t nr = min((uint32_t)kRays, n - i0);
-            f3 d[kRays];
+    rgb avg{0.0f, 0.0f, 0.0f};
+    if (!valid) return;
+    if (skip) {  // every camera ray misses (the jitter only moves a ray that misses anyway)
+        avg = miss_color();
+        for (uint32_t s = 0; s < p.aa; ++s) avg = cadd(avg, miss_color());
+    } else {
+        avg = cast_ray<kBounce>(p, C, pixel_ray(p, px, y, 0), &face, false, live);
+        for (uint32_t s = 0; s < p.aa; ++s)
+            avg = cadd(avg, cast_ray<kBounce>(p, C, pixel_ray(p, px, y, 1 + s), nullptr, false, live));
+    }
+    store_pixel(p, px, py, avg, face);
+}
+
+
+// The background colour of a pixel none of whose rays hits: (1 + aa) miss colours summed, then
+// (average / aa).clamp() (engine.rs:59-77, 211-213).
+__device__ __forceinline__ rgb background_color(const FrameParams& p) {
+    rgb avg = miss_color();
+    for (uint32_t s = 0; s < p.aa; ++s) avg = cadd(avg, miss_color());
+    if (p.aa) {
+        const float n = (float)p.aa;
+        avg = rgb{rust_clamp(avg.r / n, 0.0f, 1.0f), rust_clamp(avg.g / n, 0.0f, 1.0f), rust_clamp(avg.b / n, 0.0f, 1.0f)};
+    }
+    return avg;
+}
+
+// Background of the pixels [x0, x0 + kW) x rows [py0, py0 + 4) (kW = 64 or 16), wave-wide: the
+// colour `c` (bytes `b`) as 16-byte write-through row stores, the face -1 (engine.rs:208-213).
+template <uint32_t kW>
+__device__ void fill_color(const FrameParams& p, uint32_t x0, uint32_t py0, uint32_t lane, const float (&c)[3],
+                           const uint8_t (&b)[3]) {
+    if (p.aligned && x0 + kW <= p.cam_w && py0 + kBinH <= p.rows) {
+        constexpr uint32_t kRow4 = kW * 3 / 4, kRow16 = kW * 3 / 16, kFace4 = kW / 4;
+        if (p.out_rgb) {
 #pragma unroll
-            for (uint32_t r = 0; r < (uint32_t)kRays; ++r) d[r] = r < nr ? ray_dir(i0 + r) : mk3(0.0f, 0.0f, -1.0f);
-            Hit h[kRays];
-            camera_hits(p, C, d, nr, valid, bin, s_chunk[wave], h);
-            if (!valid) continue;
-            for (uint32_t r = 0; r < nr; ++r) {
-                const Hit hr = pick(h, r);
-                rgb c = miss_color();
-                if (hr.f >= 0) {
-                    Level L;
-                    fill_level(p, C, pick(d, r), hr, L);
-                    c = walk<kBounce>(p, L);
-                }
-                if (i0 + r == 0) {
-                    avg = c;
-                    face = hr.f;
-                } else {
-                    avg = cadd(avg, c);
-                }
+            for (uint32_t i = lane; i < kBinH * kRow4; i += 64) {
+                const uint32_t r = i / kRow4, q = i % kRow4, ph = q % 3;  // float offset 4q: component (4q) % 3
+                const float4 w = make_float4(c[ph], c[(ph + 1) % 3], c[(ph + 2) % 3], c[ph]);
+                stream16(p.out_rgb, reinterpret_cast<float4*>(p.out_rgb + 3 * ((size_t)(py0 + r) * p.img_w + x0)) + q, w);
             }
         }
-        if (!valid) return;
-    } else {
-        if (!valid) return;
-        if (skip) {  // every camera ray misses (the jitter only moves a ray that misses anyway)
-            avg = miss_color();
-            for (uint32_t s = 0; s < p.aa; ++s) avg = cadd(avg, miss_color());
-        } else {
-            avg = cast_ray<kBounce>(p, C, ray_dir(0), &face, false, live);
-            for (uint32_t s = 0; s < p.aa; ++s)
-                avg = cadd(avg, cast_ray<kBounce>(p, C, ray_dir(1 + s), nullptr, false, live));
+        if (p.out_ppm && lane < kBinH * kRow16) {
+            const uint32_t r = lane / kRow16, q = lane % kRow16;
+            uint32_t w[4];
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {  // byte 16q + 4k + j: component (q + 4k + j) % 3
+                w[k] = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) w[k] |= (uint32_t)b[(q + 4 * k + j) % 3] << (8 * j);
+            }
+            const size_t row = (size_t)(p.rows - py0 - kBinH + r);  // file rows, bottom-up
+            stream16(p.out_ppm, reinterpret_cast<uint4*>(p.out_ppm + 3 * (row * p.img_w + x0)) + q,
+                     make_uint4(w[0], w[1], w[2], w[3]));
         }
+        if (p.out_face && lane < kBinH * kFace4) {
+            const uint32_t r = lane / kFace4, q = lane % kFace4;
+            stream16(p.out_face, reinterpret_cast<int4*>(p.out_face + (size_t)(py0 + r) * p.img_w + x0) + q,
+                     make_uint4(~0u, ~0u, ~0u, ~0u));
+        }
+        return;
     }
-    if (p.aa) {  // (average / aa as f32).clamp() (engine.rs:71-73)
-        const float n = (float)p.aa;
-        avg = rgb{rust_clamp(avg.r / n, 0.0f, 1.0f), rust_clamp(avg.g / n, 0.0f, 1.0f),
-                  rust_clamp(avg.b / n, 0.0f, 1.0f)};
+    for (uint32_t k = lane; k < kW * kBinH; k += 64) {  // image edge or unaligned output: per pixel
+        const uint32_t px = x0 + k % kW, py = py0 + k / kW;
+        if (px >= p.cam_w || py >= p.rows) continue;
+        const size_t idx = (size_t)py * p.img_w + px;
+        if (p.out_rgb) {
+            float* o = p.out_rgb + 3 * idx;
+            o[0] = c[0];
+            o[1] = c[1];
+            o[2] = c[2];
+        }
+        if (p.out_ppm) {
+            uint8_t* o = p.out_ppm + 3 * ((size_t)(p.rows - 1 - py) * p.img_w + px);
+            o[0] = b[0];
+            o[1] = b[1];
+            o[2] = b[2];
+        }
+        if (p.out_face) p.out_face[idx] = -1;
     }
-    const size_t idx = (size_t)py * p.img_w + px;
-    if (p.out_rgb) {
-        float* o = p.out_rgb + 3 * idx;
-        o[0] = avg.r;
-        o[1] = avg.g;
-        o[2] = avg.b;
+}
+
+// Scenes with binned objects (p.trace_bins): the tracer's setup lists the sub-blocks some ray of
+// which may hit a face (bins.hip: non-empty bins, small objects' rectangles — the same
+// conditions as trace_kernel's background skip), the heavy ones first, with an occupancy byte per
+// 64 x 4 block.  The grid's first trace_heavy_wgs workgroups take the heavy sub-blocks
+// (heavy_role), the next trace_fill_wgs write the background of the unlisted sub-blocks, the
+// others take the light listed sub-blocks, one per wave (camera_hits<1>).
+template <bool kBounce>
+__global__ void __launch_bounds__(256) trace_binned_kernel(FrameParams p) {
+    constexpr size_t kLds = 4 * sizeof(BinGroup<1>) > sizeof(BinGroup<4>) ? 4 * sizeof(BinGroup<1>) : sizeof(BinGroup<4>);
+    __shared__ __attribute__((aligned(16))) unsigned char s_raw[kLds];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t nheavy_wgs = p.trace_heavy_wgs, nfill = p.trace_fill_wgs;
+    if (blockIdx.x < nheavy_wgs) {  // workgroup-uniform: the heavy sub-blocks, a workgroup each
+        heavy_role<kBounce>(p, s_raw, blockIdx.x, nheavy_wgs);
+        return;
     }
-    if (p.out_ppm) {  // Color::as_bytes, rows bottom-up (image.rs:48-74, color.rs:31-37)
-        uint8_t* o = p.out_ppm + 3 * ((size_t)(p.rows - 1 - py) * p.img_w + px);
-        o[0] = (uint8_t)sat_u8(avg.r * 255.0f);
-        o[1] = (uint8_t)sat_u8(avg.g * 255.0f);
-        o[2] = (uint8_t)sat_u8(avg.b * 255.0f);
+    const uint32_t wg = blockIdx.x - nheavy_wgs;
+    if (wg < nfill) {  // workgroup-uniform: background
+        const rgb bg = background_color(p);
+        const float c[3] = {bg.r, bg.g, bg.b};
+        const uint8_t b[3] = {(uint8_t)sat_u8(bg.r * 255.0f), (uint8_t)sat_u8(bg.g * 255.0f), (uint8_t)sat_u8(bg.b * 255.0f)};
+        const uint32_t nblk = p.tiles_x * ((p.rows + kBinH - 1) / kBinH), stride = nfill * 4;
+        uint32_t occ = 0, it = 0;  // lane i: the occupancy of this wave's i-th next block
+        for (uint32_t blk = wave * nfill + wg; blk < nblk; blk += stride, ++it) {
+            if ((it & 63u) == 0) {  // one load per 64 blocks, not a dependent load per block
+                const uint32_t bl = blk + lane * stride;
+                occ = bl < nblk ? p.detail_occ[bl] : 0u;
+            }
+            const uint32_t mask = (uint32_t)__builtin_amdgcn_readlane((int)occ, (int)(it & 63u));  // listed sub-blocks
+            const uint32_t bx = blk % p.tiles_x, by = blk / p.tiles_x;
+            if (!mask) {
+                fill_color<64>(p, bx * 64, by * kBinH, lane, c, b);
+            } else if (mask != 0xfu) {
+                for (uint32_t i = 0; i < 4; ++i)
+                    if (!((mask >> i) & 1u)) fill_color<16>(p, bx * 64 + i * 16, by * kBinH, lane, c, b);
+            }
+        }
+        return;
     }
-    if (p.out_face) p.out_face[idx] = face;
+    const uint32_t heavy = p.detail_heavy[0], nl = p.detail_heavy[1];
+    const uint32_t stride = (gridDim.x - nheavy_wgs - nfill) * 4;
+    for (uint32_t j = (wg - nfill) * 4 + wave; j < nl; j += stride) {  // (wave-uniform)
+        const uint32_t sub = p.detail_list[heavy + j], sx = sub & 0xffffu, sy = sub >> 16;
+        const uint32_t px = sx * kBinW + (lane & 15), py = sy * kBinH + (lane >> 4);
+        const uint32_t y0 = band_camera_row(p.row0, p.band_shift, p.band_mask, p.band_stride, sy * kBinH);
+        const uint32_t y = y0 + (lane >> 4);
+        const uint32_t bin = ((y0 + kBinH - p.bin_phase) / kBinH) * p.bins_x + sx;
+        const bool valid = px < p.cam_w && py < p.rows;
+        rgb avg{0.0f, 0.0f, 0.0f};
+        int32_t face = -1;
+        binned_pixel<kBounce, false>(p, px, y, valid, bin, s_raw + wave * sizeof(BinGroup<1>), avg, face);
+        if (valid) store_pixel(p, px, py, avg, face);
+    }
 }
 
 }  // namespace
 
-hipError_t launch_trace(const FrameParams& p, hipStream_t s) {
+hipError_t launch_trace(const FrameParams& p0, const LaunchCtx&, hipStream_t s) {
+    FrameParams p = p0;
+    if (p.trace_bins) {  // listed sub-blocks: heavy, light and background roles
+        if (!p.detail_list || !p.detail_heavy || !p.detail_occ) return hipErrorInvalidValue;
+        static const uint32_t cus = [] {
+            int dev = 0, n = 0;
+            return (hipGetDevice(&dev) == hipSuccess &&
+                    hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+                       ? (uint32_t)n
+                       : 256u;
+        }();
+        p.trace_heavy_wgs = cus / 4;  // (heavy sub-blocks are few: poles, dense folds; dispatched first)
+        p.trace_fill_wgs = cus;       // one per CU: the background is a write stream
+        p.trace_light_wgs = cus;      // with the fill, about one round at 2 per CU (~180 VGPRs)
+        const dim3 grid(p.trace_heavy_wgs + p.trace_fill_wgs + p.trace_light_wgs);
+        if (p.bounces) hipLaunchKernelGGL(trace_binned_kernel<true>, grid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL(trace_binned_kernel<false>, grid, dim3(256), 0, s, p);
+        return hipGetLastError();
+    }
     if (p.trace_cull) {
         if (p.total_tris > kSkipTris) return hipErrorInvalidValue;
         hipLaunchKernelGGL(trace_cull_kernel, dim3(1), dim3(256), 0, s, p);
     }
-    const dim3 grid((p.cam_w + 63) / 64, (p.rows + 3) / 4);
+    const dim3 grid(((p.cam_w + 63) / 64) * ((p.rows + 3) / 4));
     if (p.bounces) hipLaunchKernelGGL(trace_kernel<true>, grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL(trace_kernel<false>, grid, dim3(256), 0, s, p);
     return hipGetLastError();

@@ -33,7 +33,7 @@ def main():
         kw = dict(out_rgb=rgb.ptr, anti_aliasing=aa, aa_seed=7)
         ctx.render(W, H, **kw)
         ctx.synchronize()
-        st = (C.c_uint64 * 10)()
+        st = (C.c_uint64 * 13)()
         L.eray_debug_bin_stats.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]
         L.eray_debug_bin_stats(ctx._h, 0, st)
         state = (C.c_uint8 * 176)()
@@ -43,7 +43,22 @@ def main():
         words = np.frombuffer(bytes(state), np.uint32)
         ctx.render_frames(a.frames, W, H, prepare_only=True, **kw)
         ms = min(ctx.render_frames(a.frames, W, H, timed=True, **kw) for _ in range(3))
-        out[f"aa{aa}"] = {"frame_ms": round(ms, 4), "bins": int(st[0]), "entries": int(st[1]),
+        heavy = int(st[10])
+        cnt = C.c_uint32()
+        tri = (C.c_uint32 * 4096)()
+        msk = (C.c_uint64 * 4096)()
+        L.eray_debug_bin_dump.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32),
+                                          C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint32)]
+        L.eray_debug_bin_dump(ctx._h, 0, heavy, tri, msk, 4096, C.byref(cnt))
+        pops = [bin(msk[i]).count("1") for i in range(min(cnt.value, 4096))]
+        faces = [int(tri[i]) for i in range(min(cnt.value, 4096))]
+        bins_x = (W + 15) // 16
+        if aa == 4:
+            np.savez(os.path.join(os.environ.get("PROBE_OUT", "/tmp"), "heavy_bin.npz"), faces=np.array(faces),
+                     masks=np.array([int(msk[i]) for i in range(len(faces))], np.uint64), bin=heavy, bins_x=bins_x)
+        out[f"aa{aa}"] = {"bins_over_64": int(st[11]), "bins_over_heavy_min": int(st[12]), "heavy_bin_xy": [16 * (heavy % bins_x), 4 * (heavy // bins_x) - 4],
+                          "heavy_pop_hist": np.histogram(pops, bins=[0, 1, 2, 4, 8, 16, 32, 65])[0].tolist(),
+                          "frame_ms": round(ms, 4), "bins": int(st[0]), "entries": int(st[1]),
                           "most_in_bin": int(st[3]), "nonempty_bins": int(st[4]), "rect": list(rect),
                           "state_bin_entries": int(words[10]), "overflow": int(words[11]),
                           "capacity": int(L.eray_debug_bin_capacity(ctx._h))}
