@@ -275,9 +275,11 @@ def anti_aliasing_line(scene, args, width, height, out) -> dict:
     rays = width * height * (AA_SAMPLES + 1)
     return {"anti_aliasing": AA_SAMPLES, "frames": frames, "frame_ms": round(ms, 6),
             "value": round(rays / (ms * 1e-3) / 1e6, 3), "unit": "Mrays/s (all AA rays)",
-            "kernel": "trace_kernel (eray_amd/csrc/trace.hip): waves no camera ray of which can reach a face skip "
-                      "the scan (culling records / object rectangles); camera rays of large objects read the "
-                      "wave's screen bin (bins.hip, every pair of each face's rectangle); shadow rays every face"}
+            "kernel": "trace.hip: waves whose rays can reach no face skip the scan (culling records / bins and "
+                      "object rectangles); with meshes over 256 faces the tracer's setup bins every face by the pixels "
+                      "its jittered rays may hit, a wave searches its bin as (entry, pixel) pairs for all the pixel's "
+                      "rays at once, heavy bins by a whole workgroup, fill roles write the background; shadow rays "
+                      "every face"}
 
 
 def main() -> None:
