@@ -149,9 +149,12 @@ struct eray_ctx {
     size_t path_cap = 0;
     CamDev* d_path_all = nullptr;
     size_t path_all_cap = 0;
-    CamDev* h_path = nullptr;
-    size_t h_path_cap = 0;
-    hipEvent_t path_ev = nullptr;  // the last path upload (h_path reusable once complete)
+    // two pinned staging buffers used in turn: a call waits only for the upload two calls back
+    // (not for the previous call's frames, which its upload is queued behind)
+    CamDev* h_path[2] = {nullptr, nullptr};
+    size_t h_path_cap[2] = {0, 0};
+    hipEvent_t path_ev[2] = {nullptr, nullptr};  // each buffer's last upload (reusable once complete)
+    uint32_t path_buf = 0;
     // batched setups of a path chunk's cameras (scenes without binned objects): per camera slot
     // its culling records, object descriptors and setup state
     TriCull* d_bcull = nullptr;
@@ -614,7 +617,8 @@ int eray_ctx_create(int device, eray_ctx** out) {
     if (e == hipSuccess) e = hipHostMalloc((void**)&ctx->h_state, sizeof(CamState), hipHostMallocDefault);
     if (e == hipSuccess) std::memset(ctx->h_state, 0, sizeof(CamState));
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->state_ev, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->path_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->path_ev[0], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->path_ev[1], hipEventDisableTiming);
     if (e != hipSuccess) {
         ctx->stream = ctx->own_stream;
         eray_ctx_destroy(ctx);
@@ -638,14 +642,15 @@ int eray_ctx_destroy(eray_ctx* ctx) {
     for (void* b : bufs)
         if (b) hipFree(b);
     if (ctx->h_state) hipHostFree(ctx->h_state);
-    if (ctx->h_path) hipHostFree(ctx->h_path);
+    for (CamDev* h : ctx->h_path)
+        if (h) hipHostFree(h);
     if (ctx->h_objs_state) hipHostFree(ctx->h_objs_state);
     if (ctx->gather_plan && ctx->gather_plan_free) ctx->gather_plan_free(ctx->gather_plan);
     for (auto& g : ctx->graphs) {
         if (g.exec) hipGraphExecDestroy(g.exec);
         if (g.graph) hipGraphDestroy(g.graph);
     }
-    for (hipEvent_t ev : {ctx->state_ev, ctx->path_ev, ctx->lc.fork, ctx->lc.join})
+    for (hipEvent_t ev : {ctx->state_ev, ctx->path_ev[0], ctx->path_ev[1], ctx->lc.fork, ctx->lc.join})
         if (ev) hipEventDestroy(ev);
     if (ctx->lc.side) hipStreamDestroy(ctx->lc.side);
     if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
@@ -1328,8 +1333,9 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
     }
     FrameParams p;
     bool empty = false;
-    // the scene camera's setup once (scene upload, bins layout, a detail count for the launch shape)
-    if (int st = prepare_render(ctx, rp, &p, &empty, SetupWait::kYes)) return st;
+    // the scene camera's setup (scene upload, bins layout; the last known detail count steers the
+    // launch shape) — enqueued, not waited for: the path's frames read their own cameras' setups
+    if (int st = prepare_render(ctx, rp, &p, &empty, SetupWait::kNo)) return st;
     if (empty || !n) return ERAY_OK;
     Ring r;
     if (int st = make_ring(ctx, rp, p, ring, &r)) return st;
@@ -1378,19 +1384,25 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
     std::memset(p.rects, 0, sizeof p.rects);
     // the cameras: staged in pinned memory, copied to the device once per call; each graph chunk
     // reads its cameras from d_path (a device-to-device copy of its slice before each replay)
-    if (ctx->h_path_cap < n) {
-        HIP_TRY(ctx, hipEventSynchronize(ctx->path_ev));
-        if (ctx->h_path) HIP_TRY(ctx, hipHostFree(ctx->h_path));
-        ctx->h_path = nullptr;
-        HIP_TRY(ctx, hipHostMalloc((void**)&ctx->h_path, sizeof(CamDev) * n, hipHostMallocDefault));
-        ctx->h_path_cap = n;
+    const uint32_t hb = ctx->path_buf;
+    ctx->path_buf ^= 1u;
+    CamDev*& h_path = ctx->h_path[hb];
+    if (ctx->h_path_cap[hb] < n) {
+        HIP_TRY(ctx, hipEventSynchronize(ctx->path_ev[hb]));
+        if (h_path) HIP_TRY(ctx, hipHostFree(h_path));
+        h_path = nullptr;
+        HIP_TRY(ctx, hipHostMalloc((void**)&h_path, sizeof(CamDev) * n, hipHostMallocDefault));
+        ctx->h_path_cap[hb] = n;
     }
-    HIP_TRY(ctx, hipEventSynchronize(ctx->path_ev));  // the previous upload has read h_path
-    for (uint32_t f = 0; f < n; ++f) ctx->h_path[f] = cam_dev(cameras[f]);
+    HIP_TRY(ctx, hipEventSynchronize(ctx->path_ev[hb]));  // the upload two calls back has read this buffer
+    for (uint32_t f = 0; f < n; ++f) h_path[f] = cam_dev(cameras[f]);
     if (int st = ensure(ctx, &ctx->d_path_all, &ctx->path_all_cap, n)) return st;
     if (int st = ensure(ctx, &ctx->d_path, &ctx->path_cap, kGraphFrames)) return st;
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_path_all, ctx->h_path, sizeof(CamDev) * n, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipEventRecord(ctx->path_ev, ctx->stream));
+    // a path of one graph chunk goes straight into the chunk's camera slots (no per-chunk copy)
+    const bool one_chunk = n <= kGraphFrames;
+    HIP_TRY(ctx, hipMemcpyAsync(one_chunk ? ctx->d_path : ctx->d_path_all, h_path, sizeof(CamDev) * n,
+                                hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipEventRecord(ctx->path_ev[hb], ctx->stream));
     const bool batched = batch_setup_ok(ctx);
     if (!batched) r.per_launch = 1;  // a setup (screen bins) per frame: one frame per launch
     const uint32_t T = ctx->total_tris, nobj = (uint32_t)ctx->objects.size();
@@ -1448,23 +1460,20 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
     Plan plan;
     if (int st = ensure_plan(ctx, key, n, body, &plan)) return st;
     auto before = [&](uint32_t first, uint32_t count) -> int {
+        if (one_chunk) return ERAY_OK;
         HIP_TRY(ctx, hipMemcpyAsync(ctx->d_path, ctx->d_path_all + first, sizeof(CamDev) * count,
                                     hipMemcpyDeviceToDevice, ctx->stream));
         return ERAY_OK;
     };
-    auto plain = [&](uint32_t f) { return frame(ctx->d_path_all + f, f); };
+    auto plain = [&](uint32_t f) { return frame((one_chunk ? ctx->d_path : ctx->d_path_all) + f, f); };
     const int st = replay(ctx, plan, n, before, plain, mean_frame_ms);
-    // the device state now belongs to the path's last camera: the scene camera is set up again
-    // at its next render; the path's bin statistics reach the host with this copy
+    if (batched) return st;  // (per-camera slots: the context's setup is still the scene camera's)
+    // the device state now belongs to the path's last camera: the scene camera is set up again at
+    // its next render (whose count copy also grows the bins' capacity when a camera needed more;
+    // no copy here: waiting for an earlier one would wait for that call's frames)
     ctx->setup_key.clear();
     ++ctx->setup_gen;
     ctx->state_known = false;
-    if (!st) {
-        if (ctx->state_pending) HIP_TRY(ctx, hipEventSynchronize(ctx->state_ev));
-        HIP_TRY(ctx, hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(CamState), hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(ctx, hipEventRecord(ctx->state_ev, ctx->stream));
-        ctx->state_pending = true;
-    }
     return st;
 }
 
