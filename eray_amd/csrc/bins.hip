@@ -68,28 +68,52 @@ __global__ void __launch_bounds__(kBinWG) bin_pairs_kernel(const TriCull* __rest
     const unsigned long long stride = (unsigned long long)gridDim.x * kBinWG;
     // workgroup-uniform loop: one slot-counter atomic per workgroup and pass (a per-wave atomic on
     // the one counter serialised thousands of times)
+    __shared__ uint32_t s_face[kBinWG];  // each lane's pair's face
+    auto face_of = [&](unsigned long long j) -> uint32_t {
+        // the chunk: the last one starting at or before j (in LDS; an empty chunk never is, the next
+        // one starts at the same pair) ...
+        uint32_t cb = 0, ce = nparts;
+        while (ce - cb > 1) {
+            const uint32_t mid = (cb + ce) >> 1;
+            if (s_boff[mid] <= j) cb = mid;
+            else ce = mid;
+        }
+        // ... then, inside it, the last face whose first pair is <= j
+        const unsigned long long jl = j - s_boff[cb];
+        uint32_t lo = cb * chunk, hi = min(lo + chunk, T);
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (first_local[mid] <= jl) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo - 1;
+    };
     for (unsigned long long base = (unsigned long long)blockIdx.x * kBinWG; base < P; base += stride) {
         const unsigned long long j = base + threadIdx.x;
+        // The wave's 64 consecutive pairs belong to a run of consecutive faces: one search for the
+        // first pair's face, then 64 faces at a time each write their face index into the slots
+        // of the wave's pairs they own (a pair-per-lane search chained ~12 dependent loads).
+        const unsigned long long j0 = base + 64ull * wave, jend = min(j0 + 64ull, P);
+        if (j0 < P) {  // wave-uniform
+            uint32_t fb = face_of(j0);
+            for (unsigned long long covered = j0; covered < jend; fb += 64) {  // wave-uniform
+                const uint32_t fi = fb + lane;
+                unsigned long long a = P, b = P;  // face fi's pairs [a, b)
+                if (fi < T) {
+                    a = first(fi);
+                    b = fi + 1 < T ? first(fi + 1) : P;
+                }
+                for (unsigned long long q = max(a, j0); q < min(b, jend); ++q) s_face[64 * wave + (uint32_t)(q - j0)] = fi;
+                covered = (unsigned long long)__shfl((long long)b, 63);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
         unsigned long long m = 0;
         uint32_t key = 0, i = 0;
         if (j < P) {
-            // the chunk: the last one starting at or before j (in LDS; an empty chunk never is, the
-            // next one starts at the same pair) ...
-            uint32_t cb = 0, ce = nparts;
-            while (ce - cb > 1) {
-                const uint32_t mid = (cb + ce) >> 1;
-                if (s_boff[mid] <= j) cb = mid;
-                else ce = mid;
-            }
-            // ... then, inside it, the last face whose first pair is <= j
-            const unsigned long long jl = j - s_boff[cb];
-            uint32_t lo = cb * chunk, hi = min(lo + chunk, T);
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (first_local[mid] <= jl) lo = mid + 1;
-                else hi = mid;
-            }
-            i = lo - 1;
+            i = s_face[threadIdx.x];
             const int4 g = range[i];
             const uint32_t w = (uint32_t)(g.y - g.x + 1);
             const uint32_t c = (uint32_t)(j - first(i));
@@ -130,7 +154,8 @@ __global__ void __launch_bounds__(kBinWG) bin_scatter_kernel(const uint32_t* __r
                                                              const uint32_t* __restrict__ start,
                                                              uint32_t* __restrict__ count,
                                                              const uint32_t* __restrict__ kbegin, uint32_t nbins,
-                                                             const TriHot* __restrict__ hot, uint32_t* __restrict__ tri,
+                                                             const TriHot* __restrict__ hot, uint32_t T1,
+                                                             uint32_t* __restrict__ tri,
                                                              unsigned long long* __restrict__ mask,
                                                              TriHot* __restrict__ hot_out) {
     const uint32_t total = min(*n, cap);
@@ -139,15 +164,15 @@ __global__ void __launch_bounds__(kBinWG) bin_scatter_kernel(const uint32_t* __r
         const uint32_t pos = start[key] + atomicSub(count + key, 1u) - 1u;
         tri[pos] = f - kbegin[key / nbins];
         mask[pos] = emask[e];
-        hot_out[pos] = hot[f];
+        hot_out[pos] = hot[T1 ? f % T1 : f];  // (several cameras: face f is face f % T1 of camera f / T1)
     }
 }
 
 // The binned objects' non-empty bins -> their pixel rectangles ((~x0, x1 + 1, ~y0, y1 + 1),
 // max-reduced); the last workgroup narrows each binned object's rectangle to them, publishes its
 // bin views (none on overflow) and resets the counters.  Keys are object-major, so a workgroup's
-// 256 keys belong to a run of binned objects [k_first, k_last]: reduced in LDS, the run's two
-// ends published as partials, inner objects' unions stored whole (no contended atomics).
+// 256 keys belong to a run of binned objects [k_first, k_last]: reduced in LDS, then atomically
+// max-merged into the objects' accumulators by the workgroups that found a non-empty bin.
 constexpr uint32_t kFinSpan = 8;    // binned objects per workgroup reduced in LDS (more: atomics)
 constexpr uint32_t kFinTab = 1024;  // binned objects the last workgroup combines in LDS
 
@@ -247,7 +272,7 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t nparts, 
                                                                ObjectDesc* __restrict__ objs, uint32_t* tri,
                                                                unsigned long long* mask, TriHot* hot,
                                                                uint32_t* __restrict__ sortq, uint32_t* __restrict__ nsort,
-                                                               CamState* __restrict__ st) {
+                                                               CamState* __restrict__ st, uint32_t ncam) {
     __shared__ uint32_t s_acc[kFinSpan][4];
     __shared__ uint32_t s_tab[kFinTab][4];
     const uint32_t keys = nb * nbins;
@@ -269,17 +294,13 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t nparts, 
     }
     __syncthreads();
     if constexpr (!kFinal) queue_sort(start, b, keys, sortq, nsort);
+    // this workgroup's objects' unions into the accumulators: only workgroups with a non-empty
+    // bin, four atomics per object (a single combining workgroup reading every workgroup's
+    // partials took 28 us at 16 cameras x 32k bins)
     const uint32_t span = !kFinal && b0 < b1 ? min(k_last - k_first + 1, kFinSpan) : 0u;
-    if (threadIdx.x < span && threadIdx.x > 0 && k_first + threadIdx.x < k_last)  // inner objects: whole
-        for (int q = 0; q < 4; ++q) acc[4 * (k_first + threadIdx.x) + q] = s_acc[threadIdx.x][q];
-    if (!kFinal && threadIdx.x == 0) {
-        uint32_t* pb = part + 10 * blockIdx.x;
-        pb[0] = b0 < b1 ? k_first : ~0u;
-        pb[5] = b0 < b1 ? k_last : ~0u;
-        for (int q = 0; q < 4; ++q) {
-            pb[1 + q] = s_acc[0][q];
-            pb[6 + q] = b0 < b1 && k_last - k_first < kFinSpan ? s_acc[k_last - k_first][q] : 0u;
-        }
+    if (threadIdx.x < span && s_acc[threadIdx.x][1] != 0u) {
+        const uint32_t a[4] = {s_acc[threadIdx.x][0], s_acc[threadIdx.x][1], s_acc[threadIdx.x][2], s_acc[threadIdx.x][3]};
+        max4(acc + 4 * (k_first + threadIdx.x), a);
     }
     if (!kFinal) return;
     const bool in_lds = nb <= kFinTab;
@@ -291,15 +312,6 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t nparts, 
             }
         __syncthreads();
     }
-    for (uint32_t g = threadIdx.x; g < nparts; g += kBinWG) {
-        const uint32_t* pb = part + 10 * g;
-        for (int e = 0; e < 2; ++e) {
-            if (pb[5 * e] == ~0u) continue;
-            const uint32_t a[4] = {pb[5 * e + 1], pb[5 * e + 2], pb[5 * e + 3], pb[5 * e + 4]};
-            max4(in_lds ? s_tab[pb[5 * e]] : acc + 4 * pb[5 * e], a);
-        }
-    }
-    __threadfence();
     __syncthreads();
     const uint32_t found = *n;
     const bool overflow = found > cap;
@@ -336,10 +348,12 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t nparts, 
         *nsort = 0u;  // (bin_sort_kernel has run)
         // the most entries any setup needed since the buffers were allocated (the host grows the
         // capacity from it), and whether any overflowed
-        st->bin_entries = max(st->bin_entries, found);
-        st->bin_overflow |= overflow ? 1u : 0u;
-        st->nrect = 0u;
-        st->total_sub = 0u;  // counted by detail_list_kernel
+        for (uint32_t k = 0; k < ncam; ++k) {  // (several cameras: every camera's state)
+            st[k].bin_entries = max(st[k].bin_entries, found);
+            st[k].bin_overflow |= overflow ? 1u : 0u;
+            st[k].nrect = 0u;
+            st[k].total_sub = 0u;  // counted by detail_list_kernel
+        }
     }
 }
 
@@ -403,9 +417,14 @@ __global__ void __launch_bounds__(kBinWG) detail_list_kernel(const ObjectDesc* _
                                                              uint32_t band_stride, uint32_t bins_x, uint32_t phase,
                                                              uint32_t tiles_x, uint32_t n,
                                                              uint32_t* __restrict__ list, uint8_t* __restrict__ occ,
-                                                             uint32_t* __restrict__ total) {
+                                                             CamState* __restrict__ st) {
     __shared__ uint32_t s_cnt[kBinWG / 64];
     __shared__ uint32_t s_base;
+    // camera blockIdx.y of a multi-camera setup: its descriptors, list, occupancy and count
+    objs += (size_t)blockIdx.y * nobj;
+    list += (size_t)blockIdx.y * n;
+    occ += (size_t)blockIdx.y * (n / 4);
+    uint32_t* total = &st[blockIdx.y].total_sub;
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t row_subs = 4 * tiles_x;
@@ -475,7 +494,8 @@ void bins_free(BinBuffers& b) {
 }
 
 hipError_t bins_alloc(BinBuffers& b, uint32_t T, uint32_t nb, const uint32_t* kbegin, const uint32_t* kobj, uint32_t W,
-                      uint32_t H, uint32_t phase, uint32_t tiles_x, uint32_t rows, size_t cap, hipStream_t s) {
+                      uint32_t H, uint32_t phase, uint32_t tiles_x, uint32_t rows, size_t cap, hipStream_t s,
+                      uint32_t ncam) {
     hipError_t e = hipStreamSynchronize(s);  // the buffers may be in use by enqueued work
     if (e != hipSuccess) return e;
     bins_free(b);
@@ -500,7 +520,8 @@ hipError_t bins_alloc(BinBuffers& b, uint32_t T, uint32_t nb, const uint32_t* kb
         (e = grow(&b.dflags, b.nsub)) != hipSuccess || (e = grow(&b.dpacked, b.nsub)) != hipSuccess ||
         (e = grow(&b.dflags_light, b.nsub)) != hipSuccess || (e = grow(&b.dlight, b.nsub)) != hipSuccess ||
         (e = grow(&b.dcount, 2)) != hipSuccess ||
-        (e = grow(&b.dlist, b.nsub)) != hipSuccess || (e = grow(&b.docc, (size_t)tiles_x * subs_y)) != hipSuccess ||
+        (e = grow(&b.dlist, b.nsub * ncam)) != hipSuccess ||
+        (e = grow(&b.docc, (size_t)tiles_x * subs_y * ncam)) != hipSuccess ||
         (e = grow(&b.sortq, std::max<size_t>(keys, 1))) != hipSuccess || (e = grow(&b.nsort, 1)) != hipSuccess)
         return e;
     // counters zero between builds (each build leaves them so)
@@ -528,28 +549,31 @@ hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tile
     hipError_t e;
     const size_t keys = (size_t)b.nb * b.nbins;
     size_t tb = b.temp_bytes;
-    if (b.T) {
-        const uint32_t nparts = setup_blocks(b.T), chunk = (b.T + nparts - 1) / nparts;  // as camera_setup_kernel
+    const bool multi = sp.ncam > 1;
+    const uint32_t ncam = multi ? sp.ncam : 1u;
+    if (sp.T) {  // (a multi-camera build may set up fewer cameras than the buffers hold)
+        const uint32_t nparts = setup_blocks(sp.T), chunk = (sp.T + nparts - 1) / nparts;  // as camera_setup_kernel
         auto* k = sp.keep_all ? bin_pairs_kernel<true> : bin_pairs_kernel<false>;
-        k<<<kPairGrid, kBinWG, 0, s>>>(sp.cull, sp.range, b.first, b.boff, nparts, chunk, sp.fkey, b.T, sp.W, sp.H, sp.phase,
+        k<<<kPairGrid, kBinWG, 0, s>>>(sp.cull, sp.range, b.first, b.boff, nparts, chunk, sp.fkey, sp.T, sp.W, sp.H, sp.phase,
                                        b.bins_x, b.nbins, (uint32_t)b.cap, b.n, b.count, b.ekey, b.eface, b.emask);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     tb = b.temp_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(b.temp, tb, b.count, b.start, (int)(keys + 1), s)) != hipSuccess) return e;
     bin_scatter_kernel<<<kPairGrid, kBinWG, 0, s>>>(b.n, (uint32_t)b.cap, b.ekey, b.eface, b.emask, b.start, b.count,
-                                                    b.kbegin, b.nbins, sp.hot, b.tri, b.mask, b.hot);
+                                                    b.kbegin, b.nbins, sp.hot, multi ? sp.T1 : 0u, b.tri, b.mask,
+                                                    b.hot);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t fgrid = (uint32_t)std::max<size_t>((keys + kBinWG - 1) / kBinWG, 1);
     bins_finalize_kernel<false><<<fgrid, kBinWG, 0, s>>>(fgrid, b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase,
                                                          b.acc, b.part, b.done, b.n, (uint32_t)b.cap, b.kobj, sp.objs,
-                                                         b.tri, b.mask, b.hot, b.sortq, b.nsort, sp.state);
+                                                         b.tri, b.mask, b.hot, b.sortq, b.nsort, sp.state, ncam);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     bin_sort_kernel<<<kSortGrid, kBinWG, 0, s>>>(b.sortq, b.nsort, b.start, b.tri, b.mask, b.hot);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     bins_finalize_kernel<true><<<1, kBinWG, 0, s>>>(fgrid, b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase, b.acc,
                                                     b.part, b.done, b.n, (uint32_t)b.cap, b.kobj, sp.objs, b.tri, b.mask,
-                                                    b.hot, b.sortq, b.nsort, sp.state);
+                                                    b.hot, b.sortq, b.nsort, sp.state, ncam);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (!b.nsub) return hipSuccess;
     const uint32_t n = (uint32_t)b.nsub;
@@ -571,10 +595,9 @@ hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tile
                                s>>>(b.dlight, b.dcount, b.dlist, sp.state);
         return hipGetLastError();
     }
-    detail_list_kernel<<<(n + kBinWG - 1) / kBinWG, kBinWG, 0, s>>>(sp.objs, sp.nobj, sp.W, sp.row0, sp.rows,
-                                                                   sp.band_shift, sp.band_mask, sp.band_stride,
-                                                                   b.bins_x, b.phase, tiles_x, n, b.dlist, b.docc,
-                                                                   &sp.state->total_sub);
+    detail_list_kernel<<<dim3((n + kBinWG - 1) / kBinWG, ncam), kBinWG, 0, s>>>(
+        sp.objs, multi ? sp.nobj1 : sp.nobj, sp.W, sp.row0, sp.rows, sp.band_shift, sp.band_mask, sp.band_stride, b.bins_x,
+        b.phase, tiles_x, n, b.dlist, b.docc, sp.state);
     return hipGetLastError();
 }
 

@@ -163,6 +163,25 @@ struct eray_ctx {
     size_t bobjs_cap = 0;
     CamState* d_bstate = nullptr;
     size_t bstate_cap = 0;
+    // camera paths of scenes with binned objects: the setups of up to mc_k cameras in one
+    // multi-camera build (SetupParams::ncam), into per-camera slices of a buffer set; two sets, so
+    // that the next cameras' build (on mc_stream) runs beside the current cameras' frames
+    struct MultiSet {
+        TriCull* cull = nullptr;
+        ObjectDesc* objs = nullptr;
+        CamState* state = nullptr;
+        uint32_t* acc = nullptr;
+        int4* range = nullptr;
+        unsigned long long* area = nullptr;
+        uint32_t* fkey = nullptr;
+        BinBuffers bins;
+    };
+    MultiSet mc[2];
+    uint32_t mc_k = 0;
+    std::vector<uint64_t> mc_layout;
+    uint64_t mc_gen = 0;          // bumped whenever the multi-camera buffers are (re)allocated
+    hipStream_t mc_stream = nullptr;
+    hipEvent_t mc_fork = nullptr, mc_ready[2] = {nullptr, nullptr}, mc_free[2] = {nullptr, nullptr};
     uint8_t* d_staging = nullptr;  // eray_gather_rows' banded staging (rank 0)
     size_t staging_cap = 0;
     LaunchCtx lc{nullptr, nullptr, nullptr};  // the separate fill's stream and events
@@ -407,6 +426,15 @@ RowSpan row_span(const eray_render_params* rp) {
     return RowSpan{rp->row0, rp->rows, shift, rp->band_rows - 1u, rp->band_stride};
 }
 
+// The binned objects' first triangles and object indices (bins_alloc's key tables).
+void binned_lists(const eray_ctx* ctx, std::vector<uint32_t>* kbegin, std::vector<uint32_t>* kobj) {
+    for (uint32_t i = 0; i < ctx->objects.size(); ++i)
+        if (ctx->objects[i].T > kDirectMax) {
+            kbegin->push_back(ctx->h_objs[i].g.tri_begin);
+            kobj->push_back(i);
+        }
+}
+
 int ensure_bins(eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs) {
     const uint32_t row0 = rs.row0, rows = rs.rows;
     const uint32_t nb = binned_objects(ctx);
@@ -425,11 +453,7 @@ int ensure_bins(eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs) {
     std::vector<uint64_t> layout{T, nb, W, H, phase, rows, ctx->bin_cap, ctx->scene_gen};
     if (layout == ctx->bins_layout) return ERAY_OK;
     std::vector<uint32_t> kbegin, kobj;
-    for (uint32_t i = 0; i < ctx->objects.size(); ++i)
-        if (ctx->objects[i].T > kDirectMax) {
-            kbegin.push_back(ctx->h_objs[i].g.tri_begin);
-            kobj.push_back(i);
-        }
+    binned_lists(ctx, &kbegin, &kobj);
     HIP_TRY(ctx, bins_alloc(ctx->bins, T, nb, kbegin.data(), kobj.data(), W, H, phase, tiles_x, rows, ctx->bin_cap,
                             ctx->stream));
     ctx->bins_layout = std::move(layout);
@@ -486,6 +510,99 @@ int enqueue_setup(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint32_t H,
     sp.keep_all = keep_all ? 1u : 0u;
     HIP_TRY(ctx, launch_camera_setup(sp, ctx->stream));
     if (sp.binned) HIP_TRY(ctx, launch_bins_build(sp, ctx->bins, (W + 63) / 64, ordered, ctx->stream));
+    return ERAY_OK;
+}
+
+// The multi-camera setup buffers (camera paths of scenes with binned objects) for the current
+// bins layout (ensure_bins ran first): two sets of mc_k copies of every per-camera array, camera
+// k's descriptors initialised with the scene's; reallocated when the layout or the scene changes
+// (mc_gen keys the captured path graphs).
+int ensure_multi(eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs) {
+    // cameras per build: the chain's kernels are latency bound at tens of thousands of faces (16
+    // cameras share one chain), work bound at millions (fewer: the buffers grow with K x faces)
+    const uint32_t K = std::max(1u, std::min(16u, (1u << 22) / std::max(ctx->total_tris, 1u)));
+    std::vector<uint64_t> layout = ctx->bins_layout;
+    layout.push_back(ctx->scene_gen);
+    if (layout == ctx->mc_layout) return ERAY_OK;
+    if (!ctx->mc_stream) {
+        HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->mc_stream, hipStreamNonBlocking));
+        for (hipEvent_t* ev : {&ctx->mc_fork, &ctx->mc_ready[0], &ctx->mc_ready[1], &ctx->mc_free[0], &ctx->mc_free[1]})
+            HIP_TRY(ctx, hipEventCreateWithFlags(ev, hipEventDisableTiming));
+    }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->mc_stream));
+    ctx->mc_layout.clear();
+    const uint32_t T = ctx->total_tris, nobj = (uint32_t)ctx->objects.size(), nb = binned_objects(ctx);
+    const size_t t = (size_t)K * (T ? T : 1);
+    const size_t acc_words = 4 * (size_t)K * nobj + 1 + 10 * (size_t)kSetupMaxBlocks;
+    // camera k's copy of binned object j: key k * nb + j, its faces from k * T + tri_begin
+    std::vector<uint32_t> kbegin, kobj, mbegin, mobj;
+    binned_lists(ctx, &kbegin, &kobj);
+    for (uint32_t k = 0; k < K; ++k)
+        for (uint32_t j = 0; j < nb; ++j) {
+            mbegin.push_back(k * T + kbegin[j]);
+            mobj.push_back(k * nobj + kobj[j]);
+        }
+    for (auto& m : ctx->mc) {
+        for (void* b : {(void*)m.cull, (void*)m.objs, (void*)m.state, (void*)m.acc, (void*)m.range, (void*)m.area,
+                        (void*)m.fkey})
+            if (b) HIP_TRY(ctx, hipFree(b));
+        m.cull = nullptr;
+        m.objs = nullptr;
+        m.state = nullptr;
+        m.acc = nullptr;
+        m.range = nullptr;
+        m.area = nullptr;
+        m.fkey = nullptr;
+        HIP_TRY(ctx, hipMalloc((void**)&m.cull, sizeof(TriCull) * t));
+        HIP_TRY(ctx, hipMalloc((void**)&m.objs, sizeof(ObjectDesc) * K * (nobj ? nobj : 1)));
+        HIP_TRY(ctx, hipMalloc((void**)&m.state, sizeof(CamState) * K));
+        HIP_TRY(ctx, hipMalloc((void**)&m.acc, 4 * acc_words));
+        HIP_TRY(ctx, hipMalloc((void**)&m.range, sizeof(int4) * t));
+        HIP_TRY(ctx, hipMalloc((void**)&m.area, sizeof(unsigned long long) * t));
+        HIP_TRY(ctx, hipMalloc((void**)&m.fkey, sizeof(uint32_t) * t));
+        HIP_TRY(ctx, hipMemsetAsync(m.acc, 0, 4 * acc_words, ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(m.state, 0, sizeof(CamState) * K, ctx->stream));
+        for (uint32_t k = 0; k < K && nobj; ++k)  // (each setup rewrites the rectangles and bin views)
+            HIP_TRY(ctx, hipMemcpyAsync(m.objs + (size_t)k * nobj, ctx->d_objs, sizeof(ObjectDesc) * nobj,
+                                        hipMemcpyDeviceToDevice, ctx->stream));
+        HIP_TRY(ctx, bins_alloc(m.bins, K * T, K * nb, mbegin.data(), mobj.data(), W, H, rs.row0 % kBinH, (W + 63) / 64,
+                                rs.rows, K * ctx->bin_cap, ctx->stream, K));
+    }
+    ctx->mc_layout = std::move(layout);
+    ctx->mc_k = K;
+    ++ctx->mc_gen;
+    return ERAY_OK;
+}
+
+// Enqueues on `s` the setups of the `ncam` cameras at d_cams (ncam <= mc_k) into buffer set `m`:
+// camera k's culling records at m.cull + k T, descriptors at m.objs + k nobj, state m.state + k,
+// detail list m.bins.dlist + k nsub (occupancy m.bins.docc + k nsub / 4).
+int enqueue_multi_setup(eray_ctx* ctx, eray_ctx::MultiSet& m, const CamDev* d_cams, uint32_t ncam, uint32_t W,
+                        uint32_t H, const RowSpan& rs, hipStream_t s) {
+    const uint32_t T = ctx->total_tris, nobj = (uint32_t)ctx->objects.size();
+    SetupParams sp = setup_params(ctx, d_cams, W, H, rs);
+    sp.ncam = ncam;
+    sp.T1 = T;
+    sp.nobj1 = nobj;
+    sp.nb1 = binned_objects(ctx);
+    sp.T = ncam * T;
+    sp.nobj = ncam * nobj;
+    sp.cull = m.cull;
+    sp.objs = m.objs;
+    sp.state = m.state;
+    sp.done = m.acc;
+    sp.part = m.acc + 1;
+    sp.acc = m.acc + 1 + 10 * (size_t)kSetupMaxBlocks;
+    sp.range = m.range;
+    sp.area = m.area;
+    sp.fkey = m.fkey;
+    sp.bins_x = m.bins.bins_x;
+    sp.phase = m.bins.phase;
+    sp.first_local = m.bins.first;
+    sp.boff = m.bins.boff;
+    HIP_TRY(ctx, launch_camera_setup(sp, s));
+    HIP_TRY(ctx, launch_bins_build(sp, m.bins, (W + 63) / 64, false, s));
     return ERAY_OK;
 }
 
@@ -635,6 +752,16 @@ int eray_ctx_destroy(eray_ctx* ctx) {
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
     if (ctx->own_stream) hipStreamSynchronize(ctx->own_stream);
     bins_free(ctx->bins);
+    if (ctx->mc_stream) hipStreamSynchronize(ctx->mc_stream);
+    for (auto& m : ctx->mc) {
+        bins_free(m.bins);
+        for (void* b : {(void*)m.cull, (void*)m.objs, (void*)m.state, (void*)m.acc, (void*)m.range, (void*)m.area,
+                        (void*)m.fkey})
+            if (b) hipFree(b);
+    }
+    for (hipEvent_t ev : {ctx->mc_fork, ctx->mc_ready[0], ctx->mc_ready[1], ctx->mc_free[0], ctx->mc_free[1]})
+        if (ev) hipEventDestroy(ev);
+    if (ctx->mc_stream) hipStreamDestroy(ctx->mc_stream);
     void* bufs[] = {ctx->d_hot,   ctx->d_shade, ctx->d_cull,  ctx->d_raw,  ctx->d_objs,  ctx->d_lights,
                     ctx->d_prog,  ctx->d_cam,   ctx->d_state, ctx->d_acc,  ctx->d_begin, ctx->d_range,
                     ctx->d_area,  ctx->d_fkey,  ctx->d_path,  ctx->d_path_all, ctx->d_staging,
@@ -1433,7 +1560,48 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
         HIP_TRY(ctx, launch_frame(ctx, q));
         return ERAY_OK;
     };
+    // scenes with binned objects: the setups of up to mc_k cameras at once (one chain of
+    // kernels for all of them, ensure_multi), then their frames, each from its camera's slices
+    const bool multi = !batched && binned_objects(ctx) > 0;
+    const RowSpan rs = row_span(rp);
+    if (multi)
+        if (int st = ensure_multi(ctx, W, H, rs)) return st;
+    // frame `slot` of a run of `count` cameras at `cams` (f: its index in the call, its ring slot):
+    // batch b = slot / K of the run is built into set b % 2; the first batch's build on the main
+    // stream, every later one on mc_stream while the previous batch's frames render (it waits for
+    // the frames of batch b - 2, the set's previous users), the frames wait for their build
+    auto multi_frame = [&](const CamDev* cams, uint32_t slot, uint32_t count, uint32_t f) -> int {
+        const uint32_t K = ctx->mc_k, k = slot % K, b = slot / K;
+        auto& m = ctx->mc[b & 1u];
+        if (k == 0) {
+            if (b == 0) {
+                if (int st = enqueue_multi_setup(ctx, m, cams, std::min(K, count), W, H, rs, ctx->stream)) return st;
+                HIP_TRY(ctx, hipEventRecord(ctx->mc_fork, ctx->stream));
+            } else {
+                HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->mc_ready[b & 1u], 0));
+            }
+            if ((b + 1) * K < count) {  // the next batch's build, beside this batch's frames
+                auto& m2 = ctx->mc[(b + 1) & 1u];
+                HIP_TRY(ctx, hipStreamWaitEvent(ctx->mc_stream, b == 0 ? ctx->mc_fork : ctx->mc_free[(b + 1) & 1u], 0));
+                if (int st = enqueue_multi_setup(ctx, m2, cams + (b + 1) * K, std::min(K, count - (b + 1) * K), W, H, rs,
+                                                 ctx->mc_stream))
+                    return st;
+                HIP_TRY(ctx, hipEventRecord(ctx->mc_ready[(b + 1) & 1u], ctx->mc_stream));
+            }
+        }
+        const uint32_t nsub = (uint32_t)m.bins.nsub;
+        FrameParams q = ring_frames(p, r, f, 1);
+        q.cam_state = m.state + k;
+        q.cull = m.cull + (size_t)k * T;
+        q.objects = m.objs + (size_t)k * nobj;
+        q.detail_list = m.bins.dlist + (size_t)k * nsub;
+        q.detail_occ = m.bins.docc + (size_t)k * (nsub / 4);
+        HIP_TRY(ctx, launch_frame(ctx, q));
+        if (k == K - 1 || slot + 1 == count) HIP_TRY(ctx, hipEventRecord(ctx->mc_free[b & 1u], ctx->stream));
+        return ERAY_OK;
+    };
     auto frame = [&](const CamDev* cam, uint32_t f) -> int {
+        if (multi) return multi_frame(cam, 0, 1, f);
         if (batched) {
             const Ring keep = r;
             r.per_launch = 1;
@@ -1446,6 +1614,7 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
         return ERAY_OK;
     };
     auto body = [&](uint32_t f, uint32_t count) {
+        if (multi) return multi_frame(ctx->d_path, f, count, f);
         return batched ? batch_frame(ctx->d_path, f, count, f) : frame(ctx->d_path + f, f);
     };
     std::vector<unsigned char> key = ring_key(params_key(p, batched ? 2 : 1), r);
@@ -1457,6 +1626,9 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
     // capacity) must never replay a graph of the old buffers, even if some addresses recur
     key.insert(key.end(), reinterpret_cast<const unsigned char*>(&ctx->bins_gen),
                reinterpret_cast<const unsigned char*>(&ctx->bins_gen) + sizeof ctx->bins_gen);
+    const uint64_t mc_gen = multi ? ctx->mc_gen : 0u;  // (likewise the multi-camera buffers)
+    key.insert(key.end(), reinterpret_cast<const unsigned char*>(&mc_gen),
+               reinterpret_cast<const unsigned char*>(&mc_gen) + sizeof mc_gen);
     Plan plan;
     if (int st = ensure_plan(ctx, key, n, body, &plan)) return st;
     auto before = [&](uint32_t first, uint32_t count) -> int {
@@ -1467,7 +1639,7 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
     };
     auto plain = [&](uint32_t f) { return frame((one_chunk ? ctx->d_path : ctx->d_path_all) + f, f); };
     const int st = replay(ctx, plan, n, before, plain, mean_frame_ms);
-    if (batched) return st;  // (per-camera slots: the context's setup is still the scene camera's)
+    if (batched || multi) return st;  // (per-camera slots: the context's setup is still the scene camera's)
     // the device state now belongs to the path's last camera: the scene camera is set up again at
     // its next render (whose count copy also grows the bins' capacity when a camera needed more;
     // no copy here: waiting for an earlier one would wait for that call's frames)

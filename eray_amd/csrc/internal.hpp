@@ -309,6 +309,12 @@ struct SetupParams {
     // its jittered anti-aliasing rays reach, bin masks of the pixels any of whose rays may pass
     // (face_rect.hpp bin_pixels_jittered)
     uint32_t keep_all;
+    // Several cameras in one setup (ncam > 1: camera paths of scenes with binned objects): the
+    // cameras sp.cam[0 .. ncam), T = ncam * T1 "faces" (face i is face i % T1 of camera i / T1:
+    // its culling record, bin rectangle and pairs), nobj = ncam * nobj1 descriptors (camera k's
+    // copy of object o at k * nobj1 + o), ncam * nb1 binned objects (camera k's copy of binned
+    // object j is k * nb1 + j), ncam CamStates; the bins and their detail lists per camera.
+    uint32_t ncam, T1, nobj1, nb1;
     const ObjectDesc* objs_src;  // batched setups: the scene's descriptors, copied into each slot
     // binned faces' first (face, bin) pair: the exclusive scan of `area`, as each chunk
     // workgroup's own scan (first_local) plus its chunk's offset boff[b] (kSetupMaxBlocks + 1
@@ -379,9 +385,10 @@ struct BinBuffers {
 };
 // (Re)allocates `b` for T triangles, nb binned objects (kbegin / kobj: host arrays), a W x H
 // camera, row phase and `rows` rendered rows, entry capacity `cap` (synchronises `s` when it
-// reallocates).
+// reallocates); the detail lists of `ncam` cameras (a multi-camera setup, SetupParams::ncam).
 hipError_t bins_alloc(BinBuffers& b, uint32_t T, uint32_t nb, const uint32_t* kbegin, const uint32_t* kobj, uint32_t W,
-                      uint32_t H, uint32_t phase, uint32_t tiles_x, uint32_t rows, size_t cap, hipStream_t s);
+                      uint32_t H, uint32_t phase, uint32_t tiles_x, uint32_t rows, size_t cap, hipStream_t s,
+                      uint32_t ncam = 1);
 void bins_free(BinBuffers& b);
 // After launch_camera_setup: the bins of the setup's camera, the binned objects' rectangles
 // narrowed to their non-empty bins and their bin views in the descriptors (or none when the

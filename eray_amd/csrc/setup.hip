@@ -100,8 +100,16 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp, 
     const uint32_t tid = threadIdx.x;
     const uint32_t chunk = kMode == 3 ? sp.T : (sp.T + gridDim.x - 1) / gridDim.x;
     const uint32_t lo = kMode == 3 ? 0u : min(blockIdx.x * chunk, sp.T), hi = min(lo + chunk, sp.T);
-    const uint32_t o_first = lo < hi ? object_of(sp.obj_begin, sp.nobj, lo) : 0u;
-    const uint32_t o_last = lo < hi ? object_of(sp.obj_begin, sp.nobj, hi - 1) : 0u;
+    // several cameras at once (sp.ncam > 1, binned scenes' camera paths): face i is face i % T1 of
+    // camera i / T1, object k * nobj1 + o of camera k is that camera's copy of object o (SetupParams)
+    const bool multi = kMode != 3 && sp.ncam > 1;
+    auto vobject = [&](uint32_t i) -> uint32_t {
+        if (!multi) return object_of(sp.obj_begin, sp.nobj, i);
+        const uint32_t k = i / sp.T1;
+        return k * sp.nobj1 + object_of(sp.obj_begin, sp.nobj1, i - k * sp.T1);
+    };
+    const uint32_t o_first = lo < hi ? vobject(lo) : 0u;
+    const uint32_t o_last = lo < hi ? vobject(hi - 1) : 0u;
     for (uint32_t j = tid; j < kSpan; j += kSetupWG)
         for (int k = 0; k < 4; ++k) s_acc[j][k] = 0u;
     __syncthreads();
@@ -112,9 +120,10 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp, 
         if (i < hi) {
             // (keep_all: the general tracer's viewport, jittered rays reach -1/W and -1/H)
             const double xa = sp.keep_all ? -2.0 / (double)sp.W : 0.0, ya = sp.keep_all ? -2.0 / (double)sp.H : 0.0;
-            const TriCull c = cull_record(sp.hot[i], cam, xa, 1.0, ya, 1.0);
+            const uint32_t kc = multi ? i / sp.T1 : 0u;  // (the face's camera)
+            const TriCull c = cull_record(sp.hot[i - kc * sp.T1], multi ? sp.cam[kc] : cam, xa, 1.0, ya, 1.0);
             sp.cull[i] = c;
-            const uint32_t obj = object_of(sp.obj_begin, sp.nobj, i);
+            const uint32_t obj = vobject(i);
             int32_t r[4];
             const bool any = face_rect(c, sp.W, sp.H, r, s_poly + tid, kSetupWG, xa, ya);
             if (any) {
@@ -124,7 +133,8 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp, 
                 else max4(sp.acc + 4 * obj, a);  // (a workgroup spanning very many objects)
             }
             if (sp.range) {  // bins.hip: the face's bin rectangle, if its object is binned
-                const uint32_t k = sp.objkey[obj];
+                uint32_t k = sp.objkey[multi ? obj % sp.nobj1 : obj];  // (camera kc's copy: kc * nb1 + k)
+                if (multi && k != ~0u) k += kc * sp.nb1;
                 int4 g = make_int4(1, 0, 1, 0);
                 if (k != ~0u && any) {
                     // bin row of camera row y: (y + kBinH - phase) / kBinH
@@ -262,6 +272,10 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp, 
     }
     __syncthreads();
     if (tid != 0) return;
+    if (multi) {  // (binned scenes: bins.hip narrows the rectangles and lists the detail sub-blocks)
+        for (uint32_t k = 0; k < sp.ncam; ++k) sp.state[k].cam = sp.cam[k];
+        return;
+    }
     CamState& st = *sp.state;
     st.cam = cam;
     if (sp.binned) return;  // bins.hip narrows the rectangles and lists the detail sub-blocks
