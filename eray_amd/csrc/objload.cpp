@@ -8,6 +8,7 @@
 // handling, not part of the per-frame path, but a 1M-face mesh should load in a fraction of a
 // second (the Python statement takes seconds).
 #include <cerrno>
+#include <charconv>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -75,6 +76,14 @@ float parse_f32(const Tok& t, size_t line) {
         ok = ok && q == e;
     }
     if (!ok) parse_fail(line, "Failed to parse coords, should be an f32: " + t.str());
+    // std::from_chars is correctly rounded like strtof (and several times faster); a leading '+'
+    // is Rust's, not from_chars', and out-of-range values (inf / 0 in Rust) go to strtof
+    {
+        const char* b = t.b + (*t.b == '+' ? 1 : 0);
+        float v;
+        const auto res = std::from_chars(b, t.e, v);
+        if (res.ec == std::errc() && res.ptr == t.e) return v;
+    }
     char buf[128];
     std::string big;
     const size_t n = (size_t)(t.e - t.b);
@@ -200,10 +209,14 @@ extern "C" int eray_obj_load(const char* path, eray_obj_mesh* out) {
     FILE* f = std::fopen(path, "rb");
     if (!f) return eray_internal_error(nullptr, ERAY_E_IO, (std::string("cannot read ") + path).c_str());
     std::vector<char> data;
-    char chunk[1 << 16];
-    size_t got;
-    while ((got = std::fread(chunk, 1, sizeof chunk, f)) > 0) data.insert(data.end(), chunk, chunk + got);
-    const bool err = std::ferror(f) != 0;
+    bool err = std::fseek(f, 0, SEEK_END) != 0;
+    const long size = err ? -1L : std::ftell(f);
+    err = err || size < 0 || std::fseek(f, 0, SEEK_SET) != 0;
+    if (!err) {  // the whole file in one read
+        data.resize((size_t)size);
+        err = std::fread(data.data(), 1, data.size(), f) != data.size();
+    }
+    err = err || std::ferror(f) != 0;
     std::fclose(f);
     if (err) return eray_internal_error(nullptr, ERAY_E_IO, (std::string("cannot read ") + path).c_str());
     Mesh m;
