@@ -183,6 +183,8 @@ SIGNATURES = {
 # Diagnostics exported beside the header's API (not part of include/eray_hip.h).
 DEBUG_SIGNATURES = {
     "eray_debug_bin_stats": (C.c_int, [_P, _U, C.POINTER(C.c_uint64)]),
+    "eray_debug_bin_dump": (C.c_int, [_P, _U, _U, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64), _U,
+                                      C.POINTER(C.c_uint32)]),
     "eray_debug_set_bin_capacity": (C.c_int, [_P, C.c_uint64]),
     "eray_debug_bin_capacity": (C.c_uint64, [_P]),
     "eray_debug_setup_state": (C.c_int, [_P, _U, _P, C.POINTER(C.c_int32)]),

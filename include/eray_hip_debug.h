@@ -1,0 +1,44 @@
+/* eray_hip_debug.h — test-only diagnostics exported by liberay_hip.so.
+ *
+ * Not part of the drop-in boundary (include/eray_hip.h): none of these replaces a reference
+ * interface, and none is called by the library's own paths.  They exist for tests/ and scripts/:
+ * each SYNCHRONISES the context's stream and copies device state to the host, so no production
+ * caller should use them.  Status codes as in eray_hip.h.
+ */
+#ifndef ERAY_HIP_DEBUG_H
+#define ERAY_HIP_DEBUG_H
+
+#include "eray_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* The screen bins of object `index` as built by the last setup: out[0] bins, out[1] entries,
+ * out[2] (face, pixel) pairs, out[3] most entries in one bin, out[4] non-empty bins, out[5] most
+ * pairs in one bin, out[6..9] the object's pixel rectangle, out[10] the fullest bin, out[11] /
+ * out[12] bins of more than 64 / 192 entries (13 words). */
+int eray_debug_bin_stats(eray_ctx* ctx, uint32_t index, uint64_t* out);
+/* The entries of bin `bin` of object `index` (faces relative to the object, pixel masks), at most
+ * `cap`; *n = the bin's entry count. */
+int eray_debug_bin_dump(eray_ctx* ctx, uint32_t index, uint32_t bin, uint32_t* tri, uint64_t* mask, uint32_t cap,
+                        uint32_t* n);
+/* Sets the bins' entry capacity (reallocated at the next setup; overflow and growth tests). */
+int eray_debug_set_bin_capacity(eray_ctx* ctx, uint64_t entries);
+uint64_t eray_debug_bin_capacity(const eray_ctx* ctx);
+/* The last setup's device state (176 B) and object `index`'s pixel rectangle. */
+int eray_debug_setup_state(eray_ctx* ctx, uint32_t index, void* state_out, int32_t* rect_out);
+/* The multi-GPU gathers' rank-0 steps for N ranks simulated on one GPU (staging: the N ranks'
+ * padded local PPM blocks): the band reorder, the coded transport's decode, the scene-camera
+ * gather's pack + assemble. */
+int eray_debug_unband(eray_ctx* ctx, const uint8_t* staging, uint8_t* frame, uint32_t height, uint32_t width,
+                      uint32_t band_rows, uint32_t nranks);
+int eray_debug_coded_unband(eray_ctx* ctx, const uint8_t* staging, uint8_t* frame, uint32_t height, uint32_t width,
+                            uint32_t band_rows, uint32_t nranks);
+int eray_debug_scene_gather(eray_ctx* ctx, const uint8_t* staging, uint8_t* frame, uint32_t height, uint32_t width,
+                            uint32_t band_rows, uint32_t nranks);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ERAY_HIP_DEBUG_H */
