@@ -1220,6 +1220,9 @@ int ensure_graph(eray_ctx* ctx, std::vector<unsigned char> key, uint32_t n, Body
     }
     hipGraphExec_t exec = nullptr;
     if (e == hipSuccess) e = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
+    // the executable's packets and arguments go to the device now, not at its first launch (a
+    // plan prepared ahead of a timed loop otherwise pays ~20 us at its first replay)
+    if (e == hipSuccess) e = hipGraphUpload(exec, ctx->stream);
     if (e != hipSuccess) {
         if (g) hipGraphDestroy(g);
         return set_error(ctx, ERAY_E_HIP, "frame graph capture: %s", hipGetErrorString(e));
@@ -1531,7 +1534,17 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
                                 hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipEventRecord(ctx->path_ev[hb], ctx->stream));
     const bool batched = batch_setup_ok(ctx);
-    if (!batched) r.per_launch = 1;  // a setup (screen bins) per frame: one frame per launch
+    // scenes with binned objects: the setups of up to mc_k cameras at once (one chain of
+    // kernels for all of them, ensure_multi), then their frames, each from its camera's slices
+    const bool multi = !batched && binned_objects(ctx) > 0;
+    const RowSpan rs = row_span(rp);
+    if (multi)
+        if (int st = ensure_multi(ctx, W, H, rs)) return st;
+    if (multi) {  // frames in flight within one multi-camera build: per_launch divides mc_k
+        while (ctx->mc_k % r.per_launch) r.per_launch /= 2;
+    } else if (!batched) {
+        r.per_launch = 1;  // a setup (screen bins) per frame: one frame per launch
+    }
     const uint32_t T = ctx->total_tris, nobj = (uint32_t)ctx->objects.size();
     if (batched) {
         if (int st = ensure(ctx, &ctx->d_bcull, &ctx->bcull_cap, (size_t)kGraphFrames * T)) return st;
@@ -1560,16 +1573,12 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
         HIP_TRY(ctx, launch_frame(ctx, q));
         return ERAY_OK;
     };
-    // scenes with binned objects: the setups of up to mc_k cameras at once (one chain of
-    // kernels for all of them, ensure_multi), then their frames, each from its camera's slices
-    const bool multi = !batched && binned_objects(ctx) > 0;
-    const RowSpan rs = row_span(rp);
-    if (multi)
-        if (int st = ensure_multi(ctx, W, H, rs)) return st;
     // frame `slot` of a run of `count` cameras at `cams` (f: its index in the call, its ring slot):
     // batch b = slot / K of the run is built into set b % 2; the first batch's build on the main
     // stream, every later one on mc_stream while the previous batch's frames render (it waits for
-    // the frames of batch b - 2, the set's previous users), the frames wait for their build
+    // the frames of batch b - 2, the set's previous users), the frames wait for their build;
+    // frames in flight: the launch of slot s (s % per_launch == 0) renders slots [s, s + n) of
+    // the batch (per_launch divides K, so a launch never spans two builds), each from its slices
     auto multi_frame = [&](const CamDev* cams, uint32_t slot, uint32_t count, uint32_t f) -> int {
         const uint32_t K = ctx->mc_k, k = slot % K, b = slot / K;
         auto& m = ctx->mc[b & 1u];
@@ -1589,15 +1598,18 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
                 HIP_TRY(ctx, hipEventRecord(ctx->mc_ready[(b + 1) & 1u], ctx->mc_stream));
             }
         }
-        const uint32_t nsub = (uint32_t)m.bins.nsub;
-        FrameParams q = ring_frames(p, r, f, 1);
+        if (slot % r.per_launch) return ERAY_OK;  // rendered by the launch of slot - slot % per_launch
+        const uint32_t nsub = (uint32_t)m.bins.nsub, nf = std::min(r.per_launch, count - slot);
+        FrameParams q = ring_frames(p, r, f, nf);
         q.cam_state = m.state + k;
         q.cull = m.cull + (size_t)k * T;
         q.objects = m.objs + (size_t)k * nobj;
         q.detail_list = m.bins.dlist + (size_t)k * nsub;
         q.detail_occ = m.bins.docc + (size_t)k * (nsub / 4);
+        q.dev_slots = nf > 1 ? 1u : 0u;
+        q.dlist_stride = nf > 1 ? nsub : 0u;
         HIP_TRY(ctx, launch_frame(ctx, q));
-        if (k == K - 1 || slot + 1 == count) HIP_TRY(ctx, hipEventRecord(ctx->mc_free[b & 1u], ctx->stream));
+        if (k + nf >= K || slot + nf >= count) HIP_TRY(ctx, hipEventRecord(ctx->mc_free[b & 1u], ctx->stream));
         return ERAY_OK;
     };
     auto frame = [&](const CamDev* cam, uint32_t f) -> int {

@@ -214,9 +214,12 @@ struct FrameParams {
     // Frames in flight: one launch renders `nframes` (>= 1) independent frames, its workgroups
     // dealt round-robin over them (frame_kernel).  Frame f writes out_* + f * *_stride (bytes,
     // multiples of 16) and, with dev_slots, reads the batched per-camera setup of slot f
-    // (cam_state + f, cull + f * total_tris, objects + f * nobj: launch_camera_setup_batch).
+    // (cam_state + f, cull + f * total_tris, objects + f * nobj: launch_camera_setup_batch) and,
+    // for scenes with binned objects (the multi-camera setup), its detail list at detail_list +
+    // f * dlist_stride and occupancy at detail_occ + f * dlist_stride / 4.
     uint32_t nframes;
     uint32_t dev_slots;
+    uint32_t dlist_stride;
     uint64_t rgb_stride, ppm_stride, face_stride;
 };
 

@@ -1228,15 +1228,15 @@ __device__ __forceinline__ bool inside(const SubRect& r, int32_t sx, int32_t sy)
 // The background of the non-detail sub-blocks: fill workgroup f of nf strides over the 64 x 4
 // blocks (shared by the frame kernel's fill roles and fill_kernel).
 template <bool kDev>
-__device__ __forceinline__ void fill_blocks(const FrameParams& p, const FrameOut& o, const CamState* cs, uint32_t f, uint32_t nf,
-                                            uint32_t wave,
+__device__ __forceinline__ void fill_blocks(const FrameParams& p, const FrameOut& o, const CamState* cs,
+                                            const uint8_t* detail_occ, uint32_t f, uint32_t nf, uint32_t wave,
                                             uint32_t lane, bool aligned) {
     constexpr uint32_t nwaves = kWG / 64;
     const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
     const uint32_t fstride = nf * nwaves;
     uint32_t occ = 0;  // detail list: lane i holds the occupancy of this wave's i-th next block
     uint32_t it = 0;
-    const uint32_t nrect = p.detail_occ ? 0u : frame_nrect<kDev>(p, cs);
+    const uint32_t nrect = detail_occ ? 0u : frame_nrect<kDev>(p, cs);
     // block coordinates advance incrementally (no integer division per block)
     const uint32_t first = wave * nf + f, step_y = fstride / p.tiles_x, step_x = fstride - step_y * p.tiles_x;
     uint32_t by = first / p.tiles_x, bx = first - by * p.tiles_x;
@@ -1250,10 +1250,10 @@ __device__ __forceinline__ void fill_blocks(const FrameParams& p, const FrameOut
             }
         }
         uint32_t mask = 0;  // detail sub-blocks of this block
-        if (p.detail_occ) {  // one load per 64 blocks, not a dependent load per block
+        if (detail_occ) {  // one load per 64 blocks, not a dependent load per block
             if ((it & 63u) == 0) {
                 const uint32_t b = blk + lane * fstride;
-                occ = b < nblk ? p.detail_occ[b] : 0u;
+                occ = b < nblk ? detail_occ[b] : 0u;
             }
             mask = (uint32_t)__builtin_amdgcn_readlane((int)occ, (int)(it & 63u));
         }
@@ -1282,9 +1282,10 @@ __device__ __forceinline__ void fill_frames(const FrameParams& p, uint32_t q, ui
                                             bool aligned) {
     const uint32_t F = p.nframes, roles = max(nf, F);
     for (uint32_t v = q; v < roles; v += nf) {
-        const uint32_t fr = v % F;
-        fill_blocks<kDev>(p, frame_out(p, fr), p.cam_state + (p.dev_slots ? fr : 0u), v / F, (roles - fr + F - 1) / F,
-                          wave, lane, aligned);
+        const uint32_t fr = v % F, slot = p.dev_slots ? fr : 0u;
+        const uint8_t* occ = p.detail_occ ? p.detail_occ + (size_t)slot * (p.dlist_stride / 4) : nullptr;
+        fill_blocks<kDev>(p, frame_out(p, fr), p.cam_state + slot, occ, v / F, (roles - fr + F - 1) / F, wave, lane,
+                          aligned);
     }
 }
 
@@ -1373,12 +1374,13 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
             const uint32_t slot = p.dev_slots ? fr : 0u;
             const ObjectDesc* objs = h_objects + (size_t)slot * nobj;
             const TriCull* culls = h_cull ? h_cull + (size_t)slot * h_total_tris : nullptr;
-            const uint32_t nrect = p.detail_list ? 0u : frame_nrect<kDev>(p, cs);
+            const uint32_t* dlist = p.detail_list ? p.detail_list + (size_t)slot * p.dlist_stride : nullptr;
+            const uint32_t nrect = dlist ? 0u : frame_nrect<kDev>(p, cs);
             const CamDev cam = frame_camera<kDev>(p, cs);
             // detail sub-block j (enumeration order) -> sub-block coordinates
             auto locate = [&](uint32_t j, int32_t& sx, int32_t& sy) {
-                if (p.detail_list) {
-                    const uint32_t e = p.detail_list[j];
+                if (dlist) {
+                    const uint32_t e = dlist[j];
                     sx = (int32_t)(e & 0xffffu);
                     sy = (int32_t)(e >> 16);
                     return;

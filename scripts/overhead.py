@@ -19,10 +19,12 @@ mesh = load_obj_file(os.path.join(ROOT, "objects", "cube.obj"))
 ctx = capi.Context(0)
 torch.cuda.init()
 sc = MainScene(ctx, *mesh, W, H, texture=1024, fov=frame_camera_fov(W, H))
-rgb = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
-ppm = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
-kw = dict(out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr())
-for K in (1, 2, 5, 20, 64, 200):
+F = ctx.frames_per_launch(W, H, slots=64)
+rgb = torch.empty((F, H, W, 3), dtype=torch.float32, device="cuda")
+ppm = torch.empty((F, H, W, 3), dtype=torch.uint8, device="cuda")
+kw = dict(out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr(), ring=capi.frame_ring(F, H, W, F))
+print(f"frames per launch {F}")
+for K in (1, 2, 5, 8, 16, 20, 24, 64, 200):
     ctx.render_frames(K, W, H, prepare_only=True, **kw)
     ctx.render_frames(K, W, H, **kw)
     torch.cuda.synchronize()
@@ -50,3 +52,7 @@ for _ in range(200):
     torch.cuda.synchronize()
     t.append(time.perf_counter() - t0)
 print(f"idle synchronize {np.median(t) * 1e6:.2f} us")
+# device time of the 20-frame call (HIP events on the library's stream) vs its wall time
+for K in (20, 200):
+    d = np.median([ctx.render_frames(K, W, H, timed=True, **kw) for _ in range(10)]) * 1e3 * K
+    print(f"K={K}: device {d:.1f} us (events around the graph launches)")

@@ -152,6 +152,45 @@ def test_camera_path_ring_every_slot_is_its_camera(gpu, cube, per_launch):
         sc.close()
 
 
+@pytest.mark.parametrize("per_launch", [0, 2, 8])
+def test_binned_camera_path_ring_every_slot_is_its_camera(gpu, standin70k_ring, per_launch):
+    """A moving camera over a binned 70k-face mesh, several frames per launch: the frames of one
+    launch read their own cameras' slices of a multi-camera setup (culling records, descriptors,
+    detail lists, occupancy).  Paths of several builds (16 cameras each), a graph chunk plus a
+    remainder, a partial build, and a 3-rank band share."""
+    W, H = 480, 270
+    sc = MainScene(gpu, *standin70k_ring, W, H, texture=256, fov=(16.0, 9.0))
+    # (on the view axis: a loaded mesh's box is the degenerate one at the origin, object.rs:306-315)
+    cams = [capi.make_camera((0.0, 0.0, 4.6 + 1.1 * math.sin(0.3 * k)), (16.0, 9.0), W, 1.0 + 0.2 * math.cos(0.5 * k))
+            for k in range(70)]
+    scene_cam = capi.make_camera((0.0, 0.0, 5.0), (16.0, 9.0), W, 1.0)
+    try:
+        for split in (None, (2, 3)):
+            kw, rows = {}, H
+            if split:
+                sp = band_split(split[0], split[1], H)
+                kw = dict(row0=sp["row0"], rows=sp["rows"], band_rows=sp["band_rows"], band_stride=sp["band_stride"])
+                rows = sp["rows"]
+            ring = Ring(gpu, 8, rows, W)
+            try:
+                for n in ((70, 37) if split is None else (21,)):
+                    refs = {}
+                    for k in range(n - 8, n):
+                        gpu.set_camera(cams[k])
+                        refs[k % 8] = single(gpu, W, H, flags=capi.RENDER_BRUTE_FORCE, **kw)
+                    assert len({r[1].tobytes() for r in refs.values()}) == 8
+                    gpu.set_camera(scene_cam)
+                    ring.clear()
+                    gpu.render_camera_path(cams[:n], W, H, ring=ring.ring(per_launch), **ring.kw(), **kw)
+                    got = ring.get()
+                    for s in range(8):
+                        check_slot(got, s, refs[s], f"binned path of {n}, split {split}, {per_launch} per launch")
+            finally:
+                ring.free()
+    finally:
+        sc.close()
+
+
 def test_ring_arguments_are_checked(gpu, cube):
     W, H = 64, 36
     sc = MainScene(gpu, *cube, W, H, texture=64, fov=(16.0, 9.0))
