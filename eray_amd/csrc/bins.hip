@@ -39,6 +39,18 @@ namespace {
 constexpr int kBinWG = 256;
 constexpr uint32_t kPairGrid = 2048;  // workgroups of the grid-stride pair and scatter loops
 
+// The entry list's slot counter is sharded: device-scope atomics execute at the memory side, and
+// one word (or one 64-B line) takes about 88 returning atomics per microsecond (MI355X_MICROARCH.md
+// dequeue row), so one counter bumped once per 256 pairs serialised the pair pass (C5's four-camera
+// build: ~115k bumps, 1.3-1.8 ms).  Workgroup b appends to shard b % kShards, which owns entries
+// [s * region, (s + 1) * region) (region = cap / kShards); its counter sits kShardStride words
+// from the next one (a line of its own).  Pairs are dealt to the workgroups in 256-pair chunks
+// round-robin, so the shards fill evenly.
+constexpr uint32_t kShards = 32, kShardStride = 32;
+// binned object k's rectangle accumulator: acc + kAccStride * k (a line per object: the
+// finaliser's per-workgroup atomics on different objects do not share a line)
+constexpr uint32_t kAccStride = 16;
+
 
 // (face, bin) pairs of the binned faces' bin rectangles (face-major, each rectangle row-major):
 // the non-empty ones appended to the entry list, counted per bin key.  kJitter: the general
@@ -65,9 +77,9 @@ __global__ void __launch_bounds__(kBinWG) bin_pairs_kernel(const TriCull* __rest
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     __shared__ uint32_t s_cnt[kBinWG / 64];
     __shared__ uint32_t s_base;
-    const unsigned long long stride = (unsigned long long)gridDim.x * kBinWG;
+    const uint32_t shard = blockIdx.x % kShards, region = cap / kShards;
     // workgroup-uniform loop: one slot-counter atomic per workgroup and pass (a per-wave atomic on
-    // the one counter serialised thousands of times)
+    // the one counter serialised thousands of times), on the workgroup's shard
     __shared__ uint32_t s_face[kBinWG];  // each lane's pair's face
     auto face_of = [&](unsigned long long j) -> uint32_t {
         // the chunk: the last one starting at or before j (in LDS; an empty chunk never is, the next
@@ -88,14 +100,21 @@ __global__ void __launch_bounds__(kBinWG) bin_pairs_kernel(const TriCull* __rest
         }
         return lo - 1;
     };
-    for (unsigned long long base = (unsigned long long)blockIdx.x * kBinWG; base < P; base += stride) {
-        const unsigned long long j = base + threadIdx.x;
-        // The wave's 64 consecutive pairs belong to a run of consecutive faces: one search for the
-        // first pair's face, then 64 faces at a time each write their face index into the slots
-        // of the wave's pairs they own (a pair-per-lane search chained ~12 dependent loads).
-        const unsigned long long j0 = base + 64ull * wave, jend = min(j0 + 64ull, P);
-        if (j0 < P) {  // wave-uniform
-            uint32_t fb = face_of(j0);
+    // Every wave walks its own contiguous range of pairs, 64 at a time: one search for the face
+    // of its first pair, after which each slice starts from the face of the previous slice's last
+    // pair.  (A grid-stride loop searched anew for every slice — ~12 dependent global loads per
+    // 64 pairs, the pass's critical path: C5's four-camera build 1.3-1.8 ms.)
+    const unsigned long long slices = (unsigned long long)gridDim.x * (kBinWG / 64) * 64ull;
+    const unsigned long long per = (P + slices - 1) / slices * 64ull;  // pairs per wave (multiple of 64)
+    const unsigned long long w_lo = ((unsigned long long)blockIdx.x * (kBinWG / 64) + wave) * per;
+    const unsigned long long w_hi = min(w_lo + per, P);
+    uint32_t fb = w_lo < P ? face_of(w_lo) : 0u;
+    for (unsigned long long pass = 0; pass < per; pass += 64) {  // workgroup-uniform
+        const unsigned long long j0 = w_lo + pass, jend = min(j0 + 64ull, w_hi);
+        const unsigned long long j = j0 + lane;
+        // The wave's 64 consecutive pairs belong to a run of consecutive faces from fb on: 64 faces
+        // at a time each write their face index into the slots of the wave's pairs they own.
+        if (j0 < w_hi) {  // wave-uniform
             for (unsigned long long covered = j0; covered < jend; fb += 64) {  // wave-uniform
                 const uint32_t fi = fb + lane;
                 unsigned long long a = P, b = P;  // face fi's pairs [a, b)
@@ -109,10 +128,11 @@ __global__ void __launch_bounds__(kBinWG) bin_pairs_kernel(const TriCull* __rest
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            fb = s_face[64 * wave + (uint32_t)(jend - 1 - j0)];  // the next slice starts in this face or later
         }
         unsigned long long m = 0;
         uint32_t key = 0, i = 0;
-        if (j < P) {
+        if (j < w_hi) {
             i = s_face[threadIdx.x];
             const int4 g = range[i];
             const uint32_t w = (uint32_t)(g.y - g.x + 1);
@@ -131,11 +151,12 @@ __global__ void __launch_bounds__(kBinWG) bin_pairs_kernel(const TriCull* __rest
             before += w < wave ? s_cnt[w] : 0u;
             total += s_cnt[w];
         }
-        if (threadIdx.x == 0) s_base = total ? atomicAdd(n, total) : 0u;
+        if (threadIdx.x == 0) s_base = total ? atomicAdd(n + shard * kShardStride, total) : 0u;
         __syncthreads();
         if (m) {
-            const uint32_t slot = s_base + before + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-            if (slot < cap) {
+            const uint32_t local = s_base + before + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+            const uint32_t slot = shard * region + local;
+            if (local < region) {
                 ekey[slot] = key;
                 eface[slot] = i;
                 emask[slot] = m;
@@ -158,13 +179,17 @@ __global__ void __launch_bounds__(kBinWG) bin_scatter_kernel(const uint32_t* __r
                                                              uint32_t* __restrict__ tri,
                                                              unsigned long long* __restrict__ mask,
                                                              TriHot* __restrict__ hot_out) {
-    const uint32_t total = min(*n, cap);
-    for (uint32_t e = blockIdx.x * kBinWG + threadIdx.x; e < total; e += gridDim.x * kBinWG) {
-        const uint32_t key = ekey[e], f = eface[e];
-        const uint32_t pos = start[key] + atomicSub(count + key, 1u) - 1u;
-        tri[pos] = f - kbegin[key / nbins];
-        mask[pos] = emask[e];
-        hot_out[pos] = hot[T1 ? f % T1 : f];  // (several cameras: face f is face f % T1 of camera f / T1)
+    const uint32_t region = cap / kShards;
+    for (uint32_t sh = 0; sh < kShards; ++sh) {  // each shard's entries [sh * region, + its count)
+        const uint32_t total = min(n[sh * kShardStride], region);
+        for (uint32_t el = blockIdx.x * kBinWG + threadIdx.x; el < total; el += gridDim.x * kBinWG) {
+            const uint32_t e = sh * region + el;
+            const uint32_t key = ekey[e], f = eface[e];
+            const uint32_t pos = start[key] + atomicSub(count + key, 1u) - 1u;
+            tri[pos] = f - kbegin[key / nbins];
+            mask[pos] = emask[e];
+            hot_out[pos] = hot[T1 ? f % T1 : f];  // (several cameras: face f is face f % T1 of camera f / T1)
+        }
     }
 }
 
@@ -175,6 +200,7 @@ __global__ void __launch_bounds__(kBinWG) bin_scatter_kernel(const uint32_t* __r
 // max-merged into the objects' accumulators by the workgroups that found a non-empty bin.
 constexpr uint32_t kFinSpan = 8;    // binned objects per workgroup reduced in LDS (more: atomics)
 constexpr uint32_t kFinTab = 1024;  // binned objects the last workgroup combines in LDS
+constexpr uint32_t kFinGrid = 512;  // workgroups of the per-key pass
 
 __device__ __forceinline__ void max4(uint32_t* dst, const uint32_t (&a)[4]) {
     for (int q = 0; q < 4; ++q) atomicMax(dst + q, a[q]);
@@ -260,10 +286,12 @@ __global__ void __launch_bounds__(kBinWG) bin_sort_kernel(const uint32_t* __rest
     }
 }
 
-// kFinal false: each workgroup reduces its 256 keys and publishes; true: one workgroup combines
-// the nparts workgroups' partials (no device-scope fence and counter per workgroup).
+// kFinal false: each workgroup reduces its `per` consecutive keys (a multiple of kBinWG: each
+// thread keeps a running union while its keys stay in one object) and publishes; true: one
+// workgroup combines.  (One workgroup per 256 keys put ~8k atomics of C5's four-camera build on
+// one line: 330 us.)
 template <bool kFinal>
-__global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t nparts, const uint32_t* __restrict__ start, uint32_t nb,
+__global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t per, const uint32_t* __restrict__ start, uint32_t nb,
                                                                uint32_t bins_x, uint32_t nbins, uint32_t W, uint32_t H,
                                                                uint32_t phase, uint32_t* __restrict__ acc,
                                                                uint32_t* __restrict__ part,
@@ -274,50 +302,72 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t nparts, 
                                                                uint32_t* __restrict__ sortq, uint32_t* __restrict__ nsort,
                                                                CamState* __restrict__ st, uint32_t ncam) {
     __shared__ uint32_t s_acc[kFinSpan][4];
-    __shared__ uint32_t s_tab[kFinTab][4];
+    __shared__ uint32_t s_tab[kFinal ? kFinTab : 1][4];
     const uint32_t keys = nb * nbins;
-    const uint32_t b0 = blockIdx.x * kBinWG, b1 = min(b0 + kBinWG, keys);
+    const uint32_t b0 = kFinal ? 0u : blockIdx.x * per, b1 = kFinal ? 0u : min(b0 + per, keys);
     const uint32_t k_first = b0 < b1 ? b0 / nbins : 0u, k_last = b0 < b1 ? (b1 - 1) / nbins : 0u;
     if (threadIdx.x < kFinSpan * 4) s_acc[threadIdx.x / 4][threadIdx.x % 4] = 0u;
     __syncthreads();
-    const uint32_t b = b0 + threadIdx.x;
-    if (!kFinal && b < keys && start[b + 1] > start[b]) {
-        const uint32_t k = b / nbins;
-        const uint32_t lb = b - k * nbins;
-        const uint32_t bx = lb % bins_x, by = lb / bins_x;
-        const int32_t y0 = (int32_t)(by * kBinH + phase) - (int32_t)kBinH;
-        const uint32_t x0 = bx * kBinW, x1 = min(x0 + kBinW, W) - 1;
-        const uint32_t r0 = (uint32_t)max(y0, 0), r1 = (uint32_t)min(y0 + (int32_t)kBinH, (int32_t)H) - 1;
-        const uint32_t a[4] = {~x0, x1 + 1u, ~r0, r1 + 1u};
-        if (k - k_first < kFinSpan) max4(s_acc[k - k_first], a);
-        else max4(acc + 4 * k, a);
+    if constexpr (!kFinal) {
+        uint32_t kc = ~0u, a[4] = {0u, 0u, 0u, 0u};  // this thread's union of object kc's bins so far
+        auto flush = [&]() {
+            if (kc == ~0u) return;
+            if (kc - k_first < kFinSpan) max4(s_acc[kc - k_first], a);
+            else max4(acc + kAccStride * kc, a);
+        };
+        for (uint32_t b = b0 + threadIdx.x; b < b0 + per; b += kBinWG) {  // workgroup-uniform trip count
+            if (b < b1 && start[b + 1] > start[b]) {
+                const uint32_t k = b / nbins;
+                const uint32_t lb = b - k * nbins;
+                const uint32_t bx = lb % bins_x, by = lb / bins_x;
+                const int32_t y0 = (int32_t)(by * kBinH + phase) - (int32_t)kBinH;
+                const uint32_t x0 = bx * kBinW, x1 = min(x0 + kBinW, W) - 1;
+                const uint32_t r0 = (uint32_t)max(y0, 0), r1 = (uint32_t)min(y0 + (int32_t)kBinH, (int32_t)H) - 1;
+                const uint32_t w[4] = {~x0, x1 + 1u, ~r0, r1 + 1u};
+                if (k != kc) {
+                    flush();
+                    kc = k;
+                    for (int q = 0; q < 4; ++q) a[q] = 0u;
+                }
+                for (int q = 0; q < 4; ++q) a[q] = max(a[q], w[q]);
+            }
+            queue_sort(start, b, keys, sortq, nsort);
+        }
+        flush();
     }
     __syncthreads();
-    if constexpr (!kFinal) queue_sort(start, b, keys, sortq, nsort);
     // this workgroup's objects' unions into the accumulators: only workgroups with a non-empty
     // bin, four atomics per object (a single combining workgroup reading every workgroup's
     // partials took 28 us at 16 cameras x 32k bins)
     const uint32_t span = !kFinal && b0 < b1 ? min(k_last - k_first + 1, kFinSpan) : 0u;
     if (threadIdx.x < span && s_acc[threadIdx.x][1] != 0u) {
         const uint32_t a[4] = {s_acc[threadIdx.x][0], s_acc[threadIdx.x][1], s_acc[threadIdx.x][2], s_acc[threadIdx.x][3]};
-        max4(acc + 4 * (k_first + threadIdx.x), a);
+        max4(acc + kAccStride * (k_first + threadIdx.x), a);
     }
     if (!kFinal) return;
     const bool in_lds = nb <= kFinTab;
     if (in_lds) {
         for (uint32_t j = threadIdx.x; j < nb; j += kBinWG)
             for (int q = 0; q < 4; ++q) {
-                s_tab[j][q] = acc[4 * j + q];
-                acc[4 * j + q] = 0u;
+                s_tab[j][q] = acc[kAccStride * j + q];
+                acc[kAccStride * j + q] = 0u;
             }
         __syncthreads();
     }
     __syncthreads();
-    const uint32_t found = *n;
-    const bool overflow = found > cap;
+    // the shards' counts: an overflow if any shard outgrew its region; the entries needed for the
+    // capacity are the fullest shard's times kShards
+    uint32_t found = 0, fullest = 0;
+    for (uint32_t sh = 0; sh < kShards; ++sh) {
+        const uint32_t c = n[sh * kShardStride];
+        found += c;
+        fullest = max(fullest, c);
+    }
+    const bool overflow = fullest > cap / kShards;
+    const uint32_t need = max(found, fullest * kShards);
     for (uint32_t j = threadIdx.x; j < nb; j += kBinWG) {
         uint32_t w[4];
-        for (int q = 0; q < 4; ++q) w[q] = in_lds ? s_tab[j][q] : atomicExch(acc + 4 * j + q, 0u);
+        for (int q = 0; q < 4; ++q) w[q] = in_lds ? s_tab[j][q] : atomicExch(acc + kAccStride * j + q, 0u);
         ObjGeom& g = objs[kobj[j]].g;
         if (overflow) {  // keep the face rectangles; the frame kernel scans through LDS tiles
             g.bin_start = nullptr;
@@ -343,13 +393,14 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t nparts, 
         g.bin_mask = mask;
         g.bin_hot = hot;
     }
+    __syncthreads();  // (every thread has read the counts)
+    if (threadIdx.x < kShards) n[threadIdx.x * kShardStride] = 0u;
     if (threadIdx.x == 0) {
-        *n = 0u;
         *nsort = 0u;  // (bin_sort_kernel has run)
         // the most entries any setup needed since the buffers were allocated (the host grows the
         // capacity from it), and whether any overflowed
         for (uint32_t k = 0; k < ncam; ++k) {  // (several cameras: every camera's state)
-            st[k].bin_entries = max(st[k].bin_entries, found);
+            st[k].bin_entries = max(st[k].bin_entries, need);
             st[k].bin_overflow |= overflow ? 1u : 0u;
             st[k].nrect = 0u;
             st[k].total_sub = 0u;  // counted by detail_list_kernel
@@ -511,8 +562,8 @@ hipError_t bins_alloc(BinBuffers& b, uint32_t T, uint32_t nb, const uint32_t* kb
     b.nsub = 4 * (size_t)tiles_x * subs_y;
     if ((e = grow(&b.first, T)) != hipSuccess || (e = grow(&b.boff, kSetupMaxBlocks + 1)) != hipSuccess || (e = grow(&b.count, keys + 1)) != hipSuccess ||
         (e = grow(&b.start, keys + 1)) != hipSuccess || (e = grow(&b.kbegin, nb)) != hipSuccess ||
-        (e = grow(&b.kobj, nb)) != hipSuccess || (e = grow(&b.n, 1)) != hipSuccess ||
-        (e = grow(&b.done, 1)) != hipSuccess || (e = grow(&b.acc, 4 * (size_t)nb)) != hipSuccess ||
+        (e = grow(&b.kobj, nb)) != hipSuccess || (e = grow(&b.n, kShards * kShardStride)) != hipSuccess ||
+        (e = grow(&b.done, 1)) != hipSuccess || (e = grow(&b.acc, kAccStride * (size_t)nb)) != hipSuccess ||
         (e = grow(&b.part, 10 * std::max<size_t>((keys + kBinWG - 1) / kBinWG, 1))) != hipSuccess ||
         (e = grow(&b.ekey, cap)) != hipSuccess || (e = grow(&b.eface, cap)) != hipSuccess ||
         (e = grow(&b.emask, cap)) != hipSuccess || (e = grow(&b.tri, cap)) != hipSuccess ||
@@ -526,10 +577,10 @@ hipError_t bins_alloc(BinBuffers& b, uint32_t T, uint32_t nb, const uint32_t* kb
         return e;
     // counters zero between builds (each build leaves them so)
     if ((e = hipMemsetAsync(b.count, 0, sizeof(uint32_t) * (keys + 1), s)) != hipSuccess ||
-        (e = hipMemsetAsync(b.n, 0, sizeof(uint32_t), s)) != hipSuccess ||
+        (e = hipMemsetAsync(b.n, 0, sizeof(uint32_t) * kShards * kShardStride, s)) != hipSuccess ||
         (e = hipMemsetAsync(b.nsort, 0, sizeof(uint32_t), s)) != hipSuccess ||
         (e = hipMemsetAsync(b.done, 0, sizeof(uint32_t), s)) != hipSuccess ||
-        (e = hipMemsetAsync(b.acc, 0, sizeof(uint32_t) * 4 * nb, s)) != hipSuccess ||
+        (e = hipMemsetAsync(b.acc, 0, sizeof(uint32_t) * kAccStride * nb, s)) != hipSuccess ||
         (e = hipMemcpyAsync(b.kbegin, kbegin, sizeof(uint32_t) * nb, hipMemcpyHostToDevice, s)) != hipSuccess ||
         (e = hipMemcpyAsync(b.kobj, kobj, sizeof(uint32_t) * nb, hipMemcpyHostToDevice, s)) != hipSuccess)
         return e;
@@ -564,14 +615,16 @@ hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tile
                                                     b.kbegin, b.nbins, sp.hot, multi ? sp.T1 : 0u, b.tri, b.mask,
                                                     b.hot);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const uint32_t fgrid = (uint32_t)std::max<size_t>((keys + kBinWG - 1) / kBinWG, 1);
-    bins_finalize_kernel<false><<<fgrid, kBinWG, 0, s>>>(fgrid, b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase,
+    // at most kFinGrid workgroups, each over `per` consecutive keys
+    const uint32_t per = (uint32_t)std::max<size_t>(kBinWG, (keys + (size_t)kFinGrid * kBinWG - 1) / ((size_t)kFinGrid * kBinWG) * kBinWG);
+    const uint32_t fgrid = (uint32_t)std::max<size_t>((keys + per - 1) / per, 1);
+    bins_finalize_kernel<false><<<fgrid, kBinWG, 0, s>>>(per, b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase,
                                                          b.acc, b.part, b.done, b.n, (uint32_t)b.cap, b.kobj, sp.objs,
                                                          b.tri, b.mask, b.hot, b.sortq, b.nsort, sp.state, ncam);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     bin_sort_kernel<<<kSortGrid, kBinWG, 0, s>>>(b.sortq, b.nsort, b.start, b.tri, b.mask, b.hot);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    bins_finalize_kernel<true><<<1, kBinWG, 0, s>>>(fgrid, b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase, b.acc,
+    bins_finalize_kernel<true><<<1, kBinWG, 0, s>>>(per, b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase, b.acc,
                                                     b.part, b.done, b.n, (uint32_t)b.cap, b.kobj, sp.objs, b.tri, b.mask,
                                                     b.hot, b.sortq, b.nsort, sp.state, ncam);
     if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -22,7 +22,7 @@ face = ctx.empty((H, W), np.int32)
 sc.render(out_rgb=rgb.ptr, out_face=face.ptr)
 ctx.synchronize()
 hits = int((face.numpy() >= 0).sum())
-out = (C.c_uint64 * 10)()
+out = (C.c_uint64 * 13)()
 lib = capi.lib()
 lib.eray_debug_bin_stats.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
 assert lib.eray_debug_bin_stats(ctx._h, 0, out) == 0
