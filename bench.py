@@ -222,8 +222,8 @@ def moving_camera(scene, args, width, height, out, ring) -> dict:
         "frames": args.steps,
         "camera": "dolly along the view axis, z 5 +- 0.5, z_dist 1 +- 0.1, a new camera every frame",
         "includes": "every frame's camera setup on the device (culling records, pixel rectangles, merged "
-                    "detail rectangles; for meshes over 256 faces the screen bins and detail list, one frame "
-                    "per launch) + frame",
+                    "detail rectangles; for meshes over 256 faces the screen bins and detail list, built for "
+                    "up to 16 cameras at once beside the previous cameras' frames) + frame",
     }
 
 

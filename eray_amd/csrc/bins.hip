@@ -26,9 +26,11 @@
 // for that camera (the frame kernel scans those objects through LDS tiles instead, still exact)
 // and CamState reports the count, so the host can grow the capacity.
 #include <algorithm>
+#include <mutex>
 
 #include <hipcub/hipcub.hpp>
 
+#include "cull_record.hpp"
 #include "face_rect.hpp"
 #include "internal.hpp"
 
@@ -66,7 +68,8 @@ __global__ void __launch_bounds__(kBinWG) bin_pairs_kernel(const TriCull* __rest
                                                            uint32_t cap, uint32_t* __restrict__ n,
                                                            uint32_t* __restrict__ count, uint32_t* __restrict__ ekey,
                                                            uint32_t* __restrict__ eface,
-                                                           unsigned long long* __restrict__ emask) {
+                                                           unsigned long long* __restrict__ emask,
+                                                           uint32_t* __restrict__ erank) {
     // face i's first pair: its setup chunk's offset + its place in the chunk's own scan
     __shared__ unsigned long long s_boff[kSetupMaxBlocks + 1];
     __shared__ double s_poly[kJitter ? 16 * kBinWG : 1];  // clip_box's workspace
@@ -75,12 +78,17 @@ __global__ void __launch_bounds__(kBinWG) bin_pairs_kernel(const TriCull* __rest
     auto first = [&](uint32_t i) { return s_boff[i / chunk] + first_local[i]; };
     const unsigned long long P = s_boff[nparts];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    __shared__ uint32_t s_cnt[kBinWG / 64];
-    __shared__ uint32_t s_base;
-    const uint32_t shard = blockIdx.x % kShards, region = cap / kShards;
-    // workgroup-uniform loop: one slot-counter atomic per workgroup and pass (a per-wave atomic on
-    // the one counter serialised thousands of times), on the workgroup's shard
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    // each wave appends to shard (global wave index) % kShards, one counter atomic per 64 kept pairs
+    const uint32_t shard = (blockIdx.x * (kBinWG / 64) + wave) % kShards, region = cap / kShards;
     __shared__ uint32_t s_face[kBinWG];  // each lane's pair's face
+    // each wave's queue of pairs that survive the bin-rectangle test: face, bin (tx | ty << 16), key
+    __shared__ uint32_t s_qf[kBinWG / 64][128], s_qt[kBinWG / 64][128], s_qk[kBinWG / 64][128];
+    auto wave_sync = []() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
     auto face_of = [&](unsigned long long j) -> uint32_t {
         // the chunk: the last one starting at or before j (in LDS; an empty chunk never is, the next
         // one starts at the same pair) ...
@@ -100,78 +108,145 @@ __global__ void __launch_bounds__(kBinWG) bin_pairs_kernel(const TriCull* __rest
         }
         return lo - 1;
     };
+    // the queue's first cnt (<= 64) pairs: pixel masks (double precision), the non-empty ones
+    // appended to the entry list (wave-uniform)
+    auto emit = [&](uint32_t cnt) {
+        unsigned long long m = 0;
+        uint32_t key = 0, i = 0;
+        if (lane < cnt) {
+            i = s_qf[wave][lane];
+            const uint32_t t = s_qt[wave][lane];
+            key = s_qk[wave][lane];
+            if constexpr (kJitter) m = bin_pixels_jittered(cull[i], W, H, phase, t & 0xffffu, t >> 16, s_poly + threadIdx.x, kBinWG);
+            else m = bin_pixels(cull[i], W, H, phase, t & 0xffffu, t >> 16);
+        }
+        const unsigned long long bal = __ballot(m != 0);
+        if (!bal) return;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(n + shard * kShardStride, (uint32_t)__popcll(bal));
+        base = (uint32_t)__shfl((int)base, 0);
+        if (m) {
+            const uint32_t local = base + (uint32_t)__popcll(bal & lt);
+            if (local < region) {
+                const uint32_t slot = shard * region + local;
+                // the entry's rank in its bin comes back with the count: the scatter needs no
+                // atomics (a returning atomic per entry there cost as much as this pass)
+                erank[slot] = atomicAdd(count + key, 1u);
+                ekey[slot] = key;
+                eface[slot] = i;
+                emask[slot] = m;
+            }
+        }
+    };
     // Every wave walks its own contiguous range of pairs, 64 at a time: one search for the face
     // of its first pair, after which each slice starts from the face of the previous slice's last
     // pair.  (A grid-stride loop searched anew for every slice — ~12 dependent global loads per
-    // 64 pairs, the pass's critical path: C5's four-camera build 1.3-1.8 ms.)
+    // 64 pairs, the pass's critical path: C5's four-camera build 1.3-1.8 ms.)  Most pairs of a
+    // face's bin rectangle are empty (C5: 7.1M pairs, 0.47M entries per camera), so each pair is
+    // first tested against the bin's whole pixel rectangle with the frame kernel's own f32 culling
+    // test (cull_rejects over the rectangle of the bin's corner rays, widened as make_bundle does:
+    // a rejected bin has no pixel whose ray can hit the face); the survivors queue in LDS and go
+    // through the per-row double-precision masks 64 at a time.
     const unsigned long long slices = (unsigned long long)gridDim.x * (kBinWG / 64) * 64ull;
     const unsigned long long per = (P + slices - 1) / slices * 64ull;  // pairs per wave (multiple of 64)
     const unsigned long long w_lo = ((unsigned long long)blockIdx.x * (kBinWG / 64) + wave) * per;
     const unsigned long long w_hi = min(w_lo + per, P);
+    const float rw = __builtin_amdgcn_rcpf((float)W), rh = __builtin_amdgcn_rcpf((float)H);
+    const float wlo = 1.0f - 0x1p-20f, whi = 1.0f + 0x1p-20f;
     uint32_t fb = w_lo < P ? face_of(w_lo) : 0u;
-    for (unsigned long long pass = 0; pass < per; pass += 64) {  // workgroup-uniform
-        const unsigned long long j0 = w_lo + pass, jend = min(j0 + 64ull, w_hi);
-        const unsigned long long j = j0 + lane;
+    // face fi's pairs [a, b) for the 64 faces from fb on (P past the last face)
+    auto face_pairs = [&](uint32_t fb0, unsigned long long& a, unsigned long long& b) {
+        const uint32_t fi = fb0 + lane;
+        a = P;
+        b = P;
+        if (fi < T) {
+            a = first(fi);
+            b = fi + 1 < T ? first(fi + 1) : P;
+        }
+    };
+    unsigned long long pa, pb;  // the next slice's first 64 faces' pairs, loaded ahead
+    face_pairs(fb, pa, pb);
+    uint32_t qn = 0;  // queued pairs (wave-uniform)
+    for (unsigned long long j0 = w_lo; j0 < w_hi; j0 += 64) {  // wave-uniform
+        const unsigned long long jend = min(j0 + 64ull, w_hi), j = j0 + lane;
         // The wave's 64 consecutive pairs belong to a run of consecutive faces from fb on: 64 faces
         // at a time each write their face index into the slots of the wave's pairs they own.
-        if (j0 < w_hi) {  // wave-uniform
-            for (unsigned long long covered = j0; covered < jend; fb += 64) {  // wave-uniform
-                const uint32_t fi = fb + lane;
-                unsigned long long a = P, b = P;  // face fi's pairs [a, b)
-                if (fi < T) {
-                    a = first(fi);
-                    b = fi + 1 < T ? first(fi + 1) : P;
-                }
-                for (unsigned long long q = max(a, j0); q < min(b, jend); ++q) s_face[64 * wave + (uint32_t)(q - j0)] = fi;
-                covered = (unsigned long long)__shfl((long long)b, 63);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            fb = s_face[64 * wave + (uint32_t)(jend - 1 - j0)];  // the next slice starts in this face or later
+        bool ahead = true;  // the first 64 faces were loaded ahead
+        for (unsigned long long covered = j0; covered < jend; fb += 64, ahead = false) {  // wave-uniform
+            unsigned long long a = pa, b = pb;
+            if (!ahead) face_pairs(fb, a, b);
+            for (unsigned long long q = max(a, j0); q < min(b, jend); ++q) s_face[64 * wave + (uint32_t)(q - j0)] = fb + lane;
+            covered = (unsigned long long)__shfl((long long)b, 63);
         }
-        unsigned long long m = 0;
-        uint32_t key = 0, i = 0;
-        if (j < w_hi) {
+        wave_sync();
+        fb = s_face[64 * wave + (uint32_t)(jend - 1 - j0)];  // the next slice starts in this face or later
+        if (jend < w_hi) face_pairs(fb, pa, pb);  // in flight while this slice's pairs are tested
+        bool keep = false;
+        uint32_t i = 0, tx = 0, ty = 0, key = 0;
+        if (j < jend) {
             i = s_face[threadIdx.x];
+            key = fkey[i];  // (in the same round trip as the face's records)
             const int4 g = range[i];
             const uint32_t w = (uint32_t)(g.y - g.x + 1);
             const uint32_t c = (uint32_t)(j - first(i));
-            const uint32_t tx = (uint32_t)g.x + c % w, ty = (uint32_t)g.z + c / w;
-            if constexpr (kJitter) m = bin_pixels_jittered(cull[i], W, H, phase, tx, ty, s_poly + threadIdx.x, kBinWG);
-            else m = bin_pixels(cull[i], W, H, phase, tx, ty);
-            key = fkey[i] * nbins + ty * bins_x + tx;
-        }
-        const unsigned long long bal = __ballot(m != 0);
-        if (lane == 0) s_cnt[wave] = (uint32_t)__popcll(bal);
-        __syncthreads();
-        uint32_t before = 0, total = 0;
-#pragma unroll
-        for (uint32_t w = 0; w < kBinWG / 64; ++w) {
-            before += w < wave ? s_cnt[w] : 0u;
-            total += s_cnt[w];
-        }
-        if (threadIdx.x == 0) s_base = total ? atomicAdd(n + shard * kShardStride, total) : 0u;
-        __syncthreads();
-        if (m) {
-            const uint32_t local = s_base + before + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-            const uint32_t slot = shard * region + local;
-            if (local < region) {
-                ekey[slot] = key;
-                eface[slot] = i;
-                emask[slot] = m;
-                atomicAdd(count + key, 1u);
+            // c / w and c % w (c < 2^24: exact in f32) by a float quotient, corrected by one
+            uint32_t qy = (uint32_t)((float)c / (float)w);
+            int32_t rx = (int32_t)(c - qy * w);
+            if (rx < 0) {
+                --qy;
+                rx += (int32_t)w;
+            } else if (rx >= (int32_t)w) {
+                ++qy;
+                rx -= (int32_t)w;
+            }
+            tx = (uint32_t)g.x + (uint32_t)rx;
+            ty = (uint32_t)g.z + qy;
+            keep = true;
+            if constexpr (!kJitter) {
+                const int32_t x0 = (int32_t)(tx * kBinW), x1 = min(x0 + (int32_t)kBinW, (int32_t)W) - 1;
+                const int32_t yb = (int32_t)(ty * kBinH + phase) - (int32_t)kBinH;
+                const int32_t y0 = max(yb, 0), y1 = min(yb + (int32_t)kBinH, (int32_t)H) - 1;
+                keep = y0 <= y1 && !cull_rejects(cull[i], ((float)x0 * rw) * wlo, ((float)x1 * rw) * whi,
+                                                 ((float)y0 * rh) * wlo, ((float)y1 * rh) * whi);
             }
         }
-        __syncthreads();  // s_cnt / s_base are rewritten by the next pass
+        const unsigned long long kb = __ballot(keep);
+        if (keep) {
+            const uint32_t pos = qn + (uint32_t)__popcll(kb & lt);
+            s_qf[wave][pos] = i;
+            s_qt[wave][pos] = tx | (ty << 16);
+            s_qk[wave][pos] = key * nbins + ty * bins_x + tx;
+        }
+        qn += (uint32_t)__popcll(kb);
+        wave_sync();
+        if (qn >= 64) {
+            emit(64);
+            const uint32_t rest = qn - 64;  // the queue's tail to its front
+            uint32_t f2 = 0, t2 = 0, k2 = 0;
+            if (lane < rest) {
+                f2 = s_qf[wave][64 + lane];
+                t2 = s_qt[wave][64 + lane];
+                k2 = s_qk[wave][64 + lane];
+            }
+            wave_sync();
+            if (lane < rest) {
+                s_qf[wave][lane] = f2;
+                s_qt[wave][lane] = t2;
+                s_qk[wave][lane] = k2;
+            }
+            wave_sync();
+            qn = rest;
+        }
     }
+    if (qn) emit(qn);
 }
 
-// every stored entry to its bin: start[key] + (the count, counted down to zero)
+// every stored entry to its bin: start[key] + its rank; the counts back to zero for the next camera
 __global__ void __launch_bounds__(kBinWG) bin_scatter_kernel(const uint32_t* __restrict__ n, uint32_t cap,
                                                              const uint32_t* __restrict__ ekey,
                                                              const uint32_t* __restrict__ eface,
                                                              const unsigned long long* __restrict__ emask,
+                                                             const uint32_t* __restrict__ erank,
                                                              const uint32_t* __restrict__ start,
                                                              uint32_t* __restrict__ count,
                                                              const uint32_t* __restrict__ kbegin, uint32_t nbins,
@@ -185,7 +260,8 @@ __global__ void __launch_bounds__(kBinWG) bin_scatter_kernel(const uint32_t* __r
         for (uint32_t el = blockIdx.x * kBinWG + threadIdx.x; el < total; el += gridDim.x * kBinWG) {
             const uint32_t e = sh * region + el;
             const uint32_t key = ekey[e], f = eface[e];
-            const uint32_t pos = start[key] + atomicSub(count + key, 1u) - 1u;
+            const uint32_t pos = start[key] + erank[e];
+            count[key] = 0u;  // (every entry of the bin stores the same zero)
             tri[pos] = f - kbegin[key / nbins];
             mask[pos] = emask[e];
             hot_out[pos] = hot[T1 ? f % T1 : f];  // (several cameras: face f is face f % T1 of camera f / T1)
@@ -523,6 +599,22 @@ __global__ void __launch_bounds__(kBinWG) detail_append_kernel(const uint32_t* _
     if (blockIdx.x == 0 && threadIdx.x == 0) st->total_sub = heavy + nl;
 }
 
+// Workgroups of kBinWG threads of kernel `k` resident at once on the device (occupancy API, per
+// kernel slot), kPairGrid if unknown.
+uint32_t resident_grid(const void* k, int slot) {
+    static std::mutex mu;
+    static int per_cu[2] = {-1, -1}, cus = -1;
+    std::lock_guard<std::mutex> lock(mu);
+    if (cus < 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 0;
+    }
+    if (per_cu[slot] < 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu[slot], k, kBinWG, 0) != hipSuccess)
+        per_cu[slot] = 0;
+    return cus > 0 && per_cu[slot] > 0 ? (uint32_t)(cus * per_cu[slot]) : kPairGrid;
+}
+
 template <typename T>
 hipError_t grow(T** p, size_t need) {
     if (*p) {
@@ -537,7 +629,7 @@ hipError_t grow(T** p, size_t need) {
 
 void bins_free(BinBuffers& b) {
     void* ptrs[] = {b.first, b.boff, b.count,  b.start,  b.kbegin, b.kobj,   b.n,       b.done,    b.acc,   b.part, b.ekey,
-                    b.eface, b.emask,  b.tri,    b.mask,   b.hot,    b.dflags,  b.dpacked, b.dlist, b.docc,
+                    b.eface, b.emask,  b.erank,  b.tri,    b.mask,   b.hot,    b.dflags,  b.dpacked, b.dlist, b.docc,
                     b.sortq, b.nsort,  b.temp,   b.dflags_light, b.dlight, b.dcount};
     for (void* p : ptrs)
         if (p) hipFree(p);
@@ -566,7 +658,7 @@ hipError_t bins_alloc(BinBuffers& b, uint32_t T, uint32_t nb, const uint32_t* kb
         (e = grow(&b.done, 1)) != hipSuccess || (e = grow(&b.acc, kAccStride * (size_t)nb)) != hipSuccess ||
         (e = grow(&b.part, 10 * std::max<size_t>((keys + kBinWG - 1) / kBinWG, 1))) != hipSuccess ||
         (e = grow(&b.ekey, cap)) != hipSuccess || (e = grow(&b.eface, cap)) != hipSuccess ||
-        (e = grow(&b.emask, cap)) != hipSuccess || (e = grow(&b.tri, cap)) != hipSuccess ||
+        (e = grow(&b.emask, cap)) != hipSuccess || (e = grow(&b.erank, cap)) != hipSuccess || (e = grow(&b.tri, cap)) != hipSuccess ||
         (e = grow(&b.mask, cap)) != hipSuccess || (e = grow(&b.hot, cap)) != hipSuccess ||
         (e = grow(&b.dflags, b.nsub)) != hipSuccess || (e = grow(&b.dpacked, b.nsub)) != hipSuccess ||
         (e = grow(&b.dflags_light, b.nsub)) != hipSuccess || (e = grow(&b.dlight, b.nsub)) != hipSuccess ||
@@ -605,13 +697,16 @@ hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tile
     if (sp.T) {  // (a multi-camera build may set up fewer cameras than the buffers hold)
         const uint32_t nparts = setup_blocks(sp.T), chunk = (sp.T + nparts - 1) / nparts;  // as camera_setup_kernel
         auto* k = sp.keep_all ? bin_pairs_kernel<true> : bin_pairs_kernel<false>;
-        k<<<kPairGrid, kBinWG, 0, s>>>(sp.cull, sp.range, b.first, b.boff, nparts, chunk, sp.fkey, sp.T, sp.W, sp.H, sp.phase,
-                                       b.bins_x, b.nbins, (uint32_t)b.cap, b.n, b.count, b.ekey, b.eface, b.emask);
+        // exactly the resident workgroups (each wave walks a fixed share of the pairs: a second
+        // round of workgroups would double the pass)
+        const uint32_t pgrid = resident_grid(reinterpret_cast<const void*>(k), sp.keep_all ? 1 : 0);
+        k<<<pgrid, kBinWG, 0, s>>>(sp.cull, sp.range, b.first, b.boff, nparts, chunk, sp.fkey, sp.T, sp.W, sp.H, sp.phase,
+                                       b.bins_x, b.nbins, (uint32_t)b.cap, b.n, b.count, b.ekey, b.eface, b.emask, b.erank);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     tb = b.temp_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(b.temp, tb, b.count, b.start, (int)(keys + 1), s)) != hipSuccess) return e;
-    bin_scatter_kernel<<<kPairGrid, kBinWG, 0, s>>>(b.n, (uint32_t)b.cap, b.ekey, b.eface, b.emask, b.start, b.count,
+    bin_scatter_kernel<<<kPairGrid, kBinWG, 0, s>>>(b.n, (uint32_t)b.cap, b.ekey, b.eface, b.emask, b.erank, b.start, b.count,
                                                     b.kbegin, b.nbins, sp.hot, multi ? sp.T1 : 0u, b.tri, b.mask,
                                                     b.hot);
     if ((e = hipGetLastError()) != hipSuccess) return e;

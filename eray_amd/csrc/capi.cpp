@@ -1729,8 +1729,8 @@ void* eray_internal_staging(eray_ctx* ctx, size_t bytes) {
 // the last setup — out[0] bins, out[1] entries, out[2] (face, pixel) pairs (mask bits),
 // out[3] most entries in one bin, out[4] non-empty bins, out[5] most pairs in one bin,
 // out[6..9] the object's pixel rectangle (x0, x1, y0, y1; int32 as uint64), out[10] the bin with
-// the most entries, out[11] / out[12] the bins of more than 64 / kTraceHeavyMin entries (out: 13
-// words).  Synchronises.
+// the most entries, out[11] / out[12] the bins of more than 64 / kTraceHeavyMin entries, out[13]
+// the pairs of the faces' bin rectangles before masking (out: 14 words).  Synchronises.
 extern "C" int eray_debug_bin_stats(eray_ctx* ctx, uint32_t index, uint64_t* out) {
     if (!ctx || !out || index >= ctx->objects.size() || ctx->objects[index].T <= kDirectMax || !ctx->bins.start)
         return ERAY_E_INVALID_ARGUMENT;
@@ -1770,6 +1770,11 @@ extern "C" int eray_debug_bin_stats(eray_ctx* ctx, uint32_t index, uint64_t* out
     out[10] = most_at;
     out[11] = over64;
     out[12] = over192;
+    // out[13]: the (face, bin) pairs of the faces' bin rectangles before masking (every object)
+    unsigned long long pairs_all = 0;
+    if (hipMemcpy(&pairs_all, b.boff + setup_blocks(ctx->total_tris), sizeof pairs_all, hipMemcpyDeviceToHost) != hipSuccess)
+        return set_error(ctx, ERAY_E_HIP, "bin stats copy failed");
+    out[13] = pairs_all;
     return ERAY_OK;
 }
 

@@ -132,45 +132,33 @@ __device__ inline CondLine cond_line(float A, float B, float K, float T, uint32_
     l.kind = A > 0.0f ? 1 : 2;
     return l;
 }
-__device__ inline void apply_line(const CondLine& l, double yf, int32_t& xl, int32_t& xr) {
-    if (l.kind == 0) return;
-    const double q = l.c0 - l.c1 * yf;
-    if (l.kind == 3) {
-        if (q > l.tol) {
-            xl = 1;
-            xr = 0;
-        }
-    } else if (l.kind == 1) {
-        const double lo = ceil(q - l.tol);
-        if (lo > (double)xl) xl = lo > 2e9 ? 2000000000 : (int32_t)lo;
-    } else {
-        const double hi = floor(q + l.tol);
-        if (hi < (double)xr) xr = hi < -2e9 ? -2000000000 : (int32_t)hi;
-    }
-}
-
 // Pixels of the kBinW x kBinH bin at (bx, by) (camera columns bx*kBinW.., rows y0..y0+3 with
 // y0 = by*kBinH + phase - kBinH) where all four conditions of record c can pass: bit
 // r * kBinW + col.  The rows' yf are the reference's f32 y/H (camera_dir).
 __device__ inline unsigned long long bin_pixels(const TriCull& c, uint32_t W, uint32_t H, uint32_t phase,
                                                 uint32_t bx, uint32_t by) {
-    const CondLine l0 = cond_line(c.A.x, c.B.x, c.K.x, c.T.x, W);
-    const CondLine l1 = cond_line(c.A.y, c.B.y, c.K.y, c.T.y, W);
-    const CondLine l2 = cond_line(c.A.z, c.B.z, c.K.z, c.T.z, W);
-    const CondLine l3 = cond_line(c.A.w, c.B.w, c.K.w, c.T.w, W);
+    const CondLine l[4] = {cond_line(c.A.x, c.B.x, c.K.x, c.T.x, W), cond_line(c.A.y, c.B.y, c.K.y, c.T.y, W),
+                           cond_line(c.A.z, c.B.z, c.K.z, c.T.z, W), cond_line(c.A.w, c.B.w, c.K.w, c.T.w, W)};
     const int32_t x_lo = (int32_t)(bx * kBinW), x_hi = min((int32_t)((bx + 1) * kBinW), (int32_t)W) - 1;
     unsigned long long pix = 0;
+    // apply_line's cases as selects (lanes hold pairs of different faces, whose condition kinds
+    // differ: branches diverged 3 ways per condition and row), the same double operations
+#pragma unroll
     for (uint32_t r = 0; r < kBinH; ++r) {
         const int32_t y = (int32_t)(by * kBinH + phase + r) - (int32_t)kBinH;
-        if (y < 0 || y >= (int32_t)H) continue;
         const double yf = (double)((float)(uint32_t)y / (float)H);
-        int32_t xl = x_lo, xr = x_hi;
-        apply_line(l0, yf, xl, xr);
-        apply_line(l1, yf, xl, xr);
-        apply_line(l2, yf, xl, xr);
-        apply_line(l3, yf, xl, xr);
-        if (xl <= xr) {
-            const uint32_t n = (uint32_t)(xr - xl + 1), s = (uint32_t)(xl - x_lo);
+        double xl = (double)x_lo, xr = (double)x_hi;
+        bool fail = y < 0 || y >= (int32_t)H;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const double q = l[k].c0 - l[k].c1 * yf;
+            const double lo = ceil(q - l[k].tol), hi = floor(q + l[k].tol);
+            xl = (l[k].kind == 1 && lo > xl) ? lo : xl;
+            xr = (l[k].kind == 2 && hi < xr) ? hi : xr;
+            fail |= l[k].kind == 3 && q > l[k].tol;
+        }
+        if (!fail && xl <= xr) {  // (xl >= x_lo, xr <= x_hi: both within the bin's columns)
+            const uint32_t n = (uint32_t)((int32_t)xr - (int32_t)xl + 1), s = (uint32_t)((int32_t)xl - x_lo);
             pix |= (unsigned long long)((((n >= 32 ? 0xffffffffu : ((1u << n) - 1u)) << s) & 0xffffu)) << (kBinW * r);
         }
     }

@@ -364,11 +364,12 @@ struct BinBuffers {
     uint32_t* kobj = nullptr;             // object index per binned object
     uint32_t* n = nullptr;                // entries found (device counter, reset by the finaliser)
     uint32_t* done = nullptr;             // workgroup counter of the finaliser
-    uint32_t* acc = nullptr;              // 4 x nb rectangle accumulators of the non-empty bins
+    uint32_t* acc = nullptr;              // rectangle accumulators of the non-empty bins (a line per object)
     uint32_t* part = nullptr;             // 10 per finaliser workgroup: its end objects' partials
     uint32_t* ekey = nullptr;             // unscattered entries (cap)
     uint32_t* eface = nullptr;
     unsigned long long* emask = nullptr;
+    uint32_t* erank = nullptr;            // the entry's place among its bin's entries (count's old value)
     uint32_t* tri = nullptr;              // bin entries in key order (cap)
     unsigned long long* mask = nullptr;
     TriHot* hot = nullptr;

@@ -125,7 +125,11 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp, 
             sp.cull[i] = c;
             const uint32_t obj = vobject(i);
             int32_t r[4];
-            const bool any = face_rect(c, sp.W, sp.H, r, s_poly + tid, kSetupWG, xa, ya);
+            // a face none of whose rays can pass anywhere in the viewport (the frame kernel's own
+            // f32 rectangle test, the viewport widened: about half of a closed mesh's faces, the
+            // back-facing ones) needs no double-precision clip
+            const bool none = cull_rejects(c, (float)xa - 1e-6f, 1.0f + 1e-6f, (float)ya - 1e-6f, 1.0f + 1e-6f);
+            const bool any = !none && face_rect(c, sp.W, sp.H, r, s_poly + tid, kSetupWG, xa, ya);
             if (any) {
                 uint32_t a[4];
                 rect_words(r, a);

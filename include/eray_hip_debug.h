@@ -17,7 +17,8 @@ extern "C" {
 /* The screen bins of object `index` as built by the last setup: out[0] bins, out[1] entries,
  * out[2] (face, pixel) pairs, out[3] most entries in one bin, out[4] non-empty bins, out[5] most
  * pairs in one bin, out[6..9] the object's pixel rectangle, out[10] the fullest bin, out[11] /
- * out[12] bins of more than 64 / 192 entries (13 words). */
+ * out[12] bins of more than 64 / 192 entries, out[13] the pairs of the faces' bin rectangles before
+ * masking (14 words). */
 int eray_debug_bin_stats(eray_ctx* ctx, uint32_t index, uint64_t* out);
 /* The entries of bin `bin` of object `index` (faces relative to the object, pixel masks), at most
  * `cap`; *n = the bin's entry count. */

@@ -33,7 +33,7 @@ def main():
         kw = dict(out_rgb=rgb.ptr, anti_aliasing=aa, aa_seed=7)
         ctx.render(W, H, **kw)
         ctx.synchronize()
-        st = (C.c_uint64 * 13)()
+        st = (C.c_uint64 * 14)()
         L.eray_debug_bin_stats.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]
         L.eray_debug_bin_stats(ctx._h, 0, st)
         state = (C.c_uint8 * 176)()

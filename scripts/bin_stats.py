@@ -22,12 +22,12 @@ face = ctx.empty((H, W), np.int32)
 sc.render(out_rgb=rgb.ptr, out_face=face.ptr)
 ctx.synchronize()
 hits = int((face.numpy() >= 0).sum())
-out = (C.c_uint64 * 13)()
+out = (C.c_uint64 * 14)()
 lib = capi.lib()
 lib.eray_debug_bin_stats.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
 assert lib.eray_debug_bin_stats(ctx._h, 0, out) == 0
 nb, n, pairs, most, nonempty, most_pairs = list(out)[:6]
-rect = [C.c_int64(v).value for v in list(out)[6:]]
+rect = [C.c_int64(v).value for v in list(out)[6:10]]
 print(f"{W}x{H} T={len(mesh[0])}: hits {hits}, bins {nb}, non-empty {nonempty}, entries {n} "
       f"({n / max(nonempty, 1):.1f}/bin, max {most}), pairs {pairs} ({pairs / max(n, 1):.2f}/entry, "
-      f"{pairs / max(hits, 1):.1f}/hit px, max {most_pairs}/bin), object rect {rect}")
+      f"{pairs / max(hits, 1):.1f}/hit px, max {most_pairs}/bin), object rect {rect}, rectangle pairs {out[13]}")
