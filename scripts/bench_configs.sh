@@ -11,8 +11,9 @@ python -m eray_amd.meshgen --triangles 69451 --seed 42 -o $M/standin70k.obj > /d
 if [ "${WITH_1M:-0}" = 1 ]; then
   python -m eray_amd.meshgen --triangles 1000000 --seed 1234 -o $M/synth1m.obj > /dev/null || exit 1
 fi
-run() {  # name timeout args...
+run() {  # name timeout args...   (ONLY="c2 c3 ...": those configs alone)
   local name=$1 t=$2; shift 2
+  if [ -n "${ONLY:-}" ] && [[ " $ONLY " != *" $name "* ]]; then return 0; fi
   echo "=== $name: $*"
   timeout -k 10 "$t" python bench.py "$@" > $OUT/$name.json.log 2>&1
   local rc=$?
