@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -1436,7 +1437,9 @@ int eray_render_frames_ring(eray_ctx* ctx, const eray_render_params* rp, const e
         HIP_TRY(ctx, launch_frame(ctx, ring_frames(p, r, f, std::min(r.per_launch, n - f))));
         return ERAY_OK;
     };
-    if (int st = ensure_plan(ctx, ring_key(params_key(p, 0), r), frames, body, &plan)) return st;
+    static const bool plain_launches = std::getenv("ERAY_PLAIN_LAUNCHES") != nullptr;  // (A/B diagnostics)
+    if (!plain_launches)
+        if (int st = ensure_plan(ctx, ring_key(params_key(p, 0), r), frames, body, &plan)) return st;
     auto none = [](uint32_t, uint32_t) { return (int)ERAY_OK; };
     auto plain = [&](uint32_t f) { return body(f, frames); };
     return replay(ctx, plan, frames, none, plain, mean_frame_ms);
