@@ -35,23 +35,59 @@ using namespace eray::dev;
 // `xa`..`yb`: the viewport coordinates the rays can take (the frame kernel's camera rays: x', y'
 // in [0, 1]; trace.hip's jittered anti-aliasing rays reach -1/W and -1/H) — only Dmax depends on
 // them, and |x'|, |y'| <= 1 is kept for the S and evaluation terms.
-__device__ inline TriCull cull_record(const TriHot& h, const CamDev& cam, double xa = 0.0, double xb = 1.0,
-                                      double ya = 0.0, double yb = 1.0) {
+// The camera's part of the record (the same for every face): the reference's f32 viewport corner
+// and width, the corner relative to the centre, the largest |D| over the x', y' range and the
+// magnitude scale S.  (Per face it cost four double square roots.)
+struct CullCam {
+    float cx, cy, cz, vw;
+    f3 bl;
+    double blc[3];
+    double dmax, S;
+};
+__device__ inline CullCam cull_cam(const CamDev& cam, double xa = 0.0, double xb = 1.0, double ya = 0.0,
+                                   double yb = 1.0) {
     const double u = 0x1p-24;
-    const float cx = cam.cx, cy = cam.cy, cz = cam.cz;
+    CullCam c;
+    c.cx = cam.cx;
+    c.cy = cam.cy;
+    c.cz = cam.cz;
+    const f3 Cf = mk3(c.cx, c.cy, c.cz);
+    // camera.rs:57-76 in f32, as the reference computes it
+    c.vw = cam.ratio * 2.0f;
+    c.bl = sub(sub(sub(Cf, divs(mk3(c.vw, 0.0f, 0.0f), 2.0f)), divs(mk3(0.0f, 2.0f, 0.0f), 2.0f)),
+               mk3(0.0f, 0.0f, cam.z_dist));
+    c.blc[0] = (double)c.bl.x - c.cx;
+    c.blc[1] = (double)c.bl.y - c.cy;
+    c.blc[2] = (double)c.bl.z - c.cz;
+    // largest |D| over the frame (corners of the x', y' range) and the magnitude scale S
+    double dmax = 0.0;
+    for (int cxr = 0; cxr < 2; ++cxr)
+        for (int cyr = 0; cyr < 2; ++cyr) {
+            const double xc = cxr ? xb : xa, yc = cyr ? yb : ya;
+            double D0 = c.blc[0] + (double)c.vw * xc, D1 = c.blc[1] + 2.0 * yc, D2 = c.blc[2];
+            double l = sqrt(D0 * D0 + D1 * D1 + D2 * D2);
+            dmax = l > dmax ? l : dmax;
+        }
+    c.S = fabs((double)c.bl.x) + fabs((double)c.bl.y) + fabs((double)c.bl.z) + fabs((double)c.vw) + 2.0 +
+          fabs((double)c.cx) + fabs((double)c.cy) + fabs((double)c.cz);
+    c.dmax = dmax * (1.0 + 1e-6) + 8.0 * u * c.S;
+    return c;
+}
+
+__device__ inline TriCull cull_record(const TriHot& h, const CullCam& cc) {
+    const double u = 0x1p-24;
+    const float cx = cc.cx, cy = cc.cy, cz = cc.cz;
     const f3 e1f = mk3(h.q0.x, h.q0.y, h.q0.z), e2f = mk3(h.q0.w, h.q1.x, h.q1.y);
     const f3 nf = mk3(h.q1.z, h.q1.w, h.q2.x), af = mk3(h.q2.y, h.q2.z, h.q2.w);
     const f3 Cf = mk3(cx, cy, cz);
     const f3 aof = sub(Cf, af);        // exactly the reference's `*ray.start() - a`
     const float atf = dot0(aof, nf);   // exactly the reference's `ao.dot_product(&n)`
-    // camera.rs:57-76 in f32, as the reference computes it
-    const float vw = cam.ratio * 2.0f;
-    const f3 bl = sub(sub(sub(Cf, divs(mk3(vw, 0.0f, 0.0f), 2.0f)), divs(mk3(0.0f, 2.0f, 0.0f), 2.0f)),
-                      mk3(0.0f, 0.0f, cam.z_dist));
+    const float vw = cc.vw;
+    const double* blc = cc.blc;
+    const double dmax = cc.dmax, S = cc.S;
     // doubles from here on
     const double e1[3] = {e1f.x, e1f.y, e1f.z}, e2[3] = {e2f.x, e2f.y, e2f.z};
     const double n[3] = {nf.x, nf.y, nf.z}, ao[3] = {aof.x, aof.y, aof.z};
-    const double blc[3] = {(double)bl.x - cx, (double)bl.y - cy, (double)bl.z - cz};
     auto n1 = [](const double* v) { return fabs(v[0]) + fabs(v[1]) + fabs(v[2]); };
     auto crs = [](const double* s, const double* o, double* r) {
         r[0] = s[1] * o[2] - s[2] * o[1];
@@ -71,18 +107,6 @@ __device__ inline TriCull cull_record(const TriHot& h, const CamDev& cam, double
     const double Ev = 8.0 * u * ne1 * nao + floor_n;
     const double En = 4.0 * u * nn;
     const double Ew = (8.0 * u * ne2 * nao) + (8.0 * u * ne1 * nao) + 1.01 * En + 3.2 * u * nn + floor_n;
-    // largest |D| over the frame (corners of the x', y' range) and the magnitude scale S
-    double dmax = 0.0;
-    for (int cxr = 0; cxr < 2; ++cxr)
-        for (int cyr = 0; cyr < 2; ++cyr) {
-            const double xc = cxr ? xb : xa, yc = cyr ? yb : ya;
-            double D0 = blc[0] + (double)vw * xc, D1 = blc[1] + 2.0 * yc, D2 = blc[2];
-            double l = sqrt(D0 * D0 + D1 * D1 + D2 * D2);
-            dmax = l > dmax ? l : dmax;
-        }
-    const double S = fabs((double)bl.x) + fabs((double)bl.y) + fabs((double)bl.z) + fabs((double)vw) + 2.0 +
-                     fabs((double)cx) + fabs((double)cy) + fabs((double)cz);
-    dmax = dmax * (1.0 + 1e-6) + 8.0 * u * S;
     const double* W[4] = {wu, wv, ww, wn};
     const double E[4] = {Eu, Ev, Ew, En};
     float A[4], B[4], K[4], Tt[4];
@@ -122,6 +146,10 @@ __device__ inline TriCull cull_record(const TriHot& h, const CamDev& cam, double
     c.K = make_float4(K[0], K[1], K[2], K[3]);
     c.T = make_float4(Tt[0], Tt[1], Tt[2], Tt[3]);
     return c;
+}
+__device__ inline TriCull cull_record(const TriHot& h, const CamDev& cam, double xa = 0.0, double xb = 1.0,
+                                      double ya = 0.0, double yb = 1.0) {
+    return cull_record(h, cull_cam(cam, xa, xb, ya, yb));
 }
 
 // true when condition k fails for every pixel of [xlo,xhi] x [ylo,yhi]

@@ -114,6 +114,8 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp, 
         for (int k = 0; k < 4; ++k) s_acc[j][k] = 0u;
     __syncthreads();
     unsigned long long run = 0;  // binned faces: pairs of this chunk's faces so far
+    CullCam cc{};
+    uint32_t cc_k = ~0u;
     for (uint32_t i0 = lo; i0 < hi && kMode != 2; i0 += kSetupWG) {  // workgroup-uniform
         const uint32_t i = i0 + tid;
         unsigned long long ar = 0;
@@ -121,7 +123,11 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp, 
             // (keep_all: the general tracer's viewport, jittered rays reach -1/W and -1/H)
             const double xa = sp.keep_all ? -2.0 / (double)sp.W : 0.0, ya = sp.keep_all ? -2.0 / (double)sp.H : 0.0;
             const uint32_t kc = multi ? i / sp.T1 : 0u;  // (the face's camera)
-            const TriCull c = cull_record(sp.hot[i - kc * sp.T1], multi ? sp.cam[kc] : cam, xa, 1.0, ya, 1.0);
+            if (kc != cc_k) {  // the camera's part of the records: once per camera and thread
+                cc = cull_cam(multi ? sp.cam[kc] : cam, xa, 1.0, ya, 1.0);
+                cc_k = kc;
+            }
+            const TriCull c = cull_record(sp.hot[i - kc * sp.T1], cc);
             sp.cull[i] = c;
             const uint32_t obj = vobject(i);
             int32_t r[4];
