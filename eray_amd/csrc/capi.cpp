@@ -1644,14 +1644,42 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
     const uint64_t mc_gen = multi ? ctx->mc_gen : 0u;  // (likewise the multi-camera buffers)
     key.insert(key.end(), reinterpret_cast<const unsigned char*>(&mc_gen),
                reinterpret_cast<const unsigned char*>(&mc_gen) + sizeof mc_gen);
-    Plan plan;
-    if (int st = ensure_plan(ctx, key, n, body, &plan)) return st;
     auto before = [&](uint32_t first, uint32_t count) -> int {
         if (one_chunk) return ERAY_OK;
         HIP_TRY(ctx, hipMemcpyAsync(ctx->d_path, ctx->d_path_all + first, sizeof(CamDev) * count,
                                     hipMemcpyDeviceToDevice, ctx->stream));
         return ERAY_OK;
     };
+    // multi-camera builds on two streams enqueued directly, chunk by chunk, instead of replayed
+    // from a captured graph (A/B knob: at C5's frame a trace showed the GPU idle for milliseconds
+    // after the first builds of a graph-replayed path)
+    static const bool multi_direct = std::getenv("ERAY_MULTI_DIRECT") != nullptr;
+    if (multi && multi_direct) {
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        if (mean_frame_ms) {
+            for (auto& e : ev) HIP_TRY(ctx, hipEventCreate(&e));
+            HIP_TRY(ctx, hipEventRecord(ev[0], ctx->stream));
+        }
+        int st = ERAY_OK;
+        for (uint32_t first = 0; first < n && !st; first += kGraphFrames) {
+            const uint32_t count = std::min(kGraphFrames, n - first);
+            st = before(first, count);
+            for (uint32_t f = 0; f < count && !st; ++f) st = multi_frame(ctx->d_path, f, count, first + f);
+        }
+        if (mean_frame_ms && !st) {
+            float ms = 0.0f;
+            hipError_t e = hipEventRecord(ev[1], ctx->stream);
+            if (e == hipSuccess) e = hipEventSynchronize(ev[1]);
+            if (e == hipSuccess) e = hipEventElapsedTime(&ms, ev[0], ev[1]);
+            if (e != hipSuccess) st = set_error(ctx, ERAY_E_HIP, "camera path timing: %s", hipGetErrorString(e));
+            else *mean_frame_ms = ms / (float)n;
+        }
+        for (auto e : ev)
+            if (e) hipEventDestroy(e);
+        return st;
+    }
+    Plan plan;
+    if (int st = ensure_plan(ctx, key, n, body, &plan)) return st;
     auto plain = [&](uint32_t f) { return frame((one_chunk ? ctx->d_path : ctx->d_path_all) + f, f); };
     const int st = replay(ctx, plan, n, before, plain, mean_frame_ms);
     if (batched || multi) return st;  // (per-camera slots: the context's setup is still the scene camera's)
