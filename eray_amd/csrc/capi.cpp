@@ -1650,11 +1650,12 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
                                     hipMemcpyDeviceToDevice, ctx->stream));
         return ERAY_OK;
     };
-    // multi-camera builds on two streams enqueued directly, chunk by chunk, instead of replayed
-    // from a captured graph (A/B knob: at C5's frame a trace showed the GPU idle for milliseconds
-    // after the first builds of a graph-replayed path)
-    static const bool multi_direct = std::getenv("ERAY_MULTI_DIRECT") != nullptr;
-    if (multi && multi_direct) {
+    // multi-camera builds on two streams: enqueued directly, chunk by chunk, not replayed from a
+    // captured graph (the graph executor left the GPU idle for milliseconds after a path's first
+    // builds; same-box A/B, scripts/ab_multi.sh: C5's frame 475-485 -> 468 us, 3840x2160 / 70k
+    // 88-91 -> 57-58 us per moving frame; ERAY_MULTI_GRAPHS=1 restores the graphs)
+    static const bool multi_graphs = std::getenv("ERAY_MULTI_GRAPHS") != nullptr;
+    if (multi && !multi_graphs) {
         hipEvent_t ev[2] = {nullptr, nullptr};
         if (mean_frame_ms) {
             for (auto& e : ev) HIP_TRY(ctx, hipEventCreate(&e));
