@@ -3,7 +3,7 @@
 # bench command, then the moving-camera profiles.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/final_b
+OUT=gpurun_out/${TAG:-final_b}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1
@@ -13,4 +13,4 @@ tail -1 $OUT/smoke.log
 timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench20.log 2>&1 || { tail -20 $OUT/bench20.log; exit 1; }
 grep '^{' $OUT/bench20.log | tail -1 > $OUT/bench20.json
 python -c "import json; d=json.load(open('$OUT/bench20.json')); print('bench20', d['value'], d['ms_per_step'], d['roofline']['frac'], 'moving', d['moving_camera']['frame_ms'])"
-TAG=final_b bash scripts/prof_moving_r03.sh
+TAG=${TAG:-final_b} bash scripts/prof_moving_r03.sh
