@@ -192,6 +192,164 @@ def cpu_baseline(mesh, width: int, height: int, fov, seconds: float = 10.0) -> d
             "sample": sample + ", single thread, oracle/eray_oracle.cpp (g++ -O2 -ffp-contract=off)"}
 
 
+class Markers:
+    """ROCTx ranges around the bench's legs (rocprofiler-sdk's roctx; a no-op without it), so that
+    a `rocprofv3 --kernel-trace --marker-trace` run of this command attributes every dispatch to
+    its leg and launch size (scripts/prof_legs.py): the committed per-leg profile rows are the
+    ones the line's kernel figures must reproduce."""
+
+    def __init__(self):
+        self._lib = None
+        import ctypes
+        for name in ("librocprofiler-sdk-roctx.so.1", "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1"):
+            try:
+                self._lib = ctypes.CDLL(name)
+                self._lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                break
+            except (OSError, AttributeError):
+                self._lib = None
+
+    def range(self, name: str):
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            if self._lib:
+                self._lib.roctxRangePushA(name.encode())
+            try:
+                yield
+            finally:
+                if self._lib:
+                    self._lib.roctxRangePop()
+        return cm()
+
+
+MARK = Markers()
+
+
+def kernel_figures(kt: dict) -> dict:
+    """eray_time_frames_ring's dispatch-timestamp durations (ms per launch) as line fields."""
+    F = kt["frames_per_launch"]
+    out = {"launches": kt["launches"], "frames_per_launch": F,
+           "frame_kernel_ms_per_launch": round(kt["frame_kernel_ms"], 6),
+           "frame_kernel_ms_min": round(kt["frame_kernel_min_ms"], 6),
+           "frame_kernel_ms_max": round(kt["frame_kernel_max_ms"], 6),
+           "frame_kernel_ms_per_frame": round(kt["frame_kernel_ms"] / F, 6)}
+    if kt["fill_kernel_ms"] > 0:
+        out["fill_kernel_ms_per_launch"] = round(kt["fill_kernel_ms"], 6)
+        out["launch_span_ms"] = round(kt["launch_span_ms"], 6)
+    return out
+
+
+def empty_scene_context(device: int, width: int, height: int, fov, stream) -> "capi.Context":
+    """The same camera and lights with no object: every pixel is the miss colour (engine.rs:
+    208-213), so its frame kernel is the fill alone — this kernel's write floor for the frame."""
+    ctx = capi.Context(device)
+    ctx.set_stream(stream.cuda_stream)
+    ctx.set_camera(capi.make_camera((0.0, 0.0, 5.0), fov, width, 1.0))
+    ctx.add_light(capi.make_light((0.0, 2.0, 0.0), "ambient", (1.0, 1.0, 1.0), 0.2))
+    ctx.add_light(capi.make_light((1.0, 1.0, 2.0), "point", (1.0, 1.0, 1.0), 1.0))
+    return ctx
+
+
+NS_FACES, NS_SEED, NS_WIDTH, NS_HEIGHT = 69451, 42, 3840, 2160  # north_star: 3840x2160 / 70k tris
+MALL_BYTES = 256 << 20  # MI355X Infinity Cache (MI355X_MICROARCH.md)
+
+
+def north_star_line(device: int, steps: int, slot_counts=None) -> dict:
+    """BASELINE.json north_star's figure: the frame kernel at 3840x2160 over the 69,451-face
+    stand-in (SURVEY.md §8(d) C3 mesh, generated here by eray_amd.meshgen, seed 42) with main.rs's
+    scene and material, against 8 TB/s and against the same kernel's fill-alone floor (an empty
+    scene: the frame's bytes with no detail work) at the same ring size.  Two ring sizes: one slot
+    (each frame rewrites the same 124 MB, which the 256 MiB Infinity Cache absorbs) and the fewest
+    slots whose bytes exceed the Infinity Cache (every frame's stores reach HBM)."""
+    import tempfile
+
+    from eray_amd import meshgen
+
+    t0 = time.perf_counter()
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, "standin_69451.obj")
+        meshgen.generate(path, NS_FACES, NS_SEED)
+        mesh = load_obj_file(path)
+    gen_s = time.perf_counter() - t0
+    W, H = NS_WIDTH, NS_HEIGHT
+    fov = frame_camera_fov(W, H)
+    frame_bytes = 15 * W * H
+    big = 1
+    while big * frame_bytes <= MALL_BYTES:
+        big *= 2
+    slot_counts = slot_counts or [1, big]
+    stream = torch.cuda.Stream()
+    ctx = capi.Context(device)
+    ctx.set_stream(stream.cuda_stream)
+    empty = empty_scene_context(device, W, H, fov, stream)
+    scene = MainScene(ctx, *mesh, W, H, texture=TEXTURE, fov=fov)
+    nmax = max(slot_counts)
+    with torch.cuda.stream(stream):
+        rgb = torch.empty((nmax, H, W, 3), dtype=torch.float32, device="cuda")
+        ppm = torch.empty((nmax, H, W, 3), dtype=torch.uint8, device="cuda")
+        face = torch.full((H, W), -1, dtype=torch.int32, device="cuda")
+    ctx.render(W, H, out_rgb=rgb.data_ptr(), out_face=face.data_ptr())
+    torch.cuda.synchronize()
+    hit = face[face >= 0]
+    hits, hit_faces = int(hit.numel()), int(torch.unique(hit).numel())
+    del face
+    alg = algorithmic_bytes(W * H, hits, hit_faces)
+    steps = max(steps, 20)
+    variants = {}
+    for slots in slot_counts:
+        ring = capi.frame_ring(slots, H, W, 1)
+        out = dict(out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr(), ring=ring)
+        tag = f"ns_slots{slots}"
+        ctx.render_frames(steps, W, H, prepare_only=True, **out)
+        ctx.render_frames(steps, W, H, **out)  # warm
+        torch.cuda.synchronize()
+        with MARK.range(f"{tag}_replay_F1"):
+            t1 = time.perf_counter()
+            ctx.render_frames(steps, W, H, **out)
+            torch.cuda.synchronize()
+            wall = time.perf_counter() - t1
+        with MARK.range(f"{tag}_timed_F1"):
+            kt = ctx.time_frames(steps, W, H, **out)
+        with MARK.range(f"{tag}_fill_floor_F1"):
+            ft = empty.time_frames(steps, W, H, **out)
+        k_ms, f_ms = kt["frame_kernel_ms"], ft["frame_kernel_ms"]
+        gbs = alg / (k_ms * 1e-3) / 1e9
+        fill_gbs = 15 * W * H / (f_ms * 1e-3) / 1e9
+        pmc_key = {"mesh": f"meshgen {NS_FACES} faces seed {NS_SEED}", "frame": [W, H], "rows_per_gpu": H,
+                   "n_gpus": 1, "brute_force": False, "frames_per_launch": 1, "ring_slots": slots}
+        variants[f"slots_{slots}"] = {
+            "ring_slots": slots,
+            "ring_bytes": slots * frame_bytes,
+            "exceeds_infinity_cache": slots * frame_bytes > MALL_BYTES,
+            "ms_per_step": round(wall / steps * 1e3, 6),
+            "value": round(W * H * steps / wall / 1e6, 3),
+            "unit": "Mrays/s",
+            "kernel": kernel_figures(kt),
+            "fill_floor": {"frame_kernel_ms": round(f_ms, 6),
+                           "achieved_gbs": round(fill_gbs, 1),
+                           "frac": round(fill_gbs / PEAK_HBM_GBS, 4),
+                           "scene": "no objects: every pixel the miss colour, same kernel and ring"},
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(gbs / PEAK_HBM_GBS, 4),
+                         "frac_of_fill_floor": round(f_ms / k_ms, 4),
+                         **counter_figures(pmc_record(pmc_key), k_ms)},
+        }
+    del rgb, ppm
+    scene.close()
+    ctx.close()
+    empty.close()
+    return {"workload": f"north_star: {NS_FACES}-face stand-in (eray_amd.meshgen, seed {NS_SEED}), {W}x{H} frame, "
+                        "main.rs scene + material graph, one frame per launch",
+            "frame": [W, H], "triangles": int(len(mesh[0])), "hit_pixels": hits, "hit_faces": hit_faces,
+            "algorithmic_bytes_per_frame": alg, "mesh_generation_s": round(gen_s, 3),
+            "bytes_model": "15 B/pixel written + 16 B texels per hit pixel + 112 B records per hit face",
+            "timing": "kernel = the frame kernel dispatch's own start / end timestamps (hipExtLaunchKernel events, "
+                      "as rocprofv3's kernel trace); step = wall time of graph-replayed frames",
+            "variants": variants}
+
+
 def mesh_label(path: str) -> str:
     """The mesh as the JSON line names it: repo-relative when it is in the tree, else the file name
     (meshes generated on the box by eray_amd.meshgen)."""
@@ -304,7 +462,16 @@ def main() -> None:
                     help="N > 1: interleaved 4-row bands (balanced, default) or contiguous row blocks")
     ap.add_argument("--gather", choices=("scene", "coded"), default="scene",
                     help="N > 1: only the objects' pixel rectangles travel (scene, sync-free) or the coded rows")
+    ap.add_argument("--no-north-star", action="store_true", help="skip the north_star sub-record (N = 1)")
+    ap.add_argument("--north-star-only", action="store_true",
+                    help="print only the north_star sub-record (profiling runs); --ns-slots picks ring sizes")
+    ap.add_argument("--ns-slots", default="", help="comma-separated ring sizes of the north_star leg")
     args = ap.parse_args()
+    if args.north_star_only:
+        torch.cuda.set_device(0)
+        slots = [int(x) for x in args.ns_slots.split(",") if x] or None
+        print(json.dumps({"north_star": north_star_line(0, args.steps, slots)}), flush=True)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -448,9 +615,10 @@ def main() -> None:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(args.steps)
-    torch.cuda.synchronize()
+    with MARK.range(f"steps_F{F}"):
+        t0 = time.perf_counter()
+        run(args.steps)
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -463,12 +631,28 @@ def main() -> None:
     # HIP events on the library's stream (mean device time per frame; F frames per launch), and
     # the latency of one frame alone per launch
     ring1 = ring_args() if world == 1 else ring_args(0, G)
-    kernel_ms = ctx.render_frames(max(args.steps // F, 1) * F, width, H, timed=True, **ring1)
-    latency_ms = None
+    with MARK.range(f"timed_F{F}"):
+        kt = ctx.time_frames(max(args.steps, 64) // F * F, width, H, **ring1)
+    kernel_ms = kt["frame_kernel_ms"] / F  # per frame
+    with MARK.range(f"replay_F{F}"):  # the same frames graph-replayed, bracketed by two events
+        replay_ms = ctx.render_frames(max(args.steps // F, 1) * F, width, H, timed=True, **ring1)
+    latency = None
+    fill_floor = None
     if not args.no_moving_camera:  # (counter runs keep to the measured launches)
         lat_args = dict(ring1)
         lat_args["ring"] = capi.frame_ring(1, alloc_rows, width, 1)
-        latency_ms = ctx.render_frames(max(min(args.steps, 64), 2), width, H, timed=True, **lat_args)
+        with MARK.range("latency_F1"):
+            latency = ctx.time_frames(max(min(args.steps, 64), 2), width, H, **lat_args)
+        if world == 1:  # the same frames with no object: the fill alone, this kernel's write floor
+            empty = empty_scene_context(device, width, H, frame_camera_fov(width, H), stream)
+            with MARK.range(f"fill_floor_F{F}"):
+                ft = empty.time_frames(max(args.steps, 64) // F * F, width, H, **ring1)
+            empty.close()
+            fill_floor = {"frame_kernel_ms_per_launch": round(ft["frame_kernel_ms"], 6),
+                          "frames_per_launch": ft["frames_per_launch"],
+                          "achieved_gbs": round(15 * width * rows * ft["frames_per_launch"] / (ft["frame_kernel_ms"] * 1e-3)
+                                                / 1e9, 1),
+                          "scene": "no objects: every pixel the miss colour, same kernel, ring and launch size"}
     rank_kernel_ms = [kernel_ms]
     gather_ms = None
     if world > 1:
@@ -487,8 +671,13 @@ def main() -> None:
     moving = None
     aa_line = None
     if world == 1 and not args.no_moving_camera:
-        moving = moving_camera(scene, args, width, H, out1, capi.frame_ring(slots, alloc_rows, width, F))
-        aa_line = anti_aliasing_line(scene, args, width, H, out1)
+        with MARK.range("moving_camera"):
+            moving = moving_camera(scene, args, width, H, out1, capi.frame_ring(slots, alloc_rows, width, F))
+        with MARK.range("anti_aliased"):
+            aa_line = anti_aliasing_line(scene, args, width, H, out1)
+    ns_line = None
+    if world == 1 and not args.no_north_star:
+        ns_line = north_star_line(device, args.steps)
 
     if rank == 0:
         # the workload a committed counter summary (profiles/rNN/pmc_traffic*.json) must match
@@ -539,7 +728,8 @@ def main() -> None:
             },
             "frame_ms": round(ms_per_step, 6),
             "render_kernel_ms": round(kernel_ms, 6),
-            "frame_latency_ms": None if latency_ms is None else round(latency_ms, 6),
+            "frame_latency_ms": None if latency is None else round(latency["frame_kernel_ms"], 6),
+            "graph_replay_ms_per_frame": round(replay_ms, 6),
             "material_graph_s": round(t_mat, 4),
             "scene_setup_ms": round(t_setup * 1e3, 3),
             "gather": ({"kind": f"{args.gather}, every frame, batches of {G} overlapped with rendering",
@@ -567,7 +757,13 @@ def main() -> None:
                 "hit_faces": hit_faces,
                 "kernel_ms_per_frame": round(kernel_ms, 6),
                 "kernel_ms_per_launch": round(launch_ms, 6),
+                "timing": "the frame kernel dispatch's own start / end timestamps (hipExtLaunchKernel events, as "
+                          "rocprofv3's kernel trace), mean over the launches of the line's launch size",
+                "kernel_launches": kernel_figures(kt),
+                **({"fill_floor": fill_floor, "frac_of_fill_floor": round(fill_floor["frame_kernel_ms_per_launch"] /
+                                                                            launch_ms, 4)} if fill_floor else {}),
             },
+            "north_star": ns_line,
         }
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(mesh, width, H, frame_camera_fov(width, H), args.cpu_seconds)

@@ -127,6 +127,12 @@ def frame_ring(slots: int, rows: int, width: int, frames_per_launch: int = 0) ->
 _P = C.c_void_p
 _U = C.c_uint32
 _F = C.c_float
+class KernelTimes(C.Structure):  # eray_kernel_times
+    _fields_ = [("launches", C.c_uint32), ("frames_per_launch", C.c_uint32), ("frame_kernel_ms", C.c_float),
+                ("frame_kernel_min_ms", C.c_float), ("frame_kernel_max_ms", C.c_float), ("fill_kernel_ms", C.c_float),
+                ("launch_span_ms", C.c_float)]
+
+
 class ObjMesh(C.Structure):
     _fields_ = [("positions", C.POINTER(C.c_float)), ("normals", C.POINTER(C.c_float)),
                 ("uvs", C.POINTER(C.c_float)), ("triangles", C.c_uint32)]
@@ -168,6 +174,8 @@ SIGNATURES = {
                                           C.POINTER(C.c_float)]),
     "eray_render_prepare_ring": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(FrameRing), _U]),
     "eray_frames_per_launch": (_U, [_P, C.POINTER(RenderParams), _U]),
+    "eray_time_frames_ring": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(FrameRing), _U,
+                                        C.POINTER(KernelTimes)]),
     "eray_render_camera_path_ring": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(FrameRing),
                                                C.POINTER(Camera), _U, C.POINTER(C.c_float)]),
     "eray_pack_ppm": (C.c_int, [_P, _P, _U, _U, _P]),
@@ -191,6 +199,7 @@ DEBUG_SIGNATURES = {
     "eray_debug_unband": (C.c_int, [_P, _P, _P, _U, _U, _U, _U]),
     "eray_debug_coded_unband": (C.c_int, [_P, _P, _P, _U, _U, _U, _U]),
     "eray_debug_scene_gather": (C.c_int, [_P, _P, _P, _U, _U, _U, _U]),
+    "eray_debug_gather_layout": (C.c_int, [C.POINTER(C.c_int32), _U, _U, _U, _U, _U, _U, C.POINTER(C.c_uint32)]),
 }
 
 _lib = None
@@ -273,6 +282,19 @@ def comm_unique_id() -> bytes:
 def band_rows(height: int, band: int, nranks: int, rank: int) -> int:
     """Camera rows of `rank` in the interleaved band split (eray_band_rows)."""
     return lib().eray_band_rows(height, band, nranks, rank)
+
+
+def gather_layout(rects, height: int, width: int, band_rows: int, nranks: int, rank: int) -> dict:
+    """The library's layout of `rank`'s share in the scene-camera gather (eray_debug_gather_layout,
+    host only): rows, bytes per frame and the rectangles (local rows l0..l1, 16-pixel column groups
+    c0..c1, pack offset, row bytes) for the objects' pixel rectangles `rects` (x0, x1, y0, y1)."""
+    flat = [int(v) for r in rects for v in r]
+    arr = (C.c_int32 * max(1, len(flat)))(*flat)
+    out = (C.c_uint32 * (4 + 8 * 8))()
+    check(lib().eray_debug_gather_layout(arr, len(rects), height, width, band_rows, nranks, rank, out))
+    rs = [dict(zip(("l0", "l1", "c0", "c1", "off", "row_bytes", "first"), out[4 + 8 * i: 4 + 8 * i + 7]))
+          for i in range(out[1])]
+    return {"rows": out[0], "bytes": out[2], "packed_rows": out[3], "rects": rs}
 
 
 def comm_destroy(comm: int) -> None:
@@ -477,6 +499,19 @@ class Context:
         ms = C.c_float()
         self._check(lib().eray_render_frames_ring(self._h, C.byref(p), rg, frames, C.byref(ms) if timed else None))
         return ms.value if timed else None
+
+    def time_frames(self, frames, image_width, image_height, row0=0, rows=None, out_rgb=None, out_ppm=None,
+                    out_face=None, flags=RENDER_DEFAULT, band_rows=0, band_stride=0, ring=None) -> dict:
+        """eray_time_frames_ring: the frames as plain launches, each frame kernel's dispatch timed by
+        its own start / end timestamps.  Returns the eray_kernel_times fields (ms per launch)."""
+        if rows is None:
+            rows = image_height - row0
+        p = RenderParams(image_width, image_height, row0, rows, 0, 0, out_rgb or None, out_ppm or None,
+                         out_face or None, flags, 0, band_rows, band_stride)
+        t = KernelTimes()
+        self._check(lib().eray_time_frames_ring(self._h, C.byref(p), C.byref(ring) if ring is not None else None,
+                                                frames, C.byref(t)))
+        return {name: getattr(t, name) for name, _ in KernelTimes._fields_}
 
     def frames_per_launch(self, image_width, image_height, rows=None, slots=64, anti_aliasing=0, bounces=0) -> int:
         """The frames per launch the library picks for a ring of `slots` (eray_frames_per_launch)."""

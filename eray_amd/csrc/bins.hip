@@ -59,11 +59,9 @@ constexpr uint32_t kAccStride = 16;
 // tracer's masks (bin_pixels_jittered, SetupParams::keep_all).
 // waves per SIMD the pair pass is built for: 6 (80 VGPRs, a few spills in the mask path) over
 // 5 (88 VGPRs): C5's moving-camera frame 491 -> 476 us; 8 (64 VGPRs, 22 spills) 525 us
-#ifndef ERAY_PAIRS_WAVES
-#define ERAY_PAIRS_WAVES 6
-#endif
+constexpr int kPairsWaves = 6;
 template <bool kJitter>
-__global__ void __launch_bounds__(kBinWG, ERAY_PAIRS_WAVES) bin_pairs_kernel(const TriCull* __restrict__ cull,
+__global__ void __launch_bounds__(kBinWG, kPairsWaves) bin_pairs_kernel(const TriCull* __restrict__ cull,
                                                            const int4* __restrict__ range,
                                                            const unsigned long long* __restrict__ first_local,
                                                            const unsigned long long* __restrict__ boff,

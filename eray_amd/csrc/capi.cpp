@@ -23,6 +23,8 @@ using namespace eray::gpu;
 
 namespace {
 thread_local std::string g_thread_error;
+constexpr size_t kMaxTags = 512;
+constexpr uint32_t kUnionRing = 4;
 
 struct HostObject {
     std::vector<float> raw;  // T*9 positions | T*9 normals | T*6 uvs
@@ -125,10 +127,26 @@ struct eray_ctx {
     bool state_pending = false;   // a copy into h_state is in flight
     bool state_known = false;     // h_state holds the results of the setup of setup_key
     std::vector<uint64_t> setup_key;  // camera, size, rows and scene generation of the last setup
-    uint64_t setup_gen = 0;       // bumped with every setup of the scene camera (eray_gather_frames' plans)
-    uint32_t setup_span[5] = {0, 0, 0, 0, 0};  // its rows: row0, rows, band_shift, band_mask, band_stride
+    FrameSource setup_src;        // the last enqueued scene-camera setup: its source key and rows
     ObjectDesc* h_objs_state = nullptr;  // pinned copy of the descriptors after that setup (pixel rectangles)
     size_t h_objs_state_cap = 0;
+    // where the frames in output buffers came from (eray_gather_frames): PPM slot address -> the
+    // source of the last render enqueued into it, most recent last (at most kMaxTags)
+    struct SlotTag {
+        uintptr_t ppm;
+        FrameSource src;
+    };
+    std::vector<SlotTag> slot_tags;
+    // camera paths: call counter (kSrcPath keys) and the union of every path camera's object
+    // rectangles — accumulated on the device (d_union_acc, captured into path graphs), then copied
+    // into ring entry seq % kUnionRing on the device and the host, with an event per entry
+    uint64_t path_seq = 0;
+    int32_t* d_union_acc = nullptr;
+    size_t union_cap = 0;  // objects per entry
+    int32_t* h_union = nullptr;
+    uint64_t union_seq[4] = {0, 0, 0, 0};
+    FrameSource union_src[4];
+    hipEvent_t union_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // eray_gather_frames' plan (comm.cpp owns it)
     void* gather_plan = nullptr;
     void (*gather_plan_free)(void*) = nullptr;
@@ -427,6 +445,50 @@ RowSpan row_span(const eray_render_params* rp) {
     return RowSpan{rp->row0, rp->rows, shift, rp->band_rows - 1u, rp->band_stride};
 }
 
+uint64_t fnv1a(const void* data, size_t n, uint64_t h = 1469598103934665603ull) {
+    const unsigned char* p = static_cast<const unsigned char*>(data);
+    for (size_t i = 0; i < n; ++i) {
+        h ^= p[i];
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+
+// The source tag of a render of the scene camera over rows rs: a hash of the camera's value, the
+// scene generation (uploads since the context was made) and Camera::size — what every rank that
+// made the same scene calls computes alike.
+FrameSource scene_source(const eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs) {
+    FrameSource s;
+    s.kind = kSrcScene;
+    uint64_t h = fnv1a(&ctx->camera, sizeof ctx->camera);
+    h = fnv1a(&ctx->scene_gen, sizeof ctx->scene_gen, h);
+    const uint32_t wh[2] = {W, H};
+    s.key = fnv1a(wh, sizeof wh, h);
+    s.W = W;
+    s.H = H;
+    s.row0 = rs.row0;
+    s.rows = rs.rows;
+    s.band_shift = rs.band_shift;
+    s.band_stride = rs.band_stride;
+    return s;
+}
+
+// Records `s` as the source of the n PPM slots ppm + k * stride (k < n).
+void tag_frames(eray_ctx* ctx, const uint8_t* ppm, uint64_t stride, uint32_t n, const FrameSource& s) {
+    if (!ppm) return;
+    auto& v = ctx->slot_tags;
+    for (uint32_t k = 0; k < n; ++k) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(ppm) + (uintptr_t)(k * stride);
+        for (size_t i = 0; i < v.size(); ++i)
+            if (v[i].ppm == a) {
+                v.erase(v.begin() + (std::ptrdiff_t)i);
+                break;
+            }
+        if (v.size() >= kMaxTags) v.erase(v.begin());
+        v.push_back({a, s});
+    }
+}
+
 // The binned objects' first triangles and object indices (bins_alloc's key tables).
 void binned_lists(const eray_ctx* ctx, std::vector<uint32_t>* kbegin, std::vector<uint32_t>* kobj) {
     for (uint32_t i = 0; i < ctx->objects.size(); ++i)
@@ -684,9 +746,7 @@ int sync_setup(eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs, bool wa
             if (nobj)
                 HIP_TRY(ctx, hipMemcpyAsync(ctx->h_objs_state, ctx->d_objs, sizeof(ObjectDesc) * nobj,
                                             hipMemcpyDeviceToHost, ctx->stream));
-            ++ctx->setup_gen;
-            const uint32_t span[5] = {rs.row0, rs.rows, rs.band_shift, rs.band_mask, rs.band_stride};
-            std::memcpy(ctx->setup_span, span, sizeof span);
+            ctx->setup_src = scene_source(ctx, W, H, rs);
             HIP_TRY(ctx, hipEventRecord(ctx->state_ev, ctx->stream));
             ctx->setup_key = std::move(key);
             ctx->state_pending = true;
@@ -766,13 +826,16 @@ int eray_ctx_destroy(eray_ctx* ctx) {
     void* bufs[] = {ctx->d_hot,   ctx->d_shade, ctx->d_cull,  ctx->d_raw,  ctx->d_objs,  ctx->d_lights,
                     ctx->d_prog,  ctx->d_cam,   ctx->d_state, ctx->d_acc,  ctx->d_begin, ctx->d_range,
                     ctx->d_area,  ctx->d_fkey,  ctx->d_path,  ctx->d_path_all, ctx->d_staging,
-                    ctx->d_bcull, ctx->d_bobjs, ctx->d_bstate, ctx->d_tcull};
+                    ctx->d_bcull, ctx->d_bobjs, ctx->d_bstate, ctx->d_tcull, ctx->d_union_acc};
     for (void* b : bufs)
         if (b) hipFree(b);
     if (ctx->h_state) hipHostFree(ctx->h_state);
     for (CamDev* h : ctx->h_path)
         if (h) hipHostFree(h);
     if (ctx->h_objs_state) hipHostFree(ctx->h_objs_state);
+    if (ctx->h_union) hipHostFree(ctx->h_union);
+    for (hipEvent_t ev : ctx->union_ev)
+        if (ev) hipEventDestroy(ev);
     if (ctx->gather_plan && ctx->gather_plan_free) ctx->gather_plan_free(ctx->gather_plan);
     for (auto& g : ctx->graphs) {
         if (g.exec) hipGraphExecDestroy(g.exec);
@@ -1170,13 +1233,25 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
 }
 
 hipError_t launch_frame(eray_ctx* ctx, const FrameParams& p) { return launch_render(p, ctx->lc, ctx->stream); }
+
+// The source tag of frames rendered with p (prepare_render of rp): the scene camera through the
+// frame kernel with its culling setup, or another kind.
+FrameSource render_source(const eray_ctx* ctx, const FrameParams& p, const eray_render_params* rp) {
+    if (p.cull && !p.aa && !p.bounces) return scene_source(ctx, p.cam_w, p.cam_h, row_span(rp));
+    FrameSource s;
+    s.kind = kSrcOther;
+    return s;
+}
 }  // namespace
 
 int eray_render(eray_ctx* ctx, const eray_render_params* rp) {
     FrameParams p;
     bool empty = false;
     if (int st = prepare_render(ctx, rp, &p, &empty)) return st;
-    if (!empty) HIP_TRY(ctx, launch_frame(ctx, p));
+    if (!empty) {
+        HIP_TRY(ctx, launch_frame(ctx, p));
+        tag_frames(ctx, p.out_ppm, 0, 1, render_source(ctx, p, rp));
+    }
     return ERAY_OK;
 }
 
@@ -1390,6 +1465,47 @@ std::vector<unsigned char> ring_key(std::vector<unsigned char> key, const Ring& 
 }
 }  // namespace
 
+// The camera-path rectangle union (eray_gather_frames' layout of path frames): device accumulator
+// for nobj objects and the pinned ring of finished unions.
+int ensure_union(eray_ctx* ctx, uint32_t nobj) {
+    if (ctx->d_union_acc && ctx->union_cap >= nobj) return ERAY_OK;
+    for (hipEvent_t& ev : ctx->union_ev) {
+        if (!ev) HIP_TRY(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIP_TRY(ctx, hipEventSynchronize(ev));  // (a copy into the ring still in flight)
+    }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->d_union_acc) HIP_TRY(ctx, hipFree(ctx->d_union_acc));
+    if (ctx->h_union) HIP_TRY(ctx, hipHostFree(ctx->h_union));
+    ctx->d_union_acc = nullptr;
+    ctx->h_union = nullptr;
+    ctx->union_cap = 0;
+    const size_t n = std::max<uint32_t>(nobj, 1u);
+    HIP_TRY(ctx, hipMalloc((void**)&ctx->d_union_acc, 4 * sizeof(int32_t) * n));
+    HIP_TRY(ctx, hipHostMalloc((void**)&ctx->h_union, 4 * sizeof(int32_t) * n * kUnionRing, hipHostMallocDefault));
+    for (auto& s : ctx->union_seq) s = 0;
+    ctx->union_cap = n;
+    return ERAY_OK;
+}
+int reset_union(eray_ctx* ctx, uint32_t nobj) {
+    if (!nobj) return ERAY_OK;
+    HIP_TRY(ctx, hipMemsetD32Async((hipDeviceptr_t)ctx->d_union_acc, 0x7fffffff, 2 * (size_t)nobj, ctx->stream));
+    HIP_TRY(ctx, hipMemsetD32Async((hipDeviceptr_t)(ctx->d_union_acc + 2 * (size_t)nobj), (int)0x80000000,
+                                   2 * (size_t)nobj, ctx->stream));
+    return ERAY_OK;
+}
+// After path call `seq`'s frames: its union into ring entry seq % kUnionRing on the host.
+int finish_union(eray_ctx* ctx, uint64_t seq, const FrameSource& src, uint32_t nobj) {
+    const uint32_t e = (uint32_t)(seq % kUnionRing);
+    HIP_TRY(ctx, hipEventSynchronize(ctx->union_ev[e]));  // the entry's copy kUnionRing paths back
+    if (nobj)
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->h_union + (size_t)e * 4 * ctx->union_cap, ctx->d_union_acc,
+                                    4 * sizeof(int32_t) * nobj, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipEventRecord(ctx->union_ev[e], ctx->stream));
+    ctx->union_seq[e] = seq;
+    ctx->union_src[e] = src;
+    return ERAY_OK;
+}
+
 extern "C" {
 
 int eray_render_prepare_ring(eray_ctx* ctx, const eray_render_params* rp, const eray_frame_ring* ring, uint32_t frames) {
@@ -1437,16 +1553,89 @@ int eray_render_frames_ring(eray_ctx* ctx, const eray_render_params* rp, const e
         HIP_TRY(ctx, launch_frame(ctx, ring_frames(p, r, f, std::min(r.per_launch, n - f))));
         return ERAY_OK;
     };
-    static const bool plain_launches = std::getenv("ERAY_PLAIN_LAUNCHES") != nullptr;  // (A/B diagnostics)
-    if (!plain_launches)
-        if (int st = ensure_plan(ctx, ring_key(params_key(p, 0), r), frames, body, &plan)) return st;
+    if (int st = ensure_plan(ctx, ring_key(params_key(p, 0), r), frames, body, &plan)) return st;
     auto none = [](uint32_t, uint32_t) { return (int)ERAY_OK; };
     auto plain = [&](uint32_t f) { return body(f, frames); };
-    return replay(ctx, plan, frames, none, plain, mean_frame_ms);
+    const int st = replay(ctx, plan, frames, none, plain, mean_frame_ms);
+    if (!st) tag_frames(ctx, p.out_ppm, r.ppm, std::min(frames, r.slots), render_source(ctx, p, rp));
+    return st;
 }
 
 int eray_render_frames(eray_ctx* ctx, const eray_render_params* rp, uint32_t frames, float* mean_frame_ms) {
     return eray_render_frames_ring(ctx, rp, nullptr, frames, mean_frame_ms);
+}
+
+int eray_time_frames_ring(eray_ctx* ctx, const eray_render_params* rp, const eray_frame_ring* ring, uint32_t frames,
+                          eray_kernel_times* out) {
+    if (!out) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "kernel timing: out is null");
+    *out = eray_kernel_times{};
+    FrameParams p;
+    bool empty = false;
+    if (int st = prepare_render(ctx, rp, &p, &empty, SetupWait::kYes)) return st;
+    if (empty || !frames) return ERAY_OK;
+    if (p.aa || p.bounces)
+        return set_error(ctx, ERAY_E_UNSUPPORTED, "kernel timing: the frame kernel only (no anti-aliasing or bounces)");
+    Ring r;
+    if (int st = make_ring(ctx, rp, p, ring, &r)) return st;
+    const uint32_t F = r.per_launch, L = std::max(1u, frames / F);
+    std::vector<hipEvent_t> ev(4 * (size_t)L, nullptr);
+    auto drop = [&]() {
+        for (auto e : ev)
+            if (e) hipEventDestroy(e);
+    };
+    int st = ERAY_OK;
+    std::vector<uint32_t> fill_used(L, 0u);
+    for (uint32_t l = 0; l < L && !st; ++l) {
+        LaunchCtx lc = ctx->lc;
+        for (int k = 0; k < 4 && !st; ++k) {
+            const hipError_t e = hipEventCreate(&ev[4 * (size_t)l + k]);
+            if (e != hipSuccess) st = set_error(ctx, ERAY_E_HIP, "hipEventCreate: %s", hipGetErrorString(e));
+        }
+        if (st) break;
+        lc.frame_t[0] = ev[4 * (size_t)l];
+        lc.frame_t[1] = ev[4 * (size_t)l + 1];
+        lc.fill_t[0] = ev[4 * (size_t)l + 2];
+        lc.fill_t[1] = ev[4 * (size_t)l + 3];
+        lc.fill_used = &fill_used[l];
+        const hipError_t e = launch_render(ring_frames(p, r, l * F, F), lc, ctx->stream);
+        if (e != hipSuccess) st = set_error(ctx, ERAY_E_HIP, "timed frame launch: %s", hipGetErrorString(e));
+    }
+    hipError_t e = st ? hipSuccess : hipStreamSynchronize(ctx->stream);
+    double sum = 0.0, fill = 0.0, span = 0.0;
+    float lo = 0.0f, hi = 0.0f;
+    uint32_t nfill = 0;
+    for (uint32_t l = 0; l < L && !st && e == hipSuccess; ++l) {
+        hipEvent_t* q = &ev[4 * (size_t)l];
+        float k = 0.0f;
+        if ((e = hipEventElapsedTime(&k, q[0], q[1])) != hipSuccess) break;
+        sum += k;
+        lo = l ? std::min(lo, k) : k;
+        hi = l ? std::max(hi, k) : k;
+        float s = k;
+        if (fill_used[l]) {  // the separate fill beside it: both kernels' span, from the frame kernel's start
+            float f0 = 0.0f, f1 = 0.0f, fk = 0.0f;
+            if ((e = hipEventElapsedTime(&fk, q[2], q[3])) != hipSuccess ||
+                (e = hipEventElapsedTime(&f0, q[0], q[2])) != hipSuccess ||
+                (e = hipEventElapsedTime(&f1, q[0], q[3])) != hipSuccess)
+                break;
+            fill += fk;
+            ++nfill;
+            s = std::max(k, f1) - std::min(0.0f, f0);
+        }
+        span += s;
+    }
+    drop();
+    if (st) return st;
+    if (e != hipSuccess) return set_error(ctx, ERAY_E_HIP, "kernel timing: %s", hipGetErrorString(e));
+    tag_frames(ctx, p.out_ppm, r.ppm, std::min(L * F, r.slots), render_source(ctx, p, rp));
+    out->launches = L;
+    out->frames_per_launch = F;
+    out->frame_kernel_ms = (float)(sum / L);
+    out->frame_kernel_min_ms = lo;
+    out->frame_kernel_max_ms = hi;
+    out->fill_kernel_ms = nfill ? (float)(fill / nfill) : 0.0f;
+    out->launch_span_ms = (float)(span / L);
+    return ERAY_OK;
 }
 
 int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, const eray_frame_ring* ring,
@@ -1498,6 +1687,9 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
             }
         }
         ctx->camera = saved;
+        FrameSource other;
+        other.kind = kSrcOther;
+        tag_frames(ctx, p.out_ppm, r.ppm, std::min(n, r.slots), other);
         if (mean_frame_ms) {
             hipError_t e = hipEventRecord(ev[1], ctx->stream);
             float ms = 0.0f;
@@ -1549,6 +1741,19 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
         r.per_launch = 1;  // a setup (screen bins) per frame: one frame per launch
     }
     const uint32_t T = ctx->total_tris, nobj = (uint32_t)ctx->objects.size();
+    // this call's frames are camera-path frames (eray_gather_frames): every camera's object
+    // rectangles fold into the union of the call
+    FrameSource psrc;
+    psrc.kind = kSrcPath;
+    psrc.key = ++ctx->path_seq;
+    psrc.W = W;
+    psrc.H = H;
+    psrc.row0 = rs.row0;
+    psrc.rows = rs.rows;
+    psrc.band_shift = rs.band_shift;
+    psrc.band_stride = rs.band_stride;
+    if (int st = ensure_union(ctx, nobj)) return st;
+    if (int st = reset_union(ctx, nobj)) return st;
     if (batched) {
         if (int st = ensure(ctx, &ctx->d_bcull, &ctx->bcull_cap, (size_t)kGraphFrames * T)) return st;
         if (int st = ensure(ctx, &ctx->d_bobjs, &ctx->bobjs_cap, (size_t)kGraphFrames * nobj)) return st;
@@ -1566,6 +1771,7 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
             sp.objs_src = ctx->d_objs;
             sp.state = ctx->d_bstate;
             HIP_TRY(ctx, launch_camera_setup_batch(sp, count, ctx->stream));
+            HIP_TRY(ctx, launch_rect_union(ctx->d_bobjs, nobj, count, ctx->d_union_acc, ctx->stream));
         }
         if (slot % r.per_launch) return ERAY_OK;
         FrameParams q = ring_frames(p, r, f, std::min(r.per_launch, count - slot));
@@ -1588,6 +1794,7 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
         if (k == 0) {
             if (b == 0) {
                 if (int st = enqueue_multi_setup(ctx, m, cams, std::min(K, count), W, H, rs, ctx->stream)) return st;
+                HIP_TRY(ctx, launch_rect_union(m.objs, nobj, std::min(K, count), ctx->d_union_acc, ctx->stream));
                 HIP_TRY(ctx, hipEventRecord(ctx->mc_fork, ctx->stream));
             } else {
                 HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->mc_ready[b & 1u], 0));
@@ -1598,6 +1805,8 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
                 if (int st = enqueue_multi_setup(ctx, m2, cams + (b + 1) * K, std::min(K, count - (b + 1) * K), W, H, rs,
                                                  ctx->mc_stream))
                     return st;
+                HIP_TRY(ctx, launch_rect_union(m2.objs, nobj, std::min(K, count - (b + 1) * K), ctx->d_union_acc,
+                                               ctx->mc_stream));
                 HIP_TRY(ctx, hipEventRecord(ctx->mc_ready[(b + 1) & 1u], ctx->mc_stream));
             }
         }
@@ -1625,6 +1834,7 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
             return st;
         }
         if (int st = enqueue_setup(ctx, cam, W, H, row_span(rp), false)) return st;
+        HIP_TRY(ctx, launch_rect_union(ctx->d_objs, nobj, 1, ctx->d_union_acc, ctx->stream));
         HIP_TRY(ctx, launch_frame(ctx, ring_frames(p, r, f, 1)));
         return ERAY_OK;
     };
@@ -1634,7 +1844,7 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
     };
     std::vector<unsigned char> key = ring_key(params_key(p, batched ? 2 : 1), r);
     for (const void* ptr : {(const void*)ctx->d_path, (const void*)ctx->d_bcull, (const void*)ctx->d_bobjs,
-                            (const void*)ctx->d_bstate})
+                            (const void*)ctx->d_bstate, (const void*)ctx->d_union_acc})
         key.insert(key.end(), reinterpret_cast<const unsigned char*>(&ptr),
                    reinterpret_cast<const unsigned char*>(&ptr) + sizeof ptr);
     // the captured setup and bins kernels hold every bin buffer's address: a reallocation (a grown
@@ -1653,9 +1863,8 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
     // multi-camera builds on two streams: enqueued directly, chunk by chunk, not replayed from a
     // captured graph (the graph executor left the GPU idle for milliseconds after a path's first
     // builds; same-box A/B, scripts/ab_multi.sh: C5's frame 475-485 -> 468 us, 3840x2160 / 70k
-    // 88-91 -> 57-58 us per moving frame; ERAY_MULTI_GRAPHS=1 restores the graphs)
-    static const bool multi_graphs = std::getenv("ERAY_MULTI_GRAPHS") != nullptr;
-    if (multi && !multi_graphs) {
+    // 88-91 -> 57-58 us per moving frame)
+    if (multi) {
         hipEvent_t ev[2] = {nullptr, nullptr};
         if (mean_frame_ms) {
             for (auto& e : ev) HIP_TRY(ctx, hipEventCreate(&e));
@@ -1667,6 +1876,8 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
             st = before(first, count);
             for (uint32_t f = 0; f < count && !st; ++f) st = multi_frame(ctx->d_path, f, count, first + f);
         }
+        if (!st) st = finish_union(ctx, psrc.key, psrc, nobj);
+        if (!st) tag_frames(ctx, p.out_ppm, r.ppm, std::min(n, r.slots), psrc);
         if (mean_frame_ms && !st) {
             float ms = 0.0f;
             hipError_t e = hipEventRecord(ev[1], ctx->stream);
@@ -1682,13 +1893,14 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
     Plan plan;
     if (int st = ensure_plan(ctx, key, n, body, &plan)) return st;
     auto plain = [&](uint32_t f) { return frame((one_chunk ? ctx->d_path : ctx->d_path_all) + f, f); };
-    const int st = replay(ctx, plan, n, before, plain, mean_frame_ms);
+    int st = replay(ctx, plan, n, before, plain, mean_frame_ms);
+    if (!st) st = finish_union(ctx, psrc.key, psrc, nobj);
+    if (!st) tag_frames(ctx, p.out_ppm, r.ppm, std::min(n, r.slots), psrc);
     if (batched || multi) return st;  // (per-camera slots: the context's setup is still the scene camera's)
     // the device state now belongs to the path's last camera: the scene camera is set up again at
     // its next render (whose count copy also grows the bins' capacity when a camera needed more;
     // no copy here: waiting for an earlier one would wait for that call's frames)
     ctx->setup_key.clear();
-    ++ctx->setup_gen;
     ctx->state_known = false;
     return st;
 }
@@ -1719,28 +1931,80 @@ int eray_ppm_header(uint32_t w, uint32_t h, char* buf, size_t cap, size_t* len) 
 
 }  // extern "C"
 
-// The scene camera's current setup as eray_gather_frames reads it (waits for its host copies).
-int eray_internal_scene_layout(eray_ctx* ctx, SceneLayout* out) {
+// The source of the n frames local + k * stride (k < n) as this context last rendered them
+// (tag_frames); every frame must have the same one.
+int eray_internal_frame_source(eray_ctx* ctx, const uint8_t* local, uint64_t stride, uint32_t n, FrameSource* out) {
     if (!ctx || !out) return ERAY_E_INVALID_ARGUMENT;
-    if (ctx->setup_key.empty())
-        return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "no current setup of the scene camera: render it first");
-    if (ctx->state_pending) {
-        HIP_TRY(ctx, hipEventSynchronize(ctx->state_ev));
-        state_arrived(ctx);
+    *out = FrameSource{};
+    for (uint32_t k = 0; k < n; ++k) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(local) + (uintptr_t)(k * stride);
+        const eray_ctx::SlotTag* t = nullptr;
+        for (auto it = ctx->slot_tags.rbegin(); it != ctx->slot_tags.rend(); ++it)
+            if (it->ppm == a) {
+                t = &*it;
+                break;
+            }
+        if (!t)
+            return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "gather: frame %u at %p was not rendered by this context", k,
+                             (const void*)a);
+        if (k == 0) {
+            *out = t->src;
+        } else if (t->src.kind != out->kind || t->src.key != out->key) {
+            return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "gather: frames 0 and %u come from different renders", k);
+        }
     }
-    if (!ctx->state_known || ctx->setup_key.empty())
-        return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "the scene camera's setup is not current: render it first");
-    out->gen = ctx->setup_gen;
-    eray_camera_size(&ctx->camera, &out->W, &out->H);
-    out->row0 = ctx->setup_span[0];
-    out->rows = ctx->setup_span[1];
-    out->band_shift = ctx->setup_span[2];
-    out->band_stride = ctx->setup_span[4];
+    if (out->kind == kSrcOther)
+        return set_error(ctx, ERAY_E_INVALID_ARGUMENT,
+                         "gather: the frames were rendered with anti-aliasing, bounces or brute force (no pixel rectangles)");
+    return ERAY_OK;
+}
+
+// The pixel rectangles of `src` (waits for their host copy): the last scene-camera setup when it
+// is src's (same camera, scene and rows), or the union of camera path src.key's cameras while it
+// is among the last kUnionRing paths.
+int eray_internal_source_layout(eray_ctx* ctx, const FrameSource& src, SceneLayout* out) {
+    if (!ctx || !out) return ERAY_E_INVALID_ARGUMENT;
+    auto same_rows = [](const FrameSource& a, const FrameSource& b) {
+        return a.W == b.W && a.H == b.H && a.row0 == b.row0 && a.rows == b.rows && a.band_shift == b.band_shift &&
+               a.band_stride == b.band_stride;
+    };
+    out->src = src;
     out->rects.clear();
-    for (size_t i = 0; i < ctx->objects.size(); ++i) {
-        const int32_t* r = ctx->h_objs_state[i].g.rect;
-        out->rects.push_back({r[0], r[1], r[2], r[3]});
+    const size_t nobj = ctx->objects.size();
+    if (src.kind == kSrcScene) {
+        const FrameSource& s = ctx->setup_src;
+        if (s.kind != kSrcScene || s.key != src.key || !same_rows(s, src))
+            return set_error(ctx, ERAY_E_INVALID_ARGUMENT,
+                             "gather: the scene camera's last setup is not the one these frames were rendered with");
+        if (ctx->state_pending) {
+            HIP_TRY(ctx, hipEventSynchronize(ctx->state_ev));
+            state_arrived(ctx);
+        }
+        for (size_t i = 0; i < nobj; ++i) {
+            const int32_t* r = ctx->h_objs_state[i].g.rect;
+            out->rects.push_back({r[0], r[1], r[2], r[3]});
+        }
+        return ERAY_OK;
     }
+    if (src.kind == kSrcPath) {
+        const uint32_t e = (uint32_t)(src.key % kUnionRing);
+        if (ctx->union_seq[e] != src.key || !same_rows(ctx->union_src[e], src))
+            return set_error(ctx, ERAY_E_INVALID_ARGUMENT,
+                             "gather: these camera-path frames are older than the last %u paths", kUnionRing);
+        HIP_TRY(ctx, hipEventSynchronize(ctx->union_ev[e]));
+        const int32_t* u = ctx->h_union + (size_t)e * 4 * ctx->union_cap;
+        for (size_t i = 0; i < nobj; ++i)
+            out->rects.push_back({u[2 * i], u[2 * nobj + 2 * i], u[2 * i + 1], u[2 * nobj + 2 * i + 1]});
+        return ERAY_OK;
+    }
+    return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "gather: frames of an unknown source");
+}
+// The source of the scene camera's last setup (diagnostics: eray_debug_scene_gather).
+int eray_internal_scene_setup_source(eray_ctx* ctx, FrameSource* out) {
+    if (!ctx || !out) return ERAY_E_INVALID_ARGUMENT;
+    if (ctx->setup_src.kind != kSrcScene)
+        return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "no setup of the scene camera: render it first");
+    *out = ctx->setup_src;
     return ERAY_OK;
 }
 void** eray_internal_gather_plan(eray_ctx* ctx, void (*free_fn)(void*)) {

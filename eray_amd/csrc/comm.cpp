@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "../../include/eray_hip.h"
@@ -24,7 +25,10 @@ static_assert(ERAY_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size");
 // the context's slot for this file's gather plan
 int eray_internal_error(eray_ctx* ctx, int code, const char* msg);
 void* eray_internal_staging(eray_ctx* ctx, size_t bytes);
-int eray_internal_scene_layout(eray_ctx* ctx, eray::gpu::SceneLayout* out);
+int eray_internal_frame_source(eray_ctx* ctx, const uint8_t* local, uint64_t stride, uint32_t n,
+                               eray::gpu::FrameSource* out);
+int eray_internal_source_layout(eray_ctx* ctx, const eray::gpu::FrameSource& src, eray::gpu::SceneLayout* out);
+int eray_internal_scene_setup_source(eray_ctx* ctx, eray::gpu::FrameSource* out);
 void** eray_internal_gather_plan(eray_ctx* ctx, void (*free_fn)(void*));
 int eray_internal_use_device(eray_ctx* ctx);
 
@@ -288,11 +292,16 @@ struct RankLayout {        // a rank's rectangles and its share of rank 0's rece
     uint32_t rows, packed_rows;
     uint32_t pad[2];
 };
-constexpr int kXchgInts = 1 + 4 * kPlanRects;
+// A rank's record in the plan exchange: [status, source kind, key low, key high | nrect, then
+// nrect x (l0, l1, c0, c1)] — every rank learns every rank's status and source, so all of them
+// accept the plan or all fail together.
+constexpr int kXchgHead = 4;
+constexpr int kXchgInts = kXchgHead + 1 + 4 * kPlanRects;
 
 struct GatherPlan {
     void* comm = nullptr;
-    uint64_t gen = 0;
+    uint32_t kind = 0;
+    uint64_t key = 0;
     uint32_t H = 0, W = 0, band = 0, nranks = 0, rank = 0;
     bool valid = false;
     std::vector<RankLayout> ranks;
@@ -329,9 +338,10 @@ RankRows rank_rows(uint32_t H, uint32_t band, uint32_t N, uint32_t rank) {
 // This rank's rectangles: the objects' pixel rectangles in its local rows and 16-pixel column
 // groups, overlapping ones merged (as camera_setup_kernel merges the detail rectangles), more than
 // kPlanRects merged into the last.
-std::vector<std::array<int32_t, 4>> my_rects(const eray::gpu::SceneLayout& L, const RankRows& rr, uint32_t W) {
+std::vector<std::array<int32_t, 4>> my_rects(const std::vector<std::array<int32_t, 4>>& rects, const RankRows& rr,
+                                             uint32_t W) {
     std::vector<std::array<int32_t, 4>> out;
-    for (const auto& q : L.rects) {
+    for (const auto& q : rects) {
         int32_t x0 = std::max(q[0], 0), x1 = std::min(q[1], (int32_t)W - 1), l0, l1;
         if (x0 > x1 || q[2] > q[3]) continue;
         eray::gpu::band_local_range(rr.row0, rr.shift, rr.stride, q[2], q[3], &l0, &l1);
@@ -358,6 +368,13 @@ std::vector<std::array<int32_t, 4>> my_rects(const eray::gpu::SceneLayout& L, co
             }
     }
     return out;
+}
+
+// The rectangle part of an exchange record (nrect, then the rectangles).
+void write_rects(const std::vector<std::array<int32_t, 4>>& mine, int32_t* rec) {
+    rec[0] = (int32_t)mine.size();
+    for (size_t i = 0; i < mine.size(); ++i)
+        for (int q = 0; q < 4; ++q) rec[1 + 4 * i + q] = mine[i][q];
 }
 
 RankLayout layout_of(const int32_t* rec, uint32_t rows) {
@@ -575,37 +592,24 @@ int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8
 }  // extern "C"
 
 namespace {
-// Builds (or reuses) the scene-camera plan of this rank: a collective (every rank calls it at the
-// same point), synchronising the stream once when the camera's setup changed.
-int scene_plan(eray_ctx* ctx, ncclComm_t c, int nranks, int rank, uint32_t H, uint32_t W, uint32_t band,
-               GatherPlan** out) {
-    GatherPlan*& P = *reinterpret_cast<GatherPlan**>(eray_internal_gather_plan(ctx, plan_free));
-    eray::gpu::SceneLayout L;
-    if (int st = eray_internal_scene_layout(ctx, &L)) return st;
-    if (P && P->valid && P->comm == (void*)c && P->gen == L.gen && P->H == H && P->W == W && P->band == band &&
-        P->nranks == (uint32_t)nranks && P->rank == (uint32_t)rank) {
-        *out = P;
-        return ERAY_OK;
-    }
-    if (!P) P = new (std::nothrow) GatherPlan();
-    if (!P) return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "gather plan");
+// Exchanges the ranks' records for a new plan (a collective: every rank calls it at the same
+// point, one stream synchronisation).  `status` is this rank's verdict (ERAY_OK, or the error it
+// met looking up its frames' source and rectangles); on success every rank holds every rank's
+// layout, otherwise every rank returns an error.
+int exchange_plan(eray_ctx* ctx, ncclComm_t c, int nranks, int rank, uint32_t H, uint32_t W, uint32_t band,
+                  const eray::gpu::FrameSource& src, int status, const std::vector<std::array<int32_t, 4>>& rects,
+                  GatherPlan* P) {
     P->valid = false;
-    if (L.W != W || L.H != H)
-        return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "scene-camera gather: the frame size is not the scene camera's");
-    const RankRows rr = rank_rows(H, band, (uint32_t)nranks, (uint32_t)rank);
-    if (L.row0 != rr.row0 || L.rows != rr.rows || L.band_shift != rr.shift || (band && L.band_stride != rr.stride))
-        return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT,
-                                   "scene-camera gather: the scene camera's last render covered other rows than this rank's share");
-    const auto mine = my_rects(L, rr, W);
-    int32_t rec[kXchgInts] = {};
-    rec[0] = (int32_t)mine.size();
-    for (size_t i = 0; i < mine.size(); ++i)
-        for (int q = 0; q < 4; ++q) rec[1 + 4 * i + q] = mine[i][q];
     hipStream_t s = (hipStream_t)eray_get_stream(ctx);
     hipError_t he;
     if (!P->xchg && (he = hipMalloc((void**)&P->xchg, sizeof(int32_t) * kXchgInts * (size_t)(kMaxCodedRanks + 1))) != hipSuccess)
         return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, hipGetErrorString(he));
-    if (nranks > kMaxCodedRanks) return eray_internal_error(ctx, ERAY_E_UNSUPPORTED, "scene-camera gather: more than 64 ranks");
+    int32_t rec[kXchgInts] = {};
+    rec[0] = status;
+    rec[1] = (int32_t)src.kind;
+    rec[2] = (int32_t)(uint32_t)src.key;
+    rec[3] = (int32_t)(uint32_t)(src.key >> 32);
+    if (status == ERAY_OK) write_rects(my_rects(rects, rank_rows(H, band, (uint32_t)nranks, (uint32_t)rank), W), rec + kXchgHead);
     std::vector<int32_t> all((size_t)kXchgInts * (size_t)nranks);
     if ((he = hipMemcpyAsync(P->xchg, rec, sizeof rec, hipMemcpyHostToDevice, s)) != hipSuccess)
         return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
@@ -615,10 +619,23 @@ int scene_plan(eray_ctx* ctx, ncclComm_t c, int nranks, int rank, uint32_t H, ui
             hipSuccess ||
         (he = hipStreamSynchronize(s)) != hipSuccess)
         return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+    for (int q = 0; q < nranks; ++q) {  // every rank reaches the same verdict from the same records
+        const int32_t* o = all.data() + (size_t)q * kXchgInts;
+        if (o[0] != ERAY_OK) {
+            if (status != ERAY_OK) return status;  // (this rank's own message is already set)
+            char msg[128];
+            std::snprintf(msg, sizeof msg, "scene-camera gather: rank %d could not use its frames (status %d)", q, o[0]);
+            return eray_internal_error(ctx, o[0], msg);
+        }
+        if (o[1] != rec[1] || o[2] != rec[2] || o[3] != rec[3])
+            return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT,
+                                       "scene-camera gather: the ranks' frames come from different cameras or paths");
+    }
     P->ranks.assign((size_t)nranks, RankLayout{});
     P->total = 0;
     for (int q = 0; q < nranks; ++q) {
-        RankLayout R = layout_of(all.data() + (size_t)q * kXchgInts, rank_rows(H, band, (uint32_t)nranks, (uint32_t)q).rows);
+        RankLayout R = layout_of(all.data() + (size_t)q * kXchgInts + kXchgHead,
+                                 rank_rows(H, band, (uint32_t)nranks, (uint32_t)q).rows);
         R.off = P->total;
         P->total += R.bytes;
         P->ranks[(size_t)q] = R;
@@ -632,14 +649,14 @@ int scene_plan(eray_ctx* ctx, ncclComm_t c, int nranks, int rank, uint32_t H, ui
             return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
     }
     P->comm = (void*)c;
-    P->gen = L.gen;
+    P->kind = src.kind;
+    P->key = src.key;
     P->H = H;
     P->W = W;
     P->band = band;
     P->nranks = (uint32_t)nranks;
     P->rank = (uint32_t)rank;
     P->valid = true;
-    *out = P;
     return ERAY_OK;
 }
 
@@ -656,14 +673,16 @@ int grow(eray_ctx* ctx, GatherPlan* P, size_t bytes) {
     return ERAY_OK;
 }
 
-// Pack (every rank), transfer, assemble (rank 0) `B` frames with plan P.
+// Pack (every rank), transfer, assemble (rank 0) `B` frames with plan P.  fail_safe (this rank's
+// own arguments are unusable): only the transfers of the plan, so the other ranks' matching
+// sends and receives complete — no kernel touches the caller's buffers.
 int scene_gather(eray_ctx* ctx, ncclComm_t c, const GatherPlan& P, const uint8_t* local, uint64_t local_stride,
-                 uint8_t* frames, uint64_t frame_stride, uint32_t B) {
+                 uint8_t* frames, uint64_t frame_stride, uint32_t B, bool fail_safe = false) {
     hipStream_t s = (hipStream_t)eray_get_stream(ctx);
     const RankLayout& me = P.ranks[P.rank];
     uint8_t* mine = P.rank == 0 ? P.buf + (size_t)B * me.off : P.buf;
     hipError_t he;
-    if (me.bytes) {
+    if (me.bytes && !fail_safe) {
         gather_pack_kernel<<<dim3(me.packed_rows, B), 256, 0, s>>>(local, local_stride, mine, me, P.W);
         if ((he = hipGetLastError()) != hipSuccess) return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
     }
@@ -681,7 +700,7 @@ int scene_gather(eray_ctx* ctx, ncclComm_t c, const GatherPlan& P, const uint8_t
         if (r != ncclSuccess) return nccl_error(ctx, "ncclSend/ncclRecv", r);
         if (r2 != ncclSuccess) return nccl_error(ctx, "ncclGroupEnd", r2);
     }
-    if (P.rank == 0) {
+    if (P.rank == 0 && !fail_safe) {
         gather_assemble_kernel<<<dim3(P.H, B), 256, 0, s>>>(P.buf, P.d_ranks, B, frames, frame_stride, P.H, P.W, P.band,
                                                            P.nranks);
         if ((he = hipGetLastError()) != hipSuccess) return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
@@ -705,12 +724,48 @@ int eray_gather_frames(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uin
     if (r == ncclSuccess) r = ncclCommUserRank(c, &rank);
     if (r != ncclSuccess) return nccl_error(ctx, "gather: communicator", r);
     if (!nframes || !height || !width) return ERAY_OK;
-    const bool aligned = width % 16 == 0 && ((reinterpret_cast<uintptr_t>(local) | reinterpret_cast<uintptr_t>(frames) |
-                                              local_stride | frame_stride) & 15) == 0;
     const bool rows_ok = band_rows ? band_rows >= 4 && !(band_rows & (band_rows - 1)) : height % (uint32_t)nranks == 0;
-    if ((flags & ERAY_GATHER_SCENE_CAMERA) && aligned && rows_ok && local && (rank != 0 || frames)) {
-        GatherPlan* P = nullptr;
-        if (int st = scene_plan(ctx, c, nranks, rank, height, width, band_rows, &P)) return st;
+    if (flags & ERAY_GATHER_SCENE_CAMERA) {
+        // The transport is chosen from arguments every rank shares (flags, the frame size, the
+        // split), never from this rank's own pointers or state, so all ranks take the same path.
+        if (width % 16 || !rows_ok)
+            return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT,
+                                       "scene-camera gather: width must be a multiple of 16 and the rows a valid split");
+        if (nranks > kMaxCodedRanks)
+            return eray_internal_error(ctx, ERAY_E_UNSUPPORTED, "scene-camera gather: more than 64 ranks");
+        // this rank's verdict on its own arguments and frames
+        const bool aligned = ((reinterpret_cast<uintptr_t>(local) | local_stride) & 15) == 0 &&
+                             (rank != 0 || ((reinterpret_cast<uintptr_t>(frames) | frame_stride) & 15) == 0);
+        int status = ERAY_OK;
+        eray::gpu::FrameSource src;
+        if (!local || (rank == 0 && !frames) || !aligned)
+            status = eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT,
+                                         "scene-camera gather: null or unaligned (16 B) buffers or strides");
+        if (status == ERAY_OK) status = eray_internal_frame_source(ctx, local, local_stride, nframes, &src);
+        const RankRows rr = rank_rows(height, band_rows, (uint32_t)nranks, (uint32_t)rank);
+        if (status == ERAY_OK && (src.W != width || src.H != height || src.row0 != rr.row0 || src.rows != rr.rows ||
+                                  src.band_shift != rr.shift || (band_rows && src.band_stride != rr.stride)))
+            status = eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT,
+                                         "scene-camera gather: the frames cover other rows or another frame size than "
+                                         "this rank's share");
+        GatherPlan*& P = *reinterpret_cast<GatherPlan**>(eray_internal_gather_plan(ctx, plan_free));
+        if (!P) P = new (std::nothrow) GatherPlan();
+        if (!P) return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "gather plan");
+        const bool cached = P->valid && P->comm == (void*)c && P->H == height && P->W == width &&
+                            P->band == band_rows && P->nranks == (uint32_t)nranks && P->rank == (uint32_t)rank;
+        if (status != ERAY_OK && cached) {
+            // the other ranks (same calls, same plan) go ahead with this plan's transfers: take part
+            // in them, touch nothing, and report the error
+            const size_t need = rank == 0 ? (size_t)nframes * P->total : (size_t)nframes * P->ranks[(size_t)rank].bytes;
+            std::string msg = eray_last_error(ctx);
+            if (grow(ctx, P, need) == ERAY_OK) scene_gather(ctx, c, *P, local, local_stride, frames, frame_stride, nframes, true);
+            return eray_internal_error(ctx, status, msg.c_str());
+        }
+        if (!cached || P->kind != src.kind || P->key != src.key) {  // a new plan: every rank exchanges
+            eray::gpu::SceneLayout L;
+            if (status == ERAY_OK) status = eray_internal_source_layout(ctx, src, &L);
+            if (int st = exchange_plan(ctx, c, nranks, rank, height, width, band_rows, src, status, L.rects, P)) return st;
+        }
         const size_t need = rank == 0 ? (size_t)nframes * P->total : (size_t)nframes * P->ranks[(size_t)rank].bytes;
         if (int st = grow(ctx, P, need)) return st;
         return scene_gather(ctx, c, *P, local, local_stride, frames, frame_stride, nframes);
@@ -719,6 +774,35 @@ int eray_gather_frames(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uin
         if (int st = eray_gather_rows(ctx, nccl_comm, local ? local + k * local_stride : nullptr,
                                       frames ? frames + k * frame_stride : nullptr, height, width, band_rows))
             return st;
+    return ERAY_OK;
+}
+
+// Diagnostics (tests, host only): rank `rank`'s share of the scene-camera gather of `nranks` ranks
+// for objects whose pixel rectangles are `rects` (n x (x0, x1, y0, y1), camera rows) — the layout
+// exchange_plan builds from that rank's record.  out (4 + 8 * 8 words): rows, nrect, bytes per
+// frame, packed rows, then per rectangle l0, l1, c0, c1 (local rows, 16-pixel column groups), its
+// byte offset in the rank's per-frame pack, its row bytes, its first packed row, 0.
+int eray_debug_gather_layout(const int32_t* rects, uint32_t n, uint32_t height, uint32_t width, uint32_t band_rows,
+                             uint32_t nranks, uint32_t rank, uint32_t* out) {
+    if ((n && !rects) || !out || !nranks || rank >= nranks || width % 16 ||
+        (band_rows && (band_rows < 4 || (band_rows & (band_rows - 1)))) || (!band_rows && height % nranks))
+        return eray_internal_error(nullptr, ERAY_E_INVALID_ARGUMENT, "gather layout: bad arguments");
+    std::vector<std::array<int32_t, 4>> rs;
+    for (uint32_t i = 0; i < n; ++i) rs.push_back({rects[4 * i], rects[4 * i + 1], rects[4 * i + 2], rects[4 * i + 3]});
+    const RankRows rr = rank_rows(height, band_rows, nranks, rank);
+    int32_t rec[kXchgInts - kXchgHead] = {};
+    write_rects(my_rects(rs, rr, width), rec);
+    const RankLayout R = layout_of(rec, rr.rows);
+    std::memset(out, 0, sizeof(uint32_t) * (4 + 8 * kPlanRects));
+    out[0] = R.rows;
+    out[1] = R.nrect;
+    out[2] = R.bytes;
+    out[3] = R.packed_rows;
+    for (uint32_t i = 0; i < R.nrect; ++i) {
+        const GatherRect& g = R.r[i];
+        const uint32_t v[8] = {(uint32_t)g.l0, (uint32_t)g.l1, (uint32_t)g.c0, (uint32_t)g.c1, g.off, g.row_bytes, g.first, 0u};
+        std::memcpy(out + 4 + 8 * i, v, sizeof v);
+    }
     return ERAY_OK;
 }
 
@@ -732,9 +816,11 @@ int eray_debug_scene_gather(eray_ctx* ctx, const uint8_t* staging, uint8_t* fram
     if (!ctx || !staging || !frame || !nranks || nranks > (uint32_t)kMaxCodedRanks || width % 16 ||
         (band_rows && (band_rows < 4 || (band_rows & (band_rows - 1)))) || (!band_rows && height % nranks))
         return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "scene gather: bad arguments");
+    eray::gpu::FrameSource src;
     eray::gpu::SceneLayout L;
-    if (int st = eray_internal_scene_layout(ctx, &L)) return st;
-    if (L.W != width || L.H != height || L.row0 != 0 || L.rows != height || L.band_shift != 31u)
+    if (int st = eray_internal_scene_setup_source(ctx, &src)) return st;
+    if (int st = eray_internal_source_layout(ctx, src, &L)) return st;
+    if (src.W != width || src.H != height || src.row0 != 0 || src.rows != height || src.band_shift != 31u)
         return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "scene gather: render the whole scene-camera frame first");
     GatherPlan P;
     P.H = height;
@@ -745,11 +831,8 @@ int eray_debug_scene_gather(eray_ctx* ctx, const uint8_t* staging, uint8_t* fram
     const uint32_t rows_max = rank_rows(height, band_rows, nranks, 0).rows;
     for (uint32_t q = 0; q < nranks; ++q) {
         const RankRows rr = rank_rows(height, band_rows, nranks, q);
-        const auto mine = my_rects(L, rr, width);
-        int32_t rec[kXchgInts] = {};
-        rec[0] = (int32_t)mine.size();
-        for (size_t i = 0; i < mine.size(); ++i)
-            for (int k = 0; k < 4; ++k) rec[1 + 4 * i + k] = mine[i][k];
+        int32_t rec[kXchgInts - kXchgHead] = {};
+        write_rects(my_rects(L.rects, rr, width), rec);
         RankLayout R = layout_of(rec, rr.rows);
         R.off = P.total;
         P.total += R.bytes;

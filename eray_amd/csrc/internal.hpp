@@ -332,15 +332,26 @@ hipError_t launch_camera_setup(const SetupParams& sp, hipStream_t s);
 // kSetupBatchMaxObjects objects (every object's union stays in the workgroup's LDS).
 constexpr uint32_t kSetupBatchMaxObjects = 256;
 hipError_t launch_camera_setup_batch(const SetupParams& sp, uint32_t ncam, hipStream_t s);
+// Folds the pixel rectangles of `ncam` cameras' descriptor copies (objs + k * nobj, k < ncam) into
+// the per-object union, atomically: acc[2 o], acc[2 o + 1] = min x0, min y0 (starting at INT_MAX),
+// acc[2 nobj + 2 o], acc[2 nobj + 2 o + 1] = max x1, max y1 (starting at INT_MIN) — a camera
+// path's gather layout.
+hipError_t launch_rect_union(const ObjectDesc* objs, uint32_t nobj, uint32_t ncam, int32_t* acc, hipStream_t s);
 // Writes `cam` into the device camera slot (kernel arguments: no host staging buffer to race).
 hipError_t launch_set_camera(const CamDev& cam, CamDev* slot, hipStream_t s);
 // Launch overrides of eray_render_params::flags (eray_hip.h ERAY_RENDER_*) the frame launcher reads.
 constexpr uint32_t kLaunchDense = 2u, kLaunchNoDense = 4u, kLaunchSeparateFill = 8u, kLaunchNoSeparateFill = 16u,
                    kLaunchSharedDetail = 32u;
 // Per-context launch resources: the separate fill kernel's stream and its fork / join events.
+// Measurement (eray_time_frames_ring): when frame_t[0] is set, the frame kernel is launched with
+// hipExtLaunchKernel's start / stop events, which take the dispatch's own begin / end timestamps
+// (the figures rocprofv3's kernel trace reports); fill_t likewise for the separate fill kernel.
 struct LaunchCtx {
     hipStream_t side;
     hipEvent_t fork, join;
+    hipEvent_t frame_t[2] = {nullptr, nullptr};
+    hipEvent_t fill_t[2] = {nullptr, nullptr};
+    uint32_t* fill_used = nullptr;  // set to 1 when the launch ran the separate fill kernel
 };
 // The frame kernel, or the general tracer (trace.hip) when p.aa or p.bounces is set.
 hipError_t launch_render(const FrameParams& p, const LaunchCtx& lc, hipStream_t s);
@@ -402,13 +413,24 @@ hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tile
 hipError_t launch_pack_ppm(const float* rgb, uint32_t w, uint32_t h, uint8_t* out, hipStream_t s);
 
 // ------------------------------------------------------------- capi.cpp internals for comm.cpp
-// The scene camera's current setup: its generation (changes with every setup), Camera::size, the
-// rendered rows (FrameParams band fields) and every object's pixel rectangle (ObjGeom::rect:
-// x0, x1, y0, y1 inclusive, camera rows; empty when x0 > x1) — outside them the frame kernel
-// writes the background colour.
+// Where a frame in an output buffer came from (eray_gather_frames' scene-camera transport): the
+// context tags every PPM output slot it renders into with the render's kind and key.  kind
+// kSrcScene: a frame kernel render of the scene camera, key = a hash of (camera, scene
+// generation, Camera::size) — the same on every rank that made the same scene calls, whatever
+// internal re-setups (bin capacity growth) a rank did; kSrcPath: a frame of a camera path, key =
+// the context's path call counter; kSrcOther: anti-aliasing / bounces / brute force.
+constexpr uint32_t kSrcNone = 0, kSrcScene = 1, kSrcPath = 2, kSrcOther = 3;
+struct FrameSource {
+    uint32_t kind = kSrcNone;
+    uint64_t key = 0;
+    uint32_t W = 0, H = 0;
+    uint32_t row0 = 0, rows = 0, band_shift = 0, band_stride = 0;  // the rendered rows
+};
+// The pixel rectangles of a source (every object's ObjGeom::rect: x0, x1, y0, y1 inclusive, camera
+// rows; empty when x0 > x1; for a camera path the union over its cameras) — outside them every
+// frame of the source is the background colour.
 struct SceneLayout {
-    uint64_t gen;
-    uint32_t W, H, row0, rows, band_shift, band_stride;
+    FrameSource src;
     std::vector<std::array<int32_t, 4>> rects;
 };
 

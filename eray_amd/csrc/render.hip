@@ -24,6 +24,8 @@
 //
 // Shadow rays (engine.rs:136-142, 218-228) go through the same LDS tiles without culling; the
 // reference's degenerate bounding box rejects almost all of them before the scan.
+#include <hip/hip_ext.h>
+
 #include <mutex>
 
 #include "cull_record.hpp"
@@ -338,10 +340,7 @@ constexpr int kUndecided = 0, kSearching = 1, kDone = 2;
 // Candidate triangles tested together per step (independent, branch-free tests: their long
 // dependent chains, division included, overlap).
 constexpr int kBatch = 4;
-#ifndef ERAY_LARGE_TEST_BATCH
-#define ERAY_LARGE_TEST_BATCH 1
-#endif
-constexpr int kLargeTestBatch = ERAY_LARGE_TEST_BATCH;
+constexpr int kLargeTestBatch = 1;  // the large-mesh builds: one candidate per step (no spills)
 
 // Tests the next kB candidates of `mask` (kB <= its population) in index order.
 template <int kB, typename Face, typename Hot>
@@ -1294,14 +1293,9 @@ __device__ __forceinline__ void fill_frames(const FrameParams& p, uint32_t q, ui
 // are VALU-issue bound and a second detail wave per SIMD doubles the issue slots (one wave alone
 // issues a VALU instruction every 4 cycles, the SIMD every 2); below one round the spills only
 // lengthen each wave's chain.
+constexpr int kDenseWgs = 3;
 template <bool kCull, bool kLdsTiles, int kMat, bool kLdsScene, bool kDense = false, bool kDev = false>
-#ifndef ERAY_SNAKE_DETAIL
-#define ERAY_SNAKE_DETAIL 1
-#endif
-#ifndef ERAY_DENSE_WGS
-#define ERAY_DENSE_WGS 3
-#endif
-__global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && !kDense) ? 1 : (kDense ? ERAY_DENSE_WGS : 3))  // 3 workgroups per CU where that fits
+__global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && !kDense) ? 1 : (kDense ? kDenseWgs : 3))  // 3 workgroups per CU where that fits
     frame_kernel(const ObjectDesc* h_objects, const LightDesc* h_lights, const TriCull* h_cull, const TriHot* h_tris,
                  const TriShade* h_shade, uint32_t h_counts, uint32_t h_total_tris, uint32_t h_total_sub,
                  uint32_t h_roles, uint32_t h_band, FrameParams p) {
@@ -1360,7 +1354,7 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
         const uint32_t heavy = (kLdsTiles && p.detail_heavy && !(p.launch_flags & kLaunchSharedDetail))
                                    ? load_const(p.detail_heavy, 0) : 0xffffffffu;
         // snake order for the ordered (heavy-first) lists of binned meshes
-        constexpr bool kSnake = kLdsTiles && ERAY_SNAKE_DETAIL;
+        constexpr bool kSnake = kLdsTiles;
         const RowMap rm{p.row0, h_band & 31u, h_band >> 5};
         const uint32_t nobj = h_counts & 0xffffu;
         // virtual detail roles v (more than nd only when nd < F): frame v % F, its (v / F)-th
@@ -1513,6 +1507,18 @@ uint32_t device_cus() {
     return cus;
 }
 
+// A kernel launch, with its dispatch's own start / stop timestamps recorded into t[0] / t[1] when
+// they are given (LaunchCtx: measurement only).
+template <typename... KArgs, typename... Args>
+hipError_t launch_k(void (*kernel)(KArgs...), uint32_t grid, size_t dyn, hipStream_t s, const hipEvent_t (&t)[2],
+                    Args... args) {
+    if (t[0])
+        hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(kWG), (uint32_t)dyn, s, t[0], t[1], 0u, (KArgs)args...);
+    else
+        kernel<<<grid, kWG, dyn, s>>>(args...);
+    return hipGetLastError();
+}
+
 template <bool C, bool L, int M, bool K, bool D = false, bool V = false>
 hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, const LaunchCtx& lc, hipStream_t s) {
     static std::mutex mu;  // resident workgroups per CU of this build, per dynamic LDS size
@@ -1548,10 +1554,7 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
                                           : 0u;
     };
     FrameParams q = p;
-#ifndef ERAY_DETAIL_SHARE
-#define ERAY_DETAIL_SHARE 2.0f
-#endif
-    q.detail_wgs = detail_wgs(L && D ? ERAY_DETAIL_SHARE : 2.0f);
+    q.detail_wgs = detail_wgs(2.0f);
     q.fill_first = 0;
     q.detail_wgs_alt = 0;
     if (!L) {
@@ -1589,20 +1592,19 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
             hipError_t e;
             if ((e = hipEventRecord(lc.fork, s)) != hipSuccess || (e = hipStreamWaitEvent(lc.side, lc.fork, 0)) != hipSuccess)
                 return e;
-            frame_kernel<C, L, M, K, D, V><<<dgrid, kWG, dyn, s>>>(q.objects, q.lights, q.cull, q.tris, q.shade,
-                                                             q.nobj | (q.nlights << 16), q.total_tris,
-                                                             q.total_sub, frame_roles(dgrid, q), band_word(q), q);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-            fill_kernel<V><<<fgrid, kWG, 0, lc.side>>>(q);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
+            if ((e = launch_k(frame_kernel<C, L, M, K, D, V>, dgrid, dyn, s, lc.frame_t, q.objects, q.lights, q.cull,
+                              q.tris, q.shade, q.nobj | (q.nlights << 16), q.total_tris, q.total_sub,
+                              frame_roles(dgrid, q), band_word(q), q)) != hipSuccess)
+                return e;
+            if ((e = launch_k(fill_kernel<V>, fgrid, 0, lc.side, lc.fill_t, q)) != hipSuccess) return e;
+            if (lc.fill_used) *lc.fill_used = 1u;
             if ((e = hipEventRecord(lc.join, lc.side)) != hipSuccess) return e;
             return hipStreamWaitEvent(s, lc.join, 0);
         }
     }
-    frame_kernel<C, L, M, K, D, V><<<grid, kWG, dyn, s>>>(q.objects, q.lights, q.cull, q.tris, q.shade,
-                                                    q.nobj | (q.nlights << 16), q.total_tris,
-                                                    q.total_sub, frame_roles(grid, q), band_word(q), q);
-    return hipGetLastError();
+    return launch_k(frame_kernel<C, L, M, K, D, V>, grid, dyn, s, lc.frame_t, q.objects, q.lights, q.cull, q.tris,
+                    q.shade, q.nobj | (q.nlights << 16), q.total_tris, q.total_sub, frame_roles(grid, q), band_word(q),
+                    q);
 }
 
 template <bool C, int M, bool V>

@@ -345,6 +345,22 @@ __global__ void set_camera_kernel(CamDev cam, CamDev* slot) {
     if (threadIdx.x == 0) *slot = cam;
 }
 
+// Folds the pixel rectangles of `ncam` cameras' descriptor copies (objs + k * nobj) into
+// acc: (x0, y0) of object o minimised at acc[2 o ..], (x1, y1) maximised at acc[2 nobj + 2 o ..];
+// empty rectangles (x0 > x1) skipped.
+__global__ void __launch_bounds__(256) rect_union_kernel(const ObjectDesc* __restrict__ objs, uint32_t nobj,
+                                                         uint32_t ncam, int32_t* __restrict__ acc) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= nobj * ncam) return;
+    const int32_t* r = objs[i].g.rect;
+    if (r[0] > r[1] || r[2] > r[3]) return;
+    const uint32_t o = i % nobj;
+    atomicMin(acc + 2 * o, r[0]);
+    atomicMin(acc + 2 * o + 1, r[2]);
+    atomicMax(acc + 2 * nobj + 2 * o, r[1]);
+    atomicMax(acc + 2 * nobj + 2 * o + 1, r[3]);
+}
+
 }  // namespace
 
 hipError_t launch_camera_setup(const SetupParams& sp, hipStream_t s) {
@@ -364,6 +380,12 @@ hipError_t launch_camera_setup_batch(const SetupParams& sp, uint32_t ncam, hipSt
     if (sp.binned || sp.nobj > kSetupBatchMaxObjects) return hipErrorInvalidValue;
     if (!ncam) return hipSuccess;
     camera_setup_kernel<3><<<ncam, kSetupWG, 0, s>>>(sp, 1u);
+    return hipGetLastError();
+}
+
+hipError_t launch_rect_union(const ObjectDesc* objs, uint32_t nobj, uint32_t ncam, int32_t* acc, hipStream_t s) {
+    if (!nobj || !ncam) return hipSuccess;
+    rect_union_kernel<<<(nobj * ncam + 255) / 256, 256, 0, s>>>(objs, nobj, ncam, acc);
     return hipGetLastError();
 }
 

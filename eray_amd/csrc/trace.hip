@@ -150,7 +150,6 @@ __device__ void fill_level(const FrameParams& p, f3 o, f3 d, const Hit& h, Level
                       wv * omf + mat.ex_b * mat.ex_factor};
         L.kd = wv;
     }
-#ifndef ERAY_TRACE_NO_PROG  // diagnostics (scripts/build_variants.sh): the texel programs' call frames
     if (mat.prog) {  // a shader graph at the texel (its outputs have no texture)
         float t3[3];
         if (texel_program(mat.prog, 0, uv0, uv1, t3)) L.color = rgb{t3[0], t3[1], t3[2]};
@@ -159,7 +158,6 @@ __device__ void fill_level(const FrameParams& p, f3 o, f3 d, const Hit& h, Level
         if (texel_program(mat.prog, 3, uv0, uv1, t3)) L.sp = t3[0];
         if (texel_program(mat.prog, 4, uv0, uv1, t3)) L.refl = t3[0];
     }
-#endif
     if (const float* c = texel(mat.color, uv0, uv1, 3)) L.color = rgb{c[0], c[1], c[2]};
     if (const float* c = texel(mat.diffuse, uv0, uv1, 1)) L.kd = *c;
     if (const float* c = texel(mat.specular, uv0, uv1, 1)) L.ks = *c;
@@ -276,10 +274,6 @@ __device__ void camera_hits(const FrameParams& p, f3 C, const f3 (&d)[kRays], ui
         }
         group_sync<kW>();
         const unsigned long long act = R.act;
-#ifdef ERAY_TRACE_NO_SEARCH  // diagnostics (scripts/build_variants.sh): the bin search's share
-        group_sync<kW>();
-        continue;
-#endif
         const uint32_t lo = act ? load_const(ob.bin_start, bin) : 0u, hi = act ? load_const(ob.bin_start, bin + 1) : 0u;
         for (uint32_t rb = lo; rb < hi; rb += 64 * kW) {
             const uint32_t j = rb + 64 * wg + lane;
@@ -550,11 +544,9 @@ __device__ void binned_pixel(const FrameParams& p, uint32_t px, uint32_t y, bool
             const Hit hr = pick(h, r);
             rgb c = miss_color();
             if (hr.f >= 0) {
-#ifndef ERAY_TRACE_NO_SHADE  // diagnostics (scripts/build_variants.sh): the shading walks' share
                 Level L;
                 fill_level(p, C, pick(d, r), hr, L);
                 c = walk<kBounce>(p, L);
-#endif
             }
             if (i0 + r == 0) {
                 avg = c;

@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define ERAY_ABI_VERSION 4
+#define ERAY_ABI_VERSION 5
 
 typedef enum eray_status {
     ERAY_OK = 0,
@@ -316,6 +316,24 @@ int eray_render_prepare_ring(eray_ctx* ctx, const eray_render_params* params, co
 /* The frames per launch the library picks (frames_per_launch = 0) for these parameters, the scene
  * camera and a ring of `slots` slots — e.g. to size a ring of exactly that many slots. */
 uint32_t eray_frames_per_launch(eray_ctx* ctx, const eray_render_params* params, uint32_t slots);
+/* Measurement: renders frames as eray_render_frames_ring does (same kernels, same ring slots;
+ * max(1, frames / frames_per_launch) full launches, as plain launches, then waits) with every
+ * frame kernel launched through hipExtLaunchKernel's start / stop events, which carry the
+ * dispatch's own begin / end timestamps — the durations rocprofv3's kernel trace reports, free
+ * of launch and graph gaps.  Frame kernel durations per launch (mean, min, max), the separate
+ * background fill kernel's (0 when the launch shape has none) and each launch's span from the
+ * first kernel's start to the last one's end. */
+typedef struct eray_kernel_times {
+    uint32_t launches;
+    uint32_t frames_per_launch;
+    float frame_kernel_ms;          /* mean over the launches */
+    float frame_kernel_min_ms;
+    float frame_kernel_max_ms;
+    float fill_kernel_ms;
+    float launch_span_ms;           /* mean */
+} eray_kernel_times;
+int eray_time_frames_ring(eray_ctx* ctx, const eray_render_params* params, const eray_frame_ring* ring,
+                          uint32_t frames, eray_kernel_times* out);
 /* Camera paths of scenes whose per-camera setups are batched (no mesh over 256 faces) render
  * frames_per_launch frames per launch; others one (each camera rebuilds the screen bins). */
 int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* params, const eray_frame_ring* ring,

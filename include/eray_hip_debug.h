@@ -38,6 +38,13 @@ int eray_debug_coded_unband(eray_ctx* ctx, const uint8_t* staging, uint8_t* fram
                             uint32_t band_rows, uint32_t nranks);
 int eray_debug_scene_gather(eray_ctx* ctx, const uint8_t* staging, uint8_t* frame, uint32_t height, uint32_t width,
                             uint32_t band_rows, uint32_t nranks);
+/* Host only (no context, no GPU): rank `rank`'s share of the scene-camera gather of `nranks` ranks
+ * for objects whose pixel rectangles are `rects` (n x (x0, x1, y0, y1), camera rows) — its rows, its
+ * rectangles in local rows / 16-pixel column groups, each one's offset in its per-frame pack.  out:
+ * 4 + 8 x 8 words (rows, nrect, bytes per frame, packed rows, then per rectangle l0, l1, c0, c1,
+ * offset, row bytes, first packed row, 0). */
+int eray_debug_gather_layout(const int32_t* rects, uint32_t n, uint32_t height, uint32_t width, uint32_t band_rows,
+                             uint32_t nranks, uint32_t rank, uint32_t* out);
 
 #ifdef __cplusplus
 }

@@ -92,3 +92,90 @@ def test_two_rank_gather_equals_single_frame(tmp_path, bands):
     got = np.load(out)
     want = _render_block(0, 2 * ROWS)
     assert got.shape == want.shape and np.array_equal(got, want)
+
+
+BG = np.array([25, 25, 51], np.uint8)  # the miss colour's PPM bytes (engine.rs:212)
+
+
+def _rects_of(frame_file_order):
+    """A conservative pixel rectangle of a frame (x0, x1, y0, y1 in camera rows): the bounding box
+    of its non-background pixels — what the objects' rectangles (ObjGeom::rect) always contain."""
+    cam = frame_file_order[::-1]
+    ys, xs = np.nonzero((cam != BG).any(axis=2))
+    return [(int(xs.min()), int(xs.max()), int(ys.min()), int(ys.max()))] if len(xs) else []
+
+
+def _pack(local, lay, W):
+    """A rank's per-frame pack in the library's layout (gather_pack_kernel restated): each
+    rectangle's local rows l0..l1 (local PPM block row rows - 1 - j), columns 48 c0 .. 48 (c1 + 1)."""
+    out = np.zeros(lay["bytes"], np.uint8)
+    flat = local.reshape(local.shape[0], W * 3)
+    for g in lay["rects"]:
+        for j in range(g["l0"], g["l1"] + 1):
+            at = g["off"] + (j - g["l0"]) * g["row_bytes"]
+            out[at:at + g["row_bytes"]] = flat[lay["rows"] - 1 - j, 48 * g["c0"]:48 * (g["c1"] + 1)]
+    return out
+
+
+def _assemble(packs, lays, H, W, band, world):
+    """Rank 0's frame from every rank's pack (gather_assemble_kernel restated): the background,
+    except inside the owning rank's rectangles."""
+    frame = np.empty((H, W * 3), np.uint8)
+    frame[:] = np.tile(BG, W)
+    for F in range(H):
+        Y = H - 1 - F
+        if band:
+            r, j = (Y // band) % world, (Y // (world * band)) * band + Y % band
+        else:
+            h = H // world
+            r = (H - 1 - Y) // h
+            j = Y - (H - (r + 1) * h)
+        for g in lays[r]["rects"]:
+            if g["l0"] <= j <= g["l1"]:
+                at = g["off"] + (j - g["l0"]) * g["row_bytes"]
+                frame[F, 48 * g["c0"]:48 * (g["c1"] + 1)] = packs[r][at:at + g["row_bytes"]]
+    return frame.reshape(H, W, 3)
+
+
+def _scene_gather_worker(rank, world, port, out_path, bands):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from eray_amd import capi
+    from eray_amd.dist import band_camera_rows, band_split
+
+    H = world * ROWS
+    full = _render_block(0, H)  # every rank knows the camera's rectangles (here: from the frame)
+    rects = _rects_of(full)
+    lay = capi.gather_layout(rects, H, W, bands, world, rank)  # the library's own layout code
+    if bands:
+        sp = band_split(rank, world, H, bands)
+        assert lay["rows"] == sp["rows"]
+        local = np.zeros((sp["alloc_rows"], W, 3), np.uint8)
+        local[: sp["rows"]] = _render_rows(band_camera_rows(rank, world, H, bands))
+    else:
+        row0, rows = row_block(rank, world, ROWS)
+        local = _render_block(row0, rows)
+    pack = _pack(local, lay, W)
+    got = [None] * world
+    dist.all_gather_object(got, (lay, pack))
+    if rank == 0:
+        frame = _assemble([p for _, p in got], [l for l, _ in got], H, W, bands, world)
+        np.save(out_path, frame)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bands", [0, 4, 8])
+def test_two_rank_scene_camera_gather_layout(tmp_path, bands):
+    """The scene-camera transport of eray_gather_frames across two gloo ranks: each rank's share
+    laid out by the library's own layout code (eray_debug_gather_layout: rank rows, rectangles in
+    local rows and column groups, pack offsets), packed and exchanged, assembled on rank 0 — equal
+    to the single-process frame byte for byte.  (The kernels doing pack and assemble on the GPU
+    are checked rank by rank in tests/test_gpu_gather.py.)"""
+    out = str(tmp_path / "frame.npy")
+    mp.start_processes(_scene_gather_worker, args=(2, _free_port(), out, bands), nprocs=2, join=True,
+                       start_method="spawn")
+    got = np.load(out)
+    want = _render_block(0, 2 * ROWS)
+    assert (want != BG).any(axis=2).any()
+    assert got.shape == want.shape and np.array_equal(got, want)

@@ -199,3 +199,105 @@ def test_one_rank_gather_frames_and_graph_capture(cube):
             a.free()
         sc.close()
         gpu.close()
+
+
+@pytest.mark.parametrize("mesh", ["cube", "standin70k"])
+def test_one_rank_gather_camera_path_frames(cube, standin70k_gather, mesh):
+    """Camera-path frames through the scene-camera transport: the plan is the union of the path's
+    cameras' pixel rectangles (accumulated on the device beside the path's setups), exchanged once
+    per path call; the gathered frames equal the rendered ones.  Cube: batched setups (graph
+    replay); 70k faces: the multi-camera builds."""
+    import math
+    W, H, S = 320, 180, 4
+    gpu = capi.Context(0)
+    sc = MainScene(gpu, *(cube if mesh == "cube" else standin70k_gather), W, H, texture=64, fov=(16.0, 9.0))
+    ring = capi.frame_ring(S, H, W)
+    rgb = gpu.empty((S, H, W, 3), np.float32)
+    local = gpu.empty((S, H, W, 3), np.uint8)
+    frames = gpu.empty((S, H, W, 3), np.uint8)
+    comm = None
+    try:
+        path = [capi.make_camera((0.0, 0.0, 5.0 + 0.6 * math.sin(k)), (16.0, 9.0), W, 1.0 + 0.1 * k) for k in range(S)]
+        gpu.render_camera_path(path, W, H, out_rgb=rgb.ptr, out_ppm=local.ptr, ring=ring)
+        gpu.synchronize()
+        want = local.numpy()
+        assert all((want[k] != np.array([25, 25, 51], np.uint8)).any() for k in range(S))
+        assert not np.array_equal(want[0], want[S - 1])  # the camera moved
+        comm = gpu.comm_init(1, 0, capi.comm_unique_id())
+        slot = H * W * 3
+        for _ in range(2):  # (the second call reuses the path's plan)
+            gpu.memset(frames.ptr, 0, frames.nbytes)
+            gpu.gather_frames(comm, local.ptr, slot, frames.ptr, slot, S, H, W, scene_camera=True)
+            gpu.synchronize()
+            assert np.array_equal(frames.numpy(), want)
+        # a second path into the same slots: a new plan, its own union
+        path2 = [capi.make_camera((0.0, 0.0, 4.2 + 0.3 * k), (16.0, 9.0), W, 1.0) for k in range(S)]
+        gpu.render_camera_path(path2, W, H, out_rgb=rgb.ptr, out_ppm=local.ptr, ring=ring)
+        gpu.synchronize()
+        want2 = local.numpy()
+        gpu.memset(frames.ptr, 0, frames.nbytes)
+        gpu.gather_frames(comm, local.ptr, slot, frames.ptr, slot, S, H, W, scene_camera=True)
+        gpu.synchronize()
+        assert np.array_equal(frames.numpy(), want2)
+    finally:
+        if comm:
+            capi.comm_destroy(comm)
+        for a in (rgb, local, frames):
+            a.free()
+        sc.close()
+        gpu.close()
+
+
+def test_scene_camera_gather_refuses_other_frames(cube):
+    """The scene-camera transport only takes frames whose pixel rectangles it knows: frames this
+    context did not render, anti-aliased frames (no rectangles), a batch mixing renders, and
+    frames of a scene camera whose setup has since been replaced all fail with
+    ERAY_E_INVALID_ARGUMENT (never a silently wrong frame); frames of the current setup still
+    gather after each refusal."""
+    W, H, S = 320, 180, 2
+    gpu = capi.Context(0)
+    sc = MainScene(gpu, *cube, W, H, texture=64, fov=(16.0, 9.0))
+    local = gpu.empty((S, H, W, 3), np.uint8)
+    frames = gpu.empty((S, H, W, 3), np.uint8)
+    other = gpu.empty((S, H, W, 3), np.uint8)
+    slot = H * W * 3
+    comm = None
+
+    def gather(ptr, n=S):
+        gpu.gather_frames(comm, ptr, slot, frames.ptr, slot, n, H, W, scene_camera=True)
+        gpu.synchronize()
+
+    def refused(ptr, n=S):
+        with pytest.raises(capi.ErayError) as e:
+            gather(ptr, n)
+        assert e.value.status == capi.E_INVALID_ARGUMENT, e.value.message
+
+    try:
+        comm = gpu.comm_init(1, 0, capi.comm_unique_id())
+        ring = capi.frame_ring(S, H, W)
+        gpu.render_frames(S, W, H, out_ppm=local.ptr, ring=ring)
+        gpu.synchronize()
+        want = local.numpy()
+        gather(local.ptr)
+        assert np.array_equal(frames.numpy(), want)
+        refused(other.ptr)  # never rendered by this context
+        gpu.render(W, H, out_ppm=local.ptr, anti_aliasing=2, aa_seed=7)  # slot 0: anti-aliased
+        refused(local.ptr)  # mixed: slot 0 anti-aliased, slot 1 the scene camera
+        refused(local.ptr, 1)  # anti-aliased alone
+        gpu.render_frames(S, W, H, out_ppm=local.ptr, ring=ring)
+        gather(local.ptr)
+        assert np.array_equal(frames.numpy(), want)
+        # the scene camera moves and is rendered elsewhere: the old frames' setup is gone
+        gpu.set_camera(capi.make_camera((0.0, 0.0, 4.0), (16.0, 9.0), W, 1.0))
+        gpu.render(W, H, out_ppm=other.ptr)
+        refused(local.ptr)
+        gather(other.ptr, 1)  # the new camera's frame
+        gpu.synchronize()
+        assert np.array_equal(frames.numpy()[0], other.numpy()[0])
+    finally:
+        if comm:
+            capi.comm_destroy(comm)
+        for a in (local, frames, other):
+            a.free()
+        sc.close()
+        gpu.close()
