@@ -31,8 +31,58 @@ struct Fail {
     throw Fail{ERAY_E_PARSE, "line " + std::to_string(line) + ": " + what};
 }
 
-// str::split_whitespace's separators within a line (ASCII; '\n' ends the line)
-inline bool is_ws(char c) { return c == ' ' || c == '\t' || c == '\v' || c == '\f' || c == '\r'; }
+// str::split_whitespace's separators within a line: char::is_whitespace, Unicode White_Space —
+// ASCII \t \v \f \r and space ('\n' ends the line), U+0085, U+00A0, U+1680, U+2000-U+200A,
+// U+2028, U+2029, U+202F, U+205F, U+3000 (as UTF-8).  Returns the separator's length in bytes,
+// or 0.  (The file is valid UTF-8 by then: read_to_string, utf8_valid.)
+inline size_t ws_len(const char* q, const char* e) {
+    const unsigned char c = (unsigned char)*q;
+    if (c == ' ' || c == '\t' || c == '\v' || c == '\f' || c == '\r') return 1;
+    if (c < 0xC2) return 0;
+    const unsigned char c1 = e - q > 1 ? (unsigned char)q[1] : 0, c2 = e - q > 2 ? (unsigned char)q[2] : 0;
+    if (c == 0xC2) return (c1 == 0x85 || c1 == 0xA0) ? 2 : 0;
+    if (c == 0xE1) return (c1 == 0x9A && c2 == 0x80) ? 3 : 0;
+    if (c == 0xE2) {
+        if (c1 == 0x80) return (c2 <= 0x8A || c2 == 0xA8 || c2 == 0xA9 || c2 == 0xAF) ? 3 : 0;
+        return (c1 == 0x81 && c2 == 0x9F) ? 3 : 0;
+    }
+    if (c == 0xE3) return (c1 == 0x80 && c2 == 0x80) ? 3 : 0;
+    return 0;
+}
+
+// std::fs::read_to_string fails (io::ErrorKind::InvalidData) unless the file is UTF-8 as
+// str::from_utf8 defines it: no stray or missing continuation bytes, no overlong forms, no
+// surrogates (U+D800-U+DFFF), nothing above U+10FFFF.
+bool utf8_valid(const unsigned char* p, size_t n) {
+    size_t i = 0;
+    while (i < n) {
+        const unsigned char c = p[i];
+        if (c < 0x80) {
+            ++i;
+            continue;
+        }
+        size_t len;
+        unsigned char lo = 0x80, hi = 0xBF;  // the allowed range of the second byte
+        if (c >= 0xC2 && c <= 0xDF) {
+            len = 2;
+        } else if (c >= 0xE0 && c <= 0xEF) {
+            len = 3;
+            if (c == 0xE0) lo = 0xA0;
+            if (c == 0xED) hi = 0x9F;
+        } else if (c >= 0xF0 && c <= 0xF4) {
+            len = 4;
+            if (c == 0xF0) lo = 0x90;
+            if (c == 0xF4) hi = 0x8F;
+        } else {
+            return false;
+        }
+        if (i + len > n || p[i + 1] < lo || p[i + 1] > hi) return false;
+        for (size_t k = 2; k < len; ++k)
+            if (p[i + k] < 0x80 || p[i + k] > 0xBF) return false;
+        i += len;
+    }
+    return true;
+}
 
 struct Tok {
     const char* b;
@@ -135,10 +185,10 @@ void load(const char* data, size_t size, Mesh& m) {
         size_t nt = 0;
         bool more = false;
         for (const char* q = lp; q < le;) {
-            while (q < le && is_ws(*q)) ++q;
+            for (size_t w; q < le && (w = ws_len(q, le)) != 0;) q += w;
             if (q == le) break;
             const char* b = q;
-            while (q < le && !is_ws(*q)) ++q;
+            while (q < le && !ws_len(q, le)) ++q;
             if (nt < 64) tok[nt++] = Tok{b, q};
             else more = true;
         }
@@ -219,6 +269,9 @@ extern "C" int eray_obj_load(const char* path, eray_obj_mesh* out) {
     err = err || std::ferror(f) != 0;
     std::fclose(f);
     if (err) return eray_internal_error(nullptr, ERAY_E_IO, (std::string("cannot read ") + path).c_str());
+    if (!utf8_valid(reinterpret_cast<const unsigned char*>(data.data()), data.size()))
+        return eray_internal_error(nullptr, ERAY_E_IO,
+                                   (std::string(path) + ": stream did not contain valid UTF-8 (read_to_string)").c_str());
     Mesh m;
     try {
         load(data.data(), data.size(), m);

@@ -21,7 +21,7 @@ import re
 
 import numpy as np
 
-from .capi import E_BUILD, E_PARSE
+from .capi import E_BUILD, E_IO, E_PARSE
 
 _FLOAT_RE = re.compile(r"^[+-]?(?:(?:\d+\.?\d*|\.\d+)(?:[eE][+-]?\d+)?|inf|infinity|nan)$",
                        re.IGNORECASE)
@@ -44,6 +44,11 @@ def _strtof(tok: str) -> np.float32:
     return np.float32(_libc.strtof(tok.encode(), None))
 
 
+# char::is_whitespace (Unicode White_Space), the separators of str::split_whitespace — not
+# Python's str.split(), which also splits on U+001C-U+001F
+_RUST_WS = re.compile("[\t\n\x0b\x0c\r \x85\xa0\u1680\u2000-\u200a\u2028\u2029\u202f\u205f\u3000]+")
+
+
 def _parse_f32(tokens: list[str], line: int) -> np.ndarray:
     for t in tokens:
         if not _FLOAT_RE.match(t):
@@ -62,7 +67,10 @@ def _parse_f32(tokens: list[str], line: int) -> np.ndarray:
 def load_obj(text: str | bytes):
     """Parse an .obj text; returns (positions (T,9), normals (T,9), uvs (T,6)) float32."""
     if isinstance(text, (bytes, bytearray)):
-        text = text.decode("utf-8")
+        try:  # std::fs::read_to_string: io::ErrorKind::InvalidData on invalid UTF-8
+            text = bytes(text).decode("utf-8", errors="strict")
+        except UnicodeDecodeError as e:
+            raise ObjError(E_IO, f"stream did not contain valid UTF-8: {e}") from None
     verts: list[np.ndarray] = []
     norms: list[np.ndarray] = []
     uvs: list[np.ndarray] = []
@@ -74,7 +82,7 @@ def load_obj(text: str | bytes):
         line = raw[:-1] if raw.endswith("\r") else raw
         if not line or line[0] == "#":
             continue
-        tok = line.split()
+        tok = [t for t in _RUST_WS.split(line) if t]  # str::split_whitespace
         if not tok:
             raise ObjError(E_PARSE, f"line {line_no}: whitespace-only line (tokens.next().unwrap())")
         m = tok[0]

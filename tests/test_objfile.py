@@ -125,3 +125,44 @@ def test_native_loader_generated_mesh(oracle, tmp_path):
     assert same(a, load_obj(p.read_text()))
     v, n, t, fv, ft, fn = meshgen.displaced_sphere(20000, 5)
     assert np.array_equal(a[0], v[fv].reshape(-1, 9))
+
+
+# ------------------------------------------------------------ text layer: read_to_string + split_whitespace
+# Object::load_obj reads the file with std::fs::read_to_string (object.rs:102: invalid UTF-8 is an
+# io::Error, InvalidData) and tokenises lines with str::split_whitespace (char::is_whitespace, the
+# Unicode White_Space set).  No reference fixture covers these bytes: parity unpinned, the rules
+# restated from the Rust standard library's documented behaviour.
+BAD_UTF8 = {
+    "stray byte": b"v 0 0 0\xff\nvn 0 0 1\n",
+    "overlong": b"# \xc0\x80\nv 0 0 0\n",
+    "surrogate": b"# \xed\xa0\x80\nv 0 0 0\n",
+    "above U+10FFFF": b"# \xf4\x90\x80\x80\nv 0 0 0\n",
+    "truncated": b"v 0 0 0\nvn 0 0 1\n# \xe2\x80",
+}
+
+
+@pytest.mark.parametrize("name", sorted(BAD_UTF8))
+def test_invalid_utf8_is_an_io_error(tmp_path, name):
+    with pytest.raises(OSError):
+        _native(tmp_path, BAD_UTF8[name])
+    with pytest.raises(ObjError) as e:
+        load_obj(BAD_UTF8[name])
+    assert e.value.status == capi.E_IO
+
+
+def test_unicode_whitespace_separates_tokens(tmp_path):
+    base = load_obj(GOOD)
+    for sep in (" ", "\u0085", "\u00a0", "\u1680", "\u2000", "\u200a", "\u2028", "\u2029", "\u202f", "\u205f", "\u3000",
+                "\x0b", "\x0c", "\t"):
+        txt = "# caf\u00e9 \u2603\n" + GOOD.replace("v 1.0 0 0", f"v{sep}1.0 0{sep}{sep}0").replace("vt 0 1", f"vt 0{sep}1")
+        assert same(load_obj(txt.encode()), base), repr(sep)
+        assert same(_native(tmp_path, txt.encode()), base), repr(sep)
+    # U+001C..U+001F are not Rust whitespace (Python's str.split() would split there): a bad float
+    for sep in ("\x1c", "\x1f", "\u200b"):
+        txt = GOOD.replace("v 1.0 0 0", f"v 1.0{sep}0 0")
+        with pytest.raises(ObjError) as e:
+            load_obj(txt)
+        assert e.value.status == capi.E_PARSE
+        with pytest.raises(ObjError) as e:
+            _native(tmp_path, txt)
+        assert e.value.status == capi.E_PARSE
