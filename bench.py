@@ -205,6 +205,8 @@ class Markers:
             try:
                 self._lib = ctypes.CDLL(name)
                 self._lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                self._lib.roctxRangePushA(b"init")  # (the library's own first-call set-up, here)
+                self._lib.roctxRangePop()
                 break
             except (OSError, AttributeError):
                 self._lib = None
@@ -615,13 +617,13 @@ def main() -> None:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    with MARK.range(f"steps_F{F}"):
+    with MARK.range(f"steps_F{F}"):  # (pushed before, popped after the clock's two readings)
         t0 = time.perf_counter()
         run(args.steps)
         torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
     if world > 1:
         elapsed = float(allreduce(elapsed, torch.float64, dist.ReduceOp.MAX))
         hits_all = int(allreduce(hits, torch.int64, dist.ReduceOp.SUM))

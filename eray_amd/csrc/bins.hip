@@ -379,7 +379,8 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t per, con
                                                                ObjectDesc* __restrict__ objs, uint32_t* tri,
                                                                unsigned long long* mask, TriHot* hot,
                                                                uint32_t* __restrict__ sortq, uint32_t* __restrict__ nsort,
-                                                               CamState* __restrict__ st, uint32_t ncam) {
+                                                               CamState* __restrict__ st, uint32_t ncam,
+                                                               int32_t* __restrict__ path_union, uint32_t union_nobj) {
     __shared__ uint32_t s_acc[kFinSpan][4];
     __shared__ uint32_t s_tab[kFinal ? kFinTab : 1][4];
     const uint32_t keys = nb * nbins;
@@ -453,6 +454,7 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t per, con
             g.bin_tri = nullptr;
             g.bin_mask = nullptr;
             g.bin_hot = nullptr;
+            if (path_union) union_rect(path_union, union_nobj, kobj[j] % union_nobj, g.rect);
             continue;
         }
         // a pixel of an empty bin has no face whose culling bounds can pass there (bin_pixels),
@@ -467,6 +469,7 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t per, con
             r[2] = max(r[2], (int32_t)~w[2]);
             r[3] = min(r[3], (int32_t)w[3] - 1);
         }
+        if (path_union) union_rect(path_union, union_nobj, kobj[j] % union_nobj, r);
         g.bin_start = start + (size_t)j * nbins;
         g.bin_tri = tri;
         g.bin_mask = mask;
@@ -718,13 +721,15 @@ hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tile
     const uint32_t fgrid = (uint32_t)std::max<size_t>((keys + per - 1) / per, 1);
     bins_finalize_kernel<false><<<fgrid, kBinWG, 0, s>>>(per, b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase,
                                                          b.acc, b.part, b.done, b.n, (uint32_t)b.cap, b.kobj, sp.objs,
-                                                         b.tri, b.mask, b.hot, b.sortq, b.nsort, sp.state, ncam);
+                                                         b.tri, b.mask, b.hot, b.sortq, b.nsort, sp.state, ncam, nullptr,
+                                                         1u);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     bin_sort_kernel<<<kSortGrid, kBinWG, 0, s>>>(b.sortq, b.nsort, b.start, b.tri, b.mask, b.hot);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     bins_finalize_kernel<true><<<1, kBinWG, 0, s>>>(per, b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase, b.acc,
                                                     b.part, b.done, b.n, (uint32_t)b.cap, b.kobj, sp.objs, b.tri, b.mask,
-                                                    b.hot, b.sortq, b.nsort, sp.state, ncam);
+                                                    b.hot, b.sortq, b.nsort, sp.state, ncam, sp.path_union,
+                                                    sp.union_nobj ? sp.union_nobj : 1u);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (!b.nsub) return hipSuccess;
     const uint32_t n = (uint32_t)b.nsub;

@@ -144,6 +144,7 @@ struct eray_ctx {
     int32_t* d_union_acc = nullptr;
     size_t union_cap = 0;  // objects per entry
     int32_t* h_union = nullptr;
+    int32_t* d_union_host = nullptr;  // h_union's device address (mapped)
     uint64_t union_seq[4] = {0, 0, 0, 0};
     FrameSource union_src[4];
     hipEvent_t union_ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -568,9 +569,11 @@ SetupParams setup_params(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint
 // camera paths append it in one launch instead (bins.hip detail_list_kernel)
 // keep_all: the general tracer's bins (SetupParams::keep_all)
 int enqueue_setup(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint32_t H, const RowSpan& rs, bool ordered,
-                  bool keep_all = false) {
+                  bool keep_all = false, int32_t* path_union = nullptr) {
     SetupParams sp = setup_params(ctx, d_camera, W, H, rs);
     sp.keep_all = keep_all ? 1u : 0u;
+    sp.path_union = path_union;
+    sp.union_nobj = sp.nobj;
     HIP_TRY(ctx, launch_camera_setup(sp, ctx->stream));
     if (sp.binned) HIP_TRY(ctx, launch_bins_build(sp, ctx->bins, (W + 63) / 64, ordered, ctx->stream));
     return ERAY_OK;
@@ -642,7 +645,7 @@ int ensure_multi(eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs) {
 // camera k's culling records at m.cull + k T, descriptors at m.objs + k nobj, state m.state + k,
 // detail list m.bins.dlist + k nsub (occupancy m.bins.docc + k nsub / 4).
 int enqueue_multi_setup(eray_ctx* ctx, eray_ctx::MultiSet& m, const CamDev* d_cams, uint32_t ncam, uint32_t W,
-                        uint32_t H, const RowSpan& rs, hipStream_t s) {
+                        uint32_t H, const RowSpan& rs, hipStream_t s, int32_t* path_union = nullptr) {
     const uint32_t T = ctx->total_tris, nobj = (uint32_t)ctx->objects.size();
     SetupParams sp = setup_params(ctx, d_cams, W, H, rs);
     sp.ncam = ncam;
@@ -664,6 +667,8 @@ int enqueue_multi_setup(eray_ctx* ctx, eray_ctx::MultiSet& m, const CamDev* d_ca
     sp.phase = m.bins.phase;
     sp.first_local = m.bins.first;
     sp.boff = m.bins.boff;
+    sp.path_union = path_union;
+    sp.union_nobj = nobj;
     HIP_TRY(ctx, launch_camera_setup(sp, s));
     HIP_TRY(ctx, launch_bins_build(sp, m.bins, (W + 63) / 64, false, s));
     return ERAY_OK;
@@ -1465,41 +1470,38 @@ std::vector<unsigned char> ring_key(std::vector<unsigned char> key, const Ring& 
 }
 }  // namespace
 
-// The camera-path rectangle union (eray_gather_frames' layout of path frames): device accumulator
-// for nobj objects and the pinned ring of finished unions.
+// The camera-path rectangle union (eray_gather_frames' layout of path frames): the device
+// accumulator for nobj objects (SetupParams::path_union: the path's setup kernels fold every
+// camera's rectangles into it) and a ring of kUnionRing finished unions in mapped pinned memory.
 int ensure_union(eray_ctx* ctx, uint32_t nobj) {
     if (ctx->d_union_acc && ctx->union_cap >= nobj) return ERAY_OK;
     for (hipEvent_t& ev : ctx->union_ev) {
         if (!ev) HIP_TRY(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        HIP_TRY(ctx, hipEventSynchronize(ev));  // (a copy into the ring still in flight)
+        HIP_TRY(ctx, hipEventSynchronize(ev));  // (a flush into the ring still in flight)
     }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (ctx->d_union_acc) HIP_TRY(ctx, hipFree(ctx->d_union_acc));
     if (ctx->h_union) HIP_TRY(ctx, hipHostFree(ctx->h_union));
     ctx->d_union_acc = nullptr;
     ctx->h_union = nullptr;
+    ctx->d_union_host = nullptr;
     ctx->union_cap = 0;
-    const size_t n = std::max<uint32_t>(nobj, 1u);
+    const uint32_t n = std::max<uint32_t>(nobj, 1u);
     HIP_TRY(ctx, hipMalloc((void**)&ctx->d_union_acc, 4 * sizeof(int32_t) * n));
-    HIP_TRY(ctx, hipHostMalloc((void**)&ctx->h_union, 4 * sizeof(int32_t) * n * kUnionRing, hipHostMallocDefault));
+    HIP_TRY(ctx, hipHostMalloc((void**)&ctx->h_union, 4 * sizeof(int32_t) * n * kUnionRing, hipHostMallocMapped));
+    HIP_TRY(ctx, hipHostGetDevicePointer((void**)&ctx->d_union_host, ctx->h_union, 0));
+    HIP_TRY(ctx, launch_union_flush(ctx->d_union_acc, n, nullptr, ctx->stream));  // the initial reset
     for (auto& s : ctx->union_seq) s = 0;
     ctx->union_cap = n;
     return ERAY_OK;
 }
-int reset_union(eray_ctx* ctx, uint32_t nobj) {
-    if (!nobj) return ERAY_OK;
-    HIP_TRY(ctx, hipMemsetD32Async((hipDeviceptr_t)ctx->d_union_acc, 0x7fffffff, 2 * (size_t)nobj, ctx->stream));
-    HIP_TRY(ctx, hipMemsetD32Async((hipDeviceptr_t)(ctx->d_union_acc + 2 * (size_t)nobj), (int)0x80000000,
-                                   2 * (size_t)nobj, ctx->stream));
-    return ERAY_OK;
-}
-// After path call `seq`'s frames: its union into ring entry seq % kUnionRing on the host.
+// After path call `seq`'s frames: its union into ring entry seq % kUnionRing (and the accumulator
+// reset for the next path), one kernel on the stream.
 int finish_union(eray_ctx* ctx, uint64_t seq, const FrameSource& src, uint32_t nobj) {
     const uint32_t e = (uint32_t)(seq % kUnionRing);
-    HIP_TRY(ctx, hipEventSynchronize(ctx->union_ev[e]));  // the entry's copy kUnionRing paths back
-    if (nobj)
-        HIP_TRY(ctx, hipMemcpyAsync(ctx->h_union + (size_t)e * 4 * ctx->union_cap, ctx->d_union_acc,
-                                    4 * sizeof(int32_t) * nobj, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipEventSynchronize(ctx->union_ev[e]));  // the entry's flush kUnionRing paths back
+    HIP_TRY(ctx, launch_union_flush(ctx->d_union_acc, std::max(nobj, 1u),
+                                    ctx->d_union_host + (size_t)e * 4 * ctx->union_cap, ctx->stream));
     HIP_TRY(ctx, hipEventRecord(ctx->union_ev[e], ctx->stream));
     ctx->union_seq[e] = seq;
     ctx->union_src[e] = src;
@@ -1753,7 +1755,6 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
     psrc.band_shift = rs.band_shift;
     psrc.band_stride = rs.band_stride;
     if (int st = ensure_union(ctx, nobj)) return st;
-    if (int st = reset_union(ctx, nobj)) return st;
     if (batched) {
         if (int st = ensure(ctx, &ctx->d_bcull, &ctx->bcull_cap, (size_t)kGraphFrames * T)) return st;
         if (int st = ensure(ctx, &ctx->d_bobjs, &ctx->bobjs_cap, (size_t)kGraphFrames * nobj)) return st;
@@ -1770,8 +1771,9 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
             sp.objs = ctx->d_bobjs;
             sp.objs_src = ctx->d_objs;
             sp.state = ctx->d_bstate;
+            sp.path_union = ctx->d_union_acc;
+            sp.union_nobj = nobj;
             HIP_TRY(ctx, launch_camera_setup_batch(sp, count, ctx->stream));
-            HIP_TRY(ctx, launch_rect_union(ctx->d_bobjs, nobj, count, ctx->d_union_acc, ctx->stream));
         }
         if (slot % r.per_launch) return ERAY_OK;
         FrameParams q = ring_frames(p, r, f, std::min(r.per_launch, count - slot));
@@ -1793,8 +1795,8 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
         auto& m = ctx->mc[b & 1u];
         if (k == 0) {
             if (b == 0) {
-                if (int st = enqueue_multi_setup(ctx, m, cams, std::min(K, count), W, H, rs, ctx->stream)) return st;
-                HIP_TRY(ctx, launch_rect_union(m.objs, nobj, std::min(K, count), ctx->d_union_acc, ctx->stream));
+                if (int st = enqueue_multi_setup(ctx, m, cams, std::min(K, count), W, H, rs, ctx->stream, ctx->d_union_acc))
+                    return st;
                 HIP_TRY(ctx, hipEventRecord(ctx->mc_fork, ctx->stream));
             } else {
                 HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->mc_ready[b & 1u], 0));
@@ -1803,10 +1805,8 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
                 auto& m2 = ctx->mc[(b + 1) & 1u];
                 HIP_TRY(ctx, hipStreamWaitEvent(ctx->mc_stream, b == 0 ? ctx->mc_fork : ctx->mc_free[(b + 1) & 1u], 0));
                 if (int st = enqueue_multi_setup(ctx, m2, cams + (b + 1) * K, std::min(K, count - (b + 1) * K), W, H, rs,
-                                                 ctx->mc_stream))
+                                                 ctx->mc_stream, ctx->d_union_acc))
                     return st;
-                HIP_TRY(ctx, launch_rect_union(m2.objs, nobj, std::min(K, count - (b + 1) * K), ctx->d_union_acc,
-                                               ctx->mc_stream));
                 HIP_TRY(ctx, hipEventRecord(ctx->mc_ready[(b + 1) & 1u], ctx->mc_stream));
             }
         }
@@ -1833,8 +1833,7 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
             r = keep;
             return st;
         }
-        if (int st = enqueue_setup(ctx, cam, W, H, row_span(rp), false)) return st;
-        HIP_TRY(ctx, launch_rect_union(ctx->d_objs, nobj, 1, ctx->d_union_acc, ctx->stream));
+        if (int st = enqueue_setup(ctx, cam, W, H, row_span(rp), false, false, ctx->d_union_acc)) return st;
         HIP_TRY(ctx, launch_frame(ctx, ring_frames(p, r, f, 1)));
         return ERAY_OK;
     };

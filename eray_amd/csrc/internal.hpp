@@ -324,6 +324,11 @@ struct SetupParams {
     // entries; boff[nparts] = all pairs) — bins.hip bin_pairs_kernel reads them
     unsigned long long* first_local;
     unsigned long long* boff;
+    // Camera paths (eray_gather_frames' layout of path frames): every camera's final object
+    // rectangles also fold into this union (object o % union_nobj: x0, y0 minimised at
+    // path_union[2 o ..], x1, y1 maximised at path_union[2 union_nobj + 2 o ..]), or null
+    int32_t* path_union;
+    uint32_t union_nobj;
 };
 hipError_t launch_camera_setup(const SetupParams& sp, hipStream_t s);
 // The setups of `ncam` cameras sp.cam[0 .. ncam) at once, one workgroup each, into per-camera
@@ -332,11 +337,18 @@ hipError_t launch_camera_setup(const SetupParams& sp, hipStream_t s);
 // kSetupBatchMaxObjects objects (every object's union stays in the workgroup's LDS).
 constexpr uint32_t kSetupBatchMaxObjects = 256;
 hipError_t launch_camera_setup_batch(const SetupParams& sp, uint32_t ncam, hipStream_t s);
-// Folds the pixel rectangles of `ncam` cameras' descriptor copies (objs + k * nobj, k < ncam) into
-// the per-object union, atomically: acc[2 o], acc[2 o + 1] = min x0, min y0 (starting at INT_MAX),
-// acc[2 nobj + 2 o], acc[2 nobj + 2 o + 1] = max x1, max y1 (starting at INT_MIN) — a camera
-// path's gather layout.
-hipError_t launch_rect_union(const ObjectDesc* objs, uint32_t nobj, uint32_t ncam, int32_t* acc, hipStream_t s);
+// A camera path's rectangle union (SetupParams::path_union, 4 nobj words) copied to `host` (mapped
+// pinned memory, read by the host after the stream passes this point) and reset for the next
+// path: x0, y0 to INT_MAX, x1, y1 to INT_MIN.  host null: the reset alone.
+hipError_t launch_union_flush(int32_t* acc, uint32_t nobj, int32_t* host, hipStream_t s);
+// Folds an object's final pixel rectangle r (x0, x1, y0, y1; skipped when empty) into the union.
+__device__ __forceinline__ void union_rect(int32_t* u, uint32_t nobj, uint32_t o, const int32_t* r) {
+    if (r[0] > r[1] || r[2] > r[3]) return;
+    atomicMin(u + 2 * o, r[0]);
+    atomicMin(u + 2 * o + 1, r[2]);
+    atomicMax(u + 2 * nobj + 2 * o, r[1]);
+    atomicMax(u + 2 * nobj + 2 * o + 1, r[3]);
+}
 // Writes `cam` into the device camera slot (kernel arguments: no host staging buffer to race).
 hipError_t launch_set_camera(const CamDev& cam, CamDev* slot, hipStream_t s);
 // Launch overrides of eray_render_params::flags (eray_hip.h ERAY_RENDER_*) the frame launcher reads.

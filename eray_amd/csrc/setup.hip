@@ -277,6 +277,9 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp, 
         }
         if (kMode == 3) sp.objs[j] = sp.objs_src[j];  // the slot's descriptor, then its rectangle
         for (int k = 0; k < 4; ++k) sp.objs[j].g.rect[k] = r[k];
+        // a camera path's union (binned objects: bins.hip folds in their narrowed rectangles)
+        if (sp.path_union && sp.objkey[multi ? j % sp.nobj1 : j] == ~0u)
+            union_rect(sp.path_union, sp.union_nobj, j % sp.union_nobj, r);
         if (j < kTab)
             for (int k = 0; k < 4; ++k) s_tab[j][k] = (uint32_t)r[k];
     }
@@ -345,20 +348,12 @@ __global__ void set_camera_kernel(CamDev cam, CamDev* slot) {
     if (threadIdx.x == 0) *slot = cam;
 }
 
-// Folds the pixel rectangles of `ncam` cameras' descriptor copies (objs + k * nobj) into
-// acc: (x0, y0) of object o minimised at acc[2 o ..], (x1, y1) maximised at acc[2 nobj + 2 o ..];
-// empty rectangles (x0 > x1) skipped.
-__global__ void __launch_bounds__(256) rect_union_kernel(const ObjectDesc* __restrict__ objs, uint32_t nobj,
-                                                         uint32_t ncam, int32_t* __restrict__ acc) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= nobj * ncam) return;
-    const int32_t* r = objs[i].g.rect;
-    if (r[0] > r[1] || r[2] > r[3]) return;
-    const uint32_t o = i % nobj;
-    atomicMin(acc + 2 * o, r[0]);
-    atomicMin(acc + 2 * o + 1, r[2]);
-    atomicMax(acc + 2 * nobj + 2 * o, r[1]);
-    atomicMax(acc + 2 * nobj + 2 * o + 1, r[3]);
+__global__ void __launch_bounds__(256) union_flush_kernel(int32_t* __restrict__ acc, uint32_t nobj,
+                                                          int32_t* __restrict__ host) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < 4 * nobj; i += gridDim.x * 256u) {
+        if (host) host[i] = acc[i];
+        acc[i] = i < 2 * nobj ? 0x7fffffff : (int32_t)0x80000000;
+    }
 }
 
 }  // namespace
@@ -383,9 +378,9 @@ hipError_t launch_camera_setup_batch(const SetupParams& sp, uint32_t ncam, hipSt
     return hipGetLastError();
 }
 
-hipError_t launch_rect_union(const ObjectDesc* objs, uint32_t nobj, uint32_t ncam, int32_t* acc, hipStream_t s) {
-    if (!nobj || !ncam) return hipSuccess;
-    rect_union_kernel<<<(nobj * ncam + 255) / 256, 256, 0, s>>>(objs, nobj, ncam, acc);
+hipError_t launch_union_flush(int32_t* acc, uint32_t nobj, int32_t* host, hipStream_t s) {
+    if (!nobj) return hipSuccess;
+    union_flush_kernel<<<(4 * nobj + 255) / 256 < 64 ? (4 * nobj + 255) / 256 : 64, 256, 0, s>>>(acc, nobj, host);
     return hipGetLastError();
 }
 

@@ -27,12 +27,12 @@ def _find(d: str, suffix: str) -> list[str]:
 
 def _short(name: str) -> str:
     """frame_kernel<...> / fill_kernel<...> / other kernels by their base name."""
-    base = name.split("(")[0]
+    base = name.replace("(anonymous namespace)", "")
     for k in ("frame_kernel", "fill_kernel", "trace_kernel", "trace_binned_kernel", "trace_heavy_kernel",
               "trace_cull_kernel", "camera_setup_kernel", "bin_pairs_kernel", "material_example_kernel"):
         if k in base:
             return k
-    return base.split("::")[-1].split("<")[0]
+    return base.split("(")[0].split("<")[0].split("::")[-1].strip() or name[:40]
 
 
 def ranges(d: str) -> list[tuple[str, int, int]]:

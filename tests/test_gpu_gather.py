@@ -251,7 +251,7 @@ def test_one_rank_gather_camera_path_frames(cube, standin70k_gather, mesh):
 def test_scene_camera_gather_refuses_other_frames(cube):
     """The scene-camera transport only takes frames whose pixel rectangles it knows: frames this
     context did not render, anti-aliased frames (no rectangles), a batch mixing renders, and
-    frames of a scene camera whose setup has since been replaced all fail with
+    frames of a scene camera whose setup and plan have since been replaced all fail with
     ERAY_E_INVALID_ARGUMENT (never a silently wrong frame); frames of the current setup still
     gather after each refusal."""
     W, H, S = 320, 180, 2
@@ -287,13 +287,16 @@ def test_scene_camera_gather_refuses_other_frames(cube):
         gpu.render_frames(S, W, H, out_ppm=local.ptr, ring=ring)
         gather(local.ptr)
         assert np.array_equal(frames.numpy(), want)
-        # the scene camera moves and is rendered elsewhere: the old frames' setup is gone
+        # the scene camera moves and is rendered elsewhere: the old frames still gather with the
+        # plan made for their camera ...
         gpu.set_camera(capi.make_camera((0.0, 0.0, 4.0), (16.0, 9.0), W, 1.0))
         gpu.render(W, H, out_ppm=other.ptr)
-        refused(local.ptr)
-        gather(other.ptr, 1)  # the new camera's frame
-        gpu.synchronize()
+        gather(local.ptr)
+        assert np.array_equal(frames.numpy(), want)
+        gather(other.ptr, 1)  # the new camera's frame: a new plan
         assert np.array_equal(frames.numpy()[0], other.numpy()[0])
+        # ... but once that plan is replaced, their camera's setup is gone: refused
+        refused(local.ptr)
     finally:
         if comm:
             capi.comm_destroy(comm)
