@@ -629,9 +629,9 @@ def main() -> None:
         hits_all = int(allreduce(hits, torch.int64, dist.ReduceOp.SUM))
     else:
         hits_all = hits
-    # the frame kernel's duration on this rank: the same frames replayed once more, bracketed by
-    # HIP events on the library's stream (mean device time per frame; F frames per launch), and
-    # the latency of one frame alone per launch
+    # the frame kernel's duration on this rank: launches of the line's size, each timed by its
+    # dispatch's own start / end timestamps (eray_time_frames_ring); the same frames graph-replayed
+    # between two events (launch gaps included); the latency of one frame alone per launch
     ring1 = ring_args() if world == 1 else ring_args(0, G)
     with MARK.range(f"timed_F{F}"):
         kt = ctx.time_frames(max(args.steps, 64) // F * F, width, H, **ring1)
@@ -640,6 +640,7 @@ def main() -> None:
         replay_ms = ctx.render_frames(max(args.steps // F, 1) * F, width, H, timed=True, **ring1)
     latency = None
     fill_floor = None
+    beyond = None
     if not args.no_moving_camera:  # (counter runs keep to the measured launches)
         lat_args = dict(ring1)
         lat_args["ring"] = capi.frame_ring(1, alloc_rows, width, 1)
@@ -649,12 +650,35 @@ def main() -> None:
             empty = empty_scene_context(device, width, H, frame_camera_fov(width, H), stream)
             with MARK.range(f"fill_floor_F{F}"):
                 ft = empty.time_frames(max(args.steps, 64) // F * F, width, H, **ring1)
-            empty.close()
             fill_floor = {"frame_kernel_ms_per_launch": round(ft["frame_kernel_ms"], 6),
                           "frames_per_launch": ft["frames_per_launch"],
                           "achieved_gbs": round(15 * width * rows * ft["frames_per_launch"] / (ft["frame_kernel_ms"] * 1e-3)
                                                 / 1e9, 1),
                           "scene": "no objects: every pixel the miss colour, same kernel, ring and launch size"}
+            # the same launches into a ring whose slots exceed the 256 MiB Infinity Cache: every
+            # frame's stores reach HBM (the line's own ring of F slots may stay cache-resident)
+            if slots * slot_px * 15 <= MALL_BYTES:
+                big = slots
+                while big * slot_px * 15 <= MALL_BYTES:
+                    big *= 2
+                with torch.cuda.stream(stream):
+                    brgb = torch.empty((big, alloc_rows, width, 3), dtype=torch.float32, device="cuda")
+                    bppm = torch.empty((big, alloc_rows, width, 3), dtype=torch.uint8, device="cuda")
+                bkw = dict(row0=row0, rows=rows, flags=flags, out_rgb=brgb.data_ptr(), out_ppm=bppm.data_ptr(),
+                           ring=capi.frame_ring(big, alloc_rows, width, F), **band_args)
+                ctx.render_frames(big, width, H, **bkw)  # (the slots' pages touched once)
+                with MARK.range(f"beyond_mall_timed_F{F}"):
+                    bt = ctx.time_frames(max(args.steps, 64) // F * F, width, H, **bkw)
+                with MARK.range(f"beyond_mall_fill_floor_F{F}"):
+                    bft = empty.time_frames(max(args.steps, 64) // F * F, width, H, **bkw)
+                del brgb, bppm
+                b_ms = bt["frame_kernel_ms"]
+                b_gbs = algorithmic_bytes(width * rows, hits, hit_faces) * F / (b_ms * 1e-3) / 1e9
+                beyond = {"ring_slots": big, "ring_bytes": big * slot_px * 15, "kernel": kernel_figures(bt),
+                          "achieved": round(b_gbs, 1), "frac": round(b_gbs / PEAK_HBM_GBS, 4),
+                          "fill_floor_ms_per_launch": round(bft["frame_kernel_ms"], 6),
+                          "frac_of_fill_floor": round(bft["frame_kernel_ms"] / b_ms, 4)}
+            empty.close()
     rank_kernel_ms = [kernel_ms]
     gather_ms = None
     if world > 1:
@@ -764,6 +788,10 @@ def main() -> None:
                 "kernel_launches": kernel_figures(kt),
                 **({"fill_floor": fill_floor, "frac_of_fill_floor": round(fill_floor["frame_kernel_ms_per_launch"] /
                                                                             launch_ms, 4)} if fill_floor else {}),
+                "ring_slots": slots,
+                "ring_bytes": slots * slot_px * 15,
+                "exceeds_infinity_cache": slots * slot_px * 15 > MALL_BYTES,
+                "beyond_infinity_cache": beyond,
             },
             "north_star": ns_line,
         }

@@ -17,6 +17,10 @@ Fixtures
   c5_spans.npz      C5 (the 1M-face synthetic mesh, meshgen seed 1234, at 7680x4320, main.rs
                     scene): pixel spans across the silhouette, the mesh centre and the row-tile
                     boundary of the 8-GPU split (oracle_render_span), f32 RGB and faces
+  ns_spans.npz      north_star (the 69,451-face stand-in, meshgen seed 42, at 3840x2160, main.rs
+                    scene): the two camera rows through the mesh centre in full, and spans across
+                    the top and bottom silhouettes (the first and last hit rows of the centre
+                    column and their neighbours), f32 RGB and faces — `python make_golden.py ns`
 """
 import hashlib
 import json
@@ -67,6 +71,38 @@ def c5_spans() -> None:
     np.savez_compressed(os.path.join(HERE, "c5_spans.npz"), **out)
 
 
+NS_W, NS_H = 3840, 2160
+
+
+def ns_mesh():
+    v, n, t, fv, ft, fn = meshgen.displaced_sphere(**meshgen.STANDIN_70K)
+    return (np.ascontiguousarray(v[fv].reshape(-1, 9)), np.ascontiguousarray(n[fn].reshape(-1, 9)),
+            np.ascontiguousarray(t[ft].reshape(-1, 6)))
+
+
+def ns_spans() -> None:
+    """north_star rows: the centre rows 1079 and 1080 whole (both silhouettes of the row), and
+    the top and bottom silhouettes found on the centre column (its first and last hit rows),
+    each with its neighbours as 640-pixel spans around the centre column."""
+    import concurrent.futures as cf
+    scene = O.main_rs_scene(*ns_mesh(), texture=1024)
+    cam = O.camera((0.0, 0.0, 5.0), (16.0, 9.0), NS_W, 1.0)
+    assert O.camera_size(cam) == (NS_W, NS_H)
+    cx = NS_W // 2
+    col = [O.render_span(scene, cam, y, 1, cx, 1)[1][0, 0] for y in range(NS_H // 2 - 320, NS_H // 2 + 320)]
+    hit = [NS_H // 2 - 320 + i for i, f in enumerate(col) if f >= 0]
+    y_lo, y_hi = min(hit), max(hit)
+    spans = [(1079, 0, NS_W), (1080, 0, NS_W)]
+    spans += [(y, cx - 320, 640) for y in (y_lo - 1, y_lo, y_lo + 1, y_hi - 1, y_hi, y_hi + 1)]
+    with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:  # (ctypes drops the GIL)
+        res = list(ex.map(lambda s: O.render_span(scene, cam, s[0], 1, s[1], s[2]), spans))
+    out = {"spans": np.array(spans, np.int32)}
+    for k, (rgb, face, _) in enumerate(res):
+        out[f"rgb{k}"] = rgb[0]
+        out[f"face{k}"] = face[0]
+    np.savez_compressed(os.path.join(HERE, "ns_spans.npz"), **out)
+
+
 def main() -> None:
     mesh = load_obj_file(os.path.join(ROOT, "objects", "cube.obj"))
     digests = {}
@@ -114,4 +150,7 @@ def main() -> None:
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["ns"]:
+        ns_spans()
+    else:
+        main()

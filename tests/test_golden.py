@@ -79,6 +79,21 @@ def test_oracle_reproduces_c5_span_fixture(oracle):
         assert rgb[0].view(np.uint32).tobytes() == fx[f"rgb{k}"].view(np.uint32).tobytes()
 
 
+def test_oracle_reproduces_north_star_span_fixture(oracle):
+    """Two of the north_star spans (the 70k stand-in at 3840x2160): the top silhouette row and its
+    neighbour above (tests/golden/make_golden.py ns)."""
+    from tests.golden.make_golden import ns_mesh
+    fx = np.load(os.path.join(GOLDEN, "ns_spans.npz"))
+    scene = oracle.main_rs_scene(*ns_mesh(), texture=1024)
+    cam = oracle.camera((0.0, 0.0, 5.0), (16.0, 9.0), 3840, 1.0)
+    for k in (6, 7):
+        y, x0, cols = (int(v) for v in fx["spans"][k])
+        rgb, face, _ = oracle.render_span(scene, cam, y, 1, x0, cols)
+        assert (face[0] >= 0).any() or k == 7
+        assert np.array_equal(face[0], fx[f"face{k}"])
+        assert rgb[0].view(np.uint32).tobytes() == fx[f"rgb{k}"].view(np.uint32).tobytes()
+
+
 def test_oracle_reproduces_texture_fixture(oracle):
     fx = np.load(os.path.join(GOLDEN, "texture_8x4.npz"))
     color, diffuse = oracle.example_material(8, 4)

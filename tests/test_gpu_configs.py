@@ -213,7 +213,8 @@ def test_north_star_4k_70k_full_frame_binned_equals_brute_force(gpu):
     detail list), the 2-per-CU build, and the dense build with the separate fill kernel — equals
     the brute-force scan over the whole frame, bit for bit (object.rs:63-78: first hit by index);
     so do two frames in flight per launch, the 4-band split's ranks and the scene-camera gather of
-    their rows."""
+    their rows.  Against the oracle (not HIP against HIP): the committed rows of the frame through
+    the mesh centre and its top and bottom silhouettes (tests/golden/ns_spans.npz)."""
     mesh = _mesh(**meshgen.STANDIN_70K)
     W, H = 3840, 2160
     sc = MainScene(gpu, *mesh, W, H, texture=1024, fov=(16.0, 9.0))
@@ -221,6 +222,12 @@ def test_north_star_4k_70k_full_frame_binned_equals_brute_force(gpu):
     try:
         ref = [x.copy() for x in fr.render(W, H, flags=capi.RENDER_BRUTE_FORCE)]
         assert (ref[1] >= 0).sum() > 100_000
+        fx = np.load(os.path.join(GOLDEN, "ns_spans.npz"))
+        got = [x.copy() for x in fr.render(W, H)]  # the library's own launch choice
+        for k, (y, x0, cols) in enumerate(fx["spans"].tolist()):
+            for tag, fr_ in (("binned", got), ("brute force", ref)):
+                assert np.array_equal(fr_[1][y, x0:x0 + cols], fx[f"face{k}"]), f"{tag} span {k} faces"
+                assert_bit_equal(fr_[0][y, x0:x0 + cols], fx[f"rgb{k}"], f"{tag} span {k} ({y}, {x0}+{cols})")
         for flags in (capi.RENDER_DEFAULT, capi.RENDER_NO_DENSE_DETAIL, capi.RENDER_SHARED_DETAIL,
                       capi.RENDER_NO_DENSE_DETAIL | capi.RENDER_SHARED_DETAIL,
                       capi.RENDER_DENSE_DETAIL | capi.RENDER_SEPARATE_FILL):
