@@ -214,6 +214,21 @@ __device__ SceneLds preload_scene(const FrameHot& p, char* dyn, Meanwhile&& mean
                     reinterpret_cast<const TriShade*>(dyn + L.shade), p.objects, p.lights, p.tris, p.cull};
 }
 
+// A word of a read-only array through the vector memory path (buffer load; every lane the same
+// address): its wait counts with the wave's vector loads (vmcnt, in order), not with its LDS
+// operations (lgkmcnt, which an outstanding scalar load would hold up) — for loads issued one
+// sub-block ahead and used in the next.
+__device__ __forceinline__ uint32_t vload_u32(const uint32_t* base, uint32_t i) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(base), 0, -1, 0x00020000);
+    return __builtin_amdgcn_raw_buffer_load_b32(r, 4u * i, 0, 0);
+}
+
+// A bin range [lo, hi) loaded ahead (render_sub's pipelining), or none (ok false).
+struct PreRange {
+    uint32_t lo, hi;
+    bool ok;
+};
+
 // Lanes whose Triangle::intersects could pass: the det and t conditions of exact_test, from the
 // same expressions (so the same values).  t = dot(ao, n) * (1 / det) is >= 0 exactly when
 // dot(ao, n) >= 0, except where the product underflows to -0 or 1 / det is 0 — those lanes are
@@ -501,12 +516,13 @@ constexpr uint32_t kBinLdsBytes = (sizeof(BinLds) + 15) / 16 * 16;
 template <typename Activate>
 __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32_t bin, int& st, const f3& o,
                                  const f3& d, Activate&& activate, int& found, float& hu, float& hv, float& ht,
-                                 char* s_bins) {
+                                 char* s_bins, PreRange pre) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr uint32_t kWaves = kWG / 64;
     BinLds& L = *reinterpret_cast<BinLds*>(s_bins + wave * kBinLdsBytes);
     uint32_t* s_range = reinterpret_cast<uint32_t*>(s_bins + kWaves * kBinLdsBytes);  // [lo, hi] per wave
-    uint32_t lo = load_const(ob.bin_start, bin), hi = load_const(ob.bin_start, bin + 1);
+    // the bin's entries [lo, hi): loaded one sub-block ahead when the caller has them (pre)
+    uint32_t lo = pre.ok ? pre.lo : load_const(ob.bin_start, bin), hi = pre.ok ? pre.hi : load_const(ob.bin_start, bin + 1);
     if (lo != hi && __any(st == kUndecided)) {  // every pixel's ray and bbox verdict, up front
         const bool a = activate();
         if (st == kUndecided) st = a ? kSearching : kDone;
@@ -652,10 +668,11 @@ constexpr uint32_t kWaveBinMaxTris = (1u << 26) - 1u;
 // not re-read from memory.
 template <typename Activate>
 __device__ void first_hit_binned_wave(const ObjGeom& ob, uint32_t bin, int& st, const f3& o, const f3& d,
-                                      Activate&& activate, int& found, float& hu, float& hv, float& ht, char* s_bins) {
+                                      Activate&& activate, int& found, float& hu, float& hv, float& ht, char* s_bins,
+                                      PreRange pre) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     BinLds& L = *reinterpret_cast<BinLds*>(s_bins + wave * kBinLdsBytes);
-    const uint32_t lo = load_const(ob.bin_start, bin), hi = load_const(ob.bin_start, bin + 1);
+    const uint32_t lo = pre.ok ? pre.lo : load_const(ob.bin_start, bin), hi = pre.ok ? pre.hi : load_const(ob.bin_start, bin + 1);
     if (lo == hi) return;
     if (__any(st == kUndecided)) {  // every pixel's ray and bbox verdict, up front
         const bool a = activate();
@@ -892,11 +909,19 @@ __device__ __forceinline__ bool rect_meets(const ObjGeom& ob, const RowMap& rm, 
 // powf is not the identity), kMatExample (main.rs's graph evaluated per hit texel); a kernel
 // without them carries none of their code or registers.
 constexpr int kMatSpecPow = 1, kMatExample = 2;
-template <bool kCull, bool kLdsTiles, int kMat, typename Scene>
+// Pipelining across a wave's sub-blocks (binned meshes): `pre` (or null) holds the bin range of
+// this sub-block for object `pre_obj`, loaded during the wave's previous sub-block; `mid()` runs
+// once the first hits are known (the next sub-block's range loads are issued there).
+struct NoMid {
+    __device__ void operator()() const {}
+};
+template <bool kCull, bool kLdsTiles, int kMat, typename Scene, typename Mid = NoMid>
 __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut& fo, const CamDev& cam, const RowMap& rm,
                                            const Scene& sc, uint32_t wx0, uint32_t py0,
                                            bool active, TriHot* s_hot, TriCull* s_cull, char* s_bins, float4* s_rgb,
-                                           uint32_t* s_ppm, bool aligned, const f3* given_d = nullptr, bool coop = true) {
+                                           uint32_t* s_ppm, bool aligned, const f3* given_d = nullptr, bool coop = true,
+                                           PreRange pre = PreRange{0u, 0u, false}, uint32_t pre_obj = ~0u,
+                                           Mid&& mid = Mid{}) {
     // coop (workgroup-uniform): the workgroup's four sub-blocks share their large objects' work —
     // binned chunks dealt over the waves, shadow rays through shared LDS tiles — with barriers;
     // otherwise (light sub-blocks) every wave searches its own bins and shadow rays alone
@@ -944,10 +969,12 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
                                     v, t);
         } else if (wave_bins) {  // this wave's own bin, no barrier
             const uint32_t bin = ((cam_row(rm, py0) + kBinH - p.bin_phase) / kBinH) * p.bins_x + wx0 / kBinW;
-            first_hit_binned_wave(ob, bin, st, C, d, activate, f, u, v, t, s_bins);
+            first_hit_binned_wave(ob, bin, st, C, d, activate, f, u, v, t, s_bins,
+                                  oi == pre_obj ? pre : PreRange{0u, 0u, false});
         } else if (kCull && ob.bin_start && coop) {  // the workgroup's four sub-blocks together
             const uint32_t bin = ((cam_row(rm, py0) + kBinH - p.bin_phase) / kBinH) * p.bins_x + wx0 / kBinW;
-            first_hit_binned(p, ob, bin, st, C, d, activate, f, u, v, t, s_bins);
+            first_hit_binned(p, ob, bin, st, C, d, activate, f, u, v, t, s_bins,
+                             oi == pre_obj ? pre : PreRange{0u, 0u, false});
         } else if (!coop) {  // no bins (or too many faces for the wave's keys): this wave scans alone
             first_hit<kCull, false, false, kTestB>(p, sc, ob.tri_begin, ob.tri_count, st, C, d, bd, s_hot, s_cull,
                                                    activate, f, u, v, t);
@@ -970,6 +997,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
         }
     }
 
+    mid();
     ERAY_TRACE_WAVE0(5);
     // ---- hit data and Material::get (material.rs:56-94) --------------------------
     // The object loop only finds each lane's texel addresses; the loads are issued once after
@@ -1409,20 +1437,74 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
                 // of the second round.  (A device-wide atomic work counter instead measured
                 // 2.5x slower at 3840x2160 / 70k: one hot address under the frame's write stream.)
                 const uint32_t round = nk * nwaves;
-                for (uint32_t r = 0;; ++r) {  // workgroup-uniform
+                auto job = [&](uint32_t r, bool& valid, bool& coop) {  // round r's sub-block of this wave
                     const bool odd = (r & 1u) && kSnake;
-                    // the workgroup's first sub-block of round r (odd rounds reversed)
                     const uint32_t first = r * round + (odd ? round - nwaves - c0 : c0);
-                    if (first >= total) break;
-                    const uint32_t j = odd ? first + (nwaves - 1 - wave) : first + wave;
+                    valid = first < total;
+                    coop = first < heavy;
+                    return odd ? first + (nwaves - 1 - wave) : first + wave;
+                };
+                // Binned meshes with a detail list: the wave's next sub-block — its list entry and
+                // its bin range in the first binned object — is loaded during the current one
+                // (vector loads, used one sub-block later), so a round after the first starts
+                // with its search, not with two dependent round trips.
+                uint32_t pobj = ~0u;
+                const uint32_t* pstart = nullptr;
+                if constexpr (kLdsTiles && kCull) {
+                    if (dlist)
+                        for (uint32_t oi = 0; oi < nobj; ++oi) {
+                            const ObjGeom g = sc.geom(oi);
+                            if (g.bin_start) {
+                                pobj = oi;
+                                pstart = g.bin_start;
+                                break;
+                            }
+                        }
+                }
+                uint32_t nx_e = 0, nx_lo = 0, nx_hi = 0;  // (VGPRs: the loads' results)
+                bool nx_range = false;                    // nx_lo / nx_hi were issued
+                for (uint32_t r = 0;; ++r) {  // workgroup-uniform
+                    bool valid, coop;
+                    const uint32_t j = job(r, valid, coop);
+                    if (!valid) break;
                     const bool active = j < total;
                     int32_t sx = sx0, sy = sy0;
-                    if (r != 0 && active) locate(j, sx, sy);
+                    PreRange pre{0u, 0u, false};
+                    const bool have_pre = pstart && r != 0 && nx_range;
+                    if (r != 0 && active) {
+                        if (pstart) {  // prefetched during the previous sub-block
+                            const uint32_t e = __builtin_amdgcn_readfirstlane(nx_e);
+                            sx = (int32_t)(e & 0xffffu);
+                            sy = (int32_t)(e >> 16);
+                        } else {
+                            locate(j, sx, sy);
+                        }
+                    }
+                    if (have_pre && active)
+                        pre = PreRange{(uint32_t)__builtin_amdgcn_readfirstlane(nx_lo),
+                                       (uint32_t)__builtin_amdgcn_readfirstlane(nx_hi), true};
+                    // the next round's sub-block of this wave: its list entry now, its bin range
+                    // once this sub-block's first hits are known (mid)
+                    bool nvalid = false, ncoop = false;
+                    const uint32_t jn = job(r + 1, nvalid, ncoop);
+                    const bool nactive = nvalid && jn < total && pstart;
+                    if (nactive) nx_e = vload_u32(dlist, jn);
+                    nx_range = false;
+                    auto mid = [&]() {
+                        if (!nactive) return;
+                        const uint32_t e = __builtin_amdgcn_readfirstlane(nx_e);
+                        const uint32_t bin = ((cam_row(rm, (e >> 16) * kBlkH) + kBinH - p.bin_phase) / kBinH) * p.bins_x +
+                                             (e & 0xffffu);
+                        nx_lo = vload_u32(pstart, bin);
+                        nx_hi = vload_u32(pstart, bin + 1);
+                        nx_range = true;
+                    };
                     // the ordered detail list's heavy sub-blocks (bins of several chunks) come
                     // first: an iteration meeting one shares the work across the workgroup
                     render_sub<kCull, kLdsTiles, kMat>(p, fo, cam, rm, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH,
                                                        active, s_hot, s_cull, s_bins, s_rgb, s_ppm, aligned,
-                                                       (kGivenRay && r == 0) ? &d0 : nullptr, first < heavy);
+                                                       (kGivenRay && r == 0) ? &d0 : nullptr, coop,
+                                                       pre, pobj, mid);
                 }
             };
             if constexpr (kLdsScene) {

@@ -1,0 +1,76 @@
+"""Same-box A/B of library builds (diagnostics): each configuration's frame kernel timed per
+dispatch (eray_time_frames_ring) with the library ERAY_LIB selects.  Run once per build, alternating
+(scripts/ab_session.sh); prints one JSON line.
+
+    ERAY_LIB=eray_amd/lib/liberay_hip_base.so python scripts/ab_probe.py [--configs c2,ns1,ns4]
+
+Configs: c2 (cube 1920x1080, 8 frames per launch into 8 slots), c3 (70k stand-in 1920x1080, 4
+per launch), ns1 / ns4 (70k stand-in 3840x2160, one frame per launch, 1 / 4 ring slots), c5
+(1M faces 7680x4320), moving_ns (a moving camera over the 70k stand-in at 3840x2160)."""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from bench import dolly_path, frame_camera_fov  # noqa: E402
+from eray_amd import capi, meshgen  # noqa: E402
+from eray_amd.frame import MainScene  # noqa: E402
+from eray_amd.objfile import load_obj_file  # noqa: E402
+
+MESHES = {"cube": None, "70k": (69451, 42), "1m": (1_000_000, 1234)}
+CONFIGS = {"c2": ("cube", 1920, 1080, 8, 8), "c3": ("70k", 1920, 1080, 4, 4), "ns1": ("70k", 3840, 2160, 1, 1),
+           "ns4": ("70k", 3840, 2160, 4, 1), "c5": ("1m", 7680, 4320, 1, 1), "moving_ns": ("70k", 3840, 2160, 1, 1)}
+
+
+def mesh_of(kind):
+    if kind == "cube":
+        return load_obj_file(os.path.join(ROOT, "objects", "cube.obj"))
+    faces, seed = MESHES[kind]
+    path = os.path.join(tempfile.gettempdir(), f"standin_{faces}_{seed}.obj")
+    if not os.path.exists(path):
+        meshgen.generate(path, faces, seed)
+    return load_obj_file(path)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c2,c3,ns1,ns4")
+    ap.add_argument("--launches", type=int, default=40)
+    args = ap.parse_args()
+    out = {"lib": os.path.basename(capi.LIB_PATH)}
+    st = torch.cuda.Stream()
+    for name in args.configs.split(","):
+        kind, W, H, slots, F = CONFIGS[name]
+        ctx = capi.Context(0)
+        ctx.set_stream(st.cuda_stream)
+        sc = MainScene(ctx, *mesh_of(kind), W, H, texture=1024, fov=frame_camera_fov(W, H))
+        with torch.cuda.stream(st):
+            rgb = torch.empty((slots, H, W, 3), dtype=torch.float32, device="cuda")
+            ppm = torch.empty((slots, H, W, 3), dtype=torch.uint8, device="cuda")
+        kw = dict(out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr(), ring=capi.frame_ring(slots, H, W, F))
+        if name.startswith("moving"):
+            path = dolly_path(32, frame_camera_fov(W, H), W)
+            ctx.render_camera_path(path, W, H, **kw)
+            out[name] = {"device_ms_per_frame": min(ctx.render_camera_path(path, W, H, timed=True, **kw)
+                                                    for _ in range(3))}
+        else:
+            ctx.render_frames(max(slots, 4), W, H, **kw)
+            n = max(args.launches // (4 if name == "c5" else 1), 2) * F
+            out[name] = ctx.time_frames(n, W, H, **kw)
+        torch.cuda.synchronize()
+        del rgb, ppm
+        sc.close()
+        ctx.close()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
