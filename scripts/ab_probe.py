@@ -6,7 +6,9 @@ dispatch (eray_time_frames_ring) with the library ERAY_LIB selects.  Run once pe
 
 Configs: c2 (cube 1920x1080, 8 frames per launch into 8 slots), c3 (70k stand-in 1920x1080, 4
 per launch), ns1 / ns4 (70k stand-in 3840x2160, one frame per launch, 1 / 4 ring slots), c5
-(1M faces 7680x4320), moving_ns (a moving camera over the 70k stand-in at 3840x2160)."""
+(1M faces 7680x4320), moving_ns (a moving camera over the 70k stand-in at 3840x2160), aa2 / aa_ns
+(anti-aliasing = 4 through the general tracer: C2, the 70k stand-in at 3840x2160; graph-replayed
+frames, device ms per frame), fill* (the same camera and lights, no object)."""
 from __future__ import annotations
 
 import argparse
@@ -26,8 +28,12 @@ from eray_amd.frame import MainScene  # noqa: E402
 from eray_amd.objfile import load_obj_file  # noqa: E402
 
 MESHES = {"cube": None, "70k": (69451, 42), "1m": (1_000_000, 1234)}
-CONFIGS = {"c2": ("cube", 1920, 1080, 8, 8), "c3": ("70k", 1920, 1080, 4, 4), "ns1": ("70k", 3840, 2160, 1, 1),
-           "ns4": ("70k", 3840, 2160, 4, 1), "c5": ("1m", 7680, 4320, 1, 1), "moving_ns": ("70k", 3840, 2160, 1, 1)}
+CONFIGS = {"fill4k1": ("none", 3840, 2160, 1, 1), "fill4k4": ("none", 3840, 2160, 4, 1),
+           "fill8k": ("none", 7680, 4320, 1, 1), "fillc2": ("none", 1920, 1080, 8, 8),
+           "c2": ("cube", 1920, 1080, 8, 8), "c3": ("70k", 1920, 1080, 4, 4), "ns1": ("70k", 3840, 2160, 1, 1),
+           "ns4": ("70k", 3840, 2160, 4, 1), "c5": ("1m", 7680, 4320, 1, 1), "moving_ns": ("70k", 3840, 2160, 1, 1),
+           "moving_c5": ("1m", 7680, 4320, 1, 1),
+           "aa2": ("cube", 1920, 1080, 1, 1), "aa_ns": ("70k", 3840, 2160, 1, 1)}
 
 
 def mesh_of(kind):
@@ -51,12 +57,23 @@ def main() -> None:
         kind, W, H, slots, F = CONFIGS[name]
         ctx = capi.Context(0)
         ctx.set_stream(st.cuda_stream)
-        sc = MainScene(ctx, *mesh_of(kind), W, H, texture=1024, fov=frame_camera_fov(W, H))
+        if kind == "none":  # the same camera and lights, no object: the fill alone
+            from bench import empty_scene_context
+            ctx.close()
+            ctx = empty_scene_context(0, W, H, frame_camera_fov(W, H), st)
+            sc = None
+        else:
+            sc = MainScene(ctx, *mesh_of(kind), W, H, texture=1024, fov=frame_camera_fov(W, H))
         with torch.cuda.stream(st):
             rgb = torch.empty((slots, H, W, 3), dtype=torch.float32, device="cuda")
             ppm = torch.empty((slots, H, W, 3), dtype=torch.uint8, device="cuda")
         kw = dict(out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr(), ring=capi.frame_ring(slots, H, W, F))
-        if name.startswith("moving"):
+        if name.startswith("aa"):  # the general tracer, anti_aliasing = 4 (bench.py anti_aliasing_line)
+            akw = dict(kw, anti_aliasing=4, aa_seed=12345)
+            del akw["ring"]
+            ctx.render_frames(20, W, H, prepare_only=True, **akw)
+            out[name] = {"frame_ms": min(ctx.render_frames(20, W, H, timed=True, **akw) for _ in range(3))}
+        elif name.startswith("moving"):
             path = dolly_path(32, frame_camera_fov(W, H), W)
             ctx.render_camera_path(path, W, H, **kw)
             out[name] = {"device_ms_per_frame": min(ctx.render_camera_path(path, W, H, timed=True, **kw)
@@ -67,7 +84,8 @@ def main() -> None:
             out[name] = ctx.time_frames(n, W, H, **kw)
         torch.cuda.synchronize()
         del rgb, ppm
-        sc.close()
+        if sc:
+            sc.close()
         ctx.close()
     print(json.dumps(out), flush=True)
 
