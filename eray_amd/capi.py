@@ -191,6 +191,7 @@ SIGNATURES = {
 # Diagnostics exported beside the header's API (not part of include/eray_hip.h).
 DEBUG_SIGNATURES = {
     "eray_debug_bin_stats": (C.c_int, [_P, _U, C.POINTER(C.c_uint64)]),
+    "eray_debug_set_bin_form": (C.c_int, [_P, C.c_int]),
     "eray_debug_bin_dump": (C.c_int, [_P, _U, _U, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64), _U,
                                       C.POINTER(C.c_uint32)]),
     "eray_debug_set_bin_capacity": (C.c_int, [_P, C.c_uint64]),
@@ -237,6 +238,8 @@ def lib():
             fn.restype = res
             fn.argtypes = args
         for name, (res, args) in DEBUG_SIGNATURES.items():
+            if os.environ.get("ERAY_LIB") and not hasattr(L, name):
+                continue  # (an older diagnostics build under A/B: debug entry points it predates)
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

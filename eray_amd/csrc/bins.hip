@@ -54,9 +54,138 @@ constexpr uint32_t kShards = 32, kShardStride = 32;
 constexpr uint32_t kAccStride = 16;
 
 
+// Inclusive prefix max over the wave's lanes (DPP row shifts, then the row broadcasts; an invalid
+// source lane reads 0, the identity).  Every lane of the wave calls.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint32_t dpp_max_step(uint32_t v) {
+    return max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, kRowMask, 0xf, false));
+}
+__device__ __forceinline__ uint32_t wave_prefix_max(uint32_t v) {
+    v = dpp_max_step<0x111, 0xf>(v);  // row_shr:1
+    v = dpp_max_step<0x112, 0xf>(v);  // row_shr:2
+    v = dpp_max_step<0x114, 0xf>(v);  // row_shr:4
+    v = dpp_max_step<0x118, 0xf>(v);  // row_shr:8: each row's inclusive prefix
+    v = dpp_max_step<0x142, 0xa>(v);  // row_bcast:15 (rows 1 and 3)
+    return dpp_max_step<0x143, 0xc>(v);  // row_bcast:31 (rows 2 and 3)
+}
+
+// The setup enumerates units of every binned face — the (face, bin) pairs of its bin rectangle,
+// or the rectangle's bin rows (segments, below) — in face order, with face i's first unit at
+// boff[i / chunk] + first_local[i] (its setup chunk's offset + its place in the chunk's own scan)
+// and all P units at boff[nparts].  Every wave walks its own contiguous range of units, 64 at a
+// time: one search for the face of its first unit, after which each slice starts from the face of
+// the previous slice's last unit (the next slice's face ranges loaded ahead).  (A grid-stride
+// loop searched anew for every slice — ~12 dependent global loads per 64 units, the pass's
+// critical path: C5's four-camera build 1.3-1.8 ms.)  body(j, valid, face) runs once per slice
+// with every lane of the wave (lane = unit j; `valid`: j is one of the wave's units).
+struct UnitWalk {
+    const unsigned long long* s_boff;  // (LDS) boff
+    const unsigned long long* first_local;
+    uint32_t nparts, chunk, T;
+    uint32_t* s_face;  // (LDS) kBinWG words: the faces starting at each lane's unit
+};
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+template <typename Body>
+__device__ __forceinline__ void walk_units(const UnitWalk& u, Body&& body) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned long long P = u.s_boff[u.nparts];
+    auto first = [&](uint32_t i) { return u.s_boff[i / u.chunk] + u.first_local[i]; };
+    auto face_of = [&](unsigned long long j) -> uint32_t {
+        // the chunk: the last one starting at or before j (in LDS; an empty chunk never is, the next
+        // one starts at the same unit) ...
+        uint32_t cb = 0, ce = u.nparts;
+        while (ce - cb > 1) {
+            const uint32_t mid = (cb + ce) >> 1;
+            if (u.s_boff[mid] <= j) cb = mid;
+            else ce = mid;
+        }
+        // ... then, inside it, the last face whose first unit is <= j
+        const unsigned long long jl = j - u.s_boff[cb];
+        uint32_t lo = cb * u.chunk, hi = min(lo + u.chunk, u.T);
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (u.first_local[mid] <= jl) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo - 1;
+    };
+    const unsigned long long slices = (unsigned long long)gridDim.x * (kBinWG / 64) * 64ull;
+    const unsigned long long per = (P + slices - 1) / slices * 64ull;  // units per wave (multiple of 64)
+    const unsigned long long w_lo = ((unsigned long long)blockIdx.x * (kBinWG / 64) + wave) * per;
+    const unsigned long long w_hi = min(w_lo + per, P);
+    uint32_t fb = w_lo < P ? face_of(w_lo) : 0u;
+    // face fi's units [a, b) for the 64 faces from fb on (P past the last face)
+    auto face_units = [&](uint32_t fb0, unsigned long long& a, unsigned long long& b) {
+        const uint32_t fi = fb0 + lane;
+        a = P;
+        b = P;
+        if (fi < u.T) {
+            a = first(fi);
+            b = fi + 1 < u.T ? first(fi + 1) : P;
+        }
+    };
+    unsigned long long pa, pb;  // the next slice's first 64 faces' units, loaded ahead
+    face_units(fb, pa, pb);
+    for (unsigned long long j0 = w_lo; j0 < w_hi; j0 += 64) {  // wave-uniform
+        const unsigned long long jend = min(j0 + 64ull, w_hi), j = j0 + lane;
+        // The wave's 64 consecutive units belong to a run of consecutive faces from fb on: each
+        // non-empty face starting inside the slice writes its index at its first unit's slot (no
+        // two do: the ranges are contiguous), then a prefix max over the lanes gives every slot
+        // the last face starting at or before it — its owner; slot 0's owner may start earlier,
+        // and is then fb, the previous slice's last face (a face starting at j0 overrides it).
+        u.s_face[threadIdx.x] = lane ? 0u : fb;
+        wave_sync();
+        bool ahead = true;  // the first 64 faces were loaded ahead
+        for (unsigned long long covered = j0; covered < jend; fb += 64, ahead = false) {  // wave-uniform
+            unsigned long long a = pa, b = pb;
+            if (!ahead) face_units(fb, a, b);
+            if (a < b && a >= j0 && a < jend) u.s_face[64 * wave + (uint32_t)(a - j0)] = fb + lane;
+            covered = (unsigned long long)__shfl((long long)b, 63);
+        }
+        wave_sync();
+        const uint32_t owner = wave_prefix_max(u.s_face[threadIdx.x]);
+        fb = (uint32_t)__builtin_amdgcn_readlane((int)owner, (int)(jend - 1 - j0));  // the next slice starts in this face or later
+        if (jend < w_hi) face_units(fb, pa, pb);  // in flight while this slice's units are processed
+        body(j, j < jend, owner, j < jend ? j - first(owner) : 0ull);
+    }
+}
+
+// Entries appended to the shard's region of the entry list (one counter atomic per wave and
+// call), each with its rank in its bin from the bin's count atomic (the scatter then needs no
+// atomics: a returning atomic per entry there cost as much as this pass).  Every lane calls; m == 0:
+// no entry.
+struct EntryOut {
+    uint32_t *n, *count, *ekey, *eface, *erank;
+    unsigned long long* emask;
+    uint32_t shard, region;
+};
+__device__ __forceinline__ void append_entries(const EntryOut& o, unsigned long long m, uint32_t key, uint32_t face) {
+    const uint32_t lane = threadIdx.x & 63;
+    const unsigned long long bal = __ballot(m != 0);
+    if (!bal) return;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(o.n + o.shard * kShardStride, (uint32_t)__popcll(bal));
+    base = (uint32_t)__shfl((int)base, 0);
+    if (m) {
+        const uint32_t local = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+        if (local < o.region) {
+            const uint32_t slot = o.shard * o.region + local;
+            o.erank[slot] = atomicAdd(o.count + key, 1u);
+            o.ekey[slot] = key;
+            o.eface[slot] = face;
+            o.emask[slot] = m;
+        }
+    }
+}
+
 // (face, bin) pairs of the binned faces' bin rectangles (face-major, each rectangle row-major):
-// the non-empty ones appended to the entry list, counted per bin key.  kJitter: the general
-// tracer's masks (bin_pixels_jittered, SetupParams::keep_all).
+// the non-empty ones appended to the entry list, counted per bin key.  The general tracer's setup
+// (kJitter, SetupParams::keep_all: bin_pixels_jittered's masks) and frames wider than 65535
+// pixels; otherwise bin_segments_kernel.
 // waves per SIMD the pair pass is built for: 6 (80 VGPRs, a few spills in the mask path) over
 // 5 (88 VGPRs): C5's moving-camera frame 491 -> 476 us; 8 (64 VGPRs, 22 spills) 525 us
 constexpr int kPairsWaves = 6;
@@ -84,14 +213,9 @@ __global__ void __launch_bounds__(kBinWG, kPairsWaves) bin_pairs_kernel(const Tr
     const unsigned long long lt = (1ull << lane) - 1ull;
     // each wave appends to shard (global wave index) % kShards, one counter atomic per 64 kept pairs
     const uint32_t shard = (blockIdx.x * (kBinWG / 64) + wave) % kShards, region = cap / kShards;
-    __shared__ uint32_t s_face[kBinWG];  // each lane's pair's face
+    __shared__ uint32_t s_face[kBinWG];  // the faces starting at each lane's pair (then the prefix max)
     // each wave's queue of pairs that survive the bin-rectangle test: face, bin (tx | ty << 16), key
     __shared__ uint32_t s_qf[kBinWG / 64][128], s_qt[kBinWG / 64][128], s_qk[kBinWG / 64][128];
-    auto wave_sync = []() {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
     auto face_of = [&](unsigned long long j) -> uint32_t {
         // the chunk: the last one starting at or before j (in LDS; an empty chunk never is, the next
         // one starts at the same pair) ...
@@ -172,22 +296,28 @@ __global__ void __launch_bounds__(kBinWG, kPairsWaves) bin_pairs_kernel(const Tr
     uint32_t qn = 0;  // queued pairs (wave-uniform)
     for (unsigned long long j0 = w_lo; j0 < w_hi; j0 += 64) {  // wave-uniform
         const unsigned long long jend = min(j0 + 64ull, w_hi), j = j0 + lane;
-        // The wave's 64 consecutive pairs belong to a run of consecutive faces from fb on: 64 faces
-        // at a time each write their face index into the slots of the wave's pairs they own.
+        // The wave's 64 consecutive pairs belong to a run of consecutive faces from fb on: each
+        // non-empty face starting inside the slice writes its index at its first pair's slot (no
+        // two do: the ranges are contiguous), then a prefix max over the lanes gives every slot
+        // the last face starting at or before it — its owner; slot 0's owner may start earlier,
+        // and is then fb, the previous slice's last face (a face starting at j0 overrides it).
+        s_face[threadIdx.x] = lane ? 0u : fb;
+        wave_sync();
         bool ahead = true;  // the first 64 faces were loaded ahead
         for (unsigned long long covered = j0; covered < jend; fb += 64, ahead = false) {  // wave-uniform
             unsigned long long a = pa, b = pb;
             if (!ahead) face_pairs(fb, a, b);
-            for (unsigned long long q = max(a, j0); q < min(b, jend); ++q) s_face[64 * wave + (uint32_t)(q - j0)] = fb + lane;
+            if (a < b && a >= j0 && a < jend) s_face[64 * wave + (uint32_t)(a - j0)] = fb + lane;
             covered = (unsigned long long)__shfl((long long)b, 63);
         }
         wave_sync();
-        fb = s_face[64 * wave + (uint32_t)(jend - 1 - j0)];  // the next slice starts in this face or later
+        const uint32_t owner = wave_prefix_max(s_face[threadIdx.x]);
+        fb = (uint32_t)__builtin_amdgcn_readlane((int)owner, (int)(jend - 1 - j0));  // the next slice starts in this face or later
         if (jend < w_hi) face_pairs(fb, pa, pb);  // in flight while this slice's pairs are tested
         bool keep = false;
         uint32_t i = 0, tx = 0, ty = 0, key = 0;
         if (j < jend) {
-            i = s_face[threadIdx.x];
+            i = owner;
             key = fkey[i];  // (in the same round trip as the face's records)
             const int4 g = range[i];
             const uint32_t w = (uint32_t)(g.y - g.x + 1);
@@ -242,6 +372,86 @@ __global__ void __launch_bounds__(kBinWG, kPairsWaves) bin_pairs_kernel(const Tr
         }
     }
     if (qn) emit(qn);
+}
+
+// Segments (frame setups): the units are the bin rows of each binned face's bin rectangle.  A
+// segment's four camera rows each get the pixel range where all four culling conditions of the
+// face can pass — bin_pixels' own double-precision lines (face_rect.hpp row_range), over the
+// rectangle's columns instead of one bin's 16: the same values, so a bin's bin_pixels mask is
+// exactly those ranges cut to its columns — and only the bins the ranges reach become pairs,
+// dealt over the wave's lanes (lane = pair) so that one long segment (a sliver across the frame)
+// does not serialise its wave.  Every pair bin_pixels would mark non-empty is appended, with the
+// same mask, so the entries are the rectangle form's (which also drops pairs its f32 pre-test
+// rejects: the frame kernel's exact tests decide either way).  C5: 7.06M rectangle pairs per
+// camera for 0.47M entries — the rectangle form spent its time walking the empty ones.
+__global__ void __launch_bounds__(kBinWG, kPairsWaves) bin_segments_kernel(const TriCull* __restrict__ cull,
+                                                              const int4* __restrict__ range,
+                                                              const unsigned long long* __restrict__ first_local,
+                                                              const unsigned long long* __restrict__ boff,
+                                                              uint32_t nparts, uint32_t chunk,
+                                                              const uint32_t* __restrict__ fkey, uint32_t T, uint32_t W,
+                                                              uint32_t H, uint32_t phase, uint32_t bins_x,
+                                                              uint32_t nbins, uint32_t cap, uint32_t* __restrict__ n,
+                                                              uint32_t* __restrict__ count, uint32_t* __restrict__ ekey,
+                                                              uint32_t* __restrict__ eface,
+                                                              unsigned long long* __restrict__ emask,
+                                                              uint32_t* __restrict__ erank) {
+    __shared__ unsigned long long s_boff[kSetupMaxBlocks + 1];
+    __shared__ uint32_t s_face[kBinWG];
+    __shared__ uint32_t s_own[kBinWG];  // the lanes whose segment's pairs start at each slot
+    for (uint32_t b = threadIdx.x; b <= nparts; b += kBinWG) s_boff[b] = boff[b];
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const EntryOut out{n, count, ekey, eface, erank, emask, (blockIdx.x * (kBinWG / 64) + wave) % kShards, cap / kShards};
+    const UnitWalk u{s_boff, first_local, nparts, chunk, T, s_face};
+    walk_units(u, [&](unsigned long long, bool valid, uint32_t i, unsigned long long c) {
+        // the lane's segment: face i, bin row ty, its rows' pixel ranges packed lo | hi << 16 (lo >
+        // hi: none) and its bins [bx0, bx0 + width)
+        uint32_t ty = 0, key = 0, bx0 = 0, width = 0;
+        uint32_t rr[kBinH] = {1u, 1u, 1u, 1u};
+        if (valid) {
+            const int4 g = range[i];
+            key = fkey[i];
+            ty = (uint32_t)g.z + (uint32_t)c;
+            const int32_t xa = g.x * (int32_t)kBinW, xb = min((g.y + 1) * (int32_t)kBinW, (int32_t)W) - 1;
+            int32_t lo = INT32_MAX, hi = INT32_MIN;
+            row_ranges(cull[i], W, H, phase, ty, xa, xb, rr, lo, hi);
+            if (lo <= hi) {
+                bx0 = (uint32_t)lo / kBinW;
+                width = (uint32_t)hi / kBinW - bx0 + 1;
+            }
+        }
+        // the wave's pairs: lane l's segment owns [start_l, start_l + width_l)
+        uint32_t incl = width;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, off);
+            if ((int)lane >= off) incl += y;
+        }
+        const uint32_t total = (uint32_t)__shfl((int)incl, 63), start = incl - width;
+        uint32_t cur = 0;  // the lane owning the pair before the window
+        for (uint32_t t0 = 0; t0 < total; t0 += 64) {  // (wave-uniform)
+            s_own[threadIdx.x] = lane ? 0u : cur;
+            wave_sync();
+            if (width && start >= t0 && start < t0 + 64) s_own[64 * wave + (start - t0)] = lane;
+            wave_sync();
+            const uint32_t o = wave_prefix_max(s_own[threadIdx.x]);  // (lanes in segment order)
+            cur = (uint32_t)__builtin_amdgcn_readlane((int)o, 63);
+            const uint32_t t = t0 + lane;
+            // the owner's segment
+            const uint32_t oi = (uint32_t)__shfl((int)i, (int)o), oty = (uint32_t)__shfl((int)ty, (int)o);
+            const uint32_t okey = (uint32_t)__shfl((int)key, (int)o), obx0 = (uint32_t)__shfl((int)bx0, (int)o);
+            const uint32_t ostart = (uint32_t)__shfl((int)start, (int)o);
+            uint32_t orr[kBinH];
+#pragma unroll
+            for (uint32_t r = 0; r < kBinH; ++r) orr[r] = (uint32_t)__shfl((int)rr[r], (int)o);
+            unsigned long long m = 0;
+            const uint32_t bx = obx0 + (t - ostart);
+            if (t < total) m = bin_mask_of_rows(orr, bx);
+            append_entries(out, m, okey * nbins + oty * bins_x + bx, oi);
+            wave_sync();  // (s_own is rewritten by the next window)
+        }
+    });
 }
 
 // every stored entry to its bin: start[key] + its rank; the counts back to zero for the next camera
@@ -609,7 +819,7 @@ __global__ void __launch_bounds__(kBinWG) detail_append_kernel(const uint32_t* _
 // kernel slot), kPairGrid if unknown.
 uint32_t resident_grid(const void* k, int slot) {
     static std::mutex mu;
-    static int per_cu[2] = {-1, -1}, cus = -1;
+    static int per_cu[3] = {-1, -1, -1}, cus = -1;
     std::lock_guard<std::mutex> lock(mu);
     if (cus < 0) {
         int dev = 0;
@@ -702,10 +912,10 @@ hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tile
     const uint32_t ncam = multi ? sp.ncam : 1u;
     if (sp.T) {  // (a multi-camera build may set up fewer cameras than the buffers hold)
         const uint32_t nparts = setup_blocks(sp.T), chunk = (sp.T + nparts - 1) / nparts;  // as camera_setup_kernel
-        auto* k = sp.keep_all ? bin_pairs_kernel<true> : bin_pairs_kernel<false>;
-        // exactly the resident workgroups (each wave walks a fixed share of the pairs: a second
+        auto* k = bin_segments(sp) ? bin_segments_kernel : sp.keep_all ? bin_pairs_kernel<true> : bin_pairs_kernel<false>;
+        // exactly the resident workgroups (each wave walks a fixed share of the units: a second
         // round of workgroups would double the pass)
-        const uint32_t pgrid = resident_grid(reinterpret_cast<const void*>(k), sp.keep_all ? 1 : 0);
+        const uint32_t pgrid = resident_grid(reinterpret_cast<const void*>(k), bin_segments(sp) ? 2 : sp.keep_all ? 1 : 0);
         k<<<pgrid, kBinWG, 0, s>>>(sp.cull, sp.range, b.first, b.boff, nparts, chunk, sp.fkey, sp.T, sp.W, sp.H, sp.phase,
                                        b.bins_x, b.nbins, (uint32_t)b.cap, b.n, b.count, b.ekey, b.eface, b.emask, b.erank);
         if ((e = hipGetLastError()) != hipSuccess) return e;

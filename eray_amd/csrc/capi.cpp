@@ -127,6 +127,7 @@ struct eray_ctx {
     bool state_pending = false;   // a copy into h_state is in flight
     bool state_known = false;     // h_state holds the results of the setup of setup_key
     std::vector<uint64_t> setup_key;  // camera, size, rows and scene generation of the last setup
+    std::vector<uint64_t> tcull_key;  // camera, size, scene generation and stream of d_tcull's records
     FrameSource setup_src;        // the last enqueued scene-camera setup: its source key and rows
     ObjectDesc* h_objs_state = nullptr;  // pinned copy of the descriptors after that setup (pixel rectangles)
     size_t h_objs_state_cap = 0;
@@ -163,6 +164,7 @@ struct eray_ctx {
     std::vector<uint64_t> bins_layout;
     uint64_t bins_gen = 0;        // bumped whenever bins_alloc (re)allocates the bin buffers
     size_t bin_cap = 0;           // entry capacity to allocate (grown when a setup overflows)
+    bool rect_pairs = false;      // (diagnostics) setups walk the bin rectangles' pairs (bins.hip)
     // camera paths (eray_render_camera_path): the cameras of the current graph chunk on the
     // device, the whole path staged in pinned memory
     CamDev* d_path = nullptr;
@@ -553,6 +555,7 @@ SetupParams setup_params(eray_ctx* ctx, const CamDev* d_camera, uint32_t W, uint
     sp.acc = ctx->d_acc + 1 + 10 * (size_t)kSetupMaxBlocks;
     const bool binned = binned_objects(ctx) > 0;
     sp.binned = binned ? 1u : 0u;
+    sp.rect_pairs = ctx->rect_pairs ? 1u : 0u;
     if (binned) {
         sp.range = ctx->d_range;
         sp.area = ctx->d_area;
@@ -1202,6 +1205,18 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
     p.seed_hi = (uint32_t)(rp->aa_seed >> 32);
     p.trace_cull = (general && !(rp->flags & ERAY_RENDER_BRUTE_FORCE) && ctx->total_tris <= kTraceSkipTris)
                        ? ctx->d_tcull : nullptr;
+    if (p.trace_cull) {  // the tracer's culling records of this camera (enqueued when it or the scene changed)
+        std::vector<uint64_t> key(sizeof(eray_camera) / 4 + 3);
+        std::memcpy(key.data(), &ctx->camera, sizeof(eray_camera));
+        key[key.size() - 3] = ctx->scene_gen;
+        key[key.size() - 2] = ((uint64_t)W << 32) | H;
+        key[key.size() - 1] = (uint64_t)reinterpret_cast<uintptr_t>(ctx->stream);
+        if (key != ctx->tcull_key) {
+            ctx->tcull_key.clear();
+            HIP_TRY(ctx, launch_trace_cull(p, ctx->stream));
+            ctx->tcull_key = std::move(key);
+        }
+    }
     p.trace_bins = trace_bins ? 1u : 0u;
     if (trace_bins) {  // the setup's detail list (trace.hip trace_binned_kernel, trace_heavy_kernel)
         p.detail_list = ctx->bins.dlist;
@@ -2025,7 +2040,8 @@ void* eray_internal_staging(eray_ctx* ctx, size_t bytes) {
 // out[3] most entries in one bin, out[4] non-empty bins, out[5] most pairs in one bin,
 // out[6..9] the object's pixel rectangle (x0, x1, y0, y1; int32 as uint64), out[10] the bin with
 // the most entries, out[11] / out[12] the bins of more than 64 / kTraceHeavyMin entries, out[13]
-// the pairs of the faces' bin rectangles before masking (out: 14 words).  Synchronises.
+// the units the pair pass walked: the faces' bin-rectangle rows (segments) or their (face, bin)
+// pairs (the tracer's setups, eray_debug_set_bin_form) (out: 14 words).  Synchronises.
 extern "C" int eray_debug_bin_stats(eray_ctx* ctx, uint32_t index, uint64_t* out) {
     if (!ctx || !out || index >= ctx->objects.size() || ctx->objects[index].T <= kDirectMax || !ctx->bins.start)
         return ERAY_E_INVALID_ARGUMENT;
@@ -2065,7 +2081,7 @@ extern "C" int eray_debug_bin_stats(eray_ctx* ctx, uint32_t index, uint64_t* out
     out[10] = most_at;
     out[11] = over64;
     out[12] = over192;
-    // out[13]: the (face, bin) pairs of the faces' bin rectangles before masking (every object)
+    // out[13]: the units of the faces' bin rectangles (every object)
     unsigned long long pairs_all = 0;
     if (hipMemcpy(&pairs_all, b.boff + setup_blocks(ctx->total_tris), sizeof pairs_all, hipMemcpyDeviceToHost) != hipSuccess)
         return set_error(ctx, ERAY_E_HIP, "bin stats copy failed");
@@ -2105,6 +2121,16 @@ extern "C" int eray_debug_set_bin_capacity(eray_ctx* ctx, uint64_t entries) {
     return ERAY_OK;
 }
 extern "C" uint64_t eray_debug_bin_capacity(const eray_ctx* ctx) { return ctx ? (uint64_t)ctx->bins.cap : 0u; }
+// Diagnostics: the frame setups' pair pass walks every (face, bin) pair of the faces' bin
+// rectangles (rect_pairs != 0) instead of the rectangles' rows (bins.hip bin_segments_kernel);
+// the next setup rebuilds the bins (tests compare the two forms' entries).
+extern "C" int eray_debug_set_bin_form(eray_ctx* ctx, int rect_pairs) {
+    if (!ctx) return ERAY_E_INVALID_ARGUMENT;
+    ctx->rect_pairs = rect_pairs != 0;
+    ctx->setup_key.clear();
+    ctx->mc_layout.clear();
+    return ERAY_OK;
+}
 // Diagnostics: the last setup's device state (CamState, 176 B) and object `index`'s pixel
 // rectangle as the frame kernel reads them (synchronises).
 extern "C" int eray_debug_setup_state(eray_ctx* ctx, uint32_t index, void* state_out, int32_t* rect_out) {

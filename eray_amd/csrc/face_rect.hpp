@@ -132,35 +132,85 @@ __device__ inline CondLine cond_line(float A, float B, float K, float T, uint32_
     l.kind = A > 0.0f ? 1 : 2;
     return l;
 }
+// Row r of bin row `by` (camera row y = by * kBinH + phase + r - kBinH; yf the reference's f32
+// y / H, camera_dir): the columns [xl, xr] of [x_lo, x_hi] where all four lines can pass; false
+// when there are none.  (apply_line's cases as selects: lanes hold pairs of different faces,
+// whose condition kinds differ — branches diverged 3 ways per condition and row.)
+__device__ inline bool row_span(const CondLine (&l)[4], uint32_t H, uint32_t phase, uint32_t by, uint32_t r,
+                                int32_t x_lo, int32_t x_hi, int32_t& xl_out, int32_t& xr_out) {
+    const int32_t y = (int32_t)(by * kBinH + phase + r) - (int32_t)kBinH;
+    const double yf = (double)((float)(uint32_t)y / (float)H);
+    double xl = (double)x_lo, xr = (double)x_hi;
+    bool fail = y < 0 || y >= (int32_t)H;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double q = l[k].c0 - l[k].c1 * yf;
+        const double lo = ceil(q - l[k].tol), hi = floor(q + l[k].tol);
+        xl = (l[k].kind == 1 && lo > xl) ? lo : xl;
+        xr = (l[k].kind == 2 && hi < xr) ? hi : xr;
+        fail |= l[k].kind == 3 && q > l[k].tol;
+    }
+    if (fail || !(xl <= xr)) return false;  // (xl >= x_lo, xr <= x_hi)
+    xl_out = (int32_t)xl;
+    xr_out = (int32_t)xr;
+    return true;
+}
+__device__ inline void cond_lines(const TriCull& c, uint32_t W, CondLine (&l)[4]) {
+    l[0] = cond_line(c.A.x, c.B.x, c.K.x, c.T.x, W);
+    l[1] = cond_line(c.A.y, c.B.y, c.K.y, c.T.y, W);
+    l[2] = cond_line(c.A.z, c.B.z, c.K.z, c.T.z, W);
+    l[3] = cond_line(c.A.w, c.B.w, c.K.w, c.T.w, W);
+}
+// bits [xl, xr] of a bin starting at column x_lo, in its row r (bit r * kBinW + column)
+__device__ __forceinline__ unsigned long long row_bits(int32_t xl, int32_t xr, int32_t x_lo, uint32_t r) {
+    const uint32_t n = (uint32_t)(xr - xl + 1), s = (uint32_t)(xl - x_lo);
+    return (unsigned long long)((((n >= 32 ? 0xffffffffu : ((1u << n) - 1u)) << s) & 0xffffu)) << (kBinW * r);
+}
+
 // Pixels of the kBinW x kBinH bin at (bx, by) (camera columns bx*kBinW.., rows y0..y0+3 with
 // y0 = by*kBinH + phase - kBinH) where all four conditions of record c can pass: bit
-// r * kBinW + col.  The rows' yf are the reference's f32 y/H (camera_dir).
+// r * kBinW + col.
 __device__ inline unsigned long long bin_pixels(const TriCull& c, uint32_t W, uint32_t H, uint32_t phase,
                                                 uint32_t bx, uint32_t by) {
-    const CondLine l[4] = {cond_line(c.A.x, c.B.x, c.K.x, c.T.x, W), cond_line(c.A.y, c.B.y, c.K.y, c.T.y, W),
-                           cond_line(c.A.z, c.B.z, c.K.z, c.T.z, W), cond_line(c.A.w, c.B.w, c.K.w, c.T.w, W)};
+    CondLine l[4];
+    cond_lines(c, W, l);
     const int32_t x_lo = (int32_t)(bx * kBinW), x_hi = min((int32_t)((bx + 1) * kBinW), (int32_t)W) - 1;
     unsigned long long pix = 0;
-    // apply_line's cases as selects (lanes hold pairs of different faces, whose condition kinds
-    // differ: branches diverged 3 ways per condition and row), the same double operations
 #pragma unroll
     for (uint32_t r = 0; r < kBinH; ++r) {
-        const int32_t y = (int32_t)(by * kBinH + phase + r) - (int32_t)kBinH;
-        const double yf = (double)((float)(uint32_t)y / (float)H);
-        double xl = (double)x_lo, xr = (double)x_hi;
-        bool fail = y < 0 || y >= (int32_t)H;
+        int32_t xl, xr;
+        if (row_span(l, H, phase, by, r, x_lo, x_hi, xl, xr)) pix |= row_bits(xl, xr, x_lo, r);
+    }
+    return pix;
+}
+
+// The same rows over the columns [xa, xb] of a face's bin rectangle (bins.hip
+// bin_segments_kernel): rr[r] = xl | xr << 16 (1: no column; columns < 65536), [lo, hi] the rows'
+// extent (lo > hi: none).  A bin's bin_pixels mask is these ranges cut to its 16 columns
+// (bin_mask_of_rows): the lines and each row's bounds are the same double values, and a bin's
+// range is max / min of them with its own first / last column.
+__device__ inline void row_ranges(const TriCull& c, uint32_t W, uint32_t H, uint32_t phase, uint32_t by, int32_t xa,
+                                  int32_t xb, uint32_t (&rr)[kBinH], int32_t& lo, int32_t& hi) {
+    CondLine l[4];
+    cond_lines(c, W, l);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const double q = l[k].c0 - l[k].c1 * yf;
-            const double lo = ceil(q - l[k].tol), hi = floor(q + l[k].tol);
-            xl = (l[k].kind == 1 && lo > xl) ? lo : xl;
-            xr = (l[k].kind == 2 && hi < xr) ? hi : xr;
-            fail |= l[k].kind == 3 && q > l[k].tol;
+    for (uint32_t r = 0; r < kBinH; ++r) {
+        int32_t xl, xr;
+        rr[r] = 1u;
+        if (row_span(l, H, phase, by, r, xa, xb, xl, xr)) {
+            rr[r] = (uint32_t)xl | ((uint32_t)xr << 16);
+            lo = min(lo, xl);
+            hi = max(hi, xr);
         }
-        if (!fail && xl <= xr) {  // (xl >= x_lo, xr <= x_hi: both within the bin's columns)
-            const uint32_t n = (uint32_t)((int32_t)xr - (int32_t)xl + 1), s = (uint32_t)((int32_t)xl - x_lo);
-            pix |= (unsigned long long)((((n >= 32 ? 0xffffffffu : ((1u << n) - 1u)) << s) & 0xffffu)) << (kBinW * r);
-        }
+    }
+}
+__device__ __forceinline__ unsigned long long bin_mask_of_rows(const uint32_t (&rr)[kBinH], uint32_t bx) {
+    const int32_t x_lo = (int32_t)(bx * kBinW), x_hi = x_lo + (int32_t)kBinW - 1;
+    unsigned long long pix = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < kBinH; ++r) {
+        const int32_t xl = max((int32_t)(rr[r] & 0xffffu), x_lo), xr = min((int32_t)(rr[r] >> 16), x_hi);
+        if (xl <= xr) pix |= row_bits(xl, xr, x_lo, r);
     }
     return pix;
 }

@@ -106,6 +106,85 @@ __device__ __forceinline__ bool bbox_hit(const ObjGeom& ob, f3 s, f3 d) {
     return true;
 }
 
+// Wave-wide min and max of six floats at once (lanes that must not count pass +inf / -inf):
+// the floats as order-preserving integer keys, DPP row shifts and row broadcasts (an invalid
+// source lane reads the identity), the six reductions interleaved; results in SGPRs.
+__device__ __forceinline__ int32_t float_key(float x) {
+    const int32_t b = __float_as_int(x);
+    return b ^ ((b >> 31) & 0x7fffffff);  // signed order of keys = numeric order of floats
+}
+__device__ __forceinline__ float key_float(int32_t k) { return __int_as_float(k ^ ((k >> 31) & 0x7fffffff)); }
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ void dpp_minmax_step(int32_t (&v)[6]) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const int32_t id = i < 3 ? 0x7fffffff : (int32_t)0x80000000;  // identity: fuses into v_min/max_dpp
+        const int32_t o = __builtin_amdgcn_update_dpp(id, v[i], kCtrl, kRowMask, 0xf, false);
+        v[i] = i < 3 ? min(v[i], o) : max(v[i], o);
+    }
+}
+// v[0..2]: values to minimise, v[3..5]: values to maximise
+__device__ __forceinline__ void wave_minmax6(const float (&in)[6], float (&out)[6]) {
+    int32_t v[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) v[i] = float_key(in[i]);
+    dpp_minmax_step<0x111, 0xf>(v);  // row_shr:1
+    dpp_minmax_step<0x112, 0xf>(v);  // row_shr:2
+    dpp_minmax_step<0x114, 0xf>(v);  // row_shr:4
+    dpp_minmax_step<0x118, 0xf>(v);  // row_shr:8: lane 15 of each row holds the row's
+    dpp_minmax_step<0x142, 0xa>(v);  // row_bcast:15
+    dpp_minmax_step<0x143, 0xc>(v);  // row_bcast:31: lane 63 holds the wave's
+#pragma unroll
+    for (int i = 0; i < 6; ++i) out[i] = key_float(__builtin_amdgcn_readlane(v[i], 63));
+}
+
+// The box of the wave's hit points P (lanes with a hit), for the shadow rays' face bounds.
+struct HitBox {
+    float lo[3], hi[3];
+    bool ok;  // some lane has a hit and every hit lane's P and N are finite
+};
+__device__ __forceinline__ HitBox hit_box(bool have, f3 P, f3 N) {
+    const float inf = __builtin_inff();
+    const bool finite = __builtin_isfinite(P.x) && __builtin_isfinite(P.y) && __builtin_isfinite(P.z) &&
+                        __builtin_isfinite(N.x) && __builtin_isfinite(N.y) && __builtin_isfinite(N.z);
+    const bool use = have && finite;
+    const float in[6] = {use ? P.x : inf, use ? P.y : inf, use ? P.z : inf,
+                         use ? P.x : -inf, use ? P.y : -inf, use ? P.z : -inf};
+    float out[6];
+    wave_minmax6(in, out);
+    HitBox b;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        b.lo[k] = out[k];
+        b.hi[k] = out[3 + k];
+    }
+    b.ok = __any(have) && !__any(have && !finite);
+    return b;
+}
+
+// Can a shadow ray Ray::new(P + N * 0.1, Lp - P) of a hit point P in box `b` pass this face's
+// det and t conditions (primitives.rs:47-66)?  det >= 1e-6 needs dot(P - Lp, n) > 0 and t >= 0
+// needs dot(S - a, n) >= 0 for the origin S, which lies within 0.1 (|N| = 1) of the box; both
+// are linear, so their maxima over the box decide.  The tolerance (1e-4 of the terms'
+// magnitudes) dwarfs the f32 rounding of every quantity involved, so a face some lane's exact
+// test accepts is never dropped; non-finite bounds keep the face.
+__device__ __forceinline__ bool shadow_box_may_hit(const TriHot& r, f3 Lp, const HitBox& b) {
+    const float n[3] = {r.q1.z, r.q1.w, r.q2.x}, a[3] = {r.q2.y, r.q2.z, r.q2.w};
+    const float lp[3] = {Lp.x, Lp.y, Lp.z};
+    const float g = 0.1001f;
+    float m1 = 0.0f, m2 = 0.0f, mag = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const bool pos = n[k] >= 0.0f;
+        m1 += n[k] * ((pos ? b.hi[k] : b.lo[k]) - lp[k]);
+        m2 += n[k] * ((pos ? b.hi[k] + g : b.lo[k] - g) - a[k]);
+        mag += __builtin_fabsf(n[k]) *
+               (__builtin_fabsf(b.lo[k]) + __builtin_fabsf(b.hi[k]) + __builtin_fabsf(lp[k]) + __builtin_fabsf(a[k]) + 1.0f);
+    }
+    const float tol = 1e-4f * mag + 1e-30f;
+    return ((m1 >= -tol) & (m2 >= -tol)) | !(mag < 1e30f);
+}
+
 // i % n for the texture sizes of Image::mod_get (image.rs:36-38); n is wave-uniform and a power
 // of two in practice, where the modulo is a mask
 __device__ __forceinline__ uint32_t mod_size(uint32_t i, uint32_t n) {

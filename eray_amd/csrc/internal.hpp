@@ -187,6 +187,7 @@ struct FrameParams {
     uint32_t detail_wgs;  // most workgroups of the frame kernel's grid doing detail work (0: all)
     uint32_t fill_first;  // the fill workgroups take the grid's first block indices (dispatched first)
     uint32_t separate_fill;  // the frame kernel does detail work only; fill_kernel writes the background
+    uint32_t fill_cap;       // at most this many workgroups write the background (0: no cap)
     // device-camera mode: camera, detail rectangles and detail count come from the setup
     // kernels' CamState (the host has not read them back); null: the fields above hold them
     const CamState* cam_state;
@@ -200,7 +201,7 @@ struct FrameParams {
     uint32_t aa, bounces;
     uint32_t seed_lo, seed_hi;
     // trace_kernel's culling records for this camera (scenes of at most kTraceSkipTris faces;
-    // null: no background skip), written by trace_cull_kernel before the frame
+    // null: no background skip), written by trace_cull_kernel when the camera or the scene changes
     TriCull* trace_cull;
     // trace_kernel's camera rays scan the binned objects' screen bins (a setup with
     // SetupParams::keep_all; the descriptors' bin views and rectangles), else every face
@@ -302,8 +303,8 @@ struct SetupParams {
     uint32_t* done;             // workgroup counter (last-workgroup finalisation), zero between setups
     uint32_t* part;             // kSetupMaxBlocks x 10: each workgroup's boundary objects' partials
     uint32_t binned;            // some object is binned: bins.hip narrows rects + builds the detail list
-    // binned objects' faces (bins.hip): bin rectangle and its number of bins per face (zero for
-    // other faces), the binned-object index per face
+    // binned objects' faces (bins.hip): bin rectangle and its number of units per face (bin_segments:
+    // rows of the rectangle, else its bins; zero for other faces), the binned-object index per face
     int4* range;
     unsigned long long* area;
     uint32_t* fkey;
@@ -312,6 +313,7 @@ struct SetupParams {
     // its jittered anti-aliasing rays reach, bin masks of the pixels any of whose rays may pass
     // (face_rect.hpp bin_pixels_jittered)
     uint32_t keep_all;
+    uint32_t rect_pairs;  // (diagnostics) the rectangle-pair form where segments apply (bin_segments)
     // Several cameras in one setup (ncam > 1: camera paths of scenes with binned objects): the
     // cameras sp.cam[0 .. ncam), T = ncam * T1 "faces" (face i is face i % T1 of camera i / T1:
     // its culling record, bin rectangle and pairs), nobj = ncam * nobj1 descriptors (camera k's
@@ -319,9 +321,9 @@ struct SetupParams {
     // object j is k * nb1 + j), ncam CamStates; the bins and their detail lists per camera.
     uint32_t ncam, T1, nobj1, nb1;
     const ObjectDesc* objs_src;  // batched setups: the scene's descriptors, copied into each slot
-    // binned faces' first (face, bin) pair: the exclusive scan of `area`, as each chunk
-    // workgroup's own scan (first_local) plus its chunk's offset boff[b] (kSetupMaxBlocks + 1
-    // entries; boff[nparts] = all pairs) — bins.hip bin_pairs_kernel reads them
+    // binned faces' first unit: the exclusive scan of `area`, as each chunk workgroup's own scan
+    // (first_local) plus its chunk's offset boff[b] (kSetupMaxBlocks + 1 entries; boff[nparts] =
+    // all units) — bins.hip bin_segments_kernel / bin_pairs_kernel read them
     unsigned long long* first_local;
     unsigned long long* boff;
     // Camera paths (eray_gather_frames' layout of path frames): every camera's final object
@@ -331,6 +333,13 @@ struct SetupParams {
     uint32_t union_nobj;
 };
 hipError_t launch_camera_setup(const SetupParams& sp, hipStream_t s);
+// The units the setup enumerates per binned face (`area`, and the scan first_local / boff over
+// them): its bin rectangle's rows (bins.hip bin_segments_kernel) for the frame kernel's bins, its
+// (face, bin) pairs for the general tracer's (bin_pairs_kernel) and for frames wider than the
+// segments' 16-bit columns.
+__host__ __device__ inline bool bin_segments(const SetupParams& sp) {
+    return !sp.keep_all && !sp.rect_pairs && sp.W <= 65535u;
+}
 // The setups of `ncam` cameras sp.cam[0 .. ncam) at once, one workgroup each, into per-camera
 // slots: culling records sp.cull + k * T, descriptors sp.objs + k * nobj (sp.objs_src with the
 // camera's rectangles), state sp.state + k.  Scenes without binned objects and at most
@@ -368,6 +377,7 @@ struct LaunchCtx {
 // The frame kernel, or the general tracer (trace.hip) when p.aa or p.bounces is set.
 hipError_t launch_render(const FrameParams& p, const LaunchCtx& lc, hipStream_t s);
 hipError_t launch_trace(const FrameParams& p, const LaunchCtx& lc, hipStream_t s);
+hipError_t launch_trace_cull(const FrameParams& p, hipStream_t s);
 
 // ------------------------------------------------------------- screen bins (bins.hip)
 // Device arrays of the binned objects' screen bins for one layout (camera size, row phase, the

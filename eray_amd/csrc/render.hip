@@ -265,85 +265,6 @@ __device__ __forceinline__ unsigned long long plane_mask(const TriHot& mine, uin
     return mask;
 }
 
-// Wave-wide min and max of six floats at once (lanes that must not count pass +inf / -inf):
-// the floats as order-preserving integer keys, DPP row shifts and row broadcasts (an invalid
-// source lane reads the identity), the six reductions interleaved; results in SGPRs.
-__device__ __forceinline__ int32_t float_key(float x) {
-    const int32_t b = __float_as_int(x);
-    return b ^ ((b >> 31) & 0x7fffffff);  // signed order of keys = numeric order of floats
-}
-__device__ __forceinline__ float key_float(int32_t k) { return __int_as_float(k ^ ((k >> 31) & 0x7fffffff)); }
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ void dpp_minmax_step(int32_t (&v)[6]) {
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        const int32_t id = i < 3 ? 0x7fffffff : (int32_t)0x80000000;  // identity: fuses into v_min/max_dpp
-        const int32_t o = __builtin_amdgcn_update_dpp(id, v[i], kCtrl, kRowMask, 0xf, false);
-        v[i] = i < 3 ? min(v[i], o) : max(v[i], o);
-    }
-}
-// v[0..2]: values to minimise, v[3..5]: values to maximise
-__device__ __forceinline__ void wave_minmax6(const float (&in)[6], float (&out)[6]) {
-    int32_t v[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) v[i] = float_key(in[i]);
-    dpp_minmax_step<0x111, 0xf>(v);  // row_shr:1
-    dpp_minmax_step<0x112, 0xf>(v);  // row_shr:2
-    dpp_minmax_step<0x114, 0xf>(v);  // row_shr:4
-    dpp_minmax_step<0x118, 0xf>(v);  // row_shr:8: lane 15 of each row holds the row's
-    dpp_minmax_step<0x142, 0xa>(v);  // row_bcast:15
-    dpp_minmax_step<0x143, 0xc>(v);  // row_bcast:31: lane 63 holds the wave's
-#pragma unroll
-    for (int i = 0; i < 6; ++i) out[i] = key_float(__builtin_amdgcn_readlane(v[i], 63));
-}
-
-// The box of the wave's hit points P (lanes with a hit), for the shadow rays' face bounds.
-struct HitBox {
-    float lo[3], hi[3];
-    bool ok;  // some lane has a hit and every hit lane's P and N are finite
-};
-__device__ __forceinline__ HitBox hit_box(bool have, f3 P, f3 N) {
-    const float inf = __builtin_inff();
-    const bool finite = __builtin_isfinite(P.x) && __builtin_isfinite(P.y) && __builtin_isfinite(P.z) &&
-                        __builtin_isfinite(N.x) && __builtin_isfinite(N.y) && __builtin_isfinite(N.z);
-    const bool use = have && finite;
-    const float in[6] = {use ? P.x : inf, use ? P.y : inf, use ? P.z : inf,
-                         use ? P.x : -inf, use ? P.y : -inf, use ? P.z : -inf};
-    float out[6];
-    wave_minmax6(in, out);
-    HitBox b;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        b.lo[k] = out[k];
-        b.hi[k] = out[3 + k];
-    }
-    b.ok = __any(have) && !__any(have && !finite);
-    return b;
-}
-
-// Can a shadow ray Ray::new(P + N * 0.1, Lp - P) of a hit point P in box `b` pass this face's
-// det and t conditions (primitives.rs:47-66)?  det >= 1e-6 needs dot(P - Lp, n) > 0 and t >= 0
-// needs dot(S - a, n) >= 0 for the origin S, which lies within 0.1 (|N| = 1) of the box; both
-// are linear, so their maxima over the box decide.  The tolerance (1e-4 of the terms'
-// magnitudes) dwarfs the f32 rounding of every quantity involved, so a face some lane's exact
-// test accepts is never dropped; non-finite bounds keep the face.
-__device__ __forceinline__ bool shadow_box_may_hit(const TriHot& r, f3 Lp, const HitBox& b) {
-    const float n[3] = {r.q1.z, r.q1.w, r.q2.x}, a[3] = {r.q2.y, r.q2.z, r.q2.w};
-    const float lp[3] = {Lp.x, Lp.y, Lp.z};
-    const float g = 0.1001f;
-    float m1 = 0.0f, m2 = 0.0f, mag = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const bool pos = n[k] >= 0.0f;
-        m1 += n[k] * ((pos ? b.hi[k] : b.lo[k]) - lp[k]);
-        m2 += n[k] * ((pos ? b.hi[k] + g : b.lo[k] - g) - a[k]);
-        mag += __builtin_fabsf(n[k]) *
-               (__builtin_fabsf(b.lo[k]) + __builtin_fabsf(b.hi[k]) + __builtin_fabsf(lp[k]) + __builtin_fabsf(a[k]) + 1.0f);
-    }
-    const float tol = 1e-4f * mag + 1e-30f;
-    return ((m1 >= -tol) & (m2 >= -tol)) | !(mag < 1e30f);
-}
-
 // --------------------------------------------------------------------- first hit -----------
 // Per-ray search state: kUndecided (ray and bounding-box test not evaluated yet), kSearching,
 // kDone (hit found, bbox rejected, or not a pixel of the image).
@@ -1264,8 +1185,9 @@ __device__ __forceinline__ void fill_blocks(const FrameParams& p, const FrameOut
     uint32_t occ = 0;  // detail list: lane i holds the occupancy of this wave's i-th next block
     uint32_t it = 0;
     const uint32_t nrect = detail_occ ? 0u : frame_nrect<kDev>(p, cs);
-    // block coordinates advance incrementally (no integer division per block)
-    const uint32_t first = wave * nf + f, step_y = fstride / p.tiles_x, step_x = fstride - step_y * p.tiles_x;
+    // block coordinates advance incrementally (no integer division per block); the workgroup's
+    // four waves take four neighbouring blocks, the workgroups consecutive runs of four
+    const uint32_t first = f * nwaves + wave, step_y = fstride / p.tiles_x, step_x = fstride - step_y * p.tiles_x;
     uint32_t by = first / p.tiles_x, bx = first - by * p.tiles_x;
     for (uint32_t blk = first; blk < nblk; blk += fstride, ++it) {
         if (it) {
@@ -1527,18 +1449,59 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
 
     // ---- background of the non-detail sub-blocks ---------------------------------------------
     if (separate_fill) return;  // fill_kernel writes the background beside this launch
-    const uint32_t nf = nd < grid ? grid - nd : grid;  // filling workgroups
+    const uint32_t nf = min(nd < grid ? grid - nd : grid, p.fill_cap ? p.fill_cap : grid);  // filling workgroups
     const uint32_t f = nd < grid ? bid - nd : bid;
+    if (f >= nf) return;
     ERAY_TRACE_POINT(2);
     fill_frames<kDev>(p, f, nf, wave, lane, aligned);
     ERAY_TRACE_POINT(3);
 }
 
+// One output array of the background in flat order: thread t writes 16-B chunks t, t + nt, ... of
+// the array (nt = the grid's threads), skipping those of detail sub-blocks (occupancy bits) and
+// those past the camera's width.  A 16-pixel sub-block row is kPer chunks (RGB 12, PPM 3, faces
+// 4), so each chunk belongs to one sub-block, and a sub-block starts at a chunk index divisible by
+// 3: the background word is the chunk's phase mod 3.  kFlip: the PPM's bottom-up file rows.
+template <uint32_t kPer, bool kFlip, typename T, typename Word>
+__device__ __forceinline__ void fill_flat_array(const FrameParams& p, T* base, const uint8_t* occ, uint32_t t, uint32_t nt,
+                                                Word&& word) {
+    const uint32_t per_row = p.img_w / 16 * kPer;
+    const uint32_t n = per_row * p.rows;  // (< 2^28: FrameParams::aligned keeps the f32 RGB under 4 GB)
+    uint32_t row = t / per_row, col = t - row * per_row;  // chunk c = row * per_row + col, advanced by nt
+    const uint32_t drow = nt / per_row, dcol = nt - drow * per_row;
+    for (uint32_t c = t; c < n; c += nt) {
+        const uint32_t s = col / kPer;  // the chunk's sub-block column
+        const uint32_t py = kFlip ? p.rows - 1 - row : row;
+        bool write = s * kSubW < p.cam_w;
+        if (write) write = !((occ[(py / kBlkH) * p.tiles_x + s / 4] >> (s & 3u)) & 1u);
+        if (write) stream16(base, reinterpret_cast<const char*>(base) + 16 * (size_t)c, word(col % 3));
+        col += dcol;
+        row += drow;
+        if (col >= per_row) {
+            col -= per_row;
+            ++row;
+        }
+    }
+}
+
 // The background alone, beside a detail-only frame kernel on another stream (FrameParams::
 // separate_fill): small workgroups that hold few registers, so the fill waves do not take the
-// register budget of the large-mesh detail build.
+// register budget of the large-mesh detail build.  A frame of its own (args mode, one frame per
+// launch, 16-px-aligned rows): every output array in flat order (fill_flat_array) — one workgroup
+// per CU then writes one contiguous ~1 MB window of the array at a time: 7680x4320 (498 MB,
+// beyond the 256 MB MALL) at 6.9 TB/s against 5.2 in 64 x 4 blocks (scripts/microbench/
+// fill_pat.hip, profiles/r04/fill_pat.txt).  Otherwise 64 x 4 blocks (fill_frames).
 template <bool kDev>
 __global__ void __launch_bounds__(kWG) fill_kernel(FrameParams p) {
+    if (!kDev && p.nframes == 1 && p.aligned && p.detail_occ && p.cam_w % kSubW == 0) {
+        const FrameOut o = frame_out(p, 0);
+        const uint32_t t = blockIdx.x * kWG + threadIdx.x, nt = gridDim.x * kWG;
+        if (o.rgb) fill_flat_array<12, false>(p, o.rgb, p.detail_occ, t, nt, [](uint32_t ph) { return bg_rgb4(ph); });
+        if (o.ppm) fill_flat_array<3, true>(p, o.ppm, p.detail_occ, t, nt, [](uint32_t ph) { return bg_ppm16(ph); });
+        if (o.face)
+            fill_flat_array<4, false>(p, o.face, p.detail_occ, t, nt, [](uint32_t) { return make_uint4(~0u, ~0u, ~0u, ~0u); });
+        return;
+    }
     fill_frames<kDev>(p, blockIdx.x, gridDim.x, threadIdx.x >> 6, threadIdx.x & 63, p.aligned != 0);
 }
 
@@ -1588,6 +1551,8 @@ uint32_t device_cus() {
     }();
     return cus;
 }
+
+constexpr uint32_t kFillWgsPerCu = 1;
 
 // A kernel launch, with its dispatch's own start / stop timestamps recorded into t[0] / t[1] when
 // they are given (LaunchCtx: measurement only).
@@ -1652,6 +1617,13 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
     // 22.4 us (profiles/r03/ab/)
     if (L) q.fill_first = 1;
     q.separate_fill = 0;
+    // Fill workgroups: one per CU writes the background where the fill has the GPU (nearly) to
+    // itself — fewer concurrent write streams keep the HBM pages open (scripts/microbench/
+    // fill_pat.hip: 3840x2160 beyond the cache 23-24 us with 2-4 per CU, 18.6 us with one; the
+    // empty-scene floor 24.5 -> 21.3 us, C2's 37.2 -> 34.0 us per 8 frames) — but not beside
+    // the binned meshes' detail waves, which take issue slots from fewer fill waves (3840x2160 /
+    // 70k: 22.6 -> 28.2 us with one per CU), same-box A/B (profiles/r04/ab/ab_fill_cap.txt).
+    q.fill_cap = L ? 0u : kFillWgsPerCu * cus;
     if constexpr (D) {
         // Separate fill: the dense build does detail work only, at most 2 workgroups per CU, and
         // fill_kernel's small workgroups (58 VGPRs) write the background beside it from a second
@@ -1670,7 +1642,9 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
             q.detail_wgs = 0;
             q.fill_first = 0;
             const uint32_t dgrid = max(1u, min(min(grid, 2u * cus), (total_sub + kWG / 64 - 1) / (kWG / 64)));
-            const uint32_t fgrid = max(1u, min(2u * cus, (nblk + 3) / 4));
+            // (one per CU for a frame of its own, C5: 152 -> 133 us; two beside a moving camera's
+            // setup chain on the other stream, which one per CU slows: 408 -> 434 us)
+            const uint32_t fgrid = max(1u, min((V ? 2u : kFillWgsPerCu) * cus, (nblk + 3) / 4));
             hipError_t e;
             if ((e = hipEventRecord(lc.fork, s)) != hipSuccess || (e = hipStreamWaitEvent(lc.side, lc.fork, 0)) != hipSuccess)
                 return e;

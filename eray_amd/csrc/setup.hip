@@ -151,14 +151,15 @@ __global__ void __launch_bounds__(kSetupWG) camera_setup_kernel(SetupParams sp, 
                     g = make_int4(r[0] / (int32_t)kBinW, r[1] / (int32_t)kBinW,
                                   (r[2] + (int32_t)kBinH - (int32_t)sp.phase) / (int32_t)kBinH,
                                   (r[3] + (int32_t)kBinH - (int32_t)sp.phase) / (int32_t)kBinH);
-                    ar = (unsigned long long)(g.y - g.x + 1) * (unsigned long long)(g.w - g.z + 1);
+                    ar = (unsigned long long)(g.w - g.z + 1) *  // (units: rows, or bins)
+                         (bin_segments(sp) ? 1ull : (unsigned long long)(g.y - g.x + 1));
                 }
                 sp.range[i] = g;
                 sp.area[i] = ar;
                 sp.fkey[i] = k;
             }
         }
-        if (sp.range) {  // the chunk's exclusive scan of the areas, in face order
+        if (sp.range) {  // the chunk's exclusive scan of the units, in face order
             unsigned long long all = 0;
             const unsigned long long ex = block_exclusive_scan(ar, s_scan, &all);
             if (i < hi) sp.first_local[i] = run + ex;

@@ -17,13 +17,16 @@ extern "C" {
 /* The screen bins of object `index` as built by the last setup: out[0] bins, out[1] entries,
  * out[2] (face, pixel) pairs, out[3] most entries in one bin, out[4] non-empty bins, out[5] most
  * pairs in one bin, out[6..9] the object's pixel rectangle, out[10] the fullest bin, out[11] /
- * out[12] bins of more than 64 / 192 entries, out[13] the pairs of the faces' bin rectangles before
- * masking (14 words). */
+ * out[12] bins of more than 64 / 192 entries, out[13] the units the pair pass walked (the faces'
+ * bin-rectangle rows, or their (face, bin) pairs) (14 words). */
 int eray_debug_bin_stats(eray_ctx* ctx, uint32_t index, uint64_t* out);
 /* The entries of bin `bin` of object `index` (faces relative to the object, pixel masks), at most
  * `cap`; *n = the bin's entry count. */
 int eray_debug_bin_dump(eray_ctx* ctx, uint32_t index, uint32_t bin, uint32_t* tri, uint64_t* mask, uint32_t cap,
                         uint32_t* n);
+/* The frame setups' pair pass over every (face, bin) pair of the faces' bin rectangles
+ * (rect_pairs != 0) instead of the rectangles' rows; the next setup rebuilds the bins. */
+int eray_debug_set_bin_form(eray_ctx* ctx, int rect_pairs);
 /* Sets the bins' entry capacity (reallocated at the next setup; overflow and growth tests). */
 int eray_debug_set_bin_capacity(eray_ctx* ctx, uint64_t entries);
 uint64_t eray_debug_bin_capacity(const eray_ctx* ctx);

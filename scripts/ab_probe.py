@@ -80,6 +80,7 @@ def main() -> None:
                                                     for _ in range(3))}
         else:
             ctx.render_frames(max(slots, 4), W, H, **kw)
+            ctx.time_frames(2 * F, W, H, **kw)  # (warm: a first launch after the setup can take ms)
             n = max(args.launches // (4 if name == "c5" else 1), 2) * F
             out[name] = ctx.time_frames(n, W, H, **kw)
         torch.cuda.synchronize()

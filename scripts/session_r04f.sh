@@ -14,4 +14,4 @@ if [ $rc -ne 0 ]; then
 fi
 timeout -k 10 180 scripts/microbench/fill_8k > $OUT/fill_8k.txt 2>&1 || { cat $OUT/fill_8k.txt; exit 1; }
 cat $OUT/fill_8k.txt
-TAG=${TAG:-r04f}/ab LIBS="${LIBS:-fi product pf fo xcd}" ROUNDS=${ROUNDS:-2} CONFIGS=${CONFIGS:-aa2,aa_ns,fill4k1,fill8k,fillc2,c2,ns1,ns4,c5,moving_ns,moving_c5} bash scripts/ab_session.sh
+TAG=${TAG:-r04f}/ab LIBS="${LIBS:-fi product lb3 fo xcd}" ROUNDS=${ROUNDS:-2} CONFIGS=${CONFIGS:-aa2,aa_ns,fill4k1,fill8k,fillc2,c2,ns1,ns4,c5,moving_ns,moving_c5} bash scripts/ab_session.sh

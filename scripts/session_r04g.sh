@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 4: the GPU suite on the product build (segment-form bins, fill order, tracer changes),
+# the fill-pattern microbenchmark, then a same-box A/B against HEAD (pf), the product without the
+# fill order (nofo) and the tracer steps (t0: culling records per camera, t1: + 16-B skip fill).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${TAG:-r04g}
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests > $OUT/tests.log 2>&1
+rc=$?; tail -3 $OUT/tests.log
+if [ $rc -ne 0 ]; then
+  grep -B5 -A40 "FAIL\|Error" $OUT/tests.log | head -120
+  [ $rc -eq 1 ] || exit $rc  # a crash or a time limit: nothing more on the GPU
+fi
+timeout -k 10 240 scripts/microbench/fill_pat > $OUT/fill_pat.txt 2>&1 || { cat $OUT/fill_pat.txt; exit 1; }
+cat $OUT/fill_pat.txt
+TAG=${TAG:-r04g}/ab LIBS="${LIBS:-product pf nofo t0 t1}" ROUNDS=${ROUNDS:-2} CONFIGS=${CONFIGS:-aa2,aa_ns,fill4k1,fill4k4,fill8k,fillc2,c2,ns1,ns4,c5,moving_ns,moving_c5} bash scripts/ab_session.sh

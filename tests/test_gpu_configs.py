@@ -9,6 +9,7 @@ centre and the middle tile boundary) and, for the binned large-mesh path, agains
 brute-force scan (the reference's per-pixel loop, engine.rs:52-78, first hit by index,
 object.rs:63-78) on row blocks at every tile boundary and through the mesh centre.
 """
+import ctypes
 import hashlib
 import json
 import os
@@ -345,3 +346,60 @@ def test_culling_margins_on_pixel_corner_rays(gpu, faces):
     finally:
         blk.free()
         sc.close()
+
+
+def _all_bins(gpu):
+    """Every bin of object 0 as built by the last setup: {bin: sorted [(face, mask)]}."""
+    L = capi.lib()
+    st = (ctypes.c_uint64 * 14)()
+    assert L.eray_debug_bin_stats(gpu.handle, 0, st) == 0
+    cap = 4096
+    tri, mask, n = (ctypes.c_uint32 * cap)(), (ctypes.c_uint64 * cap)(), ctypes.c_uint32()
+    out = {}
+    for b in range(int(st[0])):
+        assert L.eray_debug_bin_dump(gpu.handle, 0, b, tri, mask, cap, ctypes.byref(n)) == 0
+        assert n.value <= cap
+        if n.value:
+            out[b] = sorted(zip(tri[: n.value], mask[: n.value]))
+    return out, int(st[13])
+
+
+def test_bin_segments_equal_rectangle_pairs(gpu):
+    """The frame setups' pair pass over the faces' bin-rectangle rows (bins.hip
+    bin_segments_kernel: per-row pixel ranges from bin_pixels' own double-precision lines) against
+    the rectangle-pair form: every bin holds the same (face, pixel mask) entries — the segment form
+    may add a few the pair form's f32 pre-test drops, never with another mask — at bin phase 0 and
+    at phase 1 (a row tile from row 1), and the frames are bit-identical."""
+    mesh = _mesh(**meshgen.STANDIN_70K)
+    W, H = 1920, 1080
+    sc = MainScene(gpu, *mesh, W, H, texture=1024, fov=(16.0, 9.0))
+    fr = Frame(gpu, W, H)
+    L = capi.lib()
+    try:
+        for row0 in (0, 1):
+            got = []
+            for rect in (1, 0):
+                assert L.eray_debug_set_bin_form(gpu.handle, rect) == 0
+                img = [x.copy() for x in fr.render(W, H, row0=row0)]
+                bins, units = _all_bins(gpu)
+                got.append((img, bins, units))
+            (ia, ba, ua), (ib, bb, ub) = got
+            assert np.array_equal(ia[1], ib[1]) and np.array_equal(ia[2], ib[2])
+            assert_bit_equal(ia[0], ib[0], f"segments vs rectangle pairs, row0 {row0}")
+            assert ub <= ua, (ub, ua)  # (rows of the rectangles, at most their bins)
+            n_pairs = sum(len(v) for v in ba.values())
+            assert n_pairs > 10_000
+            extra = 0
+            for b, seg in bb.items():
+                pairs = dict(ba.get(b, []))
+                seg_d = dict(seg)
+                assert len(seg_d) == len(seg), f"bin {b}: a face twice"
+                for f, m in pairs.items():
+                    assert seg_d.get(f) == m, f"bin {b} face {f}: mask {seg_d.get(f)} vs {m} (row0 {row0})"
+                extra += len(seg_d) - len(pairs)
+            assert set(ba) <= set(bb)
+            assert extra <= n_pairs // 20, (extra, n_pairs)
+    finally:
+        assert L.eray_debug_set_bin_form(gpu.handle, 0) == 0
+        sc.close()
+        fr.free()
