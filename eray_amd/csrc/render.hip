@@ -1457,51 +1457,14 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     ERAY_TRACE_POINT(3);
 }
 
-// One output array of the background in flat order: thread t writes 16-B chunks t, t + nt, ... of
-// the array (nt = the grid's threads), skipping those of detail sub-blocks (occupancy bits) and
-// those past the camera's width.  A 16-pixel sub-block row is kPer chunks (RGB 12, PPM 3, faces
-// 4), so each chunk belongs to one sub-block, and a sub-block starts at a chunk index divisible by
-// 3: the background word is the chunk's phase mod 3.  kFlip: the PPM's bottom-up file rows.
-template <uint32_t kPer, bool kFlip, typename T, typename Word>
-__device__ __forceinline__ void fill_flat_array(const FrameParams& p, T* base, const uint8_t* occ, uint32_t t, uint32_t nt,
-                                                Word&& word) {
-    const uint32_t per_row = p.img_w / 16 * kPer;
-    const uint32_t n = per_row * p.rows;  // (< 2^28: FrameParams::aligned keeps the f32 RGB under 4 GB)
-    uint32_t row = t / per_row, col = t - row * per_row;  // chunk c = row * per_row + col, advanced by nt
-    const uint32_t drow = nt / per_row, dcol = nt - drow * per_row;
-    for (uint32_t c = t; c < n; c += nt) {
-        const uint32_t s = col / kPer;  // the chunk's sub-block column
-        const uint32_t py = kFlip ? p.rows - 1 - row : row;
-        bool write = s * kSubW < p.cam_w;
-        if (write) write = !((occ[(py / kBlkH) * p.tiles_x + s / 4] >> (s & 3u)) & 1u);
-        if (write) stream16(base, reinterpret_cast<const char*>(base) + 16 * (size_t)c, word(col % 3));
-        col += dcol;
-        row += drow;
-        if (col >= per_row) {
-            col -= per_row;
-            ++row;
-        }
-    }
-}
-
 // The background alone, beside a detail-only frame kernel on another stream (FrameParams::
 // separate_fill): small workgroups that hold few registers, so the fill waves do not take the
-// register budget of the large-mesh detail build.  A frame of its own (args mode, one frame per
-// launch, 16-px-aligned rows): every output array in flat order (fill_flat_array) — one workgroup
-// per CU then writes one contiguous ~1 MB window of the array at a time: 7680x4320 (498 MB,
-// beyond the 256 MB MALL) at 6.9 TB/s against 5.2 in 64 x 4 blocks (scripts/microbench/
-// fill_pat.hip, profiles/r04/fill_pat.txt).  Otherwise 64 x 4 blocks (fill_frames).
+// register budget of the large-mesh detail build.  (A flat order — every output array as one
+// byte range, one workgroup per CU, 6.9 TB/s alone at 7680x4320 in scripts/microbench/
+// fill_pat.hip — wrote C5's background in 263 us beside the detail kernel against 151 us in
+// blocks from two workgroups per CU: profiles/r04/ab/ab_flat_fill.txt, launch spans.)
 template <bool kDev>
 __global__ void __launch_bounds__(kWG) fill_kernel(FrameParams p) {
-    if (!kDev && p.nframes == 1 && p.aligned && p.detail_occ && p.cam_w % kSubW == 0) {
-        const FrameOut o = frame_out(p, 0);
-        const uint32_t t = blockIdx.x * kWG + threadIdx.x, nt = gridDim.x * kWG;
-        if (o.rgb) fill_flat_array<12, false>(p, o.rgb, p.detail_occ, t, nt, [](uint32_t ph) { return bg_rgb4(ph); });
-        if (o.ppm) fill_flat_array<3, true>(p, o.ppm, p.detail_occ, t, nt, [](uint32_t ph) { return bg_ppm16(ph); });
-        if (o.face)
-            fill_flat_array<4, false>(p, o.face, p.detail_occ, t, nt, [](uint32_t) { return make_uint4(~0u, ~0u, ~0u, ~0u); });
-        return;
-    }
     fill_frames<kDev>(p, blockIdx.x, gridDim.x, threadIdx.x >> 6, threadIdx.x & 63, p.aligned != 0);
 }
 
@@ -1642,9 +1605,9 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
             q.detail_wgs = 0;
             q.fill_first = 0;
             const uint32_t dgrid = max(1u, min(min(grid, 2u * cus), (total_sub + kWG / 64 - 1) / (kWG / 64)));
-            // (one per CU for a frame of its own, C5: 152 -> 133 us; two beside a moving camera's
-            // setup chain on the other stream, which one per CU slows: 408 -> 434 us)
-            const uint32_t fgrid = max(1u, min((V ? 2u : kFillWgsPerCu) * cus, (nblk + 3) / 4));
+            // (two per CU: beside the detail waves one per CU writes C5's background in 186 us
+            // instead of 151, profiles/r04/ab/ab_fill_cap.txt launch spans)
+            const uint32_t fgrid = max(1u, min(2u * cus, (nblk + 3) / 4));
             hipError_t e;
             if ((e = hipEventRecord(lc.fork, s)) != hipSuccess || (e = hipStreamWaitEvent(lc.side, lc.fork, 0)) != hipSuccess)
                 return e;

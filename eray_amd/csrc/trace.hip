@@ -706,9 +706,9 @@ __device__ void fill_color(const FrameParams& p, uint32_t x0, uint32_t py0, uint
 // 64 x 4 block.  The grid's first trace_heavy_wgs workgroups take the heavy sub-blocks
 // (heavy_role), the next trace_fill_wgs write the background of the unlisted sub-blocks, the
 // others take the light listed sub-blocks, one per wave (camera_hits<1>).
-// Three workgroups per CU (168 VGPRs, a few spilled; LDS 45 KB each) and two light workgroups
-// per CU: 3840x2160 / 70k with AA = 4 178 -> 130 us per frame against two per CU (178 VGPRs),
-// same-box A/B.
+// Three workgroups per CU (168 VGPRs, a few spilled; LDS 45 KB each): 3840x2160 / 70k with
+// AA = 4 178 -> 130 us per frame against two per CU (178 VGPRs), same-box A/B
+// (profiles/r04/ab/ab_r04f.txt).
 template <bool kBounce>
 __global__ void __launch_bounds__(256, 3) trace_binned_kernel(FrameParams p) {
     constexpr size_t kLds = 4 * sizeof(BinGroup<1>) > sizeof(BinGroup<4>) ? 4 * sizeof(BinGroup<1>) : sizeof(BinGroup<4>);
@@ -780,7 +780,10 @@ hipError_t launch_trace(const FrameParams& p0, const LaunchCtx&, hipStream_t s) 
         }();
         p.trace_heavy_wgs = cus / 4;  // (heavy sub-blocks are few: poles, dense folds; dispatched first)
         p.trace_fill_wgs = cus;       // one per CU: the background is a write stream
-        p.trace_light_wgs = 2 * cus;  // with the fill, about one round at 3 per CU
+        // light sub-blocks: one per wave where the list allows (the workgroups past its end return
+        // at once, and the dispatcher hands the freed slots to the next ones: 3840x2160 / 70k with
+        // AA = 4 129 -> 111 us against two per CU, profiles/r04/ab/ab_r04k.txt)
+        p.trace_light_wgs = 8 * cus;
         const dim3 grid(p.trace_heavy_wgs + p.trace_fill_wgs + p.trace_light_wgs);
         if (p.bounces) hipLaunchKernelGGL(trace_binned_kernel<true>, grid, dim3(256), 0, s, p);
         else hipLaunchKernelGGL(trace_binned_kernel<false>, grid, dim3(256), 0, s, p);

@@ -33,7 +33,11 @@ CONFIGS = {"fill4k1": ("none", 3840, 2160, 1, 1), "fill4k4": ("none", 3840, 2160
            "c2": ("cube", 1920, 1080, 8, 8), "c3": ("70k", 1920, 1080, 4, 4), "ns1": ("70k", 3840, 2160, 1, 1),
            "ns4": ("70k", 3840, 2160, 4, 1), "c5": ("1m", 7680, 4320, 1, 1), "moving_ns": ("70k", 3840, 2160, 1, 1),
            "moving_c5": ("1m", 7680, 4320, 1, 1),
-           "aa2": ("cube", 1920, 1080, 1, 1), "aa_ns": ("70k", 3840, 2160, 1, 1)}
+           "aa2": ("cube", 1920, 1080, 1, 1), "aa_ns": ("70k", 3840, 2160, 1, 1),
+           "ns1sep": ("70k", 3840, 2160, 1, 1), "ns4sep": ("70k", 3840, 2160, 4, 1)}
+# launch-shape overrides (eray_render_params::flags) of the *sep configs: the dense build beside a
+# separate fill kernel
+SEPARATE = ("ns1sep", "ns4sep")
 
 
 def mesh_of(kind):
@@ -68,6 +72,8 @@ def main() -> None:
             rgb = torch.empty((slots, H, W, 3), dtype=torch.float32, device="cuda")
             ppm = torch.empty((slots, H, W, 3), dtype=torch.uint8, device="cuda")
         kw = dict(out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr(), ring=capi.frame_ring(slots, H, W, F))
+        if name in SEPARATE:
+            kw["flags"] = capi.RENDER_DENSE_DETAIL | capi.RENDER_SEPARATE_FILL
         if name.startswith("aa"):  # the general tracer, anti_aliasing = 4 (bench.py anti_aliasing_line)
             akw = dict(kw, anti_aliasing=4, aa_seed=12345)
             del akw["ring"]

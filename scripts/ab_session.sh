@@ -20,7 +20,7 @@ agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for r in rows:
     for k, v in r.items():
         if k != "lib":
-            agg[k][r["lib"]].append(v.get("frame_kernel_ms", v.get("device_ms_per_frame", v.get("frame_ms"))) * 1e3)
+            agg[k][r["lib"]].append(v.get("launch_span_ms", v.get("device_ms_per_frame", v.get("frame_ms"))) * 1e3)
 for k, d in agg.items():
     print(k, {l: [round(x, 2) for x in v] for l, v in d.items()})
 PY
