@@ -14,14 +14,13 @@
 // The general tracer's setup (SetupParams::keep_all) masks the pixels any of whose jittered
 // anti-aliasing rays may pass instead (bin_pixels_jittered; trace.hip).
 //
-// Per camera, after camera_setup_kernel (each binned face's bin rectangle and its number of bins):
-//   exclusive scan of the rectangles' areas -> one thread per (face, bin) pair (a wave-uniform
-//   grid-stride loop over the total read on the device; the face found by binary search — a
-//   near-silhouette face's rectangle can span thousands of bins) computes the pair's pixel mask
-//   and appends the non-empty pairs (wave-aggregated slot counter) with a per-bin count ->
-//   exclusive scan of the counts -> each entry scattered to its bin (the per-bin count counted
-//   back down to zero for the next camera) -> the binned objects' rectangles narrowed to their
-//   non-empty bins, their bin views in the descriptors -> the detail sub-block list.
+// Per camera, after camera_setup_kernel (each binned face's bin rectangle and its number of units,
+// bin rows or bins): exclusive scan of the units -> the pair pass (bin_segments_kernel /
+// bin_pairs_kernel below) computes the (face, bin) pairs' pixel masks and appends the non-empty
+// pairs (wave-aggregated slot counter) with a per-bin count -> exclusive scan of the counts ->
+// each entry scattered to its bin (one 64-B BinEntry line: record, mask, face) -> the counts
+// zeroed for the next camera, the binned objects' rectangles narrowed to their non-empty bins,
+// their bin views in the descriptors -> the detail sub-block list.
 // Buffers are preallocated (bins_alloc); if the pairs exceed the capacity the bins are dropped
 // for that camera (the frame kernel scans those objects through LDS tiles instead, still exact)
 // and CamState reports the count, so the host can grow the capacity.
@@ -454,30 +453,30 @@ __global__ void __launch_bounds__(kBinWG, kPairsWaves) bin_segments_kernel(const
     });
 }
 
-// every stored entry to its bin: start[key] + its rank; the counts back to zero for the next camera
+// every stored entry to its bin: start[key] + its rank, as one 64-B line (BinEntry: the face's
+// intersection record, its pixel mask and its index in the object); the finaliser zeroes the
+// counts for the next camera (coalesced over the keys, not a scattered word per entry)
 __global__ void __launch_bounds__(kBinWG) bin_scatter_kernel(const uint32_t* __restrict__ n, uint32_t cap,
                                                              const uint32_t* __restrict__ ekey,
                                                              const uint32_t* __restrict__ eface,
                                                              const unsigned long long* __restrict__ emask,
                                                              const uint32_t* __restrict__ erank,
                                                              const uint32_t* __restrict__ start,
-                                                             uint32_t* __restrict__ count,
                                                              const uint32_t* __restrict__ kbegin, uint32_t nbins,
                                                              const TriHot* __restrict__ hot, uint32_t T1,
-                                                             uint32_t* __restrict__ tri,
-                                                             unsigned long long* __restrict__ mask,
-                                                             TriHot* __restrict__ hot_out) {
+                                                             BinEntry* __restrict__ ent) {
     const uint32_t region = cap / kShards;
     for (uint32_t sh = 0; sh < kShards; ++sh) {  // each shard's entries [sh * region, + its count)
         const uint32_t total = min(n[sh * kShardStride], region);
         for (uint32_t el = blockIdx.x * kBinWG + threadIdx.x; el < total; el += gridDim.x * kBinWG) {
             const uint32_t e = sh * region + el;
             const uint32_t key = ekey[e], f = eface[e];
-            const uint32_t pos = start[key] + erank[e];
-            count[key] = 0u;  // (every entry of the bin stores the same zero)
-            tri[pos] = f - kbegin[key / nbins];
-            mask[pos] = emask[e];
-            hot_out[pos] = hot[T1 ? f % T1 : f];  // (several cameras: face f is face f % T1 of camera f / T1)
+            BinEntry x;
+            x.hot = hot[T1 ? f % T1 : f];  // (several cameras: face f is face f % T1 of camera f / T1)
+            x.mask = emask[e];
+            x.tri = f - kbegin[key / nbins];
+            x.pad = 0u;
+            ent[start[key] + erank[e]] = x;
         }
     }
 }
@@ -527,15 +526,11 @@ __device__ __forceinline__ void queue_sort(const uint32_t* __restrict__ start, u
 __global__ void __launch_bounds__(kBinWG) bin_sort_kernel(const uint32_t* __restrict__ sortq,
                                                           const uint32_t* __restrict__ nsort,
                                                           const uint32_t* __restrict__ start,
-                                                          uint32_t* __restrict__ tri,
-                                                          unsigned long long* __restrict__ mask,
-                                                          TriHot* __restrict__ hot) {
-    __shared__ uint32_t s_tri[kBinWG / 64][kSortMax];
-    __shared__ unsigned long long s_mask[kBinWG / 64][kSortMax];
-    __shared__ TriHot s_hot[kBinWG / 64][kSortMax];
+                                                          BinEntry* __restrict__ ent) {
+    __shared__ BinEntry s_ent[kBinWG / 64][kSortMax];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t items = *nsort;
-    uint32_t* st = s_tri[wave];
+    BinEntry* se = s_ent[wave];
     for (uint32_t it = blockIdx.x * (kBinWG / 64) + wave; it < items; it += gridDim.x * (kBinWG / 64)) {
         const uint32_t key = sortq[it];  // wave-uniform
         const uint32_t s0 = start[key], n = start[key + 1] - s0;
@@ -546,28 +541,22 @@ __global__ void __launch_bounds__(kBinWG) bin_sort_kernel(const uint32_t* __rest
             v[q] = 0xffffffffu;
             r[q] = 0;
             if (e < n) {
-                v[q] = tri[s0 + e];
-                st[e] = v[q];
-                s_mask[wave][e] = mask[s0 + e];
-                s_hot[wave][e] = hot[s0 + e];
+                se[e] = ent[s0 + e];
+                v[q] = se[e].tri;
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         for (uint32_t j = 0; j < n; ++j) {
-            const uint32_t f = st[j];
+            const uint32_t f = se[j].tri;
 #pragma unroll
             for (uint32_t q = 0; q < kSortPer; ++q) r[q] += f < v[q] ? 1u : 0u;
         }
 #pragma unroll
         for (uint32_t q = 0; q < kSortPer; ++q) {
             const uint32_t e = lane + 64 * q;
-            if (e < n) {
-                tri[s0 + r[q]] = v[q];
-                mask[s0 + r[q]] = s_mask[wave][e];
-                hot[s0 + r[q]] = s_hot[wave][e];
-            }
+            if (e < n) ent[s0 + r[q]] = se[e];
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();  // the LDS is rewritten by the next bin
@@ -586,8 +575,8 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t per, con
                                                                uint32_t* __restrict__ part,
                                                                uint32_t* __restrict__ done, uint32_t* __restrict__ n,
                                                                uint32_t cap, const uint32_t* __restrict__ kobj,
-                                                               ObjectDesc* __restrict__ objs, uint32_t* tri,
-                                                               unsigned long long* mask, TriHot* hot,
+                                                               ObjectDesc* __restrict__ objs, const BinEntry* ent,
+                                                               uint32_t* __restrict__ count,
                                                                uint32_t* __restrict__ sortq, uint32_t* __restrict__ nsort,
                                                                CamState* __restrict__ st, uint32_t ncam,
                                                                int32_t* __restrict__ path_union, uint32_t union_nobj) {
@@ -606,6 +595,7 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t per, con
             else max4(acc + kAccStride * kc, a);
         };
         for (uint32_t b = b0 + threadIdx.x; b < b0 + per; b += kBinWG) {  // workgroup-uniform trip count
+            if (b < b1) count[b] = 0u;  // (the scatter has read the ranks: zero for the next camera)
             if (b < b1 && start[b + 1] > start[b]) {
                 const uint32_t k = b / nbins;
                 const uint32_t lb = b - k * nbins;
@@ -661,9 +651,7 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t per, con
         ObjGeom& g = objs[kobj[j]].g;
         if (overflow) {  // keep the face rectangles; the frame kernel scans through LDS tiles
             g.bin_start = nullptr;
-            g.bin_tri = nullptr;
-            g.bin_mask = nullptr;
-            g.bin_hot = nullptr;
+            g.bin_ent = nullptr;
             if (path_union) union_rect(path_union, union_nobj, kobj[j] % union_nobj, g.rect);
             continue;
         }
@@ -681,9 +669,7 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t per, con
         }
         if (path_union) union_rect(path_union, union_nobj, kobj[j] % union_nobj, r);
         g.bin_start = start + (size_t)j * nbins;
-        g.bin_tri = tri;
-        g.bin_mask = mask;
-        g.bin_hot = hot;
+        g.bin_ent = ent;
     }
     __syncthreads();  // (every thread has read the counts)
     if (threadIdx.x < kShards) n[threadIdx.x * kShardStride] = 0u;
@@ -845,7 +831,7 @@ hipError_t grow(T** p, size_t need) {
 
 void bins_free(BinBuffers& b) {
     void* ptrs[] = {b.first, b.boff, b.count,  b.start,  b.kbegin, b.kobj,   b.n,       b.done,    b.acc,   b.part, b.ekey,
-                    b.eface, b.emask,  b.erank,  b.tri,    b.mask,   b.hot,    b.dflags,  b.dpacked, b.dlist, b.docc,
+                    b.eface, b.emask,  b.erank,  b.ent,    b.dflags,  b.dpacked, b.dlist, b.docc,
                     b.sortq, b.nsort,  b.temp,   b.dflags_light, b.dlight, b.dcount};
     for (void* p : ptrs)
         if (p) hipFree(p);
@@ -874,8 +860,7 @@ hipError_t bins_alloc(BinBuffers& b, uint32_t T, uint32_t nb, const uint32_t* kb
         (e = grow(&b.done, 1)) != hipSuccess || (e = grow(&b.acc, kAccStride * (size_t)nb)) != hipSuccess ||
         (e = grow(&b.part, 10 * std::max<size_t>((keys + kBinWG - 1) / kBinWG, 1))) != hipSuccess ||
         (e = grow(&b.ekey, cap)) != hipSuccess || (e = grow(&b.eface, cap)) != hipSuccess ||
-        (e = grow(&b.emask, cap)) != hipSuccess || (e = grow(&b.erank, cap)) != hipSuccess || (e = grow(&b.tri, cap)) != hipSuccess ||
-        (e = grow(&b.mask, cap)) != hipSuccess || (e = grow(&b.hot, cap)) != hipSuccess ||
+        (e = grow(&b.emask, cap)) != hipSuccess || (e = grow(&b.erank, cap)) != hipSuccess || (e = grow(&b.ent, cap)) != hipSuccess ||
         (e = grow(&b.dflags, b.nsub)) != hipSuccess || (e = grow(&b.dpacked, b.nsub)) != hipSuccess ||
         (e = grow(&b.dflags_light, b.nsub)) != hipSuccess || (e = grow(&b.dlight, b.nsub)) != hipSuccess ||
         (e = grow(&b.dcount, 2)) != hipSuccess ||
@@ -922,23 +907,21 @@ hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tile
     }
     tb = b.temp_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(b.temp, tb, b.count, b.start, (int)(keys + 1), s)) != hipSuccess) return e;
-    bin_scatter_kernel<<<kPairGrid, kBinWG, 0, s>>>(b.n, (uint32_t)b.cap, b.ekey, b.eface, b.emask, b.erank, b.start, b.count,
-                                                    b.kbegin, b.nbins, sp.hot, multi ? sp.T1 : 0u, b.tri, b.mask,
-                                                    b.hot);
+    bin_scatter_kernel<<<kPairGrid, kBinWG, 0, s>>>(b.n, (uint32_t)b.cap, b.ekey, b.eface, b.emask, b.erank, b.start,
+                                                    b.kbegin, b.nbins, sp.hot, multi ? sp.T1 : 0u, b.ent);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // at most kFinGrid workgroups, each over `per` consecutive keys
     const uint32_t per = (uint32_t)std::max<size_t>(kBinWG, (keys + (size_t)kFinGrid * kBinWG - 1) / ((size_t)kFinGrid * kBinWG) * kBinWG);
     const uint32_t fgrid = (uint32_t)std::max<size_t>((keys + per - 1) / per, 1);
     bins_finalize_kernel<false><<<fgrid, kBinWG, 0, s>>>(per, b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase,
                                                          b.acc, b.part, b.done, b.n, (uint32_t)b.cap, b.kobj, sp.objs,
-                                                         b.tri, b.mask, b.hot, b.sortq, b.nsort, sp.state, ncam, nullptr,
-                                                         1u);
+                                                         b.ent, b.count, b.sortq, b.nsort, sp.state, ncam, nullptr, 1u);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    bin_sort_kernel<<<kSortGrid, kBinWG, 0, s>>>(b.sortq, b.nsort, b.start, b.tri, b.mask, b.hot);
+    bin_sort_kernel<<<kSortGrid, kBinWG, 0, s>>>(b.sortq, b.nsort, b.start, b.ent);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     bins_finalize_kernel<true><<<1, kBinWG, 0, s>>>(per, b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase, b.acc,
-                                                    b.part, b.done, b.n, (uint32_t)b.cap, b.kobj, sp.objs, b.tri, b.mask,
-                                                    b.hot, b.sortq, b.nsort, sp.state, ncam, sp.path_union,
+                                                    b.part, b.done, b.n, (uint32_t)b.cap, b.kobj, sp.objs, b.ent, b.count,
+                                                    b.sortq, b.nsort, sp.state, ncam, sp.path_union,
                                                     sp.union_nobj ? sp.union_nobj : 1u);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (!b.nsub) return hipSuccess;

@@ -88,23 +88,31 @@ constexpr uint32_t kMaxBounces = 16;
 // Frames one launch may render (eray_frame_ring::frames_per_launch <= slots <= 64).
 constexpr uint32_t kMaxFramesPerLaunch = 64;
 
-struct ObjGeom {  // what the triangle scans need of an object, 80 B
+// One entry of a screen bin (bins.hip): a face that may be hit in the bin, its intersection
+// record, the bin's pixels it may cover (bit row * kBinW + column) and its index relative to the
+// object's first face — one 64-B line, so the scatter that places an entry in its bin writes one
+// line and a detail wave reads a 64-entry chunk as 4 KB of consecutive lines.
+struct alignas(16) BinEntry {
+    TriHot hot;
+    unsigned long long mask;
+    uint32_t tri, pad;
+};
+static_assert(sizeof(BinEntry) == 64, "one 64-B line per bin entry");
+
+struct ObjGeom {  // what the triangle scans need of an object, 64 B
     uint32_t tri_begin, tri_count;
     // Camera pixels whose primary ray can hit the object: x0..x1 x y0..y1 (inclusive, camera
     // rows), from the culling records (tri_rect_kernel); empty when x0 > x1.
     int32_t rect[4];
     float bb_lo[3], bb_hi[3];
-    // Screen bins of a large object's faces (bins.hip), or null: bin b's faces, in increasing
-    // index, are bin_tri[bin_start[b] .. bin_start[b + 1]) (indices relative to tri_begin);
-    // bin_mask[] holds the bin's pixels each may cover (bit row * kBinW + column) and bin_hot[]
-    // its intersection record, at the same positions.
+    // Screen bins of a large object's faces (bins.hip), or null: bin b's entries are
+    // bin_ent[bin_start[b] .. bin_start[b + 1]) (bins of 65..kBinSortMax entries in increasing
+    // face index).
     const uint32_t* bin_start;
-    const uint32_t* bin_tri;
-    const unsigned long long* bin_mask;
-    const TriHot* bin_hot;
+    const BinEntry* bin_ent;
 };
 
-struct alignas(16) ObjectDesc {  // 208 B: the LDS scene copy moves whole 16-B words
+struct alignas(16) ObjectDesc {  // 192 B: the LDS scene copy moves whole 16-B words
     ObjGeom g;
     MaterialDesc mat;
 };
@@ -403,9 +411,7 @@ struct BinBuffers {
     uint32_t* eface = nullptr;
     unsigned long long* emask = nullptr;
     uint32_t* erank = nullptr;            // the entry's place among its bin's entries (count's old value)
-    uint32_t* tri = nullptr;              // bin entries in key order (cap)
-    unsigned long long* mask = nullptr;
-    TriHot* hot = nullptr;
+    BinEntry* ent = nullptr;              // bin entries in key order (cap)
     // detail sub-block list of the rendered rows
     uint8_t* dflags = nullptr;            // listed sub-blocks whose bin holds more than one chunk
     uint8_t* dflags_light = nullptr;      // ... and the other listed ones

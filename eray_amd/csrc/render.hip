@@ -481,16 +481,18 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
             live = __ballot(T.best[lane] > base);
             if (!live) continue;
             if (j < end) {
+                const BinEntry x = as_global_rec(ob.bin_ent + j);  // (one 64-B line per entry)
                 fj = j;
-                pm = ob.bin_mask[j];
-                L.cand[lane] = ob.bin_hot[j];
+                pm = x.mask;
+                L.cand[lane] = x.hot;
                 L.key[lane] = j;
             }
         } else {
             if (j < end) {
-                fj = ob.bin_tri[j];
-                pm = ob.bin_mask[j];
-                L.cand[lane] = ob.bin_hot[j];
+                const BinEntry x = as_global_rec(ob.bin_ent + j);
+                fj = x.tri;
+                pm = x.mask;
+                L.cand[lane] = x.hot;
                 L.key[lane] = fj;
             }
             uint32_t cmin = fj;  // the chunk's smallest face
@@ -561,8 +563,9 @@ __device__ void first_hit_binned(const FrameParams& p, const ObjGeom& ob, uint32
     if (st == kSearching && mine != 0xffffffffu) {
         float u, v, t;
         if (hi - lo > 64 && hi - lo <= kBinSortMax) {  // the winner again, for u, v, t
-            exact_test(ob.bin_hot[mine], o, d, u, v, t);
-            found = (int)ob.bin_tri[mine];
+            const BinEntry x = as_global_rec(ob.bin_ent + mine);
+            exact_test(x.hot, o, d, u, v, t);
+            found = (int)x.tri;
         } else {
             exact_test(as_global_rec(p.tris + ob.tri_begin + mine), o, d, u, v, t);
             found = (int)mine;
@@ -610,9 +613,10 @@ __device__ void first_hit_binned_wave(const ObjGeom& ob, uint32_t bin, int& st, 
         uint32_t fj = 0xffffffffu;
         unsigned long long pm = 0;
         if (j < hi) {
-            fj = ob.bin_tri[j];
-            pm = ob.bin_mask[j];
-            L.cand[lane] = ob.bin_hot[j];
+            const BinEntry x = as_global_rec(ob.bin_ent + j);
+            fj = x.tri;
+            pm = x.mask;
+            L.cand[lane] = x.hot;
         }
         uint32_t cmin = fj;  // the chunk's smallest face
 #pragma unroll

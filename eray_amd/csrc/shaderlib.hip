@@ -14,8 +14,7 @@ namespace gpu {
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kVec = 4;  // (the 16-B stores below assume 4)
-static_assert(kVec == 4, "store_rgb4 and the diffuse store write 4 texels");
+constexpr int kVec = 4;
 
 inline unsigned grid_for1(size_t items) {
     size_t blocks = (items + kBlock - 1) / kBlock;
@@ -129,41 +128,19 @@ __global__ void __launch_bounds__(kBlock) mix_kernel(uint32_t w, uint32_t h, Tex
 __global__ void __launch_bounds__(kBlock) material_example_kernel(
     uint32_t w, uint32_t h, float xf, float yf, float r, float g, float b, float factor,
     float* __restrict__ color, float* __restrict__ diffuse) {
-    // kVec consecutive texels per thread: kVec independent cosf chains in flight (the chain is
-    // latency-bound, one per thread left the kernel at a quarter of the write rate) and 16-B
-    // stores (3 for the color texels, 1 for the diffuse ones)
     const size_t n = (size_t)w * h;
     const float omf = 1.0f - factor;
-    const size_t stride = (size_t)gridDim.x * kBlock * kVec;
-    for (size_t i0 = ((size_t)blockIdx.x * kBlock + threadIdx.x) * kVec; i0 < n; i0 += stride) {
-        uint32_t y = (uint32_t)(i0 / w), x = (uint32_t)(i0 - (size_t)y * w);
-        float v[kVec];
-#pragma unroll
-        for (int k = 0; k < kVec; ++k) {
-            v[k] = wave_value(x, y, xf, yf);  // (texels past the end are computed, not stored)
-            if (++x == w) {
-                x = 0;
-                ++y;
-            }
-        }
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        const uint32_t y = (uint32_t)(i / w), x = (uint32_t)(i - (size_t)y * w);
+        const float v = wave_value(x, y, xf, yf);
         if (color) {
-            float c[kVec][3];
-#pragma unroll
-            for (int k = 0; k < kVec; ++k) {
-                c[k][0] = v[k] * omf + r * factor;
-                c[k][1] = v[k] * omf + g * factor;
-                c[k][2] = v[k] * omf + b * factor;
-            }
-            store_rgb4(color, i0, n, c);
+            float* c = color + 3 * i;
+            c[0] = v * omf + r * factor;
+            c[1] = v * omf + g * factor;
+            c[2] = v * omf + b * factor;
         }
-        if (diffuse) {
-            float* p = diffuse + i0;
-            if (i0 + kVec <= n && ((reinterpret_cast<uintptr_t>(p) & 15) == 0)) {
-                *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-            } else {
-                for (int k = 0; k < kVec && i0 + k < n; ++k) p[k] = v[k];
-            }
-        }
+        if (diffuse) diffuse[i] = v;
     }
 }
 
@@ -201,7 +178,7 @@ hipError_t launch_material_example(uint32_t w, uint32_t h, float xf, float yf, f
                                    hipStream_t s) {
     size_t n = (size_t)w * h;
     if (!n) return hipSuccess;
-    material_example_kernel<<<grid_for(n), kBlock, 0, s>>>(w, h, xf, yf, r, g, b, factor, color,
+    material_example_kernel<<<grid_for1(n), kBlock, 0, s>>>(w, h, xf, yf, r, g, b, factor, color,
                                                            diffuse);
     return hipGetLastError();
 }

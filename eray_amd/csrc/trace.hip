@@ -279,9 +279,10 @@ __device__ void camera_hits(const FrameParams& p, f3 C, const f3 (&d)[kRays], ui
             const uint32_t j = rb + 64 * wg + lane;
             unsigned long long m = 0;
             if (j < hi) {
-                m = ob.bin_mask[j] & act;
-                E.tri[lane] = ob.bin_tri[j];
-                E.hot[lane] = ob.bin_hot[j];
+                const BinEntry x = ob.bin_ent[j];  // (one 64-B line per entry)
+                m = x.mask & act;
+                E.tri[lane] = x.tri;
+                E.hot[lane] = x.hot;
             }
             const uint32_t pop = (uint32_t)__popcll(m);
             const bool narrow = pop && pop <= kWide;
