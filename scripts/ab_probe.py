@@ -34,7 +34,8 @@ CONFIGS = {"fill4k1": ("none", 3840, 2160, 1, 1), "fill4k4": ("none", 3840, 2160
            "ns4": ("70k", 3840, 2160, 4, 1), "c5": ("1m", 7680, 4320, 1, 1), "moving_ns": ("70k", 3840, 2160, 1, 1),
            "moving_c5": ("1m", 7680, 4320, 1, 1),
            "aa2": ("cube", 1920, 1080, 1, 1), "aa_ns": ("70k", 3840, 2160, 1, 1),
-           "ns1sep": ("70k", 3840, 2160, 1, 1), "ns4sep": ("70k", 3840, 2160, 4, 1)}
+           "ns1sep": ("70k", 3840, 2160, 1, 1), "ns4sep": ("70k", 3840, 2160, 4, 1),
+           "ns1ex": ("70k", 3840, 2160, 1, 1), "ns4ex": ("70k", 3840, 2160, 4, 1), "c2ex": ("cube", 1920, 1080, 8, 8)}
 # launch-shape overrides (eray_render_params::flags) of the *sep configs: the dense build beside a
 # separate fill kernel
 SEPARATE = ("ns1sep", "ns4sep")
@@ -67,7 +68,10 @@ def main() -> None:
             ctx = empty_scene_context(0, W, H, frame_camera_fov(W, H), st)
             sc = None
         else:
-            sc = MainScene(ctx, *mesh_of(kind), W, H, texture=1024, fov=frame_camera_fov(W, H))
+            # (*ex: main.rs's graph evaluated at the hit texel, eray_scene_set_object_example_material:
+            # bit-identical frames, no texture reads)
+            sc = MainScene(ctx, *mesh_of(kind), W, H, texture=1024, fov=frame_camera_fov(W, H),
+                           material="example" if name.endswith("ex") else "textures")
         with torch.cuda.stream(st):
             rgb = torch.empty((slots, H, W, 3), dtype=torch.float32, device="cuda")
             ppm = torch.empty((slots, H, W, 3), dtype=torch.uint8, device="cuda")

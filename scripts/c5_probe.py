@@ -34,6 +34,10 @@ def main() -> None:
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--shares", default="0,3,7")
+    ap.add_argument("--no-full", action="store_true", help="skip the full frame (profiling one share)")
+    ap.add_argument("--shapes", default="default,separate_fill,single_launch",
+                    help="comma-separated launch shapes to time")
+    ap.add_argument("--no-empty", action="store_true", help="skip the empty-scene fill")
     args = ap.parse_args()
     W, H = args.width, args.height
     path = os.path.join(tempfile.gettempdir(), f"standin_{args.faces}_{args.seed}.obj")
@@ -51,7 +55,8 @@ def main() -> None:
     out = {"mesh_s": round(gen, 2), "frame": [W, H], "faces": int(len(mesh[0]))}
     shapes = {"default": capi.RENDER_DEFAULT, "separate_fill": capi.RENDER_DENSE_DETAIL | capi.RENDER_SEPARATE_FILL,
               "single_launch": capi.RENDER_DENSE_DETAIL | capi.RENDER_NO_SEPARATE_FILL}
-    for name, flags in shapes.items():
+    shapes = {k: v for k, v in shapes.items() if k in args.shapes.split(",")}
+    for name, flags in (() if args.no_full else shapes.items()):
         kw = dict(out_rgb=rgb.ptr, out_ppm=ppm.ptr, flags=flags)
         ctx.render(W, H, **kw)
         ctx.synchronize()
@@ -64,14 +69,15 @@ def main() -> None:
             ctx.render(W, H, **kw)
             ctx.synchronize()
             out[f"share{r}of{args.world}_{name}"] = ctx.time_frames(args.launches, W, H, **kw)
-    empty = capi.Context(0)  # the same camera, no object: the fill alone (this kernel's write floor)
-    empty.set_stream(st.cuda_stream)
-    empty.set_camera(capi.make_camera((0.0, 0.0, 5.0), (16.0, 9.0), W, 1.0))
-    empty.add_light(capi.make_light((1.0, 1.0, 2.0), "point"))
-    empty.render(W, H, out_rgb=rgb.ptr, out_ppm=ppm.ptr)
-    empty.synchronize()
-    out["full_empty_scene"] = empty.time_frames(args.launches, W, H, out_rgb=rgb.ptr, out_ppm=ppm.ptr)
-    empty.close()
+    if not args.no_empty:
+        empty = capi.Context(0)  # the same camera, no object: the fill alone (this kernel's write floor)
+        empty.set_stream(st.cuda_stream)
+        empty.set_camera(capi.make_camera((0.0, 0.0, 5.0), (16.0, 9.0), W, 1.0))
+        empty.add_light(capi.make_light((1.0, 1.0, 2.0), "point"))
+        empty.render(W, H, out_rgb=rgb.ptr, out_ppm=ppm.ptr)
+        empty.synchronize()
+        out["full_empty_scene"] = empty.time_frames(args.launches, W, H, out_rgb=rgb.ptr, out_ppm=ppm.ptr)
+        empty.close()
     rgb.free()
     ppm.free()
     sc.close()

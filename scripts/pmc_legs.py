@@ -1,6 +1,7 @@
 """Frame-kernel counter summaries per workload (round 4), from rocprofv3 --pmc passes of bench.py.
 
     python scripts/pmc_legs.py <pass dir under gpurun_out> <output json> [--north-star SLOTS]
+                                                                        [--workload JSON]
 
 Each pass directory holds one rocprofv3 counter run per counter group (scripts/session_r04b.sh:
 `sq`, `fetch`, `write`, each its own run, kernel trace only).  Per counter the median over the
@@ -45,8 +46,8 @@ def main() -> None:
         fetch += f.get("FETCH_SIZE", 0.0) * 1024
         write += f.get("WRITE_SIZE", 0.0) * 1024
         name += " + " + fills[0]
-    workload = None
-    for log in glob.glob(os.path.join(src, "*.log")):
+    workload = json.loads(sys.argv[sys.argv.index("--workload") + 1]) if "--workload" in sys.argv else None
+    for log in ([] if workload else glob.glob(os.path.join(src, "*.log"))):
         for line in open(log):
             if not line.startswith("{"):
                 continue
