@@ -682,6 +682,8 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t per, con
             st[k].bin_overflow |= overflow ? 1u : 0u;
             st[k].nrect = 0u;
             st[k].total_sub = 0u;  // counted by detail_list_kernel
+            st[k].heavy_sub = 0u;
+            st[k].light_sub = 0u;
         }
     }
 }
@@ -735,11 +737,13 @@ __global__ void __launch_bounds__(kBinWG) detail_flags_kernel(const ObjectDesc* 
 }
 
 // Appended form (camera paths: one launch instead of four): the same flags, the listed sub-blocks
-// appended with one counter atomic per workgroup (raster order within a workgroup's 256
-// sub-blocks; the frame kernel needs no order, though the raster order is 2 % faster at
-// 3840x2160 / 70k, so one-camera setups keep it); the count lands in CamState::total_sub (zeroed
-// by the finaliser).  (Carrying the bin range in the entry,
-// one scalar load fewer per sub-block, measured slower: C3 +0.3 us, 3840x2160 / 70k +1 us.)
+// appended with one counter atomic per workgroup and kind — heavy ones (a bin of more than one
+// 64-entry chunk) from the front of the camera's list, light ones from its back — so the frame
+// kernel still deals the heavy sub-blocks first and searches the light ones one wave each
+// (FrameParams::dlist_split; unordered, every sub-block was shared by a workgroup: the moving
+// 3840x2160 / 70k frame kernel ran 40 us against 22.6 static).  The counts land in CamState
+// (total_sub, heavy_sub, light_sub; zeroed by the finaliser).  (Carrying the bin range in the
+// entry, one scalar load fewer per sub-block, measured slower: C3 +0.3 us, 3840x2160 / 70k +1 us.)
 __global__ void __launch_bounds__(kBinWG) detail_list_kernel(const ObjectDesc* __restrict__ objs, uint32_t nobj,
                                                              uint32_t cam_w, uint32_t row0, uint32_t rows,
                                                              uint32_t band_shift, uint32_t band_mask,
@@ -747,48 +751,62 @@ __global__ void __launch_bounds__(kBinWG) detail_list_kernel(const ObjectDesc* _
                                                              uint32_t tiles_x, uint32_t n,
                                                              uint32_t* __restrict__ list, uint8_t* __restrict__ occ,
                                                              CamState* __restrict__ st) {
-    __shared__ uint32_t s_cnt[kBinWG / 64];
-    __shared__ uint32_t s_base;
-    // camera blockIdx.y of a multi-camera setup: its descriptors, list, occupancy and count
+    __shared__ uint32_t s_cnt[2][kBinWG / 64];
+    __shared__ uint32_t s_base[2];
+    // camera blockIdx.y of a multi-camera setup: its descriptors, list, occupancy and counts
     objs += (size_t)blockIdx.y * nobj;
     list += (size_t)blockIdx.y * n;
     occ += (size_t)blockIdx.y * (n / 4);
-    uint32_t* total = &st[blockIdx.y].total_sub;
+    CamState& cs = st[blockIdx.y];
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t row_subs = 4 * tiles_x;
     const uint32_t sx = s % row_subs, sy = s / row_subs;
-    bool hit = false;
+    bool hit = false, heavy = false;
     if (s < n && sx * kBinW < cam_w) {
         const int32_t x0 = (int32_t)(sx * kBinW), x1 = x0 + (int32_t)kBinW - 1;
         // the sub-block's camera rows (one band: bands are multiples of kBinH rows)
         const int32_t y0 = (int32_t)band_camera_row(row0, band_shift, band_mask, band_stride, sy * kBinH);
         const int32_t y1 = y0 + (int32_t)min(kBinH, rows - sy * kBinH) - 1;
-        for (uint32_t oi = 0; oi < nobj && !hit; ++oi) {
+        for (uint32_t oi = 0; oi < nobj; ++oi) {
             const ObjGeom& g = objs[oi].g;
             if (!g.tri_count) continue;
             if (g.bin_start) {
                 const uint32_t bin = (((uint32_t)y0 + kBinH - phase) / kBinH) * bins_x + sx;
-                hit = g.bin_start[bin + 1] > g.bin_start[bin];
+                const uint32_t cnt = g.bin_start[bin + 1] - g.bin_start[bin];
+                hit |= cnt != 0;
+                heavy |= cnt > 64;
             } else {
-                hit = x0 <= g.rect[1] && x1 >= g.rect[0] && y0 <= g.rect[3] && y1 >= g.rect[2];
+                hit |= x0 <= g.rect[1] && x1 >= g.rect[0] && y0 <= g.rect[3] && y1 >= g.rect[2];
             }
         }
     }
     // the block's four flags: lanes 4b .. 4b + 3 of the wave (row_subs is a multiple of 4)
-    const unsigned long long bal = __ballot(hit);
+    const unsigned long long bal = __ballot(hit), bh = __ballot(hit && heavy), bl = bal & ~bh;
     if (s < n && (threadIdx.x & 3) == 0) occ[s / 4] = (uint8_t)((bal >> (threadIdx.x & 63)) & 0xfu);
-    if (lane == 0) s_cnt[wave] = (uint32_t)__popcll(bal);
-    __syncthreads();
-    uint32_t before = 0, all = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < kBinWG / 64; ++w) {
-        before += w < wave ? s_cnt[w] : 0u;
-        all += s_cnt[w];
+    if (lane == 0) {
+        s_cnt[0][wave] = (uint32_t)__popcll(bh);
+        s_cnt[1][wave] = (uint32_t)__popcll(bl);
     }
-    if (threadIdx.x == 0) s_base = all ? atomicAdd(total, all) : 0u;
     __syncthreads();
-    if (hit) list[s_base + before + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = (sy << 16) | sx;
+    uint32_t before[2] = {0u, 0u}, all[2] = {0u, 0u};
+#pragma unroll
+    for (uint32_t w = 0; w < kBinWG / 64; ++w)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            before[k] += w < wave ? s_cnt[k][w] : 0u;
+            all[k] += s_cnt[k][w];
+        }
+    if (threadIdx.x == 0) {
+        s_base[0] = all[0] ? atomicAdd(&cs.heavy_sub, all[0]) : 0u;
+        s_base[1] = all[1] ? atomicAdd(&cs.light_sub, all[1]) : 0u;
+        if (all[0] + all[1]) atomicAdd(&cs.total_sub, all[0] + all[1]);
+    }
+    __syncthreads();
+    const uint32_t e = (sy << 16) | sx;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    if (hit && heavy) list[s_base[0] + before[0] + (uint32_t)__popcll(bh & lt)] = e;
+    else if (hit) list[n - 1 - (s_base[1] + before[1] + (uint32_t)__popcll(bl & lt))] = e;
 }
 
 // The light sub-blocks after the heavy ones (ordered detail list); the list's length into CamState.

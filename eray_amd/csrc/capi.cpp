@@ -1725,9 +1725,10 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
         return ERAY_OK;
     }
     // device-camera mode: every frame reads its setup's CamState; the per-frame detail lists are
-    // appended unordered (no heavy count)
+    // appended split (heavy sub-blocks from the front, light ones from the back: CamState counts)
     p.cam_state = ctx->d_state;
     p.detail_heavy = nullptr;
+    p.dlist_split = p.detail_list ? (uint32_t)ctx->bins.nsub : 0u;
     p.nrect = 0;
     std::memset(p.rects, 0, sizeof p.rects);
     // the cameras: staged in pinned memory, copied to the device once per call; each graph chunk
@@ -1841,6 +1842,7 @@ int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, co
         q.detail_occ = m.bins.docc + (size_t)k * (nsub / 4);
         q.dev_slots = nf > 1 ? 1u : 0u;
         q.dlist_stride = nf > 1 ? nsub : 0u;
+        q.dlist_split = nsub;
         HIP_TRY(ctx, launch_frame(ctx, q));
         if (k + nf >= K || slot + nf >= count) HIP_TRY(ctx, hipEventRecord(ctx->mc_free[b & 1u], ctx->stream));
         return ERAY_OK;
@@ -2142,7 +2144,7 @@ extern "C" int eray_debug_set_bin_form(eray_ctx* ctx, int rect_pairs) {
     ctx->mc_layout.clear();
     return ERAY_OK;
 }
-// Diagnostics: the last setup's device state (CamState, 176 B) and object `index`'s pixel
+// Diagnostics: the last setup's device state (CamState, 192 B) and object `index`'s pixel
 // rectangle as the frame kernel reads them (synchronises).
 extern "C" int eray_debug_setup_state(eray_ctx* ctx, uint32_t index, void* state_out, int32_t* rect_out) {
     if (!ctx || !state_out || !rect_out || index >= ctx->objects.size()) return ERAY_E_INVALID_ARGUMENT;

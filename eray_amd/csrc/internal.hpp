@@ -140,6 +140,9 @@ struct alignas(16) CamState {
     uint32_t total_sub;           // detail sub-blocks (rectangles' area, or the detail list's length)
     uint32_t bin_entries;         // (face, bin) entries the bins needed (host capacity sizing)
     uint32_t bin_overflow;        // the bins did not fit: binned objects fall back to LDS tiles
+    // a split detail list (FrameParams::dlist_split, camera paths): heavy sub-blocks appended from
+    // the front, light ones from the back (bins.hip detail_list_kernel)
+    uint32_t heavy_sub, light_sub;
     int32_t rects[kMaxRects][4];  // x0, x1, y0, y1 (inclusive)
 };
 
@@ -229,6 +232,9 @@ struct FrameParams {
     uint32_t nframes;
     uint32_t dev_slots;
     uint32_t dlist_stride;
+    // device-camera mode with a split detail list of this capacity (0: none): list position j of
+    // CamState::heavy_sub heavy sub-blocks is j, of a light one dlist_split - 1 - (j - heavy_sub)
+    uint32_t dlist_split;
     uint64_t rgb_stride, ppm_stride, face_stride;
 };
 

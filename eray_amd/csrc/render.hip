@@ -1305,8 +1305,8 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     // ---- detail sub-blocks -------------------------------------------------------------------
     if (bid < nd) {
         // the ordered detail list's heavy count (no count: every iteration shares its work)
-        const uint32_t heavy = (kLdsTiles && p.detail_heavy && !(p.launch_flags & kLaunchSharedDetail))
-                                   ? load_const(p.detail_heavy, 0) : 0xffffffffu;
+        const bool counted = kLdsTiles && !(p.launch_flags & kLaunchSharedDetail);
+        const uint32_t heavy0 = (counted && p.detail_heavy) ? load_const(p.detail_heavy, 0) : 0xffffffffu;
         // snake order for the ordered (heavy-first) lists of binned meshes
         constexpr bool kSnake = kLdsTiles;
         const RowMap rm{p.row0, h_band & 31u, h_band >> 5};
@@ -1325,10 +1325,15 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
             const uint32_t* dlist = p.detail_list ? p.detail_list + (size_t)slot * p.dlist_stride : nullptr;
             const uint32_t nrect = dlist ? 0u : frame_nrect<kDev>(p, cs);
             const CamDev cam = frame_camera<kDev>(p, cs);
+            // a split list (camera paths): the frame's heavy sub-blocks from the front, the light
+            // ones from the back (bins.hip detail_list_kernel)
+            const bool split = kDev && p.dlist_split && dlist;
+            const uint32_t heavy = split ? (counted ? load_const(&cs->heavy_sub, 0) : 0xffffffffu) : heavy0;
+            auto lpos = [&](uint32_t j) { return split && j >= heavy ? p.dlist_split - 1u - (j - heavy) : j; };
             // detail sub-block j (enumeration order) -> sub-block coordinates
             auto locate = [&](uint32_t j, int32_t& sx, int32_t& sy) {
                 if (dlist) {
-                    const uint32_t e = dlist[j];
+                    const uint32_t e = dlist[lpos(j)];
                     sx = (int32_t)(e & 0xffffu);
                     sy = (int32_t)(e >> 16);
                     return;
@@ -1414,7 +1419,7 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
                     bool nvalid = false, ncoop = false;
                     const uint32_t jn = job(r + 1, nvalid, ncoop);
                     const bool nactive = nvalid && jn < total && pstart;
-                    if (nactive) nx_e = vload_u32(dlist, jn);
+                    if (nactive) nx_e = vload_u32(dlist, lpos(jn));
                     nx_range = false;
                     auto mid = [&]() {
                         if (!nactive) return;

@@ -30,7 +30,7 @@ int eray_debug_set_bin_form(eray_ctx* ctx, int rect_pairs);
 /* Sets the bins' entry capacity (reallocated at the next setup; overflow and growth tests). */
 int eray_debug_set_bin_capacity(eray_ctx* ctx, uint64_t entries);
 uint64_t eray_debug_bin_capacity(const eray_ctx* ctx);
-/* The last setup's device state (176 B) and object `index`'s pixel rectangle. */
+/* The last setup's device state (192 B) and object `index`'s pixel rectangle. */
 int eray_debug_setup_state(eray_ctx* ctx, uint32_t index, void* state_out, int32_t* rect_out);
 /* The multi-GPU gathers' rank-0 steps for N ranks simulated on one GPU (staging: the N ranks'
  * padded local PPM blocks): the band reorder, the coded transport's decode, the scene-camera
