@@ -7,9 +7,9 @@
 
 Metric (BASELINE.json): Mrays/s + frame ms at 1920x1080 cube.obj, 1/2/4/8-GPU tile scaling.
 Workload (configs[1]): objects/cube.obj with src/main.rs's scene and material
-graph, a 1920x1080 frame.  One step = one frame: camera rays, first-hit triangle scan, shading
-with shadow rays, the f32 image and the PPM bytes (fused), and for N > 1 the frame assembled on
-rank 0.  Inputs (mesh, material textures) are resident in HBM before timing; the material graph is
+graph, a 1920x1080 frame.  One step = one batch of frames (the single-GPU launch size, 8 frames at
+C2; --frames-per-step), each frame: camera rays, first-hit triangle scan, shading with shadow rays,
+the f32 image and the PPM bytes (fused), and for N > 1 the frame assembled on one GPU.  Inputs (mesh, material textures) are resident in HBM before timing; the material graph is
 evaluated once, as Material::update is (reported separately).
 
 Frames in flight: a serving loop renders a stream of independent frames, so the frames go
@@ -20,10 +20,11 @@ per launch beside it.
 
 Multi-GPU (row tiles), default --scaling strong: the same 1920x1080 frame split over
 the N GPUs in interleaved 4-row bands (equal work wherever the cube sits); N = 1 is exactly C2.
-Every frame is assembled on rank 0 (eray_gather_frames): the ranks render batches of frames into
-one half of a two-half ring while the previous batch's rows travel over xGMI (RCCL point-to-point,
-only the objects' pixel rectangles: ERAY_GATHER_SCENE_CAMERA) on a second stream and rank 0 writes
-the frames.  --scaling weak widens the frame to (1920 N) x 1080 instead (not a BASELINE config).
+Every frame is assembled whole on one GPU (eray_gather_frames): the ranks render batches of frames
+into one half of a two-half ring while the previous batch's rows travel over xGMI (RCCL
+point-to-point, only the objects' pixel rectangles: ERAY_GATHER_SCENE_CAMERA) on a second stream;
+frame k of a batch is assembled on rank k % N (ERAY_GATHER_ROTATE_ROOT, default) or every frame on
+rank 0 (--gather-root 0).  --scaling weak widens the frame to (1920 N) x 1080 instead (not a BASELINE config).
 C4 (--width 3840 --height 2160) and C5 (7680x4320, a 1M-face mesh) are available by flag.
 
 Prints ONE JSON line on rank 0 (metric "Mrays/s": primary rays of all frames / wall time).
@@ -475,6 +476,10 @@ def main() -> None:
     ap.add_argument("--height", type=int, default=HEIGHT, help="frame height (C2: 1080)")
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
                     help="strong: one width x height frame split N ways (BASELINE); weak: a (width N) x height frame")
+    ap.add_argument("--frames-per-step", type=int, default=0,
+                    help="frames per step (0: the single-GPU launch size of the full frame, the same for every N)")
+    ap.add_argument("--gather-root", choices=("rotate", "0"), default="rotate",
+                    help="N > 1, scene gather: frame k assembled on rank k %% N (rotate) or all on rank 0")
     ap.add_argument("--frames-per-launch", type=int, default=0,
                     help="frames in flight per kernel launch (0: the library's choice, eray_frames_per_launch)")
     ap.add_argument("--brute-force", action="store_true", help="disable the exact wave culling")
@@ -555,6 +560,9 @@ def main() -> None:
     F = args.frames_per_launch or ctx.frames_per_launch(width, H, rows=rows, slots=64)
     G = F
     slots = F if world == 1 else 2 * G
+    # frames per step: one single-GPU launch of the full frame, so a step is the same work at every N
+    fps = args.frames_per_step or ctx.frames_per_launch(args.width, H, rows=H, slots=64)
+    n_timed = args.steps * fps
     slot_px = alloc_rows * width
     rgb = torch.empty((slots, alloc_rows, width, 3), dtype=torch.float32, device="cuda")
     ppm = torch.zeros((slots, alloc_rows, width, 3), dtype=torch.uint8, device="cuda")
@@ -581,8 +589,12 @@ def main() -> None:
 
     gather = None
     frames_out = None
+    rotate = False
     if world > 1:
-        frames_out = torch.empty((G, H, width, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
+        rotate = args.gather_root == "rotate" and args.gather == "scene" and not rehearsal
+        # the frames this rank assembles per batch: k = rank, rank + N, ... (rotating roots) or all on rank 0
+        n_out = (G - rank + world - 1) // world if rotate else (G if rank == 0 else 0)
+        frames_out = torch.empty((n_out, H, width, 3), dtype=torch.uint8, device="cuda") if n_out else None
         gstream = torch.cuda.Stream()
         if not rehearsal:
             rccl = RowGather(ctx, world, rank)
@@ -591,7 +603,7 @@ def main() -> None:
                 ctx.set_stream(gstream.cuda_stream)
                 ctx.gather_frames(rccl.comm, ppm[half * G].data_ptr(), slot_px * 3,
                                   frames_out.data_ptr() if frames_out is not None else 0, H * width * 3, n, H, width,
-                                  band_rows=band, scene_camera=args.gather == "scene")
+                                  band_rows=band, scene_camera=args.gather == "scene", rotate_root=rotate)
                 ctx.set_stream(stream.cuda_stream)
         else:
             def gather(half, n):  # plumbing only: gloo through host memory
@@ -627,12 +639,12 @@ def main() -> None:
 
     # launch plans (graphs) of every batch size, the gather plan and buffers, then W warmup frames,
     # all outside the timed region
-    sizes = {min(G, args.steps)} | ({args.steps % G} if world > 1 and args.steps % G else set())
+    sizes = {min(G, n_timed)} | ({n_timed % G} if world > 1 and n_timed % G else set())
     for n in sizes:
         ctx.render_frames(n, width, H, prepare_only=True, **(ring_args() if world == 1 else ring_args(0, G)))
     if world == 1:
-        ctx.render_frames(args.steps, width, H, prepare_only=True, **ring_args())
-    run(max(args.warmup, 1))
+        ctx.render_frames(n_timed, width, H, prepare_only=True, **ring_args())
+    run(max(args.warmup, 1) * fps)
     if world > 1:
         for n in sizes:
             run(n)
@@ -642,7 +654,7 @@ def main() -> None:
     torch.cuda.synchronize()
     with MARK.range(f"steps_F{F}"):  # (pushed before, popped after the clock's two readings)
         t0 = time.perf_counter()
-        run(args.steps)
+        run(n_timed)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -735,7 +747,8 @@ def main() -> None:
         is_c2 = (width, H) == (WIDTH, HEIGHT) and args.mesh.endswith("objects/cube.obj") and not args.brute_force
         pixels = width * rows
         ms_per_step = elapsed / args.steps * 1e3
-        rays = width * H * args.steps
+        frame_ms = elapsed / n_timed * 1e3
+        rays = width * H * n_timed
         value = rays / elapsed / 1e6
         alg = algorithmic_bytes(pixels, hits, hit_faces)
         gbs = alg / (kernel_ms * 1e-3) / 1e9
@@ -757,10 +770,11 @@ def main() -> None:
                      + ", procedural material graph"),
             "config": {
                 "workload": f"{'C2: ' if is_c2 else ''}{os.path.basename(args.mesh)}, {width}x{H} frame, "
-                            f"{width}x{rows} rows on rank 0, main.rs scene + material graph; step = one frame (camera "
+                            f"{width}x{rows} rows on rank 0, main.rs scene + material graph; step = {fps} frames, each: camera "
                             "rays, first-hit scan, shading + shadow rays, f32 image and PPM bytes"
-                            + (", assembled on rank 0: scene-camera gather over RCCL point-to-point" if world > 1 else "")
-                            + f"); {F} frames in flight per launch",
+                            + ((", assembled on rank k % N" if rotate else ", assembled on rank 0")
+                               + ": scene-camera gather over RCCL point-to-point" if world > 1 else "")
+                            + f"; {F} frames in flight per launch",
                 "mesh": mesh_label(args.mesh),
                 "triangles": int(len(mesh[0])),
                 "frame": [width, H],
@@ -768,6 +782,7 @@ def main() -> None:
                 "texture": TEXTURE,
                 "parallelism": (f"row tiles x{world} ({'interleaved 4-row bands' if bands else 'contiguous blocks'})"
                                 if world > 1 else "single GPU"),
+                "frames_per_step": fps,
                 "frames_per_launch": F,
                 "ring_slots": slots,
                 "camera": "static (value); see moving_camera",
@@ -775,14 +790,15 @@ def main() -> None:
                    if world > 1 and args.scaling == "weak" else {}),
                 "culling": not args.brute_force,
             },
-            "frame_ms": round(ms_per_step, 6),
+            "frame_ms": round(frame_ms, 6),
             "render_kernel_ms": round(kernel_ms, 6),
             "frame_latency_ms": None if latency is None else round(latency["frame_kernel_ms"], 6),
             "graph_replay_ms_per_frame": round(replay_ms, 6),
             "material_graph_s": round(t_mat, 4),
             "material_update": material_line,
             "scene_setup_ms": round(t_setup * 1e3, 3),
-            "gather": ({"kind": f"{args.gather}, every frame, batches of {G} overlapped with rendering",
+            "gather": ({"kind": f"{args.gather}, every frame, batches of {G} overlapped with rendering, "
+                                + ("frame k on rank k % N" if rotate else "every frame on rank 0"),
                         "ms_per_frame_alone": round(gather_ms, 5)} if world > 1 else None),
             "rank_kernel_ms": [round(v, 6) for v in rank_kernel_ms],
             "moving_camera": moving,

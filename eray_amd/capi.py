@@ -40,6 +40,7 @@ RENDER_SHARED_DETAIL = 32
 
 GATHER_DEFAULT = 0
 GATHER_SCENE_CAMERA = 1
+GATHER_ROTATE_ROOT = 2
 
 LIGHT_POINT = 0
 LIGHT_AMBIENT = 1
@@ -201,6 +202,8 @@ DEBUG_SIGNATURES = {
     "eray_debug_coded_unband": (C.c_int, [_P, _P, _P, _U, _U, _U, _U]),
     "eray_debug_scene_gather": (C.c_int, [_P, _P, _P, _U, _U, _U, _U]),
     "eray_debug_gather_layout": (C.c_int, [C.POINTER(C.c_int32), _U, _U, _U, _U, _U, _U, C.POINTER(C.c_uint32)]),
+    "eray_debug_scene_gather_batch": (C.c_int, [_P, _P, _P, _U, _U, _U, _U, _U, _U]),
+    "eray_debug_gather_schedule": (C.c_int, [C.POINTER(C.c_uint32), _U, _U, _U, _U, C.POINTER(C.c_uint64), _U]),
 }
 
 _lib = None
@@ -298,6 +301,22 @@ def gather_layout(rects, height: int, width: int, band_rows: int, nranks: int, r
     rs = [dict(zip(("l0", "l1", "c0", "c1", "off", "row_bytes", "first"), out[4 + 8 * i: 4 + 8 * i + 7]))
           for i in range(out[1])]
     return {"rows": out[0], "bytes": out[2], "packed_rows": out[3], "rects": rs}
+
+
+def gather_schedule(rank_bytes, rank: int, nframes: int, rotate: bool) -> dict:
+    """The library's schedule of `rank` for a batch of `nframes` frames in the scene-camera gather
+    (eray_debug_gather_schedule, host only) when rank q packs rank_bytes[q] bytes per frame: its
+    buffer size, how many frames it assembles, each frame's pack offset, where each rank's packs
+    start in its receive area, and its point-to-point transfers (peer, send, offset, bytes)."""
+    n = len(rank_bytes)
+    cap = 3 + nframes + 9 * n
+    rb = (C.c_uint32 * n)(*[int(b) for b in rank_bytes])
+    out = (C.c_uint64 * cap)()
+    check(lib().eray_debug_gather_schedule(rb, n, rank, nframes, int(bool(rotate)), out, cap))
+    v = list(out)
+    k = 3 + nframes + n
+    ops = [dict(zip(("peer", "send", "off", "bytes"), v[k + 4 * i: k + 4 * i + 4])) for i in range(v[2])]
+    return {"need": v[0], "mine": v[1], "pack": v[3:3 + nframes], "recv": v[3 + nframes:k], "ops": ops}
 
 
 def comm_destroy(comm: int) -> None:
@@ -553,12 +572,15 @@ class Context:
         self._check(lib().eray_gather_rows(self._h, comm, local_ptr, frame_ptr or None, height, width, band_rows))
 
     def gather_frames(self, comm: int, local_ptr, local_stride: int, frames_ptr, frame_stride: int, nframes: int,
-                      height: int, width: int, band_rows: int = 0, scene_camera: bool = False) -> None:
+                      height: int, width: int, band_rows: int = 0, scene_camera: bool = False,
+                      rotate_root: bool = False) -> None:
         """eray_gather_frames: `nframes` frames' rows (local + k * local_stride) into rank 0's frames
-        (frames + k * frame_stride); scene_camera: only the objects' pixel rectangles travel."""
+        (frames + k * frame_stride); scene_camera: only the objects' pixel rectangles travel;
+        rotate_root (with scene_camera): frame k is assembled on rank k % N, at its frames + (k // N)
+        * frame_stride."""
+        flags = (GATHER_SCENE_CAMERA if scene_camera else GATHER_DEFAULT) | (GATHER_ROTATE_ROOT if rotate_root else 0)
         self._check(lib().eray_gather_frames(self._h, comm, local_ptr, local_stride, frames_ptr or None, frame_stride,
-                                             nframes, height, width, band_rows,
-                                             GATHER_SCENE_CAMERA if scene_camera else GATHER_DEFAULT))
+                                             nframes, height, width, band_rows, flags))
 
     def pack_ppm(self, rgb_ptr, w, h, out_ptr) -> None:
         self._check(lib().eray_pack_ppm(self._h, rgb_ptr, w, h, out_ptr))

@@ -292,6 +292,28 @@ struct RankLayout {        // a rank's rectangles and its share of rank 0's rece
     uint32_t rows, packed_rows;
     uint32_t pad[2];
 };
+// Which rank assembles frame k of a batch of B: rank 0, or (ERAY_GATHER_ROTATE_ROOT) rank k % n,
+// which spreads the assembly's frame writes and the inbound xGMI bytes of a stream of frames over
+// every GPU instead of piling them on rank 0.  A rank's pack of the batch holds its frames grouped
+// by root (one transfer per rank pair moves each group); the frames it assembles itself are packed
+// straight into its receive area.
+struct Roots {
+    uint32_t B, n;  // n == 0: every frame's root is rank 0
+    __host__ __device__ uint32_t root(uint32_t k) const { return n ? k % n : 0u; }
+    __host__ __device__ uint32_t index(uint32_t k) const { return n ? k / n : k; }  // among its root's frames
+    __host__ __device__ uint32_t count(uint32_t r) const {
+        return n ? (r < B ? (B - 1u - r) / n + 1u : 0u) : (r ? 0u : B);
+    }
+    __host__ __device__ uint32_t before(uint32_t r) const {  // frames whose root is below r
+        return n ? (B / n) * r + (B % n < r ? B % n : r) : 0u;
+    }
+    // frame k's slot in rank `me`'s send area (frames of other roots, grouped by root)
+    __host__ __device__ uint32_t send_slot(uint32_t k, uint32_t me) const {
+        const uint32_t r = root(k);
+        return before(r) - (r > me ? count(me) : 0u) + index(k);
+    }
+};
+
 // A rank's record in the plan exchange: [status, source kind, key low, key high | nrect, then
 // nrect x (l0, l1, c0, c1)] — every rank learns every rank's status and source, so all of them
 // accept the plan or all fail together.
@@ -306,8 +328,8 @@ struct GatherPlan {
     bool valid = false;
     std::vector<RankLayout> ranks;
     uint64_t total = 0;            // every rank's bytes per frame
-    RankLayout* d_ranks = nullptr; // rank 0: the assembly's table
-    uint8_t* buf = nullptr;        // this rank's packed frames (rank 0: the receive buffer of all ranks)
+    RankLayout* d_ranks = nullptr; // the assembly's table (every rank: any may be a root)
+    uint8_t* buf = nullptr;        // [receive area: its frames x every rank's packs | send area: its packs]
     size_t buf_cap = 0;
     int32_t* xchg = nullptr;       // the all-gather of the ranks' rectangles
 };
@@ -399,23 +421,26 @@ RankLayout layout_of(const int32_t* rec, uint32_t rows) {
     return R;
 }
 
-// Rank r's rows of frame blockIdx.y, rectangle by rectangle, into out + frame * bytes (16-B words:
-// rows of W % 16 == 0 pixels on 16-B aligned buffers, column groups of 48 B).
+// Rank `me`'s rows of frame blockIdx.y, rectangle by rectangle (16-B words: rows of W % 16 == 0
+// pixels on 16-B aligned buffers, column groups of 48 B), into its slot: own + index * bytes when
+// `me` assembles the frame, else send + send_slot * bytes.
 __global__ void __launch_bounds__(256) gather_pack_kernel(const uint8_t* __restrict__ local, uint64_t local_stride,
-                                                          uint8_t* __restrict__ out, RankLayout L, uint32_t W) {
+                                                          uint8_t* __restrict__ send, uint8_t* __restrict__ own,
+                                                          RankLayout L, uint32_t W, Roots R, uint32_t me) {
     const uint32_t q = blockIdx.x, k = blockIdx.y;
+    uint8_t* out = R.root(k) == me ? own + (size_t)R.index(k) * L.bytes : send + (size_t)R.send_slot(k, me) * L.bytes;
     uint32_t i = 0;
     while (i + 1 < L.nrect && q >= L.r[i + 1].first) ++i;
     const GatherRect& g = L.r[i];
     const uint32_t j = (uint32_t)g.l0 + (q - g.first);
     const uint4* src = reinterpret_cast<const uint4*>(local + k * local_stride + (size_t)(L.rows - 1 - j) * W * 3u +
                                                       48u * (uint32_t)g.c0);
-    uint4* dst = reinterpret_cast<uint4*>(out + (size_t)k * L.bytes + g.off + (size_t)(q - g.first) * g.row_bytes);
+    uint4* dst = reinterpret_cast<uint4*>(out + g.off + (size_t)(q - g.first) * g.row_bytes);
     for (uint32_t w = threadIdx.x; w < g.row_bytes / 16u; w += blockDim.x) dst[w] = src[w];
 }
 
-// Rank 0: file row blockIdx.x of frame blockIdx.y — the miss colour, except inside the owning
-// rank's rectangles, whose bytes come from that rank's block of the receive buffer.
+// A root: file row blockIdx.x of its frame blockIdx.y (of B) — the miss colour, except inside the
+// owning rank's rectangles, whose bytes come from that rank's block of the receive area.
 __global__ void __launch_bounds__(256) gather_assemble_kernel(const uint8_t* __restrict__ recv,
                                                               const RankLayout* __restrict__ lay, uint32_t B,
                                                               uint8_t* __restrict__ frames, uint64_t frame_stride,
@@ -640,14 +665,12 @@ int exchange_plan(eray_ctx* ctx, ncclComm_t c, int nranks, int rank, uint32_t H,
         P->total += R.bytes;
         P->ranks[(size_t)q] = R;
     }
-    if (rank == 0) {
-        if (P->d_ranks) hipFree(P->d_ranks);
-        P->d_ranks = nullptr;
-        if ((he = hipMalloc((void**)&P->d_ranks, sizeof(RankLayout) * (size_t)nranks)) != hipSuccess ||
-            (he = hipMemcpy(P->d_ranks, P->ranks.data(), sizeof(RankLayout) * (size_t)nranks, hipMemcpyHostToDevice)) !=
-                hipSuccess)
-            return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
-    }
+    if (P->d_ranks) hipFree(P->d_ranks);
+    P->d_ranks = nullptr;
+    if ((he = hipMalloc((void**)&P->d_ranks, sizeof(RankLayout) * (size_t)nranks)) != hipSuccess ||
+        (he = hipMemcpy(P->d_ranks, P->ranks.data(), sizeof(RankLayout) * (size_t)nranks, hipMemcpyHostToDevice)) !=
+            hipSuccess)
+        return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
     P->comm = (void*)c;
     P->kind = src.kind;
     P->key = src.key;
@@ -673,36 +696,71 @@ int grow(eray_ctx* ctx, GatherPlan* P, size_t bytes) {
     return ERAY_OK;
 }
 
-// Pack (every rank), transfer, assemble (rank 0) `B` frames with plan P.  fail_safe (this rank's
-// own arguments are unusable): only the transfers of the plan, so the other ranks' matching
-// sends and receives complete — no kernel touches the caller's buffers.
-int scene_gather(eray_ctx* ctx, ncclComm_t c, const GatherPlan& P, const uint8_t* local, uint64_t local_stride,
-                 uint8_t* frames, uint64_t frame_stride, uint32_t B, bool fail_safe = false) {
+// One rank's part of a batch of B frames: where its packs go in its buffer, how much buffer it
+// needs, and its point-to-point transfers (offsets into the buffer).  Its receive area holds, for
+// each of the `mine` frames it assembles, every rank's pack (rank q's at mine * off_q + j * bytes_q,
+// the layout gather_assemble_kernel reads); its send area the frames of the other roots, grouped
+// by root, so each (rank, root) pair is one transfer.
+struct Xfer {
+    uint32_t peer;
+    bool send;
+    size_t off, bytes;
+};
+struct Schedule {
+    Roots R;
+    uint32_t mine;             // frames this rank assembles
+    size_t send_base, own;     // its send area; its own packs' block in the receive area
+    size_t need;               // buffer bytes
+    std::vector<Xfer> ops;
+};
+Schedule schedule(const std::vector<RankLayout>& ranks, uint64_t total, uint32_t rank, uint32_t B, bool rotate) {
+    Schedule S;
+    const uint32_t N = (uint32_t)ranks.size();
+    S.R = Roots{B, rotate ? N : 0u};
+    S.mine = S.R.count(rank);
+    const RankLayout& me = ranks[rank];
+    S.send_base = (size_t)S.mine * total;
+    S.own = (size_t)S.mine * me.off;
+    S.need = S.send_base + (size_t)(B - S.mine) * me.bytes;
+    for (uint32_t q = 0; q < N; ++q) {
+        if (q == rank) continue;
+        if (S.R.count(q) && me.bytes)
+            S.ops.push_back({q, true, S.send_base + (size_t)(S.R.before(q) - (q > rank ? S.mine : 0u)) * me.bytes,
+                             (size_t)S.R.count(q) * me.bytes});
+        if (S.mine && ranks[q].bytes)
+            S.ops.push_back({q, false, (size_t)S.mine * ranks[q].off, (size_t)S.mine * ranks[q].bytes});
+    }
+    return S;
+}
+
+// Pack (every rank), transfer, assemble (each frame's root) `B` frames with plan P.  fail_safe
+// (this rank's own arguments are unusable): only the transfers of the plan, so the other ranks'
+// matching sends and receives complete — no kernel touches the caller's buffers.
+int scene_gather(eray_ctx* ctx, ncclComm_t c, const GatherPlan& P, const Schedule& S, const uint8_t* local,
+                 uint64_t local_stride, uint8_t* frames, uint64_t frame_stride, uint32_t B, bool fail_safe = false) {
     hipStream_t s = (hipStream_t)eray_get_stream(ctx);
     const RankLayout& me = P.ranks[P.rank];
-    uint8_t* mine = P.rank == 0 ? P.buf + (size_t)B * me.off : P.buf;
     hipError_t he;
     if (me.bytes && !fail_safe) {
-        gather_pack_kernel<<<dim3(me.packed_rows, B), 256, 0, s>>>(local, local_stride, mine, me, P.W);
+        gather_pack_kernel<<<dim3(me.packed_rows, B), 256, 0, s>>>(local, local_stride, P.buf + S.send_base,
+                                                                   P.buf + S.own, me, P.W, S.R, P.rank);
         if ((he = hipGetLastError()) != hipSuccess) return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
     }
-    if (P.nranks > 1) {
+    if (!S.ops.empty()) {
         ncclResult_t r = ncclGroupStart();
         if (r != ncclSuccess) return nccl_error(ctx, "ncclGroupStart", r);
-        if (P.rank == 0) {
-            for (uint32_t q = 1; q < P.nranks && r == ncclSuccess; ++q)
-                if (P.ranks[q].bytes)
-                    r = ncclRecv(P.buf + (size_t)B * P.ranks[q].off, (size_t)B * P.ranks[q].bytes, ncclUint8, (int)q, c, s);
-        } else if (me.bytes) {
-            r = ncclSend(mine, (size_t)B * me.bytes, ncclUint8, 0, c, s);
+        for (size_t i = 0; i < S.ops.size() && r == ncclSuccess; ++i) {
+            const Xfer& x = S.ops[i];
+            r = x.send ? ncclSend(P.buf + x.off, x.bytes, ncclUint8, (int)x.peer, c, s)
+                       : ncclRecv(P.buf + x.off, x.bytes, ncclUint8, (int)x.peer, c, s);
         }
         const ncclResult_t r2 = ncclGroupEnd();
         if (r != ncclSuccess) return nccl_error(ctx, "ncclSend/ncclRecv", r);
         if (r2 != ncclSuccess) return nccl_error(ctx, "ncclGroupEnd", r2);
     }
-    if (P.rank == 0 && !fail_safe) {
-        gather_assemble_kernel<<<dim3(P.H, B), 256, 0, s>>>(P.buf, P.d_ranks, B, frames, frame_stride, P.H, P.W, P.band,
-                                                           P.nranks);
+    if (S.mine && !fail_safe) {
+        gather_assemble_kernel<<<dim3(P.H, S.mine), 256, 0, s>>>(P.buf, P.d_ranks, S.mine, frames, frame_stride, P.H, P.W,
+                                                                 P.band, P.nranks);
         if ((he = hipGetLastError()) != hipSuccess) return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
     }
     return ERAY_OK;
@@ -715,8 +773,11 @@ int eray_gather_frames(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uin
                        uint64_t frame_stride, uint32_t nframes, uint32_t height, uint32_t width, uint32_t band_rows,
                        uint32_t flags) {
     if (!ctx || !nccl_comm) return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "gather: null context or comm");
-    if (flags & ~(uint32_t)ERAY_GATHER_SCENE_CAMERA)
+    if (flags & ~(uint32_t)(ERAY_GATHER_SCENE_CAMERA | ERAY_GATHER_ROTATE_ROOT))
         return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "gather: unknown flags");
+    const bool rotate = (flags & ERAY_GATHER_ROTATE_ROOT) != 0;
+    if (rotate && !(flags & ERAY_GATHER_SCENE_CAMERA))
+        return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "gather: rotating roots need ERAY_GATHER_SCENE_CAMERA");
     if (int st = eray_internal_use_device(ctx)) return st;
     ncclComm_t c = (ncclComm_t)nccl_comm;
     int nranks = 0, rank = 0;
@@ -734,11 +795,12 @@ int eray_gather_frames(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uin
         if (nranks > kMaxCodedRanks)
             return eray_internal_error(ctx, ERAY_E_UNSUPPORTED, "scene-camera gather: more than 64 ranks");
         // this rank's verdict on its own arguments and frames
+        const bool assembles = rotate ? (uint32_t)rank < nframes : rank == 0;
         const bool aligned = ((reinterpret_cast<uintptr_t>(local) | local_stride) & 15) == 0 &&
-                             (rank != 0 || ((reinterpret_cast<uintptr_t>(frames) | frame_stride) & 15) == 0);
+                             (!assembles || ((reinterpret_cast<uintptr_t>(frames) | frame_stride) & 15) == 0);
         int status = ERAY_OK;
         eray::gpu::FrameSource src;
-        if (!local || (rank == 0 && !frames) || !aligned)
+        if (!local || (assembles && !frames) || !aligned)
             status = eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT,
                                          "scene-camera gather: null or unaligned (16 B) buffers or strides");
         if (status == ERAY_OK) status = eray_internal_frame_source(ctx, local, local_stride, nframes, &src);
@@ -756,9 +818,10 @@ int eray_gather_frames(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uin
         if (status != ERAY_OK && cached) {
             // the other ranks (same calls, same plan) go ahead with this plan's transfers: take part
             // in them, touch nothing, and report the error
-            const size_t need = rank == 0 ? (size_t)nframes * P->total : (size_t)nframes * P->ranks[(size_t)rank].bytes;
+                const Schedule S = schedule(P->ranks, P->total, (uint32_t)rank, nframes, rotate);
             std::string msg = eray_last_error(ctx);
-            if (grow(ctx, P, need) == ERAY_OK) scene_gather(ctx, c, *P, local, local_stride, frames, frame_stride, nframes, true);
+            if (grow(ctx, P, S.need) == ERAY_OK)
+                scene_gather(ctx, c, *P, S, local, local_stride, frames, frame_stride, nframes, true);
             return eray_internal_error(ctx, status, msg.c_str());
         }
         if (!cached || P->kind != src.kind || P->key != src.key) {  // a new plan: every rank exchanges
@@ -766,9 +829,9 @@ int eray_gather_frames(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uin
             if (status == ERAY_OK) status = eray_internal_source_layout(ctx, src, &L);
             if (int st = exchange_plan(ctx, c, nranks, rank, height, width, band_rows, src, status, L.rects, P)) return st;
         }
-        const size_t need = rank == 0 ? (size_t)nframes * P->total : (size_t)nframes * P->ranks[(size_t)rank].bytes;
-        if (int st = grow(ctx, P, need)) return st;
-        return scene_gather(ctx, c, *P, local, local_stride, frames, frame_stride, nframes);
+        const Schedule S = schedule(P->ranks, P->total, (uint32_t)rank, nframes, rotate);
+        if (int st = grow(ctx, P, S.need)) return st;
+        return scene_gather(ctx, c, *P, S, local, local_stride, frames, frame_stride, nframes);
     }
     for (uint32_t k = 0; k < nframes; ++k)  // one frame at a time through eray_gather_rows
         if (int st = eray_gather_rows(ctx, nccl_comm, local ? local + k * local_stride : nullptr,
@@ -806,14 +869,52 @@ int eray_debug_gather_layout(const int32_t* rects, uint32_t n, uint32_t height, 
     return ERAY_OK;
 }
 
-// Diagnostics (tests): the scene-camera gather of N ranks simulated on one GPU.  The context has
+// Diagnostics (tests, host only): rank `rank`'s schedule for a batch of `nframes` frames when the
+// ranks' packs are rank_bytes[q] bytes per frame (rank order = receive-area order) — what
+// eray_gather_frames' pack kernel and point-to-point transfers do.  out (u64): buffer bytes,
+// frames this rank assembles, number of transfers; then per frame k its pack's offset in the
+// buffer; then per rank q where q's packs of this rank's frames start (frame j: + j * bytes_q);
+// then per transfer: peer, 1 = send / 0 = receive, offset, bytes.
+int eray_debug_gather_schedule(const uint32_t* rank_bytes, uint32_t nranks, uint32_t rank, uint32_t nframes,
+                               uint32_t rotate, uint64_t* out, uint32_t cap) {
+    if (!rank_bytes || !out || !nranks || nranks > (uint32_t)kMaxCodedRanks || rank >= nranks ||
+        cap < 3u + nframes + nranks + 8u * nranks)
+        return eray_internal_error(nullptr, ERAY_E_INVALID_ARGUMENT, "gather schedule: bad arguments");
+    std::vector<RankLayout> ranks(nranks, RankLayout{});
+    uint64_t total = 0;
+    for (uint32_t q = 0; q < nranks; ++q) {
+        ranks[q].bytes = rank_bytes[q];
+        ranks[q].off = total;
+        total += rank_bytes[q];
+    }
+    const Schedule S = schedule(ranks, total, rank, nframes, rotate != 0);
+    const uint64_t bytes = rank_bytes[rank];
+    out[0] = S.need;
+    out[1] = S.mine;
+    out[2] = S.ops.size();
+    for (uint32_t k = 0; k < nframes; ++k)
+        out[3 + k] = S.R.root(k) == rank ? S.own + S.R.index(k) * bytes : S.send_base + S.R.send_slot(k, rank) * bytes;
+    for (uint32_t q = 0; q < nranks; ++q) out[3 + nframes + q] = (uint64_t)S.mine * ranks[q].off;
+    for (size_t i = 0; i < S.ops.size(); ++i) {
+        uint64_t* o = out + 3 + nframes + nranks + 4 * i;
+        o[0] = S.ops[i].peer;
+        o[1] = S.ops[i].send ? 1u : 0u;
+        o[2] = S.ops[i].off;
+        o[3] = S.ops[i].bytes;
+    }
+    return ERAY_OK;
+}
+
+// Diagnostics (tests): the scene-camera gather of a batch of `nframes` frames by N ranks,
+// simulated on one GPU with the real pack and assembly kernels and each rank's schedule (its
+// point-to-point transfers as device copies between the ranks' buffers).  The context has
 // rendered the scene camera's whole frame (its setup's rectangles stand for every rank's);
-// staging holds the N ranks' padded local PPM blocks (rows_max = rank 0's rows, band_rows > 0:
-// bands, 0: blocks); each is packed with its rank's layout into one receive buffer, which is
-// assembled into frame.
-int eray_debug_scene_gather(eray_ctx* ctx, const uint8_t* staging, uint8_t* frame, uint32_t height, uint32_t width,
-                            uint32_t band_rows, uint32_t nranks) {
-    if (!ctx || !staging || !frame || !nranks || nranks > (uint32_t)kMaxCodedRanks || width % 16 ||
+// staging holds frame k of rank q's padded local PPM block at (k * N + q) * rows_max rows
+// (rows_max = rank 0's rows; band_rows > 0: bands, 0: blocks).  Root r's assembled frames land at
+// frames + (frames of roots below r + j) * H W 3 — in batch order unless `rotate`.
+int eray_debug_scene_gather_batch(eray_ctx* ctx, const uint8_t* staging, uint8_t* frames, uint32_t nframes,
+                                  uint32_t height, uint32_t width, uint32_t band_rows, uint32_t nranks, uint32_t rotate) {
+    if (!ctx || !staging || !frames || !nframes || !nranks || nranks > (uint32_t)kMaxCodedRanks || width % 16 ||
         (band_rows && (band_rows < 4 || (band_rows & (band_rows - 1)))) || (!band_rows && height % nranks))
         return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "scene gather: bad arguments");
     eray::gpu::FrameSource src;
@@ -838,21 +939,46 @@ int eray_debug_scene_gather(eray_ctx* ctx, const uint8_t* staging, uint8_t* fram
         P.total += R.bytes;
         P.ranks.push_back(R);
     }
+    std::vector<Schedule> S;
+    std::vector<size_t> base;  // rank q's buffer inside P.buf
+    size_t all = 0;
+    for (uint32_t q = 0; q < nranks; ++q) {
+        S.push_back(schedule(P.ranks, P.total, q, nframes, rotate != 0));
+        base.push_back(all);
+        all += (S.back().need + 255) & ~(size_t)255;
+    }
+    const size_t block = (size_t)rows_max * width * 3u, frame_bytes = (size_t)height * width * 3u;
     hipStream_t s = (hipStream_t)eray_get_stream(ctx);
     hipError_t he = hipMalloc((void**)&P.d_ranks, sizeof(RankLayout) * nranks);
-    if (he == hipSuccess) he = hipMalloc((void**)&P.buf, std::max<size_t>(P.total, 256));
+    if (he == hipSuccess) he = hipMalloc((void**)&P.buf, std::max<size_t>(all, 256));
     if (he == hipSuccess)
         he = hipMemcpyAsync(P.d_ranks, P.ranks.data(), sizeof(RankLayout) * nranks, hipMemcpyHostToDevice, s);
-    for (uint32_t q = 0; q < nranks && he == hipSuccess; ++q) {
+    for (uint32_t q = 0; q < nranks && he == hipSuccess; ++q) {  // every rank packs its frames
         const RankLayout& R = P.ranks[q];
         if (!R.bytes) continue;
-        gather_pack_kernel<<<dim3(R.packed_rows, 1), 256, 0, s>>>(staging + (size_t)q * rows_max * width * 3u, 0,
-                                                                  P.buf + R.off, R, width);
+        gather_pack_kernel<<<dim3(R.packed_rows, nframes), 256, 0, s>>>(staging + q * block, nranks * block,
+                                                                        P.buf + base[q] + S[q].send_base,
+                                                                        P.buf + base[q] + S[q].own, R, width, S[q].R, q);
         he = hipGetLastError();
     }
-    if (he == hipSuccess) {
-        gather_assemble_kernel<<<dim3(height, 1), 256, 0, s>>>(P.buf, P.d_ranks, 1, frame, 0, height, width, band_rows,
-                                                              nranks);
+    for (uint32_t q = 0; q < nranks && he == hipSuccess; ++q)  // each send meets its peer's receive
+        for (const Xfer& x : S[q].ops) {
+            if (!x.send) continue;
+            const Xfer* m = nullptr;
+            for (const Xfer& y : S[x.peer].ops)
+                if (!y.send && y.peer == q) m = &y;
+            if (!m || m->bytes != x.bytes) {
+                he = hipErrorInvalidValue;
+                break;
+            }
+            he = hipMemcpyAsync(P.buf + base[x.peer] + m->off, P.buf + base[q] + x.off, x.bytes, hipMemcpyDeviceToDevice, s);
+            if (he != hipSuccess) break;
+        }
+    for (uint32_t r = 0; r < nranks && he == hipSuccess; ++r) {  // every root assembles its frames
+        if (!S[r].mine) continue;
+        gather_assemble_kernel<<<dim3(height, S[r].mine), 256, 0, s>>>(P.buf + base[r], P.d_ranks, S[r].mine,
+                                                                       frames + S[r].R.before(r) * frame_bytes,
+                                                                       frame_bytes, height, width, band_rows, nranks);
         he = hipGetLastError();
     }
     if (he == hipSuccess) he = hipStreamSynchronize(s);
@@ -862,6 +988,12 @@ int eray_debug_scene_gather(eray_ctx* ctx, const uint8_t* staging, uint8_t* fram
     P.buf = nullptr;
     P.xchg = nullptr;
     return he == hipSuccess ? ERAY_OK : eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+}
+
+// One frame of eray_debug_scene_gather_batch (staging: the N ranks' blocks; frame: rank 0's).
+int eray_debug_scene_gather(eray_ctx* ctx, const uint8_t* staging, uint8_t* frame, uint32_t height, uint32_t width,
+                            uint32_t band_rows, uint32_t nranks) {
+    return eray_debug_scene_gather_batch(ctx, staging, frame, 1, height, width, band_rows, nranks, 0);
 }
 
 }  // extern "C"

@@ -379,9 +379,16 @@ int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8
  *     ranks exchange their rectangles once per camera setup (the first call after a new setup
  *     synchronises the context's stream; a batch size's first call allocates); every later call
  *     only enqueues kernels and transfers — no host round trip, capturable in a HIP graph.
- *     Needs width % 16 == 0 and 16-byte aligned buffers and strides (else per-frame gathers). */
+ *     Needs width % 16 == 0 and 16-byte aligned buffers and strides (else ERAY_E_INVALID_ARGUMENT
+ *     on every rank).
+ *   ERAY_GATHER_ROTATE_ROOT   — with ERAY_GATHER_SCENE_CAMERA: frame k of the batch is assembled
+ *     on rank k % nranks instead of rank 0, so the assembly writes and the inbound xGMI traffic of
+ *     a stream of frames spread over every GPU.  Rank r's frames k = r, r + nranks, ... land at
+ *     frames + j * frame_stride, j = (k - r) / nranks (every rank with r < nframes passes
+ *     `frames`).  Each frame is still one complete PPM body on one GPU. */
 #define ERAY_GATHER_DEFAULT 0u
 #define ERAY_GATHER_SCENE_CAMERA 1u
+#define ERAY_GATHER_ROTATE_ROOT 2u
 int eray_gather_frames(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint64_t local_stride, uint8_t* frames,
                        uint64_t frame_stride, uint32_t nframes, uint32_t height, uint32_t width, uint32_t band_rows,
                        uint32_t flags);

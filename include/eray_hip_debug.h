@@ -41,6 +41,17 @@ int eray_debug_coded_unband(eray_ctx* ctx, const uint8_t* staging, uint8_t* fram
                             uint32_t band_rows, uint32_t nranks);
 int eray_debug_scene_gather(eray_ctx* ctx, const uint8_t* staging, uint8_t* frame, uint32_t height, uint32_t width,
                             uint32_t band_rows, uint32_t nranks);
+/* A batch of nframes frames (frame k of rank q at staging block k * nranks + q) with every rank's
+ * transfer schedule played as device copies; rotate: ERAY_GATHER_ROTATE_ROOT's roots.  Root r's
+ * frames land at frames + (frames of roots below r + j) * height * width * 3. */
+int eray_debug_scene_gather_batch(eray_ctx* ctx, const uint8_t* staging, uint8_t* frames, uint32_t nframes,
+                                  uint32_t height, uint32_t width, uint32_t band_rows, uint32_t nranks, uint32_t rotate);
+/* Host only: rank `rank`'s part of a batch's scene-camera gather when rank q packs rank_bytes[q]
+ * bytes per frame.  out (u64, cap >= 3 + nframes + 9 nranks): buffer bytes, frames it assembles,
+ * transfer count; per frame its pack's offset in the buffer; per rank q the receive offset of q's
+ * packs; per transfer peer, 1 send / 0 receive, offset, bytes. */
+int eray_debug_gather_schedule(const uint32_t* rank_bytes, uint32_t nranks, uint32_t rank, uint32_t nframes,
+                               uint32_t rotate, uint64_t* out, uint32_t cap);
 /* Host only (no context, no GPU): rank `rank`'s share of the scene-camera gather of `nranks` ranks
  * for objects whose pixel rectangles are `rects` (n x (x0, x1, y0, y1), camera rows) — its rows, its
  * rectangles in local rows / 16-pixel column groups, each one's offset in its per-frame pack.  out:

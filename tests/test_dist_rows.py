@@ -179,3 +179,89 @@ def test_two_rank_scene_camera_gather_layout(tmp_path, bands):
     want = _render_block(0, 2 * ROWS)
     assert (want != BG).any(axis=2).any()
     assert got.shape == want.shape and np.array_equal(got, want)
+
+
+def _rotating_gather_worker(rank, world, port, out_dir, bands, B, rotate):
+    """Every rank packs B different frames (frame k: the rendered rows shifted by 37 k) where the
+    library's schedule puts them, runs the schedule's point-to-point transfers over gloo, and
+    assembles the frames it roots from its receive area."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from eray_amd import capi
+    from eray_amd.dist import band_camera_rows, band_split
+
+    H = world * ROWS
+    rects = _rects_of(_render_block(0, H))
+    lay = capi.gather_layout(rects, H, W, bands, world, rank)
+    sp = band_split(rank, world, H, bands)
+    local = np.zeros((sp["alloc_rows"], W, 3), np.uint8)
+    local[: sp["rows"]] = _render_rows(band_camera_rows(rank, world, H, bands))
+    lays = [None] * world
+    dist.all_gather_object(lays, lay)
+    sched = capi.gather_schedule([l["bytes"] for l in lays], rank, B, rotate)
+    buf = np.zeros(max(sched["need"], 1), np.uint8)
+    for k in range(B):
+        at = sched["pack"][k]
+        buf[at:at + lay["bytes"]] = _pack((local.astype(np.int32) + 37 * k).astype(np.uint8), lay, W)
+    t = torch.from_numpy(buf)
+    reqs = [(dist.isend if op["send"] else dist.irecv)(t[op["off"]:op["off"] + op["bytes"]], int(op["peer"]))
+            for op in sched["ops"]]
+    for q in reqs:
+        q.wait()
+    for j in range(sched["mine"]):
+        packs = [buf[sched["recv"][q] + j * lays[q]["bytes"]:][:lays[q]["bytes"]] for q in range(world)]
+        np.save(os.path.join(out_dir, f"r{rank}_f{j}.npy"), _assemble(packs, lays, H, W, bands, world))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("B,rotate", [(3, True), (4, True), (3, False)])
+def test_two_rank_gather_schedule_rotating_roots(tmp_path, B, rotate):
+    """eray_gather_frames' batch schedule (the library's own: eray_debug_gather_schedule — pack
+    offsets, receive areas, point-to-point transfers) across two gloo ranks: with
+    ERAY_GATHER_ROTATE_ROOT frame k is assembled on rank k % 2 as its (k // 2)-th frame, else
+    every frame on rank 0; each equals the frame restated from the ranks' packs in one process."""
+    world, bands = 2, 4
+    mp.start_processes(_rotating_gather_worker, args=(world, _free_port(), str(tmp_path), bands, B, rotate),
+                       nprocs=world, join=True, start_method="spawn")
+    from eray_amd import capi
+    from eray_amd.dist import band_camera_rows, band_split
+    H = world * ROWS
+    full = _render_block(0, H)
+    lays = [capi.gather_layout(_rects_of(full), H, W, bands, world, q) for q in range(world)]
+    locals_ = []
+    for q in range(world):
+        sp = band_split(q, world, H, bands)
+        loc = np.zeros((sp["alloc_rows"], W, 3), np.uint8)
+        loc[: sp["rows"]] = _render_rows(band_camera_rows(q, world, H, bands))
+        locals_.append(loc)
+    for k in range(B):
+        root, j = (k % world, k // world) if rotate else (0, k)
+        got = np.load(str(tmp_path / f"r{root}_f{j}.npy"))
+        packs = [_pack((locals_[q].astype(np.int32) + 37 * k).astype(np.uint8), lays[q], W) for q in range(world)]
+        assert np.array_equal(got, _assemble(packs, lays, H, W, bands, world)), k
+    assert np.array_equal(np.load(str(tmp_path / "r0_f0.npy")), full)
+
+
+def test_gather_schedules_pair_up():
+    """Host-only check of every rank's schedule for N = 1..8 ranks and batches of 1..12 frames:
+    each send meets one receive of the same size from its peer, the packs of a rank's frames do
+    not overlap and fit its buffer, and each rank roots the frames its rotation gives it."""
+    from eray_amd import capi
+    rng = np.random.default_rng(3)
+    for N in range(1, 9):
+        for B in (1, 2, 3, 7, 8, 12):
+            for rotate in (False, True):
+                nb = [int(48 * rng.integers(0, 40)) for _ in range(N)]
+                S = [capi.gather_schedule(nb, r, B, rotate) for r in range(N)]
+                for r in range(N):
+                    assert S[r]["mine"] == (len(range(r, B, N)) if rotate else (B if r == 0 else 0))
+                    spans = sorted((S[r]["pack"][k], S[r]["pack"][k] + nb[r]) for k in range(B))
+                    assert all(a[1] <= b[0] for a, b in zip(spans, spans[1:])) and (not spans or spans[-1][1] <= S[r]["need"])
+                    for op in S[r]["ops"]:
+                        assert op["off"] + op["bytes"] <= S[r]["need"]
+                        if op["send"]:
+                            m = [o for o in S[op["peer"]]["ops"] if not o["send"] and o["peer"] == r]
+                            assert len(m) == 1 and m[0]["bytes"] == op["bytes"], (N, B, rotate, r, op)
+                    sends = sum(op["bytes"] for op in S[r]["ops"] if op["send"])
+                    assert sends == nb[r] * (B - S[r]["mine"]) or nb[r] == 0

@@ -156,6 +156,46 @@ def test_scene_camera_gather_layout(gpu, cube, standin70k_gather, mesh):
         sc.close()
 
 
+def test_scene_camera_gather_batch_rotating_roots(gpu, cube):
+    """A batch of B different frames through N simulated ranks (real pack and assembly kernels,
+    each rank's transfer schedule played as device copies): with rank 0 assembling every frame and
+    with ERAY_GATHER_ROTATE_ROOT (frame k on rank k % N, root r's frames contiguous in root
+    order), every assembled frame is the frame the ranks rendered — the same bytes either way."""
+    W, H = 320, 180
+    sc = MainScene(gpu, *cube, W, H, texture=64, fov=(16.0, 9.0))
+    ppm = gpu.empty((H, W, 3), np.uint8)
+    try:
+        gpu.render(W, H, out_ppm=ppm.ptr)
+        base = ppm.numpy()
+        for world, B, band in ((1, 3, 4), (2, 5, 4), (3, 7, 8), (4, 4, 4), (8, 11, 4), (8, 3, 4), (5, 9, 0)):
+            if not band and H % world:
+                continue
+            # frame k: the rendered frame with every byte shifted by 37 k (inside the rectangles
+            # only those bytes travel; outside, the assembly writes the miss colour)
+            fr = [(base.astype(np.int32) + 37 * k).astype(np.uint8) for k in range(B)]
+            blocks = np.stack([_blocks_of(f, H, W, band, world) for f in fr])  # [k][q] rows
+            staging = gpu.to_device(np.ascontiguousarray(blocks))
+            out = gpu.empty((B, H, W, 3), np.uint8)
+            try:
+                got = {}
+                for rotate in (0, 1):
+                    gpu.memset(out.ptr, 0, out.nbytes)
+                    assert capi.lib().eray_debug_scene_gather_batch(gpu.handle, staging.ptr, out.ptr, B, H, W, band,
+                                                                    world, rotate) == 0
+                    got[rotate] = out.numpy()
+                assert np.array_equal(got[0][0], base), (world, B, band)
+                order = [k for r in range(world) for k in range(r, B, world)]  # root-grouped batch order
+                for pos, k in enumerate(order):
+                    assert np.array_equal(got[1][pos], got[0][k]), (world, B, band, k)
+                assert not np.array_equal(got[0][0], got[0][B - 1])
+            finally:
+                staging.free()
+                out.free()
+    finally:
+        ppm.free()
+        sc.close()
+
+
 def test_one_rank_gather_frames_and_graph_capture(cube):
     """eray_gather_frames on a one-rank communicator: a ring of rendered frames, gathered per
     frame (coded path) and scene-camera style, then the scene-camera gather captured in a HIP
@@ -179,11 +219,14 @@ def test_one_rank_gather_frames_and_graph_capture(cube):
         assert (want[0] != np.array([25, 25, 51], np.uint8)).any()
         comm = gpu.comm_init(1, 0, capi.comm_unique_id())
         slot = H * W * 3
-        for scene_camera in (False, True):
+        for scene_camera, rotate in ((False, False), (True, False), (True, True)):
             gpu.memset(frames.ptr, 0, frames.nbytes)
-            gpu.gather_frames(comm, local.ptr, slot, frames.ptr, slot, S, H, W, scene_camera=scene_camera)
+            gpu.gather_frames(comm, local.ptr, slot, frames.ptr, slot, S, H, W, scene_camera=scene_camera,
+                              rotate_root=rotate)
             gpu.synchronize()
-            assert np.array_equal(frames.numpy(), want), scene_camera
+            assert np.array_equal(frames.numpy(), want), (scene_camera, rotate)
+        with pytest.raises(capi.ErayError):  # rotating roots are a scene-camera transport
+            gpu.gather_frames(comm, local.ptr, slot, frames.ptr, slot, S, H, W, rotate_root=True)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=st):
             gpu.gather_frames(comm, local.ptr, slot, frames.ptr, slot, S, H, W, scene_camera=True)
