@@ -672,11 +672,12 @@ def main() -> None:
     # dispatch's own start / end timestamps (eray_time_frames_ring); the same frames graph-replayed
     # between two events (launch gaps included); the latency of one frame alone per launch
     ring1 = ring_args() if world == 1 else ring_args(0, G)
+    n_kt = max(n_timed, 256) // F * F  # dispatch-timed frames: 32 launches of 8 at C2
     with MARK.range(f"timed_F{F}"):
-        kt = ctx.time_frames(max(args.steps, 64) // F * F, width, H, **ring1)
+        kt = ctx.time_frames(n_kt, width, H, **ring1)
     kernel_ms = kt["frame_kernel_ms"] / F  # per frame
     with MARK.range(f"replay_F{F}"):  # the same frames graph-replayed, bracketed by two events
-        replay_ms = ctx.render_frames(max(args.steps // F, 1) * F, width, H, timed=True, **ring1)
+        replay_ms = ctx.render_frames(max(n_timed // F, 1) * F, width, H, timed=True, **ring1)
     latency = None
     fill_floor = None
     beyond = None
@@ -688,7 +689,7 @@ def main() -> None:
         if world == 1:  # the same frames with no object: the fill alone, this kernel's write floor
             empty = empty_scene_context(device, width, H, frame_camera_fov(width, H), stream)
             with MARK.range(f"fill_floor_F{F}"):
-                ft = empty.time_frames(max(args.steps, 64) // F * F, width, H, **ring1)
+                ft = empty.time_frames(n_kt, width, H, **ring1)
             fill_floor = {"frame_kernel_ms_per_launch": round(ft["frame_kernel_ms"], 6),
                           "frames_per_launch": ft["frames_per_launch"],
                           "achieved_gbs": round(15 * width * rows * ft["frames_per_launch"] / (ft["frame_kernel_ms"] * 1e-3)
@@ -707,9 +708,9 @@ def main() -> None:
                            ring=capi.frame_ring(big, alloc_rows, width, F), **band_args)
                 ctx.render_frames(big, width, H, **bkw)  # (the slots' pages touched once)
                 with MARK.range(f"beyond_mall_timed_F{F}"):
-                    bt = ctx.time_frames(max(args.steps, 64) // F * F, width, H, **bkw)
+                    bt = ctx.time_frames(n_kt, width, H, **bkw)
                 with MARK.range(f"beyond_mall_fill_floor_F{F}"):
-                    bft = empty.time_frames(max(args.steps, 64) // F * F, width, H, **bkw)
+                    bft = empty.time_frames(n_kt, width, H, **bkw)
                 del brgb, bppm
                 b_ms = bt["frame_kernel_ms"]
                 b_gbs = algorithmic_bytes(width * rows, hits, hit_faces) * F / (b_ms * 1e-3) / 1e9
