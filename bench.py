@@ -46,7 +46,7 @@ import torch  # noqa: E402  (imported before the HIP library: one HIP runtime pe
 import torch.distributed as dist  # noqa: E402
 
 from eray_amd import capi  # noqa: E402
-from eray_amd.dist import BAND_ROWS, RowGather, band_split, gather_ppm_rows, row_block  # noqa: E402
+from eray_amd.dist import BAND_ROWS, RowGather, band_split, frames_assembled, gather_ppm_rows, row_block  # noqa: E402
 from eray_amd.frame import MainScene  # noqa: E402
 from eray_amd.objfile import load_obj_file  # noqa: E402
 
@@ -597,7 +597,7 @@ def main() -> None:
     if world > 1:
         rotate = args.gather_root == "rotate" and args.gather == "scene" and not rehearsal
         # the frames this rank assembles per batch: k = rank, rank + N, ... (rotating roots) or all on rank 0
-        n_out = (G - rank + world - 1) // world if rotate else (G if rank == 0 else 0)
+        n_out = frames_assembled(G, world, rank, rotate)
         frames_out = torch.empty((n_out, H, width, 3), dtype=torch.uint8, device="cuda") if n_out else None
         gstream = torch.cuda.Stream()
         if not rehearsal:
@@ -672,7 +672,7 @@ def main() -> None:
     # dispatch's own start / end timestamps (eray_time_frames_ring); the same frames graph-replayed
     # between two events (launch gaps included); the latency of one frame alone per launch
     ring1 = ring_args() if world == 1 else ring_args(0, G)
-    n_kt = max(n_timed, 256) // F * F  # dispatch-timed frames: 32 launches of 8 at C2
+    n_kt = max(64, F) // F * F  # dispatch-timed frames: 8 launches of 8 at C2
     with MARK.range(f"timed_F{F}"):
         kt = ctx.time_frames(n_kt, width, H, **ring1)
     kernel_ms = kt["frame_kernel_ms"] / F  # per frame

@@ -50,6 +50,15 @@ def band_split(rank: int, world: int, height: int, band: int = BAND_ROWS) -> dic
     return dict(row0=rank * band, rows=rows, band_rows=band, band_stride=world * band, alloc_rows=rows0)
 
 
+def frames_assembled(batch: int, world: int, rank: int, rotate: bool) -> int:
+    """Frames of a batch of `batch` that `rank` assembles in eray_gather_frames' scene-camera
+    gather: every frame on rank 0, or (ERAY_GATHER_ROTATE_ROOT) frames k = rank, rank + world, ...
+    — the size of the frames buffer that rank passes."""
+    if not rotate:
+        return batch if rank == 0 else 0
+    return max(0, (batch - rank + world - 1) // world)
+
+
 def band_camera_rows(rank: int, world: int, height: int, band: int = BAND_ROWS) -> list[int]:
     """The camera rows of rank's local rows, in order (tests)."""
     sp = band_split(rank, world, height, band)

@@ -265,3 +265,16 @@ def test_gather_schedules_pair_up():
                             assert len(m) == 1 and m[0]["bytes"] == op["bytes"], (N, B, rotate, r, op)
                     sends = sum(op["bytes"] for op in S[r]["ops"] if op["send"])
                     assert sends == nb[r] * (B - S[r]["mine"]) or nb[r] == 0
+
+
+def test_bench_frames_buffers_match_the_schedule():
+    """bench.py sizes each rank's assembled-frames buffer with dist.frames_assembled; it must be
+    what the library's schedule has the rank assemble (eray_debug_gather_schedule), for both
+    root choices."""
+    from eray_amd import capi
+    from eray_amd.dist import frames_assembled
+    for N in range(1, 9):
+        for B in (1, 3, 8, 16, 32):
+            for rotate in (False, True):
+                for r in range(N):
+                    assert frames_assembled(B, N, r, rotate) == capi.gather_schedule([48] * N, r, B, rotate)["mine"]
