@@ -367,8 +367,8 @@ int eray_comm_destroy(void* nccl_comm);
 int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8_t* frame, uint32_t height,
                      uint32_t width, uint32_t band_rows);
 /* `nframes` frames at once (frame k: local + k * local_stride on every rank, frames + k *
- * frame_stride on rank 0), e.g. a ring of eray_render_frames_ring slots gathered while the next
- * frames render on another stream.  flags:
+ * frame_stride on rank 0, or on its root with ERAY_GATHER_ROTATE_ROOT), e.g. a ring of
+ * eray_render_frames_ring slots gathered while the next frames render on another stream.  flags:
  *   ERAY_GATHER_DEFAULT       — eray_gather_rows per frame.
  *   ERAY_GATHER_SCENE_CAMERA  — the local rows are this context's renders of its scene camera
  *     (eray_render / eray_render_frames[_ring] without anti-aliasing or bounces, over this rank's
