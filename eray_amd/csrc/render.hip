@@ -850,6 +850,13 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
     // coop (workgroup-uniform): the workgroup's four sub-blocks share their large objects' work —
     // binned chunks dealt over the waves, shadow rays through shared LDS tiles — with barriers;
     // otherwise (light sub-blocks) every wave searches its own bins and shadow rays alone
+    // Culled large-mesh builds (screen bins): every sub-block is searched by its own wave
+    // (first_hit_binned_wave handles bins of any length), the cooperative paths are compiled out —
+    // 139 instead of 161 VGPRs and 1.5-2.7 % faster frames at 3840x2160 / 70k, C3, C5 and moving
+    // cameras, where switching them off at run time gained nothing (profiles/r04/ab/ab_r04am.txt,
+    // ab_r04an.txt).  A large object without bins (a bin-capacity overflow's fallback frame) is
+    // then scanned by each wave alone; brute-force builds (!kCull) keep the LDS tiles.
+    if constexpr (kCull && kLdsTiles) coop = false;
     constexpr bool kSpecPow = (kMat & kMatSpecPow) != 0, kExample = (kMat & kMatExample) != 0;
     // candidates tested together by the per-wave scans (small objects, shadow rays): four for ILP,
     // one in the large-mesh builds, whose registers bound their resident waves
@@ -1431,7 +1438,8 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
                         nx_range = true;
                     };
                     // the ordered detail list's heavy sub-blocks (bins of several chunks) come
-                    // first: an iteration meeting one shares the work across the workgroup
+                    // first, so the longest chains start in the first round (coop: shared by the
+                    // workgroup in builds that keep the cooperative paths, render_sub)
                     render_sub<kCull, kLdsTiles, kMat>(p, fo, cam, rm, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH,
                                                        active, s_hot, s_cull, s_bins, s_rgb, s_ppm, aligned,
                                                        (kGivenRay && r == 0) ? &d0 : nullptr, coop,
