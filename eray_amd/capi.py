@@ -204,6 +204,10 @@ DEBUG_SIGNATURES = {
     "eray_debug_gather_layout": (C.c_int, [C.POINTER(C.c_int32), _U, _U, _U, _U, _U, _U, C.POINTER(C.c_uint32)]),
     "eray_debug_scene_gather_batch": (C.c_int, [_P, _P, _P, _U, _U, _U, _U, _U, _U]),
     "eray_debug_gather_schedule": (C.c_int, [C.POINTER(C.c_uint32), _U, _U, _U, _U, C.POINTER(C.c_uint64), _U]),
+    "eray_debug_gather_write_headers": (C.c_int, [C.POINTER(C.c_uint32), _U, _U, _U, _U, C.c_int32, _U, C.c_uint64,
+                                                  _P]),
+    "eray_debug_gather_check": (C.c_int, [C.POINTER(C.c_uint32), _U, _U, _U, _U, _U, C.c_uint64, _P]),
+    "eray_debug_plan_verdict": (C.c_int, [C.POINTER(C.c_int32), _U, _U]),
 }
 
 _lib = None
@@ -309,14 +313,46 @@ def gather_schedule(rank_bytes, rank: int, nframes: int, rotate: bool) -> dict:
     buffer size, how many frames it assembles, each frame's pack offset, where each rank's packs
     start in its receive area, and its point-to-point transfers (peer, send, offset, bytes)."""
     n = len(rank_bytes)
-    cap = 3 + nframes + 9 * n
+    cap = 5 + nframes + 12 * n
     rb = (C.c_uint32 * n)(*[int(b) for b in rank_bytes])
     out = (C.c_uint64 * cap)()
     check(lib().eray_debug_gather_schedule(rb, n, rank, nframes, int(bool(rotate)), out, cap))
     v = list(out)
     k = 3 + nframes + n
     ops = [dict(zip(("peer", "send", "off", "bytes"), v[k + 4 * i: k + 4 * i + 4])) for i in range(v[2])]
-    return {"need": v[0], "mine": v[1], "pack": v[3:3 + nframes], "recv": v[3 + nframes:k], "ops": ops}
+    h = k + 4 * v[2]
+    hdrs = v[h + 1:h + 1 + v[h]]
+    peer_hdr = [None if x == 2 ** 64 - 1 else x for x in v[h + 1 + v[h]:h + 1 + v[h] + n]]
+    return {"need": v[0], "mine": v[1], "pack": v[3:3 + nframes], "recv": v[3 + nframes:k], "ops": ops,
+            "headers": hdrs, "peer_headers": peer_hdr}
+
+
+def gather_write_headers(rank_bytes, rank: int, nframes: int, rotate: bool, buf: np.ndarray, status: int = 0,
+                         kind: int = 1, key: int = 0) -> None:
+    """Writes `rank`'s transfer headers (its verdict and its frames' source) into the host copy
+    `buf` of its gather buffer (eray_debug_gather_write_headers, host only)."""
+    n = len(rank_bytes)
+    rb = (C.c_uint32 * n)(*[int(b) for b in rank_bytes])
+    assert buf.dtype == np.uint8 and buf.flags.c_contiguous
+    check(lib().eray_debug_gather_write_headers(rb, n, rank, nframes, int(bool(rotate)), status, kind, key,
+                                                buf.ctypes.data))
+
+
+def gather_check(rank_bytes, rank: int, nframes: int, rotate: bool, buf: np.ndarray, kind: int = 1,
+                 key: int = 0) -> int:
+    """A root's verdict on its received batch (the assembly's header check, eray_debug_gather_check,
+    host only): E_OK or the error status; raises nothing."""
+    n = len(rank_bytes)
+    rb = (C.c_uint32 * n)(*[int(b) for b in rank_bytes])
+    return lib().eray_debug_gather_check(rb, n, rank, nframes, int(bool(rotate)), kind, key, buf.ctypes.data)
+
+
+def plan_verdict(records, rank: int) -> int:
+    """A new gather plan's verdict on `rank` (exchange_plan's, eray_debug_plan_verdict, host only)
+    from every rank's (status, kind, key low, key high): E_OK or the error status."""
+    flat = [int(x) for r in records for x in r]
+    arr = (C.c_int32 * len(flat))(*flat)
+    return lib().eray_debug_plan_verdict(arr, len(records), rank)
 
 
 def comm_destroy(comm: int) -> None:

@@ -149,6 +149,8 @@ struct eray_ctx {
     int32_t* d_union_host = nullptr;  // h_union's device address (mapped)
     uint64_t union_seq[4] = {0, 0, 0, 0};
     FrameSource union_src[4];
+    uint32_t union_nobj[4] = {0, 0, 0, 0};  // objects and scene generation the entry's union covers
+    uint64_t union_gen[4] = {0, 0, 0, 0};
     hipEvent_t union_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // eray_gather_frames' plan (comm.cpp owns it)
     void* gather_plan = nullptr;
@@ -477,17 +479,25 @@ FrameSource scene_source(const eray_ctx* ctx, uint32_t W, uint32_t H, const RowS
     return s;
 }
 
-// Records `s` as the source of the n PPM slots ppm + k * stride (k < n).
+// A tagged slot's PPM bytes: [ppm, ppm + rows * W * 3).
+uintptr_t tag_end(const eray_ctx::SlotTag& t) { return t.ppm + (uintptr_t)t.src.rows * t.src.W * 3u; }
+// Forgets the source of every tagged slot whose bytes meet [a, a + bytes): memory written (or
+// freed) by anything but a render of that source no longer holds its frame.
+void untag_range(eray_ctx* ctx, uintptr_t a, size_t bytes) {
+    if (!bytes) return;
+    auto& v = ctx->slot_tags;
+    v.erase(std::remove_if(v.begin(), v.end(),
+                           [&](const eray_ctx::SlotTag& t) { return t.ppm < a + bytes && a < std::max(tag_end(t), t.ppm + 1); }),
+            v.end());
+}
+// Records `s` as the source of the n PPM slots ppm + k * stride (k < n); any other tag whose
+// bytes the new frames overwrite is dropped.
 void tag_frames(eray_ctx* ctx, const uint8_t* ppm, uint64_t stride, uint32_t n, const FrameSource& s) {
     if (!ppm) return;
     auto& v = ctx->slot_tags;
     for (uint32_t k = 0; k < n; ++k) {
         const uintptr_t a = reinterpret_cast<uintptr_t>(ppm) + (uintptr_t)(k * stride);
-        for (size_t i = 0; i < v.size(); ++i)
-            if (v[i].ppm == a) {
-                v.erase(v.begin() + (std::ptrdiff_t)i);
-                break;
-            }
+        untag_range(ctx, a, std::max<size_t>((size_t)s.rows * s.W * 3u, 1));
         if (v.size() >= kMaxTags) v.erase(v.begin());
         v.push_back({a, s});
     }
@@ -891,6 +901,10 @@ int eray_device_alloc(eray_ctx* ctx, size_t bytes, void** dev_ptr) {
 int eray_device_free(eray_ctx* ctx, void* dev_ptr) {
     if (int st = use_device(ctx)) return st;
     if (!dev_ptr) return ERAY_OK;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, dev_ptr) == hipSuccess)  // (frames in it lose their source)
+        untag_range(ctx, reinterpret_cast<uintptr_t>(base), size);
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     HIP_TRY(ctx, hipFree(dev_ptr));
     return ERAY_OK;
@@ -900,6 +914,7 @@ int eray_memset(eray_ctx* ctx, void* dev_ptr, int value, size_t bytes) {
     if (int st = use_device(ctx)) return st;
     if (!bytes) return ERAY_OK;
     if (!dev_ptr) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "dev_ptr is null");
+    untag_range(ctx, reinterpret_cast<uintptr_t>(dev_ptr), bytes);
     HIP_TRY(ctx, hipMemsetAsync(dev_ptr, value, bytes, ctx->stream));
     return ERAY_OK;
 }
@@ -908,6 +923,7 @@ int eray_copy_to_device(eray_ctx* ctx, void* dst, const void* src, size_t bytes)
     if (int st = use_device(ctx)) return st;
     if (!bytes) return ERAY_OK;
     if (!dst || !src) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "null pointer");
+    untag_range(ctx, reinterpret_cast<uintptr_t>(dst), bytes);
     HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return ERAY_OK;
@@ -1526,6 +1542,8 @@ int finish_union(eray_ctx* ctx, uint64_t seq, const FrameSource& src, uint32_t n
     HIP_TRY(ctx, hipEventRecord(ctx->union_ev[e], ctx->stream));
     ctx->union_seq[e] = seq;
     ctx->union_src[e] = src;
+    ctx->union_nobj[e] = nobj;
+    ctx->union_gen[e] = ctx->scene_gen;
     return ERAY_OK;
 }
 
@@ -1935,6 +1953,7 @@ int eray_render_camera_path(eray_ctx* ctx, const eray_render_params* rp, const e
 int eray_pack_ppm(eray_ctx* ctx, const float* rgb, uint32_t w, uint32_t h, uint8_t* out) {
     if (int st = use_device(ctx)) return st;
     if ((size_t)w * h && (!rgb || !out)) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "null pointer");
+    untag_range(ctx, reinterpret_cast<uintptr_t>(out), (size_t)w * h * 3u);
     HIP_TRY(ctx, launch_pack_ppm(rgb, w, h, out, ctx->stream));
     return ERAY_OK;
 }
@@ -2013,6 +2032,11 @@ int eray_internal_source_layout(eray_ctx* ctx, const FrameSource& src, SceneLayo
         if (ctx->union_seq[e] != src.key || !same_rows(ctx->union_src[e], src))
             return set_error(ctx, ERAY_E_INVALID_ARGUMENT,
                              "gather: these camera-path frames are older than the last %u paths", kUnionRing);
+        // (the union covers the objects of the scene the path was rendered from; a scene change
+        // since makes the path's frames ungatherable, as their objects no longer exist)
+        if (ctx->union_nobj[e] != nobj || ctx->union_gen[e] != ctx->scene_gen || nobj > ctx->union_cap)
+            return set_error(ctx, ERAY_E_INVALID_ARGUMENT,
+                             "gather: the scene changed after these camera-path frames were rendered");
         HIP_TRY(ctx, hipEventSynchronize(ctx->union_ev[e]));
         const int32_t* u = ctx->h_union + (size_t)e * 4 * ctx->union_cap;
         for (size_t i = 0; i < nobj; ++i)
@@ -2037,6 +2061,9 @@ int eray_internal_use_device(eray_ctx* ctx) { return use_device(ctx); }
 
 // Error reporting and the gather's staging buffer for the other translation units (comm.cpp).
 int eray_internal_error(eray_ctx* ctx, int code, const char* msg) { return set_error(ctx, code, "%s", msg); }
+void eray_internal_untag(eray_ctx* ctx, const void* p, size_t bytes) {
+    if (ctx && p) untag_range(ctx, reinterpret_cast<uintptr_t>(p), bytes);
+}
 void* eray_internal_staging(eray_ctx* ctx, size_t bytes) {
     if (!ctx) return nullptr;
     if (ensure(ctx, &ctx->d_staging, &ctx->staging_cap, bytes)) return nullptr;

@@ -31,6 +31,7 @@ int eray_internal_source_layout(eray_ctx* ctx, const eray::gpu::FrameSource& src
 int eray_internal_scene_setup_source(eray_ctx* ctx, eray::gpu::FrameSource* out);
 void** eray_internal_gather_plan(eray_ctx* ctx, void (*free_fn)(void*));
 int eray_internal_use_device(eray_ctx* ctx);
+void eray_internal_untag(eray_ctx* ctx, const void* p, size_t bytes);
 
 namespace {
 // camera rows of `rank` in the interleaved band split (eray_band_rows)
@@ -73,6 +74,7 @@ __global__ void __launch_bounds__(256) unband_rows_kernel(const uint8_t* __restr
 constexpr uint32_t kSegPx = 64, kSegBytes = 3 * kSegPx;
 constexpr uint32_t kUniform = 0x80000000u;
 constexpr int kMaxCodedRanks = 64;
+constexpr uint32_t kCountFailed = 0xffffffffu;  // a rank's count word when it cannot take part
 struct RankOffsets {
     uint32_t v[kMaxCodedRanks];  // first packed segment of each rank in rank 0's staging
 };
@@ -288,7 +290,7 @@ struct GatherRect {        // one rectangle of a rank's rows, 32 B
 struct RankLayout {        // a rank's rectangles and its share of rank 0's receive buffer
     GatherRect r[kPlanRects];
     uint32_t nrect, bytes;  // bytes per frame (a multiple of 48)
-    uint64_t off;           // per-frame offset of the rank's block: its frames start at B * off
+    uint64_t off;           // per-frame offset of the rank's block (prefix sum of bytes)
     uint32_t rows, packed_rows;
     uint32_t pad[2];
 };
@@ -312,7 +314,33 @@ struct Roots {
         const uint32_t r = root(k);
         return before(r) - (r > me ? count(me) : 0u) + index(k);
     }
+    // roots with frames (0 .. roots() - 1), and root r's group among me's send groups
+    __host__ __device__ uint32_t roots() const { return n ? (B < n ? B : n) : 1u; }
+    __host__ __device__ uint32_t group(uint32_t r, uint32_t me) const {
+        const uint32_t R = roots();
+        return (r < R ? r : R) - (me < r && me < R ? 1u : 0u);
+    }
 };
+
+// Every transfer of the scene-camera gather ends with its sender's header: the sender's verdict
+// on its own arguments and the source (kind, key) of the frames it packed.  A root assembles its
+// frames only when every header it uses says ERAY_OK and the plan's source; otherwise it writes
+// none of them and raises the plan's fault word, which the context's next eray_gather_frames
+// reports — a rank that could not use its arguments still takes part in the transfers, and its
+// stale bytes never become a frame.
+struct XferHeader {
+    int32_t status;
+    uint32_t kind, key_lo, key_hi;
+};
+constexpr size_t kHdr = sizeof(XferHeader);
+static_assert(kHdr == 16, "one 16-B word");
+__host__ __device__ inline bool header_ok(const XferHeader& h, uint32_t kind, uint64_t key) {
+    return h.status == 0 && h.kind == kind && h.key_lo == (uint32_t)key && h.key_hi == (uint32_t)(key >> 32);
+}
+// Rank q's block in a receive area of `mine` frames: its packs (mine x bytes), then its header.
+__host__ __device__ inline uint64_t recv_block(const RankLayout& L, uint32_t q, uint32_t mine) {
+    return (uint64_t)mine * L.off + kHdr * q;
+}
 
 // A rank's record in the plan exchange: [status, source kind, key low, key high | nrect, then
 // nrect x (l0, l1, c0, c1)] — every rank learns every rank's status and source, so all of them
@@ -322,6 +350,8 @@ constexpr int kXchgInts = kXchgHead + 1 + 4 * kPlanRects;
 
 struct GatherPlan {
     void* comm = nullptr;
+    int32_t* fault = nullptr;      // mapped host word: a root met a failed or foreign header
+    int32_t* d_fault = nullptr;    // (its device address)
     uint32_t kind = 0;
     uint64_t key = 0;
     uint32_t H = 0, W = 0, band = 0, nranks = 0, rank = 0;
@@ -333,12 +363,20 @@ struct GatherPlan {
     size_t buf_cap = 0;
     int32_t* xchg = nullptr;       // the all-gather of the ranks' rectangles
 };
+void plan_release(GatherPlan& P) {
+    if (P.d_ranks) (void)hipFree(P.d_ranks);
+    if (P.buf) (void)hipFree(P.buf);
+    if (P.xchg) (void)hipFree(P.xchg);
+    if (P.fault) (void)hipHostFree(P.fault);
+    P.d_ranks = nullptr;
+    P.buf = nullptr;
+    P.xchg = nullptr;
+    P.fault = P.d_fault = nullptr;
+}
 void plan_free(void* v) {
     auto* P = static_cast<GatherPlan*>(v);
     if (!P) return;
-    if (P->d_ranks) hipFree(P->d_ranks);
-    if (P->buf) hipFree(P->buf);
-    if (P->xchg) hipFree(P->xchg);
+    plan_release(*P);
     delete P;
 }
 
@@ -428,7 +466,9 @@ __global__ void __launch_bounds__(256) gather_pack_kernel(const uint8_t* __restr
                                                           uint8_t* __restrict__ send, uint8_t* __restrict__ own,
                                                           RankLayout L, uint32_t W, Roots R, uint32_t me) {
     const uint32_t q = blockIdx.x, k = blockIdx.y;
-    uint8_t* out = R.root(k) == me ? own + (size_t)R.index(k) * L.bytes : send + (size_t)R.send_slot(k, me) * L.bytes;
+    const uint32_t rk = R.root(k);
+    uint8_t* out = rk == me ? own + (size_t)R.index(k) * L.bytes
+                            : send + (size_t)R.send_slot(k, me) * L.bytes + kHdr * R.group(rk, me);
     uint32_t i = 0;
     while (i + 1 < L.nrect && q >= L.r[i + 1].first) ++i;
     const GatherRect& g = L.r[i];
@@ -444,8 +484,23 @@ __global__ void __launch_bounds__(256) gather_pack_kernel(const uint8_t* __restr
 __global__ void __launch_bounds__(256) gather_assemble_kernel(const uint8_t* __restrict__ recv,
                                                               const RankLayout* __restrict__ lay, uint32_t B,
                                                               uint8_t* __restrict__ frames, uint64_t frame_stride,
-                                                              uint32_t H, uint32_t W, uint32_t band, uint32_t N) {
+                                                              uint32_t H, uint32_t W, uint32_t band, uint32_t N,
+                                                              uint32_t kind, uint64_t key, int32_t* fault) {
     __shared__ RankLayout s_L;
+    // every sender's header (and this root's own): all ERAY_OK and the plan's source, or no frame
+    bool bad = false;
+    if (threadIdx.x < N) {
+        const RankLayout& Lq = lay[threadIdx.x];
+        if (Lq.bytes) {
+            const XferHeader h = *reinterpret_cast<const XferHeader*>(recv + recv_block(Lq, threadIdx.x, B) +
+                                                                      (size_t)B * Lq.bytes);
+            bad = !header_ok(h, kind, key);
+        }
+    }
+    if (__syncthreads_or(bad)) {
+        if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
     const uint32_t F = blockIdx.x, k = blockIdx.y;
     const uint32_t Y = H - 1 - F;  // camera row
     uint32_t r, j;
@@ -462,7 +517,7 @@ __global__ void __launch_bounds__(256) gather_assemble_kernel(const uint8_t* __r
     __syncthreads();
     uint32_t bg[3];
     pattern_words(25u | (25u << 8) | (51u << 16), bg);  // sat_u8(0.1 * 255), sat_u8(0.2 * 255)
-    const uint8_t* base = recv + (size_t)B * s_L.off + (size_t)k * s_L.bytes;
+    const uint8_t* base = recv + recv_block(s_L, r, B) + (size_t)k * s_L.bytes;
     uint4* dst = reinterpret_cast<uint4*>(frames + k * frame_stride + (size_t)F * W * 3u);
     for (uint32_t w = threadIdx.x; w < W * 3u / 16u; w += blockDim.x) {
         const uint32_t c = w / 3u;  // 16-pixel column group (48 B = 3 words)
@@ -479,6 +534,15 @@ __global__ void __launch_bounds__(256) gather_assemble_kernel(const uint8_t* __r
         }
         dst[w] = v;
     }
+}
+
+// The headers a rank writes into its buffer: one after each send group, one after its own packs.
+struct HeaderSpots {
+    uint64_t off[kMaxCodedRanks + 1];
+    uint32_t n;
+};
+__global__ void gather_header_kernel(uint8_t* __restrict__ buf, HeaderSpots at, XferHeader h) {
+    if (threadIdx.x < at.n) *reinterpret_cast<XferHeader*>(buf + at.off[threadIdx.x]) = h;
 }
 
 int nccl_error(eray_ctx* ctx, const char* what, ncclResult_t r) {
@@ -535,22 +599,48 @@ int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8
         return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "gather: band_rows must be a power of two >= 4");
     if (!band_rows && height % (uint32_t)nranks)
         return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "gather: height does not split into equal blocks");
+    if (band_rows && nranks > kMaxCodedRanks)
+        return eray_internal_error(ctx, ERAY_E_UNSUPPORTED, "gather: bands over more than 64 ranks");
     const size_t row_bytes = (size_t)width * 3u;
     const uint32_t rows = band_rows ? band_rows_of(height, band_rows, (uint32_t)nranks, 0) : height / (uint32_t)nranks;
     const size_t bytes = (size_t)rows * row_bytes;
-    if (bytes && !local) return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "gather: local rows are null");
-    if (bytes && rank == 0 && !frame) return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "gather: frame is null");
-    if (!bytes) return ERAY_OK;
+    if (!bytes) return ERAY_OK;  // (shared arguments: every rank returns here)
+    // this rank's verdict on its own buffers: a failing rank still takes part in the status
+    // exchange below, and every rank returns an error before any rows move
+    int status = ERAY_OK;
+    if (!local) status = eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "gather: local rows are null");
+    else if (rank == 0 && !frame) status = eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "gather: frame is null");
     hipStream_t s = (hipStream_t)eray_get_stream(ctx);
+    hipError_t he;
     if (!band_rows) {
-        // rank order = PPM file order: rank r's block lands at frame + r * bytes on rank 0 (in place
-        // when rank 0's local rows already sit at frame + 0)
+        // every rank's status (one word each, all-gathered, one stream synchronisation), then the
+        // rows: rank order = PPM file order, rank r's block lands at frame + r * bytes on rank 0 (in
+        // place when rank 0's local rows already sit at frame + 0)
+        int32_t* words = static_cast<int32_t*>(eray_internal_staging(ctx, 4u * ((size_t)nranks + 1)));
+        if (!words) {
+            ncclCommAbort(c);  // (this rank cannot take part: release the others)
+            return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "gather: status words (communicator aborted)");
+        }
+        std::vector<int32_t> all((size_t)nranks);
+        if ((he = hipMemcpyAsync(words, &status, 4, hipMemcpyHostToDevice, s)) != hipSuccess)
+            return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+        r = ncclAllGather(words, words + 1, 1, ncclInt32, c, s);
+        if (r != ncclSuccess) return nccl_error(ctx, "ncclAllGather (gather status)", r);
+        if ((he = hipMemcpyAsync(all.data(), words + 1, 4u * (size_t)nranks, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+            (he = hipStreamSynchronize(s)) != hipSuccess)
+            return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+        if (status != ERAY_OK) return status;
+        for (int q = 0; q < nranks; ++q)
+            if (all[(size_t)q] != ERAY_OK) {
+                char msg[96];
+                std::snprintf(msg, sizeof msg, "gather: rank %d could not use its buffers (status %d)", q, all[(size_t)q]);
+                return eray_internal_error(ctx, all[(size_t)q], msg);
+            }
         r = ncclGather(local, rank == 0 ? frame : nullptr, bytes, ncclUint8, 0, c, s);
         if (r != ncclSuccess) return nccl_error(ctx, "ncclGather", r);
         return ERAY_OK;
     }
-    hipError_t he;
-    if (nranks <= kMaxCodedRanks) {
+    {
         // bands, coded (see seg_classify_kernel): every rank encodes its rows; the packed counts
         // reach every host (one all-gather of a word each, then a stream synchronisation: the
         // point-to-point sizes must be known to post them); rank 0 receives every rank's code
@@ -558,16 +648,33 @@ int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8
         const uint32_t S = (width + kSegPx - 1) / kSegPx, G = rows * S;
         const uint32_t mine = band_rows_of(height, band_rows, (uint32_t)nranks, (uint32_t)rank);
         CodedBufs b;
-        if (!coded_bufs(ctx, G, rank == 0 ? (uint32_t)nranks : 1u, (uint32_t)nranks, &b))
-            return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "gather: staging buffer");
-        if ((he = encode_rows(local, mine, rows, width, S, b.code, b.packed, b, s)) != hipSuccess)
+        if (!coded_bufs(ctx, G, rank == 0 ? (uint32_t)nranks : 1u, (uint32_t)nranks, &b)) {
+            ncclCommAbort(c);  // (this rank cannot take part: release the others)
+            return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "gather: staging buffer (communicator aborted)");
+        }
+        // the packed-segment counts carry the ranks' verdicts: a rank that cannot use its
+        // buffers sends kCountFailed, and every rank returns an error before the transfers
+        if (status == ERAY_OK) {
+            he = encode_rows(local, mine, rows, width, S, b.code, b.packed, b, s);
+            if (he != hipSuccess) status = eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+        }
+        if (status != ERAY_OK && (he = hipMemsetAsync(b.count, 0xff, 4, s)) != hipSuccess) {
+            ncclCommAbort(c);
             return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+        }
         r = ncclAllGather(b.count, b.counts, 1, ncclUint32, c, s);
         if (r != ncclSuccess) return nccl_error(ctx, "ncclAllGather", r);
         std::vector<uint32_t> counts((size_t)nranks);
         if ((he = hipMemcpyAsync(counts.data(), b.counts, 4u * (size_t)nranks, hipMemcpyDeviceToHost, s)) != hipSuccess ||
             (he = hipStreamSynchronize(s)) != hipSuccess)
             return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+        if (status != ERAY_OK) return status;
+        for (int q = 0; q < nranks; ++q)
+            if (counts[(size_t)q] == kCountFailed) {
+                char msg[80];
+                std::snprintf(msg, sizeof msg, "gather: rank %d could not use its buffers", q);
+                return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, msg);
+            }
         RankOffsets off{};
         for (int k = 1; k < nranks; ++k) off.v[k] = off.v[k - 1] + counts[(size_t)k - 1];
         if (nranks > 1) {
@@ -595,28 +702,34 @@ int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8
         }
         return ERAY_OK;
     }
-    // bands, more ranks than the coded offsets hold: every rank sends rows_max rows (rank 0's
-    // count; the others' buffers are padded), rank 0 gathers them into its staging buffer and
-    // puts each row at its file row
-    uint8_t* staging = nullptr;
-    if (rank == 0) {
-        staging = static_cast<uint8_t*>(eray_internal_staging(ctx, bytes * (size_t)nranks));
-        if (!staging) return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "gather: staging buffer");
-    }
-    r = ncclGather(local, staging, bytes, ncclUint8, 0, c, s);
-    if (r != ncclSuccess) return nccl_error(ctx, "ncclGather", r);
-    if (rank == 0) {
-        unband_rows_kernel<<<height, 256, 0, s>>>(staging, frame, height, (uint32_t)row_bytes, band_rows, (uint32_t)nranks,
-                                                   rows);
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(e));
-    }
-    return ERAY_OK;
 }
 
 }  // extern "C"
 
 namespace {
+// Every rank's verdict on a plan exchange from the same records (so all accept the plan or all
+// fail together): the first rank's failure, or a source other than this rank's.  status: this
+// rank's own verdict (its message already set).
+int plan_verdict(eray_ctx* ctx, const int32_t* all, int nranks, int status, const int32_t* mine) {
+    for (int q = 0; q < nranks; ++q) {
+        const int32_t* o = all + (size_t)q * kXchgInts;
+        if (o[0] != ERAY_OK) {
+            if (status != ERAY_OK) return status;
+            char msg[128];
+            std::snprintf(msg, sizeof msg, "scene-camera gather: rank %d could not use its frames (status %d)", q, o[0]);
+            return eray_internal_error(ctx, o[0], msg);
+        }
+    }
+    if (status != ERAY_OK) return status;
+    for (int q = 0; q < nranks; ++q) {
+        const int32_t* o = all + (size_t)q * kXchgInts;
+        if (o[1] != mine[1] || o[2] != mine[2] || o[3] != mine[3])
+            return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT,
+                                       "scene-camera gather: the ranks' frames come from different cameras or paths");
+    }
+    return ERAY_OK;
+}
+
 // Exchanges the ranks' records for a new plan (a collective: every rank calls it at the same
 // point, one stream synchronisation).  `status` is this rank's verdict (ERAY_OK, or the error it
 // met looking up its frames' source and rectangles); on success every rank holds every rank's
@@ -627,8 +740,22 @@ int exchange_plan(eray_ctx* ctx, ncclComm_t c, int nranks, int rank, uint32_t H,
     P->valid = false;
     hipStream_t s = (hipStream_t)eray_get_stream(ctx);
     hipError_t he;
-    if (!P->xchg && (he = hipMalloc((void**)&P->xchg, sizeof(int32_t) * kXchgInts * (size_t)(kMaxCodedRanks + 1))) != hipSuccess)
-        return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, hipGetErrorString(he));
+    if (!P->xchg && (he = hipMalloc((void**)&P->xchg, sizeof(int32_t) * kXchgInts * (size_t)(kMaxCodedRanks + 1))) != hipSuccess) {
+        // without the exchange buffer this rank cannot take part: release the other ranks
+        // (their all-gather fails instead of waiting for this rank forever)
+        ncclCommAbort(c);
+        return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "gather plan: exchange buffer (communicator aborted)");
+    }
+    if (status == ERAY_OK && !P->fault) {  // the roots' fault word (a failure here is this rank's verdict)
+        if (hipHostMalloc((void**)&P->fault, sizeof(int32_t), hipHostMallocMapped) != hipSuccess ||
+            hipHostGetDevicePointer((void**)&P->d_fault, P->fault, 0) != hipSuccess) {
+            if (P->fault) (void)hipHostFree(P->fault);
+            P->fault = P->d_fault = nullptr;
+            status = eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "gather plan: fault word");
+        } else {
+            *P->fault = 0;
+        }
+    }
     int32_t rec[kXchgInts] = {};
     rec[0] = status;
     rec[1] = (int32_t)src.kind;
@@ -644,18 +771,7 @@ int exchange_plan(eray_ctx* ctx, ncclComm_t c, int nranks, int rank, uint32_t H,
             hipSuccess ||
         (he = hipStreamSynchronize(s)) != hipSuccess)
         return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
-    for (int q = 0; q < nranks; ++q) {  // every rank reaches the same verdict from the same records
-        const int32_t* o = all.data() + (size_t)q * kXchgInts;
-        if (o[0] != ERAY_OK) {
-            if (status != ERAY_OK) return status;  // (this rank's own message is already set)
-            char msg[128];
-            std::snprintf(msg, sizeof msg, "scene-camera gather: rank %d could not use its frames (status %d)", q, o[0]);
-            return eray_internal_error(ctx, o[0], msg);
-        }
-        if (o[1] != rec[1] || o[2] != rec[2] || o[3] != rec[3])
-            return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT,
-                                       "scene-camera gather: the ranks' frames come from different cameras or paths");
-    }
+    if (int st = plan_verdict(ctx, all.data(), nranks, status, rec)) return st;
     P->ranks.assign((size_t)nranks, RankLayout{});
     P->total = 0;
     for (int q = 0; q < nranks; ++q) {
@@ -665,7 +781,7 @@ int exchange_plan(eray_ctx* ctx, ncclComm_t c, int nranks, int rank, uint32_t H,
         P->total += R.bytes;
         P->ranks[(size_t)q] = R;
     }
-    if (P->d_ranks) hipFree(P->d_ranks);
+    if (P->d_ranks) (void)hipFree(P->d_ranks);
     P->d_ranks = nullptr;
     if ((he = hipMalloc((void**)&P->d_ranks, sizeof(RankLayout) * (size_t)nranks)) != hipSuccess ||
         (he = hipMemcpy(P->d_ranks, P->ranks.data(), sizeof(RankLayout) * (size_t)nranks, hipMemcpyHostToDevice)) !=
@@ -683,24 +799,27 @@ int exchange_plan(eray_ctx* ctx, ncclComm_t c, int nranks, int rank, uint32_t H,
     return ERAY_OK;
 }
 
+// The plan's transfer buffer grown to `bytes` (the first call of a batch size): the new buffer is
+// allocated before the old one is released, so a failure leaves the plan as it was.
 int grow(eray_ctx* ctx, GatherPlan* P, size_t bytes) {
     if (bytes <= P->buf_cap && P->buf) return ERAY_OK;
     hipStream_t s = (hipStream_t)eray_get_stream(ctx);
-    hipError_t he = hipStreamSynchronize(s);  // (growth only: the first call of a batch size)
-    if (he == hipSuccess && P->buf) he = hipFree(P->buf);
-    P->buf = nullptr;
-    P->buf_cap = 0;
-    if (he == hipSuccess) he = hipMalloc((void**)&P->buf, std::max<size_t>(bytes, 256));
+    uint8_t* nb = nullptr;
+    hipError_t he = hipStreamSynchronize(s);  // (the old buffer's transfers are done)
+    if (he == hipSuccess) he = hipMalloc((void**)&nb, std::max<size_t>(bytes, 256));
     if (he != hipSuccess) return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, hipGetErrorString(he));
+    if (P->buf) (void)hipFree(P->buf);
+    P->buf = nb;
     P->buf_cap = std::max<size_t>(bytes, 256);
     return ERAY_OK;
 }
 
 // One rank's part of a batch of B frames: where its packs go in its buffer, how much buffer it
 // needs, and its point-to-point transfers (offsets into the buffer).  Its receive area holds, for
-// each of the `mine` frames it assembles, every rank's pack (rank q's at mine * off_q + j * bytes_q,
-// the layout gather_assemble_kernel reads); its send area the frames of the other roots, grouped
-// by root, so each (rank, root) pair is one transfer.
+// each of the `mine` frames it assembles, every rank's pack and then that rank's header (rank q's
+// block at recv_block: mine * off_q + 16 q, frame j at + j * bytes_q, the layout
+// gather_assemble_kernel reads); its send area the frames of the other roots, grouped by root,
+// each group followed by this rank's header, so each (rank, root) pair is one transfer.
 struct Xfer {
     uint32_t peer;
     bool send;
@@ -712,6 +831,8 @@ struct Schedule {
     size_t send_base, own;     // its send area; its own packs' block in the receive area
     size_t need;               // buffer bytes
     std::vector<Xfer> ops;
+    HeaderSpots hdr;           // where this rank writes its header (after each send group, after its own packs)
+    std::vector<uint64_t> peer_hdr;  // per rank: its header in this rank's receive area (~0: not used)
 };
 Schedule schedule(const std::vector<RankLayout>& ranks, uint64_t total, uint32_t rank, uint32_t B, bool rotate) {
     Schedule S;
@@ -719,28 +840,46 @@ Schedule schedule(const std::vector<RankLayout>& ranks, uint64_t total, uint32_t
     S.R = Roots{B, rotate ? N : 0u};
     S.mine = S.R.count(rank);
     const RankLayout& me = ranks[rank];
-    S.send_base = (size_t)S.mine * total;
-    S.own = (size_t)S.mine * me.off;
-    S.need = S.send_base + (size_t)(B - S.mine) * me.bytes;
+    S.send_base = (size_t)S.mine * total + kHdr * N;
+    S.own = recv_block(me, rank, S.mine);
+    S.hdr.n = 0;
+    S.peer_hdr.assign(N, ~0ull);
+    size_t groups = 0;
     for (uint32_t q = 0; q < N; ++q) {
-        if (q == rank) continue;
-        if (S.R.count(q) && me.bytes)
-            S.ops.push_back({q, true, S.send_base + (size_t)(S.R.before(q) - (q > rank ? S.mine : 0u)) * me.bytes,
-                             (size_t)S.R.count(q) * me.bytes});
-        if (S.mine && ranks[q].bytes)
-            S.ops.push_back({q, false, (size_t)S.mine * ranks[q].off, (size_t)S.mine * ranks[q].bytes});
+        if (q != rank && S.R.count(q) && me.bytes) {
+            const size_t off = S.send_base + (size_t)(S.R.before(q) - (q > rank ? S.mine : 0u)) * me.bytes +
+                               kHdr * S.R.group(q, rank);
+            const size_t bytes = (size_t)S.R.count(q) * me.bytes;
+            S.ops.push_back({q, true, off, bytes + kHdr});
+            S.hdr.off[S.hdr.n++] = off + bytes;
+            ++groups;
+        }
+        if (S.mine && ranks[q].bytes) {
+            const size_t off = recv_block(ranks[q], q, S.mine), bytes = (size_t)S.mine * ranks[q].bytes;
+            if (q != rank) S.ops.push_back({q, false, off, bytes + kHdr});
+            S.peer_hdr[q] = off + bytes;
+        }
     }
+    if (S.mine) S.hdr.off[S.hdr.n++] = S.own + (size_t)S.mine * me.bytes;
+    S.need = S.send_base + (size_t)(B - S.mine) * me.bytes + kHdr * groups;
     return S;
 }
 
-// Pack (every rank), transfer, assemble (each frame's root) `B` frames with plan P.  fail_safe
-// (this rank's own arguments are unusable): only the transfers of the plan, so the other ranks'
-// matching sends and receives complete — no kernel touches the caller's buffers.
+// Pack (every rank), transfer, assemble (each frame's root) `B` frames with plan P.  status != OK
+// (this rank's own arguments are unusable): its headers carry the status and it runs only the
+// plan's transfers, so the other ranks' matching sends and receives complete and their roots
+// refuse the batch — no kernel touches the caller's buffers.
 int scene_gather(eray_ctx* ctx, ncclComm_t c, const GatherPlan& P, const Schedule& S, const uint8_t* local,
-                 uint64_t local_stride, uint8_t* frames, uint64_t frame_stride, uint32_t B, bool fail_safe = false) {
+                 uint64_t local_stride, uint8_t* frames, uint64_t frame_stride, uint32_t B, int status = ERAY_OK) {
     hipStream_t s = (hipStream_t)eray_get_stream(ctx);
     const RankLayout& me = P.ranks[P.rank];
+    const bool fail_safe = status != ERAY_OK;
     hipError_t he;
+    if (S.hdr.n) {
+        const XferHeader h{status, P.kind, (uint32_t)P.key, (uint32_t)(P.key >> 32)};
+        gather_header_kernel<<<1, 64, 0, s>>>(P.buf, S.hdr, h);
+        if ((he = hipGetLastError()) != hipSuccess) return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+    }
     if (me.bytes && !fail_safe) {
         gather_pack_kernel<<<dim3(me.packed_rows, B), 256, 0, s>>>(local, local_stride, P.buf + S.send_base,
                                                                    P.buf + S.own, me, P.W, S.R, P.rank);
@@ -760,7 +899,7 @@ int scene_gather(eray_ctx* ctx, ncclComm_t c, const GatherPlan& P, const Schedul
     }
     if (S.mine && !fail_safe) {
         gather_assemble_kernel<<<dim3(P.H, S.mine), 256, 0, s>>>(P.buf, P.d_ranks, S.mine, frames, frame_stride, P.H, P.W,
-                                                                 P.band, P.nranks);
+                                                                 P.band, P.nranks, P.kind, P.key, P.d_fault);
         if ((he = hipGetLastError()) != hipSuccess) return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
     }
     return ERAY_OK;
@@ -794,16 +933,28 @@ int eray_gather_frames(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uin
                                        "scene-camera gather: width must be a multiple of 16 and the rows a valid split");
         if (nranks > kMaxCodedRanks)
             return eray_internal_error(ctx, ERAY_E_UNSUPPORTED, "scene-camera gather: more than 64 ranks");
-        // this rank's verdict on its own arguments and frames
+        // This rank's verdict on its own arguments and frames.  Whatever it is, the rank takes
+        // part in the same collectives as the others (which choose their path from the same
+        // shared arguments and, under the SPMD precondition, the same frame sources), then
+        // returns its error.
         const bool assembles = rotate ? (uint32_t)rank < nframes : rank == 0;
         const bool aligned = ((reinterpret_cast<uintptr_t>(local) | local_stride) & 15) == 0 &&
                              (!assembles || ((reinterpret_cast<uintptr_t>(frames) | frame_stride) & 15) == 0);
         int status = ERAY_OK;
-        eray::gpu::FrameSource src;
         if (!local || (assembles && !frames) || !aligned)
             status = eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT,
                                          "scene-camera gather: null or unaligned (16 B) buffers or strides");
-        if (status == ERAY_OK) status = eray_internal_frame_source(ctx, local, local_stride, nframes, &src);
+        // the frames' source, looked up whenever `local` is usable: the re-plan decision below
+        // then follows the frames even on a rank that fails for another reason
+        eray::gpu::FrameSource src;
+        bool src_known = false;
+        if (local) {
+            std::string keep = status != ERAY_OK ? eray_last_error(ctx) : std::string();
+            const int st = eray_internal_frame_source(ctx, local, local_stride, nframes, &src);
+            src_known = st == ERAY_OK;
+            if (status == ERAY_OK) status = st;
+            else eray_internal_error(ctx, status, keep.c_str());  // (the first failure's message)
+        }
         const RankRows rr = rank_rows(height, band_rows, (uint32_t)nranks, (uint32_t)rank);
         if (status == ERAY_OK && (src.W != width || src.H != height || src.row0 != rr.row0 || src.rows != rr.rows ||
                                   src.band_shift != rr.shift || (band_rows && src.band_stride != rr.stride)))
@@ -812,26 +963,41 @@ int eray_gather_frames(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uin
                                          "this rank's share");
         GatherPlan*& P = *reinterpret_cast<GatherPlan**>(eray_internal_gather_plan(ctx, plan_free));
         if (!P) P = new (std::nothrow) GatherPlan();
-        if (!P) return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "gather plan");
+        if (!P) {  // no plan object: this rank still takes part in the (first) exchange, with its error
+            GatherPlan tmp;
+            eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "gather plan");
+            const int st = exchange_plan(ctx, c, nranks, rank, height, width, band_rows, src, ERAY_E_OUT_OF_MEMORY, {}, &tmp);
+            plan_release(tmp);
+            return st ? st : ERAY_E_OUT_OF_MEMORY;
+        }
+        // a failed or foreign batch met by one of this context's earlier assemblies (reported
+        // once, after this call's own collectives)
+        const bool faulted = P->fault && __atomic_exchange_n(P->fault, 0, __ATOMIC_RELAXED) != 0;
         const bool cached = P->valid && P->comm == (void*)c && P->H == height && P->W == width &&
                             P->band == band_rows && P->nranks == (uint32_t)nranks && P->rank == (uint32_t)rank;
-        if (status != ERAY_OK && cached) {
-            // the other ranks (same calls, same plan) go ahead with this plan's transfers: take part
-            // in them, touch nothing, and report the error
-                const Schedule S = schedule(P->ranks, P->total, (uint32_t)rank, nframes, rotate);
-            std::string msg = eray_last_error(ctx);
-            if (grow(ctx, P, S.need) == ERAY_OK)
-                scene_gather(ctx, c, *P, S, local, local_stride, frames, frame_stride, nframes, true);
-            return eray_internal_error(ctx, status, msg.c_str());
-        }
-        if (!cached || P->kind != src.kind || P->key != src.key) {  // a new plan: every rank exchanges
+        if (!cached || (src_known && (P->kind != src.kind || P->key != src.key))) {  // a new plan: every rank exchanges
             eray::gpu::SceneLayout L;
             if (status == ERAY_OK) status = eray_internal_source_layout(ctx, src, &L);
             if (int st = exchange_plan(ctx, c, nranks, rank, height, width, band_rows, src, status, L.rects, P)) return st;
         }
         const Schedule S = schedule(P->ranks, P->total, (uint32_t)rank, nframes, rotate);
-        if (int st = grow(ctx, P, S.need)) return st;
-        return scene_gather(ctx, c, *P, S, local, local_stride, frames, frame_stride, nframes);
+        if (grow(ctx, P, S.need) != ERAY_OK) {
+            // no buffer for this batch's transfers: release the other ranks rather than leave
+            // their sends and receives waiting for this one
+            ncclCommAbort(c);
+            P->valid = false;
+            return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "scene-camera gather: transfer buffer (communicator aborted)");
+        }
+        std::string msg = status != ERAY_OK ? eray_last_error(ctx) : std::string();
+        const int st = scene_gather(ctx, c, *P, S, local, local_stride, frames, frame_stride, nframes, status);
+        if (status != ERAY_OK) return eray_internal_error(ctx, status, msg.c_str());
+        if (st) return st;
+        if (S.mine) eray_internal_untag(ctx, frames, (size_t)(S.mine - 1) * frame_stride + (size_t)height * width * 3u);
+        if (faulted)
+            return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT,
+                                       "scene-camera gather: an earlier batch assembled here had a rank that could not "
+                                       "use its frames; its frames were left unwritten");
+        return ERAY_OK;
     }
     for (uint32_t k = 0; k < nframes; ++k)  // one frame at a time through eray_gather_rows
         if (int st = eray_gather_rows(ctx, nccl_comm, local ? local + k * local_stride : nullptr,
@@ -869,17 +1035,12 @@ int eray_debug_gather_layout(const int32_t* rects, uint32_t n, uint32_t height, 
     return ERAY_OK;
 }
 
-// Diagnostics (tests, host only): rank `rank`'s schedule for a batch of `nframes` frames when the
-// ranks' packs are rank_bytes[q] bytes per frame (rank order = receive-area order) — what
-// eray_gather_frames' pack kernel and point-to-point transfers do.  out (u64): buffer bytes,
-// frames this rank assembles, number of transfers; then per frame k its pack's offset in the
-// buffer; then per rank q where q's packs of this rank's frames start (frame j: + j * bytes_q);
-// then per transfer: peer, 1 = send / 0 = receive, offset, bytes.
-int eray_debug_gather_schedule(const uint32_t* rank_bytes, uint32_t nranks, uint32_t rank, uint32_t nframes,
-                               uint32_t rotate, uint64_t* out, uint32_t cap) {
-    if (!rank_bytes || !out || !nranks || nranks > (uint32_t)kMaxCodedRanks || rank >= nranks ||
-        cap < 3u + nframes + nranks + 8u * nranks)
-        return eray_internal_error(nullptr, ERAY_E_INVALID_ARGUMENT, "gather schedule: bad arguments");
+}  // extern "C"
+
+namespace {
+// The schedule of eray_debug_gather_* for packs of rank_bytes[q] bytes per frame (no plan).
+Schedule debug_schedule(const uint32_t* rank_bytes, uint32_t nranks, uint32_t rank, uint32_t nframes, uint32_t rotate,
+                        std::vector<RankLayout>* ranks_out = nullptr) {
     std::vector<RankLayout> ranks(nranks, RankLayout{});
     uint64_t total = 0;
     for (uint32_t q = 0; q < nranks; ++q) {
@@ -887,22 +1048,94 @@ int eray_debug_gather_schedule(const uint32_t* rank_bytes, uint32_t nranks, uint
         ranks[q].off = total;
         total += rank_bytes[q];
     }
-    const Schedule S = schedule(ranks, total, rank, nframes, rotate != 0);
+    if (ranks_out) *ranks_out = ranks;
+    return schedule(ranks, total, rank, nframes, rotate != 0);
+}
+bool debug_schedule_args(const uint32_t* rank_bytes, uint32_t nranks, uint32_t rank) {
+    return rank_bytes && nranks && nranks <= (uint32_t)kMaxCodedRanks && rank < nranks;
+}
+}  // namespace
+
+extern "C" {
+
+// Diagnostics (tests, host only): rank `rank`'s schedule for a batch of `nframes` frames when the
+// ranks' packs are rank_bytes[q] bytes per frame (rank order = receive-area order) — what
+// eray_gather_frames' pack kernel and point-to-point transfers do.  out (u64): buffer bytes,
+// frames this rank assembles, number of transfers T; then per frame k its pack's offset in the
+// buffer; then per rank q where q's packs of this rank's frames start (frame j: + j * bytes_q);
+// then per transfer: peer, 1 = send / 0 = receive, offset, bytes (each transfer ends with its
+// sender's 16-B header); then the number of headers this rank writes and their offsets (T + 1
+// slots); then per rank q the offset of q's header in this rank's receive area (~0: unused).
+int eray_debug_gather_schedule(const uint32_t* rank_bytes, uint32_t nranks, uint32_t rank, uint32_t nframes,
+                               uint32_t rotate, uint64_t* out, uint32_t cap) {
+    if (!debug_schedule_args(rank_bytes, nranks, rank) || !out || cap < 5u + nframes + 12u * nranks)
+        return eray_internal_error(nullptr, ERAY_E_INVALID_ARGUMENT, "gather schedule: bad arguments");
+    std::vector<RankLayout> ranks;
+    const Schedule S = debug_schedule(rank_bytes, nranks, rank, nframes, rotate, &ranks);
     const uint64_t bytes = rank_bytes[rank];
     out[0] = S.need;
     out[1] = S.mine;
     out[2] = S.ops.size();
-    for (uint32_t k = 0; k < nframes; ++k)
-        out[3 + k] = S.R.root(k) == rank ? S.own + S.R.index(k) * bytes : S.send_base + S.R.send_slot(k, rank) * bytes;
-    for (uint32_t q = 0; q < nranks; ++q) out[3 + nframes + q] = (uint64_t)S.mine * ranks[q].off;
-    for (size_t i = 0; i < S.ops.size(); ++i) {
-        uint64_t* o = out + 3 + nframes + nranks + 4 * i;
-        o[0] = S.ops[i].peer;
-        o[1] = S.ops[i].send ? 1u : 0u;
-        o[2] = S.ops[i].off;
-        o[3] = S.ops[i].bytes;
+    for (uint32_t k = 0; k < nframes; ++k) {
+        const uint32_t r = S.R.root(k);
+        out[3 + k] = r == rank ? S.own + S.R.index(k) * bytes
+                               : S.send_base + S.R.send_slot(k, rank) * bytes + (bytes ? kHdr * S.R.group(r, rank) : 0);
+    }
+    for (uint32_t q = 0; q < nranks; ++q) out[3 + nframes + q] = recv_block(ranks[q], q, S.mine);
+    uint64_t* o = out + 3 + nframes + nranks;
+    for (const Xfer& x : S.ops) {
+        o[0] = x.peer;
+        o[1] = x.send ? 1u : 0u;
+        o[2] = x.off;
+        o[3] = x.bytes;
+        o += 4;
+    }
+    *o++ = S.hdr.n;
+    for (uint32_t i = 0; i < S.hdr.n; ++i) *o++ = S.hdr.off[i];
+    for (uint32_t q = 0; q < nranks; ++q) *o++ = S.peer_hdr[q];
+    return ERAY_OK;
+}
+
+// Diagnostics (tests, host only): the headers rank `rank` writes into its transfer buffer `buf`
+// (host memory of the schedule's size) — its verdict `status` and its frames' source (kind, key).
+int eray_debug_gather_write_headers(const uint32_t* rank_bytes, uint32_t nranks, uint32_t rank, uint32_t nframes,
+                                    uint32_t rotate, int32_t status, uint32_t kind, uint64_t key, uint8_t* buf) {
+    if (!debug_schedule_args(rank_bytes, nranks, rank) || !buf)
+        return eray_internal_error(nullptr, ERAY_E_INVALID_ARGUMENT, "gather headers: bad arguments");
+    const Schedule S = debug_schedule(rank_bytes, nranks, rank, nframes, rotate);
+    const XferHeader h{status, kind, (uint32_t)key, (uint32_t)(key >> 32)};
+    for (uint32_t i = 0; i < S.hdr.n; ++i) std::memcpy(buf + S.hdr.off[i], &h, kHdr);
+    return ERAY_OK;
+}
+
+// Diagnostics (tests, host only): a root's verdict on its received batch (gather_assemble_kernel's
+// check, on a host copy of its buffer): ERAY_OK when every header it uses says ERAY_OK and the
+// plan's source (kind, key), else ERAY_E_INVALID_ARGUMENT (the root writes none of the frames).
+int eray_debug_gather_check(const uint32_t* rank_bytes, uint32_t nranks, uint32_t rank, uint32_t nframes,
+                            uint32_t rotate, uint32_t kind, uint64_t key, const uint8_t* buf) {
+    if (!debug_schedule_args(rank_bytes, nranks, rank) || !buf)
+        return eray_internal_error(nullptr, ERAY_E_INVALID_ARGUMENT, "gather check: bad arguments");
+    const Schedule S = debug_schedule(rank_bytes, nranks, rank, nframes, rotate);
+    for (uint32_t q = 0; q < nranks; ++q) {
+        if (S.peer_hdr[q] == ~0ull) continue;
+        XferHeader h;
+        std::memcpy(&h, buf + S.peer_hdr[q], kHdr);
+        if (!header_ok(h, kind, key))
+            return eray_internal_error(nullptr, ERAY_E_INVALID_ARGUMENT, "gather: a rank could not use its frames");
     }
     return ERAY_OK;
+}
+
+// Diagnostics (tests, host only): a new plan's verdict on this rank (exchange_plan's): records
+// holds every rank's (status, kind, key low, key high), `rank`'s own among them.
+int eray_debug_plan_verdict(const int32_t* records, uint32_t nranks, uint32_t rank) {
+    if (!records || !nranks || nranks > (uint32_t)kMaxCodedRanks || rank >= nranks)
+        return eray_internal_error(nullptr, ERAY_E_INVALID_ARGUMENT, "plan verdict: bad arguments");
+    std::vector<int32_t> all((size_t)kXchgInts * nranks, 0);
+    for (uint32_t q = 0; q < nranks; ++q) std::memcpy(all.data() + (size_t)q * kXchgInts, records + 4 * q, 4 * sizeof(int32_t));
+    const int32_t* mine = all.data() + (size_t)rank * kXchgInts;
+    if (mine[0] != ERAY_OK) eray_internal_error(nullptr, mine[0], "plan verdict: this rank's own failure");
+    return plan_verdict(nullptr, all.data(), (int)nranks, mine[0], mine);
 }
 
 // Diagnostics (tests): the scene-camera gather of a batch of `nframes` frames by N ranks,
@@ -929,6 +1162,8 @@ int eray_debug_scene_gather_batch(eray_ctx* ctx, const uint8_t* staging, uint8_t
     P.band = band_rows;
     P.nranks = nranks;
     P.rank = 0;
+    P.kind = src.kind;
+    P.key = src.key;
     const uint32_t rows_max = rank_rows(height, band_rows, nranks, 0).rows;
     for (uint32_t q = 0; q < nranks; ++q) {
         const RankRows rr = rank_rows(height, band_rows, nranks, q);
@@ -951,6 +1186,14 @@ int eray_debug_scene_gather_batch(eray_ctx* ctx, const uint8_t* staging, uint8_t
     hipStream_t s = (hipStream_t)eray_get_stream(ctx);
     hipError_t he = hipMalloc((void**)&P.d_ranks, sizeof(RankLayout) * nranks);
     if (he == hipSuccess) he = hipMalloc((void**)&P.buf, std::max<size_t>(all, 256));
+    if (he == hipSuccess) he = hipMalloc((void**)&P.d_fault, sizeof(int32_t));
+    if (he == hipSuccess) he = hipMemsetAsync(P.d_fault, 0, sizeof(int32_t), s);
+    const XferHeader hdr{ERAY_OK, P.kind, (uint32_t)P.key, (uint32_t)(P.key >> 32)};
+    for (uint32_t q = 0; q < nranks && he == hipSuccess; ++q) {  // every rank's headers
+        if (!S[q].hdr.n) continue;
+        gather_header_kernel<<<1, 64, 0, s>>>(P.buf + base[q], S[q].hdr, hdr);
+        he = hipGetLastError();
+    }
     if (he == hipSuccess)
         he = hipMemcpyAsync(P.d_ranks, P.ranks.data(), sizeof(RankLayout) * nranks, hipMemcpyHostToDevice, s);
     for (uint32_t q = 0; q < nranks && he == hipSuccess; ++q) {  // every rank packs its frames
@@ -978,16 +1221,18 @@ int eray_debug_scene_gather_batch(eray_ctx* ctx, const uint8_t* staging, uint8_t
         if (!S[r].mine) continue;
         gather_assemble_kernel<<<dim3(height, S[r].mine), 256, 0, s>>>(P.buf + base[r], P.d_ranks, S[r].mine,
                                                                        frames + S[r].R.before(r) * frame_bytes,
-                                                                       frame_bytes, height, width, band_rows, nranks);
+                                                                       frame_bytes, height, width, band_rows, nranks,
+                                                                       P.kind, P.key, P.d_fault);
         he = hipGetLastError();
     }
+    int32_t fault = 0;
+    if (he == hipSuccess) he = hipMemcpyAsync(&fault, P.d_fault, sizeof fault, hipMemcpyDeviceToHost, s);
     if (he == hipSuccess) he = hipStreamSynchronize(s);
-    if (P.d_ranks) hipFree(P.d_ranks);
-    if (P.buf) hipFree(P.buf);
-    P.d_ranks = nullptr;
-    P.buf = nullptr;
-    P.xchg = nullptr;
-    return he == hipSuccess ? ERAY_OK : eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+    if (P.d_fault) (void)hipFree(P.d_fault);
+    P.d_fault = nullptr;  // (not the mapped word plan_release frees)
+    plan_release(P);
+    if (he != hipSuccess) return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+    return fault ? eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "scene gather: a root refused its batch") : ERAY_OK;
 }
 
 // One frame of eray_debug_scene_gather_batch (staging: the N ranks' blocks; frame: rank 0's).

@@ -163,10 +163,10 @@ __device__ __forceinline__ bool cull_one(float A, float B, float K, float T, flo
 __device__ __forceinline__ bool cull_rejects(const TriCull c, float xlo, float xhi, float ylo,
                                              float yhi) {
     // all four conditions, no short-circuit: the record is one 64-byte load
-    return cull_one(c.A.x, c.B.x, c.K.x, c.T.x, xlo, xhi, ylo, yhi) |
-           cull_one(c.A.y, c.B.y, c.K.y, c.T.y, xlo, xhi, ylo, yhi) |
-           cull_one(c.A.z, c.B.z, c.K.z, c.T.z, xlo, xhi, ylo, yhi) |
-           cull_one(c.A.w, c.B.w, c.K.w, c.T.w, xlo, xhi, ylo, yhi);
+    return ((int)cull_one(c.A.x, c.B.x, c.K.x, c.T.x, xlo, xhi, ylo, yhi) |
+            (int)cull_one(c.A.y, c.B.y, c.K.y, c.T.y, xlo, xhi, ylo, yhi) |
+            (int)cull_one(c.A.z, c.B.z, c.K.z, c.T.z, xlo, xhi, ylo, yhi) |
+            (int)cull_one(c.A.w, c.B.w, c.K.w, c.T.w, xlo, xhi, ylo, yhi)) != 0;
 }
 
 }  // namespace gpu

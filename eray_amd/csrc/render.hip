@@ -39,6 +39,7 @@
 #ifndef ERAY_TRACE_POINT
 #define ERAY_TRACE_POINT(k)
 #define ERAY_TRACE_WAVE0(k)
+#define ERAY_TRACE_VALUE(k, v)
 #endif
 
 namespace eray {
@@ -602,6 +603,7 @@ __device__ void first_hit_binned_wave(const ObjGeom& ob, uint32_t bin, int& st, 
         const bool a = activate();
         if (st == kUndecided) st = a ? kSearching : kDone;
     }
+    ERAY_TRACE_WAVE0(8);
     if (!__any(st == kSearching)) return;
     L.dir[0][lane] = d.x;
     L.dir[1][lane] = d.y;
@@ -621,6 +623,7 @@ __device__ void first_hit_binned_wave(const ObjGeom& ob, uint32_t bin, int& st, 
         uint32_t cmin = fj;  // the chunk's smallest face
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) cmin = min(cmin, (uint32_t)__shfl_xor((int)cmin, off));
+        ERAY_TRACE_WAVE0(9);
         const unsigned long long live = __ballot((best >> 6) > cmin);  // pixels this chunk can still improve
         if (!live) continue;
         const unsigned long long pix = pm & live;
@@ -685,6 +688,8 @@ __device__ void first_hit_binned_wave(const ObjGeom& ob, uint32_t bin, int& st, 
         __builtin_amdgcn_wave_barrier();  // L.cand / L.pairs are rewritten by the next chunk
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    ERAY_TRACE_WAVE0(10);
+    ERAY_TRACE_VALUE(15, (hi - lo + 63) / 64);
     if (st == kSearching && found >= 0) st = kDone;
 }
 
@@ -726,7 +731,7 @@ __device__ __forceinline__ f3 camera_dir(const CamDev& cam, const FrameParams& p
 //    loads must not wait behind their own stores (a CDNA wave's vmcnt counts both).
 
 // Rank-local row -> camera row (interleaved bands or a contiguous block), from the frame kernel's
-// preloaded band word (h_band: shift | stride << 5) and row0.
+// band word (h_band: shift | stride << 5) and row0.
 struct RowMap {
     uint32_t row0, shift, stride;
 };
@@ -821,6 +826,57 @@ __device__ __forceinline__ void fill_background(const FrameParams& p, const Fram
     }
 }
 
+// A full 64 x 4 background block's stores (fill_background<kBlkW> for aligned blocks inside the
+// frame), per lane: the 16-B words it writes and their byte offsets from the block's first byte in
+// each output array.  They are the same for every block, so the fill loop adds a wave-uniform
+// block base as the buffer store's scalar offset and issues the stores: no per-store address
+// arithmetic or pattern selects (the fill waves share their SIMDs' issue slots with the detail
+// waves, and a frame's background is ~99 % of its stores).
+struct BlockFill {
+    uint4 rgb[3];
+    uint32_t rgb_off[3];
+    uint4 ppm;
+    uint32_t ppm_off;
+    uint32_t face_off;
+};
+__device__ __forceinline__ BlockFill block_fill(uint32_t img_w, uint32_t lane) {
+    constexpr uint32_t kRow4 = kBlkW * 3 / 4;    // float4 per RGB row (48)
+    constexpr uint32_t kRow16 = kBlkW * 3 / 16;  // 16-byte words per PPM row (12)
+    constexpr uint32_t kFace4 = kBlkW / 4;       // int4 per face row (16)
+    BlockFill b;
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) {
+        const uint32_t i = lane + 64u * k, r = i / kRow4, c = i % kRow4;
+        b.rgb_off[k] = r * img_w * 12u + c * 16u;
+        const float4 v = bg_rgb4(c % 3u);
+        b.rgb[k] = make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w));
+    }
+    const uint32_t r = lane / kRow16, c = lane % kRow16;  // lanes < kBlkH * kRow16 store
+    b.ppm_off = r * img_w * 3u + c * 16u;
+    b.ppm = bg_ppm16(c % 3u);
+    b.face_off = (lane / kFace4) * img_w * 4u + (lane % kFace4) * 16u;
+    return b;
+}
+template <typename B>
+__device__ __forceinline__ void stream16_at(B* base, uint32_t voff, uint32_t soff, uint4 v) {
+    const u32x4 w{v.x, v.y, v.z, v.w};
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, -1, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(w, rs, voff, soff, kStoreSc1);
+}
+// The block (bx, by) (block units, rank-local rows; wave-uniform) from the lane constants.
+__device__ __forceinline__ void fill_block_fast(const FrameParams& p, const FrameOut& o, const BlockFill& bf, uint32_t bx,
+                                                uint32_t by, uint32_t lane) {
+    const uint32_t x0 = bx * kBlkW, py0 = by * kBlkH;
+    if (o.rgb) {
+        const uint32_t base = (py0 * p.img_w + x0) * 12u;
+#pragma unroll
+        for (uint32_t k = 0; k < 3; ++k) stream16_at(o.rgb, bf.rgb_off[k], base, bf.rgb[k]);
+    }
+    if (o.ppm && lane < kBlkH * (kBlkW * 3 / 16))
+        stream16_at(o.ppm, bf.ppm_off, ((p.rows - py0 - kBlkH) * p.img_w + x0) * 3u, bf.ppm);
+    if (o.face) stream16_at(o.face, bf.face_off, (py0 * p.img_w + x0) * 4u, make_uint4(~0u, ~0u, ~0u, ~0u));
+}
+
 // the pixel rectangle of `ob` (camera rows) meets the sub-block's pixels
 __device__ __forceinline__ bool rect_meets(const ObjGeom& ob, const RowMap& rm, uint32_t wx0, uint32_t py0) {
     const int32_t x0 = (int32_t)wx0, y0 = (int32_t)cam_row(rm, py0);
@@ -840,6 +896,29 @@ constexpr int kMatSpecPow = 1, kMatExample = 2;
 struct NoMid {
     __device__ void operator()() const {}
 };
+
+// Staged outputs of a wave's sub-block: its 16 x 4 pixels' f32 RGB rows (768 B) and PPM byte rows
+// (192 B, file order) in an LDS slice.
+constexpr uint32_t kWavePix = kSubW * kBlkH;
+constexpr uint32_t kSliceRgbBytes = 3 * 4 * kWavePix, kSlicePpmBytes = 3 * kWavePix;
+// The 16-B row stores of a staged slice (sub-block at (wx0, py0), rank-local rows).
+__device__ __forceinline__ void store_slice(const FrameParams& p, const FrameOut& fo, uint32_t wx0, uint32_t py0,
+                                            const float* wrgb, const uint8_t* wppm, uint32_t lane) {
+    constexpr uint32_t kRgbRow4 = kSubW * 3 / 4;    // float4 per wave row (12)
+    constexpr uint32_t kPpmRow16 = kSubW * 3 / 16;  // 16-byte words per wave row (3)
+    if (fo.rgb && lane < kBlkH * kRgbRow4) {
+        const uint32_t r = lane / kRgbRow4, c = lane % kRgbRow4;
+        float4* dst = reinterpret_cast<float4*>(fo.rgb + 3 * ((size_t)(py0 + r) * p.img_w + wx0)) + c;
+        stream16(fo.rgb, dst, reinterpret_cast<const float4*>(wrgb)[lane]);
+    }
+    if (fo.ppm && lane < kBlkH * kPpmRow16) {
+        const uint32_t r = lane / kPpmRow16, c = lane % kPpmRow16;  // r-th byte row of the block
+        const size_t row = (size_t)(p.rows - py0 - kBlkH + r);
+        uint4* dst = reinterpret_cast<uint4*>(fo.ppm + 3 * (row * p.img_w + wx0)) + c;
+        stream16(fo.ppm, dst, reinterpret_cast<const uint4*>(wppm)[lane]);
+    }
+}
+
 template <bool kCull, bool kLdsTiles, int kMat, typename Scene, typename Mid = NoMid>
 __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut& fo, const CamDev& cam, const RowMap& rm,
                                            const Scene& sc, uint32_t wx0, uint32_t py0,
@@ -879,6 +958,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
     int best_face = -1;
     for (uint32_t oi = 0; oi < p.nobj; ++oi) {
         const ObjGeom ob = sc.geom(oi);  // uniform
+        ERAY_TRACE_WAVE0(16);
         const bool direct = !kLdsTiles || ob.tri_count <= kDirectMax;
         const bool wave_bins = kCull && !direct && !coop && ob.bin_start && ob.tri_count <= kWaveBinMaxTris;
         // outside the object's pixel rectangle no primary ray can hit it (only where skipping
@@ -942,6 +1022,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
         if (!__any(have && best_obj == oi)) continue;
         const ObjGeom ob = sc.geom(oi);
         const MaterialDesc mat = sc.mat(oi);
+        ERAY_TRACE_WAVE0(17);
         if (!(have && best_obj == oi)) continue;
         const TriShade sh = sc.shade(ob.tri_begin + (uint32_t)best_face);
         P = add(C, mul(d, bt));
@@ -1117,9 +1198,8 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
     if (valid && fo.face) fo.face[(size_t)py * p.img_w + px] = have ? best_face : -1;
     if (active && aligned && wx0 + kSubW <= p.cam_w && py0 + kBlkH <= p.rows) {
         // the wave's 16 x 4 pixels leave through its own LDS slice as 16-B row stores
-        constexpr uint32_t kWavePix = kSubW * kBlkH;
-        float* wrgb = reinterpret_cast<float*>(s_rgb) + 3 * kWavePix * wave;
-        uint8_t* wppm = reinterpret_cast<uint8_t*>(s_ppm) + 3 * kWavePix * wave;
+        float* wrgb = reinterpret_cast<float*>(reinterpret_cast<char*>(s_rgb) + kSliceRgbBytes * wave);
+        uint8_t* wppm = reinterpret_cast<uint8_t*>(s_ppm) + kSlicePpmBytes * wave;
         const uint32_t wl = lane % kSubW;
         float* srgb = wrgb + 3 * (ly * kSubW + wl);
         srgb[0] = acc.r;
@@ -1132,19 +1212,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        constexpr uint32_t kRgbRow4 = kSubW * 3 / 4;    // float4 per wave row (12)
-        constexpr uint32_t kPpmRow16 = kSubW * 3 / 16;  // 16-byte words per wave row (3)
-        if (fo.rgb && lane < kBlkH * kRgbRow4) {
-            const uint32_t r = lane / kRgbRow4, c = lane % kRgbRow4;
-            float4* dst = reinterpret_cast<float4*>(fo.rgb + 3 * ((size_t)(py0 + r) * p.img_w + wx0)) + c;
-            stream16(fo.rgb, dst, reinterpret_cast<const float4*>(wrgb)[lane]);
-        }
-        if (fo.ppm && lane < kBlkH * kPpmRow16) {
-            const uint32_t r = lane / kPpmRow16, c = lane % kPpmRow16;  // r-th byte row of the block
-            const size_t row = (size_t)(p.rows - py0 - kBlkH + r);
-            uint4* dst = reinterpret_cast<uint4*>(fo.ppm + 3 * (row * p.img_w + wx0)) + c;
-            stream16(fo.ppm, dst, reinterpret_cast<const uint4*>(wppm)[lane]);
-        }
+        store_slice(p, fo, wx0, py0, wrgb, wppm, lane);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next block
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1191,8 +1259,12 @@ __device__ __forceinline__ void fill_blocks(const FrameParams& p, const FrameOut
                                             const uint8_t* detail_occ, uint32_t f, uint32_t nf, uint32_t wave,
                                             uint32_t lane, bool aligned) {
     constexpr uint32_t nwaves = kWG / 64;
+    wave = __builtin_amdgcn_readfirstlane(wave);  // (block coordinates in SGPRs)
     const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
     const uint32_t fstride = nf * nwaves;
+    const BlockFill bf = block_fill(p.img_w, lane);
+    // blocks (bx, by) with bx < full_x and by < full_y are whole 64 x 4 blocks inside the frame
+    const uint32_t full_x = aligned ? p.cam_w / kBlkW : 0u, full_y = p.rows / kBlkH;
     uint32_t occ = 0;  // detail list: lane i holds the occupancy of this wave's i-th next block
     uint32_t it = 0;
     const uint32_t nrect = detail_occ ? 0u : frame_nrect<kDev>(p, cs);
@@ -1227,7 +1299,10 @@ __device__ __forceinline__ void fill_blocks(const FrameParams& p, const FrameOut
             }
         }
         if (!mask) {
-            fill_background<kBlkW>(p, o, bx * kBlkW, by * kBlkH, aligned, lane);
+            if (bx < full_x && by < full_y)
+                fill_block_fast(p, o, bf, bx, by, lane);
+            else
+                fill_background<kBlkW>(p, o, bx * kBlkW, by * kBlkH, aligned, lane);
         } else if (mask != 0xfu) {
             for (uint32_t i = 0; i < 4; ++i)
                 if (!((mask >> i) & 1u)) fill_background<kSubW>(p, o, bx * kBlkW + i * kSubW, by * kBlkH, aligned, lane);
@@ -1258,22 +1333,28 @@ constexpr int kDenseWgs = 3;
 template <bool kCull, bool kLdsTiles, int kMat, bool kLdsScene, bool kDense = false, bool kDev = false>
 __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && !kDense) ? 1 : (kDense ? kDenseWgs : 3))  // 3 workgroups per CU where that fits
     frame_kernel(const ObjectDesc* h_objects, const LightDesc* h_lights, const TriCull* h_cull, const TriHot* h_tris,
-                 const TriShade* h_shade, uint32_t h_counts, uint32_t h_total_tris, uint32_t h_total_sub,
+                 const void* h_aux, uint32_t h_counts, uint32_t h_total_tris, uint32_t h_total_sub,
                  uint32_t h_roles, uint32_t h_band, FrameParams p) {
+    // h_aux (preloaded): the TriShade array in the LDS-scene builds (the scene preload reads it
+    // first), else the detail list (p.detail_list), whose first entry is each detail wave's first
+    // load.  (gfx950 preloads 14 argument dwords — 16 user SGPRs less the argument pointer — so
+    // h_band and everything after it are loads.)
     // h_roles (a preloaded argument, see frame_roles): the grid size, the detail workgroups and
     // the role flags, so the role decision — and the scene preload behind it — does not wait for
     // a kernel-argument load from memory
-    const uint32_t grid = h_roles & 0x7fffu;  // == gridDim.x, without the implicit-argument load
-    uint32_t detail_wgs = (h_roles >> 15) & 0x7fffu;
+    const uint32_t grid = h_roles & 0xfffu;  // == gridDim.x, without the implicit-argument load
+    uint32_t detail_wgs = (h_roles >> 12) & 0xfffu;
     bool fill_first = (h_roles >> 30) & 1u;
     const bool separate_fill = (h_roles >> 31) & 1u;
     // large objects: LDS tiles (shadow rays, brute force) and, aliased, the per-wave binned
     // primary search (first_hit ends its tile loop on a barrier, so the two never overlap)
-    constexpr size_t kTileBytes = kTriTile * (sizeof(TriHot) + ((kCull && kLdsTiles) ? sizeof(TriCull) : 0));
+    // (the culled large-mesh builds search bins wave by wave and scan shadow rays per wave: no
+    // workgroup tiles)
+    constexpr size_t kTileBytes = (kCull && kLdsTiles) ? 0 : kTriTile * sizeof(TriHot);
     constexpr size_t kBinBytes = (kCull && kLdsTiles) ? (kWG / 64) * kBinLdsBytes + 2 * (kWG / 64) * 4 : 0;
     __shared__ __attribute__((aligned(16))) char s_large[kLdsTiles ? (kTileBytes > kBinBytes ? kTileBytes : kBinBytes) : 16];
     TriHot* s_hot = reinterpret_cast<TriHot*>(s_large);
-    TriCull* s_cull = reinterpret_cast<TriCull*>(s_large + kTriTile * sizeof(TriHot));
+    TriCull* s_cull = nullptr;
     char* s_bins = s_large;
     __shared__ float4 s_rgb[kBlkW * kBlkH * 3 / 4];    // each wave's f32 RGB rows, staged
     __shared__ uint32_t s_ppm[kBlkW * kBlkH * 3 / 4];  // ... and its PPM byte rows
@@ -1284,7 +1365,7 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     // Frames in flight: the launch renders F independent frames; detail and fill workgroups are
     // dealt round-robin over them (frame v % F), so one frame's latency-bound detail chains
     // overlap the others' fill stores instead of ending the launch alone.
-    const uint32_t F = p.nframes;
+    const uint32_t F = ((h_roles >> 24) & 63u) + 1u;  // == p.nframes (the role decision needs no load)
     auto cam_state = [&](uint32_t fr) { return p.cam_state + (p.dev_slots ? fr : 0u); };
     // detail sub-blocks per frame (device-camera mode: counted by the setup kernels; the most of
     // any frame sizes the detail roles), and the small-scene fill reservation chosen from that
@@ -1311,9 +1392,23 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     ERAY_TRACE_POINT(0);
     // ---- detail sub-blocks -------------------------------------------------------------------
     if (bid < nd) {
-        // the ordered detail list's heavy count (no count: every iteration shares its work)
+        // the ordered detail list's heavy count: the threshold of the cooperative (workgroup-shared)
+        // sub-blocks in builds that keep those paths (brute-force large meshes; no count: every
+        // iteration shares its work)
         const bool counted = kLdsTiles && !(p.launch_flags & kLaunchSharedDetail);
-        const uint32_t heavy0 = (counted && p.detail_heavy) ? load_const(p.detail_heavy, 0) : 0xffffffffu;
+        const uint32_t heavy0 =
+            (!kCull && counted && p.detail_heavy) ? load_const(p.detail_heavy, 0) : 0xffffffffu;
+        // the detail list (preloaded in h_aux outside the LDS-scene builds, which have none)
+        const uint32_t* list_base = kLdsScene ? p.detail_list : static_cast<const uint32_t*>(h_aux);
+        // One camera (args mode): the wave's first list entry (role bid) depends on preloaded
+        // arguments only, so it is loaded first, beside the kernel-argument loads that follow
+        // (branch-free: without a list it reads a word of the descriptors, unused).
+        uint32_t e_first = 0;
+        if constexpr (!kDev && !kLdsScene) {
+            const uint32_t c = (bid / F) * nwaves + wave;
+            e_first = vload_u32(list_base ? list_base : reinterpret_cast<const uint32_t*>(h_objects),
+                                list_base && c < h_total_sub ? c : 0u);
+        }
         // snake order for the ordered (heavy-first) lists of binned meshes
         constexpr bool kSnake = kLdsTiles;
         const RowMap rm{p.row0, h_band & 31u, h_band >> 5};
@@ -1323,24 +1418,32 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
         const uint32_t roles = max(nd, F);
         for (uint32_t v = bid; v < roles; v += nd) {
             const uint32_t fr = v % F, kw = v / F, nk = (roles - fr + F - 1) / F;
+            const uint32_t c0 = kw * nwaves;
             const CamState* cs = cam_state(fr);
             const uint32_t total = kDev ? load_const(&cs->total_sub, 0) : h_total_sub;
+            // (per-frame setup slots exist only in device-camera mode)
+            const uint32_t slot = (kDev && p.dev_slots) ? fr : 0u;
+            const uint32_t* dlist = list_base ? (kDev ? list_base + (size_t)slot * p.dlist_stride : list_base) : nullptr;
             const FrameOut fo = frame_out(p, fr);
-            const uint32_t slot = p.dev_slots ? fr : 0u;
             const ObjectDesc* objs = h_objects + (size_t)slot * nobj;
             const TriCull* culls = h_cull ? h_cull + (size_t)slot * h_total_tris : nullptr;
-            const uint32_t* dlist = p.detail_list ? p.detail_list + (size_t)slot * p.dlist_stride : nullptr;
             const uint32_t nrect = dlist ? 0u : frame_nrect<kDev>(p, cs);
             const CamDev cam = frame_camera<kDev>(p, cs);
             // a split list (camera paths): the frame's heavy sub-blocks from the front, the light
-            // ones from the back (bins.hip detail_list_kernel)
+            // ones from the back (bins.hip detail_list_kernel) — list positions always follow the
+            // setup's heavy count; `heavy` is the cooperative threshold (none without a count)
             const bool split = kDev && p.dlist_split && dlist;
-            const uint32_t heavy = split ? (counted ? load_const(&cs->heavy_sub, 0) : 0xffffffffu) : heavy0;
-            auto lpos = [&](uint32_t j) { return split && j >= heavy ? p.dlist_split - 1u - (j - heavy) : j; };
+            const uint32_t split_heavy = split ? load_const(&cs->heavy_sub, 0) : 0u;
+            const uint32_t heavy = split ? (counted ? split_heavy : 0xffffffffu) : heavy0;
+            auto lpos = [&](uint32_t j) {
+                return split && j >= split_heavy ? p.dlist_split - 1u - (j - split_heavy) : j;
+            };
             // detail sub-block j (enumeration order) -> sub-block coordinates
-            auto locate = [&](uint32_t j, int32_t& sx, int32_t& sy) {
+            auto locate = [&](uint32_t j, int32_t& sx, int32_t& sy, bool first = false) {
                 if (dlist) {
-                    const uint32_t e = dlist[lpos(j)];
+                    const uint32_t e = __builtin_amdgcn_readfirstlane((!kDev && !kLdsScene && first && v == bid)
+                                                                          ? e_first
+                                                                          : vload_u32(dlist, lpos(j)));
                     sx = (int32_t)(e & 0xffffu);
                     sy = (int32_t)(e >> 16);
                     return;
@@ -1359,16 +1462,16 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
             };
             // the wave's first sub-block and its camera rays, before the scene is in: the kernel
             // arguments' scalar loads and the ray arithmetic overlap the preload's round trip
-            const uint32_t c0 = kw * nwaves;
             int32_t sx0 = 0, sy0 = 0;
             f3 d0;
             constexpr bool kGivenRay = true;
             auto first_rays = [&]() {
-                if (c0 + wave < total) locate(c0 + wave, sx0, sy0);
+                if (c0 + wave < total) locate(c0 + wave, sx0, sy0, true);
+                ERAY_TRACE_WAVE0(11);
                 d0 = camera_dir(cam, p, (uint32_t)sx0 * kSubW + lane % kSubW, cam_row(rm, (uint32_t)sy0 * kBlkH + lane / kSubW));
                 asm volatile("" : "+v"(d0.x), "+v"(d0.y), "+v"(d0.z));  // here, not after the barrier
             };
-            auto detail = [&](const auto& sc) {
+            auto detail = [&](const auto& sc, const uint32_t pobj, const uint32_t* pstart) {
                 // Rounds of nk * 4 sub-blocks, dealt in snake order: in odd rounds the last
                 // workgroup takes the first sub-blocks, so the waves whose first sub-block came
                 // from the ordered list's heavy head (the longest chains) take the light tail
@@ -1383,22 +1486,9 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
                     return odd ? first + (nwaves - 1 - wave) : first + wave;
                 };
                 // Binned meshes with a detail list: the wave's next sub-block — its list entry and
-                // its bin range in the first binned object — is loaded during the current one
-                // (vector loads, used one sub-block later), so a round after the first starts
-                // with its search, not with two dependent round trips.
-                uint32_t pobj = ~0u;
-                const uint32_t* pstart = nullptr;
-                if constexpr (kLdsTiles && kCull) {
-                    if (dlist)
-                        for (uint32_t oi = 0; oi < nobj; ++oi) {
-                            const ObjGeom g = sc.geom(oi);
-                            if (g.bin_start) {
-                                pobj = oi;
-                                pstart = g.bin_start;
-                                break;
-                            }
-                        }
-                }
+                // its bin range in the first binned object pobj (bin starts pstart) — is loaded
+                // during the current one (vector loads, used one sub-block later), so a round
+                // after the first starts with its search, not with two dependent round trips.
                 uint32_t nx_e = 0, nx_lo = 0, nx_hi = 0;  // (VGPRs: the loads' results)
                 bool nx_range = false;                    // nx_lo / nx_hi were issued
                 for (uint32_t r = 0;; ++r) {  // workgroup-uniform
@@ -1442,20 +1532,39 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
                     // workgroup in builds that keep the cooperative paths, render_sub)
                     render_sub<kCull, kLdsTiles, kMat>(p, fo, cam, rm, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH,
                                                        active, s_hot, s_cull, s_bins, s_rgb, s_ppm, aligned,
-                                                       (kGivenRay && r == 0) ? &d0 : nullptr, coop,
-                                                       pre, pobj, mid);
+                                                       (kGivenRay && r == 0) ? &d0 : nullptr, coop, pre, pobj, mid);
                 }
             };
             if constexpr (kLdsScene) {
                 if (v != bid) __syncthreads();  // the previous frame's reads of the LDS scene are done
-                const FrameHot hf{objs, h_lights, culls, h_tris, h_shade, h_counts, h_total_tris, h_total_sub, grid};
+                const FrameHot hf{objs, h_lights, culls, h_tris, static_cast<const TriShade*>(h_aux), h_counts, h_total_tris,
+                                  h_total_sub, grid};
                 const SceneLds sc = preload_scene(hf, dyn, first_rays);
                 __syncthreads();
-                detail(sc);
+                detail(sc, ~0u, nullptr);
             } else {
                 const SceneGlobal sc{p, objs, culls};
-                first_rays();
-                detail(sc);
+                uint32_t pobj = ~0u;  // the first binned object (culled large-mesh builds with a list)
+                const uint32_t* pstart = nullptr;
+                if constexpr (kLdsTiles && kCull) {
+                    // the first object's descriptor is loaded before the list entry is waited for:
+                    // the first sub-block's two inputs in one round trip
+                    const ObjGeom g0 = nobj ? sc.geom(0) : ObjGeom{};
+                    first_rays();
+                    if (dlist)
+                        for (uint32_t oi = 0; oi < nobj; ++oi) {
+                            const ObjGeom g = oi == 0 ? g0 : sc.geom(oi);
+                            if (g.bin_start) {
+                                pobj = oi;
+                                pstart = g.bin_start;
+                                break;
+                            }
+                        }
+                } else {
+                    first_rays();
+                }
+                ERAY_TRACE_WAVE0(12);
+                detail(sc, pobj, pstart);
             }
         }
         ERAY_TRACE_POINT(1);
@@ -1512,14 +1621,22 @@ hipError_t launch_tri_precompute(const float* pos, const float* nrm, const float
 namespace {
 // Persistent grid: as many workgroups as are resident at once (occupancy API), capped by the
 // work (fill blocks or detail sub-blocks, whichever needs more workgroups).
-// frame_kernel's h_roles: grid | detail_wgs << 15 | fill_first << 30 | separate_fill << 31
+// frame_kernel's h_roles (a preloaded dword): grid | detail_wgs << 12 | (frames - 1) << 24 |
+// fill_first << 30 | separate_fill << 31 (grid <= kMaxFrameGrid, frames <= kMaxFramesPerLaunch)
+constexpr uint32_t kMaxFrameGrid = 4095;
 uint32_t frame_roles(uint32_t grid, const FrameParams& q) {
-    return (grid & 0x7fffu) | ((q.detail_wgs & 0x7fffu) << 15) | ((q.fill_first ? 1u : 0u) << 30) |
+    return (grid & 0xfffu) | ((q.detail_wgs & 0xfffu) << 12) | (((q.nframes - 1u) & 63u) << 24) |
+           ((q.fill_first ? 1u : 0u) << 30) |
            ((q.separate_fill ? 1u : 0u) << 31);
 }
 
-// frame_kernel's h_band: the band shift and stride of the row mapping in one preloaded dword
+// frame_kernel's h_band: the band shift and stride of the row mapping in one dword
 uint32_t band_word(const FrameParams& q) { return (q.band_shift & 31u) | (q.band_stride << 5); }
+// frame_kernel's h_aux: TriShade records (LDS-scene builds) or the detail list
+template <bool K>
+const void* aux_arg(const FrameParams& q) {
+    return K ? static_cast<const void*>(q.shade) : static_cast<const void*>(q.detail_list);
+}
 
 uint32_t device_cus() {
     static const uint32_t cus = [] {  // (thread-safe initialisation)
@@ -1564,7 +1681,7 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
         wg_cu = per_cu;
     }
     const uint32_t cus = device_cus();
-    const uint32_t grid = min(want, (uint32_t)wg_cu * cus);
+    const uint32_t grid = min(min(want, (uint32_t)wg_cu * cus), kMaxFrameGrid);
     // Workgroups kept for the fill so that it overlaps a large detail area instead of following
     // it: one per 64 background blocks, at most 1/share of the grid.  Measured (graph-replayed
     // frames, profiles/ab/ab_knobs*.log): the fill needs enough store-issuing waves on every CU
@@ -1629,7 +1746,7 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
             if ((e = hipEventRecord(lc.fork, s)) != hipSuccess || (e = hipStreamWaitEvent(lc.side, lc.fork, 0)) != hipSuccess)
                 return e;
             if ((e = launch_k(frame_kernel<C, L, M, K, D, V>, dgrid, dyn, s, lc.frame_t, q.objects, q.lights, q.cull,
-                              q.tris, q.shade, q.nobj | (q.nlights << 16), q.total_tris, q.total_sub,
+                              q.tris, aux_arg<K>(q), q.nobj | (q.nlights << 16), q.total_tris, q.total_sub,
                               frame_roles(dgrid, q), band_word(q), q)) != hipSuccess)
                 return e;
             if ((e = launch_k(fill_kernel<V>, fgrid, 0, lc.side, lc.fill_t, q)) != hipSuccess) return e;
@@ -1639,7 +1756,7 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
         }
     }
     return launch_k(frame_kernel<C, L, M, K, D, V>, grid, dyn, s, lc.frame_t, q.objects, q.lights, q.cull, q.tris,
-                    q.shade, q.nobj | (q.nlights << 16), q.total_tris, q.total_sub, frame_roles(grid, q), band_word(q),
+                    aux_arg<K>(q), q.nobj | (q.nlights << 16), q.total_tris, q.total_sub, frame_roles(grid, q), band_word(q),
                     q);
 }
 
@@ -1668,7 +1785,8 @@ hipError_t launch_frame_cs(const FrameParams& p, uint32_t want, const LaunchCtx&
 }  // namespace
 
 hipError_t launch_render(const FrameParams& p, const LaunchCtx& lc, hipStream_t s) {
-    if (p.nframes < 1 || ((p.aa || p.bounces) && p.nframes != 1)) return hipErrorInvalidValue;
+    if (p.nframes < 1 || p.nframes > kMaxFramesPerLaunch || ((p.aa || p.bounces) && p.nframes != 1))
+        return hipErrorInvalidValue;
     if (p.aa || p.bounces) return launch_trace(p, lc, s);
     const uint32_t by_n = (p.rows + kBlkH - 1) / kBlkH;
     const uint32_t nblk = p.tiles_x * by_n;

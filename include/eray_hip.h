@@ -362,8 +362,13 @@ int eray_comm_destroy(void* nccl_comm);
  * 64-pixel row segment whose pixels are all equal as one 4-byte word, the others as their bytes
  * (a frame is mostly the miss colour, engine.rs:212), so the transfer into rank 0 shrinks with
  * the background; the packed sizes are exchanged first and the call synchronises the context's
- * stream once (not capturable in a graph).  Replaces the reference's single-process image
- * write (engine.rs:85-98 render_to_path -> save_as_ppm). */
+ * stream once (not capturable in a graph).  Without bands the ranks exchange a status word
+ * first (one small all-gather, one stream synchronisation).  Either way every rank learns every
+ * rank's verdict on its own buffers before any rows move: a rank with a null `local` (or rank 0
+ * with a null `frame`) still takes part, and every rank returns an error.  (A rank that cannot
+ * allocate its staging buffer aborts the communicator, so the others fail instead of waiting.)
+ * Replaces the reference's single-process image write (engine.rs:85-98 render_to_path ->
+ * save_as_ppm). */
 int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8_t* frame, uint32_t height,
                      uint32_t width, uint32_t band_rows);
 /* `nframes` frames at once (frame k: local + k * local_stride on every rank, frames + k *
@@ -379,8 +384,15 @@ int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8
  *     ranks exchange their rectangles once per camera setup (the first call after a new setup
  *     synchronises the context's stream; a batch size's first call allocates); every later call
  *     only enqueues kernels and transfers — no host round trip, capturable in a HIP graph.
- *     Needs width % 16 == 0 and 16-byte aligned buffers and strides (else ERAY_E_INVALID_ARGUMENT
- *     on every rank).
+ *     Needs width % 16 == 0 (else ERAY_E_INVALID_ARGUMENT on every rank) and 16-byte aligned
+ *     buffers and strides.  Collective safety: the ranks choose their path from shared arguments
+ *     and their frames' source (the same on every rank: SPMD); a rank whose own buffers or frames
+ *     are unusable still takes part — in a new plan's exchange, whose verdict every rank then
+ *     returns, or in a cached plan's transfers, whose headers carry its error — and returns its
+ *     error; a root assembles a batch only when every transfer's header says ERAY_OK and the
+ *     plan's source, otherwise it writes none of the batch's frames and its context's next
+ *     eray_gather_frames returns ERAY_E_INVALID_ARGUMENT.  A rank that cannot allocate its
+ *     transfer buffer aborts the communicator (the others fail instead of waiting).
  *   ERAY_GATHER_ROTATE_ROOT   — with ERAY_GATHER_SCENE_CAMERA: frame k of the batch is assembled
  *     on rank k % nranks instead of rank 0, so the assembly writes and the inbound xGMI traffic of
  *     a stream of frames spread over every GPU.  Rank r's frames k = r, r + nranks, ... land at

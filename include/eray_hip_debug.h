@@ -47,11 +47,24 @@ int eray_debug_scene_gather(eray_ctx* ctx, const uint8_t* staging, uint8_t* fram
 int eray_debug_scene_gather_batch(eray_ctx* ctx, const uint8_t* staging, uint8_t* frames, uint32_t nframes,
                                   uint32_t height, uint32_t width, uint32_t band_rows, uint32_t nranks, uint32_t rotate);
 /* Host only: rank `rank`'s part of a batch's scene-camera gather when rank q packs rank_bytes[q]
- * bytes per frame.  out (u64, cap >= 3 + nframes + 9 nranks): buffer bytes, frames it assembles,
- * transfer count; per frame its pack's offset in the buffer; per rank q the receive offset of q's
- * packs; per transfer peer, 1 send / 0 receive, offset, bytes. */
+ * bytes per frame.  out (u64, cap >= 5 + nframes + 12 nranks): buffer bytes, frames it assembles,
+ * transfer count T; per frame its pack's offset in the buffer; per rank q the receive offset of
+ * q's packs; per transfer peer, 1 send / 0 receive, offset, bytes (a transfer ends with its
+ * sender's 16-byte header); the number of headers the rank writes and their offsets (T + 1
+ * slots); per rank q the offset of q's header in the rank's receive area (~0: unused). */
 int eray_debug_gather_schedule(const uint32_t* rank_bytes, uint32_t nranks, uint32_t rank, uint32_t nframes,
                                uint32_t rotate, uint64_t* out, uint32_t cap);
+/* Host only: the headers rank `rank` writes into (a host copy of) its transfer buffer — its own
+ * verdict `status` and its frames' source (kind, key) — and a root's verdict on a received
+ * buffer (every header it uses ERAY_OK and the plan's source; else ERAY_E_INVALID_ARGUMENT and the
+ * root writes none of the batch's frames). */
+int eray_debug_gather_write_headers(const uint32_t* rank_bytes, uint32_t nranks, uint32_t rank, uint32_t nframes,
+                                    uint32_t rotate, int32_t status, uint32_t kind, uint64_t key, uint8_t* buf);
+int eray_debug_gather_check(const uint32_t* rank_bytes, uint32_t nranks, uint32_t rank, uint32_t nframes,
+                            uint32_t rotate, uint32_t kind, uint64_t key, const uint8_t* buf);
+/* Host only: a new gather plan's verdict on rank `rank` from every rank's exchange record
+ * (status, kind, key low, key high; 4 words each) — all ranks accept or all fail together. */
+int eray_debug_plan_verdict(const int32_t* records, uint32_t nranks, uint32_t rank);
 /* Host only (no context, no GPU): rank `rank`'s share of the scene-camera gather of `nranks` ranks
  * for objects whose pixel rectangles are `rects` (n x (x0, x1, y0, y1), camera rows) — its rows, its
  * rectangles in local rows / 16-pixel column groups, each one's offset in its per-frame pack.  out:

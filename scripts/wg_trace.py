@@ -1,6 +1,7 @@
 """Per-workgroup timeline of one frame_kernel launch (diagnostics; needs the trace build,
 scripts/build_trace.sh, selected with ERAY_LIB=eray_amd/lib/liberay_hip_trace.so).
-Usage: python scripts/wg_trace.py MESH W H"""
+Usage: python scripts/wg_trace.py MESH W H [SLOTS]   (SLOTS > 1: a ring of frame slots, one frame
+per launch, so that the traced frame's stores go to HBM when the ring exceeds the Infinity Cache)"""
 import ctypes as C
 import os
 import sys
@@ -19,21 +20,24 @@ mesh = load_obj_file(sys.argv[1])
 W, H = int(sys.argv[2]), int(sys.argv[3])
 ctx = capi.Context(0)
 sc = MainScene(ctx, *mesh, W, H, fov=frame_camera_fov(W, H))
-rgb = ctx.empty((H, W, 3), np.float32)
-ppm = ctx.empty((H, W, 3), np.uint8)
+slots = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+rgb = ctx.empty((slots, H, W, 3), np.float32)
+ppm = ctx.empty((slots, H, W, 3), np.uint8)
 lib = capi.lib()
 lib.eray_debug_read_trace.argtypes = [C.c_void_p, C.c_size_t]
 kw = dict(out_rgb=rgb.ptr, out_ppm=ppm.ptr)
+if slots > 1:
+    kw["ring"] = capi.frame_ring(slots, H, W, 1)
 ctx.render_frames(50, W, H, **kw)
 ctx.synchronize()
-n = 8192 * 16
+n = 8192 * 64  # (scripts/microbench/render_trace.hip kTraceSlots)
 for rep in range(3):
     assert lib.eray_debug_clear_trace() == 0
     ctx.render_frames(1, W, H, **kw)
     ctx.synchronize()
     buf = (C.c_uint64 * n)()
     assert lib.eray_debug_read_trace(buf, n) == 0
-    t = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 16).astype(np.int64)
+    t = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 64).astype(np.int64)
     used = t[:, 0] > 0
     t = t[used]
     t0 = t[:, 0].min()
@@ -48,24 +52,33 @@ for rep in range(3):
         print(f"  detail {det.sum()}: end p10 {np.percentile(us(t[det, 1]), 10):.2f} p50 {np.median(us(t[det, 1])):.2f} "
               f"p90 {np.percentile(us(t[det, 1]), 90):.2f} max {us(t[det, 1]).max():.2f}; duration p50 {np.median(d):.2f} "
               f"p90 {np.percentile(d, 90):.2f} max {d.max():.2f}")
-        ph = t[det][:, 4:8] / 100.0
-        ok = (ph > 0).all(axis=1)
-        ph = ph[ok]
-        print(f"  wave 0's latest sub-block: search p50 {np.median(ph[:, 1] - ph[:, 0]):.2f} us "
-              f"(p90 {np.percentile(ph[:, 1] - ph[:, 0], 90):.2f}), shading p50 {np.median(ph[:, 2] - ph[:, 1]):.2f} "
-              f"(p90 {np.percentile(ph[:, 2] - ph[:, 1], 90):.2f}), outputs p50 {np.median(ph[:, 3] - ph[:, 2]):.2f}, "
-              f"to workgroup end p50 {np.median(t[det][ok, 1] / 100.0 - ph[:, 3]):.2f}; first start p50 "
-              f"{np.median(us(t[det][ok, 4])):.2f}")
-        P = t[det][ok]
-        names = [(4, 8, "range+rays"), (8, 9, "barrier1"), (9, 10, "chunks"), (10, 11, "barrier2"),
-                 (11, 12, "re-test"), (12, 5, "to object-loop end"), (5, 13, "hit records"), (13, 14, "shadow"),
+        names = [(4, 16, "ObjGeom"), (16, 8, "rays+bbox"), (8, 9, "first chunk"), (9, 10, "chunks"),
+                 (10, 5, "to object-loop end"), (5, 17, "MaterialDesc"), (17, 13, "hit records"), (13, 14, "shadow"),
                  (14, 6, "shading"), (6, 7, "outputs")]
-        parts = []
-        for a, b, nm in names:
-            m = (P[:, a] > 0) & (P[:, b] > 0)
-            if m.any():
-                parts.append(f"{nm} {np.median((P[m, b] - P[m, a]) / 100.0):.2f}")
-        print("  wave 0 phases p50 (us):", ", ".join(parts))
+        S = t[det]
+        m = (S[:, 32 + 11] > 0) & (S[:, 32 + 12] > 0) & (S[:, 32 + 4] > 0)
+        if m.any():
+            print(f"  startup p50 (us): WG start -> list entry {np.median((S[m, 43] - S[m, 0]) / 100.0):.2f}, "
+                  f"-> binned object {np.median((S[m, 44] - S[m, 43]) / 100.0):.2f}, "
+                  f"-> first sub-block {np.median((S[m, 36] - S[m, 44]) / 100.0):.2f}")
+        for label, off in (("first", 32), ("latest", 0)):
+            P = t[det]
+            ok = (P[:, off + 4] > 0) & (P[:, off + 7] > 0)
+            P = P[ok]
+            if not len(P):
+                continue
+            start = us(P[:, off + 4])
+            total = (P[:, off + 7] - P[:, off + 4]) / 100.0
+            parts = []
+            for a, b, nm in names:
+                m = (P[:, off + a] > 0) & (P[:, off + b] > 0)
+                if m.any():
+                    parts.append(f"{nm} {np.median((P[m, off + b] - P[m, off + a]) / 100.0):.2f}")
+            ch = P[:, off + 15]
+            print(f"  wave 0's {label} sub-block: start p50 {np.median(start):.2f}, length p50 {np.median(total):.2f} "
+                  f"p90 {np.percentile(total, 90):.2f}; chunks p50 {np.median(ch):.0f} p90 {np.percentile(ch, 90):.0f} "
+                  f"max {ch.max()}")
+            print(f"    phases p50 (us): " + ", ".join(parts))
         hist, edges = np.histogram(us(t[det, 1]), bins=12)
         print("  detail end histogram:", " ".join(f"{e:.1f}:{h}" for e, h in zip(edges, hist)))
     if fil.any():

@@ -181,10 +181,17 @@ def test_two_rank_scene_camera_gather_layout(tmp_path, bands):
     assert got.shape == want.shape and np.array_equal(got, want)
 
 
-def _rotating_gather_worker(rank, world, port, out_dir, bands, B, rotate):
+KEY = 0x1234_5678_9ABC_DEF0  # the frames' source key every rank's headers carry (kind 1: scene camera)
+
+
+def _rotating_gather_worker(rank, world, port, out_dir, bands, B, rotate, fail_rank=-1, foreign_rank=-1):
     """Every rank packs B different frames (frame k: the rendered rows shifted by 37 k) where the
-    library's schedule puts them, runs the schedule's point-to-point transfers over gloo, and
-    assembles the frames it roots from its receive area."""
+    library's schedule puts them, writes its transfer headers (the library's), runs the
+    schedule's point-to-point transfers over gloo, and each root checks the headers it received
+    (the library's assembly check) before it assembles its frames from its receive area.
+    fail_rank: that rank cannot use its arguments (status ERAY_E_INVALID_ARGUMENT in its headers,
+    no packs — the library's fail-safe path); foreign_rank: that rank's frames come from another
+    source key.  Each rank saves the status it would return."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from eray_amd import capi
@@ -198,19 +205,27 @@ def _rotating_gather_worker(rank, world, port, out_dir, bands, B, rotate):
     local[: sp["rows"]] = _render_rows(band_camera_rows(rank, world, H, bands))
     lays = [None] * world
     dist.all_gather_object(lays, lay)
-    sched = capi.gather_schedule([l["bytes"] for l in lays], rank, B, rotate)
+    nb = [l["bytes"] for l in lays]
+    sched = capi.gather_schedule(nb, rank, B, rotate)
     buf = np.zeros(max(sched["need"], 1), np.uint8)
-    for k in range(B):
-        at = sched["pack"][k]
-        buf[at:at + lay["bytes"]] = _pack((local.astype(np.int32) + 37 * k).astype(np.uint8), lay, W)
+    status = capi.E_INVALID_ARGUMENT if rank == fail_rank else 0
+    if not status:
+        for k in range(B):
+            at = sched["pack"][k]
+            buf[at:at + lay["bytes"]] = _pack((local.astype(np.int32) + 37 * k).astype(np.uint8), lay, W)
+    capi.gather_write_headers(nb, rank, B, rotate, buf, status=status, key=KEY + (rank == foreign_rank))
     t = torch.from_numpy(buf)
     reqs = [(dist.isend if op["send"] else dist.irecv)(t[op["off"]:op["off"] + op["bytes"]], int(op["peer"]))
             for op in sched["ops"]]
     for q in reqs:
         q.wait()
-    for j in range(sched["mine"]):
-        packs = [buf[sched["recv"][q] + j * lays[q]["bytes"]:][:lays[q]["bytes"]] for q in range(world)]
-        np.save(os.path.join(out_dir, f"r{rank}_f{j}.npy"), _assemble(packs, lays, H, W, bands, world))
+    if not status and sched["mine"]:
+        status = capi.gather_check(nb, rank, B, rotate, buf, key=KEY)
+    if not status:
+        for j in range(sched["mine"]):
+            packs = [buf[sched["recv"][q] + j * lays[q]["bytes"]:][:lays[q]["bytes"]] for q in range(world)]
+            np.save(os.path.join(out_dir, f"r{rank}_f{j}.npy"), _assemble(packs, lays, H, W, bands, world))
+    np.save(os.path.join(out_dir, f"status{rank}.npy"), np.array([status]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -241,6 +256,54 @@ def test_two_rank_gather_schedule_rotating_roots(tmp_path, B, rotate):
         packs = [_pack((locals_[q].astype(np.int32) + 37 * k).astype(np.uint8), lays[q], W) for q in range(world)]
         assert np.array_equal(got, _assemble(packs, lays, H, W, bands, world)), k
     assert np.array_equal(np.load(str(tmp_path / "r0_f0.npy")), full)
+    assert all(np.load(str(tmp_path / f"status{q}.npy"))[0] == 0 for q in range(world))
+
+
+@pytest.mark.parametrize("fail_rank,foreign_rank", [(1, -1), (0, -1), (-1, 1)])
+def test_two_rank_gather_with_a_failed_rank(tmp_path, fail_rank, foreign_rank):
+    """ADVICE r04 / VERDICT r04 item 5: a rank that cannot use its own arguments (null or unaligned
+    buffers, frames it did not render) still takes part in the batch's transfers — its headers
+    carry its error — and returns the error; the root of every frame finds the failed header
+    (or, foreign_rank, a header of another source) and refuses the batch.  Both ranks return an
+    error, no frame is written, and neither blocks (the gloo ranks join)."""
+    world, bands, B = 2, 4, 3
+    mp.start_processes(_rotating_gather_worker,
+                       args=(world, _free_port(), str(tmp_path), bands, B, True, fail_rank, foreign_rank),
+                       nprocs=world, join=True, start_method="spawn")
+    from eray_amd import capi
+    for q in range(world):
+        assert np.load(str(tmp_path / f"status{q}.npy"))[0] == capi.E_INVALID_ARGUMENT, q
+    assert not [f for f in os.listdir(tmp_path) if f.startswith("r")], "a root wrote a frame"
+
+
+def _plan_verdict_worker(rank, world, port, out_dir, fail_rank, key_rank):
+    """Each rank's record of a new plan exchange (status, kind, key), all-gathered over gloo, and
+    the library's verdict on it (exchange_plan's)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from eray_amd import capi
+    status = capi.E_OUT_OF_MEMORY if rank == fail_rank else 0
+    key = KEY + (rank == key_rank)
+    rec = (status, 1, key & 0x7FFFFFFF, (key >> 32) & 0x7FFFFFFF)
+    recs = [None] * world
+    dist.all_gather_object(recs, rec)
+    np.save(os.path.join(out_dir, f"verdict{rank}.npy"), np.array([capi.plan_verdict(recs, rank)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_rank,key_rank,want", [(-1, -1, 0), (1, -1, "E_OUT_OF_MEMORY"),
+                                                     (0, -1, "E_OUT_OF_MEMORY"), (-1, 0, "E_INVALID_ARGUMENT")])
+def test_two_rank_plan_exchange_fails_together(tmp_path, fail_rank, key_rank, want):
+    """A new plan's exchange (eray_gather_frames' first call after a new setup): one rank's own
+    failure (an allocation, a frame lookup) or frames of another source makes every rank return
+    the same kind of error; otherwise every rank accepts the plan."""
+    world = 2
+    mp.start_processes(_plan_verdict_worker, args=(world, _free_port(), str(tmp_path), fail_rank, key_rank),
+                       nprocs=world, join=True, start_method="spawn")
+    from eray_amd import capi
+    expect = 0 if want == 0 else getattr(capi, want)
+    assert [int(np.load(str(tmp_path / f"verdict{q}.npy"))[0]) for q in range(world)] == [expect] * world
 
 
 def test_gather_schedules_pair_up():
@@ -263,8 +326,10 @@ def test_gather_schedules_pair_up():
                         if op["send"]:
                             m = [o for o in S[op["peer"]]["ops"] if not o["send"] and o["peer"] == r]
                             assert len(m) == 1 and m[0]["bytes"] == op["bytes"], (N, B, rotate, r, op)
-                    sends = sum(op["bytes"] for op in S[r]["ops"] if op["send"])
-                    assert sends == nb[r] * (B - S[r]["mine"]) or nb[r] == 0
+                    send_ops = [op for op in S[r]["ops"] if op["send"]]
+                    # (every transfer ends with its sender's 16-B header)
+                    assert sum(op["bytes"] for op in send_ops) == nb[r] * (B - S[r]["mine"]) + 16 * len(send_ops)
+                    assert len(S[r]["headers"]) == len(send_ops) + (1 if S[r]["mine"] else 0)
 
 
 def test_bench_frames_buffers_match_the_schedule():

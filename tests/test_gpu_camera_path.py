@@ -168,10 +168,13 @@ def standin70k():
             np.ascontiguousarray(t[ft].reshape(-1, 6)))
 
 
-@pytest.mark.parametrize("flags", [0, capi.RENDER_DENSE_DETAIL | capi.RENDER_SEPARATE_FILL])
+@pytest.mark.parametrize("flags", [0, capi.RENDER_DENSE_DETAIL | capi.RENDER_SEPARATE_FILL,
+                                   capi.RENDER_SHARED_DETAIL])
 def test_binned_camera_path_equals_brute_force(gpu, standin70k, flags):
     """A 70k-face object: each path frame's bins are rebuilt on the device; the frame equals the
-    brute-force scan for that camera."""
+    brute-force scan for that camera.  RENDER_SHARED_DETAIL: the split detail list's
+    light sub-blocks sit at the back of the list, so list positions must follow the setup's heavy
+    count whatever the flag says about sharing work."""
     W, H = 480, 270
     sc = MainScene(gpu, *standin70k, W, H, texture=256, fov=(16.0, 9.0))
     out = Out(gpu, W, H)
