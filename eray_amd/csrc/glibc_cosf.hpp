@@ -31,41 +31,21 @@
 namespace eray {
 namespace libm {
 
-struct SinCosCoeffs {
-    double sign[4];
-    double hpi_inv;  // 2/pi * 2^24
-    double hpi;      // pi/2
-    double c0, c1, c2, c3, c4;
-    double s1, s2, s3;
-};
+// The published coefficient tables (sincosf_data.c): the sin/cos polynomials' coefficients, 2/pi
+// scaled by 2^24 and pi/2.  The library's second table (quadrants with bit 1 set) differs from the
+// first only in the cos coefficients' signs; every cos-polynomial step is an FMA or a product, and
+// fma(a, -b, -c) == -fma(a, b, c) and (float)-v == -(float)v exactly (round-to-nearest is
+// symmetric; a cos value on [-pi/4, pi/4] is never 0), so the second table's result is the first's
+// negated.  Immediates here, not a table in memory: on the GPU a per-lane table pointer made every
+// coefficient a dependent vector load.
+constexpr double kHpiInv = 0x1.45F306DC9C883p+23;  // 2/pi * 2^24
+constexpr double kHpi = 0x1.921FB54442D18p0;       // pi/2
+constexpr double kC0 = 0x1p0, kC1 = -0x1.ffffffd0c621cp-2, kC2 = 0x1.55553e1068f19p-5,
+                 kC3 = -0x1.6c087e89a359dp-10, kC4 = 0x1.99343027bf8c3p-16;
+constexpr double kS1 = -0x1.555545995a603p-3, kS2 = 0x1.1107605230bc4p-7, kS3 = -0x1.994eb3774cf24p-13;
 
-ERAY_HD inline const SinCosCoeffs& sincos_coeffs(int which) {
-    static const SinCosCoeffs kTab[2] = {
-        {{1.0, -1.0, -1.0, 1.0},
-         0x1.45F306DC9C883p+23,
-         0x1.921FB54442D18p0,
-         0x1p0,
-         -0x1.ffffffd0c621cp-2,
-         0x1.55553e1068f19p-5,
-         -0x1.6c087e89a359dp-10,
-         0x1.99343027bf8c3p-16,
-         -0x1.555545995a603p-3,
-         0x1.1107605230bc4p-7,
-         -0x1.994eb3774cf24p-13},
-        {{1.0, -1.0, -1.0, 1.0},
-         0x1.45F306DC9C883p+23,
-         0x1.921FB54442D18p0,
-         -0x1p0,
-         0x1.ffffffd0c621cp-2,
-         -0x1.55553e1068f19p-5,
-         0x1.6c087e89a359dp-10,
-         -0x1.99343027bf8c3p-16,
-         -0x1.555545995a603p-3,
-         0x1.1107605230bc4p-7,
-         -0x1.994eb3774cf24p-13},
-    };
-    return kTab[which];
-}
+// the table's sign[q & 3] = {1, -1, -1, 1}: negative when bits 0 and 1 of q differ
+ERAY_HD inline double quadrant_sign(int q) { return ((q ^ (q >> 1)) & 1) ? -1.0 : 1.0; }
 
 ERAY_HD inline uint32_t inv_pio4(int i) {
     static const uint32_t kInvPio4[24] = {
@@ -91,21 +71,23 @@ ERAY_HD inline double fma_d(double a, double b, double c) {
 #endif
 }
 
-// sin (n even) or cos (n odd) polynomial of the reduced argument, rounded to float.
-ERAY_HD inline float sincos_poly(double x, double x2, const SinCosCoeffs& p, int n) {
+// sin (n even) or cos (n odd) polynomial of the reduced argument, rounded to float; `neg`: the
+// second coefficient table (the cos result negated, see above).
+ERAY_HD inline float sincos_poly(double x, double x2, int n, bool neg) {
     if ((n & 1) == 0) {
         double x3 = x * x2;
-        double s1 = fma_d(x2, p.s3, p.s2);
+        double s1 = fma_d(x2, kS3, kS2);
         double x7 = x3 * x2;
-        double s = fma_d(x3, p.s1, x);
+        double s = fma_d(x3, kS1, x);
         return (float)fma_d(x7, s1, s);
     }
     double x4 = x2 * x2;
-    double c2 = fma_d(x2, p.c4, p.c3);
-    double c1 = fma_d(x2, p.c1, p.c0);
+    double c2 = fma_d(x2, kC4, kC3);
+    double c1 = fma_d(x2, kC1, kC0);
     double x6 = x4 * x2;
-    double c = fma_d(x4, p.c2, c1);
-    return (float)fma_d(x6, c2, c);
+    double c = fma_d(x4, kC2, c1);
+    const float f = (float)fma_d(x6, c2, c);
+    return neg ? -f : f;
 }
 
 // Reduction of |x| >= 120 with 4/pi to 96 significant bits: returns r in [-pi/4, pi/4]
@@ -130,26 +112,22 @@ ERAY_HD inline double reduce_large(uint32_t xi, int* np) {
 // cosf(y) as computed by the reference platform's libm.
 ERAY_HD inline float cosf_glibc(float y) {
     double x = y;
-    const SinCosCoeffs* p = &sincos_coeffs(0);
     int n;
     if (abstop12(y) < abstop12(0x1.921FB6p-1f)) {  // |y| < pi/4
         double x2 = x * x;
         if (abstop12(y) < abstop12(0x1p-12f)) return 1.0f;
-        return sincos_poly(x, x2, *p, 1);
+        return sincos_poly(x, x2, 1, false);
     } else if (abstop12(y) < abstop12(120.0f)) {
-        double r = x * p->hpi_inv;
+        double r = x * kHpiInv;
         n = ((int32_t)r + 0x800000) >> 24;
-        x = fma_d(-(double)n, p->hpi, x);
-        double s = p->sign[n & 3];
-        if (n & 2) p = &sincos_coeffs(1);
-        return sincos_poly(x * s, x * x, *p, n ^ 1);
+        x = fma_d(-(double)n, kHpi, x);
+        return sincos_poly(x * quadrant_sign(n), x * x, n ^ 1, (n & 2) != 0);
     } else if (abstop12(y) < abstop12(__builtin_inff())) {
         uint32_t xi = f32_bits(y);
         int sign = (int)(xi >> 31);
         x = reduce_large(xi, &n);
-        double s = p->sign[(n + sign) & 3];
-        if ((n + sign) & 2) p = &sincos_coeffs(1);
-        return sincos_poly(x * s, x * x, *p, n ^ 1);
+        const int q = n + sign;
+        return sincos_poly(x * quadrant_sign(q), x * x, n ^ 1, (q & 2) != 0);
     }
     return (y - y) / (y - y);  // inf or NaN -> NaN
 }

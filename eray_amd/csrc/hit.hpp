@@ -20,18 +20,33 @@ using namespace eray::dev;
 // evict the scene and the textures the next frame reads.  Measured at C2: 10.5 -> 8.6 us per
 // frame vs non-temporal stores (which keep the line).  `base` is the wave-uniform output array
 // (the buffer resource); byte offsets fit 32 bits (FrameParams::aligned requires it).
+//
+// Round 5: a launch whose outputs exceed the 256 MiB Infinity Cache (C5's 7680x4320 frame, 498 MB)
+// adds the NT (streaming) policy — measured, C5's launch span 156 -> 123 us: its frame lines no
+// longer push the bins and records the detail waves read out of the Infinity Cache — while frames
+// that fit it keep plain sc1 (with NT the 3840x2160 / 70k frame in one ring slot 19.9 -> 26.3 us:
+// a frame rewritten in place is absorbed by the cache).  FrameParams::store_nt, chosen per launch.
 using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
 constexpr int kStoreSc1 = 16;  // CPol::SC1 (buffer instruction aux bits on gfx940+)
-template <typename B>
-__device__ __forceinline__ void stream16(B* base, const void* dst, uint4 v) {
+constexpr int kStoreNt = 2;    // CPol::NT
+template <bool kNt, typename B>
+__device__ __forceinline__ void stream16_pol(B* base, uint32_t voff, uint32_t soff, uint4 v) {
     const u32x4 w{v.x, v.y, v.z, v.w};
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, -1, 0x00020000);
-    const uint32_t off = (uint32_t)(reinterpret_cast<const char*>(dst) - reinterpret_cast<const char*>(base));
-    __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, kStoreSc1);
+    __builtin_amdgcn_raw_buffer_store_b128(w, r, voff, soff, kNt ? (kStoreSc1 | kStoreNt) : kStoreSc1);
 }
 template <typename B>
-__device__ __forceinline__ void stream16(B* base, const void* dst, float4 v) {
-    stream16(base, dst, make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)));
+__device__ __forceinline__ void stream16(B* base, const void* dst, uint4 v, bool nt = false) {
+    const uint32_t off = (uint32_t)(reinterpret_cast<const char*>(dst) - reinterpret_cast<const char*>(base));
+    if (nt)
+        stream16_pol<true>(base, off, 0u, v);
+    else
+        stream16_pol<false>(base, off, 0u, v);
+}
+template <typename B>
+__device__ __forceinline__ void stream16(B* base, const void* dst, float4 v, bool nt = false) {
+    stream16(base, dst, make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)),
+             nt);
 }
 
 // A wave-uniform record read through the constant address space: scalar loads (the data was

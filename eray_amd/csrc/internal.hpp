@@ -87,6 +87,8 @@ constexpr int kMaxRects = 8;
 constexpr uint32_t kMaxBounces = 16;
 // Frames one launch may render (eray_frame_ring::frames_per_launch <= slots <= 64).
 constexpr uint32_t kMaxFramesPerLaunch = 64;
+// The MI355X Infinity Cache (the die's last-level cache, MI355X_MICROARCH.md).
+constexpr uint64_t kInfinityCacheBytes = 256ull << 20;
 
 // One entry of a screen bin (bins.hip): a face that may be hit in the bin, its intersection
 // record, the bin's pixels it may cover (bit row * kBinW + column) and its index relative to the
@@ -236,6 +238,9 @@ struct FrameParams {
     // CamState::heavy_sub heavy sub-blocks is j, of a light one dlist_split - 1 - (j - heavy_sub)
     uint32_t dlist_split;
     uint64_t rgb_stride, ppm_stride, face_stride;
+    // frame stores also non-temporal (launch_render: a launch whose outputs exceed the 256 MiB
+    // Infinity Cache — the frame's lines then do not evict what the detail waves read back)
+    uint32_t store_nt;
 };
 
 // Camera row of rank-local row j (FrameParams::band_shift; shifts and masks: no division in the

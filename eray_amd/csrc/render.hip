@@ -70,6 +70,22 @@ __device__ __forceinline__ T as_global_rec(const T* ptr) {  // per-lane record r
     return out;
 }
 
+// Record `index` of a wave-uniform array by buffer loads: the array base lives in SGPRs (the
+// buffer resource) and each lane only carries a 32-bit byte offset — no 64-bit per-lane address
+// arithmetic or registers (arrays below 4 GB: triangle records, bin entries).
+template <typename T>
+__device__ __forceinline__ T load_rec(const T* base, uint32_t index) {
+    static_assert(sizeof(T) % 16 == 0, "16-byte records only");
+    using v4 = unsigned int __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(base), 0, -1, 0x00020000);
+    T out;
+    v4* dst = reinterpret_cast<v4*>(&out);
+#pragma unroll
+    for (uint32_t k = 0; k < sizeof(T) / 16; ++k)
+        dst[k] = __builtin_amdgcn_raw_buffer_load_b128(r, index * (uint32_t)sizeof(T) + 16u * k, 0, 0);
+    return out;
+}
+
 // --------------------------------------------------------------------- triangle setup ------
 // Triangle::intersects recomputes e1 = b - a, e2 = c - a, n = e1 x e2 for every test
 // (primitives.rs:44-46); they do not depend on the ray, so they are computed once here with
@@ -139,13 +155,14 @@ struct SceneGlobal {
     const ObjectDesc* objects;  // the frame's descriptors and culling records (a batched camera
     const TriCull* culls;       // setup's slot: FrameParams::dev_slots)
     __device__ ObjGeom geom(uint32_t i) const { return load_const(&objects[i].g, 0); }
+    __device__ const ObjGeom* geom_ptr(uint32_t i) const { return &objects[i].g; }
     __device__ MaterialDesc mat(uint32_t i) const { return load_const(&objects[i].mat, 0); }
     __device__ LightDesc light(uint32_t i) const { return load_const(p.lights, i); }
     __device__ TriCull cull(uint32_t g) const { return culls[g]; }          // per lane
     __device__ const TriCull* cull_array() const { return culls; }
     __device__ TriHot hot(uint32_t g) const { return load_const(p.tris, g); }  // uniform
-    __device__ TriHot hot_lane(uint32_t g) const { return as_global_rec(p.tris + g); }  // per lane
-    __device__ TriShade shade(uint32_t g) const { return p.shade[g]; }     // per lane
+    __device__ TriHot hot_lane(uint32_t g) const { return load_rec(p.tris, g); }  // per lane
+    __device__ TriShade shade(uint32_t g) const { return load_rec(p.shade, g); }  // per lane
 };
 
 struct SceneLds {
@@ -162,6 +179,7 @@ struct SceneLds {
     // not LDS reads + readfirstlane: C2 8.67 -> 8.40 us per frame (profiles/ab/ab_c2chain.log),
     // though one wave's chain alone is 0.2 us longer (7.26 -> 7.44 us, a 4-row frame).
     __device__ ObjGeom geom(uint32_t i) const { return load_const(&g_objs[i].g, 0); }
+    __device__ const ObjGeom* geom_ptr(uint32_t i) const { return &g_objs[i].g; }
     __device__ MaterialDesc mat(uint32_t i) const { return load_const(&g_objs[i].mat, 0); }
     __device__ LightDesc light(uint32_t i) const { return load_const(g_lights, i); }
     __device__ TriCull cull(uint32_t g) const { return culls[g]; }
@@ -615,7 +633,7 @@ __device__ void first_hit_binned_wave(const ObjGeom& ob, uint32_t bin, int& st, 
         uint32_t fj = 0xffffffffu;
         unsigned long long pm = 0;
         if (j < hi) {
-            const BinEntry x = as_global_rec(ob.bin_ent + j);
+            const BinEntry x = load_rec(ob.bin_ent, j);
             fj = x.tri;
             pm = x.mask;
             L.cand[lane] = x.hot;
@@ -720,7 +738,7 @@ __device__ __forceinline__ f3 camera_dir(const CamDev& cam, const FrameParams& p
 // sub-block inside one of the frame's detail rectangles (FrameParams::rects: the objects' pixel
 // rectangles, ObjectDesc::rect, in sub-block units) is "detail": one wave runs Engine::cast_ray
 // for its 64 pixels, one pixel per lane.  Every other sub-block is background
-// (engine.rs:208-213) with no test at all.  One persistent launch does both:
+// (engine.rs:211-213) with no test at all.  One persistent launch does both:
 //  * detail: the detail sub-blocks are enumerated rectangle by rectangle (the host makes the
 //    rectangles disjoint) and dealt out round-robin over the first
 //    workgroups, four consecutive ones per workgroup, so the latency-bound shading is spread
@@ -755,15 +773,17 @@ struct FrameOut {
     float* rgb;
     uint8_t* ppm;
     int32_t* face;
+    bool nt;  // stores also non-temporal (FrameParams::store_nt)
 };
 __device__ __forceinline__ FrameOut frame_out(const FrameParams& p, uint32_t fr) {
     return FrameOut{p.out_rgb ? reinterpret_cast<float*>(reinterpret_cast<char*>(p.out_rgb) + fr * p.rgb_stride) : nullptr,
                     p.out_ppm ? p.out_ppm + fr * p.ppm_stride : nullptr,
                     p.out_face ? reinterpret_cast<int32_t*>(reinterpret_cast<char*>(p.out_face) + fr * p.face_stride)
-                               : nullptr};
+                               : nullptr,
+                    p.store_nt != 0};
 }
 
-// background (engine.rs:208-213) and its bytes: sat_u8(0.1*255) = 25, sat_u8(0.2*255) = 51
+// background (engine.rs:211-213) and its bytes: sat_u8(0.1*255) = 25, sat_u8(0.2*255) = 51
 __device__ __forceinline__ float4 bg_rgb4(uint32_t phase) {  // 16-byte word at float offset 4c
     const float a = 0.1f, b = 0.2f;
     return phase == 0 ? make_float4(a, a, b, a) : phase == 1 ? make_float4(a, b, a, a) : make_float4(b, a, a, b);
@@ -777,7 +797,8 @@ __device__ __forceinline__ uint4 bg_ppm16(uint32_t phase) {  // 16-byte word at 
 }
 
 // Background for the pixels [x0, x0 + w) x rows [py0, py0 + kBlkH) (w = 64 or 16), wave-wide.
-template <uint32_t kW>
+// (kNt: non-temporal stores, FrameOut::nt — a template argument, not a per-store select)
+template <uint32_t kW, bool kNt = false>
 __device__ __forceinline__ void fill_background(const FrameParams& p, const FrameOut& o, uint32_t x0, uint32_t py0, bool aligned,
                                                 uint32_t lane) {
     if (aligned && x0 + kW <= p.cam_w && py0 + kBlkH <= p.rows) {
@@ -789,18 +810,18 @@ __device__ __forceinline__ void fill_background(const FrameParams& p, const Fram
             for (uint32_t i = lane; i < kBlkH * kRow4; i += 64) {
                 const uint32_t r = i / kRow4, c = i % kRow4;
                 stream16(o.rgb, reinterpret_cast<float4*>(o.rgb + 3 * ((size_t)(py0 + r) * p.img_w + x0)) + c,
-                         bg_rgb4(c % 3));
+                         bg_rgb4(c % 3), kNt);
             }
         }
         if (o.ppm && lane < kBlkH * kRow16) {
             const uint32_t r = lane / kRow16, c = lane % kRow16;
             const size_t row = (size_t)(p.rows - py0 - kBlkH + r);  // file rows, bottom-up
-            stream16(o.ppm, reinterpret_cast<uint4*>(o.ppm + 3 * (row * p.img_w + x0)) + c, bg_ppm16(c % 3));
+            stream16(o.ppm, reinterpret_cast<uint4*>(o.ppm + 3 * (row * p.img_w + x0)) + c, bg_ppm16(c % 3), kNt);
         }
         if (o.face && lane < kBlkH * kFace4) {
             const uint32_t r = lane / kFace4, c = lane % kFace4;
             stream16(o.face, reinterpret_cast<int4*>(o.face + (size_t)(py0 + r) * p.img_w + x0) + c,
-                     make_uint4(~0u, ~0u, ~0u, ~0u));
+                     make_uint4(~0u, ~0u, ~0u, ~0u), kNt);
         }
     } else {  // image edge or unaligned output: per pixel
         const float4 b = bg_rgb4(0);
@@ -857,24 +878,23 @@ __device__ __forceinline__ BlockFill block_fill(uint32_t img_w, uint32_t lane) {
     b.face_off = (lane / kFace4) * img_w * 4u + (lane % kFace4) * 16u;
     return b;
 }
-template <typename B>
+template <bool kNt = false, typename B>
 __device__ __forceinline__ void stream16_at(B* base, uint32_t voff, uint32_t soff, uint4 v) {
-    const u32x4 w{v.x, v.y, v.z, v.w};
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, -1, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(w, rs, voff, soff, kStoreSc1);
+    stream16_pol<kNt>(base, voff, __builtin_amdgcn_readfirstlane(soff), v);
 }
 // The block (bx, by) (block units, rank-local rows; wave-uniform) from the lane constants.
+template <bool kNt>
 __device__ __forceinline__ void fill_block_fast(const FrameParams& p, const FrameOut& o, const BlockFill& bf, uint32_t bx,
                                                 uint32_t by, uint32_t lane) {
     const uint32_t x0 = bx * kBlkW, py0 = by * kBlkH;
     if (o.rgb) {
         const uint32_t base = (py0 * p.img_w + x0) * 12u;
 #pragma unroll
-        for (uint32_t k = 0; k < 3; ++k) stream16_at(o.rgb, bf.rgb_off[k], base, bf.rgb[k]);
+        for (uint32_t k = 0; k < 3; ++k) stream16_at<kNt>(o.rgb, bf.rgb_off[k], base, bf.rgb[k]);
     }
     if (o.ppm && lane < kBlkH * (kBlkW * 3 / 16))
-        stream16_at(o.ppm, bf.ppm_off, ((p.rows - py0 - kBlkH) * p.img_w + x0) * 3u, bf.ppm);
-    if (o.face) stream16_at(o.face, bf.face_off, (py0 * p.img_w + x0) * 4u, make_uint4(~0u, ~0u, ~0u, ~0u));
+        stream16_at<kNt>(o.ppm, bf.ppm_off, ((p.rows - py0 - kBlkH) * p.img_w + x0) * 3u, bf.ppm);
+    if (o.face) stream16_at<kNt>(o.face, bf.face_off, (py0 * p.img_w + x0) * 4u, make_uint4(~0u, ~0u, ~0u, ~0u));
 }
 
 // the pixel rectangle of `ob` (camera rows) meets the sub-block's pixels
@@ -902,20 +922,30 @@ struct NoMid {
 constexpr uint32_t kWavePix = kSubW * kBlkH;
 constexpr uint32_t kSliceRgbBytes = 3 * 4 * kWavePix, kSlicePpmBytes = 3 * kWavePix;
 // The 16-B row stores of a staged slice (sub-block at (wx0, py0), rank-local rows).
+// (wave-uniform sub-block: 32-bit lane offsets, the sub-block's base as the scalar offset)
 __device__ __forceinline__ void store_slice(const FrameParams& p, const FrameOut& fo, uint32_t wx0, uint32_t py0,
                                             const float* wrgb, const uint8_t* wppm, uint32_t lane) {
     constexpr uint32_t kRgbRow4 = kSubW * 3 / 4;    // float4 per wave row (12)
     constexpr uint32_t kPpmRow16 = kSubW * 3 / 16;  // 16-byte words per wave row (3)
+    // (the lane offsets are recomputed here, a few instructions, rather than kept live across the
+    // detail rounds, where the 4-per-CU build would spill them)
+    asm volatile("" : "+v"(lane));
     if (fo.rgb && lane < kBlkH * kRgbRow4) {
         const uint32_t r = lane / kRgbRow4, c = lane % kRgbRow4;
-        float4* dst = reinterpret_cast<float4*>(fo.rgb + 3 * ((size_t)(py0 + r) * p.img_w + wx0)) + c;
-        stream16(fo.rgb, dst, reinterpret_cast<const float4*>(wrgb)[lane]);
+        const float4 v = reinterpret_cast<const float4*>(wrgb)[lane];
+        const uint4 w = make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w));
+        if (fo.nt)
+            stream16_at<true>(fo.rgb, r * p.img_w * 12u + c * 16u, (py0 * p.img_w + wx0) * 12u, w);
+        else
+            stream16_at<false>(fo.rgb, r * p.img_w * 12u + c * 16u, (py0 * p.img_w + wx0) * 12u, w);
     }
     if (fo.ppm && lane < kBlkH * kPpmRow16) {
         const uint32_t r = lane / kPpmRow16, c = lane % kPpmRow16;  // r-th byte row of the block
-        const size_t row = (size_t)(p.rows - py0 - kBlkH + r);
-        uint4* dst = reinterpret_cast<uint4*>(fo.ppm + 3 * (row * p.img_w + wx0)) + c;
-        stream16(fo.ppm, dst, reinterpret_cast<const uint4*>(wppm)[lane]);
+        const uint4 w = reinterpret_cast<const uint4*>(wppm)[lane];
+        if (fo.nt)
+            stream16_at<true>(fo.ppm, r * p.img_w * 3u + c * 16u, ((p.rows - py0 - kBlkH) * p.img_w + wx0) * 3u, w);
+        else
+            stream16_at<false>(fo.ppm, r * p.img_w * 3u + c * 16u, ((p.rows - py0 - kBlkH) * p.img_w + wx0) * 3u, w);
     }
 }
 
@@ -923,7 +953,8 @@ template <bool kCull, bool kLdsTiles, int kMat, typename Scene, typename Mid = N
 __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut& fo, const CamDev& cam, const RowMap& rm,
                                            const Scene& sc, uint32_t wx0, uint32_t py0,
                                            bool active, TriHot* s_hot, TriCull* s_cull, char* s_bins, float4* s_rgb,
-                                           uint32_t* s_ppm, bool aligned, const f3* given_d = nullptr, bool coop = true,
+                                           uint32_t* s_ppm, bool aligned, bool has_given = false,
+                                           f3 given_d = f3{0.0f, 0.0f, 0.0f}, bool coop = true,
                                            PreRange pre = PreRange{0u, 0u, false}, uint32_t pre_obj = ~0u,
                                            Mid&& mid = Mid{}) {
     // coop (workgroup-uniform): the workgroup's four sub-blocks share their large objects' work —
@@ -936,6 +967,8 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
     // ab_r04an.txt).  A large object without bins (a bin-capacity overflow's fallback frame) is
     // then scanned by each wave alone; brute-force builds (!kCull) keep the LDS tiles.
     if constexpr (kCull && kLdsTiles) coop = false;
+    wx0 = __builtin_amdgcn_readfirstlane(wx0);  // (wave-uniform: scalar registers)
+    py0 = __builtin_amdgcn_readfirstlane(py0);
     constexpr bool kSpecPow = (kMat & kMatSpecPow) != 0, kExample = (kMat & kMatExample) != 0;
     // candidates tested together by the per-wave scans (small objects, shadow rays): four for ILP,
     // one in the large-mesh builds, whose registers bound their resident waves
@@ -950,8 +983,8 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
 
     // ---- cast_ray (engine.rs:112-216): closest object among first hits -----------
     ERAY_TRACE_WAVE0(4);
-    f3 d = given_d ? *given_d : mk3(0.0f, 0.0f, 0.0f);  // the camera ray, when the caller has it
-    bool ray_ready = given_d != nullptr;
+    f3 d = given_d;  // the camera ray, when the caller has it (has_given)
+    bool ray_ready = has_given;
     bool have = false;
     float closest = 0.0f, bu = 0.0f, bv = 0.0f, bt = 0.0f;
     uint32_t best_obj = 0;
@@ -1018,13 +1051,23 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
     rgb color{0.0f, 0.0f, 0.0f};
     float kd = 0.5f, ks = 0.5f, sp = 1.0f;
     const float *tc = nullptr, *tkd = nullptr, *tks = nullptr, *tsp = nullptr;  // texels, if any
+    // every hit lane's shading record in one load from a wave-uniform point (a lane without a
+    // hit reads record 0)
+    TriShade sh = TriShade{};
+    if (__any(have)) {
+        uint32_t g = 0;
+        for (uint32_t oi = 0; oi < p.nobj; ++oi) {
+            if (!__any(have && best_obj == oi)) continue;
+            const uint32_t tb = load_const(&sc.geom_ptr(oi)->tri_begin, 0);
+            if (have && best_obj == oi) g = tb + (uint32_t)best_face;
+        }
+        sh = sc.shade(g);
+    }
     for (uint32_t oi = 0; oi < p.nobj; ++oi) {  // per-lane object, read from uniform copies
         if (!__any(have && best_obj == oi)) continue;
-        const ObjGeom ob = sc.geom(oi);
         const MaterialDesc mat = sc.mat(oi);
         ERAY_TRACE_WAVE0(17);
         if (!(have && best_obj == oi)) continue;
-        const TriShade sh = sc.shade(ob.tri_begin + (uint32_t)best_face);
         P = add(C, mul(d, bt));
         const f3 na = mk3(sh.s0.x, sh.s0.y, sh.s0.z), nb = mk3(sh.s0.w, sh.s1.x, sh.s1.y);
         const f3 nc = mk3(sh.s1.z, sh.s1.w, sh.s2.x);
@@ -1083,7 +1126,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
     };
     ERAY_TRACE_WAVE0(13);
     const HitBox hb = hit_box(have, P, N);  // (wave-uniform; shadow-ray face bounds)
-    // Point lights first (engine.rs:274-279), 32 at a time: every light's shadow ray, then the
+    // Point lights first (engine.rs:130-135), 32 at a time: every light's shadow ray, then the
     // shading of the lights that reach the hit, in list order.  The texture loads above are
     // still in flight during the first shadow scan; the shading is their first use.
     for (uint32_t li0 = 0; li0 < p.nlights; li0 += 32) {
@@ -1093,7 +1136,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
             const LightDesc L = sc.light(li);
             if (L.variant == 1 || (!(kLdsTiles && coop) && !__any(have))) continue;  // (LDS tiles: barriers)
             const f3 Lp = mk3(L.pos[0], L.pos[1], L.pos[2]);
-            // reaches_light(Ray::new(P + N * 0.1, Lp - P)) (engine.rs:280-286, 218-228)
+            // reaches_light(Ray::new(P + N * 0.1, Lp - P)) (engine.rs:136-142, 218-228)
             f3 S = mk3(0.0f, 0.0f, 0.0f);
             f3 sd = mk3(0.0f, 0.0f, 1.0f);
             float dist = 0.0f;
@@ -1159,7 +1202,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
         material();
         for (uint32_t li = li0; li < li1; ++li) {
             const LightDesc L = sc.light(li);
-            if (L.variant == 1 || !((lit >> (li - li0)) & 1u)) continue;  // engine.rs:287-322
+            if (L.variant == 1 || !((lit >> (li - li0)) & 1u)) continue;  // engine.rs:143-178
             const f3 Lp = mk3(L.pos[0], L.pos[1], L.pos[2]);
             const f3 LmP = sub(Lp, P);
             float prod = rust_clamp(dot0(N, LmP), 0.0f, 1.0f);
@@ -1181,7 +1224,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
     }
     if (have) {
         material();
-        for (uint32_t li = 0; li < p.nlights; ++li) {  // ambient lights (engine.rs:341-352)
+        for (uint32_t li = 0; li < p.nlights; ++li) {  // ambient lights (engine.rs:197-209)
             const LightDesc L = sc.light(li);
             if (L.variant != 1) continue;
             const rgb m{rust_min(L.color[0], color.r), rust_min(L.color[1], color.g),
@@ -1189,7 +1232,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
             push(cmul(cmul(m, kd), L.brightness));
         }
     } else {
-        push(rgb{0.1f, 0.1f, 0.2f});  // engine.rs:208-213
+        push(rgb{0.1f, 0.1f, 0.2f});  // engine.rs:211-213
     }
 
     ERAY_TRACE_WAVE0(6);
@@ -1254,7 +1297,7 @@ __device__ __forceinline__ bool inside(const SubRect& r, int32_t sx, int32_t sy)
 
 // The background of the non-detail sub-blocks: fill workgroup f of nf strides over the 64 x 4
 // blocks (shared by the frame kernel's fill roles and fill_kernel).
-template <bool kDev>
+template <bool kDev, bool kNt>
 __device__ __forceinline__ void fill_blocks(const FrameParams& p, const FrameOut& o, const CamState* cs,
                                             const uint8_t* detail_occ, uint32_t f, uint32_t nf, uint32_t wave,
                                             uint32_t lane, bool aligned) {
@@ -1300,12 +1343,12 @@ __device__ __forceinline__ void fill_blocks(const FrameParams& p, const FrameOut
         }
         if (!mask) {
             if (bx < full_x && by < full_y)
-                fill_block_fast(p, o, bf, bx, by, lane);
+                fill_block_fast<kNt>(p, o, bf, bx, by, lane);
             else
-                fill_background<kBlkW>(p, o, bx * kBlkW, by * kBlkH, aligned, lane);
+                fill_background<kBlkW, kNt>(p, o, bx * kBlkW, by * kBlkH, aligned, lane);
         } else if (mask != 0xfu) {
             for (uint32_t i = 0; i < 4; ++i)
-                if (!((mask >> i) & 1u)) fill_background<kSubW>(p, o, bx * kBlkW + i * kSubW, by * kBlkH, aligned, lane);
+                if (!((mask >> i) & 1u)) fill_background<kSubW, kNt>(p, o, bx * kBlkW + i * kSubW, by * kBlkH, aligned, lane);
         }
     }
 }
@@ -1319,17 +1362,21 @@ __device__ __forceinline__ void fill_frames(const FrameParams& p, uint32_t q, ui
     for (uint32_t v = q; v < roles; v += nf) {
         const uint32_t fr = v % F, slot = p.dev_slots ? fr : 0u;
         const uint8_t* occ = p.detail_occ ? p.detail_occ + (size_t)slot * (p.dlist_stride / 4) : nullptr;
-        fill_blocks<kDev>(p, frame_out(p, fr), p.cam_state + slot, occ, v / F, (roles - fr + F - 1) / F, wave, lane,
-                          aligned);
+        const FrameOut o = frame_out(p, fr);
+        if (o.nt)
+            fill_blocks<kDev, true>(p, o, p.cam_state + slot, occ, v / F, (roles - fr + F - 1) / F, wave, lane, aligned);
+        else
+            fill_blocks<kDev, false>(p, o, p.cam_state + slot, occ, v / F, (roles - fr + F - 1) / F, wave, lane, aligned);
     }
 }
 
-// kDense (large meshes only): 3 workgroups per CU instead of 2 (168 VGPRs, a few spilled), for
-// frames whose detail sub-blocks exceed one round of the 2-per-CU grid — there the detail waves
-// are VALU-issue bound and a second detail wave per SIMD doubles the issue slots (one wave alone
-// issues a VALU instruction every 4 cycles, the SIMD every 2); below one round the spills only
-// lengthen each wave's chain.
-constexpr int kDenseWgs = 3;
+// kDense (large meshes only): 4 workgroups per CU instead of 2 (at most 128 VGPRs), for frames
+// whose detail sub-blocks exceed one round of the 2-per-CU grid — there the detail waves are
+// latency bound and more resident detail waves mean fewer rounds.  Round 5 (profiles/r05/ab/):
+// the culled large-mesh path lost its 64-bit per-lane addresses (buffer loads of records and
+// bin entries, scalar store offsets) and fits 4 per CU; with the fill at one workgroup per CU
+// (launch_frame_kernel) 3840x2160 / 70k 22.2 -> 20.1 us, its moving camera 50.0 -> 46.7 us.
+constexpr int kDenseWgs = 4;
 template <bool kCull, bool kLdsTiles, int kMat, bool kLdsScene, bool kDense = false, bool kDev = false>
 __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && !kDense) ? 1 : (kDense ? kDenseWgs : 3))  // 3 workgroups per CU where that fits
     frame_kernel(const ObjectDesc* h_objects, const LightDesc* h_lights, const TriCull* h_cull, const TriHot* h_tris,
@@ -1530,9 +1577,10 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
                     // the ordered detail list's heavy sub-blocks (bins of several chunks) come
                     // first, so the longest chains start in the first round (coop: shared by the
                     // workgroup in builds that keep the cooperative paths, render_sub)
+                    // (the first sub-block's rays by value: a pointer would keep them in scratch memory)
                     render_sub<kCull, kLdsTiles, kMat>(p, fo, cam, rm, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH,
                                                        active, s_hot, s_cull, s_bins, s_rgb, s_ppm, aligned,
-                                                       (kGivenRay && r == 0) ? &d0 : nullptr, coop, pre, pobj, mid);
+                                                       kGivenRay && r == 0, d0, coop, pre, pobj, mid);
                 }
             };
             if constexpr (kLdsScene) {
@@ -1698,7 +1746,9 @@ hipError_t launch_frame_kernel(const FrameParams& p, uint32_t want, size_t dyn, 
                                           : 0u;
     };
     FrameParams q = p;
-    q.detail_wgs = detail_wgs(2.0f);
+    // (the dense large-mesh build, 4 workgroups per CU: one per CU fills, three do detail work —
+    // the fill's store stream no longer needs the issue slots it did, round 5)
+    q.detail_wgs = detail_wgs((L && D) ? 4.0f : 2.0f);
     q.fill_first = 0;
     q.detail_wgs_alt = 0;
     if (!L) {
@@ -1784,9 +1834,15 @@ hipError_t launch_frame_cs(const FrameParams& p, uint32_t want, const LaunchCtx&
 }
 }  // namespace
 
-hipError_t launch_render(const FrameParams& p, const LaunchCtx& lc, hipStream_t s) {
+hipError_t launch_render(const FrameParams& p_in, const LaunchCtx& lc, hipStream_t s) {
+    FrameParams p = p_in;
     if (p.nframes < 1 || p.nframes > kMaxFramesPerLaunch || ((p.aa || p.bounces) && p.nframes != 1))
         return hipErrorInvalidValue;
+    {  // the launch's output bytes against the Infinity Cache (FrameParams::store_nt)
+        const uint64_t px = (uint64_t)p.nframes * p.rows * p.img_w;
+        const uint64_t out = px * ((p.out_rgb ? 12u : 0u) + (p.out_ppm ? 3u : 0u) + (p.out_face ? 4u : 0u));
+        p.store_nt = out > kInfinityCacheBytes ? 1u : 0u;
+    }
     if (p.aa || p.bounces) return launch_trace(p, lc, s);
     const uint32_t by_n = (p.rows + kBlkH - 1) / kBlkH;
     const uint32_t nblk = p.tiles_x * by_n;

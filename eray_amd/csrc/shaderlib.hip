@@ -16,12 +16,6 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kVec = 4;
 
-inline unsigned grid_for1(size_t items) {
-    size_t blocks = (items + kBlock - 1) / kBlock;
-    if (blocks > 8192) blocks = 8192;
-    return blocks ? (unsigned)blocks : 1u;
-}
-
 inline unsigned grid_for(size_t items) {
     size_t blocks = (items + (size_t)kBlock * kVec - 1) / ((size_t)kBlock * kVec);
     if (blocks > 2048) blocks = 2048;
@@ -34,15 +28,41 @@ __device__ __forceinline__ float wave_value(uint32_t x, uint32_t y, float xf, fl
     return __builtin_fabsf(libm::cosf_glibc(arg));
 }
 
-// One texel per thread: the restated cosf is a chain of dependent double-precision steps, so
-// latency is hidden by occupancy rather than by per-thread ILP; stores stay 256 B per wave.
+// kVec consecutive texels of the row-major image per thread, from index i0 (x advances with a
+// wrap instead of a division per texel; texels past n are computed and not stored).
+template <typename F>
+__device__ __forceinline__ void wave_values(size_t i0, uint32_t w, float xf, float yf, F&& each) {
+    uint32_t y = (uint32_t)(i0 / w), x = (uint32_t)(i0 - (size_t)y * w);
+#pragma unroll
+    for (int k = 0; k < kVec; ++k) {
+        each(k, wave_value(x, y, xf, yf));
+        if (++x == w) {
+            x = 0;
+            ++y;
+        }
+    }
+}
+
+__device__ __forceinline__ void store4(float* __restrict__ out, size_t i0, size_t n, const float (&v)[kVec]) {
+    float* p = out + i0;
+    if (i0 + kVec <= n && ((reinterpret_cast<uintptr_t>(p) & 15) == 0)) {
+        *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+        for (int k = 0; k < kVec && i0 + k < n; ++k) p[k] = v[k];
+    }
+}
+
+// The restated cosf's coefficients are immediates (glibc_cosf.hpp), so a texel is a short chain
+// of double-precision steps; kVec texels per thread give each wave four independent chains and
+// 16-B stores.
 __global__ void __launch_bounds__(kBlock) wave_kernel(uint32_t w, uint32_t h, float xf, float yf,
                                                       float* __restrict__ out) {
     const size_t n = (size_t)w * h;
-    const size_t stride = (size_t)gridDim.x * kBlock;
-    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-        const uint32_t y = (uint32_t)(i / w), x = (uint32_t)(i - (size_t)y * w);
-        out[i] = wave_value(x, y, xf, yf);
+    const size_t stride = (size_t)gridDim.x * kBlock * kVec;
+    for (size_t i0 = ((size_t)blockIdx.x * kBlock + threadIdx.x) * kVec; i0 < n; i0 += stride) {
+        float v[kVec];
+        wave_values(i0, w, xf, yf, [&](int k, float x) { v[k] = x; });
+        store4(out, i0, n, v);
     }
 }
 
@@ -124,23 +144,25 @@ __global__ void __launch_bounds__(kBlock) mix_kernel(uint32_t w, uint32_t h, Tex
 
 // main.rs:80-144 fused: wave -> rgb(wave, wave, wave) -> mix(.., flat(r, g, b), factor);
 // diffuse = wave.  Every node's image has the graph's width x height, so mix's mod_get is the
-// identity and the chain reduces to per-texel arithmetic in the nodes' own operation order.
+// identity and the chain reduces to per-texel arithmetic in the nodes' own operation order
+// (r * factor is the same product per texel, so it is formed once).
 __global__ void __launch_bounds__(kBlock) material_example_kernel(
     uint32_t w, uint32_t h, float xf, float yf, float r, float g, float b, float factor,
     float* __restrict__ color, float* __restrict__ diffuse) {
     const size_t n = (size_t)w * h;
-    const float omf = 1.0f - factor;
-    const size_t stride = (size_t)gridDim.x * kBlock;
-    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-        const uint32_t y = (uint32_t)(i / w), x = (uint32_t)(i - (size_t)y * w);
-        const float v = wave_value(x, y, xf, yf);
-        if (color) {
-            float* c = color + 3 * i;
-            c[0] = v * omf + r * factor;
-            c[1] = v * omf + g * factor;
-            c[2] = v * omf + b * factor;
-        }
-        if (diffuse) diffuse[i] = v;
+    const float omf = 1.0f - factor, rf = r * factor, gf = g * factor, bf = b * factor;
+    const size_t stride = (size_t)gridDim.x * kBlock * kVec;
+    for (size_t i0 = ((size_t)blockIdx.x * kBlock + threadIdx.x) * kVec; i0 < n; i0 += stride) {
+        float v[kVec], c[kVec][3];
+        wave_values(i0, w, xf, yf, [&](int k, float x) {
+            v[k] = x;
+            const float m = x * omf;
+            c[k][0] = m + rf;
+            c[k][1] = m + gf;
+            c[k][2] = m + bf;
+        });
+        if (color) store_rgb4(color, i0, n, c);
+        if (diffuse) store4(diffuse, i0, n, v);
     }
 }
 
@@ -149,7 +171,7 @@ __global__ void __launch_bounds__(kBlock) material_example_kernel(
 hipError_t launch_wave(uint32_t w, uint32_t h, float xf, float yf, float* out, hipStream_t s) {
     size_t n = (size_t)w * h;
     if (!n) return hipSuccess;
-    wave_kernel<<<grid_for1(n), kBlock, 0, s>>>(w, h, xf, yf, out);
+    wave_kernel<<<grid_for(n), kBlock, 0, s>>>(w, h, xf, yf, out);
     return hipGetLastError();
 }
 hipError_t launch_rgb(uint32_t w, uint32_t h, const float* r, const float* g, const float* b,
@@ -178,7 +200,7 @@ hipError_t launch_material_example(uint32_t w, uint32_t h, float xf, float yf, f
                                    hipStream_t s) {
     size_t n = (size_t)w * h;
     if (!n) return hipSuccess;
-    material_example_kernel<<<grid_for1(n), kBlock, 0, s>>>(w, h, xf, yf, r, g, b, factor, color,
+    material_example_kernel<<<grid_for(n), kBlock, 0, s>>>(w, h, xf, yf, r, g, b, factor, color,
                                                            diffuse);
     return hipGetLastError();
 }

@@ -458,7 +458,7 @@ __device__ __forceinline__ T pick(const T (&a)[kRays], uint32_t r) {
 // jittered anti-aliasing rays — goes through the viewport rectangle [x0 - 1, x0 + 16] x [y0 - 1,
 // y0 + 4] / (W, H) (jitter in [-1, 1), engine.rs:62-69).  A wave that can show that none of those
 // rays reaches any face casts none: every one of its rays is the reference's miss
-// (engine.rs:208-213) — cast_ray's own miss path, the same float sums — and the shadow and
+// (engine.rs:211-213) — cast_ray's own miss path, the same float sums — and the shadow and
 // reflected rays, which start only at a hit, never exist.
 //  * Scenes of at most kSkipTris triangles: trace_cull_kernel computes every triangle's culling
 //    record for this camera (cull_record.hpp, the frame kernel's conservative bounds, with the
@@ -647,7 +647,7 @@ __device__ __forceinline__ rgb background_color(const FrameParams& p) {
 }
 
 // Background of the pixels [x0, x0 + kW) x rows [py0, py0 + 4) (kW = 64 or 16), wave-wide: the
-// colour `c` (bytes `b`) as 16-byte write-through row stores, the face -1 (engine.rs:208-213).
+// colour `c` (bytes `b`) as 16-byte write-through row stores, the face -1 (engine.rs:211-213).
 template <uint32_t kW>
 __device__ void fill_color(const FrameParams& p, uint32_t x0, uint32_t py0, uint32_t lane, const float (&c)[3],
                            const uint8_t (&b)[3]) {

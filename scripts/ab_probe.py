@@ -8,7 +8,8 @@ Configs: c2 (cube 1920x1080, 8 frames per launch into 8 slots), c3 (70k stand-in
 per launch), ns1 / ns4 (70k stand-in 3840x2160, one frame per launch, 1 / 4 ring slots), c5
 (1M faces 7680x4320), moving_ns (a moving camera over the 70k stand-in at 3840x2160), aa2 / aa_ns
 (anti-aliasing = 4 through the general tracer: C2, the 70k stand-in at 3840x2160; graph-replayed
-frames, device ms per frame), fill* (the same camera and lights, no object)."""
+frames, device ms per frame), fill* (the same camera and lights, no object), mat (main.rs's
+Material::update of a 1024 x 1024 texture, bench.py material_roofline)."""
 from __future__ import annotations
 
 import argparse
@@ -35,7 +36,8 @@ CONFIGS = {"fill4k1": ("none", 3840, 2160, 1, 1), "fill4k4": ("none", 3840, 2160
            "moving_c5": ("1m", 7680, 4320, 1, 1),
            "aa2": ("cube", 1920, 1080, 1, 1), "aa_ns": ("70k", 3840, 2160, 1, 1),
            "ns1sep": ("70k", 3840, 2160, 1, 1), "ns4sep": ("70k", 3840, 2160, 4, 1),
-           "ns1ex": ("70k", 3840, 2160, 1, 1), "ns4ex": ("70k", 3840, 2160, 4, 1), "c2ex": ("cube", 1920, 1080, 8, 8)}
+           "ns1ex": ("70k", 3840, 2160, 1, 1), "ns4ex": ("70k", 3840, 2160, 4, 1), "c2ex": ("cube", 1920, 1080, 8, 8),
+           "mat": ("cube", 1920, 1080, 1, 1)}
 # launch-shape overrides (eray_render_params::flags) of the *sep configs: the dense build beside a
 # separate fill kernel
 SEPARATE = ("ns1sep", "ns4sep")
@@ -78,7 +80,10 @@ def main() -> None:
         kw = dict(out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr(), ring=capi.frame_ring(slots, H, W, F))
         if name in SEPARATE:
             kw["flags"] = capi.RENDER_DENSE_DETAIL | capi.RENDER_SEPARATE_FILL
-        if name.startswith("aa"):  # the general tracer, anti_aliasing = 4 (bench.py anti_aliasing_line)
+        if name == "mat":
+            from bench import material_roofline
+            out[name] = {"frame_ms": min(material_roofline(sc, st, reps=50)["us_per_update"] for _ in range(3)) / 1e3}
+        elif name.startswith("aa"):  # the general tracer, anti_aliasing = 4 (bench.py anti_aliasing_line)
             akw = dict(kw, anti_aliasing=4, aa_seed=12345)
             del akw["ring"]
             ctx.render_frames(20, W, H, prepare_only=True, **akw)

@@ -3,7 +3,7 @@
     python scripts/pmc_legs.py <pass dir under gpurun_out> <output json> [--north-star SLOTS]
                                                                         [--workload JSON]
 
-Each pass directory holds one rocprofv3 counter run per counter group (scripts/session_r04b.sh:
+Each pass directory holds one rocprofv3 counter run per counter group (scripts/gpu_pmc.sh:
 `sq`, `fetch`, `write`, each its own run, kernel trace only).  Per counter the median over the
 dispatches of the frame kernel instantiation with the most dispatches (the bench's measured
 launches of one launch size outnumber its one instrumented frame; in a north_star run the
