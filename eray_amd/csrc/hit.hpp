@@ -121,6 +121,27 @@ __device__ __forceinline__ bool bbox_hit(const ObjGeom& ob, f3 s, f3 d) {
     return true;
 }
 
+// BoundingBox::intersects' first early return (object.rs:345-347) for a box that is a point in
+// x and y (the loaded meshes' (0,0,0) box), decided without the shadow ray's direction.  With
+// S = P + N * 0.1, w = Lp - P, d = normalize(w) and a = box - S, the test computes
+// tx = a.x * (1 / d.x) and ty = a.y * (1 / d.y) and rejects when tx != ty (neither NaN).  Both
+// carry the same positive factor |w| and at most ~3 roundings each: tx = (a.x / w.x) |w| (1 + dx)
+// with |dx| <= 3.01 * 2^-24 while no value is subnormal or infinite.  q = a / w by the hardware
+// reciprocal (1 ulp) and a product is within 3 * 2^-24 of a.x / w.x, so |qx - qy| above
+// (|qx| + |qy|) * 2^-20 proves tx != ty.  Returns true only when bbox_hit(ob, S, d) is certainly
+// false; false means undecided (the caller runs the exact test).
+__device__ __forceinline__ bool point_box_rejects(const ObjGeom& ob, f3 S, f3 w) {
+    const float ax = ob.bb_lo[0] - S.x, ay = ob.bb_lo[1] - S.y;
+    const float wx = __builtin_fabsf(w.x), wy = __builtin_fabsf(w.y), ws = wx + wy + __builtin_fabsf(w.z);
+    auto sane = [](float a) { return a == 0.0f || (__builtin_fabsf(a) >= 0x1p-60f && __builtin_fabsf(a) <= 0x1p20f); };
+    const bool ok = ws >= 0x1p-60f && ws <= 0x1p60f && wx >= ws * 0x1p-100f && wy >= ws * 0x1p-100f && sane(ax) && sane(ay);
+    const float qx = ax * __builtin_amdgcn_rcpf(w.x), qy = ay * __builtin_amdgcn_rcpf(w.y);
+    return ok && __builtin_fabsf(qx - qy) > (__builtin_fabsf(qx) + __builtin_fabsf(qy)) * 0x1p-20f;
+}
+__device__ __forceinline__ bool point_box_xy(const ObjGeom& ob) {
+    return ob.bb_lo[0] == ob.bb_hi[0] && ob.bb_lo[1] == ob.bb_hi[1];
+}
+
 // Wave-wide min and max of six floats at once (lanes that must not count pass +inf / -inf):
 // the floats as order-preserving integer keys, DPP row shifts and row broadcasts (an invalid
 // source lane reads the identity), the six reductions interleaved; results in SGPRs.

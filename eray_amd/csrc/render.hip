@@ -1153,6 +1153,12 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
             };
             for (uint32_t oj = 0; oj < p.nobj; ++oj) {
                 const ObjGeom ob = sc.geom(oj);
+                // A point box (the loaded meshes'): when it certainly rejects every lane's shadow
+                // ray (point_box_rejects), bbox_hit is false for all of them — no ray, no face
+                // load (not where the LDS tiles' barriers need every wave)
+                if (!(kLdsTiles && coop && ob.tri_count > kDirectMax) && point_box_xy(ob) &&
+                    !__any(have && !decided && !point_box_rejects(ob, add(P, mul(N, 0.1f)), sub(Lp, P))))
+                    continue;
                 int f = -1;
                 float u, v, t;
                 if (!kLdsTiles || ob.tri_count <= kDirectMax) {
@@ -1297,10 +1303,13 @@ __device__ __forceinline__ bool inside(const SubRect& r, int32_t sx, int32_t sy)
 
 // The background of the non-detail sub-blocks: fill workgroup f of nf strides over the 64 x 4
 // blocks (shared by the frame kernel's fill roles and fill_kernel).
+// s_waitcnt immediate (gfx9 encoding: vmcnt bits 3:0 and 15:14, expcnt 6:4, lgkmcnt 11:8) of the
+// fill's per-block pacing: vmcnt(0), expcnt / lgkmcnt not waited for
+constexpr int kFillPace = 0x0f70;
 template <bool kDev, bool kNt>
 __device__ __forceinline__ void fill_blocks(const FrameParams& p, const FrameOut& o, const CamState* cs,
                                             const uint8_t* detail_occ, uint32_t f, uint32_t nf, uint32_t wave,
-                                            uint32_t lane, bool aligned) {
+                                            uint32_t lane, bool aligned, bool pace) {
     constexpr uint32_t nwaves = kWG / 64;
     wave = __builtin_amdgcn_readfirstlane(wave);  // (block coordinates in SGPRs)
     const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
@@ -1329,6 +1338,7 @@ __device__ __forceinline__ void fill_blocks(const FrameParams& p, const FrameOut
             if ((it & 63u) == 0) {
                 const uint32_t b = blk + lane * fstride;
                 occ = b < nblk ? detail_occ[b] : 0u;
+                asm volatile("" : "+v"(occ));  // (waited for here; the pacing below is explicit)
             }
             mask = (uint32_t)__builtin_amdgcn_readlane((int)occ, (int)(it & 63u));
         }
@@ -1341,8 +1351,19 @@ __device__ __forceinline__ void fill_blocks(const FrameParams& p, const FrameOut
                 mask |= (sx >= r.sx0 && sx <= r.sx1) ? (1u << i) : 0u;
             }
         }
+        // Pacing beside detail work: each block's stores wait until the wave's earlier stores are
+        // acknowledged (vmcnt counts them).  Unpaced fill waves flood the memory system and
+        // lengthen the detail waves' load chains — 3840x2160 / 70k 19.8 -> 24.6 us per frame, C3
+        // 22.2 -> 27.2, C5 128 -> 141; C2 (8 frames) 40.9 -> 43.5 — and a looser bound (vmcnt(5)
+        // or (10)) is no better; a fill with the GPU to itself is faster unpaced (3840x2160 18.3
+        // vs 21.5 us), same-box A/B profiles/r05/ab/.
+        if (pace) __builtin_amdgcn_s_waitcnt(kFillPace);
         if (!mask) {
-            if (bx < full_x && by < full_y)
+            // the hoisted-offset stores where the fill is paced and cached (C2 8 frames 52.8 ->
+            // 41.2 us); unpaced or non-temporal, the per-block address form writes faster (fill
+            // alone at 3840x2160 in 4 slots 23.3 -> 19.8 us, C5 130 -> 123 us), same-box A/B
+            // profiles/r05/ab/
+            if (!kNt && pace && bx < full_x && by < full_y)
                 fill_block_fast<kNt>(p, o, bf, bx, by, lane);
             else
                 fill_background<kBlkW, kNt>(p, o, bx * kBlkW, by * kBlkH, aligned, lane);
@@ -1357,16 +1378,18 @@ __device__ __forceinline__ void fill_blocks(const FrameParams& p, const FrameOut
 // frame v % F, its (v / F)-th fill workgroup.
 template <bool kDev>
 __device__ __forceinline__ void fill_frames(const FrameParams& p, uint32_t q, uint32_t nf, uint32_t wave, uint32_t lane,
-                                            bool aligned) {
+                                            bool aligned, bool pace) {
     const uint32_t F = p.nframes, roles = max(nf, F);
     for (uint32_t v = q; v < roles; v += nf) {
         const uint32_t fr = v % F, slot = p.dev_slots ? fr : 0u;
         const uint8_t* occ = p.detail_occ ? p.detail_occ + (size_t)slot * (p.dlist_stride / 4) : nullptr;
         const FrameOut o = frame_out(p, fr);
         if (o.nt)
-            fill_blocks<kDev, true>(p, o, p.cam_state + slot, occ, v / F, (roles - fr + F - 1) / F, wave, lane, aligned);
+            fill_blocks<kDev, true>(p, o, p.cam_state + slot, occ, v / F, (roles - fr + F - 1) / F, wave, lane, aligned,
+                                    pace);
         else
-            fill_blocks<kDev, false>(p, o, p.cam_state + slot, occ, v / F, (roles - fr + F - 1) / F, wave, lane, aligned);
+            fill_blocks<kDev, false>(p, o, p.cam_state + slot, occ, v / F, (roles - fr + F - 1) / F, wave, lane, aligned,
+                                     pace);
     }
 }
 
@@ -1627,7 +1650,7 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     const uint32_t f = nd < grid ? bid - nd : bid;
     if (f >= nf) return;
     ERAY_TRACE_POINT(2);
-    fill_frames<kDev>(p, f, nf, wave, lane, aligned);
+    fill_frames<kDev>(p, f, nf, wave, lane, aligned, nd != 0);  // (paced beside detail work)
     ERAY_TRACE_POINT(3);
 }
 
@@ -1639,7 +1662,7 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
 // blocks from two workgroups per CU: profiles/r04/ab/ab_flat_fill.txt, launch spans.)
 template <bool kDev>
 __global__ void __launch_bounds__(kWG) fill_kernel(FrameParams p) {
-    fill_frames<kDev>(p, blockIdx.x, gridDim.x, threadIdx.x >> 6, threadIdx.x & 63, p.aligned != 0);
+    fill_frames<kDev>(p, blockIdx.x, gridDim.x, threadIdx.x >> 6, threadIdx.x & 63, p.aligned != 0, true);
 }
 
 // Image<Color>::save_as_ppm body: byte row k = image row h-1-k.
