@@ -14,7 +14,8 @@
 // against the host glibc over every finite float (tests/test_libm_restatement.py).
 //
 // The 4/pi table is the binary expansion of 4/pi in sliding 32-bit windows (8 new bits per
-// entry); it is derived from first principles in tests/test_libm_restatement.py.
+// entry), kept here as the packed bit string (inv_pio4_word); it is derived from first principles
+// in tests/test_libm_restatement.py.
 #pragma once
 
 #include <stdint.h>
@@ -47,13 +48,23 @@ constexpr double kS1 = -0x1.555545995a603p-3, kS2 = 0x1.1107605230bc4p-7, kS3 = 
 // the table's sign[q & 3] = {1, -1, -1, 1}: negative when bits 0 and 1 of q differ
 ERAY_HD inline double quadrant_sign(int q) { return ((q ^ (q >> 1)) & 1) ? -1.0 : 1.0; }
 
-ERAY_HD inline uint32_t inv_pio4(int i) {
-    static const uint32_t kInvPio4[24] = {
-        0xa2u,       0xa2f9u,     0xa2f983u,   0xa2f9836eu, 0xf9836e4eu, 0x836e4e44u,
-        0x6e4e4415u, 0x4e441529u, 0x441529fcu, 0x1529fc27u, 0x29fc2757u, 0xfc2757d1u,
-        0x2757d1f5u, 0x57d1f534u, 0xd1f534ddu, 0xf534ddc0u, 0x34ddc0dbu, 0xddc0db62u,
-        0xc0db6295u, 0xdb629599u, 0x6295993cu, 0x95993c43u, 0x993c4390u, 0x3c439041u};
-    return kInvPio4[i];
+// The published 24-entry table (sincosf_data.c __inv_pio4): entry i holds the 32 bits at bit 8i
+// of the string "24 zero bits, then 4/pi's bits".  That string as 32-bit words, selected by
+// index (immediates: a per-lane table index made every large-argument reduction three dependent
+// vector loads on the GPU); checked against 4/pi derived from first principles in
+// tests/test_libm_restatement.py.
+ERAY_HD inline uint32_t inv_pio4_word(int j) {  // j in 0..6
+    return j == 0 ? 0x000000a2u
+         : j == 1 ? 0xf9836e4eu
+         : j == 2 ? 0x441529fcu
+         : j == 3 ? 0x2757d1f5u
+         : j == 4 ? 0x34ddc0dbu
+         : j == 5 ? 0x6295993cu
+                  : 0x439041feu;
+}
+// the 32 bits at bit 8 * (4j + q) of the string (words j, j + 1; q in 0..3): table entry 4j + q
+ERAY_HD inline uint32_t inv_pio4_window(uint32_t hi, uint32_t lo, int q) {
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (32 - 8 * q));
 }
 
 ERAY_HD inline uint32_t f32_bits(float f) {
@@ -97,9 +108,31 @@ ERAY_HD inline double reduce_large(uint32_t xi, int* np) {
     int shift = (int)((xi >> 23) & 7);
     xi = (xi & 0xffffffu) | 0x800000u;
     xi <<= shift;
-    uint64_t res0 = (uint64_t)(uint32_t)(xi * inv_pio4(base));
-    uint64_t res1 = (uint64_t)xi * inv_pio4(base + 4);
-    uint64_t res2 = (uint64_t)xi * inv_pio4(base + 8);
+    // the table's entries base, base + 4 and base + 8 (base <= 15: words up to 6)
+    uint32_t t0, t4, t8;
+    auto entries = [&](int b) {
+        const int j = b >> 2, q = b & 3;
+        const uint32_t w0 = inv_pio4_word(j), w1 = inv_pio4_word(j + 1), w2 = inv_pio4_word(j + 2),
+                       w3 = inv_pio4_word(j + 3);
+        t0 = inv_pio4_window(w0, w1, q);
+        t4 = inv_pio4_window(w1, w2, q);
+        t8 = inv_pio4_window(w2, w3, q);
+    };
+#if defined(__HIP_DEVICE_COMPILE__)
+    // a wave whose lanes share the row (main.rs's arguments 120..205 all do) selects it with
+    // scalar instructions (kept apart from the per-lane path, which the compiler would merge)
+    const int ub = __builtin_amdgcn_readfirstlane(base);
+    if (__all(base == ub)) {
+        entries(ub);
+        asm volatile("" : "+s"(t0), "+s"(t4), "+s"(t8));
+    } else
+#endif
+    {
+        entries(base);
+    }
+    uint64_t res0 = (uint64_t)(uint32_t)(xi * t0);
+    uint64_t res1 = (uint64_t)xi * t4;
+    uint64_t res2 = (uint64_t)xi * t8;
     res0 = (res2 >> 32) | (res0 << 32);
     res0 += res1;
     uint64_t n = (res0 + (1ULL << 61)) >> 62;
@@ -107,6 +140,24 @@ ERAY_HD inline double reduce_large(uint32_t xi, int* np) {
     double x = (double)(int64_t)res0;
     *np = (int)n;
     return x * 0x1.921FB54442D18p-62;
+}
+
+// a / 10.0f, correctly rounded (wave.rs:127's `/ 10.`): for biased exponents 32..254 a product
+// by 0.1f and one FMA correction (q0 = a * 0.1f, r = a - 10 q0 exactly, q0 + r * 0.1f) equals the
+// IEEE quotient — checked for every float of that range in tests/test_libm_restatement.py (it
+// differs only for subnormal-range and non-finite inputs, which take the division)
+ERAY_HD inline float div10_f32(float a) {
+    const uint32_t e = (f32_bits(a) >> 23) & 0xffu;
+    if (e >= 32u && e <= 254u) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const float q0 = a * 0x1.99999ap-4f;
+        return __builtin_fmaf(__builtin_fmaf(-q0, 10.0f, a), 0x1.99999ap-4f, q0);
+#else
+        const float q0 = a * 0x1.99999ap-4f;
+        return fmaf(fmaf(-q0, 10.0f, a), 0x1.99999ap-4f, q0);
+#endif
+    }
+    return a / 10.0f;
 }
 
 // cosf(y) as computed by the reference platform's libm.

@@ -267,7 +267,7 @@ __device__ __noinline__ bool texel_program(const uint32_t* prog, uint32_t out, f
     for (uint32_t k = n; k-- > 0;) {
         const TexelInstr& t = ins[k];
         if (t.kind == 0) {  // wave
-            vr[k] = __builtin_fabsf(libm::cosf_glibc(((float)cx[k] * t.p[0] + (float)cy[k] * t.p[1]) / 10.0f));
+            vr[k] = __builtin_fabsf(libm::cosf_glibc(libm::div10_f32((float)cx[k] * t.p[0] + (float)cy[k] * t.p[1])));
         } else if (t.kind == 1) {  // rgb
             vr[k] = vr[t.c[0]];
             vg[k] = vr[t.c[1]];

@@ -1078,7 +1078,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
         if (kExample && mat.example) {  // main.rs's graph at the texel Material::get would read
             const uint32_t ix = mod_size(sat_u32(uv0 * (float)mat.ex_w), mat.ex_w);
             const uint32_t iy = mod_size(sat_u32(uv1 * (float)mat.ex_h), mat.ex_h);
-            const float wv = __builtin_fabsf(libm::cosf_glibc(((float)ix * mat.ex_xf + (float)iy * mat.ex_yf) / 10.0f));
+            const float wv = __builtin_fabsf(libm::cosf_glibc(libm::div10_f32((float)ix * mat.ex_xf + (float)iy * mat.ex_yf)));
             const float omf = 1.0f - mat.ex_factor;  // mix_color.rs:89 (material_example_kernel)
             color = rgb{wv * omf + mat.ex_r * mat.ex_factor, wv * omf + mat.ex_g * mat.ex_factor,
                         wv * omf + mat.ex_b * mat.ex_factor};
@@ -1306,15 +1306,17 @@ __device__ __forceinline__ bool inside(const SubRect& r, int32_t sx, int32_t sy)
 // s_waitcnt immediate (gfx9 encoding: vmcnt bits 3:0 and 15:14, expcnt 6:4, lgkmcnt 11:8) of the
 // fill's per-block pacing: vmcnt(0), expcnt / lgkmcnt not waited for
 constexpr int kFillPace = 0x0f70;
-template <bool kDev, bool kNt>
+template <bool kDev, bool kNt, bool kPace>
 __device__ __forceinline__ void fill_blocks(const FrameParams& p, const FrameOut& o, const CamState* cs,
                                             const uint8_t* detail_occ, uint32_t f, uint32_t nf, uint32_t wave,
-                                            uint32_t lane, bool aligned, bool pace) {
+                                            uint32_t lane, bool aligned) {
     constexpr uint32_t nwaves = kWG / 64;
     wave = __builtin_amdgcn_readfirstlane(wave);  // (block coordinates in SGPRs)
     const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
     const uint32_t fstride = nf * nwaves;
-    const BlockFill bf = block_fill(p.img_w, lane);
+    constexpr bool kFast = kPace && !kNt;  // (below)
+    BlockFill bf;
+    if constexpr (kFast) bf = block_fill(p.img_w, lane);
     // blocks (bx, by) with bx < full_x and by < full_y are whole 64 x 4 blocks inside the frame
     const uint32_t full_x = aligned ? p.cam_w / kBlkW : 0u, full_y = p.rows / kBlkH;
     uint32_t occ = 0;  // detail list: lane i holds the occupancy of this wave's i-th next block
@@ -1357,13 +1359,13 @@ __device__ __forceinline__ void fill_blocks(const FrameParams& p, const FrameOut
         // 22.2 -> 27.2, C5 128 -> 141; C2 (8 frames) 40.9 -> 43.5 — and a looser bound (vmcnt(5)
         // or (10)) is no better; a fill with the GPU to itself is faster unpaced (3840x2160 18.3
         // vs 21.5 us), same-box A/B profiles/r05/ab/.
-        if (pace) __builtin_amdgcn_s_waitcnt(kFillPace);
+        if constexpr (kPace) __builtin_amdgcn_s_waitcnt(kFillPace);
         if (!mask) {
             // the hoisted-offset stores where the fill is paced and cached (C2 8 frames 52.8 ->
             // 41.2 us); unpaced or non-temporal, the per-block address form writes faster (fill
             // alone at 3840x2160 in 4 slots 23.3 -> 19.8 us, C5 130 -> 123 us), same-box A/B
             // profiles/r05/ab/
-            if (!kNt && pace && bx < full_x && by < full_y)
+            if (kFast && bx < full_x && by < full_y)
                 fill_block_fast<kNt>(p, o, bf, bx, by, lane);
             else
                 fill_background<kBlkW, kNt>(p, o, bx * kBlkW, by * kBlkH, aligned, lane);
@@ -1384,12 +1386,18 @@ __device__ __forceinline__ void fill_frames(const FrameParams& p, uint32_t q, ui
         const uint32_t fr = v % F, slot = p.dev_slots ? fr : 0u;
         const uint8_t* occ = p.detail_occ ? p.detail_occ + (size_t)slot * (p.dlist_stride / 4) : nullptr;
         const FrameOut o = frame_out(p, fr);
-        if (o.nt)
-            fill_blocks<kDev, true>(p, o, p.cam_state + slot, occ, v / F, (roles - fr + F - 1) / F, wave, lane, aligned,
-                                    pace);
+        const uint32_t g = v / F, ng = (roles - fr + F - 1) / F;
+        const CamState* cs = p.cam_state + slot;
+        // (separate loops: the unpaced fill, without the paced one's lane constants in its
+        // registers, writes a 4-slot 3840x2160 frame in 19.8 instead of 22.3 us)
+        if (o.nt && pace)
+            fill_blocks<kDev, true, true>(p, o, cs, occ, g, ng, wave, lane, aligned);
+        else if (o.nt)
+            fill_blocks<kDev, true, false>(p, o, cs, occ, g, ng, wave, lane, aligned);
+        else if (pace)
+            fill_blocks<kDev, false, true>(p, o, cs, occ, g, ng, wave, lane, aligned);
         else
-            fill_blocks<kDev, false>(p, o, p.cam_state + slot, occ, v / F, (roles - fr + F - 1) / F, wave, lane, aligned,
-                                     pace);
+            fill_blocks<kDev, false, false>(p, o, cs, occ, g, ng, wave, lane, aligned);
     }
 }
 
@@ -1621,7 +1629,19 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
                     // the first object's descriptor is loaded before the list entry is waited for:
                     // the first sub-block's two inputs in one round trip
                     const ObjGeom g0 = nobj ? sc.geom(0) : ObjGeom{};
+                    // The scalar cache lines of what the shading reads after the search — the first
+                    // object's MaterialDesc (its two 64-B lines) and the lights — touched now, in
+                    // the same round trip: their first reads come after the search, each a scalar
+                    // cache miss in a dependent chain otherwise
+                    uint32_t warm = 0;
+                    if (nobj) {
+                        const uint32_t* od = reinterpret_cast<const uint32_t*>(objs);
+                        warm = load_const(od + 16, 0) ^ load_const(od + 32, 0);
+                    }
+                    if (h_counts >> 16) warm ^= load_const(reinterpret_cast<const uint32_t*>(h_lights), 0);
+                    if ((h_counts >> 16) > 2u) warm ^= load_const(reinterpret_cast<const uint32_t*>(h_lights + 2), 0);
                     first_rays();
+                    asm volatile("" ::"s"(warm));
                     if (dlist)
                         for (uint32_t oi = 0; oi < nobj; ++oi) {
                             const ObjGeom g = oi == 0 ? g0 : sc.geom(oi);

@@ -2,11 +2,13 @@
 // and the fused evaluation of main.rs's material graph.
 //
 // All of them are streaming, HBM-write-bound kernels (0 reads for wave/flat, 12 B/texel of
-// reads for rgb, 24 for mix): each thread produces kVec consecutive texels so that every
-// store is a 16-B-per-lane (dwordx4) store when the row is aligned, with a scalar tail.
-// The grid is capped at 256 CUs x 8 blocks and strides over the image.
+// reads for rgb, 24 for mix).  rgb, flat and mix produce kVec consecutive texels per thread so
+// that every store is a 16-B-per-lane (dwordx4) store when the row is aligned, with a scalar
+// tail; wave and the fused material kernel one texel per thread (below).  Grids stride over the
+// image.
 #include "device_math.hpp"
 #include "glibc_cosf.hpp"
+#include "int_div.hpp"
 #include "internal.hpp"
 
 namespace eray {
@@ -30,45 +32,45 @@ inline unsigned grid_for(size_t items) {
 
 // wave.rs:127 — |cos((x as f32 * x_fac + y as f32 * y_fac) / 10.)|
 __device__ __forceinline__ float wave_value(uint32_t x, uint32_t y, float xf, float yf) {
-    float arg = ((float)x * xf + (float)y * yf) / 10.0f;
+    const float arg = libm::div10_f32((float)x * xf + (float)y * yf);
     return __builtin_fabsf(libm::cosf_glibc(arg));
 }
 
-// kVec consecutive texels of the row-major image per thread, from index i0 (x advances with a
-// wrap instead of a division per texel; texels past n are computed and not stored).
-template <typename F>
-__device__ __forceinline__ void wave_values(size_t i0, uint32_t w, float xf, float yf, F&& each) {
-    uint32_t y = (uint32_t)(i0 / w), x = (uint32_t)(i0 - (size_t)y * w);
-#pragma unroll
-    for (int k = 0; k < kVec; ++k) {
-        each(k, wave_value(x, y, xf, yf));
-        if (++x == w) {
-            x = 0;
-            ++y;
-        }
-    }
+// One texel per thread: the restated cosf is a chain of dependent double-precision steps, so
+// its latency is hidden by resident waves (measured faster than four texels per thread with 16-B
+// stores: 6.9 vs 10.1 us per 1024 x 1024 material update, profiles/r05/ab/).  Below 2^32 texels
+// (and 4 GB of output) the texel's row is a multiply-high by the launch's invariant divisor
+// (int_div.hpp) and the stores buffer stores with 32-bit offsets: the index arithmetic is a few
+// of the ~110 VALU instructions per texel the cosf leaves (profiles/r05/material_pmc.json).
+struct TexelIndex {
+    uint32_t w;
+    DivU32 dw;  // texel index / w
+};
+__device__ __forceinline__ void texel_xy(uint32_t i, const TexelIndex& t, uint32_t& x, uint32_t& y) {
+    y = div_u32(i, t.dw);
+    x = i - y * t.w;
+}
+__device__ __forceinline__ void store_f32(float* base, uint32_t byte_off, float v) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, -1, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, byte_off, 0, 0);
 }
 
-__device__ __forceinline__ void store4(float* __restrict__ out, size_t i0, size_t n, const float (&v)[kVec]) {
-    float* p = out + i0;
-    if (i0 + kVec <= n && ((reinterpret_cast<uintptr_t>(p) & 15) == 0)) {
-        *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-    } else {
-        for (int k = 0; k < kVec && i0 + k < n; ++k) p[k] = v[k];
-    }
-}
-
-// The restated cosf's coefficients are immediates (glibc_cosf.hpp), so a texel is a short chain
-// of double-precision steps; kVec texels per thread give each wave four independent chains and
-// 16-B stores.
-__global__ void __launch_bounds__(kBlock) wave_kernel(uint32_t w, uint32_t h, float xf, float yf,
+template <bool kWide>  // kWide: 64-bit indices (2^32 texels or more)
+__global__ void __launch_bounds__(kBlock) wave_kernel(TexelIndex t, uint32_t h, float xf, float yf,
                                                       float* __restrict__ out) {
-    const size_t n = (size_t)w * h;
-    const size_t stride = (size_t)gridDim.x * kBlock * kVec;
-    for (size_t i0 = ((size_t)blockIdx.x * kBlock + threadIdx.x) * kVec; i0 < n; i0 += stride) {
-        float v[kVec];
-        wave_values(i0, w, xf, yf, [&](int k, float x) { v[k] = x; });
-        store4(out, i0, n, v);
+    if constexpr (kWide) {
+        const size_t n = (size_t)t.w * h, stride = (size_t)gridDim.x * kBlock;
+        for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+            const uint32_t y = (uint32_t)(i / t.w), x = (uint32_t)(i - (size_t)y * t.w);
+            out[i] = wave_value(x, y, xf, yf);
+        }
+    } else {
+        const uint32_t n = t.w * h, stride = gridDim.x * kBlock;
+        for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+            uint32_t x, y;
+            texel_xy(i, t, x, y);
+            store_f32(out, 4u * i, wave_value(x, y, xf, yf));
+        }
     }
 }
 
@@ -151,19 +153,16 @@ __global__ void __launch_bounds__(kBlock) mix_kernel(uint32_t w, uint32_t h, Tex
 // main.rs:80-144 fused: wave -> rgb(wave, wave, wave) -> mix(.., flat(r, g, b), factor);
 // diffuse = wave.  Every node's image has the graph's width x height, so mix's mod_get is the
 // identity and the chain reduces to per-texel arithmetic in the nodes' own operation order
-// (r * factor is the same product per texel, so it is formed once).  kMatTexels texels per
-// thread (1: the cosf chains' latency is hidden by resident waves, measured faster than 4 texels
-// per thread with 16-B stores: 7.3 vs 10.1 us per 1024 x 1024 update, profiles/r05/ab/).
-constexpr int kMatTexels = 1;
+// (r * factor is the same product per texel, so it is formed once).
+template <bool kWide>
 __global__ void __launch_bounds__(kBlock) material_example_kernel(
-    uint32_t w, uint32_t h, float xf, float yf, float r, float g, float b, float factor,
+    TexelIndex t, uint32_t h, float xf, float yf, float r, float g, float b, float factor,
     float* __restrict__ color, float* __restrict__ diffuse) {
-    const size_t n = (size_t)w * h;
     const float omf = 1.0f - factor, rf = r * factor, gf = g * factor, bf = b * factor;
-    if constexpr (kMatTexels == 1) {
-        const size_t stride = (size_t)gridDim.x * kBlock;
+    if constexpr (kWide) {
+        const size_t n = (size_t)t.w * h, stride = (size_t)gridDim.x * kBlock;
         for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-            const uint32_t y = (uint32_t)(i / w), x = (uint32_t)(i - (size_t)y * w);
+            const uint32_t y = (uint32_t)(i / t.w), x = (uint32_t)(i - (size_t)y * t.w);
             const float v = wave_value(x, y, xf, yf), m = v * omf;
             if (color) {
                 float* c = color + 3 * i;
@@ -174,28 +173,34 @@ __global__ void __launch_bounds__(kBlock) material_example_kernel(
             if (diffuse) diffuse[i] = v;
         }
     } else {
-        const size_t stride = (size_t)gridDim.x * kBlock * kVec;
-        for (size_t i0 = ((size_t)blockIdx.x * kBlock + threadIdx.x) * kVec; i0 < n; i0 += stride) {
-            float v[kVec], c[kVec][3];
-            wave_values(i0, w, xf, yf, [&](int k, float x) {
-                v[k] = x;
-                const float m = x * omf;
-                c[k][0] = m + rf;
-                c[k][1] = m + gf;
-                c[k][2] = m + bf;
-            });
-            if (color) store_rgb4(color, i0, n, c);
-            if (diffuse) store4(diffuse, i0, n, v);
+        const uint32_t n = t.w * h, stride = gridDim.x * kBlock;
+        for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+            uint32_t x, y;
+            texel_xy(i, t, x, y);
+            const float v = wave_value(x, y, xf, yf), m = v * omf;
+            if (color) {
+                store_f32(color, 12u * i, m + rf);
+                store_f32(color, 12u * i + 4u, m + gf);
+                store_f32(color, 12u * i + 8u, m + bf);
+            }
+            if (diffuse) store_f32(diffuse, 4u * i, v);
         }
     }
 }
 
 }  // namespace
 
+// 32-bit texel indices and byte offsets while the largest output (12 B per texel) stays below 4 GB
+inline bool narrow_texels(size_t n) { return n * 12 <= UINT32_MAX; }
+
 hipError_t launch_wave(uint32_t w, uint32_t h, float xf, float yf, float* out, hipStream_t s) {
     size_t n = (size_t)w * h;
     if (!n) return hipSuccess;
-    wave_kernel<<<grid_for(n), kBlock, 0, s>>>(w, h, xf, yf, out);
+    const TexelIndex t{w, make_div_u32(w)};
+    if (narrow_texels(n))
+        wave_kernel<false><<<grid_for1(n), kBlock, 0, s>>>(t, h, xf, yf, out);
+    else
+        wave_kernel<true><<<grid_for1(n), kBlock, 0, s>>>(t, h, xf, yf, out);
     return hipGetLastError();
 }
 hipError_t launch_rgb(uint32_t w, uint32_t h, const float* r, const float* g, const float* b,
@@ -224,8 +229,11 @@ hipError_t launch_material_example(uint32_t w, uint32_t h, float xf, float yf, f
                                    hipStream_t s) {
     size_t n = (size_t)w * h;
     if (!n) return hipSuccess;
-    material_example_kernel<<<kMatTexels == 1 ? grid_for1(n) : grid_for(n), kBlock, 0, s>>>(w, h, xf, yf, r, g, b, factor, color,
-                                                           diffuse);
+    const TexelIndex t{w, make_div_u32(w)};
+    if (narrow_texels(n))
+        material_example_kernel<false><<<grid_for1(n), kBlock, 0, s>>>(t, h, xf, yf, r, g, b, factor, color, diffuse);
+    else
+        material_example_kernel<true><<<grid_for1(n), kBlock, 0, s>>>(t, h, xf, yf, r, g, b, factor, color, diffuse);
     return hipGetLastError();
 }
 

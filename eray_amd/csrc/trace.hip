@@ -144,7 +144,7 @@ __device__ void fill_level(const FrameParams& p, f3 o, f3 d, const Hit& h, Level
     if (mat.example) {  // main.rs's graph at the texel Material::get reads
         const uint32_t ix = mod_size(sat_u32(uv0 * (float)mat.ex_w), mat.ex_w);
         const uint32_t iy = mod_size(sat_u32(uv1 * (float)mat.ex_h), mat.ex_h);
-        const float wv = __builtin_fabsf(libm::cosf_glibc(((float)ix * mat.ex_xf + (float)iy * mat.ex_yf) / 10.0f));
+        const float wv = __builtin_fabsf(libm::cosf_glibc(libm::div10_f32((float)ix * mat.ex_xf + (float)iy * mat.ex_yf)));
         const float omf = 1.0f - mat.ex_factor;
         L.color = rgb{wv * omf + mat.ex_r * mat.ex_factor, wv * omf + mat.ex_g * mat.ex_factor,
                       wv * omf + mat.ex_b * mat.ex_factor};

@@ -49,8 +49,42 @@ def test_cosf_matches_host_glibc(tmp_path):
     assert bad == 0, f"{bad} of {tot} differ from glibc cosf"
 
 
+DIV10_PROG = r"""
+#include "%s"
+#include <cstdio>
+int main() {
+  long bad = 0, fast = 0;
+#pragma omp parallel for reduction(+:bad,fast) schedule(dynamic, 1)
+  for (long hi = 0; hi < 256; ++hi)
+    for (unsigned lo = 0; lo < (1u << 24); ++lo) {
+      unsigned u = (unsigned)(hi << 24) | lo; float a; memcpy(&a, &u, 4);
+      volatile float ten = 10.0f;
+      const float g = a / ten, r = eray::libm::div10_f32(a);
+      const unsigned e = (u >> 23) & 0xffu;
+      if (e >= 32u && e <= 254u) ++fast;
+      if (!(g != g && r != r) && eray::libm::f32_bits(g) != eray::libm::f32_bits(r)) ++bad;
+    }
+  printf("%%ld %%ld\n", bad, fast);
+  return 0;
+}
+"""
+
+
+def test_div10_is_the_ieee_quotient_for_every_float(tmp_path):
+    """div10_f32 (the wave node's `/ 10.`) against the host's IEEE division, all 2^32 inputs."""
+    src = tmp_path / "d.cpp"
+    src.write_text(DIV10_PROG % HDR)
+    exe = tmp_path / "d"
+    subprocess.run(["g++", "-O2", "-fopenmp", "-ffp-contract=off", "-std=c++17", str(src), "-o", str(exe), "-lm"],
+                   check=True)
+    bad, fast = map(int, subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split())
+    assert fast > 3_700_000_000  # the product-and-correction path covers all but the extremes
+    assert bad == 0
+
+
 def test_inv_pio4_table_is_four_over_pi():
-    """The 24-entry table holds 4/pi's bits in 32-bit windows advancing 8 bits per entry."""
+    """The published 24-entry table holds 4/pi's bits in 32-bit windows advancing 8 bits per entry:
+    the header keeps the string "24 zero bits, then 4/pi" as 32-bit words (inv_pio4_word)."""
     prec = 400
     one = 1 << prec
 
@@ -65,17 +99,16 @@ def test_inv_pio4_table_is_four_over_pi():
 
     pi = 4 * (4 * arctan_inv(5) - arctan_inv(239))
     bits = bin((4 << (2 * prec)) // pi)[2:]
-    byts = [int(bits[i * 8:(i + 1) * 8], 2) for i in range(30)]
-    want = []
-    for k in range(24):
-        w = 0
-        for j in range(k - 3, k + 1):
-            w = (w << 8) | (byts[j] if j >= 0 else 0)
-        want.append(w & 0xFFFFFFFF)
+    byts = [0, 0, 0] + [int(bits[i * 8:(i + 1) * 8], 2) for i in range(30)]
+    want = [int.from_bytes(bytes(byts[4 * j:4 * j + 4]), "big") for j in range(7)]
     text = open(HDR).read()
-    block = text[text.index("kInvPio4[24]"):]
-    got = [int(h, 16) for h in re.findall(r"0x([0-9a-f]+)u", block)[:24]]
+    block = text[text.index("inline uint32_t inv_pio4_word"):]
+    got = [int(h, 16) for h in re.findall(r"0x([0-9a-f]+)u", block)[:7]]
     assert got == want
+    # the windows of the table's 24 entries (the published values, sliding 8 bits per entry)
+    word = int("".join(f"{w:032b}" for w in got), 2)
+    entries = [(word >> (7 * 32 - 32 - 8 * i)) & 0xFFFFFFFF for i in range(24)]
+    assert entries[:4] == [0xa2, 0xa2f9, 0xa2f983, 0xa2f9836e] and entries[23] == 0x3c439041
 
 
 # ----------------------------------------------------------------------------------- powf ---
