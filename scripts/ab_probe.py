@@ -37,7 +37,11 @@ CONFIGS = {"fill4k1": ("none", 3840, 2160, 1, 1), "fill4k4": ("none", 3840, 2160
            "aa2": ("cube", 1920, 1080, 1, 1), "aa_ns": ("70k", 3840, 2160, 1, 1),
            "ns1sep": ("70k", 3840, 2160, 1, 1), "ns4sep": ("70k", 3840, 2160, 4, 1),
            "ns1ex": ("70k", 3840, 2160, 1, 1), "ns4ex": ("70k", 3840, 2160, 4, 1), "c2ex": ("cube", 1920, 1080, 8, 8),
-           "mat": ("cube", 1920, 1080, 1, 1)}
+           "mat": ("cube", 1920, 1080, 1, 1),
+           # C5's 8-GPU split on one GPU: rank r's share (row0 = 4r, 4-row bands every 32 rows)
+           **{f"c5s{r}": ("1m", 7680, 4320, 1, 1) for r in range(8)},
+           # ... with frames in flight: 4 frames per launch into 4 slots (and the whole frame, 2 per launch)
+           **{f"c5s{r}f4": ("1m", 7680, 4320, 4, 4) for r in range(8)}, "c5f2": ("1m", 7680, 4320, 2, 2)}
 # launch-shape overrides (eray_render_params::flags) of the *sep configs: the dense build beside a
 # separate fill kernel
 SEPARATE = ("ns1sep", "ns4sep")
@@ -78,6 +82,12 @@ def main() -> None:
             rgb = torch.empty((slots, H, W, 3), dtype=torch.float32, device="cuda")
             ppm = torch.empty((slots, H, W, 3), dtype=torch.uint8, device="cuda")
         kw = dict(out_rgb=rgb.data_ptr(), out_ppm=ppm.data_ptr(), ring=capi.frame_ring(slots, H, W, F))
+        if name.startswith("c5s"):
+            from eray_amd.dist import band_split
+            sp = band_split(int(name[3]), 8, H, 4)
+            kw.update(row0=sp["row0"], rows=sp["rows"], band_rows=sp["band_rows"], band_stride=sp["band_stride"])
+            if F == 1:
+                del kw["ring"]
         if name in SEPARATE:
             kw["flags"] = capi.RENDER_DENSE_DETAIL | capi.RENDER_SEPARATE_FILL
         if name == "mat":
@@ -96,7 +106,7 @@ def main() -> None:
         else:
             ctx.render_frames(max(slots, 4), W, H, **kw)
             ctx.time_frames(2 * F, W, H, **kw)  # (warm: a first launch after the setup can take ms)
-            n = max(args.launches // (4 if name == "c5" else 1), 2) * F
+            n = max(args.launches // (4 if name.startswith("c5") and "s" not in name else 1), 2) * F
             out[name] = ctx.time_frames(n, W, H, **kw)
         torch.cuda.synchronize()
         del rgb, ppm

@@ -1,7 +1,8 @@
 """Per-workgroup timeline of one frame_kernel launch (diagnostics; needs the trace build,
 scripts/build_trace.sh, selected with ERAY_LIB=eray_amd/lib/liberay_hip_trace.so).
-Usage: python scripts/wg_trace.py MESH W H [SLOTS]   (SLOTS > 1: a ring of frame slots, one frame
-per launch, so that the traced frame's stores go to HBM when the ring exceeds the Infinity Cache)"""
+Usage: python scripts/wg_trace.py MESH W H [SLOTS [FRAMES]]   (SLOTS > 1: a ring of frame slots, one
+frame per launch unless FRAMES (frames per launch, C2: 8 8), so that the traced frame's stores go to
+HBM when the ring exceeds the Infinity Cache)"""
 import ctypes as C
 import os
 import sys
@@ -21,19 +22,20 @@ W, H = int(sys.argv[2]), int(sys.argv[3])
 ctx = capi.Context(0)
 sc = MainScene(ctx, *mesh, W, H, fov=frame_camera_fov(W, H))
 slots = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+frames = int(sys.argv[5]) if len(sys.argv) > 5 else 1
 rgb = ctx.empty((slots, H, W, 3), np.float32)
 ppm = ctx.empty((slots, H, W, 3), np.uint8)
 lib = capi.lib()
 lib.eray_debug_read_trace.argtypes = [C.c_void_p, C.c_size_t]
 kw = dict(out_rgb=rgb.ptr, out_ppm=ppm.ptr)
 if slots > 1:
-    kw["ring"] = capi.frame_ring(slots, H, W, 1)
+    kw["ring"] = capi.frame_ring(slots, H, W, frames)
 ctx.render_frames(50, W, H, **kw)
 ctx.synchronize()
 n = 8192 * 64  # (scripts/microbench/render_trace.hip kTraceSlots)
 for rep in range(3):
     assert lib.eray_debug_clear_trace() == 0
-    ctx.render_frames(1, W, H, **kw)
+    ctx.render_frames(frames, W, H, **kw)
     ctx.synchronize()
     buf = (C.c_uint64 * n)()
     assert lib.eray_debug_read_trace(buf, n) == 0
