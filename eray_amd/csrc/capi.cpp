@@ -1245,7 +1245,7 @@ int prepare_render(eray_ctx* ctx, const eray_render_params* rp, FrameParams* out
         p.detail_heavy = ctx->bins.dcount;
         p.detail_occ = ctx->bins.docc;
     }
-    p.launch_flags = rp->flags & ~ERAY_RENDER_BRUTE_FORCE;
+    p.launch_flags = rp->flags & ~(ERAY_RENDER_BRUTE_FORCE | kLaunchRingBeyondCache);
     if (!cull) {  // every pixel in detail: one rectangle, the frame (sub-block units)
         if (p.nobj) {
             p.nrect = 1;
@@ -1496,6 +1496,8 @@ FrameParams ring_frames(const FrameParams& p, const Ring& r, uint32_t f, uint32_
     if (q.out_rgb) q.out_rgb = reinterpret_cast<float*>(reinterpret_cast<char*>(q.out_rgb) + slot * r.rgb);
     if (q.out_ppm) q.out_ppm += slot * r.ppm;
     if (q.out_face) q.out_face = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(q.out_face) + slot * r.face);
+    const uint64_t ring_bytes = (uint64_t)r.slots * ((q.out_rgb ? r.rgb : 0) + (q.out_ppm ? r.ppm : 0) + (q.out_face ? r.face : 0));
+    if (ring_bytes > kInfinityCacheBytes) q.launch_flags |= kLaunchRingBeyondCache;
     return q;
 }
 

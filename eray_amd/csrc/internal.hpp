@@ -382,6 +382,8 @@ hipError_t launch_set_camera(const CamDev& cam, CamDev* slot, hipStream_t s);
 // Launch overrides of eray_render_params::flags (eray_hip.h ERAY_RENDER_*) the frame launcher reads.
 constexpr uint32_t kLaunchDense = 2u, kLaunchNoDense = 4u, kLaunchSeparateFill = 8u, kLaunchNoSeparateFill = 16u,
                    kLaunchSharedDetail = 32u;
+// (internal, set per launch by the ring plan: the ring's slots together exceed the Infinity Cache)
+constexpr uint32_t kLaunchRingBeyondCache = 1u << 16;
 // Per-context launch resources: the separate fill kernel's stream and its fork / join events.
 // Measurement (eray_time_frames_ring): when frame_t[0] is set, the frame kernel is launched with
 // hipExtLaunchKernel's start / stop events, which take the dispatch's own begin / end timestamps

@@ -1670,7 +1670,11 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
     const uint32_t f = nd < grid ? bid - nd : bid;
     if (f >= nf) return;
     ERAY_TRACE_POINT(2);
-    fill_frames<kDev>(p, f, nf, wave, lane, aligned, nd != 0);  // (paced beside detail work)
+    // paced beside detail work — except small scenes whose ring of frames exceeds the Infinity Cache
+    // (C2 in 16 slots: 55.7 paced, 51.7 us unpaced per 8 frames; the binned north-star frame in
+    // 4 slots 25.1 paced, 29.7 unpaced), profiles/r05/ab/
+    const bool pace = nd != 0 && (p.detail_occ || !(p.launch_flags & kLaunchRingBeyondCache));
+    fill_frames<kDev>(p, f, nf, wave, lane, aligned, pace);
     ERAY_TRACE_POINT(3);
 }
 

@@ -31,7 +31,7 @@ from eray_amd.objfile import load_obj_file  # noqa: E402
 MESHES = {"cube": None, "70k": (69451, 42), "1m": (1_000_000, 1234)}
 CONFIGS = {"fill4k1": ("none", 3840, 2160, 1, 1), "fill4k4": ("none", 3840, 2160, 4, 1),
            "fill8k": ("none", 7680, 4320, 1, 1), "fillc2": ("none", 1920, 1080, 8, 8),
-           "c2": ("cube", 1920, 1080, 8, 8), "c3": ("70k", 1920, 1080, 4, 4), "ns1": ("70k", 3840, 2160, 1, 1),
+           "c2": ("cube", 1920, 1080, 8, 8), "c2b": ("cube", 1920, 1080, 16, 8), "c3": ("70k", 1920, 1080, 4, 4), "ns1": ("70k", 3840, 2160, 1, 1),
            "ns4": ("70k", 3840, 2160, 4, 1), "c5": ("1m", 7680, 4320, 1, 1), "moving_ns": ("70k", 3840, 2160, 1, 1),
            "moving_c5": ("1m", 7680, 4320, 1, 1),
            "aa2": ("cube", 1920, 1080, 1, 1), "aa_ns": ("70k", 3840, 2160, 1, 1),
