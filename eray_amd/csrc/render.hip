@@ -1306,12 +1306,16 @@ __device__ __forceinline__ bool inside(const SubRect& r, int32_t sx, int32_t sy)
 // s_waitcnt immediate (gfx9 encoding: vmcnt bits 3:0 and 15:14, expcnt 6:4, lgkmcnt 11:8) of the
 // fill's per-block pacing: vmcnt(0), expcnt / lgkmcnt not waited for
 constexpr int kFillPace = 0x0f70;
-template <bool kDev, bool kNt, bool kPace>
+// kSgpr: block coordinates in SGPRs (the store offsets' block part a scalar); without it they are
+// per-lane values and every store a full per-lane offset — faster for an unpaced fill into a ring
+// beyond the Infinity Cache (3840x2160 in 4 slots 23.0 -> 19.8 us), slower elsewhere (C2's fill
+// alone 34.7 -> 35.8 us, 3840x2160 / 70k 19.8 -> 20.1 us), same-box A/B profiles/r05/ab/ab_r05ah.txt
+template <bool kDev, bool kNt, bool kPace, bool kSgpr = true>
 __device__ __forceinline__ void fill_blocks(const FrameParams& p, const FrameOut& o, const CamState* cs,
                                             const uint8_t* detail_occ, uint32_t f, uint32_t nf, uint32_t wave,
                                             uint32_t lane, bool aligned) {
     constexpr uint32_t nwaves = kWG / 64;
-    wave = __builtin_amdgcn_readfirstlane(wave);  // (block coordinates in SGPRs)
+    if constexpr (kSgpr) wave = __builtin_amdgcn_readfirstlane(wave);
     const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
     const uint32_t fstride = nf * nwaves;
     constexpr bool kFast = kPace && !kNt;  // (below)
@@ -1396,6 +1400,8 @@ __device__ __forceinline__ void fill_frames(const FrameParams& p, uint32_t q, ui
             fill_blocks<kDev, true, false>(p, o, cs, occ, g, ng, wave, lane, aligned);
         else if (pace)
             fill_blocks<kDev, false, true>(p, o, cs, occ, g, ng, wave, lane, aligned);
+        else if (p.launch_flags & kLaunchRingBeyondCache)
+            fill_blocks<kDev, false, false, false>(p, o, cs, occ, g, ng, wave, lane, aligned);
         else
             fill_blocks<kDev, false, false>(p, o, cs, occ, g, ng, wave, lane, aligned);
     }
