@@ -83,6 +83,26 @@ def test_static_ring_every_slot_is_the_frame(gpu, cube, per_launch):
         sc.close()
 
 
+def test_ring_beyond_the_infinity_cache(gpu, cube):
+    """A ring whose slots together exceed the 256 MiB Infinity Cache (16 slots of 1920x1080: 630 MB)
+    takes the unpaced per-lane-coordinate fill (render.hip kLaunchRingBeyondCache): every slot is
+    still the frame eray_render writes."""
+    W, H = 1920, 1080
+    sc = MainScene(gpu, *cube, W, H, texture=256, fov=(16.0, 9.0))
+    ring = Ring(gpu, 16, H, W)
+    try:
+        ref = single(gpu, W, H)
+        assert (ref[1] >= 0).any()
+        ring.clear()
+        gpu.render_frames(16, W, H, ring=ring.ring(8), **ring.kw())
+        got = ring.get()
+        for s in range(16):
+            check_slot(got, s, ref, "16-slot ring")
+    finally:
+        ring.free()
+        sc.close()
+
+
 def test_static_ring_large_mesh_and_bands(gpu, standin70k_ring):
     """A binned 70k-face mesh (screen bins, detail list), whole frames and a 3-rank band share."""
     W, H = 480, 270
