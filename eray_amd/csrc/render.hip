@@ -1245,7 +1245,14 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
     // ---- outputs: Image::set + Color::as_bytes, rows bottom-up (image.rs:41-74) ---
     const uint32_t b0 = sat_u8(acc.r * 255.0f), b1 = sat_u8(acc.g * 255.0f), b2 = sat_u8(acc.b * 255.0f);
     if (valid && fo.face) fo.face[(size_t)py * p.img_w + px] = have ? best_face : -1;
-    if (active && aligned && wx0 + kSubW <= p.cam_w && py0 + kBlkH <= p.rows) {
+    // Frames into a ring beyond the Infinity Cache (non-temporal launches aside) leave through the
+    // wave's LDS slice as write-through 16-B row stores (3840x2160 / 70k in 4 slots 25.6 -> 24.8
+    // us); elsewhere each lane stores its own pixel with plain (write-back) stores: C5 123.5 ->
+    // 116, C2 40.6 -> 40.3 us (no LDS round trip and wave barriers in the chain).  Write-through
+    // partial stores lose badly (C5 154 us).  Same-box A/B profiles/r05/ab/ab_r05ao.txt ..
+    // ab_r05aq.txt
+    const bool staged = (p.launch_flags & kLaunchRingBeyondCache) && !fo.nt;
+    if (staged && active && aligned && wx0 + kSubW <= p.cam_w && py0 + kBlkH <= p.rows) {
         // the wave's 16 x 4 pixels leave through its own LDS slice as 16-B row stores
         float* wrgb = reinterpret_cast<float*>(reinterpret_cast<char*>(s_rgb) + kSliceRgbBytes * wave);
         uint8_t* wppm = reinterpret_cast<uint8_t*>(s_ppm) + kSlicePpmBytes * wave;
