@@ -949,7 +949,9 @@ __device__ __forceinline__ void store_slice(const FrameParams& p, const FrameOut
     }
 }
 
-template <bool kCull, bool kLdsTiles, int kMat, typename Scene, typename Mid = NoMid>
+// kStaging: the build keeps the LDS-staged output path (only the dense large-mesh builds, whose
+// 4-slot north-star frames use it; the others store per lane only and carry none of its registers)
+template <bool kCull, bool kLdsTiles, int kMat, bool kStaging = true, typename Scene, typename Mid = NoMid>
 __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut& fo, const CamDev& cam, const RowMap& rm,
                                            const Scene& sc, uint32_t wx0, uint32_t py0,
                                            bool active, TriHot* s_hot, TriCull* s_cull, char* s_bins, float4* s_rgb,
@@ -1245,13 +1247,13 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
     // ---- outputs: Image::set + Color::as_bytes, rows bottom-up (image.rs:41-74) ---
     const uint32_t b0 = sat_u8(acc.r * 255.0f), b1 = sat_u8(acc.g * 255.0f), b2 = sat_u8(acc.b * 255.0f);
     if (valid && fo.face) fo.face[(size_t)py * p.img_w + px] = have ? best_face : -1;
-    // Frames into a ring beyond the Infinity Cache (non-temporal launches aside) leave through the
-    // wave's LDS slice as write-through 16-B row stores (3840x2160 / 70k in 4 slots 25.6 -> 24.8
-    // us); elsewhere each lane stores its own pixel with plain (write-back) stores: C5 123.5 ->
+    // Frames into a ring beyond the Infinity Cache (non-temporal launches aside; dense builds
+    // only: C2 in 16 slots is no faster staged) leave through the wave's LDS slice as
+    // write-through 16-B row stores (3840x2160 / 70k in 4 slots 25.6 -> 24.8 us); elsewhere each lane stores its own pixel with plain (write-back) stores: C5 123.5 ->
     // 116, C2 40.6 -> 40.3 us (no LDS round trip and wave barriers in the chain).  Write-through
     // partial stores lose badly (C5 154 us).  Same-box A/B profiles/r05/ab/ab_r05ao.txt ..
     // ab_r05aq.txt
-    const bool staged = (p.launch_flags & kLaunchRingBeyondCache) && !fo.nt;
+    const bool staged = kStaging && (p.launch_flags & kLaunchRingBeyondCache) && !fo.nt;
     if (staged && active && aligned && wx0 + kSubW <= p.cam_w && py0 + kBlkH <= p.rows) {
         // the wave's 16 x 4 pixels leave through its own LDS slice as 16-B row stores
         float* wrgb = reinterpret_cast<float*>(reinterpret_cast<char*>(s_rgb) + kSliceRgbBytes * wave);
@@ -1625,7 +1627,7 @@ __global__ void __launch_bounds__(kWG, (kMat & kMatSpecPow) ? 1 : (kLdsTiles && 
                     // first, so the longest chains start in the first round (coop: shared by the
                     // workgroup in builds that keep the cooperative paths, render_sub)
                     // (the first sub-block's rays by value: a pointer would keep them in scratch memory)
-                    render_sub<kCull, kLdsTiles, kMat>(p, fo, cam, rm, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH,
+                    render_sub<kCull, kLdsTiles, kMat, kDense>(p, fo, cam, rm, sc, (uint32_t)sx * kSubW, (uint32_t)sy * kBlkH,
                                                        active, s_hot, s_cull, s_bins, s_rgb, s_ppm, aligned,
                                                        kGivenRay && r == 0, d0, coop, pre, pobj, mid);
                 }
