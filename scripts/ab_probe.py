@@ -31,7 +31,7 @@ from eray_amd.objfile import load_obj_file  # noqa: E402
 MESHES = {"cube": None, "70k": (69451, 42), "1m": (1_000_000, 1234)}
 CONFIGS = {"fill4k1": ("none", 3840, 2160, 1, 1), "fill4k4": ("none", 3840, 2160, 4, 1),
            "fill8k": ("none", 7680, 4320, 1, 1), "fillc2": ("none", 1920, 1080, 8, 8),
-           "c2": ("cube", 1920, 1080, 8, 8), "c2b": ("cube", 1920, 1080, 16, 8), "c3": ("70k", 1920, 1080, 4, 4), "ns1": ("70k", 3840, 2160, 1, 1),
+           "c2": ("cube", 1920, 1080, 8, 8), "c2b": ("cube", 1920, 1080, 16, 8), "c3": ("70k", 1920, 1080, 4, 4), "c3dense": ("70k", 1920, 1080, 4, 4), "c3nodense": ("70k", 1920, 1080, 4, 4), "ns1": ("70k", 3840, 2160, 1, 1),
            "ns4": ("70k", 3840, 2160, 4, 1), "c5": ("1m", 7680, 4320, 1, 1), "moving_ns": ("70k", 3840, 2160, 1, 1),
            "moving_c5": ("1m", 7680, 4320, 1, 1),
            "aa2": ("cube", 1920, 1080, 1, 1), "aa_ns": ("70k", 3840, 2160, 1, 1),
@@ -90,6 +90,10 @@ def main() -> None:
                 del kw["ring"]
         if name in SEPARATE:
             kw["flags"] = capi.RENDER_DENSE_DETAIL | capi.RENDER_SEPARATE_FILL
+        elif name.endswith("nodense"):  # launch-shape overrides: the 2-per-CU / dense detail builds
+            kw["flags"] = capi.RENDER_NO_DENSE_DETAIL
+        elif name.endswith("dense"):
+            kw["flags"] = capi.RENDER_DENSE_DETAIL
         if name == "mat":
             from bench import material_roofline
             out[name] = {"frame_ms": min(material_roofline(sc, st, reps=50)["us_per_update"] for _ in range(3)) / 1e3}
