@@ -244,6 +244,17 @@ def kernel_figures(kt: dict) -> dict:
     return out
 
 
+def write_ceiling_fields(ct: dict, launch_bytes: int, floor_ms: float) -> dict:
+    """eray_time_write_ceiling's figures: the same launches' background bytes written by a plain
+    block-strided store stream (one workgroup per CU, no other work) into the same ring slots, in
+    this process — the chip's own write rate for the ring, against which the fill floor is read."""
+    gbs = launch_bytes / (ct["frame_kernel_ms"] * 1e-3) / 1e9
+    return {"kernel_ms_per_launch": round(ct["frame_kernel_ms"], 6), "kernel_ms_min": round(ct["frame_kernel_min_ms"], 6),
+            "achieved_gbs": round(gbs, 1), "frac": round(gbs / PEAK_HBM_GBS, 4),
+            "fill_floor_over_ceiling": round(floor_ms / ct["frame_kernel_ms"], 4),
+            "kernel": "ceiling_fill_kernel (render.hip): 64x4 blocks, 1 workgroup per CU, unpaced write-through stores"}
+
+
 def empty_scene_context(device: int, width: int, height: int, fov, stream) -> "capi.Context":
     """The same camera and lights with no object: every pixel is the miss colour (engine.rs:
     208-213), so its frame kernel is the fill alone — this kernel's write floor for the frame."""
@@ -321,6 +332,8 @@ def north_star_line(device: int, steps: int, slot_counts=None) -> dict:
             kt = ctx.time_frames(max(steps, 64), W, H, **out)
         with MARK.range(f"{tag}_fill_floor_F1"):
             ft = empty.time_frames(max(steps, 64), W, H, **out)
+        with MARK.range(f"{tag}_write_ceiling_F1"):
+            ct = empty.time_write_ceiling(max(steps, 64), W, H, **out)
         k_ms, f_ms = kt["frame_kernel_ms"], ft["frame_kernel_ms"]
         gbs = alg / (k_ms * 1e-3) / 1e9
         fill_gbs = 15 * W * H / (f_ms * 1e-3) / 1e9
@@ -337,7 +350,8 @@ def north_star_line(device: int, steps: int, slot_counts=None) -> dict:
             "fill_floor": {"frame_kernel_ms": round(f_ms, 6),
                            "achieved_gbs": round(fill_gbs, 1),
                            "frac": round(fill_gbs / PEAK_HBM_GBS, 4),
-                           "scene": "no objects: every pixel the miss colour, same kernel and ring"},
+                           "scene": "no objects: every pixel the miss colour, same kernel and ring",
+                           "write_ceiling": write_ceiling_fields(ct, frame_bytes, f_ms)},
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(gbs / PEAK_HBM_GBS, 4),
                          "frac_of_fill_floor": round(f_ms / k_ms, 4),
@@ -692,11 +706,15 @@ def main() -> None:
             empty = empty_scene_context(device, width, H, frame_camera_fov(width, H), stream)
             with MARK.range(f"fill_floor_F{F}"):
                 ft = empty.time_frames(n_kt, width, H, **ring1)
+            with MARK.range(f"write_ceiling_F{F}"):
+                ct = empty.time_write_ceiling(n_kt, width, H, ring=ring1["ring"], out_rgb=ring1["out_rgb"],
+                                              out_ppm=ring1["out_ppm"])
             fill_floor = {"frame_kernel_ms_per_launch": round(ft["frame_kernel_ms"], 6),
                           "frames_per_launch": ft["frames_per_launch"],
                           "achieved_gbs": round(15 * width * rows * ft["frames_per_launch"] / (ft["frame_kernel_ms"] * 1e-3)
                                                 / 1e9, 1),
-                          "scene": "no objects: every pixel the miss colour, same kernel, ring and launch size"}
+                          "scene": "no objects: every pixel the miss colour, same kernel, ring and launch size",
+                          "write_ceiling": write_ceiling_fields(ct, 15 * width * rows * F, ft["frame_kernel_ms"])}
             # the same launches into a ring whose slots exceed the 256 MiB Infinity Cache: every
             # frame's stores reach HBM (the line's own ring of F slots may stay cache-resident)
             if slots * slot_px * 15 <= MALL_BYTES:
@@ -713,13 +731,17 @@ def main() -> None:
                     bt = ctx.time_frames(n_kt, width, H, **bkw)
                 with MARK.range(f"beyond_mall_fill_floor_F{F}"):
                     bft = empty.time_frames(n_kt, width, H, **bkw)
+                with MARK.range(f"beyond_mall_write_ceiling_F{F}"):
+                    bct = empty.time_write_ceiling(n_kt, width, H, ring=bkw["ring"], out_rgb=bkw["out_rgb"],
+                                                   out_ppm=bkw["out_ppm"])
                 del brgb, bppm
                 b_ms = bt["frame_kernel_ms"]
                 b_gbs = algorithmic_bytes(width * rows, hits, hit_faces) * F / (b_ms * 1e-3) / 1e9
                 beyond = {"ring_slots": big, "ring_bytes": big * slot_px * 15, "kernel": kernel_figures(bt),
                           "achieved": round(b_gbs, 1), "frac": round(b_gbs / PEAK_HBM_GBS, 4),
                           "fill_floor_ms_per_launch": round(bft["frame_kernel_ms"], 6),
-                          "frac_of_fill_floor": round(bft["frame_kernel_ms"] / b_ms, 4)}
+                          "frac_of_fill_floor": round(bft["frame_kernel_ms"] / b_ms, 4),
+                          "write_ceiling": write_ceiling_fields(bct, 15 * width * rows * F, bft["frame_kernel_ms"])}
             empty.close()
     rank_kernel_ms = [kernel_ms]
     gather_ms = None

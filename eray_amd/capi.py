@@ -177,6 +177,8 @@ SIGNATURES = {
     "eray_frames_per_launch": (_U, [_P, C.POINTER(RenderParams), _U]),
     "eray_time_frames_ring": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(FrameRing), _U,
                                         C.POINTER(KernelTimes)]),
+    "eray_time_write_ceiling": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(FrameRing), _U, _U,
+                                          C.POINTER(KernelTimes)]),
     "eray_render_camera_path_ring": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(FrameRing),
                                                C.POINTER(Camera), _U, C.POINTER(C.c_float)]),
     "eray_pack_ppm": (C.c_int, [_P, _P, _U, _U, _P]),
@@ -208,6 +210,7 @@ DEBUG_SIGNATURES = {
                                                   _P]),
     "eray_debug_gather_check": (C.c_int, [C.POINTER(C.c_uint32), _U, _U, _U, _U, _U, C.c_uint64, _P]),
     "eray_debug_plan_verdict": (C.c_int, [C.POINTER(C.c_int32), _U, _U]),
+    "eray_debug_gather_replan": (C.c_int, [_U, _U, C.c_uint64, _U, C.c_uint64]),
 }
 
 _lib = None
@@ -353,6 +356,12 @@ def plan_verdict(records, rank: int) -> int:
     flat = [int(x) for r in records for x in r]
     arr = (C.c_int32 * len(flat))(*flat)
     return lib().eray_debug_plan_verdict(arr, len(records), rank)
+
+
+def gather_replan(cached: bool, plan_kind: int, plan_key: int, cur_kind: int, cur_key: int) -> bool:
+    """eray_gather_frames' re-plan decision (eray_debug_gather_replan, host only): from whether the
+    cached plan fits the call's shared arguments, its source and the context's latest render."""
+    return bool(lib().eray_debug_gather_replan(int(bool(cached)), plan_kind, plan_key, cur_kind, cur_key))
 
 
 def comm_destroy(comm: int) -> None:
@@ -569,6 +578,17 @@ class Context:
         t = KernelTimes()
         self._check(lib().eray_time_frames_ring(self._h, C.byref(p), C.byref(ring) if ring is not None else None,
                                                 frames, C.byref(t)))
+        return {name: getattr(t, name) for name, _ in KernelTimes._fields_}
+
+    def time_write_ceiling(self, frames, image_width, image_height, out_rgb=None, out_ppm=None, out_face=None,
+                           ring=None, wgs_per_cu=1) -> dict:
+        """eray_time_write_ceiling: the same launches' background bytes as a plain block-strided
+        store stream (wgs_per_cu workgroups per CU), dispatch-timed; eray_kernel_times fields."""
+        p = RenderParams(image_width, image_height, 0, image_height, 0, 0, out_rgb or None, out_ppm or None,
+                         out_face or None, 0, 0, 0, 0)
+        t = KernelTimes()
+        self._check(lib().eray_time_write_ceiling(self._h, C.byref(p), C.byref(ring) if ring is not None else None,
+                                                  frames, wgs_per_cu, C.byref(t)))
         return {name: getattr(t, name) for name, _ in KernelTimes._fields_}
 
     def frames_per_launch(self, image_width, image_height, rows=None, slots=64, anti_aliasing=0, bounces=0) -> int:

@@ -207,6 +207,10 @@ struct eray_ctx {
     uint64_t mc_gen = 0;          // bumped whenever the multi-camera buffers are (re)allocated
     hipStream_t mc_stream = nullptr;
     hipEvent_t mc_fork = nullptr, mc_ready[2] = {nullptr, nullptr}, mc_free[2] = {nullptr, nullptr};
+    // the latest render of the scene camera or of a camera path (tag_frames): what a scene-camera
+    // gather plans for — state every rank holds alike when the ranks make the same render calls
+    FrameSource gather_src;
+    uint8_t* d_coll = nullptr;     // kCollScratchBytes: the gathers' status exchanges (comm.cpp)
     uint8_t* d_staging = nullptr;  // eray_gather_rows' banded staging (rank 0)
     size_t staging_cap = 0;
     LaunchCtx lc{nullptr, nullptr, nullptr};  // the separate fill's stream and events
@@ -494,6 +498,7 @@ void untag_range(eray_ctx* ctx, uintptr_t a, size_t bytes) {
 // bytes the new frames overwrite is dropped.
 void tag_frames(eray_ctx* ctx, const uint8_t* ppm, uint64_t stride, uint32_t n, const FrameSource& s) {
     if (!ppm) return;
+    if (s.kind == kSrcScene || s.kind == kSrcPath) ctx->gather_src = s;
     auto& v = ctx->slot_tags;
     for (uint32_t k = 0; k < n; ++k) {
         const uintptr_t a = reinterpret_cast<uintptr_t>(ppm) + (uintptr_t)(k * stride);
@@ -525,7 +530,7 @@ int ensure_bins(eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs) {
     size_t binned_tris = 0;
     for (auto& o : ctx->objects)
         if (o.T > kDirectMax) binned_tris += o.T;
-    if (!ctx->bin_cap) ctx->bin_cap = std::max<size_t>(2 * binned_tris, 1u << 16);
+    if (!ctx->bin_cap) ctx->bin_cap = std::min(std::max<size_t>(2 * binned_tris, 1u << 16), kMaxBinEntries);
     const uint32_t phase = row0 % kBinH, tiles_x = (W + 63) / 64;
     std::vector<uint64_t> layout{T, nb, W, H, phase, rows, ctx->bin_cap, ctx->scene_gen};
     if (layout == ctx->bins_layout) return ERAY_OK;
@@ -650,7 +655,7 @@ int ensure_multi(eray_ctx* ctx, uint32_t W, uint32_t H, const RowSpan& rs) {
             HIP_TRY(ctx, hipMemcpyAsync(m.objs + (size_t)k * nobj, ctx->d_objs, sizeof(ObjectDesc) * nobj,
                                         hipMemcpyDeviceToDevice, ctx->stream));
         HIP_TRY(ctx, bins_alloc(m.bins, K * T, K * nb, mbegin.data(), mobj.data(), W, H, rs.row0 % kBinH, (W + 63) / 64,
-                                rs.rows, K * ctx->bin_cap, ctx->stream, K));
+                                rs.rows, std::min((size_t)K * ctx->bin_cap, kMaxBinEntries), ctx->stream, K));
     }
     ctx->mc_layout = std::move(layout);
     ctx->mc_k = K;
@@ -710,8 +715,9 @@ CamDev cam_dev(const eray_camera& c) {
 void state_arrived(eray_ctx* ctx) {
     ctx->state_pending = false;
     ctx->state_known = true;
-    if (ctx->h_state->bin_entries > ctx->bin_cap) {
-        ctx->bin_cap = 2 * (size_t)ctx->h_state->bin_entries;
+    if (ctx->h_state->bin_entries > ctx->bin_cap && ctx->bin_cap < kMaxBinEntries) {
+        // (at most kMaxBinEntries: beyond, the setups keep overflowing into the exact LDS-tile scan)
+        ctx->bin_cap = std::min(2 * (size_t)ctx->h_state->bin_entries, kMaxBinEntries);
         ctx->state_known = false;
         ctx->setup_key.clear();  // rebuilt with the larger capacity
     }
@@ -815,6 +821,7 @@ int eray_ctx_create(int device, eray_ctx** out) {
     if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_cam, sizeof(CamDev));
     if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_state, sizeof(CamState));
     if (e == hipSuccess) e = hipMemset(ctx->d_state, 0, sizeof(CamState));
+    if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_coll, kCollScratchBytes);
 
     if (e == hipSuccess) e = hipHostMalloc((void**)&ctx->h_state, sizeof(CamState), hipHostMallocDefault);
     if (e == hipSuccess) std::memset(ctx->h_state, 0, sizeof(CamState));
@@ -850,7 +857,7 @@ int eray_ctx_destroy(eray_ctx* ctx) {
     void* bufs[] = {ctx->d_hot,   ctx->d_shade, ctx->d_cull,  ctx->d_raw,  ctx->d_objs,  ctx->d_lights,
                     ctx->d_prog,  ctx->d_cam,   ctx->d_state, ctx->d_acc,  ctx->d_begin, ctx->d_range,
                     ctx->d_area,  ctx->d_fkey,  ctx->d_path,  ctx->d_path_all, ctx->d_staging,
-                    ctx->d_bcull, ctx->d_bobjs, ctx->d_bstate, ctx->d_tcull, ctx->d_union_acc};
+                    ctx->d_bcull, ctx->d_bobjs, ctx->d_bstate, ctx->d_tcull, ctx->d_union_acc, ctx->d_coll};
     for (void* b : bufs)
         if (b) hipFree(b);
     if (ctx->h_state) hipHostFree(ctx->h_state);
@@ -1089,7 +1096,9 @@ int eray_scene_add_object(eray_ctx* ctx, const eray_object* obj, uint32_t* index
         return set_error(ctx, ERAY_E_OUT_OF_BOUNDS, "material image with zero width or height (mod_get by 0)");
     uint64_t total = T;
     for (auto& o : ctx->objects) total += o.T;
-    if (total > (1ull << 31)) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "too many triangles");
+    if (total > kMaxSceneTris)
+        return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "too many triangles: %llu in the scene (at most %llu)",
+                         (unsigned long long)total, (unsigned long long)kMaxSceneTris);
     HostObject h;
     h.T = T;
     h.raw.resize((size_t)T * 24);
@@ -1681,6 +1690,55 @@ int eray_time_frames_ring(eray_ctx* ctx, const eray_render_params* rp, const era
     return ERAY_OK;
 }
 
+int eray_time_write_ceiling(eray_ctx* ctx, const eray_render_params* rp, const eray_frame_ring* ring, uint32_t frames,
+                            uint32_t wgs_per_cu, eray_kernel_times* out) {
+    if (!out) return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "write ceiling: out is null");
+    *out = eray_kernel_times{};
+    if (wgs_per_cu < 1 || wgs_per_cu > 8)
+        return set_error(ctx, ERAY_E_INVALID_ARGUMENT, "write ceiling: %u workgroups per CU (1..8)", wgs_per_cu);
+    FrameParams p;
+    bool empty = false;
+    if (int st = prepare_render(ctx, rp, &p, &empty, SetupWait::kYes)) return st;
+    if (empty || !frames) return ERAY_OK;
+    if (!p.aligned || p.img_w % 64u || p.rows % 4u)
+        return set_error(ctx, ERAY_E_UNSUPPORTED, "write ceiling: whole 64x4 blocks only (%ux%u, aligned %u)", p.img_w,
+                         p.rows, p.aligned);
+    Ring r;
+    if (int st = make_ring(ctx, rp, p, ring, &r)) return st;
+    const uint32_t F = r.per_launch, L = std::max(1u, frames / F);
+    std::vector<hipEvent_t> ev(2 * (size_t)L, nullptr);
+    int st = ERAY_OK;
+    hipError_t e = hipSuccess;
+    for (size_t k = 0; k < ev.size() && e == hipSuccess; ++k) e = hipEventCreate(&ev[k]);
+    for (uint32_t l = 0; l < L && e == hipSuccess; ++l) {
+        const hipEvent_t t[2] = {ev[2 * (size_t)l], ev[2 * (size_t)l + 1]};
+        e = launch_write_ceiling(ring_frames(p, r, l * F, F), wgs_per_cu, t, ctx->stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    double sum = 0.0;
+    float lo = 0.0f, hi = 0.0f;
+    for (uint32_t l = 0; l < L && e == hipSuccess; ++l) {
+        float k = 0.0f;
+        if ((e = hipEventElapsedTime(&k, ev[2 * (size_t)l], ev[2 * (size_t)l + 1])) != hipSuccess) break;
+        sum += k;
+        lo = l ? std::min(lo, k) : k;
+        hi = l ? std::max(hi, k) : k;
+    }
+    for (auto x : ev)
+        if (x) hipEventDestroy(x);
+    if (e != hipSuccess) st = set_error(ctx, ERAY_E_HIP, "write ceiling: %s", hipGetErrorString(e));
+    if (st) return st;
+    // the slots now hold background frames, not renders of the scene
+    tag_frames(ctx, p.out_ppm, r.ppm, std::min(L * F, r.slots), FrameSource{kSrcOther});
+    out->launches = L;
+    out->frames_per_launch = F;
+    out->frame_kernel_ms = (float)(sum / L);
+    out->frame_kernel_min_ms = lo;
+    out->frame_kernel_max_ms = hi;
+    out->launch_span_ms = out->frame_kernel_ms;
+    return ERAY_OK;
+}
+
 int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* rp, const eray_frame_ring* ring,
                                  const eray_camera* cameras, uint32_t n, float* mean_frame_ms) {
     if (int st = use_device(ctx)) return st;
@@ -2055,6 +2113,10 @@ int eray_internal_scene_setup_source(eray_ctx* ctx, FrameSource* out) {
     *out = ctx->setup_src;
     return ERAY_OK;
 }
+// The context's latest render of the scene camera or of a camera path (kind kSrcNone: none yet).
+void eray_internal_gather_source(const eray_ctx* ctx, FrameSource* out) { *out = ctx->gather_src; }
+// The context's collective scratch block (kCollScratchBytes of device memory, made with it).
+uint8_t* eray_internal_coll_scratch(eray_ctx* ctx) { return ctx->d_coll; }
 void** eray_internal_gather_plan(eray_ctx* ctx, void (*free_fn)(void*)) {
     ctx->gather_plan_free = free_fn;
     return &ctx->gather_plan;
@@ -2158,7 +2220,7 @@ extern "C" int eray_debug_bin_dump(eray_ctx* ctx, uint32_t index, uint32_t bin, 
 // objects through LDS tiles and the capacity grows once the host sees the count (tests).
 extern "C" int eray_debug_set_bin_capacity(eray_ctx* ctx, uint64_t entries) {
     if (!ctx || !entries) return ERAY_E_INVALID_ARGUMENT;
-    ctx->bin_cap = (size_t)entries;
+    ctx->bin_cap = std::min((size_t)entries, kMaxBinEntries);
     ctx->setup_key.clear();
     return ERAY_OK;
 }

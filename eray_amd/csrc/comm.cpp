@@ -32,6 +32,8 @@ int eray_internal_scene_setup_source(eray_ctx* ctx, eray::gpu::FrameSource* out)
 void** eray_internal_gather_plan(eray_ctx* ctx, void (*free_fn)(void*));
 int eray_internal_use_device(eray_ctx* ctx);
 void eray_internal_untag(eray_ctx* ctx, const void* p, size_t bytes);
+void eray_internal_gather_source(const eray_ctx* ctx, eray::gpu::FrameSource* out);
+uint8_t* eray_internal_coll_scratch(eray_ctx* ctx);
 
 namespace {
 // camera rows of `rank` in the interleaved band split (eray_band_rows)
@@ -73,7 +75,7 @@ __global__ void __launch_bounds__(256) unband_rows_kernel(const uint8_t* __restr
 // ~0.2 MB, and the gather into rank 0 is no longer bound by its xGMI links.
 constexpr uint32_t kSegPx = 64, kSegBytes = 3 * kSegPx;
 constexpr uint32_t kUniform = 0x80000000u;
-constexpr int kMaxCodedRanks = 64;
+constexpr int kMaxCodedRanks = eray::gpu::kMaxGatherRanks;
 constexpr uint32_t kCountFailed = 0xffffffffu;  // a rank's count word when it cannot take part
 struct RankOffsets {
     uint32_t v[kMaxCodedRanks];  // first packed segment of each rank in rank 0's staging
@@ -234,22 +236,22 @@ __global__ void __launch_bounds__(256) seg_decode_kernel(const uint32_t* __restr
     }
 }
 
-// Device buffers of one rank's coded gather, carved from one staging allocation (rank 0: a code
-// block and packed room for every rank).
+// Device buffers of one rank's coded gather: the code words and packed segments carved from one
+// staging allocation (rank 0: a code block and packed room for every rank); the packed count and
+// the all-gathered counts in the context's collective scratch (no allocation can keep a rank out
+// of the count exchange).
 struct CodedBufs {
-    uint32_t *code, *count, *counts;
-    uint8_t* packed;
+    uint32_t *code = nullptr, *count = nullptr, *counts = nullptr;
+    uint8_t* packed = nullptr;
 };
-bool coded_bufs(eray_ctx* ctx, uint32_t G, uint32_t slots, uint32_t nranks, CodedBufs* b) {
+bool coded_bufs(eray_ctx* ctx, uint32_t G, uint32_t slots, CodedBufs* b) {
     auto up = [](size_t x) { return (x + 255) / 256 * 256; };
-    const size_t n_code = up((size_t)slots * G * 4), n_cnt = up(4u * (nranks + 1));
+    const size_t n_code = up((size_t)slots * G * 4);
     const size_t n_packed = (size_t)slots * G * kSegBytes;
-    uint8_t* base = static_cast<uint8_t*>(eray_internal_staging(ctx, n_code + n_cnt + n_packed));
+    uint8_t* base = static_cast<uint8_t*>(eray_internal_staging(ctx, n_code + n_packed));
     if (!base) return false;
     b->code = reinterpret_cast<uint32_t*>(base);
-    b->count = reinterpret_cast<uint32_t*>(base + n_code);
-    b->counts = b->count + 1;
-    b->packed = base + n_code + n_cnt;
+    b->packed = base + n_code;
     return true;
 }
 
@@ -348,30 +350,42 @@ __host__ __device__ inline uint64_t recv_block(const RankLayout& L, uint32_t q, 
 constexpr int kXchgHead = 4;
 constexpr int kXchgInts = kXchgHead + 1 + 4 * kPlanRects;
 
+// The context's collective scratch (eray_internal_coll_scratch, allocated with the context):
+// status and count words at kScrWords, the plan exchange's records at kScrXchg, the plan's rank
+// table (the assembly kernels' RankLayout array) at kScrRanks.
+constexpr size_t kScrWords = 0, kScrXchg = 1024, kScrRanks = kScrXchg + 12288;
+static_assert(4 * (kMaxCodedRanks + 2) <= kScrXchg, "status words");
+static_assert(kScrXchg + sizeof(int32_t) * kXchgInts * (kMaxCodedRanks + 1) <= kScrRanks, "plan records");
+static_assert(kScrRanks + sizeof(RankLayout) * kMaxCodedRanks <= eray::gpu::kCollScratchBytes, "rank table");
+
 struct GatherPlan {
     void* comm = nullptr;
     int32_t* fault = nullptr;      // mapped host word: a root met a failed or foreign header
     int32_t* d_fault = nullptr;    // (its device address)
+    hipEvent_t asm_ev = nullptr;   // after the last assembly enqueued outside a graph capture
+    bool asm_pending = false;      // ... whose fault word has not been read yet
     uint32_t kind = 0;
     uint64_t key = 0;
     uint32_t H = 0, W = 0, band = 0, nranks = 0, rank = 0;
     bool valid = false;
     std::vector<RankLayout> ranks;
     uint64_t total = 0;            // every rank's bytes per frame
-    RankLayout* d_ranks = nullptr; // the assembly's table (every rank: any may be a root)
+    RankLayout* d_ranks = nullptr; // the assembly's table (every rank: any may be a root), in the scratch
     uint8_t* buf = nullptr;        // [receive area: its frames x every rank's packs | send area: its packs]
     size_t buf_cap = 0;
-    int32_t* xchg = nullptr;       // the all-gather of the ranks' rectangles
+    // batch sizes whose transfer buffers every rank has confirmed since the plan was made (a new
+    // size's first call agrees on that before any transfer)
+    std::vector<uint32_t> batches;
 };
 void plan_release(GatherPlan& P) {
-    if (P.d_ranks) (void)hipFree(P.d_ranks);
     if (P.buf) (void)hipFree(P.buf);
-    if (P.xchg) (void)hipFree(P.xchg);
     if (P.fault) (void)hipHostFree(P.fault);
+    if (P.asm_ev) (void)hipEventDestroy(P.asm_ev);
     P.d_ranks = nullptr;
     P.buf = nullptr;
-    P.xchg = nullptr;
     P.fault = P.d_fault = nullptr;
+    P.asm_ev = nullptr;
+    P.asm_pending = false;
 }
 void plan_free(void* v) {
     auto* P = static_cast<GatherPlan*>(v);
@@ -550,6 +564,32 @@ int nccl_error(eray_ctx* ctx, const char* what, ncclResult_t r) {
     std::snprintf(buf, sizeof buf, "%s: %s", what, ncclGetErrorString(r));
     return eray_internal_error(ctx, ERAY_E_HIP, buf);
 }
+
+// Every rank's status word, all-gathered through the collective scratch (one stream
+// synchronisation): this rank's own failure, else the first failing rank's, else ERAY_OK — the
+// same outcome on every rank, so they all go on to the next collective or all return.
+int agree(eray_ctx* ctx, ncclComm_t c, int nranks, int status, const char* what) {
+    hipStream_t s = (hipStream_t)eray_get_stream(ctx);
+    int32_t* words = reinterpret_cast<int32_t*>(eray_internal_coll_scratch(ctx) + kScrWords);
+    const int32_t mine = status;
+    std::vector<int32_t> all((size_t)nranks);
+    hipError_t he;
+    if ((he = hipMemcpyAsync(words, &mine, 4, hipMemcpyHostToDevice, s)) != hipSuccess)
+        return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+    const ncclResult_t r = ncclAllGather(words, words + 1, 1, ncclInt32, c, s);
+    if (r != ncclSuccess) return nccl_error(ctx, what, r);
+    if ((he = hipMemcpyAsync(all.data(), words + 1, 4u * (size_t)nranks, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (he = hipStreamSynchronize(s)) != hipSuccess)
+        return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+    if (status != ERAY_OK) return status;
+    for (int q = 0; q < nranks; ++q)
+        if (all[(size_t)q] != ERAY_OK) {
+            char msg[128];
+            std::snprintf(msg, sizeof msg, "%s: rank %d could not take part (status %d)", what, q, all[(size_t)q]);
+            return eray_internal_error(ctx, all[(size_t)q], msg);
+        }
+    return ERAY_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -599,8 +639,8 @@ int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8
         return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "gather: band_rows must be a power of two >= 4");
     if (!band_rows && height % (uint32_t)nranks)
         return eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "gather: height does not split into equal blocks");
-    if (band_rows && nranks > kMaxCodedRanks)
-        return eray_internal_error(ctx, ERAY_E_UNSUPPORTED, "gather: bands over more than 64 ranks");
+    if (nranks > kMaxCodedRanks)  // (shared arguments: every rank returns here)
+        return eray_internal_error(ctx, ERAY_E_UNSUPPORTED, "gather: more than 64 ranks");
     const size_t row_bytes = (size_t)width * 3u;
     const uint32_t rows = band_rows ? band_rows_of(height, band_rows, (uint32_t)nranks, 0) : height / (uint32_t)nranks;
     const size_t bytes = (size_t)rows * row_bytes;
@@ -616,26 +656,7 @@ int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8
         // every rank's status (one word each, all-gathered, one stream synchronisation), then the
         // rows: rank order = PPM file order, rank r's block lands at frame + r * bytes on rank 0 (in
         // place when rank 0's local rows already sit at frame + 0)
-        int32_t* words = static_cast<int32_t*>(eray_internal_staging(ctx, 4u * ((size_t)nranks + 1)));
-        if (!words) {
-            ncclCommAbort(c);  // (this rank cannot take part: release the others)
-            return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "gather: status words (communicator aborted)");
-        }
-        std::vector<int32_t> all((size_t)nranks);
-        if ((he = hipMemcpyAsync(words, &status, 4, hipMemcpyHostToDevice, s)) != hipSuccess)
-            return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
-        r = ncclAllGather(words, words + 1, 1, ncclInt32, c, s);
-        if (r != ncclSuccess) return nccl_error(ctx, "ncclAllGather (gather status)", r);
-        if ((he = hipMemcpyAsync(all.data(), words + 1, 4u * (size_t)nranks, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-            (he = hipStreamSynchronize(s)) != hipSuccess)
-            return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
-        if (status != ERAY_OK) return status;
-        for (int q = 0; q < nranks; ++q)
-            if (all[(size_t)q] != ERAY_OK) {
-                char msg[96];
-                std::snprintf(msg, sizeof msg, "gather: rank %d could not use its buffers (status %d)", q, all[(size_t)q]);
-                return eray_internal_error(ctx, all[(size_t)q], msg);
-            }
+        if (int st = agree(ctx, c, nranks, status, "gather")) return st;
         r = ncclGather(local, rank == 0 ? frame : nullptr, bytes, ncclUint8, 0, c, s);
         if (r != ncclSuccess) return nccl_error(ctx, "ncclGather", r);
         return ERAY_OK;
@@ -648,20 +669,19 @@ int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8
         const uint32_t S = (width + kSegPx - 1) / kSegPx, G = rows * S;
         const uint32_t mine = band_rows_of(height, band_rows, (uint32_t)nranks, (uint32_t)rank);
         CodedBufs b;
-        if (!coded_bufs(ctx, G, rank == 0 ? (uint32_t)nranks : 1u, (uint32_t)nranks, &b)) {
-            ncclCommAbort(c);  // (this rank cannot take part: release the others)
-            return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "gather: staging buffer (communicator aborted)");
-        }
-        // the packed-segment counts carry the ranks' verdicts: a rank that cannot use its
-        // buffers sends kCountFailed, and every rank returns an error before the transfers
+        b.count = reinterpret_cast<uint32_t*>(eray_internal_coll_scratch(ctx) + kScrWords);
+        b.counts = b.count + 1;
+        if (status == ERAY_OK && !coded_bufs(ctx, G, rank == 0 ? (uint32_t)nranks : 1u, &b))
+            status = eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "gather: staging buffer");
+        // the packed-segment counts carry the ranks' verdicts: a rank that cannot use its buffers
+        // (or allocate its staging) sends kCountFailed, and every rank returns an error before the
+        // transfers
         if (status == ERAY_OK) {
             he = encode_rows(local, mine, rows, width, S, b.code, b.packed, b, s);
             if (he != hipSuccess) status = eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
         }
-        if (status != ERAY_OK && (he = hipMemsetAsync(b.count, 0xff, 4, s)) != hipSuccess) {
-            ncclCommAbort(c);
+        if (status != ERAY_OK && (he = hipMemsetAsync(b.count, 0xff, 4, s)) != hipSuccess)
             return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
-        }
         r = ncclAllGather(b.count, b.counts, 1, ncclUint32, c, s);
         if (r != ncclSuccess) return nccl_error(ctx, "ncclAllGather", r);
         std::vector<uint32_t> counts((size_t)nranks);
@@ -738,14 +758,12 @@ int exchange_plan(eray_ctx* ctx, ncclComm_t c, int nranks, int rank, uint32_t H,
                   const eray::gpu::FrameSource& src, int status, const std::vector<std::array<int32_t, 4>>& rects,
                   GatherPlan* P) {
     P->valid = false;
+    P->batches.clear();
     hipStream_t s = (hipStream_t)eray_get_stream(ctx);
     hipError_t he;
-    if (!P->xchg && (he = hipMalloc((void**)&P->xchg, sizeof(int32_t) * kXchgInts * (size_t)(kMaxCodedRanks + 1))) != hipSuccess) {
-        // without the exchange buffer this rank cannot take part: release the other ranks
-        // (their all-gather fails instead of waiting for this rank forever)
-        ncclCommAbort(c);
-        return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "gather plan: exchange buffer (communicator aborted)");
-    }
+    // (the records travel through the context's collective scratch: nothing to allocate before
+    // the all-gather, so this rank always takes part)
+    int32_t* xchg = reinterpret_cast<int32_t*>(eray_internal_coll_scratch(ctx) + kScrXchg);
     if (status == ERAY_OK && !P->fault) {  // the roots' fault word (a failure here is this rank's verdict)
         if (hipHostMalloc((void**)&P->fault, sizeof(int32_t), hipHostMallocMapped) != hipSuccess ||
             hipHostGetDevicePointer((void**)&P->d_fault, P->fault, 0) != hipSuccess) {
@@ -756,6 +774,10 @@ int exchange_plan(eray_ctx* ctx, ncclComm_t c, int nranks, int rank, uint32_t H,
             *P->fault = 0;
         }
     }
+    if (status == ERAY_OK && !P->asm_ev && hipEventCreateWithFlags(&P->asm_ev, hipEventDisableTiming) != hipSuccess) {
+        P->asm_ev = nullptr;
+        status = eray_internal_error(ctx, ERAY_E_HIP, "gather plan: assembly event");
+    }
     int32_t rec[kXchgInts] = {};
     rec[0] = status;
     rec[1] = (int32_t)src.kind;
@@ -763,11 +785,11 @@ int exchange_plan(eray_ctx* ctx, ncclComm_t c, int nranks, int rank, uint32_t H,
     rec[3] = (int32_t)(uint32_t)(src.key >> 32);
     if (status == ERAY_OK) write_rects(my_rects(rects, rank_rows(H, band, (uint32_t)nranks, (uint32_t)rank), W), rec + kXchgHead);
     std::vector<int32_t> all((size_t)kXchgInts * (size_t)nranks);
-    if ((he = hipMemcpyAsync(P->xchg, rec, sizeof rec, hipMemcpyHostToDevice, s)) != hipSuccess)
+    if ((he = hipMemcpyAsync(xchg, rec, sizeof rec, hipMemcpyHostToDevice, s)) != hipSuccess)
         return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
-    const ncclResult_t r = ncclAllGather(P->xchg, P->xchg + kXchgInts, kXchgInts, ncclInt32, c, s);
+    const ncclResult_t r = ncclAllGather(xchg, xchg + kXchgInts, kXchgInts, ncclInt32, c, s);
     if (r != ncclSuccess) return nccl_error(ctx, "ncclAllGather (gather plan)", r);
-    if ((he = hipMemcpyAsync(all.data(), P->xchg + kXchgInts, sizeof(int32_t) * all.size(), hipMemcpyDeviceToHost, s)) !=
+    if ((he = hipMemcpyAsync(all.data(), xchg + kXchgInts, sizeof(int32_t) * all.size(), hipMemcpyDeviceToHost, s)) !=
             hipSuccess ||
         (he = hipStreamSynchronize(s)) != hipSuccess)
         return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
@@ -781,9 +803,10 @@ int exchange_plan(eray_ctx* ctx, ncclComm_t c, int nranks, int rank, uint32_t H,
         P->total += R.bytes;
         P->ranks[(size_t)q] = R;
     }
-    if (P->d_ranks) (void)hipFree(P->d_ranks);
-    P->d_ranks = nullptr;
-    if ((he = hipMalloc((void**)&P->d_ranks, sizeof(RankLayout) * (size_t)nranks)) != hipSuccess ||
+    // the rank table lives in the scratch: the previous plan's assemblies (on any stream) read it
+    // until they finish, so the device drains first (a re-plan is once per camera)
+    P->d_ranks = reinterpret_cast<RankLayout*>(eray_internal_coll_scratch(ctx) + kScrRanks);
+    if ((he = hipDeviceSynchronize()) != hipSuccess ||
         (he = hipMemcpy(P->d_ranks, P->ranks.data(), sizeof(RankLayout) * (size_t)nranks, hipMemcpyHostToDevice)) !=
             hipSuccess)
         return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
@@ -805,7 +828,7 @@ int grow(eray_ctx* ctx, GatherPlan* P, size_t bytes) {
     if (bytes <= P->buf_cap && P->buf) return ERAY_OK;
     hipStream_t s = (hipStream_t)eray_get_stream(ctx);
     uint8_t* nb = nullptr;
-    hipError_t he = hipStreamSynchronize(s);  // (the old buffer's transfers are done)
+    hipError_t he = hipDeviceSynchronize();  // (the old buffer's transfers are done, on whichever stream)
     if (he == hipSuccess) he = hipMalloc((void**)&nb, std::max<size_t>(bytes, 256));
     if (he != hipSuccess) return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, hipGetErrorString(he));
     if (P->buf) (void)hipFree(P->buf);
@@ -869,7 +892,7 @@ Schedule schedule(const std::vector<RankLayout>& ranks, uint64_t total, uint32_t
 // (this rank's own arguments are unusable): its headers carry the status and it runs only the
 // plan's transfers, so the other ranks' matching sends and receives complete and their roots
 // refuse the batch — no kernel touches the caller's buffers.
-int scene_gather(eray_ctx* ctx, ncclComm_t c, const GatherPlan& P, const Schedule& S, const uint8_t* local,
+int scene_gather(eray_ctx* ctx, ncclComm_t c, GatherPlan& P, const Schedule& S, const uint8_t* local,
                  uint64_t local_stride, uint8_t* frames, uint64_t frame_stride, uint32_t B, int status = ERAY_OK) {
     hipStream_t s = (hipStream_t)eray_get_stream(ctx);
     const RankLayout& me = P.ranks[P.rank];
@@ -901,8 +924,23 @@ int scene_gather(eray_ctx* ctx, ncclComm_t c, const GatherPlan& P, const Schedul
         gather_assemble_kernel<<<dim3(P.H, S.mine), 256, 0, s>>>(P.buf, P.d_ranks, S.mine, frames, frame_stride, P.H, P.W,
                                                                  P.band, P.nranks, P.kind, P.key, P.d_fault);
         if ((he = hipGetLastError()) != hipSuccess) return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+        // the next call reads the fault word once this assembly is done (not under a graph capture,
+        // whose replays' refusals the first call after them reads)
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone &&
+            hipEventRecord(P.asm_ev, s) == hipSuccess)
+            P.asm_pending = true;
     }
     return ERAY_OK;
+}
+
+// The re-plan decision of eray_gather_frames' scene-camera transport.  Its inputs are the state
+// every rank holds alike when the ranks make the same calls (SPMD): the shared arguments, whether
+// the cached plan was made for them (by an exchange whose verdict every rank shares), and the
+// context's latest scene-camera or camera-path render — never this rank's own buffers or their
+// tags, so a rank whose `local` is unusable enters the same collectives as its peers.
+bool gather_replan(bool cached, uint32_t plan_kind, uint64_t plan_key, uint32_t cur_kind, uint64_t cur_key) {
+    return !cached || plan_kind != cur_kind || plan_key != cur_key;
 }
 }  // namespace
 
@@ -934,9 +972,8 @@ int eray_gather_frames(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uin
         if (nranks > kMaxCodedRanks)
             return eray_internal_error(ctx, ERAY_E_UNSUPPORTED, "scene-camera gather: more than 64 ranks");
         // This rank's verdict on its own arguments and frames.  Whatever it is, the rank takes
-        // part in the same collectives as the others (which choose their path from the same
-        // shared arguments and, under the SPMD precondition, the same frame sources), then
-        // returns its error.
+        // part in the same collectives as the others (chosen from the shared arguments and the
+        // shared render history, gather_replan), then returns its error.
         const bool assembles = rotate ? (uint32_t)rank < nframes : rank == 0;
         const bool aligned = ((reinterpret_cast<uintptr_t>(local) | local_stride) & 15) == 0 &&
                              (!assembles || ((reinterpret_cast<uintptr_t>(frames) | frame_stride) & 15) == 0);
@@ -944,17 +981,20 @@ int eray_gather_frames(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uin
         if (!local || (assembles && !frames) || !aligned)
             status = eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT,
                                          "scene-camera gather: null or unaligned (16 B) buffers or strides");
-        // the frames' source, looked up whenever `local` is usable: the re-plan decision below
-        // then follows the frames even on a rank that fails for another reason
+        // what the plan is for: the context's latest render of the scene camera or of a camera path
+        eray::gpu::FrameSource cur;
+        eray_internal_gather_source(ctx, &cur);
+        if (status == ERAY_OK && cur.kind != eray::gpu::kSrcScene && cur.kind != eray::gpu::kSrcPath)
+            status = eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT,
+                                         "scene-camera gather: this context has rendered neither its scene camera nor a "
+                                         "camera path");
+        // this rank's frames must be frames of that render, over this rank's share
         eray::gpu::FrameSource src;
-        bool src_known = false;
-        if (local) {
-            std::string keep = status != ERAY_OK ? eray_last_error(ctx) : std::string();
-            const int st = eray_internal_frame_source(ctx, local, local_stride, nframes, &src);
-            src_known = st == ERAY_OK;
-            if (status == ERAY_OK) status = st;
-            else eray_internal_error(ctx, status, keep.c_str());  // (the first failure's message)
-        }
+        if (status == ERAY_OK) status = eray_internal_frame_source(ctx, local, local_stride, nframes, &src);
+        if (status == ERAY_OK && (src.kind != cur.kind || src.key != cur.key))
+            status = eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT,
+                                         "scene-camera gather: the frames are not of this context's latest scene-camera "
+                                         "or camera-path render");
         const RankRows rr = rank_rows(height, band_rows, (uint32_t)nranks, (uint32_t)rank);
         if (status == ERAY_OK && (src.W != width || src.H != height || src.row0 != rr.row0 || src.rows != rr.rows ||
                                   src.band_shift != rr.shift || (band_rows && src.band_stride != rr.stride)))
@@ -966,27 +1006,42 @@ int eray_gather_frames(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uin
         if (!P) {  // no plan object: this rank still takes part in the (first) exchange, with its error
             GatherPlan tmp;
             eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "gather plan");
-            const int st = exchange_plan(ctx, c, nranks, rank, height, width, band_rows, src, ERAY_E_OUT_OF_MEMORY, {}, &tmp);
+            const int st = exchange_plan(ctx, c, nranks, rank, height, width, band_rows, cur, ERAY_E_OUT_OF_MEMORY, {}, &tmp);
             plan_release(tmp);
             return st ? st : ERAY_E_OUT_OF_MEMORY;
         }
-        // a failed or foreign batch met by one of this context's earlier assemblies (reported
-        // once, after this call's own collectives)
-        const bool faulted = P->fault && __atomic_exchange_n(P->fault, 0, __ATOMIC_RELAXED) != 0;
+        hipStream_t s = (hipStream_t)eray_get_stream(ctx);
+        // a failed or foreign batch met by one of this context's earlier assemblies: read once that
+        // assembly is done (reported after this call's own collectives)
+        bool faulted = false;
+        if (P->fault) {
+            hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+            const bool capturing = hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone;
+            if (P->asm_pending && !capturing) {
+                const hipError_t he = hipEventSynchronize(P->asm_ev);
+                if (he != hipSuccess && status == ERAY_OK)
+                    status = eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
+                P->asm_pending = false;
+            }
+            if (!P->asm_pending) faulted = __atomic_exchange_n(P->fault, 0, __ATOMIC_RELAXED) != 0;
+        }
         const bool cached = P->valid && P->comm == (void*)c && P->H == height && P->W == width &&
                             P->band == band_rows && P->nranks == (uint32_t)nranks && P->rank == (uint32_t)rank;
-        if (!cached || (src_known && (P->kind != src.kind || P->key != src.key))) {  // a new plan: every rank exchanges
+        if (gather_replan(cached, P->kind, P->key, cur.kind, cur.key)) {  // a new plan: every rank exchanges
             eray::gpu::SceneLayout L;
             if (status == ERAY_OK) status = eray_internal_source_layout(ctx, src, &L);
-            if (int st = exchange_plan(ctx, c, nranks, rank, height, width, band_rows, src, status, L.rects, P)) return st;
+            if (int st = exchange_plan(ctx, c, nranks, rank, height, width, band_rows, cur, status, L.rects, P)) return st;
         }
         const Schedule S = schedule(P->ranks, P->total, (uint32_t)rank, nframes, rotate);
-        if (grow(ctx, P, S.need) != ERAY_OK) {
-            // no buffer for this batch's transfers: release the other ranks rather than leave
-            // their sends and receives waiting for this one
-            ncclCommAbort(c);
-            P->valid = false;
-            return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "scene-camera gather: transfer buffer (communicator aborted)");
+        if (std::find(P->batches.begin(), P->batches.end(), nframes) == P->batches.end()) {
+            // a batch size's first call: every rank's transfer buffer for it, agreed on before any
+            // transfer (a rank that cannot allocate makes every rank return instead of leaving its
+            // peers' sends and receives waiting)
+            std::string keep = status != ERAY_OK ? eray_last_error(ctx) : std::string();
+            const int gst = grow(ctx, P, S.need);
+            if (status != ERAY_OK) eray_internal_error(ctx, status, keep.c_str());  // (the first failure's message)
+            if (int st = agree(ctx, c, nranks, gst, "scene-camera gather: transfer buffer")) return status ? status : st;
+            P->batches.push_back(nframes);
         }
         std::string msg = status != ERAY_OK ? eray_last_error(ctx) : std::string();
         const int st = scene_gather(ctx, c, *P, S, local, local_stride, frames, frame_stride, nframes, status);
@@ -1128,6 +1183,12 @@ int eray_debug_gather_check(const uint32_t* rank_bytes, uint32_t nranks, uint32_
 
 // Diagnostics (tests, host only): a new plan's verdict on this rank (exchange_plan's): records
 // holds every rank's (status, kind, key low, key high), `rank`'s own among them.
+// Diagnostics (tests, host only): eray_gather_frames' re-plan decision (gather_replan) — from the
+// cached plan's state and the context's latest render, the only inputs it has.
+int eray_debug_gather_replan(uint32_t cached, uint32_t plan_kind, uint64_t plan_key, uint32_t cur_kind, uint64_t cur_key) {
+    return gather_replan(cached != 0, plan_kind, plan_key, cur_kind, cur_key) ? 1 : 0;
+}
+
 int eray_debug_plan_verdict(const int32_t* records, uint32_t nranks, uint32_t rank) {
     if (!records || !nranks || nranks > (uint32_t)kMaxCodedRanks || rank >= nranks)
         return eray_internal_error(nullptr, ERAY_E_INVALID_ARGUMENT, "plan verdict: bad arguments");
@@ -1230,6 +1291,7 @@ int eray_debug_scene_gather_batch(eray_ctx* ctx, const uint8_t* staging, uint8_t
     if (he == hipSuccess) he = hipStreamSynchronize(s);
     if (P.d_fault) (void)hipFree(P.d_fault);
     P.d_fault = nullptr;  // (not the mapped word plan_release frees)
+    if (P.d_ranks) (void)hipFree(P.d_ranks);  // (this plan's own table, not the context's scratch)
     plan_release(P);
     if (he != hipSuccess) return eray_internal_error(ctx, ERAY_E_HIP, hipGetErrorString(he));
     return fault ? eray_internal_error(ctx, ERAY_E_INVALID_ARGUMENT, "scene gather: a root refused its batch") : ERAY_OK;
@@ -1257,7 +1319,8 @@ int eray_debug_coded_unband(eray_ctx* ctx, const uint8_t* staging, uint8_t* fram
     const uint32_t rows = band_rows_of(height, band_rows, nranks, 0);
     const uint32_t S = (width + kSegPx - 1) / kSegPx, G = rows * S;
     CodedBufs b;
-    if (!coded_bufs(ctx, G, nranks, nranks, &b))
+    b.count = reinterpret_cast<uint32_t*>(eray_internal_coll_scratch(ctx) + kScrWords);
+    if (!coded_bufs(ctx, G, nranks, &b))
         return eray_internal_error(ctx, ERAY_E_OUT_OF_MEMORY, "coded unband: staging buffer");
     RankOffsets off{};
     std::vector<uint32_t> counts(nranks);

@@ -87,6 +87,18 @@ constexpr int kMaxRects = 8;
 constexpr uint32_t kMaxBounces = 16;
 // Frames one launch may render (eray_frame_ring::frames_per_launch <= slots <= 64).
 constexpr uint32_t kMaxFramesPerLaunch = 64;
+// The frame kernel reads triangle records (TriHot 48 B, TriShade 64 B) and bin entries (64 B) by
+// buffer loads with 32-bit byte offsets (render.hip load_rec): a scene holds fewer than 2^26
+// triangles (eray_scene_add_object refuses more) and a bin buffer at most 2^26 entries (a setup
+// that needs more overflows: its objects are scanned through LDS tiles, still exact).
+constexpr uint64_t kMaxSceneTris = (1ull << 26) - 1;
+constexpr size_t kMaxBinEntries = (size_t)1 << 26;
+// The multi-GPU gathers (comm.cpp) serve at most this many ranks, and every buffer a rank needs
+// to take part in their status exchanges (status and count words, the plan records, the plan's
+// rank table) lives in a scratch block allocated with the context — so no rank can fail to enter
+// a collective its peers have entered for want of memory.
+constexpr int kMaxGatherRanks = 64;
+constexpr size_t kCollScratchBytes = 32u << 10;
 // The MI355X Infinity Cache (the die's last-level cache, MI355X_MICROARCH.md).
 constexpr uint64_t kInfinityCacheBytes = 256ull << 20;
 
@@ -398,6 +410,9 @@ struct LaunchCtx {
 // The frame kernel, or the general tracer (trace.hip) when p.aa or p.bounces is set.
 hipError_t launch_render(const FrameParams& p, const LaunchCtx& lc, hipStream_t s);
 hipError_t launch_trace(const FrameParams& p, const LaunchCtx& lc, hipStream_t s);
+// Measurement (eray_time_write_ceiling): the frames' background bytes as one plain block-strided
+// write stream of wgs_per_cu workgroups per CU (render.hip ceiling_fill_kernel), timed by t.
+hipError_t launch_write_ceiling(const FrameParams& p, uint32_t wgs_per_cu, const hipEvent_t (&t)[2], hipStream_t s);
 hipError_t launch_trace_cull(const FrameParams& p, hipStream_t s);
 
 // ------------------------------------------------------------- screen bins (bins.hip)

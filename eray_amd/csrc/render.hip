@@ -1136,6 +1136,7 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
         uint32_t lit = 0;  // bit li - li0: point light li reaches the lane's hit
         for (uint32_t li = li0; li < li1; ++li) {
             const LightDesc L = sc.light(li);
+            ERAY_TRACE_WAVE0(18);
             if (L.variant == 1 || (!(kLdsTiles && coop) && !__any(have))) continue;  // (LDS tiles: barriers)
             const f3 Lp = mk3(L.pos[0], L.pos[1], L.pos[2]);
             // reaches_light(Ray::new(P + N * 0.1, Lp - P)) (engine.rs:136-142, 218-228)
@@ -1155,12 +1156,16 @@ __device__ __forceinline__ void render_sub(const FrameParams& p, const FrameOut&
             };
             for (uint32_t oj = 0; oj < p.nobj; ++oj) {
                 const ObjGeom ob = sc.geom(oj);
+                ERAY_TRACE_WAVE0(19);
                 // A point box (the loaded meshes'): when it certainly rejects every lane's shadow
                 // ray (point_box_rejects), bbox_hit is false for all of them — no ray, no face
                 // load (not where the LDS tiles' barriers need every wave)
                 if (!(kLdsTiles && coop && ob.tri_count > kDirectMax) && point_box_xy(ob) &&
-                    !__any(have && !decided && !point_box_rejects(ob, add(P, mul(N, 0.1f)), sub(Lp, P))))
+                    !__any(have && !decided && !point_box_rejects(ob, add(P, mul(N, 0.1f)), sub(Lp, P)))) {
+                    ERAY_TRACE_VALUE(20, 1u + oj);  // (diagnostics: the skip fired for object oj)
                     continue;
+                }
+                ERAY_TRACE_VALUE(21, 1u + oj);  // (... the shadow scan of object oj ran)
                 int f = -1;
                 float u, v, t;
                 if (!kLdsTiles || ob.tri_count <= kDirectMax) {
@@ -1707,6 +1712,43 @@ __global__ void __launch_bounds__(kWG) fill_kernel(FrameParams p) {
     fill_frames<kDev>(p, blockIdx.x, gridDim.x, threadIdx.x >> 6, threadIdx.x & 63, p.aligned != 0, true);
 }
 
+// Measurement only (eray_time_write_ceiling): the launch's frames' background bytes written by the
+// plainest store stream there is — scripts/microbench/fill_pace.hip's `blk` pattern: one
+// workgroup per CU, wave w of the grid's W takes 64 x 4 blocks w, w + W, ... over all the
+// launch's frames, each block's 16-B write-through stores at per-lane offsets computed per block,
+// no pacing, no role logic, no scene.  The same bytes as the frame kernel's background, into the
+// same ring slots, so the frame kernel's fill floor can be compared with the chip's own write
+// rate for that ring in the same process.  Whole blocks only (aligned frames, rows % 4 == 0).
+__global__ void __launch_bounds__(kWG) ceiling_fill_kernel(FrameParams p) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t tiles_x = p.img_w / kBlkW, bands = p.rows / kBlkH, nblk = tiles_x * bands;
+    const uint32_t nw = gridDim.x * (kWG / 64), w = blockIdx.x * (kWG / 64) + wave;
+    for (uint32_t b = w; b < nblk * p.nframes; b += nw) {
+        const uint32_t fr = b / nblk, k = b - fr * nblk, bx = k % tiles_x, by = k / tiles_x;
+        const FrameOut o = frame_out(p, fr);
+        if (o.rgb) {
+#pragma unroll
+            for (uint32_t i = lane; i < kBlkH * 48u; i += 64) {
+                const uint32_t r = i / 48u, c = i % 48u;
+                const float4 v = bg_rgb4(c % 3u);
+                stream16_pol<false>(o.rgb, 12u * ((by * kBlkH + r) * p.img_w + bx * kBlkW) + 16u * c, 0u,
+                                    make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
+                                               __float_as_uint(v.w)));
+            }
+        }
+        if (o.ppm && lane < 48u) {
+            const uint32_t r = lane / 12u, c = lane % 12u;
+            stream16_pol<false>(o.ppm, 3u * ((p.rows - kBlkH - by * kBlkH + r) * p.img_w + bx * kBlkW) + 16u * c, 0u,
+                                bg_ppm16(c % 3u));
+        }
+        if (o.face) {
+            const uint32_t r = lane / 16u, c = lane % 16u;
+            stream16_pol<false>(o.face, 4u * ((by * kBlkH + r) * p.img_w + bx * kBlkW) + 16u * c, 0u,
+                                make_uint4(~0u, ~0u, ~0u, ~0u));
+        }
+    }
+}
+
 // Image<Color>::save_as_ppm body: byte row k = image row h-1-k.
 __global__ void __launch_bounds__(256) pack_ppm_kernel(const float* __restrict__ rgb, uint32_t w,
                                                        uint32_t h, uint8_t* __restrict__ out) {
@@ -1940,6 +1982,12 @@ hipError_t launch_render(const FrameParams& p_in, const LaunchCtx& lc, hipStream
         case kMatExample: return launch_frame_cs<false, kMatExample, false>(p, want, lc, s);
         default: return launch_frame_cs<false, kMatSpecPow | kMatExample, false>(p, want, lc, s);
     }
+}
+
+hipError_t launch_write_ceiling(const FrameParams& p, uint32_t wgs_per_cu, const hipEvent_t (&t)[2], hipStream_t s) {
+    if (!p.aligned || p.img_w % kBlkW || p.rows % kBlkH || p.nframes < 1 || !wgs_per_cu || wgs_per_cu > 8)
+        return hipErrorInvalidValue;
+    return launch_k(ceiling_fill_kernel, wgs_per_cu * device_cus(), 0, s, t, p);
 }
 
 hipError_t launch_pack_ppm(const float* rgb, uint32_t w, uint32_t h, uint8_t* out, hipStream_t s) {

@@ -154,7 +154,9 @@ __global__ void __launch_bounds__(kBlock) mix_kernel(uint32_t w, uint32_t h, Tex
 // diffuse = wave.  Every node's image has the graph's width x height, so mix's mod_get is the
 // identity and the chain reduces to per-texel arithmetic in the nodes' own operation order
 // (r * factor is the same product per texel, so it is formed once).
-template <bool kWide>
+// kTexels > 1: each thread evaluates texels i, i + stride, ... (stride = the grid's threads)
+// together, so their independent cosf chains interleave (ILP) over a grid that many times smaller.
+template <bool kWide, int kTexels = 1>
 __global__ void __launch_bounds__(kBlock) material_example_kernel(
     TexelIndex t, uint32_t h, float xf, float yf, float r, float g, float b, float factor,
     float* __restrict__ color, float* __restrict__ diffuse) {
@@ -174,19 +176,31 @@ __global__ void __launch_bounds__(kBlock) material_example_kernel(
         }
     } else {
         const uint32_t n = t.w * h, stride = gridDim.x * kBlock;
-        for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-            uint32_t x, y;
-            texel_xy(i, t, x, y);
-            const float v = wave_value(x, y, xf, yf), m = v * omf;
-            if (color) {
-                store_f32(color, 12u * i, m + rf);
-                store_f32(color, 12u * i + 4u, m + gf);
-                store_f32(color, 12u * i + 8u, m + bf);
+        for (uint32_t i0 = blockIdx.x * kBlock + threadIdx.x; i0 < n; i0 += kTexels * stride) {
+            float v[kTexels];
+#pragma unroll
+            for (int k = 0; k < kTexels; ++k) {
+                uint32_t x, y;
+                texel_xy(min(i0 + (uint32_t)k * stride, n - 1u), t, x, y);
+                v[k] = wave_value(x, y, xf, yf);
             }
-            if (diffuse) store_f32(diffuse, 4u * i, v);
+#pragma unroll
+            for (int k = 0; k < kTexels; ++k) {
+                const uint32_t i = i0 + (uint32_t)k * stride;
+                if (i >= n) break;
+                const float m = v[k] * omf;
+                if (color) {
+                    store_f32(color, 12u * i, m + rf);
+                    store_f32(color, 12u * i + 4u, m + gf);
+                    store_f32(color, 12u * i + 8u, m + bf);
+                }
+                if (diffuse) store_f32(diffuse, 4u * i, v[k]);
+            }
         }
     }
 }
+// texels per thread of the fused material kernel (narrow launches)
+constexpr int kMatTexels = 1;
 
 }  // namespace
 
@@ -231,7 +245,8 @@ hipError_t launch_material_example(uint32_t w, uint32_t h, float xf, float yf, f
     if (!n) return hipSuccess;
     const TexelIndex t{w, make_div_u32(w)};
     if (narrow_texels(n))
-        material_example_kernel<false><<<grid_for1(n), kBlock, 0, s>>>(t, h, xf, yf, r, g, b, factor, color, diffuse);
+        material_example_kernel<false, kMatTexels><<<grid_for1((n + kMatTexels - 1) / kMatTexels), kBlock, 0, s>>>(
+            t, h, xf, yf, r, g, b, factor, color, diffuse);
     else
         material_example_kernel<true><<<grid_for1(n), kBlock, 0, s>>>(t, h, xf, yf, r, g, b, factor, color, diffuse);
     return hipGetLastError();

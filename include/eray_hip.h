@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define ERAY_ABI_VERSION 5
+#define ERAY_ABI_VERSION 6
 
 typedef enum eray_status {
     ERAY_OK = 0,
@@ -212,7 +212,9 @@ typedef struct eray_texel_graph {
 int eray_scene_reset(eray_ctx* ctx);
 int eray_scene_set_camera(eray_ctx* ctx, const eray_camera* camera);
 int eray_scene_add_light(eray_ctx* ctx, const eray_light* light);
-/* Copies the host arrays; *object_index (optional) receives the object's position. */
+/* Copies the host arrays; *object_index (optional) receives the object's position.  A scene
+ * holds at most 2^26 - 1 triangles over all its objects (the kernels address triangle records
+ * with 32-bit byte offsets): ERAY_E_INVALID_ARGUMENT beyond, with nothing added. */
 int eray_scene_add_object(eray_ctx* ctx, const eray_object* object, uint32_t* object_index);
 /* The object's color and diffuse outputs become main.rs's graph evaluated per hit (see
  * eray_material_example_params); its other outputs stay as given. */
@@ -334,6 +336,16 @@ typedef struct eray_kernel_times {
 } eray_kernel_times;
 int eray_time_frames_ring(eray_ctx* ctx, const eray_render_params* params, const eray_frame_ring* ring,
                           uint32_t frames, eray_kernel_times* out);
+/* Measurement: the write ceiling of the same launches — every frame's background bytes (the
+ * frame kernel's fill with nothing to render) written into the same ring slots, frames per
+ * launch and launch count as eray_time_frames_ring, by a plain block-strided store stream with
+ * `wgs_per_cu` (1..8) workgroups per CU and no other work, dispatch-timed the same way
+ * (frame_kernel_* fields).  The chip's own write rate for this ring in this process: the
+ * reference point of the frame kernel's fill floor.  The slots hold background frames afterwards
+ * (tagged as such: eray_gather_frames refuses them).  Whole 64 x 4 blocks only (image_width %
+ * 64 == 0, rows % 4 == 0, aligned outputs), else ERAY_E_UNSUPPORTED. */
+int eray_time_write_ceiling(eray_ctx* ctx, const eray_render_params* params, const eray_frame_ring* ring,
+                            uint32_t frames, uint32_t wgs_per_cu, eray_kernel_times* out);
 /* Camera paths of scenes whose per-camera setups are batched (no mesh over 256 faces) render
  * frames_per_launch frames per launch; others one (each camera rebuilds the screen bins). */
 int eray_render_camera_path_ring(eray_ctx* ctx, const eray_render_params* params, const eray_frame_ring* ring,
@@ -363,10 +375,11 @@ int eray_comm_destroy(void* nccl_comm);
  * (a frame is mostly the miss colour, engine.rs:212), so the transfer into rank 0 shrinks with
  * the background; the packed sizes are exchanged first and the call synchronises the context's
  * stream once (not capturable in a graph).  Without bands the ranks exchange a status word
- * first (one small all-gather, one stream synchronisation).  Either way every rank learns every
- * rank's verdict on its own buffers before any rows move: a rank with a null `local` (or rank 0
- * with a null `frame`) still takes part, and every rank returns an error.  (A rank that cannot
- * allocate its staging buffer aborts the communicator, so the others fail instead of waiting.)
+ * first (one small all-gather, one stream synchronisation, every call).  Either way every rank
+ * learns every rank's verdict on its own buffers before any rows move: a rank with a null `local`
+ * (or rank 0 with a null `frame`, or no memory for its staging buffer) still takes part, and every
+ * rank returns an error.  The words of those exchanges live in a block allocated with the context,
+ * so no rank can fail to enter them.  At most 64 ranks (ERAY_E_UNSUPPORTED on every rank beyond).
  * Replaces the reference's single-process image write (engine.rs:85-98 render_to_path ->
  * save_as_ppm). */
 int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8_t* frame, uint32_t height,
@@ -385,14 +398,20 @@ int eray_gather_rows(eray_ctx* ctx, void* nccl_comm, const uint8_t* local, uint8
  *     synchronises the context's stream; a batch size's first call allocates); every later call
  *     only enqueues kernels and transfers — no host round trip, capturable in a HIP graph.
  *     Needs width % 16 == 0 (else ERAY_E_INVALID_ARGUMENT on every rank) and 16-byte aligned
- *     buffers and strides.  Collective safety: the ranks choose their path from shared arguments
- *     and their frames' source (the same on every rank: SPMD); a rank whose own buffers or frames
- *     are unusable still takes part — in a new plan's exchange, whose verdict every rank then
- *     returns, or in a cached plan's transfers, whose headers carry its error — and returns its
- *     error; a root assembles a batch only when every transfer's header says ERAY_OK and the
- *     plan's source, otherwise it writes none of the batch's frames and its context's next
- *     eray_gather_frames returns ERAY_E_INVALID_ARGUMENT.  A rank that cannot allocate its
- *     transfer buffer aborts the communicator (the others fail instead of waiting).
+ *     buffers and strides.  The frames must be of this context's latest render of its scene
+ *     camera or of a camera path (anti-aliased, reflecting and brute-force renders do not count):
+ *     the plan is made for that render, so older frames are refused.  Collective safety: every
+ *     rank chooses what it does from the shared arguments and that render history (the same on
+ *     every rank when the ranks make the same calls: SPMD), never from its own buffers; a rank
+ *     whose own buffers or frames are unusable still takes part — in a new plan's exchange, whose
+ *     verdict every rank then returns, or in a cached plan's transfers, whose headers carry its
+ *     error — and returns its error.  A batch size's first call agrees on every rank's transfer
+ *     buffer before any transfer (one stream synchronisation; a rank without the memory makes
+ *     every rank return an error).  A root assembles a batch only when every transfer's header
+ *     says ERAY_OK and the plan's source, otherwise it writes none of the batch's frames and its
+ *     context's next eray_gather_frames (which first waits for that assembly) returns
+ *     ERAY_E_INVALID_ARGUMENT; batches replayed from a captured graph are reported by the first
+ *     call after them.  At most 64 ranks.
  *   ERAY_GATHER_ROTATE_ROOT   — with ERAY_GATHER_SCENE_CAMERA: frame k of the batch is assembled
  *     on rank k % nranks instead of rank 0, so the assembly writes and the inbound xGMI traffic of
  *     a stream of frames spread over every GPU.  Rank r's frames k = r, r + nranks, ... land at

@@ -65,6 +65,11 @@ int eray_debug_gather_check(const uint32_t* rank_bytes, uint32_t nranks, uint32_
 /* Host only: a new gather plan's verdict on rank `rank` from every rank's exchange record
  * (status, kind, key low, key high; 4 words each) — all ranks accept or all fail together. */
 int eray_debug_plan_verdict(const int32_t* records, uint32_t nranks, uint32_t rank);
+/* Host only: eray_gather_frames' re-plan decision from its only inputs — whether the cached plan
+ * fits the call's shared arguments, the plan's source (kind, key) and the context's latest
+ * scene-camera / camera-path render's — 1: a new plan is exchanged, 0: the cached one is used. */
+int eray_debug_gather_replan(uint32_t cached, uint32_t plan_kind, uint64_t plan_key, uint32_t cur_kind,
+                             uint64_t cur_key);
 /* Host only (no context, no GPU): rank `rank`'s share of the scene-camera gather of `nranks` ranks
  * for objects whose pixel rectangles are `rects` (n x (x0, x1, y0, y1), camera rows) — its rows, its
  * rectangles in local rows / 16-pixel column groups, each one's offset in its per-frame pack.  out:

@@ -8,7 +8,8 @@ Configs: c2 (cube 1920x1080, 8 frames per launch into 8 slots), c3 (70k stand-in
 per launch), ns1 / ns4 (70k stand-in 3840x2160, one frame per launch, 1 / 4 ring slots), c5
 (1M faces 7680x4320), moving_ns (a moving camera over the 70k stand-in at 3840x2160), aa2 / aa_ns
 (anti-aliasing = 4 through the general tracer: C2, the 70k stand-in at 3840x2160; graph-replayed
-frames, device ms per frame), fill* (the same camera and lights, no object), mat (main.rs's
+frames, device ms per frame), fill* (the same camera and lights, no object), ceil* (the
+write ceiling of the fill* rings: eray_time_write_ceiling), mat (main.rs's
 Material::update of a 1024 x 1024 texture, bench.py material_roofline)."""
 from __future__ import annotations
 
@@ -31,6 +32,9 @@ from eray_amd.objfile import load_obj_file  # noqa: E402
 MESHES = {"cube": None, "70k": (69451, 42), "1m": (1_000_000, 1234)}
 CONFIGS = {"fill4k1": ("none", 3840, 2160, 1, 1), "fill4k4": ("none", 3840, 2160, 4, 1),
            "fill8k": ("none", 7680, 4320, 1, 1), "fillc2": ("none", 1920, 1080, 8, 8),
+           # the plain block-strided store stream into the same rings (eray_time_write_ceiling)
+           "ceil4k1": ("none", 3840, 2160, 1, 1), "ceil4k4": ("none", 3840, 2160, 4, 1),
+           "ceilc2": ("none", 1920, 1080, 8, 8), "ceilc2b": ("none", 1920, 1080, 16, 8),
            "c2": ("cube", 1920, 1080, 8, 8), "c2b": ("cube", 1920, 1080, 16, 8), "c3": ("70k", 1920, 1080, 4, 4), "c3dense": ("70k", 1920, 1080, 4, 4), "c3nodense": ("70k", 1920, 1080, 4, 4), "ns1": ("70k", 3840, 2160, 1, 1),
            "ns4": ("70k", 3840, 2160, 4, 1), "c5": ("1m", 7680, 4320, 1, 1), "moving_ns": ("70k", 3840, 2160, 1, 1),
            "moving_c5": ("1m", 7680, 4320, 1, 1),
@@ -94,7 +98,10 @@ def main() -> None:
             kw["flags"] = capi.RENDER_NO_DENSE_DETAIL
         elif name.endswith("dense"):
             kw["flags"] = capi.RENDER_DENSE_DETAIL
-        if name == "mat":
+        if name.startswith("ceil"):
+            ctx.time_write_ceiling(2 * F, W, H, **kw)
+            out[name] = ctx.time_write_ceiling(max(args.launches, 2) * F, W, H, **kw)
+        elif name == "mat":
             from bench import material_roofline
             out[name] = {"frame_ms": min(material_roofline(sc, st, reps=50)["us_per_update"] for _ in range(3)) / 1e3}
         elif name.startswith("aa"):  # the general tracer, anti_aliasing = 4 (bench.py anti_aliasing_line)

@@ -24,7 +24,9 @@ __shared__ unsigned int eray_trace_seen[32];
 // (7); the per-wave bin search: rays + bbox with the first chunk load in flight (8), first chunk
 // entries in registers (9), chunks done (10); hit records + texel addresses (13), shadow rays
 // (14); value 15: the bin's chunks; the first role's list entry + camera rays (11), its binned
-// object found (12); the first object's ObjGeom (16), the hit object's MaterialDesc (17)
+// object found (12); the first object's ObjGeom (16), the hit object's MaterialDesc (17); in the
+// shadow loop: a light's descriptor read (18), an object's ObjGeom read (19); values: 1 + the object
+// whose shadow scan the point-box test skipped (20) or ran (21)
 #define ERAY_TRACE_RECORD(k, v)                                                               \
     do {                                                                                      \
         if (threadIdx.x == 0 && blockIdx.x < 8192) {                                          \

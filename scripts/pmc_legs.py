@@ -1,7 +1,7 @@
 """Frame-kernel counter summaries per workload (round 4), from rocprofv3 --pmc passes of bench.py.
 
     python scripts/pmc_legs.py <pass dir under gpurun_out> <output json> [--north-star SLOTS]
-                                                                        [--workload JSON]
+                                                                        [--workload JSON] [--round rNN]
 
 Each pass directory holds one rocprofv3 counter run per counter group (scripts/gpu_pmc.sh:
 `sq`, `fetch`, `write`, each its own run, kernel trace only).  Per counter the median over the
@@ -18,6 +18,7 @@ import csv
 import glob
 import json
 import os
+import re
 import statistics
 import sys
 from collections import defaultdict
@@ -62,7 +63,10 @@ def main() -> None:
                 workload = {"mesh": cfg["mesh"], "frame": cfg["frame"], "rows_per_gpu": cfg["rows_per_gpu"],
                             "n_gpus": d["n_gpus"], "brute_force": not cfg["culling"],
                             "frames_per_launch": cfg.get("frames_per_launch", 1)}
-    out = {"round": "r04", "workload": workload, "frame_kernel": {
+    # the round the summary belongs to: --round, else the profiles/rNN/ directory it is written into
+    m = re.search(r"(?:^|/)(r\d\d)(?:/|$)", os.path.abspath(dst))
+    rnd = sys.argv[sys.argv.index("--round") + 1] if "--round" in sys.argv else (m.group(1) if m else None)
+    out = {"round": rnd, "workload": workload, "frame_kernel": {
         "kernel": name,
         "dispatches": dispatches,
         "counters_mean_per_dispatch": c,

@@ -56,6 +56,7 @@ for rep in range(3):
               f"p90 {np.percentile(d, 90):.2f} max {d.max():.2f}")
         names = [(4, 16, "ObjGeom"), (16, 8, "rays+bbox"), (8, 9, "first chunk"), (9, 10, "chunks"),
                  (10, 5, "to object-loop end"), (5, 17, "MaterialDesc"), (17, 13, "hit records"), (13, 14, "shadow"),
+                 (13, 18, "shadow: light read"), (18, 19, "shadow: ObjGeom read"), (19, 14, "shadow: skip or scan"),
                  (14, 6, "shading"), (6, 7, "outputs")]
         S = t[det]
         m = (S[:, 32 + 11] > 0) & (S[:, 32 + 12] > 0) & (S[:, 32 + 4] > 0)
@@ -81,6 +82,9 @@ for rep in range(3):
                   f"p90 {np.percentile(total, 90):.2f}; chunks p50 {np.median(ch):.0f} p90 {np.percentile(ch, 90):.0f} "
                   f"max {ch.max()}")
             print(f"    phases p50 (us): " + ", ".join(parts))
+        S = t[det]
+        print(f"  shadow point-box test (wave 0, any sub-block): skipped in {(S[:, 32 + 20] > 0).sum()} of {len(S)} "
+              f"detail workgroups, scan ran in {(S[:, 32 + 21] > 0).sum()}")
         hist, edges = np.histogram(us(t[det, 1]), bins=12)
         print("  detail end histogram:", " ".join(f"{e:.1f}:{h}" for e, h in zip(edges, hist)))
     if fil.any():

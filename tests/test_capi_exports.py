@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared_functions() if not hasattr(lib, n)]
     assert not missing, missing
     assert set(declared_functions()) == set(capi.SIGNATURES), "ctypes signatures out of sync"
-    assert lib.eray_abi_version() == 5
+    assert lib.eray_abi_version() == 6
 
 
 def test_debug_exports_are_declared_apart():

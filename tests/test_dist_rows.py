@@ -306,6 +306,58 @@ def test_two_rank_plan_exchange_fails_together(tmp_path, fail_rank, key_rank, wa
     assert [int(np.load(str(tmp_path / f"verdict{q}.npy"))[0]) for q in range(world)] == [expect] * world
 
 
+def _replan_worker(rank, world, port, out_dir, null_rank):
+    """Both ranks hold a cached plan for the old camera (kind 1, KEY), then render a new camera
+    (the context's latest render: KEY + 7 on both, SPMD); rank `null_rank` passes local = NULL, so
+    it cannot look its frames' source up.  Each rank decides with the library's own rule
+    (eray_gather_frames' gather_replan) whether to exchange a new plan; the ranks that do exchange
+    their records over gloo and take the library's verdict (exchange_plan's); a rank that would not
+    exchange runs the cached plan's transfers instead (recorded as 'transfers')."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from eray_amd import capi
+    new_key = KEY + 7
+    status = capi.E_INVALID_ARGUMENT if rank == null_rank else 0  # (null local: its own verdict)
+    replan = capi.gather_replan(True, 1, KEY, 1, new_key)  # no input of this rank's buffers
+    steps = [("exchange" if replan else "transfers")]
+    steps_all = [None] * world
+    dist.all_gather_object(steps_all, steps)  # (what each rank enters next; a mismatch would hang RCCL)
+    verdict = None
+    if replan and all(s == steps for s in steps_all):
+        rec = (status, 1, new_key & 0x7FFFFFFF, (new_key >> 32) & 0x7FFFFFFF)
+        recs = [None] * world
+        dist.all_gather_object(recs, rec)
+        verdict = capi.plan_verdict(recs, rank)
+    np.save(os.path.join(out_dir, f"replan{rank}.npy"),
+            np.array([int(replan), -1 if verdict is None else verdict, int(all(s == steps for s in steps_all))]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("null_rank", [1, 0])
+def test_two_rank_new_camera_with_a_null_local_replans_together(tmp_path, null_rank):
+    """VERDICT r05 W5 / ADVICE r05: the re-plan decision reads only state every rank shares (the
+    cached plan, the context's latest render), so after both ranks set a new camera a rank passing
+    local = NULL enters the same plan exchange as its peer — not the old plan's transfers — and
+    both return the same error; neither blocks."""
+    world = 2
+    mp.start_processes(_replan_worker, args=(world, _free_port(), str(tmp_path), null_rank),
+                       nprocs=world, join=True, start_method="spawn")
+    from eray_amd import capi
+    got = [np.load(str(tmp_path / f"replan{q}.npy")).tolist() for q in range(world)]
+    assert got == [[1, capi.E_INVALID_ARGUMENT, 1]] * world, got
+
+
+def test_gather_replan_rule():
+    """The rule itself: a new plan when none is cached for the call's shared arguments or the
+    context's latest render (kind, key) is not the plan's; the cached plan otherwise."""
+    from eray_amd import capi
+    assert capi.gather_replan(False, 1, KEY, 1, KEY)
+    assert not capi.gather_replan(True, 1, KEY, 1, KEY)
+    assert capi.gather_replan(True, 1, KEY, 1, KEY + 1)
+    assert capi.gather_replan(True, 1, KEY, 2, KEY)  # a camera path after the scene camera
+
+
 def test_gather_schedules_pair_up():
     """Host-only check of every rank's schedule for N = 1..8 ranks and batches of 1..12 frames:
     each send meets one receive of the same size from its peer, the packs of a rank's frames do

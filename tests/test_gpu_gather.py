@@ -294,8 +294,8 @@ def test_one_rank_gather_camera_path_frames(cube, standin70k_gather, mesh):
 def test_scene_camera_gather_refuses_other_frames(cube):
     """The scene-camera transport only takes frames whose pixel rectangles it knows: frames this
     context did not render, anti-aliased frames (no rectangles), a batch mixing renders, and
-    frames of a scene camera whose setup and plan have since been replaced all fail with
-    ERAY_E_INVALID_ARGUMENT (never a silently wrong frame); frames of the current setup still
+    frames older than the context's latest scene-camera render, and a null `local` all fail with
+    ERAY_E_INVALID_ARGUMENT (never a silently wrong frame); frames of the latest render still
     gather after each refusal."""
     W, H, S = 320, 180, 2
     gpu = capi.Context(0)
@@ -330,16 +330,24 @@ def test_scene_camera_gather_refuses_other_frames(cube):
         gpu.render_frames(S, W, H, out_ppm=local.ptr, ring=ring)
         gather(local.ptr)
         assert np.array_equal(frames.numpy(), want)
-        # the scene camera moves and is rendered elsewhere: the old frames still gather with the
-        # plan made for their camera ...
+        # the scene camera moves and is rendered elsewhere: the plan follows the context's latest
+        # render (state every rank shares), so the old frames are refused ...
+        old_cam = capi.make_camera((0.0, 0.0, 5.0), (16.0, 9.0), W, 1.0)  # (MainScene's camera)
         gpu.set_camera(capi.make_camera((0.0, 0.0, 4.0), (16.0, 9.0), W, 1.0))
+        gpu.render(W, H, out_ppm=other.ptr)
+        refused(local.ptr)
+        gather(other.ptr, 1)  # the new camera's frame: a new plan
+        assert np.array_equal(frames.numpy()[0], other.numpy()[0])
+        refused(local.ptr)
+        # ... until the old camera is rendered again (the same source key: its frames gather)
+        gpu.set_camera(old_cam)
         gpu.render(W, H, out_ppm=other.ptr)
         gather(local.ptr)
         assert np.array_equal(frames.numpy(), want)
-        gather(other.ptr, 1)  # the new camera's frame: a new plan
-        assert np.array_equal(frames.numpy()[0], other.numpy()[0])
-        # ... but once that plan is replaced, their camera's setup is gone: refused
-        refused(local.ptr)
+        # a null `local` is this rank's own error, after which the plan still serves
+        refused(0)
+        gather(local.ptr)
+        assert np.array_equal(frames.numpy(), want)
     finally:
         if comm:
             capi.comm_destroy(comm)
