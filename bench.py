@@ -255,6 +255,35 @@ def write_ceiling_fields(ct: dict, launch_bytes: int, floor_ms: float) -> dict:
             "kernel": "ceiling_fill_kernel (render.hip): 64x4 blocks, 1 workgroup per CU, unpaced write-through stores"}
 
 
+def merge_times(parts: list) -> dict:
+    """eray_kernel_times of several timed runs as one: launches summed, means weighted by launches."""
+    n = sum(t["launches"] for t in parts)
+    out = dict(parts[0])
+    out["launches"] = n
+    for k in ("frame_kernel_ms", "fill_kernel_ms", "launch_span_ms"):
+        out[k] = sum(t[k] * t["launches"] for t in parts) / n
+    out["frame_kernel_min_ms"] = min(t["frame_kernel_min_ms"] for t in parts)
+    out["frame_kernel_max_ms"] = max(t["frame_kernel_max_ms"] for t in parts)
+    return out
+
+
+def floor_and_ceiling(empty, frames: int, W: int, H: int, tag: str, F: int, **kw) -> tuple:
+    """The fill floor (the frame kernel with no object: eray_time_frames_ring) and the write ceiling
+    (eray_time_write_ceiling) of the same launches into the same ring, measured in four alternating
+    chunks each (ROCTx ranges {tag}fill_floor_F{F} / {tag}write_ceiling_F{F}), so that neither leg
+    inherits the ring state the other or the frame leg before them left."""
+    chunks = 4
+    per = max(frames // chunks // F, 1) * F
+    ceil_kw = {k: kw[k] for k in ("ring", "out_rgb", "out_ppm") if k in kw}
+    fl, ce = [], []
+    for _ in range(chunks):
+        with MARK.range(f"{tag}fill_floor_F{F}"):
+            fl.append(empty.time_frames(per, W, H, **kw))
+        with MARK.range(f"{tag}write_ceiling_F{F}"):
+            ce.append(empty.time_write_ceiling(per, W, H, **ceil_kw))
+    return merge_times(fl), merge_times(ce)
+
+
 def empty_scene_context(device: int, width: int, height: int, fov, stream) -> "capi.Context":
     """The same camera and lights with no object: every pixel is the miss colour (engine.rs:
     208-213), so its frame kernel is the fill alone — this kernel's write floor for the frame."""
@@ -330,10 +359,7 @@ def north_star_line(device: int, steps: int, slot_counts=None) -> dict:
         empty.time_frames(2, W, H, **out)
         with MARK.range(f"{tag}_timed_F1"):
             kt = ctx.time_frames(max(steps, 64), W, H, **out)
-        with MARK.range(f"{tag}_fill_floor_F1"):
-            ft = empty.time_frames(max(steps, 64), W, H, **out)
-        with MARK.range(f"{tag}_write_ceiling_F1"):
-            ct = empty.time_write_ceiling(max(steps, 64), W, H, **out)
+        ft, ct = floor_and_ceiling(empty, max(steps, 64), W, H, f"{tag}_", 1, **out)
         k_ms, f_ms = kt["frame_kernel_ms"], ft["frame_kernel_ms"]
         gbs = alg / (k_ms * 1e-3) / 1e9
         fill_gbs = 15 * W * H / (f_ms * 1e-3) / 1e9
@@ -704,11 +730,7 @@ def main() -> None:
             latency = ctx.time_frames(max(min(args.steps, 64), 2), width, H, **lat_args)
         if world == 1:  # the same frames with no object: the fill alone, this kernel's write floor
             empty = empty_scene_context(device, width, H, frame_camera_fov(width, H), stream)
-            with MARK.range(f"fill_floor_F{F}"):
-                ft = empty.time_frames(n_kt, width, H, **ring1)
-            with MARK.range(f"write_ceiling_F{F}"):
-                ct = empty.time_write_ceiling(n_kt, width, H, ring=ring1["ring"], out_rgb=ring1["out_rgb"],
-                                              out_ppm=ring1["out_ppm"])
+            ft, ct = floor_and_ceiling(empty, n_kt, width, H, "", F, **ring1)
             fill_floor = {"frame_kernel_ms_per_launch": round(ft["frame_kernel_ms"], 6),
                           "frames_per_launch": ft["frames_per_launch"],
                           "achieved_gbs": round(15 * width * rows * ft["frames_per_launch"] / (ft["frame_kernel_ms"] * 1e-3)
@@ -729,11 +751,7 @@ def main() -> None:
                 ctx.render_frames(big, width, H, **bkw)  # (the slots' pages touched once)
                 with MARK.range(f"beyond_mall_timed_F{F}"):
                     bt = ctx.time_frames(n_kt, width, H, **bkw)
-                with MARK.range(f"beyond_mall_fill_floor_F{F}"):
-                    bft = empty.time_frames(n_kt, width, H, **bkw)
-                with MARK.range(f"beyond_mall_write_ceiling_F{F}"):
-                    bct = empty.time_write_ceiling(n_kt, width, H, ring=bkw["ring"], out_rgb=bkw["out_rgb"],
-                                                   out_ppm=bkw["out_ppm"])
+                bft, bct = floor_and_ceiling(empty, n_kt, width, H, "beyond_mall_", F, **bkw)
                 del brgb, bppm
                 b_ms = bt["frame_kernel_ms"]
                 b_gbs = algorithmic_bytes(width * rows, hits, hit_faces) * F / (b_ms * 1e-3) / 1e9

@@ -198,6 +198,7 @@ DEBUG_SIGNATURES = {
     "eray_debug_bin_dump": (C.c_int, [_P, _U, _U, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64), _U,
                                       C.POINTER(C.c_uint32)]),
     "eray_debug_set_bin_capacity": (C.c_int, [_P, C.c_uint64]),
+    "eray_debug_bin_counts": (C.c_int, [_P, _U, C.POINTER(C.c_uint32), _U, C.POINTER(C.c_uint32)]),
     "eray_debug_bin_capacity": (C.c_uint64, [_P]),
     "eray_debug_setup_state": (C.c_int, [_P, _U, _P, C.POINTER(C.c_int32)]),
     "eray_debug_unband": (C.c_int, [_P, _P, _P, _U, _U, _U, _U]),

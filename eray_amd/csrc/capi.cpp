@@ -2215,6 +2215,25 @@ extern "C" int eray_debug_bin_dump(eray_ctx* ctx, uint32_t index, uint32_t bin, 
     return ERAY_OK;
 }
 
+// Diagnostics: the entry count of every bin of object `index` (bins.nbins of them, row-major over
+// the camera's bin rows, at most `cap`); *nbins = the object's bin count.  Synchronises.
+extern "C" int eray_debug_bin_counts(eray_ctx* ctx, uint32_t index, uint32_t* counts, uint32_t cap, uint32_t* nbins) {
+    if (!ctx || !nbins || index >= ctx->objects.size() || ctx->objects[index].T <= kDirectMax || !ctx->bins.start)
+        return ERAY_E_INVALID_ARGUMENT;
+    const BinBuffers& b = ctx->bins;
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < index; ++i) k += ctx->objects[i].T > kDirectMax;
+    *nbins = b.nbins;
+    const uint32_t m = std::min(b.nbins, cap);
+    std::vector<uint32_t> st((size_t)m + 1);
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess ||
+        (m && hipMemcpy(st.data(), b.start + (size_t)k * b.nbins, sizeof(uint32_t) * ((size_t)m + 1),
+                        hipMemcpyDeviceToHost) != hipSuccess))
+        return set_error(ctx, ERAY_E_HIP, "bin counts copy failed");
+    for (uint32_t i = 0; i < m; ++i) counts[i] = st[i + 1] - st[i];
+    return ERAY_OK;
+}
+
 // Diagnostics (not part of include/eray_hip.h): the screen bins' entry capacity.  Setting it
 // reallocates the bins at the next setup; a setup whose entries exceed it renders its binned
 // objects through LDS tiles and the capacity grows once the host sees the count (tests).

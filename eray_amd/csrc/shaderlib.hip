@@ -200,7 +200,7 @@ __global__ void __launch_bounds__(kBlock) material_example_kernel(
     }
 }
 // texels per thread of the fused material kernel (narrow launches)
-constexpr int kMatTexels = 1;
+constexpr int kMatTexels = 2;
 
 }  // namespace
 

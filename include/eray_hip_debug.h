@@ -65,6 +65,9 @@ int eray_debug_gather_check(const uint32_t* rank_bytes, uint32_t nranks, uint32_
 /* Host only: a new gather plan's verdict on rank `rank` from every rank's exchange record
  * (status, kind, key low, key high; 4 words each) — all ranks accept or all fail together. */
 int eray_debug_plan_verdict(const int32_t* records, uint32_t nranks, uint32_t rank);
+/* The entry count of every screen bin of object `index` as built for the last setup (row-major
+ * over the camera's bin rows, at most `cap`); *nbins receives the bin count.  Synchronises. */
+int eray_debug_bin_counts(eray_ctx* ctx, uint32_t index, uint32_t* counts, uint32_t cap, uint32_t* nbins);
 /* Host only: eray_gather_frames' re-plan decision from its only inputs — whether the cached plan
  * fits the call's shared arguments, the plan's source (kind, key) and the context's latest
  * scene-camera / camera-path render's — 1: a new plan is exchanged, 0: the cached one is used. */

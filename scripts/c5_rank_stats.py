@@ -65,6 +65,15 @@ def main() -> None:
         cs = CamStateHead()
         rect = (C.c_int32 * 4)()
         assert lib.eray_debug_setup_state(ctx._h, 0, C.byref(cs), rect) == 0
+        # this rank's own bin rows (camera rows 4 r + 32 k .. + 3; at phase 0 camera row y is in bin
+        # row y / 4 + 1, internal.hpp / render.hip's bin index)
+        nb = C.c_uint32()
+        cnt = np.zeros(st[0], np.uint32)
+        assert lib.eray_debug_bin_counts(ctx._h, 0, cnt.ctypes.data_as(C.POINTER(C.c_uint32)), int(st[0]), C.byref(nb)) == 0
+        bins_x = (W + 15) // 16
+        rows_b = cnt.reshape(-1, bins_x)
+        mine = rows_b[r + 1::a.world]
+        heavy = mine[mine > 64]
         times = {}
         for F in (1, 4):
             rkw = dict(kw, out_rgb=rgb.ptr, out_ppm=ppm.ptr)
@@ -75,7 +84,10 @@ def main() -> None:
             times[f"F{F}_us_per_frame"] = round(t["launch_span_ms"] * 1e3 / F, 2)
         rec = {"rank": r, "rows": rows, "hit_pixels": hits, "detail_sub_blocks": cs.total_sub,
                "heavy_bins": int(st[11]), "bin_entries": int(st[1]), "pairs": int(st[2]),
-               "nonempty_bins": int(st[4]), "most_entries_in_a_bin": int(st[3]), **times}
+               "nonempty_bins": int(st[4]), "most_entries_in_a_bin": int(st[3]),
+               "own_bins": {"entries": int(mine.sum()), "nonempty": int((mine > 0).sum()), "max_entries": int(mine.max()),
+                            "over_64": int(heavy.size), "over_256": int((mine > 256).sum()),
+                            "chunks_of_heaviest_10": sorted((((mine.ravel() + 63) // 64)).tolist())[-10:]}, **times}
         out["ranks"].append(rec)
         print(json.dumps(rec), flush=True)
         for x in (rgb, ppm, face):

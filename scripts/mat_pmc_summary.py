@@ -50,6 +50,13 @@ def main() -> None:
         out["wait_frac"] = round(c.get("SQ_WAIT_ANY", 0.0) / c["SQ_WAVE_CYCLES"], 4)
     if "SQ_INSTS_VALU" in c:
         out["valu_insts_per_texel"] = round(c["SQ_INSTS_VALU"] * 64 / TEXELS, 2)  # (per wave -> per lane)
+    f64 = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64"))
+    if f64 and c.get("SQ_INSTS_VALU"):
+        out["fp64_share_of_valu"] = round(f64 / c["SQ_INSTS_VALU"], 4)
+    if avg_ns and c.get("SQ_INST_CYCLES_VALU"):
+        # VALU issue cycles over every SIMD's cycles of the kernel (1024 SIMDs at 2.4 GHz): the
+        # fraction of the chip's VALU issue the kernel used
+        out["valu_issue_frac"] = round(c["SQ_INST_CYCLES_VALU"] / (1024 * avg_ns * 2.4), 4)
     if "WRITE_SIZE" in c:
         out["write_bytes"] = c["WRITE_SIZE"] * 1024
         out["write_over_algorithmic"] = round(c["WRITE_SIZE"] * 1024 / (TEXELS * 16), 4)
