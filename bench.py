@@ -487,9 +487,10 @@ def material_roofline(scene, stream, reps: int = 20) -> dict:
     return {"kernel": "material_example_kernel (eray_amd/csrc/shaderlib.hip)", "texels": texels,
             "bytes_per_update": texels * 16, "us_per_update": round(us, 3), "achieved_gbs": round(gbs, 1),
             "peak_gbs": PEAK_HBM_GBS, "frac": round(gbs / PEAK_HBM_GBS, 4),
-            "bound": "VALU / FP64 chain of the double-precision glibc cosf restatement, not HBM: 89 VALU "
-                     "instructions per texel, 0.43 of wave cycles waiting, WRITE_SIZE = the 16 B per texel "
-                     "(profiles/r05/material_pmc.json)"}
+            "bound": "latency of the dependent double-precision glibc cosf chain per wave (8 waves per SIMD) "
+                     "and the launch's ramp, neither VALU issue (~15 % of the chip's) nor HBM: 82 VALU "
+                     "instructions per texel (18 % FP64), 0.48 of wave cycles waiting, WRITE_SIZE = the 16 B "
+                     "per texel (profiles/r06/material_pmc.json)"}
 
 
 def anti_aliasing_line(scene, args, width, height, out) -> dict:

@@ -32,7 +32,7 @@ def main() -> None:
         with open(path) as f:
             for row in csv.DictReader(f):
                 name = row["Kernel_Name"]
-                if "frame_kernel" in name or "fill_kernel" in name:
+                if ("frame_kernel" in name or "fill_kernel" in name) and "ceiling_fill_kernel" not in name:
                     per[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
     if not per:
         raise SystemExit(f"no frame_kernel counters under {src}")
@@ -41,7 +41,8 @@ def main() -> None:
     c = {k: statistics.median(v) for k, v in per[name].items()}
     dispatches = max(len(v) for v in per[name].values())
     fetch, write = c.get("FETCH_SIZE", 0.0) * 1024, c.get("WRITE_SIZE", 0.0) * 1024
-    fills = [k for k in per if "fill_kernel" in k]
+    # (the separate fill kernel beside a dense frame kernel; not the write ceiling's stream)
+    fills = [k for k in per if "fill_kernel" in k and "ceiling_fill_kernel" not in k]
     if fills:
         f = {k: statistics.median(v) for k, v in per[fills[0]].items()}
         fetch += f.get("FETCH_SIZE", 0.0) * 1024

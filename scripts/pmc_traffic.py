@@ -66,7 +66,8 @@ def pmc(tag: str, pmc_dir: str = "pmc", out_name: str = "pmc_traffic.json", work
     fetch, write = c.get("FETCH_SIZE", 0.0) * 1024, c.get("WRITE_SIZE", 0.0) * 1024
     # frames whose background comes from the separate fill_kernel (dense large-mesh builds): one
     # fill launch per frame launch, its bytes belong to the frame
-    fills = [k for k in per if "fill_kernel" in k]
+    # (the separate fill kernel beside a dense frame kernel; not the write ceiling's stream)
+    fills = [k for k in per if "fill_kernel" in k and "ceiling_fill_kernel" not in k]
     if fills:
         f = {k: statistics.median(v) for k, v in per[fills[0]].items()}
         fetch += f.get("FETCH_SIZE", 0.0) * 1024

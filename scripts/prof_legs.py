@@ -28,7 +28,7 @@ def _find(d: str, suffix: str) -> list[str]:
 def _short(name: str) -> str:
     """frame_kernel<...> / fill_kernel<...> / other kernels by their base name."""
     base = name.replace("(anonymous namespace)", "")
-    for k in ("frame_kernel", "fill_kernel", "trace_kernel", "trace_binned_kernel", "trace_heavy_kernel",
+    for k in ("ceiling_fill_kernel", "frame_kernel", "fill_kernel", "trace_kernel", "trace_binned_kernel", "trace_heavy_kernel",
               "trace_cull_kernel", "camera_setup_kernel", "bin_pairs_kernel", "material_example_kernel"):
         if k in base:
             return k
