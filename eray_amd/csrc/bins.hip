@@ -499,45 +499,118 @@ __device__ __forceinline__ void max4(uint32_t* dst, const uint32_t (&a)[4]) {
 // in chunks of 64 entries, and a chunk whose faces all come after every live pixel's best hit so
 // far is skipped — in face order, the later chunks of a dense bin mostly are.  So each bin with
 // more than one chunk (and at most kSortMax entries; longer ones stay as they are) is sorted by
-// face index (bin_sort_kernel, one wave per bin).  The frame kernel relies on it: in a bin of 65 to kBinSortMax entries the
-// position order is the face order (render.hip first_hit_binned).
+// face index: bins of up to kSortWave entries one wave each, longer ones (the poles of the 1M-face
+// stand-in put 300-700 entries into a few bins) one workgroup each.  The frame kernel relies on
+// it: in a bin of 65 to kBinSortMax entries the position order is the face order
+// (render.hip first_hit_binned / first_hit_binned_wave), and chunk c's first two entries carry the
+// union of the masks of chunks c + 1 .. (BinEntry::pad): pixels outside it cannot be hit by
+// anything later in the bin.
 constexpr uint32_t kSortMax = kBinSortMax;
-constexpr uint32_t kSortPer = kSortMax / 64;  // entries per lane
-constexpr uint32_t kSortGrid = 1024;          // workgroups of the sort kernel's grid-stride loop
+constexpr uint32_t kSortWave = 256;            // bins sorted by one wave (whole bin in its LDS slice)
+constexpr uint32_t kSortPer = kSortWave / 64;  // entries per lane
+constexpr uint32_t kSortChunks = kSortMax / 64;
+constexpr uint32_t kSortGrid = 1024;  // workgroups of the sort kernel's grid-stride loops
+static_assert(kSortMax == (kBinWG / 64) * kSortWave, "a workgroup's sort LDS holds one longest bin");
 
-// The bins to sort, appended to a work list (one counter atomic per wave), so that the sort
-// kernel spreads them over all its waves: the dense bins sit next to each other on the screen.
+// The bins to sort, appended to a work list (one counter atomic per wave and kind), so that the
+// sort kernel spreads them over all its waves: the dense bins sit next to each other on the
+// screen.  Wave-sorted bins go to the front of sortq (count nsort[0]), workgroup-sorted ones to
+// the back (sortq[keys - 1 - i], count nsort[1]); together they are at most `keys`.
 __device__ __forceinline__ void queue_sort(const uint32_t* __restrict__ start, uint32_t b, uint32_t keys,
                                            uint32_t* __restrict__ sortq, uint32_t* __restrict__ nsort) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t cnt = b < keys ? start[b + 1] - start[b] : 0u;
-    const bool want = cnt > 64 && cnt <= kSortMax;
-    const unsigned long long bal = __ballot(want);
-    if (!bal) return;
-    const uint32_t first = (uint32_t)(__ffsll(bal) - 1);
-    uint32_t base = 0;
-    if (lane == first) base = atomicAdd(nsort, (uint32_t)__popcll(bal));
-    base = (uint32_t)__shfl((int)base, (int)first);
-    if (want) sortq[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = b;
+#pragma unroll
+    for (uint32_t big = 0; big < 2; ++big) {
+        const bool want = cnt > (big ? kSortWave : 64u) && cnt <= (big ? kSortMax : kSortWave);
+        const unsigned long long bal = __ballot(want);
+        if (!bal) continue;
+        const uint32_t first = (uint32_t)(__ffsll(bal) - 1);
+        uint32_t base = 0;
+        if (lane == first) base = atomicAdd(nsort + big, (uint32_t)__popcll(bal));
+        base = (uint32_t)__shfl((int)base, (int)first);
+        const uint32_t at = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+        if (want) sortq[big ? keys - 1u - at : at] = b;
+    }
 }
 
-// One wave per queued bin: its entries staged in LDS, each entry's rank = the number of the bin's
-// faces below its own (a face appears at most once per bin), each entry written back at its rank.
+// A sorted entry's pad word: chunk c's first two entries (rank 64 c, 64 c + 1) get the low and
+// high halves of sfx[c + 1], the union of the masks of chunks c + 1 .. (sfx[nch] = 0).
+__device__ __forceinline__ uint32_t sorted_pad(uint32_t rank, uint32_t nch, const unsigned long long* sfx) {
+    const uint32_t c = rank >> 6, k = rank & 63u;
+    if (k > 1u || c + 1u >= nch) return 0u;
+    const unsigned long long u = sfx[c + 1u];
+    return k ? (uint32_t)(u >> 32) : (uint32_t)u;
+}
+
+// Each queued bin: its entries staged in LDS, each entry's rank = the number of the bin's faces
+// below its own (a face appears at most once per bin), the chunks' mask unions OR-ed by rank and
+// suffix-combined, each entry written back at its rank.
 __global__ void __launch_bounds__(kBinWG) bin_sort_kernel(const uint32_t* __restrict__ sortq,
                                                           const uint32_t* __restrict__ nsort,
                                                           const uint32_t* __restrict__ start,
-                                                          BinEntry* __restrict__ ent) {
-    __shared__ BinEntry s_ent[kBinWG / 64][kSortMax];
+                                                          BinEntry* __restrict__ ent, uint32_t keys) {
+    __shared__ BinEntry s_ent[kBinWG / 64][kSortWave];  // a wave's bin; the workgroup's: all of it
+    __shared__ unsigned long long s_cu[kBinWG / 64][kSortChunks];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t items = *nsort;
-    BinEntry* se = s_ent[wave];
-    for (uint32_t it = blockIdx.x * (kBinWG / 64) + wave; it < items; it += gridDim.x * (kBinWG / 64)) {
-        const uint32_t key = sortq[it];  // wave-uniform
-        const uint32_t s0 = start[key], n = start[key + 1] - s0;
-        uint32_t v[kSortPer], r[kSortPer];
+    // ---- bins of 65..kSortWave entries: one wave each
+    {
+        const uint32_t items = nsort[0];
+        BinEntry* se = s_ent[wave];
+        unsigned long long* cu = s_cu[wave];
+        for (uint32_t it = blockIdx.x * (kBinWG / 64) + wave; it < items; it += gridDim.x * (kBinWG / 64)) {
+            const uint32_t key = sortq[it];  // wave-uniform
+            const uint32_t s0 = start[key], n = start[key + 1] - s0, nch = (n + 63) / 64;
+            uint32_t v[kSortPer], r[kSortPer];
 #pragma unroll
-        for (uint32_t q = 0; q < kSortPer; ++q) {
-            const uint32_t e = lane + 64 * q;
+            for (uint32_t q = 0; q < kSortPer; ++q) {
+                const uint32_t e = lane + 64 * q;
+                v[q] = 0xffffffffu;
+                r[q] = 0;
+                if (e < n) {
+                    se[e] = ent[s0 + e];
+                    v[q] = se[e].tri;
+                }
+            }
+            if (lane < kSortPer) cu[lane] = 0ull;
+            wave_sync();
+            for (uint32_t j = 0; j < n; ++j) {
+                const uint32_t f = se[j].tri;
+#pragma unroll
+                for (uint32_t q = 0; q < kSortPer; ++q) r[q] += f < v[q] ? 1u : 0u;
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < kSortPer; ++q)
+                if (lane + 64 * q < n) atomicOr(&cu[r[q] >> 6], se[lane + 64 * q].mask);
+            wave_sync();
+            if (lane == 0)
+                for (uint32_t c = nch - 1; c-- > 0;) cu[c] |= cu[c + 1];
+            wave_sync();
+#pragma unroll
+            for (uint32_t q = 0; q < kSortPer; ++q) {
+                const uint32_t e = lane + 64 * q;
+                if (e < n) {
+                    BinEntry x = se[e];
+                    x.pad = sorted_pad(r[q], nch, cu);
+                    ent[s0 + r[q]] = x;
+                }
+            }
+            wave_sync();  // the LDS is rewritten by the next bin
+        }
+    }
+    __syncthreads();  // (the workgroup's bins below use every wave's slice)
+    // ---- bins of kSortWave + 1..kSortMax entries: one workgroup each
+    const uint32_t nbig = nsort[1];
+    BinEntry* se = &s_ent[0][0];
+    unsigned long long* cu = s_cu[0];
+    constexpr uint32_t kPer = kSortMax / kBinWG;
+    for (uint32_t it = blockIdx.x; it < nbig; it += gridDim.x) {  // workgroup-uniform
+        const uint32_t key = sortq[keys - 1u - it];
+        const uint32_t s0 = start[key], n = start[key + 1] - s0, nch = (n + 63) / 64;
+        uint32_t v[kPer], r[kPer];
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; ++q) {
+            const uint32_t e = threadIdx.x + kBinWG * q;
             v[q] = 0xffffffffu;
             r[q] = 0;
             if (e < n) {
@@ -545,22 +618,30 @@ __global__ void __launch_bounds__(kBinWG) bin_sort_kernel(const uint32_t* __rest
                 v[q] = se[e].tri;
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (threadIdx.x < kSortChunks) cu[threadIdx.x] = 0ull;
+        __syncthreads();
         for (uint32_t j = 0; j < n; ++j) {
             const uint32_t f = se[j].tri;
 #pragma unroll
-            for (uint32_t q = 0; q < kSortPer; ++q) r[q] += f < v[q] ? 1u : 0u;
+            for (uint32_t q = 0; q < kPer; ++q) r[q] += f < v[q] ? 1u : 0u;
         }
 #pragma unroll
-        for (uint32_t q = 0; q < kSortPer; ++q) {
-            const uint32_t e = lane + 64 * q;
-            if (e < n) ent[s0 + r[q]] = se[e];
+        for (uint32_t q = 0; q < kPer; ++q)
+            if (threadIdx.x + kBinWG * q < n) atomicOr(&cu[r[q] >> 6], se[threadIdx.x + kBinWG * q].mask);
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (uint32_t c = nch - 1; c-- > 0;) cu[c] |= cu[c + 1];
+        __syncthreads();
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; ++q) {
+            const uint32_t e = threadIdx.x + kBinWG * q;
+            if (e < n) {
+                BinEntry x = se[e];
+                x.pad = sorted_pad(r[q], nch, cu);
+                ent[s0 + r[q]] = x;
+            }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();  // the LDS is rewritten by the next bin
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __syncthreads();  // the LDS is rewritten by the next bin
     }
 }
 
@@ -674,7 +755,7 @@ __global__ void __launch_bounds__(kBinWG) bins_finalize_kernel(uint32_t per, con
     __syncthreads();  // (every thread has read the counts)
     if (threadIdx.x < kShards) n[threadIdx.x * kShardStride] = 0u;
     if (threadIdx.x == 0) {
-        *nsort = 0u;  // (bin_sort_kernel has run)
+        nsort[0] = nsort[1] = 0u;  // (bin_sort_kernel has run)
         // the most entries any setup needed since the buffers were allocated (the host grows the
         // capacity from it), and whether any overflowed
         for (uint32_t k = 0; k < ncam; ++k) {  // (several cameras: every camera's state)
@@ -884,12 +965,12 @@ hipError_t bins_alloc(BinBuffers& b, uint32_t T, uint32_t nb, const uint32_t* kb
         (e = grow(&b.dcount, 2)) != hipSuccess ||
         (e = grow(&b.dlist, b.nsub * ncam)) != hipSuccess ||
         (e = grow(&b.docc, (size_t)tiles_x * subs_y * ncam)) != hipSuccess ||
-        (e = grow(&b.sortq, std::max<size_t>(keys, 1))) != hipSuccess || (e = grow(&b.nsort, 1)) != hipSuccess)
+        (e = grow(&b.sortq, std::max<size_t>(keys, 1))) != hipSuccess || (e = grow(&b.nsort, 2)) != hipSuccess)
         return e;
     // counters zero between builds (each build leaves them so)
     if ((e = hipMemsetAsync(b.count, 0, sizeof(uint32_t) * (keys + 1), s)) != hipSuccess ||
         (e = hipMemsetAsync(b.n, 0, sizeof(uint32_t) * kShards * kShardStride, s)) != hipSuccess ||
-        (e = hipMemsetAsync(b.nsort, 0, sizeof(uint32_t), s)) != hipSuccess ||
+        (e = hipMemsetAsync(b.nsort, 0, 2 * sizeof(uint32_t), s)) != hipSuccess ||
         (e = hipMemsetAsync(b.done, 0, sizeof(uint32_t), s)) != hipSuccess ||
         (e = hipMemsetAsync(b.acc, 0, sizeof(uint32_t) * kAccStride * nb, s)) != hipSuccess ||
         (e = hipMemcpyAsync(b.kbegin, kbegin, sizeof(uint32_t) * nb, hipMemcpyHostToDevice, s)) != hipSuccess ||
@@ -935,7 +1016,7 @@ hipError_t launch_bins_build(const SetupParams& sp, BinBuffers& b, uint32_t tile
                                                          b.acc, b.part, b.done, b.n, (uint32_t)b.cap, b.kobj, sp.objs,
                                                          b.ent, b.count, b.sortq, b.nsort, sp.state, ncam, nullptr, 1u);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    bin_sort_kernel<<<kSortGrid, kBinWG, 0, s>>>(b.sortq, b.nsort, b.start, b.ent);
+    bin_sort_kernel<<<kSortGrid, kBinWG, 0, s>>>(b.sortq, b.nsort, b.start, b.ent, (uint32_t)keys);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     bins_finalize_kernel<true><<<1, kBinWG, 0, s>>>(per, b.start, b.nb, b.bins_x, b.nbins, sp.W, sp.H, b.phase, b.acc,
                                                     b.part, b.done, b.n, (uint32_t)b.cap, b.kobj, sp.objs, b.ent, b.count,

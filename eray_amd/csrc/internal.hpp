@@ -78,9 +78,12 @@ constexpr uint32_t kCacheTris = 256, kCacheObjects = 16, kCacheLights = 16;
 constexpr uint32_t kDirectMax = 256;
 // Screen bins of large objects' faces: kBinW x kBinH pixels (one wave's 16 x 4 sub-block).
 constexpr uint32_t kBinW = 16, kBinH = 4;
-// Bins of at most this many entries are sorted by face index (bins.hip sort_bins); longer ones
-// keep the scatter's order.
-constexpr uint32_t kBinSortMax = 256;
+// Bins of 65 to this many entries are sorted by face index (bins.hip bin_sort_kernel); longer
+// ones keep the scatter's order.  In a sorted bin each full 64-entry chunk but the last also
+// carries, in the pad words of its first two entries (low, high half), the union of the pixel
+// masks of every later chunk: the frame kernel stops the bin once no pixel that can still improve
+// is covered by what is left (render.hip first_hit_binned_wave).
+constexpr uint32_t kBinSortMax = 1024;
 // Detail rectangles carried in the kernel arguments (more objects: merged into the last one).
 constexpr int kMaxRects = 8;
 // Deepest reflection recursion the general tracer keeps frames for (Engine::bounces).
@@ -109,7 +112,8 @@ constexpr uint64_t kInfinityCacheBytes = 256ull << 20;
 struct alignas(16) BinEntry {
     TriHot hot;
     unsigned long long mask;
-    uint32_t tri, pad;
+    uint32_t tri;
+    uint32_t pad;  // sorted bins: half of the later chunks' mask union (kBinSortMax), else 0
 };
 static_assert(sizeof(BinEntry) == 64, "one 64-B line per bin entry");
 
@@ -121,7 +125,7 @@ struct ObjGeom {  // what the triangle scans need of an object, 64 B
     float bb_lo[3], bb_hi[3];
     // Screen bins of a large object's faces (bins.hip), or null: bin b's entries are
     // bin_ent[bin_start[b] .. bin_start[b + 1]) (bins of 65..kBinSortMax entries in increasing
-    // face index).
+    // face index, with the later chunks' mask unions, BinEntry).
     const uint32_t* bin_start;
     const BinEntry* bin_ent;
 };

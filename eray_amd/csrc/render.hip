@@ -605,10 +605,14 @@ constexpr uint32_t kWaveBinMaxTris = (1u << 26) - 1u;
 // workgroup barrier (the light sub-blocks of a frame's ordered detail list: their bins hold at
 // most one 64-entry chunk, so sharing chunks across the workgroup's waves, as first_hit_binned
 // does, buys nothing and its barriers tie four sub-blocks' latency chains together).  The same
-// (face, pixel) pair tests; each pixel keeps the smallest key face << 6 | slot of a hitting pair
-// (LDS atomicMin), so the smallest hitting face index wins (object.rs:63-78) and its record is
-// still in the wave's LDS: the winner's u, v, t are recomputed from there after each chunk,
-// not re-read from memory.
+// (face, pixel) pair tests; each pixel keeps the smallest order key of a hitting pair (LDS
+// atomicMin), so the smallest hitting face index wins (object.rs:63-78) and its record is still
+// in the wave's LDS: the winner's u, v, t are recomputed from there after each chunk, not re-read
+// from memory.  Keys: face << 6 | slot in a bin in no order; in a sorted bin (65..kBinSortMax
+// entries, bins.hip bin_sort_kernel) the position, which grows with the face index — a pixel
+// whose best position precedes a chunk cannot improve there, and after each chunk the bin ends
+// once no pixel that still can is in the later chunks' mask union (BinEntry::pad): a heavy bin's
+// wave stops at the chunk that settles its last pixel, not at the bin's end.
 template <typename Activate>
 __device__ void first_hit_binned_wave(const ObjGeom& ob, uint32_t bin, int& st, const f3& o, const f3& d,
                                       Activate&& activate, int& found, float& hu, float& hv, float& ht, char* s_bins,
@@ -628,25 +632,35 @@ __device__ void first_hit_binned_wave(const ObjGeom& ob, uint32_t bin, int& st, 
     L.dir[2][lane] = d.z;
     uint32_t best = st == kSearching ? 0xffffffffu : 0u;  // this lane's pixel: its winning key so far
     L.best[lane] = best;
+    const bool sorted = hi - lo > 64 && hi - lo <= kBinSortMax;  // (wave-uniform)
     for (uint32_t base = lo; base < hi; base += 64) {
         const uint32_t j = base + lane;
-        uint32_t fj = 0xffffffffu;
+        uint32_t fj = 0xffffffffu, sfx = 0;
         unsigned long long pm = 0;
         if (j < hi) {
             const BinEntry x = load_rec(ob.bin_ent, j);
             fj = x.tri;
             pm = x.mask;
+            sfx = x.pad;
             L.cand[lane] = x.hot;
         }
-        uint32_t cmin = fj;  // the chunk's smallest face
+        unsigned long long live;  // pixels this chunk can still improve
+        uint32_t key;
+        if (sorted) {
+            live = __ballot(best > base - lo);
+            if (!live) break;  // (and none in any later chunk)
+            key = j - lo;
+        } else {
+            uint32_t cmin = fj;  // the chunk's smallest face
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) cmin = min(cmin, (uint32_t)__shfl_xor((int)cmin, off));
+            for (int off = 32; off > 0; off >>= 1) cmin = min(cmin, (uint32_t)__shfl_xor((int)cmin, off));
+            live = __ballot((best >> 6) > cmin);
+            if (!live) continue;
+            key = (fj << 6) | lane;
+        }
         ERAY_TRACE_WAVE0(9);
-        const unsigned long long live = __ballot((best >> 6) > cmin);  // pixels this chunk can still improve
-        if (!live) continue;
         const unsigned long long pix = pm & live;
         const uint32_t cnt = (uint32_t)__popcll(pix);
-        const uint32_t key = (fj << 6) | lane;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();  // L.cand / L.dir / L.best visible to the wave
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -697,14 +711,20 @@ __device__ void first_hit_binned_wave(const ObjGeom& ob, uint32_t bin, int& st, 
         __builtin_amdgcn_wave_barrier();  // every pair of the chunk tested
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint32_t nb = L.best[lane];
+        const uint32_t fwin = sorted ? (uint32_t)__shfl((int)fj, (int)(nb & 63u)) : nb >> 6;  // its face
         if (nb != best) {  // improved by this chunk: the winner's record is still L.cand[slot]
             best = nb;
             exact_test(L.cand[nb & 63u], o, d, hu, hv, ht);
-            found = (int)(nb >> 6);
+            found = (int)fwin;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();  // L.cand / L.pairs are rewritten by the next chunk
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (sorted) {  // the later chunks' masks (this chunk's first two entries): anything left?
+            const unsigned long long later = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)sfx, 1) << 32) |
+                                             (uint32_t)__builtin_amdgcn_readlane((int)sfx, 0);
+            if (!(__ballot(best > base + 64 - lo) & later)) break;
+        }
     }
     ERAY_TRACE_WAVE0(10);
     ERAY_TRACE_VALUE(15, (hi - lo + 63) / 64);
