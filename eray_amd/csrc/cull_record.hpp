@@ -29,7 +29,12 @@ using namespace eray::dev;
 // normalisation, so condition k fails for every pixel of the rectangle when
 //   max_rect (K + A x' + B y') < -T_k,
 //   T_k = 2 * [ (E_k + 4u|w_k|) Dmax + 4u S |w_k| + 6u (|K| + |A| + |B|) ]
-// (Dmax = largest |D| over the frame; factor 2 = safety).  t >= 0 does not depend on d: when
+// (Dmax = largest |D| over the frame; factor 2 = safety).  For det the bound is tightened to the
+// reference's own threshold: |D| det_f <= D.w_n + T_n / 2 and |D| >= |D_z| = |bl.z - C.z| (the
+// z component of D is the same for every pixel), so det_f < 1e-6 for every pixel when
+//   max_rect (K_n + A x' + B y') < 1e-6 |bl.z - C.z| - T_n
+// — the faces that graze the view (det below 1e-6 but above 0: on the 1M-face stand-in, |n| ~ 2e-5,
+// the band within ~3 degrees of edge-on) leave the bins and their pixel masks.  t >= 0 does not depend on d: when
 // ao.n < -2^-149 |n| (or |n|(1+8u) < 1e-6) no camera ray can hit the face and the whole
 // record rejects.  Any non-finite input disables culling for the face (T = +inf).
 // `xa`..`yb`: the viewport coordinates the rays can take (the frame kernel's camera rays: x', y'
@@ -115,6 +120,8 @@ __device__ inline TriCull cull_record(const TriHot& h, const CullCam& cc) {
     for (int k = 0; k < 4; ++k) {
         const double* w = W[k];
         double Kd = blc[0] * w[0] + blc[1] * w[1] + blc[2] * w[2];
+        // det's threshold (primitives.rs:47-66, 1e-6 in f32), scaled by the smallest |D|, rounded down
+        if (k == 3) Kd -= (double)1e-6f * fabs(blc[2]) * (1.0 - 0x1p-20);
         double Ad = (double)vw * w[0];
         double Bd = 2.0 * w[1];
         double thr = 2.0 * ((E[k] + 4.0 * u * n1(w)) * dmax + 4.0 * u * S * n1(w) +
