@@ -313,8 +313,12 @@ hipError_t launch_tri_precompute(const float* pos, const float* nrm, const float
 // its conservative pixel rectangle, per object the union of those (ObjGeom::rect, written into
 // the device descriptors), for binned objects each face's bin rectangle (bins.hip), and, for
 // scenes without binned objects, the merged detail rectangles of the rendered rows (CamState).
-// camera_setup_kernel's grid: at most this many workgroups, each a contiguous chunk of triangles
-constexpr uint32_t kSetupMaxBlocks = 1024;
+// camera_setup_kernel's grid: at most this many workgroups, each a contiguous chunk of triangles —
+// the workgroups resident at once on MI355X (its chunk pass holds 131 VGPRs and 36.9 KB of LDS:
+// 3 per CU x 256 CUs), so a multi-camera setup runs in one round, not 1.33 (1024: a tail round of
+// 256 workgroups; same-box A/B profiles/r06/ab/ab_r06q_setup_grid.txt: moving 3840x2160 / 70k
+// 46.2 -> 44.7 us, moving 1M faces 268.6 -> 255.5 us per frame)
+constexpr uint32_t kSetupMaxBlocks = 768;
 // camera_setup_kernel's chunk workgroups for T triangles (each a contiguous chunk of
 // ceil(T / blocks) faces)
 inline uint32_t setup_blocks(uint32_t T) {
