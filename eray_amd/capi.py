@@ -197,6 +197,8 @@ DEBUG_SIGNATURES = {
     "eray_debug_set_bin_form": (C.c_int, [_P, C.c_int]),
     "eray_debug_bin_dump": (C.c_int, [_P, _U, _U, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64), _U,
                                       C.POINTER(C.c_uint32)]),
+    "eray_debug_bin_entries": (C.c_int, [_P, _U, _U, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64),
+                                         C.POINTER(C.c_uint32), _U, C.POINTER(C.c_uint32)]),
     "eray_debug_set_bin_capacity": (C.c_int, [_P, C.c_uint64]),
     "eray_debug_bin_counts": (C.c_int, [_P, _U, C.POINTER(C.c_uint32), _U, C.POINTER(C.c_uint32)]),
     "eray_debug_bin_capacity": (C.c_uint64, [_P]),

@@ -2189,10 +2189,11 @@ extern "C" int eray_debug_bin_stats(eray_ctx* ctx, uint32_t index, uint64_t* out
     return ERAY_OK;
 }
 
-// Diagnostics: the entries of bin `bin` of object `index` (faces relative to the object, pixel
-// masks), at most `cap`; *n = the bin's entry count.  Synchronises.
-extern "C" int eray_debug_bin_dump(eray_ctx* ctx, uint32_t index, uint32_t bin, uint32_t* tri, uint64_t* mask,
-                                   uint32_t cap, uint32_t* n) {
+// Diagnostics: the entries of bin `bin` of object `index` in bin order (faces relative to the
+// object, pixel masks, pad words: a sorted bin's later-chunk mask unions, BinEntry), at most
+// `cap`; *n = the bin's entry count; `pad` may be null.  Synchronises.
+extern "C" int eray_debug_bin_entries(eray_ctx* ctx, uint32_t index, uint32_t bin, uint32_t* tri, uint64_t* mask,
+                                      uint32_t* pad, uint32_t cap, uint32_t* n) {
     if (!ctx || !n || index >= ctx->objects.size() || ctx->objects[index].T <= kDirectMax || !ctx->bins.start ||
         bin >= ctx->bins.nbins)
         return ERAY_E_INVALID_ARGUMENT;
@@ -2211,8 +2212,15 @@ extern "C" int eray_debug_bin_dump(eray_ctx* ctx, uint32_t index, uint32_t bin, 
     for (uint32_t i = 0; i < m; ++i) {
         tri[i] = ent[i].tri;
         mask[i] = ent[i].mask;
+        if (pad) pad[i] = ent[i].pad;
     }
     return ERAY_OK;
+}
+
+// Diagnostics: eray_debug_bin_entries without the pad words.
+extern "C" int eray_debug_bin_dump(eray_ctx* ctx, uint32_t index, uint32_t bin, uint32_t* tri, uint64_t* mask,
+                                   uint32_t cap, uint32_t* n) {
+    return eray_debug_bin_entries(ctx, index, bin, tri, mask, nullptr, cap, n);
 }
 
 // Diagnostics: the entry count of every bin of object `index` (bins.nbins of them, row-major over

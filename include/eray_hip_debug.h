@@ -24,6 +24,11 @@ int eray_debug_bin_stats(eray_ctx* ctx, uint32_t index, uint64_t* out);
  * `cap`; *n = the bin's entry count. */
 int eray_debug_bin_dump(eray_ctx* ctx, uint32_t index, uint32_t bin, uint32_t* tri, uint64_t* mask, uint32_t cap,
                         uint32_t* n);
+/* The same entries with their pad words (`pad` may be null): in a bin of 65..1024 entries (sorted by
+ * face), entries 64 c and 64 c + 1 hold the low / high half of the union of the masks of chunks
+ * c + 1 .. (render.hip first_hit_binned_wave's early end); every other pad is 0. */
+int eray_debug_bin_entries(eray_ctx* ctx, uint32_t index, uint32_t bin, uint32_t* tri, uint64_t* mask, uint32_t* pad,
+                           uint32_t cap, uint32_t* n);
 /* The frame setups' pair pass over every (face, bin) pair of the faces' bin rectangles
  * (rect_pairs != 0) instead of the rectangles' rows; the next setup rebuilds the bins. */
 int eray_debug_set_bin_form(eray_ctx* ctx, int rect_pairs);

@@ -298,6 +298,99 @@ def test_c5_every_64th_row_block_equals_brute_force(gpu, synth1m):
         sc.close()
 
 
+def _bin_entries(gpu, b, cap=1024):
+    tri, mask, pad = (ctypes.c_uint32 * cap)(), (ctypes.c_uint64 * cap)(), (ctypes.c_uint32 * cap)()
+    n = ctypes.c_uint32()
+    assert capi.lib().eray_debug_bin_entries(gpu.handle, 0, b, tri, mask, pad, cap, ctypes.byref(n)) == 0
+    m = min(n.value, cap)
+    return (n.value, np.frombuffer(tri, np.uint32)[:m].copy(), np.frombuffer(mask, np.uint64)[:m].copy(),
+            np.frombuffer(pad, np.uint32)[:m].copy())
+
+
+def test_c5_sorted_bins_carry_later_chunk_masks(gpu, synth1m):
+    """C5's bins (1M faces, 7680x4320) as render.hip first_hit_binned_wave relies on them
+    (bins.hip bin_sort_kernel): every bin of 65..1024 entries lists its faces in increasing index —
+    including those of more than 256 entries, sorted by a whole workgroup — and the first two
+    entries of each chunk but the last hold the low and high half of the union of the masks of the
+    later chunks; every other pad word is 0."""
+    W, H = 7680, 4320
+    sc = MainScene(gpu, *synth1m, W, H, texture=1024, fov=(16.0, 9.0))
+    fr = Frame(gpu, W, H)
+    try:
+        fr.render(W, H)  # (the scene camera's full-frame setup: its bins)
+        st = (ctypes.c_uint64 * 14)()
+        assert capi.lib().eray_debug_bin_stats(gpu.handle, 0, st) == 0
+        nbins = int(st[0])
+        counts = np.zeros(nbins, np.uint32)
+        nb = ctypes.c_uint32()
+        assert capi.lib().eray_debug_bin_counts(gpu.handle, 0, counts.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                                nbins, ctypes.byref(nb)) == 0
+        heavy = np.nonzero(counts > 64)[0]
+        assert len(heavy) > 1000 and counts.max() <= 1024
+        big = np.nonzero(counts > 256)[0]
+        assert len(big) > 0, "no bin for the workgroup sort"
+        rng = np.random.default_rng(6)
+        pick = np.concatenate([big, rng.choice(heavy, 200, replace=False), np.nonzero((counts > 0) & (counts <= 64))[0][:50]])
+        for b in pick.tolist():
+            n, tri, mask, pad = _bin_entries(gpu, b)
+            assert n == counts[b]
+            if n <= 64:
+                assert not pad.any(), f"bin {b}: pads in an unsorted bin"
+                continue
+            assert (np.diff(tri.astype(np.int64)) > 0).all(), f"bin {b} ({n} entries) not in face order"
+            nch = (n + 63) // 64
+            want = np.zeros(n, np.uint32)
+            for c in range(nch - 1):
+                u = np.bitwise_or.reduce(mask[64 * (c + 1):])
+                want[64 * c] = np.uint32(int(u) & 0xFFFFFFFF)
+                want[64 * c + 1] = np.uint32(int(u) >> 32)
+            assert np.array_equal(pad, want), f"bin {b} ({n} entries): later-chunk mask unions"
+    finally:
+        fr.free()
+        sc.close()
+
+
+def test_faces_grazing_the_view_leave_the_bins(gpu):
+    """Hand-derived (primitives.rs:47-66: a hit needs det = -(d . n) >= 1e-6): 400 small faces
+    tilted so that det lies between 0 and 1e-6 for every camera ray near them (n = e1 x e2 with
+    e1 = (s, 0, 0), e2 = (0, s eps, -s): det ~ s^2 eps = 5e-7 at s = 0.01, eps = 0.005).  The
+    culling records' det bound drops them — no bin entry, an empty object rectangle — and the
+    frame is all background, as the brute-force scan finds; tilted 200x further the
+    same faces are binned and hit (det ~ 1e-4: each face about a pixel tall), culled = brute force
+    bit for bit."""
+    W, H = 1920, 1080
+    s = 0.01
+    rng = np.random.default_rng(11)
+    cx = rng.uniform(-0.5, 0.5, 400)
+    cy = rng.uniform(-0.01, 0.01, 400)  # rays through them have |d.y| <~ 0.003: det stays in (0, 1e-6)
+    results = {}
+    for eps in (0.005, 1.0):
+        pos = np.zeros((400, 9), np.float32)
+        for i in range(400):
+            a = np.array([cx[i], cy[i], 0.0])
+            e1 = np.array([s, 0.0, 0.0])
+            e2 = np.array([0.0, s * eps, -s])
+            pos[i] = np.concatenate([a, a + e1, a + e2]).astype(np.float32)
+        nrm = np.tile(np.array([0.0, 0.0, 1.0], np.float32), (400, 3))
+        uv = rng.uniform(0.0, 1.0, (400, 6)).astype(np.float32)
+        sc = MainScene(gpu, pos, nrm, uv, W, H, texture=64, fov=(16.0, 9.0))
+        fr = Frame(gpu, W, H)
+        try:
+            a = [x.copy() for x in fr.render(W, H)]
+            st = (ctypes.c_uint64 * 14)()
+            assert capi.lib().eray_debug_bin_stats(gpu.handle, 0, st) == 0
+            b = fr.render(W, H, flags=capi.RENDER_BRUTE_FORCE)
+            assert np.array_equal(a[1], b[1]), f"faces, eps {eps}"
+            assert_bit_equal(a[0], b[0], f"grazing faces, eps {eps}")
+            assert np.array_equal(a[2], b[2])
+            results[eps] = (int(st[1]), int((b[1] >= 0).sum()))
+        finally:
+            fr.free()
+            sc.close()
+    assert results[0.005] == (0, 0), results  # no entry, no hit
+    assert results[1.0][0] > 100 and results[1.0][1] > 50, results
+
+
 def _corner_ray_point(W, H, ratio, x, y, t):
     """The point at parameter t along the (unnormalised) camera ray through pixel corner (x, y)
     of main.rs's camera (centre (0, 0, 5), z_dist 1, viewport 2*ratio x 2): camera.rs:57-76."""
