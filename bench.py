@@ -488,7 +488,7 @@ def material_roofline(scene, stream, reps: int = 20) -> dict:
             "bytes_per_update": texels * 16, "us_per_update": round(us, 3), "achieved_gbs": round(gbs, 1),
             "peak_gbs": PEAK_HBM_GBS, "frac": round(gbs / PEAK_HBM_GBS, 4),
             "bound": "latency of the dependent double-precision glibc cosf chain per wave (8 waves per SIMD) "
-                     "and the launch's ramp, neither VALU issue (~15 % of the chip's) nor HBM: 82 VALU "
+                     "(a persistent grid of fewer waves is slower), neither VALU issue (~15 % of the chip's) nor HBM: 82 VALU "
                      "instructions per texel (18 % FP64), 0.48 of wave cycles waiting, WRITE_SIZE = the 16 B "
                      "per texel (profiles/r06/material_pmc.json)"}
 
