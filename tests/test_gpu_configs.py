@@ -391,6 +391,45 @@ def test_faces_grazing_the_view_leave_the_bins(gpu):
     assert results[1.0][0] > 100 and results[1.0][1] > 50, results
 
 
+def test_faces_at_the_det_threshold_equal_brute_force(gpu):
+    """Adversarial for the culling records' det bound: 4000 faces close to the camera (distance
+    1.2-2) whose det along their centre ray is 0.6e-6..1.6e-6, so the reference's det >= 1e-6 test
+    (primitives.rs:47-66) flips across their pixels.  With a = centre, e1 = s u, e2 = s (d + b w)
+    (u, w perpendicular to the centre ray d): n = s^2 (b d - w) ... det = -(d . n) = -s^2 b.  The
+    binned frame must equal the brute-force scan bit for bit, faces and all."""
+    W, H = 1920, 1080
+    rng = np.random.default_rng(12)
+    nf = 4000
+    C = np.array([0.0, 0.0, 5.0])
+    pos = np.zeros((nf, 9), np.float32)
+    for i in range(nf):
+        dist = rng.uniform(1.2, 2.0)
+        c = C + dist * np.array([rng.uniform(-0.8, 0.8), rng.uniform(-0.45, 0.45), -1.0]) / 1.0
+        d = (c - C) / np.linalg.norm(c - C)
+        u = np.cross(d, rng.normal(size=3))
+        u /= np.linalg.norm(u)
+        w = np.cross(d, u)
+        s = rng.uniform(0.01, 0.04)
+        det = rng.uniform(0.6e-6, 1.6e-6)
+        e1 = s * u
+        e2 = s * (d - (det / (s * s)) * w)
+        pos[i] = np.concatenate([c, c + e1, c + e2]).astype(np.float32)
+    nrm = rng.normal(size=(nf, 9)).astype(np.float32)
+    uv = rng.uniform(0.0, 1.0, (nf, 6)).astype(np.float32)
+    sc = MainScene(gpu, pos, nrm, uv, W, H, texture=64, fov=(16.0, 9.0))
+    fr = Frame(gpu, W, H)
+    try:
+        a = [x.copy() for x in fr.render(W, H)]
+        b = fr.render(W, H, flags=capi.RENDER_BRUTE_FORCE)
+        assert np.array_equal(a[1], b[1]), "faces"
+        assert_bit_equal(a[0], b[0], "faces at the det threshold: binned vs brute force")
+        assert np.array_equal(a[2], b[2])
+        assert (b[1] >= 0).sum() > 100  # (222 hit pixels of 215 such faces)
+    finally:
+        fr.free()
+        sc.close()
+
+
 def _corner_ray_point(W, H, ratio, x, y, t):
     """The point at parameter t along the (unnormalised) camera ray through pixel corner (x, y)
     of main.rs's camera (centre (0, 0, 5), z_dist 1, viewport 2*ratio x 2): camera.rs:57-76."""
