@@ -715,7 +715,9 @@ def main() -> None:
     # dispatch's own start / end timestamps (eray_time_frames_ring); the same frames graph-replayed
     # between two events (launch gaps included); the latency of one frame alone per launch
     ring1 = ring_args() if world == 1 else ring_args(0, G)
-    n_kt = max(64, F) // F * F  # dispatch-timed frames: 8 launches of 8 at C2
+    # dispatch-timed frames: 32 launches of 8 at C2 (8 left the mean to a launch or two: the
+    # round-6 sessions' C2 launches spread 39.6-43.1 us)
+    n_kt = max(256, F) // F * F
     with MARK.range(f"timed_F{F}"):
         kt = ctx.time_frames(n_kt, width, H, **ring1)
     kernel_ms = kt["frame_kernel_ms"] / F  # per frame
