@@ -455,7 +455,11 @@ __global__ void __launch_bounds__(kBinWG, kPairsWaves) bin_segments_kernel(const
 
 // every stored entry to its bin: start[key] + its rank, as one 64-B line (BinEntry: the face's
 // intersection record, its pixel mask and its index in the object); the finaliser zeroes the
-// counts for the next camera (coalesced over the keys, not a scattered word per entry)
+// counts for the next camera (coalesced over the keys, not a scattered word per entry).  The
+// shards' entries are one index space (each workgroup prefix-sums the 32 shard counts in LDS), so
+// every thread of the grid takes a share: a loop over the shards gave each shard's entries to the
+// grid's first threads only, which then walked 32 dependent gather-and-store chains one after the
+// other (16 cameras at 3840x2160 / 70k: 114 us).
 __global__ void __launch_bounds__(kBinWG) bin_scatter_kernel(const uint32_t* __restrict__ n, uint32_t cap,
                                                              const uint32_t* __restrict__ ekey,
                                                              const uint32_t* __restrict__ eface,
@@ -465,19 +469,38 @@ __global__ void __launch_bounds__(kBinWG) bin_scatter_kernel(const uint32_t* __r
                                                              const uint32_t* __restrict__ kbegin, uint32_t nbins,
                                                              const TriHot* __restrict__ hot, uint32_t T1,
                                                              BinEntry* __restrict__ ent) {
+    static_assert(kShards <= 64, "one wave scans the shard counts");
+    __shared__ uint32_t s_pre[kShards + 1];  // each shard's first index in the joint space, and the total
     const uint32_t region = cap / kShards;
-    for (uint32_t sh = 0; sh < kShards; ++sh) {  // each shard's entries [sh * region, + its count)
-        const uint32_t total = min(n[sh * kShardStride], region);
-        for (uint32_t el = blockIdx.x * kBinWG + threadIdx.x; el < total; el += gridDim.x * kBinWG) {
-            const uint32_t e = sh * region + el;
-            const uint32_t key = ekey[e], f = eface[e];
-            BinEntry x;
-            x.hot = hot[T1 ? f % T1 : f];  // (several cameras: face f is face f % T1 of camera f / T1)
-            x.mask = emask[e];
-            x.tri = f - kbegin[key / nbins];
-            x.pad = 0u;
-            ent[start[key] + erank[e]] = x;
+    if (threadIdx.x < 64) {
+        const uint32_t lane = threadIdx.x;
+        const uint32_t c = lane < kShards ? min(n[lane * kShardStride], region) : 0u;
+        uint32_t incl = c;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off);
+            if ((int)lane >= off) incl += y;
         }
+        if (lane < kShards) s_pre[lane] = incl - c;
+        if (lane == kShards - 1) s_pre[kShards] = incl;
+    }
+    __syncthreads();
+    const uint32_t total = s_pre[kShards];
+    for (uint32_t g = blockIdx.x * kBinWG + threadIdx.x; g < total; g += gridDim.x * kBinWG) {
+        uint32_t lo = 0, hi = kShards;  // the shard holding g: the last one starting at or before it
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_pre[mid] <= g) lo = mid;
+            else hi = mid;
+        }
+        const uint32_t e = lo * region + (g - s_pre[lo]);
+        const uint32_t key = ekey[e], f = eface[e];
+        BinEntry x;
+        x.hot = hot[T1 ? f % T1 : f];  // (several cameras: face f is face f % T1 of camera f / T1)
+        x.mask = emask[e];
+        x.tri = f - kbegin[key / nbins];
+        x.pad = 0u;
+        ent[start[key] + erank[e]] = x;
     }
 }
 
