@@ -22,11 +22,62 @@ namespace gpu {
 // vertex by vertex each clip was a chain of LDS round trips.)
 // The bounding box [xmin, xmax] x [ymin, ymax] of the viewport points of the box [bx0, bx1] x
 // [by0, by1] where every condition of record c can pass; false when there are none.
+// Fast path (a face whose relaxed edge half-planes meet in a triangle inside the box and inside
+// the det half-plane — every face of a mesh in view but the ones crossing the frame's edge or
+// grazing the view): conditions 0..2 (u >= 0, v >= 0, u + v <= 1) are the face's edges, so the
+// three pairwise intersections of their relaxed lines are the polygon's vertices when each lies on
+// the inner side of the third line (then the three inward normals span the plane: the region is
+// that bounded triangle), inside the box and in condition 3's half-plane (convexity: the whole
+// triangle is).  The clip would return the same polygon; its box comes from three 2 x 2 solves
+// instead of four clips (camera_setup_kernel is VALU bound on them: ~1250 instructions per face).
+// Vertices computed within ~1e-15 of the relaxed ones stay far inside the 1e-9 relaxation; a
+// vertex whose check fails by rounding only sends the face to the clip (and a vertex rounded into
+// the box or condition 3's half-plane only widens the box: bbox(triangle) contains the clip's).
+__device__ inline bool tri_box(const double (&a)[4], const double (&b)[4], const double (&cc)[4], double bx0, double bx1,
+                               double by0, double by1, double& xmin, double& xmax, double& ymin, double& ymax) {
+    double vx[3], vy[3];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {  // vertex e: lines e and e + 1 (mod 3); the third line is e + 2
+        const int i = e, j = (e + 1) % 3, k = (e + 2) % 3;
+        const double det = a[i] * b[j] - a[j] * b[i];
+        if (!(fabs(det) > 1e-12 * (fabs(a[i] * b[j]) + fabs(a[j] * b[i])))) return false;  // (near-)parallel
+        const double x = (b[i] * cc[j] - b[j] * cc[i]) / det, y = (a[j] * cc[i] - a[i] * cc[j]) / det;
+        // strictly inside the third line, beyond rounding (three nearly concurrent lines, whose
+        // signs rounding could flip, leave for the clip: their region may be an unbounded wedge)
+        const double fk = a[k] * x + b[k] * y + cc[k];
+        if (!(fk > 1e-12 * (fabs(a[k] * x) + fabs(b[k] * y) + fabs(cc[k])))) return false;
+        if (!(a[3] * x + b[3] * y + cc[3] >= 0.0)) return false;
+        if (!(x >= bx0 && x <= bx1 && y >= by0 && y <= by1)) return false;
+        vx[e] = x;
+        vy[e] = y;
+    }
+    xmin = fmin(fmin(vx[0], vx[1]), vx[2]);
+    xmax = fmax(fmax(vx[0], vx[1]), vx[2]);
+    ymin = fmin(fmin(vy[0], vy[1]), vy[2]);
+    ymax = fmax(fmax(vy[0], vy[1]), vy[2]);
+    return true;
+}
+
+// (try_tri: the fast path first — for boxes that usually hold whole faces, the viewport)
 __device__ inline bool clip_box(const TriCull& c, double bx0, double bx1, double by0, double by1, double* ws,
-                                uint32_t stride, double& xmin, double& xmax, double& ymin, double& ymax) {
+                                uint32_t stride, double& xmin, double& xmax, double& ymin, double& ymax,
+                                bool try_tri = false) {
     constexpr int kMax = 8;
     const float A[4] = {c.A.x, c.A.y, c.A.z, c.A.w}, B[4] = {c.B.x, c.B.y, c.B.z, c.B.w};
     const float K[4] = {c.K.x, c.K.y, c.K.z, c.K.w}, T[4] = {c.T.x, c.T.y, c.T.z, c.T.w};
+    if (try_tri) {
+        bool finite = true;
+        double fa[4], fb[4], fc[4];  // the clip's relaxed lines, as below
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            finite = finite && T[k] < __builtin_inff() && T[k] > -__builtin_inff();
+            fa[k] = A[k];
+            fb[k] = B[k];
+            const double mag = fabs((double)K[k]) + fabs(fa[k]) + fabs(fb[k]) + fabs((double)T[k]);
+            fc[k] = (double)K[k] + (double)T[k] + 1e-9 * mag + 1e-300;
+        }
+        if (finite && tri_box(fa, fb, fc, bx0, bx1, by0, by1, xmin, xmax, ymin, ymax)) return true;
+    }
     double* qx = ws;
     double* qy = ws + kMax * stride;
     double px[kMax] = {bx0, bx1, bx1, bx0, 0.0, 0.0, 0.0, 0.0};
@@ -92,7 +143,7 @@ __device__ inline bool clip_box(const TriCull& c, double bx0, double bx1, double
 __device__ inline bool face_rect(const TriCull& c, uint32_t W, uint32_t H, int32_t (&r)[4], double* ws,
                                  uint32_t stride, double xa = 0.0, double ya = 0.0) {
     double xmin, xmax, ymin, ymax;
-    if (!clip_box(c, xa, 1.0, ya, 1.0, ws, stride, xmin, xmax, ymin, ymax)) return false;
+    if (!clip_box(c, xa, 1.0, ya, 1.0, ws, stride, xmin, xmax, ymin, ymax, true)) return false;
     r[0] = max((int32_t)floor(xmin * W) - 1, 0);
     r[1] = min((int32_t)ceil(xmax * W) + 1, (int32_t)W - 1);
     r[2] = max((int32_t)floor(ymin * H) - 1, 0);
