@@ -1355,7 +1355,7 @@ __device__ __forceinline__ void fill_blocks(const FrameParams& p, const FrameOut
     if constexpr (kSgpr) wave = __builtin_amdgcn_readfirstlane(wave);
     const uint32_t nblk = p.tiles_x * ((p.rows + kBlkH - 1) / kBlkH);
     const uint32_t fstride = nf * nwaves;
-    constexpr bool kFast = kPace && !kNt;  // (below)
+    constexpr bool kFast = kPace && !kNt && kSgpr;  // (below)
     BlockFill bf;
     if constexpr (kFast) bf = block_fill(p.img_w, lane);
     // blocks (bx, by) with bx < full_x and by < full_y are whole 64 x 4 blocks inside the frame
@@ -1435,6 +1435,11 @@ __device__ __forceinline__ void fill_frames(const FrameParams& p, uint32_t q, ui
             fill_blocks<kDev, true, true>(p, o, cs, occ, g, ng, wave, lane, aligned);
         else if (o.nt)
             fill_blocks<kDev, true, false>(p, o, cs, occ, g, ng, wave, lane, aligned);
+        else if (pace && (p.launch_flags & kLaunchRingBeyondCache))
+            // paced into a ring beyond the Infinity Cache: per-lane block coordinates and per-block
+            // addresses, as the unpaced form there (3840x2160 / 70k in 4 slots 24.06 -> 23.64 us;
+            // C2, C3 and the 1-slot frame unchanged: same-box A/B profiles/r06/ab/ab_r06ii_paced_lane.txt)
+            fill_blocks<kDev, false, true, false>(p, o, cs, occ, g, ng, wave, lane, aligned);
         else if (pace)
             fill_blocks<kDev, false, true>(p, o, cs, occ, g, ng, wave, lane, aligned);
         else if (p.launch_flags & kLaunchRingBeyondCache)
