@@ -1343,6 +1343,10 @@ constexpr int kFillPace = 0x0f70;
 // cacheable stores: two operations may stay in flight (vmcnt(2) against (0): ns1 19.5 -> 19.4,
 // C3 23.3 -> 22.7, C2 41.5 -> 41.0 us; (5) and (10) lose the pacing, profiles/r05/ab/ab_r05al.txt)
 constexpr int kFillPaceCached = 0x0f72;
+// ... cacheable stores into a ring beyond the Infinity Cache (the per-lane form): one operation in
+// flight (3840x2160 / 70k in 4 slots: vmcnt(1) 23.42, (2) 23.65, (0) 23.75, (3) 24.1 us,
+// profiles/r06/ab/ab_r06kk_pace_beyond.txt)
+constexpr int kFillPaceBeyond = 0x0f71;
 // kSgpr: block coordinates in SGPRs (the store offsets' block part a scalar); without it they are
 // per-lane values and every store a full per-lane offset — faster for an unpaced fill into a ring
 // beyond the Infinity Cache (3840x2160 in 4 slots 23.0 -> 19.8 us), slower elsewhere (C2's fill
@@ -1400,7 +1404,7 @@ __device__ __forceinline__ void fill_blocks(const FrameParams& p, const FrameOut
         // 22.2 -> 27.2, C5 128 -> 141; C2 (8 frames) 40.9 -> 43.5 — and a looser bound (vmcnt(5)
         // or (10)) is no better; a fill with the GPU to itself is faster unpaced (3840x2160 18.3
         // vs 21.5 us), same-box A/B profiles/r05/ab/.
-        if constexpr (kPace) __builtin_amdgcn_s_waitcnt(kNt ? kFillPace : kFillPaceCached);
+        if constexpr (kPace) __builtin_amdgcn_s_waitcnt(kNt ? kFillPace : kSgpr ? kFillPaceCached : kFillPaceBeyond);
         if (!mask) {
             // the hoisted-offset stores where the fill is paced and cached (C2 8 frames 52.8 ->
             // 41.2 us); unpaced or non-temporal, the per-block address form writes faster (fill
